@@ -1,0 +1,254 @@
+"""Synthetic workloads for the BASELINE.json configs.
+
+  C2  8-insn ALU-only program over 64-B random packets
+  C3  64-insn L2/L3 parse + classify (VALE-BPF style) over structured 64-B packets
+  C4  C3 + one array-map lookup per packet (array map, 256 x 8 B)
+  C5  256-insn branch-heavy filter over mixed 64-1500 B packets (offsets array)
+
+Programs are laid out with the stepping-aware assembler (layout.py) so the reference
+interpreter executes them as written; "N-insn" = N executed instructions on the main path,
+JA stride resets included.  Packets come from a seeded generator, so every config is
+reproducible bit for bit.  Everything here is input generation; nothing executes eBPF.
+"""
+import numpy as np
+
+from . import isa
+from .layout import Branch, LdDw, MapRef, assemble
+
+I = isa.Insn
+R0, R1, R2, R3, R4, R5, R6, R7, R8, R9, R10 = range(11)
+
+
+def _exit_with(v):
+    return [I("mov_imm", R0, imm=v), I("exit")]
+
+
+# --------------------------------------------------------------------------- packets
+
+def _rng(seed):
+    return np.random.default_rng(seed)
+
+
+def packets_random(n, size=64, seed=2):
+    """Uniform random bytes, fixed stride (C2)."""
+    return _rng(seed).integers(0, 256, size=(n, size), dtype=np.uint8)
+
+
+def packets_l2l3(n, size=64, seed=3):
+    """Structured Ethernet/IPv4/IPv6/ARP frames (C3/C4), fixed stride ``size`` bytes.
+    ethertype 0x0800 80 %, 0x86DD 10 %, 0x0806 10 %; IPv4 proto TCP/UDP/ICMP 60/30/10 %."""
+    g = _rng(seed)
+    p = g.integers(0, 256, size=(n, size), dtype=np.uint8)
+    u = g.random(n)
+    et = np.where(u < 0.8, 0x0800, np.where(u < 0.9, 0x86DD, 0x0806)).astype(np.uint16)
+    p[:, 12] = et >> 8
+    p[:, 13] = et & 0xff
+    v4 = et == 0x0800
+    p[v4, 14] = 0x45
+    tot = size - 14
+    p[v4, 16] = tot >> 8
+    p[v4, 17] = tot & 0xff
+    pu = g.random(n)
+    proto = np.where(pu < 0.6, 6, np.where(pu < 0.9, 17, 1)).astype(np.uint8)
+    p[v4, 23] = proto[v4]
+    ttl = g.integers(0, 256, n).astype(np.uint8)
+    ttl[g.random(n) < 0.02] = 1
+    p[v4, 22] = ttl[v4]
+    ports = np.array([80, 443, 53, 22, 8080, 123], dtype=np.uint16)
+    dp = np.where(g.random(n) < 0.7, ports[g.integers(0, len(ports), n)],
+                  g.integers(0, 65536, n)).astype(np.uint16)
+    p[v4, 36] = dp[v4] >> 8
+    p[v4, 37] = dp[v4] & 0xff
+    ten = g.random(n) < 0.1            # 10.0.0.0/16 destinations
+    sel = v4 & ten
+    p[sel, 30] = 10
+    p[sel, 31] = 0
+    v6 = et == 0x86DD
+    p[v6, 14] = 0x60
+    p[v6, 20] = np.where(g.random(int(v6.sum())) < 0.7, 6, 17)
+    return p
+
+
+IMIX = ((64, 7), (576, 4), (1500, 1))
+
+
+def packets_imix(n, seed=5):
+    """Mixed-size IPv4 frames (C5): sizes 64/576/1500 in IMIX 7:4:1, each packet starts on a
+    64-B boundary.  Returns (data uint8[total], offsets uint64[n+1], sizes uint32[n])."""
+    g = _rng(seed)
+    sizes_tab = np.array([s for s, _ in IMIX], dtype=np.uint32)
+    w = np.array([c for _, c in IMIX], dtype=np.float64)
+    sizes = sizes_tab[g.choice(len(IMIX), size=n, p=w / w.sum())]
+    padded = ((sizes.astype(np.uint64) + 63) // 64) * 64
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(padded, out=offsets[1:])
+    data = g.integers(0, 256, size=int(offsets[-1]), dtype=np.uint8)
+    base = offsets[:-1].astype(np.int64)
+    data[base + 12] = 0x08
+    data[base + 13] = 0x00
+    data[base + 14] = 0x45
+    tot = sizes - 14
+    data[base + 16] = (tot >> 8).astype(np.uint8)
+    data[base + 17] = (tot & 0xff).astype(np.uint8)
+    return data, offsets, sizes
+
+
+# --------------------------------------------------------------------------- programs
+
+def prog_c2():
+    """8 executed instructions: two 8-byte loads, ALU mixing, EXIT (29 slots)."""
+    nodes = [
+        I("ldxdw", R0, R1, 0), I("ldxdw", R2, R1, 8), I("xor64_reg", R0, R2),
+        I("mul64_imm", R0, imm=0x1E3779B1), I("rsh64_imm", R0, imm=29),
+        I("xor64_reg", R0, R2), I("and64_imm", R0, imm=0xff), I("exit"),
+    ]
+    return assemble(nodes)
+
+
+def _classify_program(with_lookup, pad, reset):
+    """Ethernet → IPv4 (TCP/UDP main path) | IPv6 | ICMP | other.  The flow hash and the
+    verdict arithmetic run first and the ACL decisions sit at the end of the path, so nearly
+    every IPv4 packet executes the full main path (no early-exit shortcut)."""
+    ipv6 = [I("ldxb", R3, R1, 20), I("ldxb", R7, R1, 21),
+            I("ldxw", R4, R1, 22), I("ldxw", R5, R1, 38), I("ldxw", R6, R1, 54),
+            I("xor64_reg", R4, R5), I("xor64_reg", R4, R6), I("mul64_imm", R4, imm=0x1E3779B1)]
+    ipv6 += [I("xor64_imm", R4, imm=0x3c6ef372 + 97 * k) if k % 2 else
+             I("mul64_imm", R4, imm=0x27d4eb2d) for k in range(24)]
+    ipv6 += [Branch(I("jle_imm", R7, imm=1), _exit_with(1)),
+             I("rsh64_imm", R4, imm=17), I("and_imm", R4, imm=7), I("add_imm", R4, imm=8),
+             I("mov_reg", R0, R4), I("exit")]
+    icmp = [I("ldxb", R6, R1, 34), I("mov_imm", R0, imm=4),
+            Branch(I("jne_imm", R6, imm=8), [I("exit")]), I("mov_imm", R0, imm=5), I("exit")]
+    head = [
+        I("ldxh", R2, R1, 12), I("be", R2, imm=16),
+        Branch(I("jeq_imm", R2, imm=0x86DD), ipv6),
+        Branch(I("jne_imm", R2, imm=0x0800), _exit_with(2)),
+        I("ldxb", R3, R1, 23),
+        Branch(I("jeq_imm", R3, imm=1), icmp),
+        I("ldxw", R4, R1, 26), I("be", R4, imm=32),
+        I("ldxw", R5, R1, 30), I("be", R5, imm=32),
+        I("ldxh", R7, R1, 34), I("be", R7, imm=16),
+        I("ldxh", R9, R1, 36), I("be", R9, imm=16),
+        # flow hash over (src, dst, sport, dport, proto)
+        I("mov_imm", R8, imm=0), I("or64_reg", R8, R4), I("lsh64_imm", R8, imm=32),
+        I("or64_reg", R8, R5), I("mul64_imm", R8, imm=0x1E3779B1),
+        I("mov_reg", R6, R9), I("lsh64_imm", R6, imm=16), I("or64_reg", R6, R7),
+        I("lsh64_imm", R6, imm=8), I("or64_reg", R6, R3),
+        I("xor64_reg", R8, R6), I("mov_reg", R6, R8), I("rsh64_imm", R6, imm=31),
+        I("xor64_reg", R8, R6), I("mul64_imm", R8, imm=0x2545F491),
+        I("mov_reg", R6, R8), I("rsh64_imm", R6, imm=29), I("xor64_reg", R8, R6),
+    ]
+    pads = [I("xor64_imm", R8, imm=0x5bd1e995 ^ (k * 0x1f1f)) if k % 2 == 0 else
+            I("mul64_imm", R8, imm=0x27d4eb2d) for k in range(pad)]
+    lookup = []
+    if with_lookup:
+        lookup = [
+            I("mov_reg", R6, R9), I("and_imm", R6, imm=0xff),
+            I("stxw", R10, R6, -4),
+            LdDw(R1, MapRef(0)),
+            I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+            I("call", imm=0),
+            Branch(I("jeq_imm", R0, imm=0), _exit_with(2)),
+            I("ldxdw", R6, R0, 0), I("xor64_reg", R8, R6),
+        ]
+    verdict = [
+        I("mov_reg", R0, R8), I("rsh_imm", R0, imm=13), I("and_imm", R0, imm=7),
+        I("add_imm", R0, imm=8),
+        # ACL at the end of the path: ssh → drop, 10.0/16 → redirect,
+        # ephemeral destination port → pass, else the hash-derived class 8..15
+        I("mov_reg", R6, R5),
+        I("and_imm", R6, imm=isa.s32(0xffff0000)),
+        Branch(I("jeq_imm", R9, imm=22), _exit_with(1)),
+        Branch(I("jeq_imm", R6, imm=0x0a000000), _exit_with(3)),
+        Branch(I("jgt_imm", R9, imm=49151), _exit_with(2)),
+        I("exit"),
+    ]
+    return assemble(head + pads + lookup + verdict, reset_stride=reset)
+
+
+def _fit(with_lookup, target, exact=True):
+    """Smallest padding whose main path executes ``target`` instructions (JA resets included)."""
+    for reset in (8, 7, 9, 6, 10):
+        for pad in range(0, 64):
+            lay = _classify_program(with_lookup, pad, reset)
+            if lay.main_path_steps == target or (not exact and lay.main_path_steps >= target):
+                return lay
+            if lay.main_path_steps > target:
+                break
+    raise ValueError("cannot hit %d executed instructions" % target)
+
+
+def prog_c3():
+    """L2/L3 parse + classify; exactly 64 executed instructions on the IPv4 TCP/UDP path."""
+    return _fit(False, 64)
+
+
+def prog_c4():
+    """C3 + one array-map lookup keyed by the low byte of the destination port: the C3 main
+    path (64) plus STXW key, LDDW map, r2 = r10-4 (3 insns), CALL, NULL check, LDXDW value and
+    XOR into the hash — 75 executed instructions on the main path."""
+    return _fit(True, 75, exact=False)
+
+
+def c4_map_values(seed=11, entries=256):
+    return _rng(seed).integers(0, 2**63, size=entries, dtype=np.uint64)
+
+
+def _c5_nodes(seed, body):
+    g = _rng(seed)
+
+    def leaf(limit):
+        n = []
+        acc = R8
+        for k in range(body):
+            if k % 4 == 0:
+                off = int(g.integers(18, limit - 8))
+                op = ("ldxb", "ldxh", "ldxw", "ldxdw")[int(g.integers(0, 4))]
+                n += [I(op, R6, R1, off), I("xor64_reg", acc, R6)]
+            elif k % 24 == 23:
+                # rare data-dependent early exit (byte == 0x5a): more divergence, no duplication
+                off = int(g.integers(18, limit - 1))
+                n += [I("ldxb", R6, R1, off),
+                      Branch(I("jeq_imm", R6, imm=0x5a), _exit_with(int(g.integers(0, 16))))]
+            else:
+                c = int(g.integers(1, 1 << 30))
+                n.append(I(("mul64_imm", "add64_imm", "xor64_imm")[k % 3], acc, imm=c))
+        n += [I("mov_reg", R0, acc), I("rsh_imm", R0, imm=7), I("and_imm", R0, imm=15),
+              I("exit")]
+        return n
+
+    def tree(limit, depth):
+        if depth == 0:
+            return leaf(limit)
+        off = int(g.integers(18, limit - 1))
+        bit = int(g.integers(0, 8))
+        test = [I("ldxb", R6, R1, off), I("rsh_imm", R6, imm=bit), I("and_imm", R6, imm=1),
+                I("xor64_reg", R8, R6)]
+        taken = tree(limit, depth - 1)
+        return test + [Branch(I("jne_imm", R6, imm=0), taken)] + tree(limit, depth - 1)
+
+    head = [I("ldxh", R7, R1, 16), I("be", R7, imm=16), I("mov_imm", R8, imm=0x1234)]
+    return head + [Branch(I("jgt_imm", R7, imm=1000), tree(1500, 2)),
+                   Branch(I("jgt_imm", R7, imm=100), tree(576, 2))] + tree(64, 2)
+
+
+def prog_c5(seed=7, target=256):
+    """Branch-heavy filter over IMIX packets: a 3-way split on the IPv4 total length, then a
+    depth-2 tree of data-dependent tests on payload bytes (within the size class) whose leaves
+    are straight segments of loads + mixing with rare data-dependent early exits.  The leaf
+    length is fitted so the main (all-not-taken) path executes ``target`` instructions."""
+    for body in range(target // 2, target):
+        lay = assemble(_c5_nodes(seed, body))
+        if lay.main_path_steps >= target:
+            return lay
+    raise ValueError("cannot fit C5")
+
+
+CONFIGS = {
+    "c2": dict(desc="8-insn ALU-only, 64 B random packets", prog=prog_c2, pkt="random"),
+    "c3": dict(desc="64-insn L2/L3 parse+classify, 64 B packets", prog=prog_c3, pkt="l2l3"),
+    "c4": dict(desc="64-insn classify + array-map lookup, 64 B packets", prog=prog_c4,
+               pkt="l2l3"),
+    "c5": dict(desc="256-insn branch-heavy filter, IMIX 64-1500 B packets", prog=prog_c5,
+               pkt="imix"),
+}

@@ -1,0 +1,158 @@
+/*
+ * ebpf.h — public C API of the MI355X eBPF engine (drop-in for generic-ebpf's libebpf.so).
+ *
+ * Every declaration here replaces the reference interface at sys/sys/ebpf.h (generic-ebpf @ v0):
+ *   limits / constants           ↔ sys/sys/ebpf.h:21-27
+ *   struct ebpf_prog_attr        ↔ :34-39   (prog_len is a BYTE count: ebpf_prog.c:53,66)
+ *   struct ebpf_map_attr         ↔ :41-47
+ *   enum ebpf_map_update_flags   ↔ :49-54
+ *   struct ebpf_map_ops          ↔ :56-66
+ *   struct ebpf_map_type         ↔ :68-71
+ *   ebpf_helper_fn / helper type ↔ :73-79
+ *   prog ops / prog type         ↔ :81-89
+ *   preprocessor ops / type      ↔ :91-98
+ *   struct ebpf_config           ↔ :100-105 (helper id = index into helper_types, ebpf_interpreter.c:283)
+ *   the 18 API functions         ↔ :107-128
+ *   the 7 exported descriptors   ↔ :130-136
+ * Layouts are byte-identical on x86-64 (checked by static asserts in the library and by
+ * tests/test_abi.py); behaviour (validation order, errno values, refcounting) follows the
+ * reference implementation files cited at each definition in generic-ebpf_amd/csrc/host/.
+ *
+ * The GPU batch extension lives in ebpf_gpu.h.
+ */
+#ifndef EBPF_AMD_EBPF_H
+#define EBPF_AMD_EBPF_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EBPF_NAME_MAX 64
+#define EBPF_TYPE_MAX 64
+#define EBPF_PROG_MAX_ATTACHED_MAPS 64
+#ifndef EBPF_PSEUDO_MAP_DESC
+#define EBPF_PSEUDO_MAP_DESC 1
+#endif
+#define EBPF_STACK_SIZE 512
+
+struct ebpf_obj;
+struct ebpf_prog;
+struct ebpf_map;
+struct ebpf_env;
+struct ebpf_inst;
+
+struct ebpf_prog_attr {
+	uint32_t type;          /* index into ebpf_config.prog_types */
+	struct ebpf_inst *prog; /* bytecode, copied at create time */
+	uint32_t prog_len;      /* length of prog in BYTES */
+	void *data;             /* caller-private */
+};
+
+struct ebpf_map_attr {
+	uint32_t type;          /* index into ebpf_config.map_types */
+	uint32_t key_size;
+	uint32_t value_size;
+	uint32_t max_entries;
+	uint32_t flags;
+};
+
+enum ebpf_map_update_flags {
+	EBPF_ANY = 0,
+	EBPF_NOEXIST = 1,
+	EBPF_EXIST = 2,
+	__EBPF_MAP_UPDATE_FLAGS_MAX
+};
+
+struct ebpf_map_ops {
+	int (*init)(struct ebpf_map *em, struct ebpf_map_attr *attr);
+	void *(*lookup_elem)(struct ebpf_map *em, void *key);
+	int (*update_elem)(struct ebpf_map *em, void *key, void *value, uint64_t flags);
+	int (*delete_elem)(struct ebpf_map *em, void *key);
+	int (*lookup_elem_from_user)(struct ebpf_map *em, void *key, void *value);
+	int (*update_elem_from_user)(struct ebpf_map *em, void *key, void *value, uint64_t flags);
+	int (*delete_elem_from_user)(struct ebpf_map *em, void *key);
+	int (*get_next_key_from_user)(struct ebpf_map *em, void *key, void *next_key);
+	void (*deinit)(struct ebpf_map *em);
+};
+
+struct ebpf_map_type {
+	char name[EBPF_NAME_MAX];
+	struct ebpf_map_ops ops;
+};
+
+/* Helpers receive r1..r5 and return r0 (ebpf_interpreter.c:282-284). */
+typedef uint64_t (*ebpf_helper_fn)(uint64_t r1, uint64_t r2, uint64_t r3, uint64_t r4, uint64_t r5);
+
+struct ebpf_helper_type {
+	char name[EBPF_NAME_MAX];
+	ebpf_helper_fn fn;
+};
+
+struct ebpf_prog_ops {
+	bool (*is_map_usable)(struct ebpf_map_type *emt);
+	bool (*is_helper_usable)(struct ebpf_helper_type *eht);
+};
+
+struct ebpf_prog_type {
+	char name[EBPF_NAME_MAX];
+	struct ebpf_prog_ops ops;
+};
+
+struct ebpf_preprocessor_ops {
+	struct ebpf_map *(*resolve_map_desc)(int32_t upper, int32_t lower, void *data);
+};
+
+struct ebpf_preprocessor_type {
+	char name[EBPF_NAME_MAX];
+	struct ebpf_preprocessor_ops ops;
+};
+
+/* The plugin tables: a program type, map type or helper is "available" iff its slot is set. */
+struct ebpf_config {
+	const struct ebpf_prog_type *prog_types[EBPF_TYPE_MAX];
+	const struct ebpf_map_type *map_types[EBPF_TYPE_MAX];
+	const struct ebpf_helper_type *helper_types[EBPF_TYPE_MAX];
+	const struct ebpf_preprocessor_type *preprocessor_type;
+};
+
+int ebpf_init(void);
+int ebpf_deinit(void);
+
+int ebpf_env_create(struct ebpf_env **eep, const struct ebpf_config *ec);
+int ebpf_env_destroy(struct ebpf_env *ee);
+
+void ebpf_obj_acquire(struct ebpf_obj *eo);
+void ebpf_obj_release(struct ebpf_obj *eo);
+
+int ebpf_prog_create(struct ebpf_env *ee, struct ebpf_prog **epp, struct ebpf_prog_attr *attr);
+void ebpf_prog_destroy(struct ebpf_prog *ep);
+/* Single-packet run on the calling CPU thread, reference semantics (ebpf_interpreter.c:23-372).
+ * For batches use ebpf_prog_run_batch* (ebpf_gpu.h), which run on the GPU. */
+uint64_t ebpf_prog_run(void *ctx, struct ebpf_prog *ep);
+
+int ebpf_map_create(struct ebpf_env *ee, struct ebpf_map **emp, struct ebpf_map_attr *attr);
+void *ebpf_map_lookup_elem(struct ebpf_map *em, void *key);
+int ebpf_map_update_elem(struct ebpf_map *em, void *key, void *value, uint64_t flags);
+int ebpf_map_delete_elem(struct ebpf_map *em, void *key);
+int ebpf_map_lookup_elem_from_user(struct ebpf_map *em, void *key, void *value);
+int ebpf_map_update_elem_from_user(struct ebpf_map *em, void *key, void *value, uint64_t flags);
+int ebpf_map_delete_elem_from_user(struct ebpf_map *em, void *key);
+int ebpf_map_get_next_key_from_user(struct ebpf_map *em, void *key, void *next_key);
+void ebpf_map_destroy(struct ebpf_map *em);
+
+extern const struct ebpf_map_type emt_array;
+extern const struct ebpf_map_type emt_percpu_array;
+extern const struct ebpf_map_type emt_hashtable;
+extern const struct ebpf_map_type emt_percpu_hashtable;
+extern const struct ebpf_helper_type eht_map_lookup_elem;
+extern const struct ebpf_helper_type eht_map_update_elem;
+extern const struct ebpf_helper_type eht_map_delete_elem;
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EBPF_AMD_EBPF_H */

@@ -1,0 +1,118 @@
+/*
+ * ebpf_gpu.h — batch execution of one loaded eBPF program over many packets on MI355X.
+ *
+ * This is the engine's C-ABI extension to the reference API (sys/sys/ebpf.h).  The reference
+ * has no batch entry point: callers loop over packets and call ebpf_prog_run(ctx, ep) once per
+ * packet (sys/dev/ebpf/ebpf_interpreter.c:23; hot loop #1 in SURVEY.md §3(C)).  Each function
+ * below replaces that caller loop:
+ *
+ *   ebpf_prog_run_batch      ↔ for (i..n) ret[i] = ebpf_prog_run(pkt_i, ep);   host buffers
+ *   ebpf_prog_run_batch_dev  ↔ the same loop over device-resident packets (the measured path)
+ *
+ * Per packet the result is bit-identical to ebpf_prog_run on the same bytes (reference
+ * semantics, including its quirks: cumulative pc stepping, MOV64 = add, NEG, logical ARSH —
+ * ebpf_interpreter.c:39,89-91,110-115,182-184,197-208).  Where the reference has no defined
+ * behaviour (it crashes, aborts, hangs or reads stray memory) the device stops that packet
+ * and records an ebpf_fault code instead; ret[i] is then 0.
+ *
+ * Plain pointers and sizes only; no torch or HIP types in any signature (a HIP stream is
+ * passed as void*).
+ */
+#ifndef EBPF_AMD_EBPF_GPU_H
+#define EBPF_AMD_EBPF_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct ebpf_prog;
+struct ebpf_map;
+
+/* Per-packet fault codes (0 = the program reached EXIT). */
+enum ebpf_fault {
+	EBPF_FAULT_NONE = 0,
+	EBPF_FAULT_BAD_OPCODE = 1,   /* opcode outside the dispatch table (ebpf_interpreter.c:367-369: abort) */
+	EBPF_FAULT_DIV_ZERO = 2,     /* DIV/MOD by 0 (reference: SIGFPE) */
+	EBPF_FAULT_MEM = 3,          /* load/store outside this packet, its stack or a map value */
+	EBPF_FAULT_SLOT = 4,         /* stepping left the program (reference reads past the buffer) */
+	EBPF_FAULT_HELPER = 5,       /* CALL id outside [0,64) or an unset helper slot (:283) */
+	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation */
+	EBPF_FAULT_BAD_REG = 7,      /* dst/src register nibble >= 11 (reference overflows reg[]) */
+	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns */
+	EBPF_FAULT_MAP_WRITE = 9,    /* store into array-map value memory (read-only during a batch) */
+	EBPF_FAULT_BAD_MAP = 10,     /* map helper called with r1 not a map of this program's env */
+	EBPF_FAULT_MAX
+};
+
+/* Batch descriptor.  Fixed-stride mode (offsets == NULL): packet i occupies
+ * [data + i*stride, data + (i+1)*stride).  Offsets mode: packet i occupies
+ * [data + offsets[i], data + offsets[i+1]) — offsets has count+1 entries. */
+struct ebpf_pkt_batch {
+	const void *data;
+	const uint64_t *offsets;
+	uint64_t count;
+	uint32_t stride;
+	uint32_t flags; /* reserved, must be 0 */
+};
+
+/* Verdict histogram: bin min(r0, 255) for packets that reached EXIT, bin 256 = faulted. */
+#define EBPF_HIST_BINS 257
+
+/* Per-call summary for the host-buffer entry point. */
+struct ebpf_batch_stats {
+	uint64_t packets;
+	uint64_t faulted;
+	uint64_t hist[EBPF_HIST_BINS];
+	double kernel_ms;     /* device time of the interpreter launches */
+	double total_ms;      /* wall time including H2D/D2H */
+};
+
+/* Number of visible GPUs (0 on a host without one). Never fails. */
+int ebpf_gpu_device_count(void);
+
+/* Translate + upload the program (and its maps) to `device`.  Called implicitly by the run
+ * functions; explicit calls move the one-time cost out of a timed region.
+ * Returns 0, ENODEV (no GPU / no device code object), E2BIG (program state graph too large),
+ * ENOMEM. */
+int ebpf_prog_prepare_device(struct ebpf_prog *ep, int device);
+
+/* Host buffers in, host buffers out; runs on the current device (ebpf_gpu_set_device).
+ * ret: count u64 (required).  faults: count u8 (optional).  stats: optional.
+ * Returns 0 or an errno; packet faults are NOT call errors. */
+int ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
+			uint64_t *ret, uint8_t *faults, struct ebpf_batch_stats *stats);
+
+/* Device-resident batch: every pointer (batch->data, batch->offsets, ret_dev, faults_dev,
+ * hist_dev) is device memory on `device`.  Enqueued on `stream` (hipStream_t, NULL = default
+ * stream) and returns without synchronising.  faults_dev / hist_dev may be NULL; hist_dev is
+ * EBPF_HIST_BINS u64 counters that the kernel ADDS to (zero it yourself). */
+int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
+			    uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev,
+			    void *stream);
+
+/* Select the device used by ebpf_prog_run_batch for the calling thread. */
+int ebpf_gpu_set_device(int device);
+
+/* Interpreter variant used by subsequent launches: 0 = default (fastest available). */
+int ebpf_gpu_set_variant(int variant);
+
+/* Information about the translated device program. */
+struct ebpf_dprog_info {
+	uint32_t nslots;       /* prog_len / 8 */
+	uint32_t nentries;     /* executed-state entries after translation */
+	uint32_t nmaps;        /* array maps resolved from LDDW immediates */
+	uint32_t max_stack;    /* deepest statically known stack access (bytes below r10) */
+};
+int ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info);
+
+/* Human-readable description of the last error on this thread ("" if none). */
+const char *ebpf_gpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EBPF_AMD_EBPF_GPU_H */

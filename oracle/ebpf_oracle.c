@@ -1,0 +1,411 @@
+/*
+ * ebpf_oracle.c — TEST INFRASTRUCTURE ONLY: CPU restatement of the reference interpreter.
+ *
+ * Follows generic-ebpf sys/dev/ebpf/ebpf_interpreter.c:23-372 case by case (line numbers in
+ * the comments), compiled for x86-64 exactly as the reference is: shift counts are masked to
+ * 5/6 bits (x86 SHL/SHR semantics, SURVEY.md Appendix A [probed]).  Parity with the genuine
+ * reference is pinned by tests/golden/ (see ebpf_oracle.h).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use this file.
+ */
+#include "ebpf_oracle.h"
+
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum {
+	F_NONE = 0, F_BAD_OPCODE = 1, F_DIV_ZERO = 2, F_MEM = 3, F_SLOT = 4, F_HELPER = 5,
+	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10
+};
+
+#define STACK_BYTES 512
+
+struct region_env {
+	uint64_t pkt_lo, pkt_hi;
+	uint64_t stk_lo, stk_hi;
+	const struct oracle_prog *p;
+};
+
+/* 0 = ok, else a fault code. write=1 for stores. */
+static inline int
+check_access(const struct region_env *re, uint64_t addr, uint64_t size, int write)
+{
+	uint64_t end = addr + size;
+	if (end < addr)
+		return F_MEM;
+	if (addr >= re->pkt_lo && end <= re->pkt_hi)
+		return 0;
+	if (addr >= re->stk_lo && end <= re->stk_hi)
+		return 0;
+	for (uint32_t m = 0; m < re->p->nmaps; m++) {
+		uint64_t lo = (uint64_t)(uintptr_t)re->p->maps[m].data;
+		uint64_t hi = lo + (uint64_t)re->p->maps[m].value_size * re->p->maps[m].max_entries;
+		if (addr >= lo && end <= hi)
+			return write ? F_MAP_WRITE : 0;
+	}
+	return F_MEM;
+}
+
+static inline uint64_t
+load_n(uint64_t addr, int size)
+{
+	const void *ptr = (const void *)(uintptr_t)addr;
+	switch (size) {
+	case 1: { uint8_t v; memcpy(&v, ptr, 1); return v; }
+	case 2: { uint16_t v; memcpy(&v, ptr, 2); return v; }
+	case 4: { uint32_t v; memcpy(&v, ptr, 4); return v; }
+	default: { uint64_t v; memcpy(&v, ptr, 8); return v; }
+	}
+}
+
+static inline void
+store_n(uint64_t addr, int size, uint64_t v)
+{
+	void *ptr = (void *)(uintptr_t)addr;
+	switch (size) {
+	case 1: { uint8_t x = (uint8_t)v; memcpy(ptr, &x, 1); break; }
+	case 2: { uint16_t x = (uint16_t)v; memcpy(ptr, &x, 2); break; }
+	case 4: { uint32_t x = (uint32_t)v; memcpy(ptr, &x, 4); break; }
+	default: memcpy(ptr, &v, 8); break;
+	}
+}
+
+static inline uint16_t bs16(uint16_t x) { return (uint16_t)((x >> 8) | (x << 8)); }
+
+/* The 90 opcodes with a case in ebpf_interpreter.c:41-366. */
+static const uint8_t k_valid_ops[] = {
+	0x04, 0x0c, 0x14, 0x1c, 0x24, 0x2c, 0x34, 0x3c, 0x44, 0x4c, 0x54, 0x5c, 0x64, 0x6c,
+	0x74, 0x7c, 0x84, 0x94, 0x9c, 0xa4, 0xac, 0xb4, 0xbc, 0xc4, 0xcc, 0xd4, 0xdc,
+	0x07, 0x0f, 0x17, 0x1f, 0x27, 0x2f, 0x37, 0x3f, 0x47, 0x4f, 0x57, 0x5f, 0x67, 0x6f,
+	0x77, 0x7f, 0x87, 0x97, 0x9f, 0xa7, 0xaf, 0xb7, 0xbf, 0xc7, 0xcf,
+	0x61, 0x69, 0x71, 0x79, 0x62, 0x6a, 0x72, 0x7a, 0x63, 0x6b, 0x73, 0x7b, 0x18,
+	0x05, 0x15, 0x1d, 0x25, 0x2d, 0x35, 0x3d, 0x45, 0x4d, 0x55, 0x5d, 0x65, 0x6d, 0x75,
+	0x7d, 0x85, 0x95, 0xa5, 0xad, 0xb5, 0xbd, 0xc5, 0xcd, 0xd5, 0xdd,
+};
+
+static inline int
+valid_op(uint8_t op)
+{
+	for (unsigned i = 0; i < sizeof(k_valid_ops); i++)
+		if (k_valid_ops[i] == op)
+			return 1;
+	return 0;
+}
+
+/* Which opcodes name a dst / src register (reg[inst->dst] / reg[inst->src] in the reference). */
+static inline int
+uses_dst(uint8_t op)
+{
+	return !(op == 0x05 || op == 0x85 || op == 0x95);
+}
+
+static inline int
+uses_src(uint8_t op)
+{
+	uint8_t cls = op & 7;
+	if (cls == 1 || cls == 3) /* LDX, STX */
+		return 1;
+	if ((cls == 4 || cls == 7 || cls == 5) && (op & 0x08)) {
+		/* REG-source ALU/JMP; LE/BE (0xd4/0xdc) and CALL/EXIT never read src */
+		if (op == 0xdc || op == 0x8d || op == 0x9d || op == 0x85 || op == 0x95)
+			return 0;
+		return 1;
+	}
+	return 0;
+}
+
+/* ebpf_map_lookup_elem (ebpf_map.c:77-84) → array_map_lookup_elem (ebpf_map_array.c:115-124) */
+static inline uint64_t
+helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
+{
+	const struct oracle_prog *p = re->p;
+	if (r1 == 0 || r2 == 0) /* em == NULL || key == NULL → NULL (ebpf_map.c:80-81) */
+		return 0;
+	const struct oracle_map *m = NULL;
+	for (uint32_t i = 0; i < p->nmaps; i++)
+		if (p->maps[i].handle == r1) {
+			m = &p->maps[i];
+			break;
+		}
+	if (m == NULL) {
+		*fault = F_BAD_MAP;
+		return 0;
+	}
+	if (checked) {
+		int f = check_access(re, r2, 4, 0);
+		if (f) {
+			*fault = f;
+			return 0;
+		}
+	}
+	uint32_t k = (uint32_t)load_n(r2, 4);
+	if (k >= m->max_entries)
+		return 0;
+	return (uint64_t)(uintptr_t)(m->data + (uint64_t)m->value_size * k);
+}
+
+static inline uint64_t
+run_one(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
+	uint64_t *steps_out)
+{
+	uint64_t reg[11];
+	uint8_t stack[STACK_BYTES];
+	struct region_env re;
+	uint64_t idx = 0; /* slot index; the reference keeps a pointer (inst) */
+	uint32_t pc = 0;  /* u32 as in ebpf_interpreter.c:26 */
+	uint64_t steps = 0;
+	int fault = F_NONE;
+	uint64_t r0 = 0;
+
+	memset(stack, p->stack_init, sizeof(stack));
+	for (int i = 0; i < 11; i++)
+		reg[i] = p->reg_init;
+	reg[1] = (uint64_t)(uintptr_t)pkt;                   /* :35 */
+	reg[10] = (uint64_t)(uintptr_t)(stack + STACK_BYTES); /* :36 */
+	re.pkt_lo = (uint64_t)(uintptr_t)pkt;
+	re.pkt_hi = re.pkt_lo + len;
+	re.stk_lo = (uint64_t)(uintptr_t)stack;
+	re.stk_hi = re.stk_lo + STACK_BYTES;
+	re.p = p;
+
+	for (;;) {
+		/* :39  inst = inst + pc++;  (cumulative stepping) */
+		uint64_t cur_idx = idx + (uint64_t)pc;
+		uint32_t cur_pc = pc + 1;
+		idx = cur_idx;
+		pc = cur_pc;
+		if (idx >= p->nslots) {
+			fault = F_SLOT;
+			break;
+		}
+		const uint8_t *ip = p->insns + idx * 8;
+		uint8_t op = ip[0];
+		uint8_t d = ip[1] & 0x0f, s = ip[1] >> 4;
+		int16_t off;
+		int32_t imm;
+		memcpy(&off, ip + 2, 2);
+		memcpy(&imm, ip + 4, 4);
+		steps++;
+		if (!valid_op(op)) {
+			fault = F_BAD_OPCODE; /* :367-369 */
+			break;
+		}
+		if ((uses_dst(op) && d >= 11) || (uses_src(op) && s >= 11)) {
+			fault = F_BAD_REG;
+			break;
+		}
+		uint64_t D = d < 11 ? reg[d] : 0, S = s < 11 ? reg[s] : 0;
+		uint32_t D32 = (uint32_t)D, S32 = (uint32_t)S, I32 = (uint32_t)imm;
+		uint64_t IS = (uint64_t)(int64_t)imm; /* int32 imm promoted to u64 (sign-extended) */
+		int taken = -1;                        /* -1: not a conditional jump */
+		int msize = 0;
+
+		switch (op) {
+		/* ---- ALU32 :41-133 — operands truncated to u32, result zero-extended ---- */
+		case 0x0c: reg[d] = (uint32_t)(D32 + S32); break;
+		case 0x04: reg[d] = (uint32_t)(D32 + I32); break;
+		case 0x1c: reg[d] = (uint32_t)(D32 - S32); break;
+		case 0x14: reg[d] = (uint32_t)(D32 - I32); break;
+		case 0x2c: reg[d] = (uint32_t)(D32 * S32); break;
+		case 0x24: reg[d] = (uint32_t)(D32 * I32); break;
+		case 0x3c: if (!S32) { fault = F_DIV_ZERO; break; } reg[d] = D32 / S32; break;
+		case 0x34: if (!I32) { fault = F_DIV_ZERO; break; } reg[d] = D32 / I32; break;
+		case 0x4c: reg[d] = D32 | S32; break;
+		case 0x44: reg[d] = D32 | I32; break;
+		case 0x5c: reg[d] = D32 & S32; break;
+		case 0x54: reg[d] = D32 & I32; break;
+		case 0x6c: reg[d] = (uint32_t)(D32 << (S32 & 31)); break;
+		case 0x64: reg[d] = (uint32_t)(D32 << (I32 & 31)); break;
+		case 0x7c: reg[d] = D32 >> (S32 & 31); break;
+		case 0x74: reg[d] = D32 >> (I32 & 31); break;
+		case 0x84: reg[d] = (uint32_t)(0u - I32); break;          /* :89-91 NEG ignores dst */
+		case 0x9c: if (!S32) { fault = F_DIV_ZERO; break; } reg[d] = D32 % S32; break;
+		case 0x94: if (!I32) { fault = F_DIV_ZERO; break; } reg[d] = D32 % I32; break;
+		case 0xac: reg[d] = D32 ^ S32; break;
+		case 0xa4: reg[d] = D32 ^ I32; break;
+		case 0xbc: reg[d] = S32; break;                            /* :104-106 */
+		case 0xb4: reg[d] = I32; break;                            /* :107-109 */
+		case 0xcc: reg[d] = D32 >> (S32 & 31); break;              /* :110-112 logical */
+		case 0xc4: reg[d] = D32 >> (I32 & 31); break;              /* :113-115 logical */
+		case 0xd4:                                                 /* :116-124 LE (x86: identity) */
+			if (imm == 16) reg[d] = (uint16_t)D;
+			else if (imm == 32) reg[d] = D32;
+			break;
+		case 0xdc:                                                 /* :125-133 BE = bswap on x86 */
+			if (imm == 16) reg[d] = bs16((uint16_t)D);
+			else if (imm == 32) reg[d] = __builtin_bswap32(D32);
+			else if (imm == 64) reg[d] = __builtin_bswap64(D);
+			break;
+		/* ---- ALU64 :134-208 ---- */
+		case 0x0f: reg[d] = D + S; break;
+		case 0x07: reg[d] = D + IS; break;
+		case 0x1f: reg[d] = D - S; break;
+		case 0x17: reg[d] = D - IS; break;
+		case 0x2f: reg[d] = D * S; break;
+		case 0x27: reg[d] = D * IS; break;
+		case 0x3f: if (!S) { fault = F_DIV_ZERO; break; } reg[d] = D / S; break;
+		case 0x37: if (!IS) { fault = F_DIV_ZERO; break; } reg[d] = D / IS; break;
+		case 0x4f: reg[d] = D | S; break;
+		case 0x47: reg[d] = D | IS; break;
+		case 0x5f: reg[d] = D & S; break;
+		case 0x57: reg[d] = D & IS; break;
+		case 0x6f: reg[d] = D << (S & 63); break;
+		case 0x67: reg[d] = D << (IS & 63); break;
+		case 0x7f: reg[d] = D >> (S & 63); break;
+		case 0x77: reg[d] = D >> (IS & 63); break;
+		case 0x87: reg[d] = D - IS; break;                          /* :182-184 NEG64 = dst - imm */
+		case 0x9f: if (!S) { fault = F_DIV_ZERO; break; } reg[d] = D % S; break;
+		case 0x97: if (!IS) { fault = F_DIV_ZERO; break; } reg[d] = D % IS; break;
+		case 0xaf: reg[d] = D ^ S; break;
+		case 0xa7: reg[d] = D ^ IS; break;
+		case 0xbf: reg[d] = D + S; break;                           /* :197-199 MOV64 adds */
+		case 0xb7: reg[d] = D + IS; break;                          /* :200-202 */
+		case 0xcf: reg[d] = D >> (S & 63); break;                   /* :203-205 logical */
+		case 0xc7: reg[d] = D >> (IS & 63); break;                  /* :206-208 logical */
+		/* ---- JMP :209-326 ---- */
+		case 0x05: taken = 1; break;
+		case 0x1d: taken = D == S; break;
+		case 0x15: taken = D == IS; break;
+		case 0x2d: taken = D > S; break;
+		case 0x25: taken = D > IS; break;
+		case 0x3d: taken = D >= S; break;
+		case 0x35: taken = D >= IS; break;
+		case 0x4d: taken = (D & S) != 0; break;
+		case 0x45: taken = (D & IS) != 0; break;
+		case 0x5d: taken = D != S; break;
+		case 0x55: taken = D != IS; break;
+		case 0x6d: taken = (int64_t)D > (int64_t)S; break;
+		case 0x65: taken = (int64_t)D > (int64_t)IS; break;
+		case 0x7d: taken = (int64_t)D >= (int64_t)S; break;
+		case 0x75: taken = (int64_t)D >= (int64_t)IS; break;
+		case 0xad: taken = D < S; break;
+		case 0xa5: taken = D < IS; break;
+		case 0xbd: taken = D <= S; break;
+		case 0xb5: taken = D <= IS; break;
+		case 0xcd: taken = (int64_t)D < (int64_t)S; break;
+		case 0xc5: taken = (int64_t)D < (int64_t)IS; break;
+		case 0xdd: taken = (int64_t)D <= (int64_t)S; break;
+		case 0xd5: taken = (int64_t)D <= (int64_t)IS; break;
+		case 0x85: {                                                /* :282-284 CALL */
+			if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
+				fault = F_HELPER;
+				break;
+			}
+			if (p->helper_kind[imm] != ORACLE_HELPER_MAP_LOOKUP) {
+				fault = F_HELPER_UNSUPPORTED;
+				break;
+			}
+			reg[0] = helper_map_lookup(&re, checked, reg[1], reg[2], &fault);
+			break;
+		}
+		case 0x95: r0 = reg[0]; goto done;                          /* :285-286 EXIT */
+		/* ---- memory :327-366 ---- */
+		case 0x71: msize = 1; goto ldx;
+		case 0x69: msize = 2; goto ldx;
+		case 0x61: msize = 4; goto ldx;
+		case 0x79: msize = 8;
+		ldx: {
+			uint64_t a = S + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 0)))
+				break;
+			reg[d] = load_n(a, msize);
+			break;
+		}
+		case 0x18:                                                  /* :339-342 LDDW */
+			if (idx + 1 >= p->nslots) { fault = F_SLOT; break; }
+			{
+				int32_t hi;
+				memcpy(&hi, p->insns + (idx + 1) * 8 + 4, 4);
+				reg[d] = (uint64_t)I32 | ((uint64_t)(uint32_t)hi << 32);
+			}
+			pc++;
+			break;
+		case 0x73: msize = 1; goto stx;
+		case 0x6b: msize = 2; goto stx;
+		case 0x63: msize = 4; goto stx;
+		case 0x7b: msize = 8;
+		stx: {
+			uint64_t a = D + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 1)))
+				break;
+			store_n(a, msize, S);
+			break;
+		}
+		case 0x72: msize = 1; goto st;
+		case 0x6a: msize = 2; goto st;
+		case 0x62: msize = 4; goto st;
+		case 0x7a: msize = 8;                                       /* STDW stores (u64)imm, sign-extended */
+		st: {
+			uint64_t a = D + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 1)))
+				break;
+			store_n(a, msize, IS);
+			break;
+		}
+		default:                                                    /* :367-369 */
+			fault = F_BAD_OPCODE;
+			break;
+		}
+		if (fault)
+			break;
+		if (taken > 0) {
+			uint32_t npc = pc + (uint32_t)(int32_t)off; /* pc += inst->offset (u32 wrap) */
+			/* next state (idx + npc, npc + 1) == current (idx, pc) → the reference spins forever */
+			if (npc == 0 && pc == 1) {
+				fault = F_LOOP;
+				break;
+			}
+			pc = npc;
+		}
+	}
+done:
+	if (fault)
+		r0 = 0;
+	if (fault_out)
+		*fault_out = (uint8_t)fault;
+	if (steps_out)
+		*steps_out = steps;
+	return r0;
+}
+
+uint64_t
+oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fault,
+	   uint64_t *steps)
+{
+	if (p->checked)
+		return run_one(p, 1, pkt, len, fault, steps);
+	return run_one(p, 0, pkt, len, fault, steps);
+}
+
+uint64_t
+oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *offsets,
+		 uint64_t count, uint32_t stride, uint64_t *ret, uint8_t *faults, int nthreads)
+{
+	uint64_t total = 0;
+	if (nthreads <= 0)
+		nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(static) reduction(+ : total)
+#endif
+	for (int64_t i = 0; i < (int64_t)count; i++) {
+		uint8_t *pkt;
+		uint64_t len;
+		if (offsets) {
+			pkt = data + offsets[i];
+			len = offsets[i + 1] - offsets[i];
+		} else {
+			pkt = data + (uint64_t)i * stride;
+			len = stride;
+		}
+		uint8_t f = 0;
+		uint64_t st = 0;
+		ret[i] = oracle_run(p, pkt, len, &f, &st);
+		if (faults)
+			faults[i] = f;
+		total += st;
+	}
+	return total;
+}
