@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Device-resident batch eBPF throughput on MI355X (BASELINE.json metric).
+
+One step = one launch of the interpreter over the rank's whole device-resident batch (the
+workload named by --config; default C4: the 64-insn VALE-BPF-style classify + one array-map
+lookup per packet over 64M x 64 B synthetic packets per GPU) plus the per-step verdict
+histogram all-reduce (RCCL) when N > 1.  Packets are synthetic (seeded generator) and resident
+in HBM before timing starts.  Multi-GPU: one process per GPU (torch.distributed.run), each
+rank runs its own 64M-packet shard (weak scaling), the only collective is the 257-bin
+histogram all-reduce.
+
+Prints ONE JSON line on rank 0 (see README / DESIGN.md for the fields).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import pkgload  # noqa: E402
+
+pkg = pkgload.load()
+from generic_ebpf_amd import native, shard, workloads  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c4", choices=sorted(workloads.CONFIGS))
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default per config)")
+    ap.add_argument("--variant", type=int, default=0, help="0 = default interpreter, 1 = HIP baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+DEFAULT_PACKETS = {"c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 26, "c5": 1 << 22}
+DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
+
+
+def build_inputs(cfg, n, rank):
+    """Host-side synthetic inputs for one rank: (layout, maps spec, packets u8, offsets|None)."""
+    lay = workloads.CONFIGS[cfg]["prog"]()
+    maps = []
+    if cfg == "c4":
+        maps = [(8, 256, workloads.c4_map_values().tobytes())]
+    if cfg == "c5":
+        data, offs, _ = workloads.packets_imix(n, seed=5 + rank)
+        return lay, maps, data, offs
+    d = min(n, DISTINCT)
+    gen = workloads.packets_random if cfg == "c2" else workloads.packets_l2l3
+    return lay, maps, gen(d, 64, seed=(2 if cfg == "c2" else 3) + 1000 * rank), None
+
+
+def cpu_baseline(cfg, lay, maps, pk, offs, budget_s):
+    """Oracle (the CPU restatement of the reference interpreter, raw-pointer mode like the
+    reference) on a bounded sample of the same workload, all host threads up to 16."""
+    import pyoracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    if offs is not None:
+        n = min(len(offs) - 1, 1 << 18)
+        data, offsets = pk[: int(offs[n])], offs[: n + 1]
+    else:
+        n = min(pk.shape[0], 1 << 20)
+        data, offsets = pk[:n].reshape(-1), None
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, maps, checked=False)
+    op.run(data, n, 64, offsets, nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        op.run(data, n, 64, offsets, nthreads=threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(n * passes / el / 1e6, 2), "unit": "Mpkt/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes over %d %s packets (%s), %d host threads, %.1f s" % (
+                passes, n, cfg.upper(), "IMIX" if offsets is not None else "64 B", threads, el)}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = a.config
+    n = a.packets or DEFAULT_PACKETS[cfg]
+
+    lay, maps_spec, pk, offs = build_inputs(cfg, n, rank)
+    env = native.Env()
+    maps = []
+    for vs, me, d in maps_spec:
+        m = native.Map(env, me, vs)
+        m.fill(d)
+        maps.append(m)
+    prog = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    native.set_variant(a.variant)
+    prog.prepare(local)
+
+    # device-resident inputs
+    if offs is None:
+        base = torch.from_numpy(pk.reshape(-1)).to(dev)
+        reps = (n + pk.shape[0] - 1) // pk.shape[0]
+        d_pk = base.repeat(reps)[: n * 64].contiguous()
+        del base
+        d_offs = None
+        bytes_per_launch = n * 64
+    else:
+        d_pk = torch.from_numpy(pk).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        sizes = np.diff(offs)
+        bytes_per_launch = int(sizes.sum()) + 8 * (n + 1)
+    d_ret = torch.empty(n, dtype=torch.int64, device=dev)
+    d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        d_hist.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        prog.run_batch_dev(local, d_pk.data_ptr(), n, 64, d_ret.data_ptr(),
+                           None if d_offs is None else d_offs.data_ptr(), None,
+                           d_hist.data_ptr(), stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        shard.reduce_hist(d_hist)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    if world > 1:
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern_ms = float(t[0]), float(t[1])
+    ms_per_step = el * 1e3 / a.steps
+    total_pkts = n * world * a.steps
+    value = total_pkts / el / 1e6
+
+    hist = d_hist.cpu().numpy()
+    faulted = int(hist[256])
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    info = prog.info()
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            maps_for_oracle = maps_spec
+            cpu = cpu_baseline(cfg, lay, maps_for_oracle, pk, offs, a.cpu_seconds)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg)
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        out = {
+            "metric": "Mpkt/s device-resident (64-insn filter, 64B pkts); achieved HBM GB/s vs peak",
+            "value": round(value, 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": cfg, "desc": workloads.CONFIGS[cfg]["desc"],
+                       "packets_per_gpu": n, "packet_bytes": 64 if offs is None else "IMIX",
+                       "main_path_insns": lay.main_path_steps, "prog_slots": lay.nslots,
+                       "dprog_entries": info.nentries, "variant": a.variant,
+                       "parallelism": "dp%d" % world, "faulted_packets": faulted},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                         "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    prog.destroy()
+    for m in maps:
+        m.destroy()
+    env.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

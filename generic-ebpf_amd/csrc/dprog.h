@@ -1,0 +1,59 @@
+// dprog.h — the device program: the reference's bytecode unrolled into its executed states.
+//
+// The reference interpreter walks slots with a cumulative counter (ebpf_interpreter.c:39
+// "inst = inst + pc++"), so what executes next depends on the pair (slot i, pc p), not on the
+// slot alone.  The translator (translate.cpp) enumerates every (i, p) state reachable from
+// (0, 1) and emits one dp_entry per state, with explicit successor indices.  The device kernels
+// then never compute slot arithmetic: they follow `next` / `target`.  JA states are folded into
+// their successors (a JA has no effect besides the state change), DIV/MOD by a zero immediate,
+// invalid opcodes, bad registers, leaving the program and self-re-entering jumps become FAULT
+// entries, and each CALL is resolved against the env's helper table at translation time.
+//
+// Shared by host C++ and HIP device code: plain C layout, 32 bytes per entry.
+#pragma once
+#include <stdint.h>
+
+enum dp_kind : uint16_t {
+	// 0x00..0xff: the eBPF opcode itself (ALU, ALU64, LDX, ST, STX, LDDW, cond jumps, EXIT)
+	DK_FAULT = 0x100,       // terminal: aux = ebpf_fault code
+	DK_CALL_LOOKUP = 0x101, // r0 = map_lookup_elem(r1, r2)  (ebpf_map.c:77-84)
+};
+
+struct dp_entry {
+	uint64_t handler; // asm interpreter: absolute handler address (patched per device)
+	uint64_t imm;     // pre-extended immediate: sext(imm) for ALU64/JMP, u32(imm) for ALU32,
+	                  // the full 64-bit value for LDDW
+	uint32_t next;    // successor when the instruction falls through / jump not taken
+	uint32_t target;  // successor when a conditional jump is taken
+	uint16_t kind;    // dp_kind or opcode
+	uint8_t dst, src;
+	int16_t off;
+	uint16_t aux;     // DK_FAULT: fault code
+};
+static_assert(sizeof(dp_entry) == 32, "dp_entry is 32 bytes");
+
+// One array map visible to device programs (resolved LDDW handle → device mirror).
+struct dp_map {
+	uint64_t handle;      // the value programs load with LDDW: the host struct ebpf_map*
+	uint64_t dev_base;    // device address of the mirror (max_entries * value_size bytes)
+	uint32_t value_size;
+	uint32_t max_entries;
+};
+static_assert(sizeof(dp_map) == 24, "dp_map is 24 bytes");
+
+// Kernel arguments (passed by value).
+struct dp_launch {
+	const dp_entry *prog;
+	const dp_map *maps;
+	uint8_t *data;
+	const uint64_t *offsets; // NULL → fixed stride; else packet i = data + offsets[i] - off_base
+	uint64_t off_base;
+	uint64_t *ret;
+	uint8_t *faults;         // may be NULL
+	unsigned long long *hist; // EBPF_HIST_BINS counters, may be NULL
+	uint64_t count;
+	uint32_t stride;
+	uint32_t start;          // entry index of the initial state (0, 1)
+	uint32_t nmaps;
+	uint32_t nentries;
+};

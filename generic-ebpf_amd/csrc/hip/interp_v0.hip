@@ -1,0 +1,308 @@
+// interp_v0.hip — portable-HIP baseline of the batch interpreter (variant 1).
+//
+// One lane = one packet; the wave walks the translated device program (dprog.h) in lockstep:
+// every step it picks the smallest entry index among its live lanes (a wave-uniform value, so
+// the entry is fetched with scalar loads) and runs that entry for the lanes sitting on it.
+// Replaces the caller's per-packet loop around ebpf_prog_run (ebpf_interpreter.c:23-372) with
+// identical per-packet results.
+//
+// This variant keeps the eBPF register file in LDS (R[reg][lane], conflict-free for a
+// wave-uniform register index) and does byte-wise, region-checked memory access.  It is the
+// correctness baseline the hand-written gfx950 assembly interpreter (variant 0, asm/) is
+// checked and timed against.
+#include <hip/hip_runtime.h>
+
+#include "../dprog.h"
+
+namespace {
+
+constexpr int kWG = 256;
+constexpr int kStack = 512;
+constexpr int kHistBins = 257;
+
+enum {
+	F_NONE = 0, F_BAD_OPCODE = 1, F_DIV_ZERO = 2, F_MEM = 3, F_SLOT = 4, F_HELPER = 5,
+	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10
+};
+
+__device__ inline uint32_t
+wave_min(uint32_t v)
+{
+	for (int o = 32; o > 0; o >>= 1)
+		v = min(v, (uint32_t)__shfl_xor((int)v, o));
+	return v;
+}
+
+struct regions {
+	uint64_t pkt_lo, pkt_len, stk_lo;
+};
+
+// 0 = ok, else fault code.  Ranges: [pkt_lo, pkt_lo+len), [stk_lo, stk_lo+512), map mirrors.
+__device__ inline int
+check(const regions &rg, const dp_launch &L, uint64_t a, uint32_t size, bool write)
+{
+	if (rg.pkt_len >= size && a - rg.pkt_lo <= rg.pkt_len - size)
+		return F_NONE;
+	if (a - rg.stk_lo <= (uint64_t)(kStack - size))
+		return F_NONE;
+	for (uint32_t m = 0; m < L.nmaps; m++) {
+		uint64_t bytes = (uint64_t)L.maps[m].value_size * L.maps[m].max_entries;
+		if (bytes >= size && a - L.maps[m].dev_base <= bytes - size)
+			return write ? F_MAP_WRITE : F_NONE;
+	}
+	return F_MEM;
+}
+
+__device__ inline uint64_t
+load_bytes(uint64_t a, uint32_t size)
+{
+	const uint8_t *p = reinterpret_cast<const uint8_t *>(a);
+	uint64_t v = 0;
+	for (uint32_t i = 0; i < size; i++)
+		v |= (uint64_t)p[i] << (8 * i);
+	return v;
+}
+
+__device__ inline void
+store_bytes(uint64_t a, uint32_t size, uint64_t v)
+{
+	uint8_t *p = reinterpret_cast<uint8_t *>(a);
+	for (uint32_t i = 0; i < size; i++)
+		p[i] = (uint8_t)(v >> (8 * i));
+}
+
+__device__ inline bool
+cond_taken(uint16_t op, uint64_t d, uint64_t s)
+{
+	switch (op & 0xf0) {
+	case 0x10: return d == s;
+	case 0x20: return d > s;
+	case 0x30: return d >= s;
+	case 0x40: return (d & s) != 0;
+	case 0x50: return d != s;
+	case 0x60: return (int64_t)d > (int64_t)s;
+	case 0x70: return (int64_t)d >= (int64_t)s;
+	case 0xa0: return d < s;
+	case 0xb0: return d <= s;
+	case 0xc0: return (int64_t)d < (int64_t)s;
+	case 0xd0: return (int64_t)d <= (int64_t)s;
+	}
+	return false;
+}
+
+__global__ __launch_bounds__(kWG) void
+ebpf_interp_v0(dp_launch L)
+{
+	__shared__ uint64_t R[11][kWG];
+	__shared__ unsigned hist[kHistBins];
+	const int tid = threadIdx.x;
+	for (int b = tid; b < kHistBins; b += kWG)
+		hist[b] = 0;
+	__syncthreads();
+
+	const uint64_t gid = (uint64_t)blockIdx.x * kWG + tid;
+	const bool live = gid < L.count;
+	uint8_t stack[kStack];
+	regions rg;
+	rg.pkt_lo = 0;
+	rg.pkt_len = 0;
+	if (live) {
+		if (L.offsets) {
+			rg.pkt_lo = (uint64_t)L.data + (L.offsets[gid] - L.off_base);
+			rg.pkt_len = L.offsets[gid + 1] - L.offsets[gid];
+		} else {
+			rg.pkt_lo = (uint64_t)L.data + gid * L.stride;
+			rg.pkt_len = L.stride;
+		}
+	}
+	rg.stk_lo = (uint64_t)(uintptr_t)&stack[0];
+	for (int r = 0; r < 11; r++)
+		R[r][tid] = 0;
+	R[1][tid] = rg.pkt_lo;
+	R[10][tid] = rg.stk_lo + kStack;
+
+	uint32_t T = L.start;
+	bool active = live;
+	int fault = F_NONE;
+	uint64_t result = 0;
+
+	for (;;) {
+		const uint64_t am = __ballot(active);
+		if (am == 0)
+			break;
+		const uint32_t t0 = (uint32_t)__shfl((int)T, __ffsll((long long)am) - 1);
+		uint32_t t = t0;
+		if (!__all(!active || T == t0))
+			t = wave_min(active ? T : 0xffffffffu);
+		t = __builtin_amdgcn_readfirstlane(t);
+		if (!(active && T == t))
+			continue;
+
+		const dp_entry e = L.prog[t];
+		const uint16_t k = e.kind;
+		T = e.next;
+		if (k == DK_FAULT) {
+			fault = e.aux;
+			active = false;
+			continue;
+		}
+		const uint32_t cls = k & 7;
+		if (k == 0x95) { // EXIT
+			result = R[0][tid];
+			active = false;
+			continue;
+		}
+		if (k == DK_CALL_LOOKUP) {
+			const uint64_t r1 = R[1][tid], r2 = R[2][tid];
+			uint64_t res = 0;
+			if (r1 != 0 && r2 != 0) {
+				int mi = -1;
+				for (uint32_t m = 0; m < L.nmaps; m++)
+					if (L.maps[m].handle == r1) {
+						mi = (int)m;
+						break;
+					}
+				if (mi < 0) {
+					fault = F_BAD_MAP;
+					active = false;
+					continue;
+				}
+				int f = check(rg, L, r2, 4, false);
+				if (f) {
+					fault = f;
+					active = false;
+					continue;
+				}
+				uint32_t key = (uint32_t)load_bytes(r2, 4);
+				if (key < L.maps[mi].max_entries)
+					res = L.maps[mi].dev_base + (uint64_t)L.maps[mi].value_size * key;
+			}
+			R[0][tid] = res;
+			continue;
+		}
+		if (cls == 0x5) { // conditional jumps (JA and CALL/EXIT handled above / folded)
+			const uint64_t d = R[e.dst][tid];
+			const uint64_t s = (k & 0x08) ? R[e.src][tid] : e.imm;
+			if (cond_taken(k, d, s))
+				T = e.target;
+			continue;
+		}
+		if (cls == 0x1) { // LDX
+			const uint32_t size = (k & 0x18) == 0x00 ? 4 : (k & 0x18) == 0x08 ? 2 : (k & 0x18) == 0x10 ? 1 : 8;
+			const uint64_t a = R[e.src][tid] + (uint64_t)(int64_t)e.off;
+			int f = check(rg, L, a, size, false);
+			if (f) {
+				fault = f;
+				active = false;
+				continue;
+			}
+			R[e.dst][tid] = load_bytes(a, size);
+			continue;
+		}
+		if (cls == 0x2 || cls == 0x3) { // ST / STX
+			const uint32_t size = (k & 0x18) == 0x00 ? 4 : (k & 0x18) == 0x08 ? 2 : (k & 0x18) == 0x10 ? 1 : 8;
+			const uint64_t a = R[e.dst][tid] + (uint64_t)(int64_t)e.off;
+			int f = check(rg, L, a, size, true);
+			if (f) {
+				fault = f;
+				active = false;
+				continue;
+			}
+			store_bytes(a, size, cls == 0x2 ? e.imm : R[e.src][tid]);
+			continue;
+		}
+		if (k == 0x18) { // LDDW
+			R[e.dst][tid] = e.imm;
+			continue;
+		}
+		// ALU / ALU64
+		const uint64_t d = R[e.dst][tid];
+		const uint64_t s = (k & 0x08) ? R[e.src][tid] : e.imm;
+		uint64_t r;
+		if (cls == 0x4) {
+			const uint32_t d32 = (uint32_t)d, s32 = (uint32_t)s;
+			switch (k & 0xf0) {
+			case 0x00: r = (uint32_t)(d32 + s32); break;
+			case 0x10: r = (uint32_t)(d32 - s32); break;
+			case 0x20: r = (uint32_t)(d32 * s32); break;
+			case 0x30:
+				if (!s32) { fault = F_DIV_ZERO; active = false; continue; }
+				r = d32 / s32;
+				break;
+			case 0x40: r = d32 | s32; break;
+			case 0x50: r = d32 & s32; break;
+			case 0x60: r = (uint32_t)(d32 << (s32 & 31)); break;
+			case 0x70: r = d32 >> (s32 & 31); break;
+			case 0x80: r = (uint32_t)(0u - (uint32_t)e.imm); break; // NEG ignores dst
+			case 0x90:
+				if (!s32) { fault = F_DIV_ZERO; active = false; continue; }
+				r = d32 % s32;
+				break;
+			case 0xa0: r = d32 ^ s32; break;
+			case 0xb0: r = s32; break;
+			case 0xc0: r = d32 >> (s32 & 31); break; // logical
+			default: { // 0xd0: LE / BE
+				const int64_t w = (int64_t)e.imm;
+				r = d;
+				if (k == 0xd4) {
+					if (w == 16) r = (uint16_t)d;
+					else if (w == 32) r = (uint32_t)d;
+				} else {
+					if (w == 16) r = __builtin_bswap16((uint16_t)d);
+					else if (w == 32) r = __builtin_bswap32((uint32_t)d);
+					else if (w == 64) r = __builtin_bswap64(d);
+				}
+			}
+			}
+		} else {
+			switch (k & 0xf0) {
+			case 0x00: r = d + s; break;
+			case 0x10: r = d - s; break;
+			case 0x20: r = d * s; break;
+			case 0x30:
+				if (!s) { fault = F_DIV_ZERO; active = false; continue; }
+				r = d / s;
+				break;
+			case 0x40: r = d | s; break;
+			case 0x50: r = d & s; break;
+			case 0x60: r = d << (s & 63); break;
+			case 0x70: r = d >> (s & 63); break;
+			case 0x80: r = d - e.imm; break; // NEG64 = dst - imm
+			case 0x90:
+				if (!s) { fault = F_DIV_ZERO; active = false; continue; }
+				r = d % s;
+				break;
+			case 0xa0: r = d ^ s; break;
+			case 0xb0: r = d + s; break; // MOV64 adds
+			default: r = d >> (s & 63); break; // 0xc0 ARSH64, logical
+			}
+		}
+		R[e.dst][tid] = r;
+	}
+
+	if (live) {
+		L.ret[gid] = fault ? 0 : result;
+		if (L.faults)
+			L.faults[gid] = (uint8_t)fault;
+		if (L.hist)
+			atomicAdd(&hist[fault ? 256 : (result < 255 ? (unsigned)result : 255u)], 1u);
+	}
+	if (L.hist) {
+		__syncthreads();
+		for (int b = tid; b < kHistBins; b += kWG)
+			if (hist[b])
+				atomicAdd(&L.hist[b], (unsigned long long)hist[b]);
+	}
+}
+
+} // namespace
+
+hipError_t
+launch_interp_v0(const dp_launch &L, hipStream_t stream)
+{
+	if (L.count == 0)
+		return hipSuccess;
+	const uint64_t blocks = (L.count + kWG - 1) / kWG;
+	hipLaunchKernelGGL(ebpf_interp_v0, dim3((unsigned)blocks), dim3(kWG), 0, stream, L);
+	return hipGetLastError();
+}

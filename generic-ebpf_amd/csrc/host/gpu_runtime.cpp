@@ -1,0 +1,479 @@
+// gpu_runtime.cpp — the GPU backend behind ebpf_gpu.h.
+//
+// Replaces the caller-side packet loop around ebpf_prog_run (hot loop #1) with
+// device launches.  Per (program, device) it keeps the translated program (translate.cpp) and
+// a table of the array maps the program references; per (map, device) a mirror of the map's
+// storage that is refreshed before a launch whenever the host copy changed (host writes bump
+// ebpf_map::version).  Launches are asynchronous on the caller's stream; nothing here ever
+// executes eBPF on the CPU — without a GPU the entry points return ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+
+#include "internal.h"
+
+hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
+hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device); // asm_runtime.cpp
+int asm_available(int device);
+int asm_link_entries(int device, std::vector<dp_entry> &entries);
+
+
+namespace {
+
+thread_local std::string t_err;
+thread_local int t_dev = 0;
+std::atomic<int> g_variant{0};
+
+int
+fail(int err, const std::string &msg)
+{
+	t_err = msg;
+	return err;
+}
+
+int
+hip_fail(hipError_t e, const char *what)
+{
+	return fail(e == hipErrorOutOfMemory ? ENOMEM : EIO,
+		    std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int
+device_count()
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}
+
+// Which interpreter runs: 0 = default (assembly if present), 1 = portable HIP baseline.
+int
+effective_variant(int device)
+{
+	int v = g_variant.load();
+	if (v == 0 && !asm_available(device))
+		return 1;
+	return v == 0 ? 0 : v;
+}
+
+int
+ensure_translated(struct ebpf_prog *ep)
+{
+	if (ep->xlated)
+		return ep->xlated->error;
+	auto x = std::make_unique<dprog_host>();
+	int err = translate_program(ep, *x);
+	if (err && x->error == 0)
+		x->error = err;
+	ep->xlated = std::move(x);
+	if (ep->xlated->error)
+		return fail(ep->xlated->error, ep->xlated->error_msg);
+	return 0;
+}
+
+int
+ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
+{
+	std::lock_guard<std::mutex> g(em->mirror_lock);
+	if ((int)em->mirrors.size() <= device)
+		em->mirrors.resize(device + 1);
+	map_mirror &m = em->mirrors[device];
+	if (m.dev == nullptr) {
+		hipError_t e = hipMalloc(&m.dev, (size_t)em->value_size * em->max_entries);
+		if (e != hipSuccess)
+			return hip_fail(e, "hipMalloc(map mirror)");
+		m.version = ~0ull;
+	}
+	*dev = m.dev;
+	return 0;
+}
+
+int
+sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
+{
+	for (struct ebpf_map *em : ep->xlated->maps) {
+		std::lock_guard<std::mutex> g(em->mirror_lock);
+		map_mirror &m = em->mirrors[device];
+		uint64_t v = em->version.load();
+		if (m.version != v) {
+			hipError_t e = hipMemcpyAsync(m.dev, em->array_storage(),
+						      (size_t)em->value_size * em->max_entries,
+						      hipMemcpyHostToDevice, stream);
+			if (e != hipSuccess)
+				return hip_fail(e, "hipMemcpyAsync(map mirror)");
+			m.version = v;
+		}
+	}
+	return 0;
+}
+
+int
+prepare(struct ebpf_prog *ep, int device, dprog_device **out)
+{
+	if (device < 0 || device >= device_count())
+		return fail(ENODEV, "no such GPU device");
+	std::lock_guard<std::mutex> g(ep->dlock);
+	int err = ensure_translated(ep);
+	if (err)
+		return err;
+	if ((int)ep->dev.size() <= device)
+		ep->dev.resize(device + 1);
+	auto &dp = ep->dev[device];
+	int variant = effective_variant(device);
+	if (dp && dp->variant_linked == variant) {
+		*out = dp.get();
+		return 0;
+	}
+	hipError_t e = hipSetDevice(device);
+	if (e != hipSuccess)
+		return hip_fail(e, "hipSetDevice");
+	if (!dp)
+		dp = std::make_unique<dprog_device>();
+	dp->device = device;
+	std::vector<dp_entry> entries = ep->xlated->entries;
+	if (variant == 0) {
+		err = asm_link_entries(device, entries);
+		if (err)
+			return err;
+	}
+	if (dp->d_entries == nullptr || dp->nentries != entries.size()) {
+		if (dp->d_entries)
+			hipFree(dp->d_entries);
+		e = hipMalloc(&dp->d_entries, entries.size() * sizeof(dp_entry));
+		if (e != hipSuccess)
+			return hip_fail(e, "hipMalloc(program)");
+	}
+	e = hipMemcpy(dp->d_entries, entries.data(), entries.size() * sizeof(dp_entry),
+		      hipMemcpyHostToDevice);
+	if (e != hipSuccess)
+		return hip_fail(e, "hipMemcpy(program)");
+	dp->nentries = (uint32_t)entries.size();
+
+	std::vector<dp_map> table;
+	for (struct ebpf_map *em : ep->xlated->maps) {
+		void *mdev = nullptr;
+		err = ensure_map_mirror(em, device, &mdev);
+		if (err)
+			return err;
+		dp_map m;
+		m.handle = (uint64_t)(uintptr_t)em;
+		m.dev_base = (uint64_t)(uintptr_t)mdev;
+		m.value_size = em->value_size;
+		m.max_entries = em->max_entries;
+		table.push_back(m);
+	}
+	if (dp->d_maps == nullptr && !table.empty()) {
+		e = hipMalloc(&dp->d_maps, table.size() * sizeof(dp_map));
+		if (e != hipSuccess)
+			return hip_fail(e, "hipMalloc(map table)");
+	}
+	if (!table.empty()) {
+		e = hipMemcpy(dp->d_maps, table.data(), table.size() * sizeof(dp_map),
+			      hipMemcpyHostToDevice);
+		if (e != hipSuccess)
+			return hip_fail(e, "hipMemcpy(map table)");
+	}
+	dp->nmaps = (uint32_t)table.size();
+	dp->variant_linked = variant;
+	*out = dp.get();
+	return 0;
+}
+
+int
+launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream)
+{
+	dp_launch L = L0;
+	L.prog = dp->d_entries;
+	L.maps = dp->d_maps;
+	L.nmaps = dp->nmaps;
+	L.nentries = dp->nentries;
+	L.start = ep->xlated->start;
+	int err = sync_map_mirrors(ep, dp->device, stream);
+	if (err)
+		return err;
+	hipError_t e = dp->variant_linked == 0 ? launch_interp_asm(L, stream, dp->device)
+					       : launch_interp_v0(L, stream);
+	if (e != hipSuccess)
+		return hip_fail(e, "kernel launch");
+	return 0;
+}
+
+int
+validate_batch(const struct ebpf_pkt_batch *b)
+{
+	if (b == nullptr || (b->data == nullptr && b->count != 0))
+		return fail(EINVAL, "batch or batch->data is NULL");
+	if (b->flags != 0)
+		return fail(EINVAL, "batch->flags must be 0");
+	if (b->offsets == nullptr && b->stride == 0 && b->count != 0)
+		return fail(EINVAL, "fixed-stride batch with stride 0");
+	return 0;
+}
+
+// Per-thread staging for the host-buffer entry point.
+struct staging {
+	int device = -1;
+	hipStream_t stream[2] = {nullptr, nullptr};
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	void *d_data[2] = {nullptr, nullptr};
+	size_t data_cap[2] = {0, 0};
+	void *d_small[2] = {nullptr, nullptr}; // ret | faults | offsets, per chunk
+	size_t small_cap[2] = {0, 0};
+	unsigned long long *d_hist = nullptr;
+	~staging() {}
+};
+thread_local staging t_stage;
+
+int
+stage_alloc(void **p, size_t *cap, size_t need)
+{
+	if (*cap >= need)
+		return 0;
+	if (*p)
+		hipFree(*p);
+	*p = nullptr;
+	*cap = 0;
+	hipError_t e = hipMalloc(p, need);
+	if (e != hipSuccess)
+		return hip_fail(e, "hipMalloc(staging)");
+	*cap = need;
+	return 0;
+}
+
+} // namespace
+
+void
+set_last_error(const std::string &msg)
+{
+	t_err = msg;
+}
+
+void
+prog_release_device_state(struct ebpf_prog *ep)
+{
+	for (auto &dp : ep->dev) {
+		if (!dp)
+			continue;
+		if (hipSetDevice(dp->device) == hipSuccess) {
+			if (dp->d_entries)
+				hipFree(dp->d_entries);
+			if (dp->d_maps)
+				hipFree(dp->d_maps);
+		}
+	}
+	ep->dev.clear();
+}
+
+void
+map_release_device_state(struct ebpf_map *em)
+{
+	for (size_t d = 0; d < em->mirrors.size(); d++)
+		if (em->mirrors[d].dev && hipSetDevice((int)d) == hipSuccess)
+			hipFree(em->mirrors[d].dev);
+	em->mirrors.clear();
+}
+
+EBPF_EXPORT int
+ebpf_gpu_device_count(void)
+{
+	return device_count();
+}
+
+EBPF_EXPORT int
+ebpf_gpu_set_device(int device)
+{
+	if (device < 0 || device >= device_count())
+		return fail(ENODEV, "no such GPU device");
+	t_dev = device;
+	return 0;
+}
+
+EBPF_EXPORT int
+ebpf_gpu_set_variant(int variant)
+{
+	if (variant < 0 || variant > 1)
+		return fail(EINVAL, "variant must be 0 (default) or 1 (portable HIP)");
+	g_variant.store(variant);
+	return 0;
+}
+
+EBPF_EXPORT const char *
+ebpf_gpu_last_error(void)
+{
+	return t_err.c_str();
+}
+
+EBPF_EXPORT int
+ebpf_prog_prepare_device(struct ebpf_prog *ep, int device)
+{
+	if (ep == nullptr)
+		return fail(EINVAL, "prog is NULL");
+	dprog_device *dp;
+	return prepare(ep, device, &dp);
+}
+
+EBPF_EXPORT int
+ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info)
+{
+	if (ep == nullptr || info == nullptr)
+		return fail(EINVAL, "NULL argument");
+	std::lock_guard<std::mutex> g(ep->dlock);
+	int err = ensure_translated(ep);
+	if (err)
+		return err;
+	info->nslots = ep->prog_len / 8;
+	info->nentries = (uint32_t)ep->xlated->entries.size();
+	info->nmaps = (uint32_t)ep->xlated->maps.size();
+	info->max_stack = ep->xlated->max_stack;
+	return 0;
+}
+
+EBPF_EXPORT int
+ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
+			uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev, void *stream)
+{
+	if (ep == nullptr || ret_dev == nullptr)
+		return fail(EINVAL, "prog or ret is NULL");
+	int err = validate_batch(batch);
+	if (err)
+		return err;
+	dprog_device *dp;
+	err = prepare(ep, device, &dp);
+	if (err)
+		return err;
+	if (batch->count == 0)
+		return 0;
+	hipError_t e = hipSetDevice(device);
+	if (e != hipSuccess)
+		return hip_fail(e, "hipSetDevice");
+	dp_launch L;
+	memset(&L, 0, sizeof(L));
+	L.data = (uint8_t *)batch->data;
+	L.offsets = batch->offsets;
+	L.off_base = 0;
+	L.ret = ret_dev;
+	L.faults = faults_dev;
+	L.hist = reinterpret_cast<unsigned long long *>(hist_dev);
+	L.count = batch->count;
+	L.stride = batch->stride;
+	return launch(ep, dp, L, static_cast<hipStream_t>(stream));
+}
+
+EBPF_EXPORT int
+ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, uint64_t *ret,
+		    uint8_t *faults, struct ebpf_batch_stats *stats)
+{
+	if (ep == nullptr || ret == nullptr)
+		return fail(EINVAL, "prog or ret is NULL");
+	int err = validate_batch(batch);
+	if (err)
+		return err;
+	auto t0 = std::chrono::steady_clock::now();
+	const int device = t_dev;
+	dprog_device *dp;
+	err = prepare(ep, device, &dp);
+	if (err)
+		return err;
+	staging &S = t_stage;
+	hipError_t e = hipSetDevice(device);
+	if (e != hipSuccess)
+		return hip_fail(e, "hipSetDevice");
+	if (S.device != device) {
+		for (int i = 0; i < 2; i++) {
+			if (hipStreamCreateWithFlags(&S.stream[i], hipStreamNonBlocking) != hipSuccess)
+				return fail(EIO, "hipStreamCreate");
+		}
+		for (auto &ev : S.ev)
+			if (hipEventCreate(&ev) != hipSuccess)
+				return fail(EIO, "hipEventCreate");
+		if (hipMalloc(&S.d_hist, EBPF_HIST_BINS * sizeof(unsigned long long)) != hipSuccess)
+			return fail(ENOMEM, "hipMalloc(hist)");
+		S.device = device;
+	}
+	const bool copy_back = ep->xlated->writes_memory;
+	const uint64_t n = batch->count;
+	// Chunked, double-buffered: chunk k's H2D overlaps chunk k-1's kernel and D2H.
+	const uint64_t chunk = batch->offsets ? (1ull << 20) : (1ull << 22);
+	hipMemsetAsync(S.d_hist, 0, EBPF_HIST_BINS * sizeof(unsigned long long), S.stream[0]);
+	hipStreamSynchronize(S.stream[0]);
+	float kernel_ms = 0;
+	bool timed[2] = {false, false};
+	auto collect = [&](int b) {
+		if (!timed[b])
+			return;
+		float ms = 0;
+		hipEventElapsedTime(&ms, S.ev[2 * b], S.ev[2 * b + 1]);
+		kernel_ms += ms;
+		timed[b] = false;
+	};
+	for (uint64_t c0 = 0, k = 0; c0 < n; c0 += chunk, k++) {
+		const int b = (int)(k & 1);
+		hipStream_t st = S.stream[b];
+		const uint64_t cn = (n - c0 < chunk) ? n - c0 : chunk;
+		uint64_t byte0, byte1;
+		if (batch->offsets) {
+			byte0 = batch->offsets[c0];
+			byte1 = batch->offsets[c0 + cn];
+		} else {
+			byte0 = c0 * batch->stride;
+			byte1 = (c0 + cn) * batch->stride;
+		}
+		hipStreamSynchronize(st); // buffers of chunk k-2 are free again
+		collect(b);
+		if ((err = stage_alloc(&S.d_data[b], &S.data_cap[b], byte1 - byte0 + 16)))
+			return err;
+		const size_t small = cn * 9 + (batch->offsets ? (cn + 1) * 8 : 0) + 64;
+		if ((err = stage_alloc(&S.d_small[b], &S.small_cap[b], small)))
+			return err;
+		uint8_t *sm = static_cast<uint8_t *>(S.d_small[b]);
+		uint64_t *d_ret = reinterpret_cast<uint64_t *>(sm);
+		uint64_t *d_offs = batch->offsets ? reinterpret_cast<uint64_t *>(sm + cn * 8) : nullptr;
+		uint8_t *d_faults = sm + cn * 8 + (batch->offsets ? (cn + 1) * 8 : 0);
+		const uint8_t *src = static_cast<const uint8_t *>(batch->data) + byte0;
+		hipMemcpyAsync(S.d_data[b], src, byte1 - byte0, hipMemcpyHostToDevice, st);
+		if (d_offs)
+			hipMemcpyAsync(d_offs, batch->offsets + c0, (cn + 1) * 8, hipMemcpyHostToDevice, st);
+		dp_launch L;
+		memset(&L, 0, sizeof(L));
+		L.data = static_cast<uint8_t *>(S.d_data[b]);
+		L.offsets = d_offs;
+		L.off_base = byte0;
+		L.ret = d_ret;
+		L.faults = d_faults;
+		L.hist = S.d_hist;
+		L.count = cn;
+		L.stride = batch->stride;
+		hipEventRecord(S.ev[2 * b], st);
+		if ((err = launch(ep, dp, L, st)))
+			return err;
+		hipEventRecord(S.ev[2 * b + 1], st);
+		hipMemcpyAsync(ret + c0, d_ret, cn * 8, hipMemcpyDeviceToHost, st);
+		if (faults)
+			hipMemcpyAsync(faults + c0, d_faults, cn, hipMemcpyDeviceToHost, st);
+		if (copy_back)
+			hipMemcpyAsync(const_cast<uint8_t *>(src), S.d_data[b], byte1 - byte0,
+				       hipMemcpyDeviceToHost, st);
+		timed[b] = true;
+	}
+	for (int i = 0; i < 2; i++) {
+		hipStreamSynchronize(S.stream[i]);
+		collect(i);
+	}
+	e = hipGetLastError();
+	if (e != hipSuccess)
+		return hip_fail(e, "batch");
+	if (stats) {
+		unsigned long long h[EBPF_HIST_BINS];
+		hipMemcpy(h, S.d_hist, sizeof(h), hipMemcpyDeviceToHost);
+		stats->packets = n;
+		stats->faulted = h[256];
+		for (int i = 0; i < EBPF_HIST_BINS; i++)
+			stats->hist[i] = h[i];
+		stats->kernel_ms = kernel_ms;
+		stats->total_ms =
+		    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	}
+	return 0;
+}

@@ -1,0 +1,112 @@
+// internal.h — object model of the engine's libebpf.so (host side).
+//
+// Mirrors the reference's object core:
+//   struct ebpf_env  ↔ sys/dev/ebpf/ebpf_env.h   (config + live-object refcount)
+//   struct ebpf_obj  ↔ sys/dev/ebpf/ebpf_obj.h:35-40 (env ref, refcount, type, dtor; first member)
+//   struct ebpf_prog ↔ sys/dev/ebpf/ebpf_prog.h:23-30
+//   struct ebpf_map  ↔ sys/dev/ebpf/ebpf_map.h:23-32
+// plus the per-device state the GPU backend keeps (translated program, map mirrors).
+#pragma once
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "ebpf.h"
+#include "ebpf_gpu.h"
+#include "ebpf_vm_isa.h"
+#include "../dprog.h"
+
+#define EBPF_EXPORT extern "C" __attribute__((visibility("default")))
+
+enum ebpf_obj_type_id : uint32_t { EBPF_OBJ_TYPE_PROG = 0, EBPF_OBJ_TYPE_MAP = 1 };
+
+struct ebpf_env {
+	std::atomic<uint32_t> ref{0};   // live objects (ebpf_env.c:31 starts at 0)
+	const struct ebpf_config *ec = nullptr;
+	std::mutex lock;
+	std::set<struct ebpf_map *> maps; // live maps: resolves LDDW handles to map objects
+};
+
+struct ebpf_obj {
+	struct ebpf_env *eo_ee;
+	std::atomic<uint32_t> eo_ref;
+	uint32_t eo_type;
+	void (*eo_dtor)(struct ebpf_obj *);
+};
+
+// Per-device mirror of one map's storage.
+struct map_mirror {
+	void *dev = nullptr;
+	uint64_t version = ~0ull; // host version last uploaded
+};
+
+struct ebpf_map {
+	struct ebpf_obj eo; // must stay first (callers cast to struct ebpf_obj *)
+	const struct ebpf_map_type *emt;
+	uint32_t key_size;
+	uint32_t value_size;
+	uint32_t map_flags;
+	uint32_t max_entries;
+	bool percpu;
+	void *data;                       // map-type private data
+	std::atomic<uint64_t> version{0}; // bumped on every host-side write
+	std::mutex mirror_lock;
+	std::vector<map_mirror> mirrors;  // indexed by device
+	// array-map storage (for device mirroring); null for other map types
+	uint8_t *array_storage() const;
+};
+
+// Per (program, device): the linked entries and the map table in device memory.
+struct dprog_device {
+	int device = -1;
+	dp_entry *d_entries = nullptr;
+	dp_map *d_maps = nullptr;
+	uint32_t nentries = 0;
+	uint32_t nmaps = 0;
+	int variant_linked = -1; // which interpreter the entries were linked for
+};
+
+struct dprog_host {
+	std::vector<dp_entry> entries;
+	uint32_t start = 0;
+	std::vector<struct ebpf_map *> maps; // referenced array maps, in dp_map table order
+	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
+	uint32_t max_stack = 0;
+	int error = 0;
+	std::string error_msg;
+};
+
+struct ebpf_prog {
+	struct ebpf_obj eo; // must stay first
+	const struct ebpf_prog_type *ept;
+	uint32_t ndep_maps;
+	uint32_t prog_len;
+	struct ebpf_inst *prog;
+	struct ebpf_map *dep_maps[EBPF_PROG_MAX_ATTACHED_MAPS];
+	// GPU backend state
+	std::mutex dlock;
+	std::unique_ptr<dprog_host> xlated;            // translation (device independent)
+	std::vector<std::unique_ptr<dprog_device>> dev; // per device
+};
+
+// env / obj helpers (ebpf_env.c, ebpf_obj.c)
+void env_acquire(struct ebpf_env *ee);
+void env_release(struct ebpf_env *ee);
+void obj_init(struct ebpf_env *ee, struct ebpf_obj *eo);
+
+// translate.cpp
+int translate_program(struct ebpf_prog *ep, dprog_host &out);
+
+// gpu_runtime.cpp
+void set_last_error(const std::string &msg);
+void prog_release_device_state(struct ebpf_prog *ep);
+void map_release_device_state(struct ebpf_map *em);

@@ -1,0 +1,343 @@
+// translate.cpp — reference bytecode → device program (dprog.h).
+//
+// The reference interpreter's next slot depends on (slot i, counter p):  "inst = inst + pc++"
+// (sys/dev/ebpf/ebpf_interpreter.c:39), a taken jump adds its offset to p (:210 etc.) and LDDW
+// adds one more (:341).  Starting from (0, 1) — the first fetch is slot 0 with pc already 1 —
+//     plain:  (i, p) -> (i + p, p + 1)      LDDW: (i, p) -> (i + p + 1, p + 2)
+//     taken:  (i, p) -> (i + p', p' + 1)    with p' = p + off  (u32 arithmetic)
+// This file enumerates the reachable states and emits one dp_entry per state with explicit
+// successors, so device code never does slot arithmetic.  Straight-line runs are emitted
+// contiguously (fallthrough successor = index + 1) and taken sides after them.
+//
+// Under this rule a state (j, q) has exactly one possible predecessor slot (j - q + 1), so the
+// state graph is a tree plus self-loops; a self-loop (a jump whose successor is its own state)
+// is the only way the reference spins forever, and becomes an EBPF_FAULT_LOOP entry.
+#include "internal.h"
+
+#include <unordered_map>
+
+namespace {
+
+bool
+valid_op(uint8_t op)
+{
+	static const uint8_t ops[] = {
+	    0x04, 0x0c, 0x14, 0x1c, 0x24, 0x2c, 0x34, 0x3c, 0x44, 0x4c, 0x54, 0x5c, 0x64, 0x6c,
+	    0x74, 0x7c, 0x84, 0x94, 0x9c, 0xa4, 0xac, 0xb4, 0xbc, 0xc4, 0xcc, 0xd4, 0xdc, 0x07,
+	    0x0f, 0x17, 0x1f, 0x27, 0x2f, 0x37, 0x3f, 0x47, 0x4f, 0x57, 0x5f, 0x67, 0x6f, 0x77,
+	    0x7f, 0x87, 0x97, 0x9f, 0xa7, 0xaf, 0xb7, 0xbf, 0xc7, 0xcf, 0x61, 0x69, 0x71, 0x79,
+	    0x62, 0x6a, 0x72, 0x7a, 0x63, 0x6b, 0x73, 0x7b, 0x18, 0x05, 0x15, 0x1d, 0x25, 0x2d,
+	    0x35, 0x3d, 0x45, 0x4d, 0x55, 0x5d, 0x65, 0x6d, 0x75, 0x7d, 0x85, 0x95, 0xa5, 0xad,
+	    0xb5, 0xbd, 0xc5, 0xcd, 0xd5, 0xdd};
+	static bool tab[256];
+	static bool init = [] {
+		for (uint8_t o : ops)
+			tab[o] = true;
+		return true;
+	}();
+	(void)init;
+	return tab[op];
+}
+
+bool
+uses_dst(uint8_t op)
+{
+	return !(op == EBPF_OP_JA || op == EBPF_OP_CALL || op == EBPF_OP_EXIT);
+}
+
+bool
+uses_src(uint8_t op)
+{
+	uint8_t cls = op & 7;
+	if (cls == EBPF_CLS_LDX || cls == EBPF_CLS_STX)
+		return true;
+	if ((cls == EBPF_CLS_ALU || cls == EBPF_CLS_ALU64 || cls == EBPF_CLS_JMP) && (op & 0x08))
+		return !(op == EBPF_OP_BE || op == EBPF_OP_CALL || op == EBPF_OP_EXIT);
+	return false;
+}
+
+constexpr uint32_t kMaxEntries = 1u << 20;
+
+struct Translator {
+	const struct ebpf_inst *code;
+	uint64_t nslots;
+	const struct ebpf_config *ec;
+	dprog_host &out;
+	std::unordered_map<uint64_t, uint32_t> state_id;
+	uint32_t fault_id[EBPF_FAULT_MAX];
+	std::vector<std::pair<uint32_t, uint64_t>> pending; // (entry, state) to fill
+	bool overflow = false;
+
+	Translator(const struct ebpf_inst *c, uint64_t n, const struct ebpf_config *e, dprog_host &o)
+	    : code(c), nslots(n), ec(e), out(o)
+	{
+		for (auto &f : fault_id)
+			f = UINT32_MAX;
+	}
+
+	static uint64_t key(uint64_t idx, uint32_t pc) { return (idx << 32) | pc; }
+
+	uint32_t new_entry()
+	{
+		if (out.entries.size() >= kMaxEntries) {
+			overflow = true;
+			return 0;
+		}
+		dp_entry e;
+		memset(&e, 0, sizeof(e));
+		out.entries.push_back(e);
+		return (uint32_t)(out.entries.size() - 1);
+	}
+
+	uint32_t fault(int code)
+	{
+		if (fault_id[code] == UINT32_MAX) {
+			uint32_t id = new_entry();
+			out.entries[id].kind = DK_FAULT;
+			out.entries[id].aux = (uint16_t)code;
+			fault_id[code] = id;
+		}
+		return fault_id[code];
+	}
+
+	// Entry for state (idx, pc), following JA chains.  New states are queued for filling.
+	uint32_t get(uint64_t idx, uint32_t pc, bool *created)
+	{
+		*created = false;
+		std::vector<uint64_t> aliases;
+		uint32_t id = UINT32_MAX;
+		for (uint64_t hops = 0;; hops++) {
+			if (idx >= nslots) {
+				id = fault(EBPF_FAULT_SLOT);
+				break;
+			}
+			auto it = state_id.find(key(idx, pc));
+			if (it != state_id.end()) {
+				id = it->second;
+				break;
+			}
+			const struct ebpf_inst &in = code[idx];
+			if (in.opcode == EBPF_OP_JA && hops <= nslots + 2) {
+				uint32_t np = pc + (uint32_t)(int32_t)in.offset;
+				uint64_t nidx = idx + np;
+				aliases.push_back(key(idx, pc));
+				if (nidx == idx && np + 1 == pc) {
+					id = fault(EBPF_FAULT_LOOP);
+					break;
+				}
+				idx = nidx;
+				pc = np + 1;
+				continue;
+			}
+			if (in.opcode == EBPF_OP_JA) { // pathological chain
+				id = fault(EBPF_FAULT_LOOP);
+				break;
+			}
+			id = new_entry();
+			state_id[key(idx, pc)] = id;
+			pending.push_back({id, key(idx, pc)});
+			*created = true;
+			break;
+		}
+		for (uint64_t a : aliases)
+			state_id[a] = id;
+		return id;
+	}
+
+	// Fill one entry; returns the fallthrough successor if it was newly created (so the
+	// caller continues the straight-line run), else UINT32_MAX.
+	void fill(uint32_t id, uint64_t idx, uint32_t pc, std::vector<uint64_t> &deferred_taken,
+		  std::vector<uint32_t> &deferred_taken_entry, uint32_t *next_new)
+	{
+		*next_new = UINT32_MAX;
+		const struct ebpf_inst &in = code[idx];
+		uint8_t op = in.opcode;
+		dp_entry &e = out.entries[id];
+		auto make_fault = [&](int c) {
+			dp_entry &x = out.entries[id];
+			x.kind = DK_FAULT;
+			x.aux = (uint16_t)c;
+		};
+		if (!valid_op(op)) {
+			make_fault(EBPF_FAULT_BAD_OPCODE);
+			return;
+		}
+		if ((uses_dst(op) && in.dst >= EBPF_REG_MAX) || (uses_src(op) && in.src >= EBPF_REG_MAX)) {
+			make_fault(EBPF_FAULT_BAD_REG);
+			return;
+		}
+		e.kind = op;
+		e.dst = in.dst;
+		e.src = in.src;
+		e.off = in.offset;
+		uint8_t cls = op & 7;
+		uint64_t sx = (uint64_t)(int64_t)in.imm;
+		uint64_t zx = (uint64_t)(uint32_t)in.imm;
+		uint64_t next_idx = idx + pc;
+		uint32_t next_pc = pc + 1;
+		switch (cls) {
+		case EBPF_CLS_ALU: {
+			uint8_t alu = op & 0xf0;
+			if ((alu == EBPF_DIV || alu == EBPF_MOD) && !(op & 0x08) && zx == 0) {
+				make_fault(EBPF_FAULT_DIV_ZERO);
+				return;
+			}
+			e.imm = (alu == EBPF_LSH || alu == EBPF_RSH || alu == EBPF_ARSH) && !(op & 0x08)
+				    ? (zx & 31)
+				    : zx;
+			if (op == EBPF_OP_LE || op == EBPF_OP_BE)
+				e.imm = sx;
+			break;
+		}
+		case EBPF_CLS_ALU64: {
+			uint8_t alu = op & 0xf0;
+			if ((alu == EBPF_DIV || alu == EBPF_MOD) && !(op & 0x08) && sx == 0) {
+				make_fault(EBPF_FAULT_DIV_ZERO);
+				return;
+			}
+			e.imm = (alu == EBPF_LSH || alu == EBPF_RSH || alu == EBPF_ARSH) && !(op & 0x08)
+				    ? (sx & 63)
+				    : sx;
+			break;
+		}
+		case EBPF_CLS_LD: // LDDW (the only LD-class opcode dispatched)
+			if (idx + 1 >= nslots) {
+				make_fault(EBPF_FAULT_SLOT);
+				return;
+			}
+			e.imm = zx | ((uint64_t)(uint32_t)code[idx + 1].imm << 32);
+			next_idx = idx + pc + 1;
+			next_pc = pc + 2;
+			break;
+		case EBPF_CLS_ST:
+			e.imm = sx;
+			if (in.dst != EBPF_R10)
+				out.writes_memory = true;
+			break;
+		case EBPF_CLS_STX:
+			if (in.dst != EBPF_R10)
+				out.writes_memory = true;
+			break;
+		case EBPF_CLS_LDX:
+			break;
+		case EBPF_CLS_JMP:
+			if (op == EBPF_OP_EXIT)
+				return;
+			if (op == EBPF_OP_CALL) {
+				const struct ebpf_helper_type *h =
+				    (in.imm >= 0 && in.imm < EBPF_TYPE_MAX) ? ec->helper_types[in.imm] : nullptr;
+				if (h == nullptr) {
+					make_fault(EBPF_FAULT_HELPER);
+					return;
+				}
+				if (h != &eht_map_lookup_elem) {
+					make_fault(EBPF_FAULT_HELPER_UNSUPPORTED);
+					return;
+				}
+				e.kind = DK_CALL_LOOKUP;
+				break;
+			}
+			e.imm = sx;
+			{
+				uint32_t np = pc + (uint32_t)(int32_t)in.offset;
+				uint64_t tidx = idx + np;
+				uint32_t tpc = np + 1;
+				if (tidx == idx && tpc == pc) {
+					uint32_t f = fault(EBPF_FAULT_LOOP); // may grow entries: no `e` after this
+					out.entries[id].target = f;
+				} else {
+					deferred_taken.push_back(key(tidx, tpc));
+					deferred_taken_entry.push_back(id);
+				}
+			}
+			break;
+		default:
+			make_fault(EBPF_FAULT_BAD_OPCODE);
+			return;
+		}
+		bool created;
+		uint32_t n = get(next_idx, next_pc, &created);
+		out.entries[id].next = n;
+		if (created)
+			*next_new = n;
+	}
+
+	int run()
+	{
+		bool created;
+		out.start = get(0, 1, &created);
+		std::vector<uint64_t> dt;
+		std::vector<uint32_t> dte;
+		size_t pi = 0, di = 0;
+		while (!overflow) {
+			// pending entries are processed in creation order; a straight run is filled
+			// eagerly so fallthrough successors get consecutive indices.
+			if (pi < pending.size()) {
+				uint32_t id = pending[pi].first;
+				uint64_t k = pending[pi].second;
+				pi++;
+				uint32_t nn;
+				fill(id, k >> 32, (uint32_t)k, dt, dte, &nn);
+				continue;
+			}
+			if (di >= dt.size())
+				break;
+			uint64_t k = dt[di];
+			uint32_t from = dte[di];
+			di++;
+			out.entries[from].target = get(k >> 32, (uint32_t)k, &created);
+		}
+		if (overflow) {
+			out.error = E2BIG;
+			out.error_msg = "program state graph exceeds the device translation limit";
+			return E2BIG;
+		}
+		return 0;
+	}
+};
+
+} // namespace
+
+int
+translate_program(struct ebpf_prog *ep, dprog_host &out)
+{
+	const struct ebpf_inst *code = ep->prog;
+	uint64_t nslots = ep->prog_len / sizeof(struct ebpf_inst);
+	Translator t(code, nslots, ep->eo.eo_ee->ec, out);
+	int err = t.run();
+	if (err)
+		return err;
+
+	// Resolve LDDW immediates that are live array maps of this env: the device map table.
+	struct ebpf_env *ee = ep->eo.eo_ee;
+	std::lock_guard<std::mutex> g(ee->lock);
+	auto add_map = [&](struct ebpf_map *m) {
+		if (m->array_storage() == nullptr)
+			return;
+		for (auto *x : out.maps)
+			if (x == m)
+				return;
+		out.maps.push_back(m);
+	};
+	for (const dp_entry &e : out.entries) {
+		if (e.kind == EBPF_OP_LDDW) {
+			auto *cand = reinterpret_cast<struct ebpf_map *>((uintptr_t)e.imm);
+			if (ee->maps.count(cand))
+				add_map(cand);
+		}
+		if (e.kind == EBPF_OP_STXB || e.kind == EBPF_OP_STXH || e.kind == EBPF_OP_STXW ||
+		    e.kind == EBPF_OP_STXDW || e.kind == EBPF_OP_STB || e.kind == EBPF_OP_STH ||
+		    e.kind == EBPF_OP_STW || e.kind == EBPF_OP_STDW) {
+			if (e.dst == EBPF_R10 && e.off < 0 && (uint32_t)(-e.off) > out.max_stack)
+				out.max_stack = (uint32_t)(-e.off);
+		}
+	}
+	for (uint32_t i = 0; i < ep->ndep_maps; i++)
+		if (ee->maps.count(ep->dep_maps[i]))
+			add_map(ep->dep_maps[i]);
+	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
+	// its map while a later batch may still read it.
+	for (struct ebpf_map *m : out.maps)
+		m->eo.eo_ref.fetch_add(1);
+	return 0;
+}

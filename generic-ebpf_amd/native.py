@@ -1,0 +1,264 @@
+"""ctypes binding of the engine's C-ABI library (lib/libebpf.so).
+
+The Python layer mirrors the reference's plugin interface: an ``Env`` owns a ``struct
+ebpf_config`` laid out like tests/test_common.hpp:59-75 of the reference (program type 0
+"test"; map types 0..3 = array, percpu array, hashtable, percpu hashtable; helpers 0..2 =
+map_lookup_elem / map_update_elem / map_delete_elem), ``Map`` and ``Prog`` wrap the map and
+program objects with the reference's errno conventions.  Batch runs go to the GPU through
+include/ebpf_gpu.h; if the library is missing, loading fails loudly.
+"""
+import ctypes
+import errno
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libebpf.so")
+
+EBPF_TYPE_MAX = 64
+EBPF_NAME_MAX = 64
+EBPF_HIST_BINS = 257
+
+MAP_TYPE_ARRAY, MAP_TYPE_PERCPU_ARRAY, MAP_TYPE_HASHTABLE, MAP_TYPE_PERCPU_HASHTABLE = range(4)
+HELPER_LOOKUP, HELPER_UPDATE, HELPER_DELETE = range(3)
+EBPF_ANY, EBPF_NOEXIST, EBPF_EXIST = 0, 1, 2
+
+FAULT_NAMES = ["NONE", "BAD_OPCODE", "DIV_ZERO", "MEM", "SLOT", "HELPER", "HELPER_UNSUPPORTED",
+               "BAD_REG", "LOOP", "MAP_WRITE", "BAD_MAP"]
+
+
+class ProgAttr(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_uint32), ("prog", ctypes.c_void_p),
+                ("prog_len", ctypes.c_uint32), ("data", ctypes.c_void_p)]
+
+
+class MapAttr(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_uint32), ("key_size", ctypes.c_uint32),
+                ("value_size", ctypes.c_uint32), ("max_entries", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+_PREDFN = ctypes.CFUNCTYPE(ctypes.c_bool, ctypes.c_void_p)
+
+
+class ProgType(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * EBPF_NAME_MAX), ("is_map_usable", _PREDFN),
+                ("is_helper_usable", _PREDFN)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("prog_types", ctypes.c_void_p * EBPF_TYPE_MAX),
+                ("map_types", ctypes.c_void_p * EBPF_TYPE_MAX),
+                ("helper_types", ctypes.c_void_p * EBPF_TYPE_MAX),
+                ("preprocessor_type", ctypes.c_void_p)]
+
+
+class PktBatch(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("count", ctypes.c_uint64), ("stride", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("packets", ctypes.c_uint64), ("faulted", ctypes.c_uint64),
+                ("hist", ctypes.c_uint64 * EBPF_HIST_BINS), ("kernel_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double)]
+
+
+class DprogInfo(ctypes.Structure):
+    _fields_ = [("nslots", ctypes.c_uint32), ("nentries", ctypes.c_uint32),
+                ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
+
+
+# Every function include/ebpf.h and include/ebpf_gpu.h declare: name -> (restype, argtypes)
+_VP, _U32, _U64, _I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+FUNCS = {
+    "ebpf_init": (_I, []), "ebpf_deinit": (_I, []),
+    "ebpf_env_create": (_I, [_VP, _VP]), "ebpf_env_destroy": (_I, [_VP]),
+    "ebpf_obj_acquire": (None, [_VP]), "ebpf_obj_release": (None, [_VP]),
+    "ebpf_prog_create": (_I, [_VP, _VP, _VP]), "ebpf_prog_destroy": (None, [_VP]),
+    "ebpf_prog_run": (_U64, [_VP, _VP]),
+    "ebpf_map_create": (_I, [_VP, _VP, _VP]), "ebpf_map_lookup_elem": (_VP, [_VP, _VP]),
+    "ebpf_map_update_elem": (_I, [_VP, _VP, _VP, _U64]),
+    "ebpf_map_delete_elem": (_I, [_VP, _VP]),
+    "ebpf_map_lookup_elem_from_user": (_I, [_VP, _VP, _VP]),
+    "ebpf_map_update_elem_from_user": (_I, [_VP, _VP, _VP, _U64]),
+    "ebpf_map_delete_elem_from_user": (_I, [_VP, _VP]),
+    "ebpf_map_get_next_key_from_user": (_I, [_VP, _VP, _VP]),
+    "ebpf_map_destroy": (None, [_VP]),
+    # ebpf_gpu.h
+    "ebpf_gpu_device_count": (_I, []), "ebpf_gpu_set_device": (_I, [_I]),
+    "ebpf_gpu_set_variant": (_I, [_I]), "ebpf_gpu_last_error": (ctypes.c_char_p, []),
+    "ebpf_prog_prepare_device": (_I, [_VP, _I]),
+    "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
+    "ebpf_prog_device_info": (_I, [_VP, _VP]),
+}
+DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_hashtable",
+                "eht_map_lookup_elem", "eht_map_update_elem", "eht_map_delete_elem"]
+
+_lib = None
+
+
+def lib():
+    """Load lib/libebpf.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError("native library not built: %s (run __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in FUNCS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def addr_of(symbol):
+    return ctypes.addressof(ctypes.c_char.in_dll(lib(), symbol))
+
+
+def last_error():
+    return (lib().ebpf_gpu_last_error() or b"").decode()
+
+
+class EbpfError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s failed: %s (%d) %s" % (what, errno.errorcode.get(code, "?"), code,
+                                                    last_error()))
+        self.code = code
+
+
+def _check(code, what):
+    if code != 0:
+        raise EbpfError(code, what)
+
+
+_always = _PREDFN(lambda _p: True)
+
+
+class Env:
+    """ebpf_env with the reference test suite's configuration (tests/test_common.hpp:59-75)."""
+
+    def __init__(self, helpers=None):
+        L = lib()
+        self._ptype = ProgType(b"test", _always, _always)
+        self.config = Config()
+        self.config.prog_types[0] = ctypes.addressof(self._ptype)
+        for i, s in enumerate(["emt_array", "emt_percpu_array", "emt_hashtable",
+                               "emt_percpu_hashtable"]):
+            self.config.map_types[i] = addr_of(s)
+        hl = helpers if helpers is not None else {
+            HELPER_LOOKUP: addr_of("eht_map_lookup_elem"),
+            HELPER_UPDATE: addr_of("eht_map_update_elem"),
+            HELPER_DELETE: addr_of("eht_map_delete_elem")}
+        for i, a in hl.items():
+            self.config.helper_types[i] = a
+        self.ptr = ctypes.c_void_p()
+        _check(L.ebpf_env_create(ctypes.byref(self.ptr), ctypes.byref(self.config)),
+               "ebpf_env_create")
+
+    def destroy(self):
+        return lib().ebpf_env_destroy(self.ptr)
+
+
+class Map:
+    def __init__(self, env, max_entries, value_size, key_size=4, type=MAP_TYPE_ARRAY):
+        self.env = env
+        self.value_size, self.max_entries = value_size, max_entries
+        attr = MapAttr(type, key_size, value_size, max_entries, 0)
+        self.ptr = ctypes.c_void_p()
+        _check(lib().ebpf_map_create(env.ptr, ctypes.byref(self.ptr), ctypes.byref(attr)),
+               "ebpf_map_create")
+
+    @property
+    def handle(self):
+        return self.ptr.value
+
+    def update(self, key, value_bytes, flags=EBPF_ANY):
+        k = ctypes.c_uint32(key)
+        v = ctypes.create_string_buffer(bytes(value_bytes), self.value_size)
+        return lib().ebpf_map_update_elem_from_user(self.ptr, ctypes.byref(k), v, flags)
+
+    def fill(self, data):
+        """data: bytes of max_entries * value_size."""
+        for k in range(self.max_entries):
+            _check(self.update(k, data[k * self.value_size:(k + 1) * self.value_size]),
+                   "map update")
+
+    def lookup(self, key):
+        k = ctypes.c_uint32(key)
+        v = ctypes.create_string_buffer(self.value_size)
+        err = lib().ebpf_map_lookup_elem_from_user(self.ptr, ctypes.byref(k), v)
+        return err, v.raw
+
+    def destroy(self):
+        lib().ebpf_map_destroy(self.ptr)
+
+
+def patch_relocs(code, relocs, handles):
+    b = bytearray(code)
+    for slot, k in relocs:
+        h = handles[k] & 0xffffffffffffffff
+        b[slot * 8 + 4: slot * 8 + 8] = (h & 0xffffffff).to_bytes(4, "little")
+        b[slot * 8 + 12: slot * 8 + 16] = (h >> 32).to_bytes(4, "little")
+    return bytes(b)
+
+
+class Prog:
+    def __init__(self, env, code, prog_type=0):
+        self.env = env
+        self._buf = ctypes.create_string_buffer(bytes(code), len(code))
+        attr = ProgAttr(prog_type, ctypes.addressof(self._buf), len(code), None)
+        self.ptr = ctypes.c_void_p()
+        _check(lib().ebpf_prog_create(env.ptr, ctypes.byref(self.ptr), ctypes.byref(attr)),
+               "ebpf_prog_create")
+
+    def destroy(self):
+        lib().ebpf_prog_destroy(self.ptr)
+
+    def info(self):
+        i = DprogInfo()
+        _check(lib().ebpf_prog_device_info(self.ptr, ctypes.byref(i)), "ebpf_prog_device_info")
+        return i
+
+    def prepare(self, device=0):
+        _check(lib().ebpf_prog_prepare_device(self.ptr, device), "ebpf_prog_prepare_device")
+
+    def run_cpu(self, packet):
+        """Single packet through ebpf_prog_run (the API's per-packet CPU entry point)."""
+        buf = ctypes.create_string_buffer(bytes(packet), len(packet))
+        return lib().ebpf_prog_run(buf, self.ptr), buf.raw
+
+    def run_batch(self, data, count, stride=0, offsets=None, want_faults=True):
+        """Host buffers: returns (ret u64[count], faults u8[count], stats).  ``data`` (a
+        contiguous uint8 numpy array) is modified in place if the program stores to packets."""
+        assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
+        ret = np.zeros(count, dtype=np.uint64)
+        faults = np.zeros(count, dtype=np.uint8) if want_faults else None
+        offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        b = PktBatch(data.ctypes.data, None if offs is None else offs.ctypes.data, count,
+                     stride, 0)
+        st = BatchStats()
+        _check(lib().ebpf_prog_run_batch(self.ptr, ctypes.byref(b), ret.ctypes.data,
+                                         None if faults is None else faults.ctypes.data,
+                                         ctypes.byref(st)), "ebpf_prog_run_batch")
+        return ret, faults, st
+
+    def run_batch_dev(self, device, data_ptr, count, stride, ret_ptr, offsets_ptr=None,
+                      faults_ptr=None, hist_ptr=None, stream=None):
+        """Device pointers (ints); asynchronous on ``stream`` (hipStream_t as int or None)."""
+        b = PktBatch(data_ptr, offsets_ptr, count, stride, 0)
+        _check(lib().ebpf_prog_run_batch_dev(self.ptr, device, ctypes.byref(b), ret_ptr,
+                                             faults_ptr, hist_ptr, stream),
+               "ebpf_prog_run_batch_dev")
+
+
+def gpu_count():
+    return lib().ebpf_gpu_device_count()
+
+
+def set_variant(v):
+    _check(lib().ebpf_gpu_set_variant(v), "ebpf_gpu_set_variant")

@@ -1,0 +1,188 @@
+"""Parity of the device interpreters with the genuine reference (golden vectors) and with the
+oracle (fresh random programs, full-size workloads, faults).  Every test calls the engine
+through the C-ABI (lib/libebpf.so): host-buffer batches (ebpf_prog_run_batch) and
+device-resident batches (ebpf_prog_run_batch_dev on torch-allocated memory)."""
+import numpy as np
+import pytest
+
+import goldens
+from helpers import device_run, make_maps, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+CASES = [c for f in goldens.all_golden_files() for c in goldens.load(f)]
+VARIANTS = [0, 1]  # 0 = default (fastest available), 1 = portable HIP baseline
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_goldens_on_device(gpu, env, variant):
+    bad = []
+    for c in CASES:
+        ret, faults, after = device_run(gpu, env, c, variant)
+        if not (np.array_equal(ret, c.expect_r0) and not faults.any()
+                and np.array_equal(after, c.expect_data)):
+            bad.append((c.name, int(np.count_nonzero(ret != c.expect_r0)),
+                        int(np.count_nonzero(faults))))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_random_programs_vs_oracle(gpu, env, variant):
+    from generic_ebpf_amd import randprog, workloads
+    g = np.random.default_rng(77)
+    bad = []
+    for k in range(120):
+        vs = int(g.choice([8, 16]))
+        me = int(g.choice([16, 256]))
+        lay = randprog.random_program(50000 + k, length=int(g.integers(10, 80)), nmaps=2,
+                                      map_value_size=vs)
+        maps = [(vs, me, g.integers(0, 256, vs * me, dtype=np.uint8).tobytes()) for _ in range(2)]
+        n = 2048
+        c = goldens.Case("r%d" % k, lay.code, lay.relocs, maps,
+                         workloads.packets_random(n, 64, seed=k), n, 64, None)
+        want, wf, wdata, _ = oracle_run(c)
+        got, gf, gdata = device_run(gpu, env, c, variant)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)
+                and np.array_equal(wdata, gdata)):
+            bad.append(k)
+    assert not bad, bad
+
+
+FAULT_PROGS = None
+
+
+def _fault_programs():
+    from generic_ebpf_amd import isa, layout
+    O, e, I = isa.OPS, isa.encode, isa.Insn
+    return {
+        "div0_imm": e(O["mov_imm"], 0, imm=1) + e(O["div_imm"], 0, imm=0),
+        "div0_reg": layout.assemble([I("mov_imm", 0, imm=5), I("ldxb", 2, 1, 0),
+                                     I("and_imm", 2, imm=1), I("mod64_reg", 0, 2),
+                                     I("exit")]).code,
+        "bad_opcode": e(0x06) + e(O["exit"]),
+        "oob_load": layout.assemble([I("ldxb", 2, 1, 0), I("and_imm", 2, imm=3),
+                                     I("add64_imm", 2, imm=61), I("mov_imm", 3, imm=0),
+                                     I("mov64_reg", 3, 1), I("add64_reg", 3, 2),
+                                     I("ldxw", 0, 3, 0), I("exit")]).code,
+        "slot": e(O["mov_imm"], 0, imm=1) + e(O["mov_imm"], 0, imm=2),
+        "helper_unset": e(O["call"], imm=9) + e(O["exit"]),
+        "helper_unsupported": e(O["call"], imm=1) + e(O["exit"]),
+        "bad_reg": e(O["mov_imm"], 11, imm=1) + e(O["exit"]),
+        "loop": e(O["ja"], off=-1) + e(O["exit"]),
+        "bad_map": layout.assemble([layout.LdDw(1, 0x1234), I("mov_imm", 2, imm=8),
+                                    I("call", imm=0), I("exit")]).code,
+        "stack_oob": layout.assemble([I("stb", 10, 0, -513, 1), I("exit")]).code,
+        # the only reachable spin under reference stepping: a jump of -1 taken at state (0, 1)
+        "cond_loop": e(O["jeq_imm"], 2, 0, -1, 0) + e(O["exit"]) * 4,
+    }
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_fault_codes_match_oracle(gpu, env, variant):
+    from generic_ebpf_amd import workloads
+    bad = {}
+    for name, code in _fault_programs().items():
+        n = 256
+        c = goldens.Case(name, code, [], [], workloads.packets_random(n, 64, seed=9), n, 64, None)
+        want, wf, _, _ = oracle_run(c)
+        got, gf, _ = device_run(gpu, env, c, variant)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad[name] = (np.unique(wf).tolist(), np.unique(gf).tolist())
+        assert wf.any(), name  # every program here faults on some packet
+    assert not bad, bad
+
+
+def _tiled_case(name, base, tiles):
+    data = np.tile(base.data, tiles)
+    return goldens.Case(name, base.code, base.relocs, base.maps, data, base.count * tiles,
+                        base.stride, None)
+
+
+@pytest.mark.parametrize("cfg,distinct,tiles", [("c2", 1 << 20, 1), ("c3", 1 << 20, 16),
+                                                 ("c4", 1 << 20, 64)])
+def test_full_size_workloads(gpu, env, cfg, distinct, tiles):
+    """BASELINE.json sizes (C2 1M, C3 16M, C4 64M packets): the device result for packet i must
+    equal the oracle's for the distinct packet it tiles (size-independent property)."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.CONFIGS[cfg]["prog"]()
+    pk = (workloads.packets_random if cfg == "c2" else workloads.packets_l2l3)(distinct, 64)
+    maps = []
+    if cfg == "c4":
+        vals = workloads.c4_map_values()
+        maps = [(8, 256, vals.tobytes())]
+    base = goldens.Case(cfg, lay.code, lay.relocs, maps, pk, distinct, 64, None)
+    want, wf, _, _ = oracle_run(base, nthreads=8)
+    assert not wf.any()
+    full = _tiled_case(cfg, base, tiles)
+    got, gf, _ = device_run(gpu, env, full, 0)
+    assert not gf.any()
+    np.testing.assert_array_equal(got.reshape(tiles, distinct), np.broadcast_to(want, (tiles, distinct)))
+
+
+def test_c5_imix_vs_oracle(gpu, env):
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c5()
+    n = 1 << 18
+    data, offs, _ = workloads.packets_imix(n)
+    c = goldens.Case("c5", lay.code, [], [], data, n, 0, offs)
+    want, wf, _, _ = oracle_run(c, nthreads=8)
+    got, gf, _ = device_run(gpu, env, c, 0)
+    np.testing.assert_array_equal(wf, gf)
+    np.testing.assert_array_equal(want, got)
+
+
+def test_device_resident_api_and_histogram(gpu, env):
+    """ebpf_prog_run_batch_dev on torch device memory, verdict histogram included."""
+    import torch
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4()
+    n = 1 << 20
+    pk = workloads.packets_l2l3(n, 64)
+    vals = workloads.c4_map_values()
+    case = goldens.Case("c4", lay.code, lay.relocs, [(8, 256, vals.tobytes())], pk, n, 64, None)
+    want, _, _, _ = oracle_run(case, nthreads=8)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+        d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream()
+        p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, d_flt.data_ptr(),
+                        d_hist.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        got = d_ret.cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(got, want)
+        h = np.zeros(257, dtype=np.int64)
+        np.add.at(h, np.minimum(want, 255).astype(np.int64), 1)
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+        assert int(d_flt.sum()) == 0
+        # a host-side map update must reach the device mirror before the next launch
+        m = maps[0]
+        m.fill(np.zeros(256, dtype=np.uint64).tobytes())
+        case2 = goldens.Case("c4z", lay.code, lay.relocs, [(8, 256, bytes(2048))], pk, n, 64, None)
+        want2, _, _, _ = oracle_run(case2, nthreads=8)
+        p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want2)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+def test_empty_and_ragged_batches(gpu, env):
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c3()
+    for n in (0, 1, 63, 65, 255, 257, 1000):
+        pk = workloads.packets_l2l3(max(n, 1), 64)[:n]
+        c = goldens.Case("c3", lay.code, [], [], pk.reshape(-1) if n else np.zeros(1, np.uint8),
+                         n, 64, None)
+        got, gf, _ = device_run(gpu, env, c, 0)
+        if n:
+            want, wf, _, _ = oracle_run(c)
+            np.testing.assert_array_equal(want, got)
+        else:
+            assert got.size == 0
