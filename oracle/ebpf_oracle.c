@@ -86,13 +86,19 @@ static const uint8_t k_valid_ops[] = {
 	0x7d, 0x85, 0x95, 0xa5, 0xad, 0xb5, 0xbd, 0xc5, 0xcd, 0xd5, 0xdd,
 };
 
+static uint8_t k_valid_tab[256];
+
+__attribute__((constructor)) static void
+init_valid_tab(void)
+{
+	for (unsigned i = 0; i < sizeof(k_valid_ops); i++)
+		k_valid_tab[k_valid_ops[i]] = 1;
+}
+
 static inline int
 valid_op(uint8_t op)
 {
-	for (unsigned i = 0; i < sizeof(k_valid_ops); i++)
-		if (k_valid_ops[i] == op)
-			return 1;
-	return 0;
+	return k_valid_tab[op];
 }
 
 /* Which opcodes name a dst / src register (reg[inst->dst] / reg[inst->src] in the reference). */
@@ -160,7 +166,8 @@ run_one(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	int fault = F_NONE;
 	uint64_t r0 = 0;
 
-	memset(stack, p->stack_init, sizeof(stack));
+	if (checked) /* raw mode leaves the stack undefined, exactly like the reference */
+		memset(stack, p->stack_init, sizeof(stack));
 	for (int i = 0; i < 11; i++)
 		reg[i] = p->reg_init;
 	reg[1] = (uint64_t)(uintptr_t)pkt;                   /* :35 */
@@ -371,13 +378,162 @@ done:
 	return r0;
 }
 
+/* Raw mode: the reference's own cost model — one switch per instruction, operands read inside
+ * each case, raw pointer memory access, no fault checks (valid programs only; used for the
+ * timed CPU baseline).  Same semantics as run_one(checked=0) on valid programs. */
+#define RD (reg[ip->dst])
+#define RS (reg[ip->src])
+#define IMM32 ((uint32_t)ip->imm)
+#define IMM64 ((uint64_t)(int64_t)ip->imm)
+#define A32(expr) RD = (uint32_t)(expr); break
+#define A64(expr) RD = (expr); break
+#define JMPIF(c) if (c) pc += (uint32_t)(int32_t)ip->offset; break
+#define MEMA(base) ((base) + (uint64_t)(int64_t)ip->offset)
+
+struct raw_inst {
+	uint8_t opcode;
+	uint8_t dst : 4;
+	uint8_t src : 4;
+	int16_t offset;
+	int32_t imm;
+};
+
+static uint64_t
+run_raw(const struct oracle_prog *p, uint8_t *pkt, uint64_t *steps_out)
+{
+	uint64_t reg[11];
+	uint8_t stack[STACK_BYTES];
+	const struct raw_inst *ip = (const struct raw_inst *)p->insns;
+	uint32_t pc = 0;
+	uint64_t steps = 0;
+	struct region_env re = {0, 0, 0, 0, p};
+	for (int i = 0; i < 11; i++)
+		reg[i] = p->reg_init;
+	reg[1] = (uint64_t)(uintptr_t)pkt;
+	reg[10] = (uint64_t)(uintptr_t)(stack + STACK_BYTES);
+	for (;;) {
+		ip += pc++;
+		steps++;
+		switch (ip->opcode) {
+		case 0x04: A32((uint32_t)RD + IMM32);
+		case 0x0c: A32((uint32_t)RD + (uint32_t)RS);
+		case 0x14: A32((uint32_t)RD - IMM32);
+		case 0x1c: A32((uint32_t)RD - (uint32_t)RS);
+		case 0x24: A32((uint32_t)RD * IMM32);
+		case 0x2c: A32((uint32_t)RD * (uint32_t)RS);
+		case 0x34: A32((uint32_t)RD / IMM32);
+		case 0x3c: A32((uint32_t)RD / (uint32_t)RS);
+		case 0x44: A32((uint32_t)RD | IMM32);
+		case 0x4c: A32((uint32_t)RD | (uint32_t)RS);
+		case 0x54: A32((uint32_t)RD & IMM32);
+		case 0x5c: A32((uint32_t)RD & (uint32_t)RS);
+		case 0x64: A32((uint32_t)RD << (IMM32 & 31));
+		case 0x6c: A32((uint32_t)RD << (RS & 31));
+		case 0x74: case 0xc4: A32((uint32_t)RD >> (IMM32 & 31));
+		case 0x7c: case 0xcc: A32((uint32_t)RD >> (RS & 31));
+		case 0x84: A32(0u - IMM32);
+		case 0x94: A32((uint32_t)RD % IMM32);
+		case 0x9c: A32((uint32_t)RD % (uint32_t)RS);
+		case 0xa4: A32((uint32_t)RD ^ IMM32);
+		case 0xac: A32((uint32_t)RD ^ (uint32_t)RS);
+		case 0xb4: A32(IMM32);
+		case 0xbc: A32((uint32_t)RS);
+		case 0xd4:
+			if (ip->imm == 16) RD = (uint16_t)RD;
+			else if (ip->imm == 32) RD = (uint32_t)RD;
+			break;
+		case 0xdc:
+			if (ip->imm == 16) RD = bs16((uint16_t)RD);
+			else if (ip->imm == 32) RD = __builtin_bswap32((uint32_t)RD);
+			else if (ip->imm == 64) RD = __builtin_bswap64(RD);
+			break;
+		case 0x07: case 0xb7: A64(RD + IMM64);
+		case 0x0f: case 0xbf: A64(RD + RS);
+		case 0x17: case 0x87: A64(RD - IMM64);
+		case 0x1f: A64(RD - RS);
+		case 0x27: A64(RD * IMM64);
+		case 0x2f: A64(RD * RS);
+		case 0x37: A64(RD / IMM64);
+		case 0x3f: A64(RD / RS);
+		case 0x47: A64(RD | IMM64);
+		case 0x4f: A64(RD | RS);
+		case 0x57: A64(RD & IMM64);
+		case 0x5f: A64(RD & RS);
+		case 0x67: A64(RD << (IMM64 & 63));
+		case 0x6f: A64(RD << (RS & 63));
+		case 0x77: case 0xc7: A64(RD >> (IMM64 & 63));
+		case 0x7f: case 0xcf: A64(RD >> (RS & 63));
+		case 0x97: A64(RD % IMM64);
+		case 0x9f: A64(RD % RS);
+		case 0xa7: A64(RD ^ IMM64);
+		case 0xaf: A64(RD ^ RS);
+		case 0x05: JMPIF(1);
+		case 0x15: JMPIF(RD == IMM64);
+		case 0x1d: JMPIF(RD == RS);
+		case 0x25: JMPIF(RD > IMM64);
+		case 0x2d: JMPIF(RD > RS);
+		case 0x35: JMPIF(RD >= IMM64);
+		case 0x3d: JMPIF(RD >= RS);
+		case 0x45: JMPIF(RD & IMM64);
+		case 0x4d: JMPIF(RD & RS);
+		case 0x55: JMPIF(RD != IMM64);
+		case 0x5d: JMPIF(RD != RS);
+		case 0x65: JMPIF((int64_t)RD > (int64_t)IMM64);
+		case 0x6d: JMPIF((int64_t)RD > (int64_t)RS);
+		case 0x75: JMPIF((int64_t)RD >= (int64_t)IMM64);
+		case 0x7d: JMPIF((int64_t)RD >= (int64_t)RS);
+		case 0xa5: JMPIF(RD < IMM64);
+		case 0xad: JMPIF(RD < RS);
+		case 0xb5: JMPIF(RD <= IMM64);
+		case 0xbd: JMPIF(RD <= RS);
+		case 0xc5: JMPIF((int64_t)RD < (int64_t)IMM64);
+		case 0xcd: JMPIF((int64_t)RD < (int64_t)RS);
+		case 0xd5: JMPIF((int64_t)RD <= (int64_t)IMM64);
+		case 0xdd: JMPIF((int64_t)RD <= (int64_t)RS);
+		case 0x85: {
+			int f = 0;
+			reg[0] = helper_map_lookup(&re, 0, reg[1], reg[2], &f);
+			break;
+		}
+		case 0x95:
+			*steps_out = steps;
+			return reg[0];
+		case 0x71: A64(load_n(MEMA(RS), 1));
+		case 0x69: A64(load_n(MEMA(RS), 2));
+		case 0x61: A64(load_n(MEMA(RS), 4));
+		case 0x79: A64(load_n(MEMA(RS), 8));
+		case 0x18:
+			RD = (uint64_t)IMM32 | ((uint64_t)(uint32_t)(ip + 1)->imm << 32);
+			pc++;
+			break;
+		case 0x73: store_n(MEMA(RD), 1, RS); break;
+		case 0x6b: store_n(MEMA(RD), 2, RS); break;
+		case 0x63: store_n(MEMA(RD), 4, RS); break;
+		case 0x7b: store_n(MEMA(RD), 8, RS); break;
+		case 0x72: store_n(MEMA(RD), 1, IMM64); break;
+		case 0x6a: store_n(MEMA(RD), 2, IMM64); break;
+		case 0x62: store_n(MEMA(RD), 4, IMM64); break;
+		case 0x7a: store_n(MEMA(RD), 8, IMM64); break;
+		default:
+			*steps_out = steps;
+			return 0;
+		}
+	}
+}
+
 uint64_t
 oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fault,
 	   uint64_t *steps)
 {
 	if (p->checked)
 		return run_one(p, 1, pkt, len, fault, steps);
-	return run_one(p, 0, pkt, len, fault, steps);
+	uint64_t st = 0;
+	uint64_t r = run_raw(p, pkt, &st);
+	if (fault)
+		*fault = 0;
+	if (steps)
+		*steps = st;
+	return r;
 }
 
 uint64_t
