@@ -1,0 +1,1010 @@
+#!/usr/bin/env python3
+"""Generate the hand-written gfx950 (CDNA4) assembly interpreter for the device program.
+
+Output: <out>.s (the code object source: two interpreter kernels sharing one handler set, the
+handler linker kernel, the handler offset table) and <out>.h (handler family ids for the host
+lowering in asm_runtime.cpp).
+
+Execution model (one lane = one packet, wavefront-lockstep dispatch):
+  * eBPF register rK lives in v[2K:2K+1] (VGPRs, never memory);
+  * every handler is specialised for its (operation, dst, src) so no register is indexed at
+    run time; a dispatch is  s_load_dwordx8 entry -> s_waitcnt -> s_setpc_b64 handler;
+  * the wave-uniform entry (32 B, dprog.h layout with `handler` linked to an absolute code
+    address) is fetched with scalar loads (K$), so decoding costs no VALU;
+  * in the staged kernel each lane's 64-B packet is loaded with 4 x global_load_dwordx4 into
+    v22..v37 and packet loads at translation-time-known offsets read registers;
+  * the 512-B eBPF stack lives in LDS (per-lane slice sized from the translated program);
+  * lanes that disagree on a conditional jump are parked (v41 = their entry) and resumed after
+    the running group retires; retirement writes r0, the fault code and an LDS histogram.
+"""
+import sys
+
+NREG = 11
+# ---------------------------------------------------------------- register plan
+PKT0 = 22            # v22..v37 staged packet dwords (staged kernel)
+V_PKT = 38           # v[38:39] packet base address
+V_LEN = 40           # packet length (bytes)
+V_T = 41             # parked entry byte offset
+V_STK = 42           # lane stack bottom (LDS byte address)
+V_GID = 43           # packet index within the launch
+V_ONE = 45           # constant 1
+H = [46, 47, 48, 49, 50, 51]         # handler temporaries
+R = list(range(52, 64))              # routine temporaries
+NVGPR = 64
+
+# SGPRs
+S_ENT = 8            # s[8:15] current entry: s[8:9] handler, s[10:11] imm, s12 next, s13 target,
+                     # s14 aux0, s15 aux1
+S_ALIVE = 16         # s[16:17]
+S_SAVE = 18          # s[18:19]
+S_PROG, S_MAPS, S_DATA, S_OFFS, S_OFFBASE, S_RET, S_FAULTS, S_HIST = 20, 22, 24, 26, 28, 30, 32, 34
+S_COUNT, S_STRIDE, S_START, S_NMAPS, S_NENT = 36, 38, 39, 40, 41
+S_STKSTRIDE, S_LDSBASE = 42, 43      # from dp_launch tail
+S_GROUP, S_GSTRIDE, S_NGROUPS = 44, 45, 46
+S_MASK = 48          # s[48:49] temp mask
+S_LINK = 50          # s[50:51] subroutine return address
+S_CODE = 52          # fault code argument
+S_T0, S_T1, S_T2, S_T3 = 53, 54, 55, 56
+S_SHARED = 58        # s[58:59] src_shared_base
+S_JUNK = 60          # s[60:61] scratch sdst
+S_WAVE = 62
+S_SEL16, S_SEL32 = 63, 64
+# routine addresses
+S_R_SCHED, S_R_DIVERGE, S_R_FAULT, S_R_EXIT, S_R_DIV, S_R_CHECK, S_R_LOOKUP = 66, 68, 70, 72, 74, 76, 78
+NSGPR = 96
+
+ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
+ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
+ALU64I = ["ADD", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD", "MOV"]   # MOV = LDDW
+ALU32I = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
+CONDS = ["JEQ", "JNE", "JGT", "JGE", "JLT", "JLE", "JSGT", "JSGE", "JSLT", "JSLE", "JSET"]
+SIZES = [1, 2, 4, 8]
+
+FAMILIES = []   # (name, arity) arity: 2 = (dst, src), 1 = (reg), 0
+
+
+def fam(name, arity):
+    FAMILIES.append((name, arity))
+
+
+for o in ALU64R:
+    fam("A64R_" + o, 2)
+for o in ALU32R:
+    fam("A32R_" + o, 2)
+for c in CONDS:
+    fam(c + "_R", 2)
+for z in SIZES:
+    fam("LDXGEN%d" % z, 2)
+for z in SIZES:
+    fam("STXGEN%d" % z, 2)
+for o in ALU64I:
+    fam("A64I_" + o, 1)
+for o in ALU32I:
+    fam("A32I_" + o, 1)
+for w in (16, 32, 64):
+    fam("BSWAP%d" % w, 1)
+for c in CONDS:
+    fam(c + "_I", 1)
+for z in SIZES:
+    fam("LDXPKTS%d" % z, 1)
+for z in SIZES:
+    fam("LDXPKTG%d" % z, 1)
+for z in SIZES:
+    fam("LDXSTK%d" % z, 1)
+for z in SIZES:
+    fam("STXSTK%d" % z, 1)
+for z in SIZES:
+    fam("STGEN%d" % z, 1)
+for z in SIZES:
+    fam("STSTK%d" % z, 0)
+for n in ("EXIT", "FAULT", "NOP", "LOOKUPSTK", "LOOKUPGEN"):
+    fam(n, 0)
+
+
+def variants(arity):
+    if arity == 2:
+        return [(d, s) for d in range(NREG) for s in range(NREG)]
+    if arity == 1:
+        return [(d, None) for d in range(NREG)]
+    return [(None, None)]
+
+
+def lo(r):
+    return "v%d" % (2 * r)
+
+
+def hi(r):
+    return "v%d" % (2 * r + 1)
+
+
+def pair(r):
+    return "v[%d:%d]" % (2 * r, 2 * r + 1)
+
+
+def v(i):
+    return "v%d" % i
+
+
+def vp(i):
+    return "v[%d:%d]" % (i, i + 1)
+
+
+def s(i):
+    return "s%d" % i
+
+
+def sp(i):
+    return "s[%d:%d]" % (i, i + 1)
+
+
+def dispatch(next_reg=12):
+    return ["s_mov_b32 s6, s%d" % next_reg,
+            "s_load_dwordx8 s[8:15], s[%d:%d], s6" % (S_PROG, S_PROG + 1),
+            "s_waitcnt lgkmcnt(0)",
+            "s_setpc_b64 s[8:9]"]
+
+
+def call(routine_sgpr):
+    return ["s_swappc_b64 %s, %s" % (sp(S_LINK), sp(routine_sgpr))]
+
+
+def fault_mask(mask_sgpr_pair, code):
+    """Retire the lanes in s[mask] with fault `code`; returns (or never, if none remain)."""
+    out = []
+    if mask_sgpr_pair != S_MASK:
+        out.append("s_mov_b64 %s, %s" % (sp(S_MASK), sp(mask_sgpr_pair)))
+    out += ["s_mov_b32 %s, %d" % (s(S_CODE), code)] + call(S_R_FAULT)
+    return out
+
+
+# ---------------------------------------------------------------- handler bodies
+def h_alu64r(op, d, sr):
+    D0, D1, S0, S1 = lo(d), hi(d), lo(sr), hi(sr)
+    t = H
+    if op == "ADD":
+        return ["v_lshl_add_u64 %s, %s, 0, %s" % (pair(d), pair(sr), pair(d))]
+    if op == "SUB":
+        return ["v_sub_co_u32 %s, vcc, %s, %s" % (D0, D0, S0),
+                "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (D1, D1, S1)]
+    if op == "MUL":
+        return ["v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t[0]), sp(S_JUNK), D0, S0),
+                "v_mul_lo_u32 %s, %s, %s" % (v(t[2]), D0, S1),
+                "v_mul_lo_u32 %s, %s, %s" % (v(t[3]), D1, S0),
+                "v_add3_u32 %s, %s, %s, %s" % (D1, v(t[1]), v(t[2]), v(t[3])),
+                "v_mov_b32 %s, %s" % (D0, v(t[0]))]
+    if op in ("OR", "AND", "XOR"):
+        m = {"OR": "v_or_b32", "AND": "v_and_b32", "XOR": "v_xor_b32"}[op]
+        return ["%s %s, %s, %s" % (m, D0, D0, S0), "%s %s, %s, %s" % (m, D1, D1, S1)]
+    if op == "LSH":
+        return ["v_lshlrev_b64 %s, %s, %s" % (pair(d), S0, pair(d))]
+    if op == "RSH":
+        return ["v_lshrrev_b64 %s, %s, %s" % (pair(d), S0, pair(d))]
+    if op in ("DIV", "MOD"):
+        return divmod_body(d, sr, None, op, 64)
+    raise ValueError(op)
+
+
+def h_alu32r(op, d, sr):
+    D0, D1, S0 = lo(d), hi(d), lo(sr)
+    body = {
+        "ADD": ["v_add_u32 %s, %s, %s" % (D0, D0, S0)],
+        "SUB": ["v_sub_u32 %s, %s, %s" % (D0, D0, S0)],
+        "MUL": ["v_mul_lo_u32 %s, %s, %s" % (D0, D0, S0)],
+        "OR": ["v_or_b32 %s, %s, %s" % (D0, D0, S0)],
+        "AND": ["v_and_b32 %s, %s, %s" % (D0, D0, S0)],
+        "XOR": ["v_xor_b32 %s, %s, %s" % (D0, D0, S0)],
+        "LSH": ["v_lshlrev_b32 %s, %s, %s" % (D0, S0, D0)],
+        "RSH": ["v_lshrrev_b32 %s, %s, %s" % (D0, S0, D0)],
+        "MOV": ["v_mov_b32 %s, %s" % (D0, S0)],
+    }
+    if op in ("DIV", "MOD"):
+        return divmod_body(d, sr, None, op, 32)
+    return body[op] + ["v_mov_b32 %s, 0" % D1]
+
+
+def h_alu64i(op, d):
+    D0, D1 = lo(d), hi(d)
+    t = H
+    if op == "ADD":
+        return ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (pair(d), pair(d))]
+    if op == "MUL":
+        return ["v_mad_u64_u32 %s, %s, %s, s10, 0" % (vp(t[0]), sp(S_JUNK), D0),
+                "v_mul_lo_u32 %s, %s, s11" % (v(t[2]), D0),
+                "v_mul_lo_u32 %s, %s, s10" % (v(t[3]), D1),
+                "v_add3_u32 %s, %s, %s, %s" % (D1, v(t[1]), v(t[2]), v(t[3])),
+                "v_mov_b32 %s, %s" % (D0, v(t[0]))]
+    if op in ("OR", "AND", "XOR"):
+        m = {"OR": "v_or_b32", "AND": "v_and_b32", "XOR": "v_xor_b32"}[op]
+        return ["%s %s, s10, %s" % (m, D0, D0), "%s %s, s11, %s" % (m, D1, D1)]
+    if op == "LSH":
+        return ["v_lshlrev_b64 %s, s10, %s" % (pair(d), pair(d))]
+    if op == "RSH":
+        return ["v_lshrrev_b64 %s, s10, %s" % (pair(d), pair(d))]
+    if op == "MOV":
+        return ["v_mov_b32 %s, s10" % D0, "v_mov_b32 %s, s11" % D1]
+    if op in ("DIV", "MOD"):
+        return divmod_body(d, None, True, op, 64)
+    raise ValueError(op)
+
+
+def h_alu32i(op, d):
+    D0, D1 = lo(d), hi(d)
+    body = {
+        "ADD": ["v_add_u32 %s, s10, %s" % (D0, D0)],
+        "SUB": ["v_subrev_u32 %s, s10, %s" % (D0, D0)],
+        "MUL": ["v_mul_lo_u32 %s, %s, s10" % (D0, D0)],
+        "OR": ["v_or_b32 %s, s10, %s" % (D0, D0)],
+        "AND": ["v_and_b32 %s, s10, %s" % (D0, D0)],
+        "XOR": ["v_xor_b32 %s, s10, %s" % (D0, D0)],
+        "LSH": ["v_lshlrev_b32 %s, s10, %s" % (D0, D0)],
+        "RSH": ["v_lshrrev_b32 %s, s10, %s" % (D0, D0)],
+        "MOV": ["v_mov_b32 %s, s10" % D0],
+    }
+    if op in ("DIV", "MOD"):
+        return divmod_body(d, None, True, op, 32)
+    return body[op] + ["v_mov_b32 %s, 0" % D1]
+
+
+def divmod_body(d, sr, imm, op, bits):
+    """Operands to R[0:1] (n) and R[2:3] (den); lanes with den == 0 fault DIV_ZERO (the
+    reference raises SIGFPE); quotient / remainder from the shared restoring divider."""
+    n0, n1, d0, d1 = v(R[0]), v(R[1]), v(R[2]), v(R[3])
+    out = ["v_mov_b32 %s, %s" % (n0, lo(d))]
+    out.append("v_mov_b32 %s, %s" % (n1, hi(d) if bits == 64 else "0"))
+    if imm:
+        out += ["v_mov_b32 %s, s10" % d0, "v_mov_b32 %s, %s" % (d1, "s11" if bits == 64 else "0")]
+    else:
+        out += ["v_mov_b32 %s, %s" % (d0, lo(sr)),
+                "v_mov_b32 %s, %s" % (d1, hi(sr) if bits == 64 else "0")]
+    if not imm:  # immediate divisors are never 0 here (the translator faults them statically)
+        out += ["v_cmp_eq_u64_e64 %s, %s, 0" % (sp(S_MASK), vp(R[2])),
+                "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+                "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+                "s_cbranch_scc1 .Ldz_%s" % "{uid}"]
+        out += fault_mask(S_MASK, 2)
+        out.append(".Ldz_{uid}:")
+    out += call(S_R_DIV)
+    q0, q1, r0, r1 = v(R[4]), v(R[5]), v(R[6]), v(R[7])
+    src = (q0, q1) if op == "DIV" else (r0, r1)
+    out += ["v_mov_b32 %s, %s" % (lo(d), src[0]),
+            "v_mov_b32 %s, %s" % (hi(d), src[1] if bits == 64 else "0")]
+    return out
+
+
+CMP = {"JEQ": "eq_u64", "JNE": "ne_u64", "JGT": "gt_u64", "JGE": "ge_u64", "JLT": "lt_u64",
+       "JLE": "le_u64", "JSGT": "gt_i64", "JSGE": "ge_i64", "JSLT": "lt_i64", "JSLE": "le_i64"}
+
+
+def h_cond(c, d, sr, imm):
+    srcop = "s[10:11]" if imm else pair(sr)
+    out = []
+    if c == "JSET":
+        if imm:
+            out += ["v_and_b32 %s, s10, %s" % (v(H[0]), lo(d)),
+                    "v_and_b32 %s, s11, %s" % (v(H[1]), hi(d))]
+        else:
+            out += ["v_and_b32 %s, %s, %s" % (v(H[0]), lo(d), lo(sr)),
+                    "v_and_b32 %s, %s, %s" % (v(H[1]), hi(d), hi(sr))]
+        out.append("v_cmp_ne_u64_e64 vcc, %s, 0" % vp(H[0]))
+    else:
+        out.append("v_cmp_%s_e64 vcc, %s, %s" % (CMP[c], pair(d), srcop))
+    out += ["s_and_b64 %s, vcc, exec" % sp(S_MASK),
+            "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
+            "s_cbranch_scc1 .Ltk_{uid}",
+            "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+            "s_cbranch_scc1 .Lnt_{uid}",
+            "s_setpc_b64 %s" % sp(S_R_DIVERGE),
+            ".Ltk_{uid}:"] + dispatch(13) + [".Lnt_{uid}:"] + dispatch(12)
+    return out, True   # (body, has own dispatch)
+
+
+def h_bswap(w, d):
+    D0, D1 = lo(d), hi(d)
+    if w == 16:
+        return ["v_perm_b32 %s, 0, %s, %s" % (D0, D0, s(S_SEL16)), "v_mov_b32 %s, 0" % D1]
+    if w == 32:
+        return ["v_perm_b32 %s, 0, %s, %s" % (D0, D0, s(S_SEL32)), "v_mov_b32 %s, 0" % D1]
+    return ["v_perm_b32 %s, 0, %s, %s" % (v(H[0]), D0, s(S_SEL32)),
+            "v_perm_b32 %s, 0, %s, %s" % (D0, D1, s(S_SEL32)),
+            "v_mov_b32 %s, %s" % (D1, v(H[0]))]
+
+
+def h_ldx_pkt_staged(z, d):
+    """s10 = dword index k of the packet byte offset, s11 = byte shift (offset % 4)."""
+    t0, t1, t2 = v(H[0]), v(H[1]), v(H[2])
+    out = ["s_set_gpr_idx_on s10, gpr_idx(SRC0)",
+           "v_mov_b32 %s, v%d" % (t0, PKT0),
+           "v_mov_b32 %s, v%d" % (t1, PKT0 + 1)]
+    if z == 8:
+        out.append("v_mov_b32 %s, v%d" % (t2, PKT0 + 2))
+    out.append("s_set_gpr_idx_off")
+    D0, D1 = lo(d), hi(d)
+    if z == 8:
+        out += ["v_alignbyte_b32 %s, %s, %s, s11" % (D0, t1, t0),
+                "v_alignbyte_b32 %s, %s, %s, s11" % (D1, t2, t1)]
+    elif z == 4:
+        out += ["v_alignbyte_b32 %s, %s, %s, s11" % (D0, t1, t0), "v_mov_b32 %s, 0" % D1]
+    else:
+        out += ["v_alignbyte_b32 %s, %s, %s, s11" % (t0, t1, t0),
+                "v_and_b32 %s, %s, %s" % (D0, "0xff" if z == 1 else "0xffff", t0),
+                "v_mov_b32 %s, 0" % D1]
+    return out
+
+
+LOADS = {1: "global_load_ubyte", 2: "global_load_ushort", 4: "global_load_dword",
+         8: "global_load_dwordx2"}
+
+
+def h_ldx_pkt_general(z, d):
+    """s[10:11] = packet byte offset (>= 0); per-lane bound check against the packet length."""
+    t = H
+    out = ["v_mov_b32 %s, s10" % v(t[0]),
+           "v_add_u32 %s, %d, %s" % (v(t[0]), z, v(t[0])),
+           "v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_MASK), v(t[0]), v(V_LEN)),
+           "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+           "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+           "s_cbranch_scc1 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:"]
+    out.append("v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(t[0]), vp(V_PKT)))
+    if z == 8:
+        out.append("%s %s, %s, off" % (LOADS[8], pair(d), vp(t[0])))
+    else:
+        out += ["%s %s, %s, off" % (LOADS[z], lo(d), vp(t[0])), "v_mov_b32 %s, 0" % hi(d)]
+    out.append("s_waitcnt vmcnt(0)")
+    return out
+
+
+DS_R = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32"}
+DS_W = {1: "ds_write_b8", 2: "ds_write_b16", 4: "ds_write_b32"}
+
+
+def h_ldx_stk(z, d):
+    """s10 = LDS byte offset from the lane's stack bottom (aligned to min(z, 4))."""
+    a = v(H[0])
+    out = ["v_add_u32 %s, s10, v%d" % (a, V_STK)]
+    if z == 8:
+        out.append("ds_read2_b32 %s, %s offset1:1" % (pair(d), a))
+    else:
+        out += ["%s %s, %s" % (DS_R[z], lo(d), a), "v_mov_b32 %s, 0" % hi(d)]
+    return out   # the dispatch's lgkmcnt(0) waits for the LDS read
+
+
+def h_stx_stk(z, sr):
+    a = v(H[0])
+    out = ["v_add_u32 %s, s10, v%d" % (a, V_STK)]
+    if z == 8:
+        out.append("ds_write2_b32 %s, %s, %s offset1:1" % (a, lo(sr), hi(sr)))
+    else:
+        out.append("%s %s, %s" % (DS_W[z], a, lo(sr)))
+    return out
+
+
+def h_st_stk(z):
+    """s[10:11] = value (sign-extended imm), s14 = LDS offset."""
+    a, x0, x1 = v(H[0]), v(H[1]), v(H[2])
+    out = ["v_add_u32 %s, s14, v%d" % (a, V_STK), "v_mov_b32 %s, s10" % x0]
+    if z == 8:
+        out += ["v_mov_b32 %s, s11" % x1, "ds_write2_b32 %s, %s, %s offset1:1" % (a, x0, x1)]
+    else:
+        out.append("%s %s, %s" % (DS_W[z], a, x0))
+    return out
+
+
+def h_ldx_gen(z, d, sr):
+    """Generic load: address = r_src + sext(off) (s[10:11]); region check, then byte-wise
+    flat loads (packet/map in global memory, stack in LDS via the shared aperture)."""
+    a0 = H[0]
+    out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 0" % s(S_T1)] + call(S_R_CHECK)
+    # byte-wise gather (alignment-agnostic)
+    acc = [v(H[2]), v(H[3])]
+    out += ["v_mov_b32 %s, 0" % acc[0], "v_mov_b32 %s, 0" % acc[1]]
+    for b in range(z):
+        out.append("flat_load_ubyte %s, %s offset:%d" % (v(H[4]), vp(a0), b))
+        out.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        tgt = acc[b // 4]
+        out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(H[4]), 8 * (b % 4), tgt))
+    out += ["v_mov_b32 %s, %s" % (lo(d), acc[0]), "v_mov_b32 %s, %s" % (hi(d), acc[1])]
+    return out
+
+
+def store_bytes(a0, vals, z):
+    out = []
+    for b in range(z):
+        src = vals[b // 4]
+        if b % 4:
+            out.append("v_lshrrev_b32 %s, %d, %s" % (v(H[4]), 8 * (b % 4), src))
+            out.append("flat_store_byte %s, %s offset:%d" % (vp(a0), v(H[4]), b))
+        else:
+            out.append("flat_store_byte %s, %s offset:%d" % (vp(a0), src, b))
+    out.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    return out
+
+
+def h_stx_gen(z, d, sr):
+    a0 = H[0]
+    out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(d)),
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(S_R_CHECK)
+    out += ["v_mov_b32 %s, %s" % (v(H[2]), lo(sr)), "v_mov_b32 %s, %s" % (v(H[3]), hi(sr))]
+    return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
+
+
+def h_st_gen(z, d):
+    """s[10:11] = value, s14 = sign-extended... no: offset comes in s15 (aux1, s16 off)."""
+    a0 = H[0]
+    out = ["s_ashr_i32 %s, s15, 31" % s(S_T3),
+           "v_mov_b32 %s, s15" % v(H[2]), "v_mov_b32 %s, %s" % (v(H[3]), s(S_T3)),
+           "v_lshl_add_u64 %s, %s, 0, %s" % (vp(a0), vp(H[2]), pair(d)),
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(S_R_CHECK)
+    out += ["v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3])]
+    return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
+
+
+def h_lookup_stk():
+    """r0 = lookup(map, *(u32*)(r10 + c)) with the map resolved at translation time:
+    s[10:11] = device base of the map mirror, s13 = max_entries, s14 = key LDS offset,
+    s15 = value_size (ebpf_map.c:77-84 -> ebpf_map_array.c:115-124)."""
+    k, vs = v(H[0]), v(H[1])
+    return ["v_add_u32 %s, s14, v%d" % (k, V_STK),
+            "ds_read_b32 %s, %s" % (k, k),
+            "v_mov_b32 %s, s15" % vs,
+            "s_waitcnt lgkmcnt(0)",
+            "v_cmp_gt_u32_e64 vcc, s13, %s" % k,
+            "v_mad_u64_u32 %s, %s, %s, %s, s[10:11]" % (vp(H[2]), sp(S_JUNK), k, vs),
+            "v_cndmask_b32 v0, 0, %s, vcc" % v(H[2]),
+            "v_cndmask_b32 v1, 0, %s, vcc" % v(H[3])]
+
+
+# ---------------------------------------------------------------- handler emission
+def handler_body(name, d, sr):
+    """Returns (lines, has_dispatch)."""
+    if name.startswith("A64R_"):
+        return h_alu64r(name[5:], d, sr), False
+    if name.startswith("A32R_"):
+        return h_alu32r(name[5:], d, sr), False
+    if name.startswith("A64I_"):
+        return h_alu64i(name[5:], d), False
+    if name.startswith("A32I_"):
+        return h_alu32i(name[5:], d), False
+    if name.startswith("BSWAP"):
+        return h_bswap(int(name[5:]), d), False
+    for c in CONDS:
+        if name == c + "_R":
+            return h_cond(c, d, sr, False)
+        if name == c + "_I":
+            return h_cond(c, d, None, True)
+    if name.startswith("LDXPKTS"):
+        return h_ldx_pkt_staged(int(name[7:]), d), False
+    if name.startswith("LDXPKTG"):
+        return h_ldx_pkt_general(int(name[7:]), d), False
+    if name.startswith("LDXSTK"):
+        return h_ldx_stk(int(name[6:]), d), False
+    if name.startswith("STXSTK"):
+        return h_stx_stk(int(name[6:]), d), False
+    if name.startswith("STSTK"):
+        return h_st_stk(int(name[5:])), False
+    if name.startswith("LDXGEN"):
+        return h_ldx_gen(int(name[6:]), d, sr), False
+    if name.startswith("STXGEN"):
+        return h_stx_gen(int(name[6:]), d, sr), False
+    if name.startswith("STGEN"):
+        return h_st_gen(int(name[5:]), d), False
+    if name == "EXIT":
+        return ["s_setpc_b64 %s" % sp(S_R_EXIT)], True
+    if name == "FAULT":
+        return ["s_mov_b32 %s, s14" % s(S_CODE), "s_mov_b64 %s, exec" % sp(S_MASK)] + \
+            call(S_R_FAULT) + ["s_endpgm"], True
+    if name == "NOP":
+        return [], False
+    if name == "LOOKUPSTK":
+        return h_lookup_stk(), False
+    if name == "LOOKUPGEN":
+        return call(S_R_LOOKUP), False
+    raise ValueError(name)
+
+
+# ---------------------------------------------------------------- shared routines
+def routines():
+    L = []
+    q0, q1, r0_, r1_ = R[4], R[5], R[6], R[7]
+
+    # --- schedule: pick the parked group of the first live lane
+    L += [".Lr_schedule:",
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          "s_cbranch_execz .Lgroup_done",
+          "s_ff1_i32_b64 %s, exec" % s(S_T0),
+          "v_readlane_b32 s6, v%d, %s" % (V_T, s(S_T0)),
+          "v_cmp_eq_u32_e64 %s, s6, v%d" % (sp(S_MASK), V_T),
+          "s_and_b64 exec, %s, %s" % (sp(S_MASK), sp(S_ALIVE)),
+          "s_load_dwordx8 s[8:15], s[%d:%d], s6" % (S_PROG, S_PROG + 1),
+          "s_waitcnt lgkmcnt(0)",
+          "s_setpc_b64 s[8:9]"]
+    # --- diverge: taken lanes (s[mask]) park at the target, the rest continue
+    L += [".Lr_diverge:",
+          "s_mov_b64 %s, exec" % sp(S_SAVE),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "v_mov_b32 v%d, s13" % V_T,
+          "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK))] + dispatch(12)
+    # EXIT: value r0
+    L += [".Lr_exit:",
+          "v_mov_b32 %s, 8" % v(R[8]),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_RET)),
+          "global_store_dwordx2 %s, v[0:1], off" % vp(R[10]),
+          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
+          "s_cbranch_scc1 .Lex_nofault",
+          "v_mov_b32 %s, 1" % v(R[8]),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_FAULTS)),
+          "v_mov_b32 %s, 0" % v(R[8]),
+          "global_store_byte %s, %s, off" % (vp(R[10]), v(R[8])),
+          ".Lex_nofault:",
+          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
+          "s_cbranch_scc1 .Lex_nohist",
+          "v_mov_b32 %s, 255" % v(R[8]),
+          "v_mov_b32 %s, 0" % v(R[9]),
+          "v_cmp_lt_u64_e64 vcc, v[0:1], %s" % vp(R[8]),
+          "v_cndmask_b32 %s, %s, v0, vcc" % (v(R[8]), v(R[8])),
+          "v_lshlrev_b32 %s, 2, %s" % (v(R[8]), v(R[8])),
+          "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
+          ".Lex_nohist:",
+          "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE)),
+          "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+    # FAULT: lanes s[mask], code s[S_CODE]; returns via s[link] unless no lane remains
+    L += [".Lr_fault:",
+          "s_mov_b64 %s, exec" % sp(S_SAVE),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "v_mov_b32 %s, 8" % v(R[8]),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_RET)),
+          "v_mov_b32 %s, 0" % v(R[8]),
+          "v_mov_b32 %s, 0" % v(R[9]),
+          "global_store_dwordx2 %s, %s, off" % (vp(R[10]), vp(R[8])),
+          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
+          "s_cbranch_scc1 .Lfl_nofault",
+          "v_mov_b32 %s, 1" % v(R[8]),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_FAULTS)),
+          "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
+          "global_store_byte %s, %s, off" % (vp(R[10]), v(R[8])),
+          ".Lfl_nofault:",
+          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
+          "s_cbranch_scc1 .Lfl_nohist",
+          "v_mov_b32 %s, 1024" % v(R[8]),
+          "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
+          ".Lfl_nohist:",
+          "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          "s_andn2_b64 %s, %s, %s" % (sp(S_ALIVE), sp(S_ALIVE), sp(S_MASK)),
+          "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
+          "s_cbranch_execz .Lfl_none",
+          "s_setpc_b64 %s" % sp(S_LINK),
+          ".Lfl_none:",
+          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+    # UDIVMOD64: n = R[0:1], d = R[2:3] (non-zero) -> q = R[4:5], r = R[6:7]; clobbers R[8:9]
+    n, dd, q, r = vp(R[0]), vp(R[2]), vp(R[4]), vp(R[6])
+    L += [".Lr_udiv:",
+          "v_mov_b32 %s, 0" % v(R[4]), "v_mov_b32 %s, 0" % v(R[5]),
+          "v_mov_b32 %s, 0" % v(R[6]), "v_mov_b32 %s, 0" % v(R[7]),
+          "s_mov_b32 %s, 64" % s(S_T2),
+          ".Ludiv_loop:",
+          "v_lshlrev_b64 %s, 1, %s" % (r, r),
+          "v_lshrrev_b32 %s, 31, %s" % (v(R[8]), v(R[1])),
+          "v_or_b32 %s, %s, %s" % (v(R[6]), v(R[6]), v(R[8])),
+          "v_lshlrev_b64 %s, 1, %s" % (n, n),
+          "v_lshlrev_b64 %s, 1, %s" % (q, q),
+          "v_cmp_ge_u64_e64 vcc, %s, %s" % (r, dd),
+          "v_sub_co_u32 %s, %s, %s, %s" % (v(R[8]), sp(S_JUNK), v(R[6]), v(R[2])),
+          "v_subb_co_u32 %s, %s, %s, %s, %s" % (v(R[9]), sp(S_JUNK), v(R[7]), v(R[3]), sp(S_JUNK)),
+          "v_cndmask_b32 %s, %s, %s, vcc" % (v(R[6]), v(R[6]), v(R[8])),
+          "v_cndmask_b32 %s, %s, %s, vcc" % (v(R[7]), v(R[7]), v(R[9])),
+          "v_cndmask_b32 %s, 0, 1, vcc" % v(R[8]),
+          "v_or_b32 %s, %s, %s" % (v(R[4]), v(R[4]), v(R[8])),
+          "s_sub_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_cmp_lg_u32 %s, 0" % s(S_T2),
+          "s_cbranch_scc1 .Ludiv_loop",
+          "s_setpc_b64 %s" % sp(S_LINK)]
+    # CHECK: address H[0:1], size s[S_T0], write s[S_T1]; lanes outside every region fault
+    # (MEM, or MAP_WRITE for a store into a map value); returns with exec = good lanes.
+    a = vp(H[0])
+    ok = sp(S_SAVE)           # accumulated ok mask
+    u = vp(R[0])
+    L += [".Lr_check:",
+          "s_mov_b64 %s, 0" % ok,
+          # packet: u = a - pkt; u_hi == 0 && len >= size && u_lo <= len - size
+          "v_sub_co_u32 %s, vcc, %s, v%d" % (v(R[0]), v(H[0]), V_PKT),
+          "v_subb_co_u32 %s, vcc, %s, v%d, vcc" % (v(R[1]), v(H[1]), V_PKT + 1),
+          "v_subrev_u32 %s, %s, v%d" % (v(R[2]), s(S_T0), V_LEN),
+          "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
+          "v_cmp_ge_u32_e64 vcc, v%d, %s" % (V_LEN, s(S_T0)),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "v_cmp_le_u32_e64 vcc, %s, %s" % (v(R[0]), v(R[2])),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
+          # stack: u = a - {shared_hi : v42}; u_hi == 0 && u_lo <= stride - size
+          "v_sub_co_u32 %s, vcc, %s, v%d" % (v(R[0]), v(H[0]), V_STK),
+          "v_mov_b32 %s, %s" % (v(R[3]), s(S_SHARED + 1)),
+          "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[3])),
+          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_STKSTRIDE), s(S_T0)),
+          "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
+          "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_T3), v(R[0])),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_cmp_ge_u32 %s, %s" % (s(S_STKSTRIDE), s(S_T0)),
+          "s_cselect_b64 %s, %s, 0" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
+          # maps: for m in table
+          "s_mov_b32 %s, 0" % s(S_T2),
+          ".Lck_map_loop:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
+          "s_cbranch_scc1 .Lck_map_done",
+          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx4 s[80:83], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_add_u32 %s, %s, 16" % (s(S_T3), s(S_T3)),
+          "s_load_dwordx2 s[84:85], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_waitcnt lgkmcnt(0)",
+          # s[82:83] = dev_base, s84 = value_size, s85 = max_entries
+          "s_mul_i32 %s, s84, s85" % s(S_T3),
+          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_T3), s(S_T0)),
+          "v_mov_b32 %s, s83" % v(R[3]),
+          "v_sub_co_u32 %s, vcc, %s, s82" % (v(R[0]), v(H[0])),
+          "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[3])),
+          "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
+          "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_T3), v(R[0])),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_mul_i32 s86, s84, s85",
+          "s_cmp_ge_u32 s86, %s" % s(S_T0),
+          "s_cselect_b64 %s, %s, 0" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_cmp_eq_u32 %s, 0" % s(S_T1),
+          "s_cbranch_scc1 .Lck_map_ok",
+          # a store into a map value: MAP_WRITE fault for those lanes
+          "s_cmp_eq_u64 %s, 0" % sp(S_JUNK),
+          "s_cbranch_scc1 .Lck_map_next",
+          "s_mov_b64 %s, %s" % (sp(S_MASK), sp(S_JUNK)),
+          "s_mov_b32 %s, 9" % s(S_CODE),
+          "s_mov_b64 s[86:87], %s" % sp(S_LINK),
+          "s_mov_b64 s[80:81], %s" % ok,
+          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_FAULT)),
+          "s_mov_b64 %s, s[86:87]" % sp(S_LINK),
+          "s_mov_b64 %s, s[80:81]" % ok,
+          "s_branch .Lck_map_next",
+          ".Lck_map_ok:",
+          "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
+          ".Lck_map_next:",
+          "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_branch .Lck_map_loop",
+          ".Lck_map_done:",
+          "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), ok),
+          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+          "s_cbranch_scc1 .Lck_ret",
+          "s_mov_b32 %s, 3" % s(S_CODE),
+          "s_setpc_b64 %s" % sp(S_R_FAULT),   # tail call: returns to our caller
+          ".Lck_ret:",
+          "s_setpc_b64 %s" % sp(S_LINK)]
+    # LOOKUP (generic): r0 = lookup(r1, r2) for any r1/r2 (NULL -> NULL, unknown map -> BAD_MAP)
+    L += [".Lr_lookup:",
+          "s_mov_b64 s[86:87], %s" % sp(S_LINK),
+          "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
+          # lanes with r1 == 0 or r2 == 0 keep r0 = NULL
+          "v_cmp_ne_u64_e64 %s, v[2:3], 0" % sp(S_JUNK),
+          "v_cmp_ne_u64_e64 vcc, v[4:5], 0",
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_mov_b64 s[88:89], exec",
+          "s_mov_b64 exec, %s" % sp(S_JUNK),
+          "s_cbranch_execz .Llk_done",
+          # which lanes name a known map
+          "s_mov_b64 s[90:91], 0",
+          "s_mov_b32 %s, 0" % s(S_T2),
+          ".Llk_scan:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
+          "s_cbranch_scc1 .Llk_scan_done",
+          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx2 s[80:81], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_waitcnt lgkmcnt(0)",
+          "v_cmp_eq_u64_e64 vcc, v[2:3], s[80:81]",
+          "s_or_b64 s[90:91], s[90:91], vcc",
+          "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_branch .Llk_scan",
+          ".Llk_scan_done:",
+          "s_andn2_b64 %s, exec, s[90:91]" % sp(S_MASK),
+          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+          "s_cbranch_scc1 .Llk_known",
+          "s_mov_b32 %s, 10" % s(S_CODE),
+          "s_andn2_b64 s[88:89], s[88:89], %s" % sp(S_MASK),
+          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_FAULT)),
+          ".Llk_known:",
+          # key = *(u32*)r2, region checked
+          "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1]),
+          "s_mov_b32 %s, 4" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1),
+          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_CHECK)),
+          "s_and_b64 s[88:89], s[88:89], -1"]   # (check may have retired lanes: alive updated)
+    key = v(H[2])
+    L += ["v_mov_b32 %s, 0" % key]
+    for b in range(4):
+        L += ["flat_load_ubyte %s, %s offset:%d" % (v(H[3]), vp(H[0]), b),
+              "s_waitcnt vmcnt(0) lgkmcnt(0)",
+              "v_lshl_or_b32 %s, %s, %d, %s" % (key, v(H[3]), 8 * b, key)]
+    L += ["s_mov_b32 %s, 0" % s(S_T2),
+          ".Llk_map:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
+          "s_cbranch_scc1 .Llk_done_lanes",
+          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx4 s[80:83], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_add_u32 %s, %s, 16" % (s(S_T3), s(S_T3)),
+          "s_load_dwordx2 s[84:85], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_waitcnt lgkmcnt(0)",
+          "v_cmp_eq_u64_e64 %s, v[2:3], s[80:81]" % sp(S_JUNK),
+          "v_cmp_gt_u32_e64 vcc, s85, %s" % key,
+          "s_and_b64 vcc, vcc, %s" % sp(S_JUNK),
+          "v_mov_b32 %s, s84" % v(H[3]),
+          "v_mad_u64_u32 %s, %s, %s, %s, s[82:83]" % (vp(H[4]), sp(S_JUNK), key, v(H[3])),
+          "v_cndmask_b32 v0, v0, %s, vcc" % v(H[4]),
+          "v_cndmask_b32 v1, v1, %s, vcc" % v(H[5]),
+          "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_branch .Llk_map",
+          ".Llk_done_lanes:",
+          ".Llk_done:",
+          "s_and_b64 exec, s[88:89], %s" % sp(S_ALIVE),
+          "s_mov_b64 %s, s[86:87]" % sp(S_LINK),
+          "s_cbranch_execz .Llk_sched",
+          "s_setpc_b64 %s" % sp(S_LINK),
+          ".Llk_sched:",
+          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+    return L
+
+
+def addr_of(label, sgpr, base_label):
+    """s[sgpr:sgpr+1] = absolute address of `label` (after base_label, which follows a getpc
+    into s[S_T0..]) — emitted right after 's_getpc_b64 s[sgpr:sgpr+1]' at base_label."""
+    return ["s_add_u32 %s, %s, %s-%s" % (s(sgpr), s(sgpr), label, base_label),
+            "s_addc_u32 %s, %s, 0" % (s(sgpr + 1), s(sgpr + 1))]
+
+
+def kernel(name, staged):
+    k = "K%s" % ("s" if staged else "g")
+    L = [".globl %s" % name, ".p2align 8", ".type %s,@function" % name, "%s:" % name]
+    # v0 = workitem id; wave index within the 256-lane workgroup
+    L += ["v_readfirstlane_b32 %s, v0" % s(S_WAVE),
+          "s_lshr_b32 %s, %s, 6" % (s(S_WAVE), s(S_WAVE)),
+          "s_load_dwordx16 s[%d:%d], s[0:1], 0x0" % (S_PROG, S_PROG + 15),
+          "s_load_dwordx8 s[%d:%d], s[0:1], 0x40" % (S_COUNT, S_COUNT + 7),
+          "s_mov_b64 %s, src_shared_base" % sp(S_SHARED),
+          "s_mov_b32 %s, 0x0c0c0001" % s(S_SEL16),
+          "s_mov_b32 %s, 0x00010203" % s(S_SEL32)]
+    # routine addresses (all routines follow the kernels' prologues in .text)
+    for lab, reg in ((".Lr_schedule", S_R_SCHED), (".Lr_diverge", S_R_DIVERGE),
+                     (".Lr_fault", S_R_FAULT), (".Lr_exit", S_R_EXIT), (".Lr_udiv", S_R_DIV),
+                     (".Lr_check", S_R_CHECK), (".Lr_lookup", S_R_LOOKUP)):
+        base = ".L%s_pc_%d" % (k, reg)
+        L += ["s_getpc_b64 %s" % sp(reg), "%s:" % base] + addr_of(lab, reg, base)
+    # lane constants
+    L += ["v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
+          "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
+          "v_mov_b32 v%d, 1" % V_ONE,
+          "s_waitcnt lgkmcnt(0)"]
+    # S_STKSTRIDE = dp_launch.stack_stride, S_LDSBASE = dp_launch.lds_stack_base
+    # lane stack bottom = lds_base + (wave*64 + lane) * stride
+    L += ["s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),
+          "v_mul_lo_u32 %s, %s, %s" % (v(H[1]), v(H[1]), s(S_STKSTRIDE)),
+          "v_add_u32 v%d, %s, %s" % (V_STK, s(S_LDSBASE), v(H[1]))]
+    # zero the LDS verdict histogram (257 bins: lanes 0..255 of the 4 waves, bin 256 by wave 0)
+    L += ["s_lshl_b32 %s, %s, 8" % (s(S_T0), s(S_WAVE)),
+          "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[0])),
+          "v_add_u32 %s, %s, %s" % (v(H[2]), s(S_T0), v(H[2])),
+          "v_mov_b32 %s, 0" % v(H[3]),
+          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
+          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
+          "s_cbranch_scc0 .L%s_hz" % k,
+          "v_mov_b32 %s, 1024" % v(H[2]),
+          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
+          ".L%s_hz:" % k,
+          "s_waitcnt lgkmcnt(0)",
+          "s_barrier"]
+    # groups of 64 packets: group = workgroup*4 + wave, stride = 4*numgroups
+    L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
+          "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
+          "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
+          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
+          "s_load_dword %s, s[0:1], 0x60" % s(S_GSTRIDE),
+          "s_waitcnt lgkmcnt(0)",
+          "s_mov_b32 s7, %s" % ("1" if staged else "0"),
+          "s_branch .Lgroup_check"]
+    return L
+
+
+def common_group_code():
+    """Shared by both kernels (mode in s7: 1 = staged 64-B packets)."""
+    L = [".Lgroup_done:",
+         "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_GSTRIDE)),
+         ".Lgroup_check:",
+         "s_mov_b64 exec, -1",
+         "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
+         "s_cbranch_scc0 .Lfinish",
+         "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
+         "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
+         "v_lshl_add_u32 v%d, %s, 6, %s" % (V_GID, s(S_GROUP), v(H[0])),
+         "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), V_GID),
+         "s_mov_b64 exec, %s" % sp(S_ALIVE),
+         # packet address / length
+         "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
+         "s_cbranch_scc0 .Lgs_offsets",
+         "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
+         "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
+                                                      v(H[1]), sp(S_DATA)),
+         "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
+         "s_branch .Lgs_addr_done",
+         ".Lgs_offsets:",
+         "v_mov_b32 %s, 8" % v(H[1]),
+         "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[2]), sp(S_JUNK), V_GID, v(H[1]), sp(S_OFFS)),
+         "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[2])),
+         "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[2])),
+         "s_waitcnt vmcnt(0)",
+         "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
+         "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
+         "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
+         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
+         "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
+         ".Lgs_addr_done:",
+         "s_cmp_eq_u32 s7, 1",
+         "s_cbranch_scc0 .Lgs_nostage"]
+    for q in range(4):
+        L.append("global_load_dwordx4 v[%d:%d], v[%d:%d], off offset:%d" % (
+            PKT0 + 4 * q, PKT0 + 4 * q + 3, V_PKT, V_PKT + 1, 16 * q))
+    L.append(".Lgs_nostage:")
+    for r in range(22):
+        L.append("v_mov_b32 v%d, 0" % r)
+    L += ["v_mov_b32 v2, v%d" % V_PKT, "v_mov_b32 v3, v%d" % (V_PKT + 1),
+          "v_add_u32 v20, %s, v%d" % (s(S_STKSTRIDE), V_STK),
+          "v_mov_b32 v21, %s" % s(S_SHARED + 1),
+          "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),
+          "v_mov_b32 v%d, %s" % (V_T, s(S_T0)),
+          "s_waitcnt vmcnt(0)",
+          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+    # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
+    L += [".Lfinish:",
+          "s_mov_b64 exec, -1",
+          "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          "s_barrier",
+          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
+          "s_cbranch_scc1 .Lfin_end",
+          "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
+          "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
+          "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # bin
+          ".Lfin_bin:",
+          "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
+          "ds_read_b32 %s, %s" % (v(H[3]), v(H[2])),
+          "s_waitcnt lgkmcnt(0)",
+          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[3]),
+          "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE),
+          "v_mov_b32 %s, 8" % v(H[4]),
+          "v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(R[0]), sp(S_JUNK), v(H[1]), v(H[4]), sp(S_HIST)),
+          "v_mov_b32 %s, 0" % v(H[4]),
+          "v_mov_b32 %s, %s" % (v(R[2]), v(H[3])),
+          "v_mov_b32 %s, 0" % v(R[3]),
+          "global_atomic_add_x2 %s, %s, off" % (vp(R[0]), vp(R[2])),
+          "s_mov_b64 exec, %s" % sp(S_SAVE),
+          # wave 0 also owns bin 256
+          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
+          "s_cbranch_scc0 .Lfin_end",
+          "s_mov_b32 %s, 1" % s(S_WAVE),       # run once more, lane 0 only, bin 256
+          "v_mov_b32 %s, 256" % v(H[1]),
+          "s_mov_b64 exec, 1",
+          "s_branch .Lfin_bin",
+          ".Lfin_end:",
+          "s_waitcnt vmcnt(0)",
+          "s_endpgm"]
+    return L
+
+
+def link_kernel():
+    """ebpf_asm_link(dp_entry *e, uint32_t n): e[i].handler (= handler id) -> absolute address."""
+    return [".globl ebpf_asm_link", ".p2align 8", ".type ebpf_asm_link,@function",
+            "ebpf_asm_link:",
+            "s_load_dwordx2 s[4:5], s[0:1], 0x0",
+            "s_load_dword s6, s[0:1], 0x8",
+            "s_getpc_b64 s[8:9]",
+            ".Llink_base:",
+            "s_add_u32 s10, s8, .Lhandler_table-.Llink_base",
+            "s_addc_u32 s11, s9, 0",
+            "v_lshl_add_u32 v1, s2, 6, v0",
+            "s_waitcnt lgkmcnt(0)",
+            "v_cmp_gt_u32_e64 vcc, s6, v1",
+            "s_and_b64 exec, exec, vcc",
+            "s_cbranch_execz .Llink_end",
+            "v_mov_b32 v2, 32",
+            "v_mad_u64_u32 v[2:3], s[12:13], v1, v2, s[4:5]",
+            "global_load_dword v4, v[2:3], off",
+            "s_waitcnt vmcnt(0)",
+            "v_mov_b32 v6, 4",
+            "v_mad_u64_u32 v[6:7], s[12:13], v4, v6, s[10:11]",
+            "global_load_dword v8, v[6:7], off",
+            "s_waitcnt vmcnt(0)",
+            "v_ashrrev_i32 v9, 31, v8",
+            "v_lshl_add_u64 v[10:11], v[8:9], 0, s[8:9]",
+            "global_store_dwordx2 v[2:3], v[10:11], off",
+            ".Llink_end:",
+            "s_waitcnt vmcnt(0)",
+            "s_endpgm"]
+
+
+def kd(name, lds, vgprs, sgprs, kernarg, wgsize):
+    return [".rodata", ".p2align 6", ".amdhsa_kernel %s" % name,
+            ".amdhsa_group_segment_fixed_size %d" % lds,
+            ".amdhsa_private_segment_fixed_size 0",
+            ".amdhsa_kernarg_size %d" % kernarg,
+            ".amdhsa_user_sgpr_count 2",
+            ".amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            ".amdhsa_system_sgpr_workgroup_id_x 1",
+            ".amdhsa_system_vgpr_workitem_id 0",
+            ".amdhsa_next_free_vgpr %d" % vgprs,
+            ".amdhsa_next_free_sgpr %d" % sgprs,
+            ".amdhsa_accum_offset %d" % vgprs,
+            ".amdhsa_reserve_vcc 1",
+            ".amdhsa_ieee_mode 0",
+            ".amdhsa_dx10_clamp 0",
+            ".end_amdhsa_kernel", ".text"]
+
+
+def metadata(kernels):
+    out = [".amdgpu_metadata", "---", "amdhsa.kernels:"]
+    for name, kernarg, lds, vgprs, sgprs, wg in kernels:
+        out += ["  - .args:",
+                "      - .offset: 0",
+                "        .size: %d" % kernarg,
+                "        .value_kind: by_value",
+                "    .group_segment_fixed_size: %d" % lds,
+                "    .kernarg_segment_align: 8",
+                "    .kernarg_segment_size: %d" % kernarg,
+                "    .max_flat_workgroup_size: %d" % wg,
+                "    .name: %s" % name,
+                "    .private_segment_fixed_size: 0",
+                "    .sgpr_count: %d" % sgprs,
+                "    .symbol: %s.kd" % name,
+                "    .vgpr_count: %d" % vgprs,
+                "    .wavefront_size: 64"]
+    out += ["amdhsa.target: amdgcn-amd-amdhsa--gfx950", "amdhsa.version:", "  - 1", "  - 2",
+            "...", ".end_amdgpu_metadata"]
+    return out
+
+
+def main():
+    out_s, out_h = sys.argv[1], sys.argv[2]
+    A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text"]
+    A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
+    A += common_group_code() + routines()
+    table = []
+    hid = 0
+    header = ["// generated by gen_interp.py — handler family ids for asm_runtime.cpp",
+              "#pragma once", "#define AH_NREGS %d" % NREG]
+    for name, arity in FAMILIES:
+        header.append("#define AH_%s %d" % (name, hid))
+        for d, sr in variants(arity):
+            label = "h_%d" % hid
+            uid = "%d" % hid
+            body, own = handler_body(name, d, sr)
+            A.append(".p2align 2")
+            A.append("%s:" % label)
+            A += [ln.replace("{uid}", uid) for ln in body]
+            if not own:
+                A += dispatch(12)
+            table.append(label)
+            hid += 1
+    header.append("#define AH_COUNT %d" % hid)
+    A += link_kernel()
+    A += [".p2align 2", ".Lhandler_table:"]
+    A += ["  .long %s-.Llink_base" % lab for lab in table]
+    kernarg = 104
+    A += kd("ebpf_interp_s64", 0, NVGPR, NSGPR, kernarg, 256)
+    A += kd("ebpf_interp_gen", 0, NVGPR, NSGPR, kernarg, 256)
+    A += kd("ebpf_asm_link", 0, 16, 16, 16, 64)
+    meta = metadata([("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR, 256),
+                   ("ebpf_interp_gen", kernarg, 0, NVGPR, NSGPR, 256),
+                   ("ebpf_asm_link", 16, 0, 16, 16, 64)])
+    with open(out_s, "w") as f:
+        f.write("\n".join(("\t" + x if not (x.endswith(":") or x.startswith(".") or x.startswith(" ")) else x)
+                          for x in A) + "\n")
+        f.write("\n".join(meta) + "\n")
+    with open(out_h, "w") as f:
+        f.write("\n".join(header) + "\n")
+
+
+if __name__ == "__main__":
+    main()

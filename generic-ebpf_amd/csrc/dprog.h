@@ -56,4 +56,10 @@ struct dp_launch {
 	uint32_t start;          // entry index of the initial state (0, 1)
 	uint32_t nmaps;
 	uint32_t nentries;
+	// assembly interpreter only:
+	uint32_t stack_stride;    // LDS bytes per lane stack slice (S' in asm_runtime.cpp)
+	uint32_t lds_stack_base;  // LDS byte offset of the first stack slice (after the histogram)
+	uint32_t total_waves;     // persistent grid: waves in the launch (group stride)
+	uint32_t pad;
 };
+static_assert(sizeof(dp_launch) == 104, "dp_launch layout is shared with the assembly kernels");

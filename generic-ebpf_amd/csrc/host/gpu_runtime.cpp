@@ -14,9 +14,12 @@
 #include "internal.h"
 
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
-hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device); // asm_runtime.cpp
+// asm_runtime.cpp
+hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode);
 int asm_available(int device);
-int asm_link_entries(int device, std::vector<dp_entry> &entries);
+bool asm_program_needs_general(const dprog_host &xl);
+int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 
 
 namespace {
@@ -67,6 +70,8 @@ ensure_translated(struct ebpf_prog *ep)
 	int err = translate_program(ep, *x);
 	if (err && x->error == 0)
 		x->error = err;
+	if (!x->error)
+		x->asm_needs_general = asm_program_needs_general(*x);
 	ep->xlated = std::move(x);
 	if (ep->xlated->error)
 		return fail(ep->xlated->error, ep->xlated->error_msg);
@@ -121,37 +126,24 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 	if ((int)ep->dev.size() <= device)
 		ep->dev.resize(device + 1);
 	auto &dp = ep->dev[device];
-	int variant = effective_variant(device);
-	if (dp && dp->variant_linked == variant) {
+	if (dp) {
 		*out = dp.get();
 		return 0;
 	}
 	hipError_t e = hipSetDevice(device);
 	if (e != hipSuccess)
 		return hip_fail(e, "hipSetDevice");
-	if (!dp)
-		dp = std::make_unique<dprog_device>();
-	dp->device = device;
-	std::vector<dp_entry> entries = ep->xlated->entries;
-	if (variant == 0) {
-		err = asm_link_entries(device, entries);
-		if (err)
-			return err;
-	}
-	if (dp->d_entries == nullptr || dp->nentries != entries.size()) {
-		if (dp->d_entries)
-			hipFree(dp->d_entries);
-		e = hipMalloc(&dp->d_entries, entries.size() * sizeof(dp_entry));
-		if (e != hipSuccess)
-			return hip_fail(e, "hipMalloc(program)");
-	}
-	e = hipMemcpy(dp->d_entries, entries.data(), entries.size() * sizeof(dp_entry),
+	auto nd = std::make_unique<dprog_device>();
+	nd->device = device;
+	const std::vector<dp_entry> &entries = ep->xlated->entries;
+	e = hipMalloc(&nd->d_entries, entries.size() * sizeof(dp_entry));
+	if (e != hipSuccess)
+		return hip_fail(e, "hipMalloc(program)");
+	e = hipMemcpy(nd->d_entries, entries.data(), entries.size() * sizeof(dp_entry),
 		      hipMemcpyHostToDevice);
 	if (e != hipSuccess)
 		return hip_fail(e, "hipMemcpy(program)");
-	dp->nentries = (uint32_t)entries.size();
-
-	std::vector<dp_map> table;
+	nd->nentries = (uint32_t)entries.size();
 	for (struct ebpf_map *em : ep->xlated->maps) {
 		void *mdev = nullptr;
 		err = ensure_map_mirror(em, device, &mdev);
@@ -162,22 +154,39 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		m.dev_base = (uint64_t)(uintptr_t)mdev;
 		m.value_size = em->value_size;
 		m.max_entries = em->max_entries;
-		table.push_back(m);
+		nd->table.push_back(m);
 	}
-	if (dp->d_maps == nullptr && !table.empty()) {
-		e = hipMalloc(&dp->d_maps, table.size() * sizeof(dp_map));
+	if (!nd->table.empty()) {
+		e = hipMalloc(&nd->d_maps, nd->table.size() * sizeof(dp_map));
 		if (e != hipSuccess)
 			return hip_fail(e, "hipMalloc(map table)");
-	}
-	if (!table.empty()) {
-		e = hipMemcpy(dp->d_maps, table.data(), table.size() * sizeof(dp_map),
+		e = hipMemcpy(nd->d_maps, nd->table.data(), nd->table.size() * sizeof(dp_map),
 			      hipMemcpyHostToDevice);
 		if (e != hipSuccess)
 			return hip_fail(e, "hipMemcpy(map table)");
 	}
-	dp->nmaps = (uint32_t)table.size();
-	dp->variant_linked = variant;
+	nd->nmaps = (uint32_t)nd->table.size();
+	dp = std::move(nd);
 	*out = dp.get();
+	return 0;
+}
+
+// Lowered assembly entries for `mode`, built on first use.
+int
+asm_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
+{
+	std::lock_guard<std::mutex> g(ep->dlock);
+	if (dp->d_asm[mode])
+		return 0;
+	if (dp->asm_err[mode])
+		return dp->asm_err[mode];
+	std::string msg;
+	int err = asm_build_entries(dp->device, *ep->xlated, mode, dp->table, &dp->d_asm[mode],
+				    &dp->asm_stride[mode], &msg);
+	if (err) {
+		dp->asm_err[mode] = err;
+		return fail(err, msg);
+	}
 	return 0;
 }
 
@@ -185,7 +194,6 @@ int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream)
 {
 	dp_launch L = L0;
-	L.prog = dp->d_entries;
 	L.maps = dp->d_maps;
 	L.nmaps = dp->nmaps;
 	L.nentries = dp->nentries;
@@ -193,8 +201,19 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	int err = sync_map_mirrors(ep, dp->device, stream);
 	if (err)
 		return err;
-	hipError_t e = dp->variant_linked == 0 ? launch_interp_asm(L, stream, dp->device)
-					       : launch_interp_v0(L, stream);
+	hipError_t e;
+	if (effective_variant(dp->device) == 0) {
+		const int mode =
+		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
+		if ((err = asm_entries(ep, dp, mode)))
+			return err;
+		L.prog = dp->d_asm[mode];
+		L.stack_stride = dp->asm_stride[mode];
+		e = launch_interp_asm(L, stream, dp->device, mode);
+	} else {
+		L.prog = dp->d_entries;
+		e = launch_interp_v0(L, stream);
+	}
 	if (e != hipSuccess)
 		return hip_fail(e, "kernel launch");
 	return 0;
@@ -261,6 +280,9 @@ prog_release_device_state(struct ebpf_prog *ep)
 				hipFree(dp->d_entries);
 			if (dp->d_maps)
 				hipFree(dp->d_maps);
+			for (auto *a : dp->d_asm)
+				if (a)
+					hipFree(a);
 		}
 	}
 	ep->dev.clear();

@@ -65,21 +65,49 @@ struct ebpf_map {
 	uint8_t *array_storage() const;
 };
 
-// Per (program, device): the linked entries and the map table in device memory.
+// Per (program, device): entries for each interpreter variant and the map table.
 struct dprog_device {
 	int device = -1;
-	dp_entry *d_entries = nullptr;
+	dp_entry *d_entries = nullptr;   // variant 1 (portable HIP): translated entries as is
 	dp_map *d_maps = nullptr;
+	std::vector<dp_map> table;
 	uint32_t nentries = 0;
 	uint32_t nmaps = 0;
-	int variant_linked = -1; // which interpreter the entries were linked for
+	dp_entry *d_asm[2] = {nullptr, nullptr}; // variant 0: lowered + linked, per mode
+	uint32_t asm_stride[2] = {0, 0};         // LDS stack bytes per lane, per mode
+	int asm_err[2] = {0, 0};
+};
+
+// Abstract value of a register (pointer provenance), computed by translate.cpp's dataflow pass
+// over the state tree.  Used to specialise device handlers: packet loads at known offsets come
+// from registers, stack accesses at known offsets from LDS, map lookups resolve statically.
+enum av_kind : uint8_t {
+	AV_UNKNOWN = 0,
+	AV_CONST,       // off = the 64-bit value
+	AV_CTX,         // packet start (r1 at entry) + off
+	AV_STACK,       // stack top (r10 at entry) + off
+	AV_MAPVAL,      // value of map #map (dp_map table index) + off, never NULL
+	AV_MAPVAL_NULL, // as AV_MAPVAL, or NULL (a lookup result not yet NULL-checked)
+};
+struct av {
+	uint8_t kind = AV_UNKNOWN;
+	int16_t map = -1;
+	int64_t off = 0;
+	bool operator==(const av &o) const { return kind == o.kind && map == o.map && off == o.off; }
+	bool operator!=(const av &o) const { return !(*this == o); }
+};
+struct dp_annot {
+	av in[EBPF_REG_MAX]; // register state before the entry executes
+	bool reached = false;
 };
 
 struct dprog_host {
 	std::vector<dp_entry> entries;
+	std::vector<dp_annot> annot;
 	uint32_t start = 0;
 	std::vector<struct ebpf_map *> maps; // referenced array maps, in dp_map table order
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
+	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	uint32_t max_stack = 0;
 	int error = 0;
 	std::string error_msg;

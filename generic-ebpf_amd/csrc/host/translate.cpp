@@ -296,6 +296,146 @@ struct Translator {
 	}
 };
 
+// ---------------------------------------------------------------- pointer-provenance dataflow
+av
+mk(uint8_t kind, int64_t off = 0, int16_t map = -1)
+{
+	av a;
+	a.kind = kind;
+	a.off = off;
+	a.map = map;
+	return a;
+}
+
+bool
+is_ptr(const av &a)
+{
+	return a.kind == AV_CTX || a.kind == AV_STACK || a.kind == AV_MAPVAL;
+}
+
+// dst + src for ADD64 / MOV64 (which adds, ebpf_interpreter.c:197-202)
+av
+add_av(const av &d, const av &s)
+{
+	if (d.kind == AV_CONST && s.kind == AV_CONST)
+		return mk(AV_CONST, (int64_t)((uint64_t)d.off + (uint64_t)s.off));
+	if (is_ptr(d) && s.kind == AV_CONST)
+		return mk(d.kind, (int64_t)((uint64_t)d.off + (uint64_t)s.off), d.map);
+	if (d.kind == AV_CONST && is_ptr(s))
+		return mk(s.kind, (int64_t)((uint64_t)s.off + (uint64_t)d.off), s.map);
+	return av();
+}
+
+void
+transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
+{
+	const uint16_t k = e.kind;
+	if (k == DK_FAULT || k == EBPF_OP_EXIT)
+		return;
+	if (k == DK_CALL_LOOKUP) {
+		av res;
+		if (r[1].kind == AV_CONST)
+			for (size_t m = 0; m < out.maps.size(); m++)
+				if ((uint64_t)r[1].off == (uint64_t)(uintptr_t)out.maps[m])
+					res = mk(AV_MAPVAL_NULL, 0, (int16_t)m);
+		r[0] = res; // r1..r5 keep their values (a plain C call in the reference)
+		return;
+	}
+	const uint8_t cls = k & 7;
+	if (cls == EBPF_CLS_JMP || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
+		return;
+	if (cls == EBPF_CLS_LDX) {
+		r[e.dst] = av();
+		return;
+	}
+	if (k == EBPF_OP_LDDW) {
+		r[e.dst] = mk(AV_CONST, (int64_t)e.imm);
+		return;
+	}
+	const av s = (k & 0x08) ? r[e.src] : mk(AV_CONST, (int64_t)e.imm);
+	av &d = r[e.dst];
+	switch (k) {
+	case EBPF_OP_ADD64_IMM: case EBPF_OP_ADD64_REG:
+	case EBPF_OP_MOV64_IMM: case EBPF_OP_MOV64_REG:
+		d = add_av(d, s);
+		break;
+	case EBPF_OP_SUB64_IMM: case EBPF_OP_SUB64_REG: case EBPF_OP_NEG64:
+		if (s.kind == AV_CONST) {
+			av neg = mk(AV_CONST, (int64_t)(0 - (uint64_t)s.off));
+			d = add_av(d, neg);
+		} else {
+			d = av();
+		}
+		break;
+	case EBPF_OP_MOV_IMM:
+		d = mk(AV_CONST, (int64_t)(uint32_t)e.imm);
+		break;
+	case EBPF_OP_MOV_REG:
+		d = s.kind == AV_CONST ? mk(AV_CONST, (int64_t)(uint32_t)s.off) : av();
+		break;
+	case EBPF_OP_NEG:
+		d = mk(AV_CONST, (int64_t)(uint32_t)(0u - (uint32_t)e.imm));
+		break;
+	default:
+		d = av();
+		break;
+	}
+}
+
+void
+dataflow(dprog_host &out)
+{
+	const size_t n = out.entries.size();
+	out.annot.assign(n, dp_annot());
+	dp_annot init;
+	for (auto &x : init.in)
+		x = mk(AV_CONST, 0); // the device zeroes r0, r2..r9 (the reference leaves them undefined)
+	init.in[1] = mk(AV_CTX, 0);
+	init.in[10] = mk(AV_STACK, 0);
+	init.reached = true;
+	out.annot[out.start] = init;
+	std::vector<uint32_t> work{out.start};
+	std::vector<char> queued(n, 0);
+	queued[out.start] = 1;
+	while (!work.empty()) {
+		uint32_t id = work.back();
+		work.pop_back();
+		queued[id] = 0;
+		const dp_entry &e = out.entries[id];
+		if (e.kind == DK_FAULT || e.kind == EBPF_OP_EXIT)
+			continue;
+		av r[EBPF_REG_MAX];
+		for (int i = 0; i < EBPF_REG_MAX; i++)
+			r[i] = out.annot[id].in[i];
+		transfer(e, out, r);
+		uint32_t succ[2] = {e.next, UINT32_MAX};
+		if ((e.kind & 7) == EBPF_CLS_JMP && e.kind != DK_CALL_LOOKUP)
+			succ[1] = e.target;
+		for (uint32_t sx : succ) {
+			if (sx == UINT32_MAX || sx >= n)
+				continue;
+			dp_annot &a = out.annot[sx];
+			bool changed = false;
+			if (!a.reached) {
+				for (int i = 0; i < EBPF_REG_MAX; i++)
+					a.in[i] = r[i];
+				a.reached = true;
+				changed = true;
+			} else {
+				for (int i = 0; i < EBPF_REG_MAX; i++)
+					if (a.in[i] != r[i] && a.in[i].kind != AV_UNKNOWN) {
+						a.in[i] = av();
+						changed = true;
+					}
+			}
+			if (changed && !queued[sx]) {
+				queued[sx] = 1;
+				work.push_back(sx);
+			}
+		}
+	}
+}
+
 } // namespace
 
 int
@@ -335,6 +475,7 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	for (uint32_t i = 0; i < ep->ndep_maps; i++)
 		if (ee->maps.count(ep->dep_maps[i]))
 			add_map(ep->dep_maps[i]);
+	dataflow(out);
 	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
 	// its map while a later batch may still read it.
 	for (struct ebpf_map *m : out.maps)
