@@ -616,16 +616,17 @@ def routines():
           "v_cmp_le_u32_e64 vcc, %s, %s" % (v(R[0]), v(R[2])),
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
-          # stack: u = a - {shared_hi : v42}; u_hi == 0 && u_lo <= stride - size
-          "v_sub_co_u32 %s, vcc, %s, v%d" % (v(R[0]), v(H[0]), V_STK),
+          # stack: the reference's 512 bytes below r10 (generic accesses force a 516-byte slice,
+          # the slice top is r10): u = a - {shared_hi : top - 512}; u_hi == 0 && u_lo <= 512 - size
+          "s_sub_u32 %s, %s, 512" % (s(S_T3), s(S_STKSTRIDE)),
+          "v_add_u32 %s, %s, v%d" % (v(R[4]), s(S_T3), V_STK),
+          "v_sub_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(H[0]), v(R[4])),
           "v_mov_b32 %s, %s" % (v(R[3]), s(S_SHARED + 1)),
           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[3])),
-          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_STKSTRIDE), s(S_T0)),
+          "s_sub_u32 %s, 512, %s" % (s(S_T3), s(S_T0)),
           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
           "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_T3), v(R[0])),
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-          "s_cmp_ge_u32 %s, %s" % (s(S_STKSTRIDE), s(S_T0)),
-          "s_cselect_b64 %s, %s, 0" % (sp(S_JUNK), sp(S_JUNK)),
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
           # maps: for m in table
           "s_mov_b32 %s, 0" % s(S_T2),

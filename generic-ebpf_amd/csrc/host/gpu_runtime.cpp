@@ -51,14 +51,12 @@ device_count()
 	return n;
 }
 
-// Which interpreter runs: 0 = default (assembly if present), 1 = portable HIP baseline.
+// Which interpreter runs: 0 = the gfx950 assembly interpreter (default; an error if its code
+// object cannot be loaded — never a silent fallback), 1 = the portable HIP baseline.
 int
-effective_variant(int device)
+effective_variant(int)
 {
-	int v = g_variant.load();
-	if (v == 0 && !asm_available(device))
-		return 1;
-	return v == 0 ? 0 : v;
+	return g_variant.load();
 }
 
 int

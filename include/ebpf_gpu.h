@@ -96,7 +96,9 @@ int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_
 /* Select the device used by ebpf_prog_run_batch for the calling thread. */
 int ebpf_gpu_set_device(int device);
 
-/* Interpreter variant used by subsequent launches: 0 = default (fastest available). */
+/* Interpreter variant used by subsequent launches: 0 = the hand-written gfx950 assembly
+ * interpreter (default; launches fail with ENOSYS if it cannot be loaded), 1 = the portable
+ * HIP interpreter (correctness baseline). */
 int ebpf_gpu_set_variant(int variant);
 
 /* Information about the translated device program. */
