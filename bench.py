@@ -43,7 +43,7 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_PACKETS = {"c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 26, "c5": 1 << 22}
+DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 26, "c5": 1 << 22}
 DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
 
 
@@ -57,8 +57,9 @@ def build_inputs(cfg, n, rank):
         data, offs, _ = workloads.packets_imix(n, seed=5 + rank)
         return lay, maps, data, offs
     d = min(n, DISTINCT)
-    gen = workloads.packets_random if cfg == "c2" else workloads.packets_l2l3
-    return lay, maps, gen(d, 64, seed=(2 if cfg == "c2" else 3) + 1000 * rank), None
+    rnd = cfg in ("c0", "c2", "nop200", "alu200")
+    gen = workloads.packets_random if rnd else workloads.packets_l2l3
+    return lay, maps, gen(d, 64, seed=(2 if rnd else 3) + 1000 * rank), None
 
 
 def cpu_baseline(cfg, lay, maps, pk, offs, budget_s):

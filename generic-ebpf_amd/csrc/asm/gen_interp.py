@@ -27,31 +27,37 @@ V_LEN = 40           # packet length (bytes)
 V_T = 41             # parked entry byte offset
 V_STK = 42           # lane stack bottom (LDS byte address)
 V_GID = 43           # packet index within the launch
+V_L16 = 44           # lane * 16 (LDS-DMA staging offset)
 V_ONE = 45           # constant 1
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
 R = list(range(52, 64))              # routine temporaries
 NVGPR = 64
 
-# SGPRs
+# SGPRs (next_free_sgpr 80 -> 8 waves per SIMD)
+S_CB = 4             # s[4:5] code base (.Lcb): routines are reached at S_CB + (label - .Lcb)
 S_ENT = 8            # s[8:15] current entry: s[8:9] handler, s[10:11] imm, s12 next, s13 target,
                      # s14 aux0, s15 aux1
 S_ALIVE = 16         # s[16:17]
 S_SAVE = 18          # s[18:19]
 S_PROG, S_MAPS, S_DATA, S_OFFS, S_OFFBASE, S_RET, S_FAULTS, S_HIST = 20, 22, 24, 26, 28, 30, 32, 34
 S_COUNT, S_STRIDE, S_START, S_NMAPS, S_NENT = 36, 38, 39, 40, 41
-S_STKSTRIDE, S_LDSBASE = 42, 43      # from dp_launch tail
-S_GROUP, S_GSTRIDE, S_NGROUPS = 44, 45, 46
+S_STKSTRIDE, S_LDSBASE = 42, 43      # dp_launch.stack_stride, .lds_stack_base
+S_GROUP, S_GSTRIDE, S_NGROUPS, S_PKTLDS = 44, 45, 46, 47
 S_MASK = 48          # s[48:49] temp mask
 S_LINK = 50          # s[50:51] subroutine return address
 S_CODE = 52          # fault code argument
 S_T0, S_T1, S_T2, S_T3 = 53, 54, 55, 56
+S_BYTES = 57         # check routine scratch
 S_SHARED = 58        # s[58:59] src_shared_base
 S_JUNK = 60          # s[60:61] scratch sdst
-S_WAVE = 62
-S_SEL16, S_SEL32 = 63, 64
-# routine addresses
-S_R_SCHED, S_R_DIVERGE, S_R_FAULT, S_R_EXIT, S_R_DIV, S_R_CHECK, S_R_LOOKUP = 66, 68, 70, 72, 74, 76, 78
-NSGPR = 96
+S_JA = 62            # s[62:63] routine jump address
+S_SEL16, S_SEL32 = 72, 73
+S_REC = 64           # s[64:71] map record {handle, dev_base, value_size, max_entries, lds_off, pad}
+S_OK = 74            # s[74:75] check: accumulated ok lanes
+S_SV0 = 76           # s[76:77] saved link (lookup / check write path)
+S_SV1 = 78           # s[78:79] saved mask (lookup / check write path)
+S_WAVE = 3
+NSGPR = 80
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -77,6 +83,8 @@ for z in SIZES:
     fam("LDXGEN%d" % z, 2)
 for z in SIZES:
     fam("STXGEN%d" % z, 2)
+for z in SIZES:
+    fam("LDXMAP%d" % z, 2)
 for o in ALU64I:
     fam("A64I_" + o, 1)
 for o in ALU32I:
@@ -144,8 +152,17 @@ def dispatch(next_reg=12):
             "s_setpc_b64 s[8:9]"]
 
 
-def call(routine_sgpr):
-    return ["s_swappc_b64 %s, %s" % (sp(S_LINK), sp(routine_sgpr))]
+def raddr(label):
+    return ["s_add_u32 %s, %s, %s-.Lcb" % (s(S_JA), s(S_CB), label),
+            "s_addc_u32 %s, %s, 0" % (s(S_JA + 1), s(S_CB + 1))]
+
+
+def call(label):
+    return raddr(label) + ["s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_JA))]
+
+
+def goto(label):
+    return raddr(label) + ["s_setpc_b64 %s" % sp(S_JA)]
 
 
 def fault_mask(mask_sgpr_pair, code):
@@ -153,7 +170,7 @@ def fault_mask(mask_sgpr_pair, code):
     out = []
     if mask_sgpr_pair != S_MASK:
         out.append("s_mov_b64 %s, %s" % (sp(S_MASK), sp(mask_sgpr_pair)))
-    out += ["s_mov_b32 %s, %d" % (s(S_CODE), code)] + call(S_R_FAULT)
+    out += ["s_mov_b32 %s, %d" % (s(S_CODE), code)] + call(".Lr_fault")
     return out
 
 
@@ -263,7 +280,7 @@ def divmod_body(d, sr, imm, op, bits):
                 "s_cbranch_scc1 .Ldz_%s" % "{uid}"]
         out += fault_mask(S_MASK, 2)
         out.append(".Ldz_{uid}:")
-    out += call(S_R_DIV)
+    out += call(".Lr_udiv")
     q0, q1, r0, r1 = v(R[4]), v(R[5]), v(R[6]), v(R[7])
     src = (q0, q1) if op == "DIV" else (r0, r1)
     out += ["v_mov_b32 %s, %s" % (lo(d), src[0]),
@@ -293,7 +310,7 @@ def h_cond(c, d, sr, imm):
             "s_cbranch_scc1 .Ltk_{uid}",
             "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
             "s_cbranch_scc1 .Lnt_{uid}",
-            "s_setpc_b64 %s" % sp(S_R_DIVERGE),
+            ] + goto(".Lr_diverge") + [
             ".Ltk_{uid}:"] + dispatch(13) + [".Lnt_{uid}:"] + dispatch(12)
     return out, True   # (body, has own dispatch)
 
@@ -394,7 +411,7 @@ def h_ldx_gen(z, d, sr):
     flat loads (packet/map in global memory, stack in LDS via the shared aperture)."""
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
-           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 0" % s(S_T1)] + call(S_R_CHECK)
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check")
     # byte-wise gather (alignment-agnostic)
     acc = [v(H[2]), v(H[3])]
     out += ["v_mov_b32 %s, 0" % acc[0], "v_mov_b32 %s, 0" % acc[1]]
@@ -404,6 +421,29 @@ def h_ldx_gen(z, d, sr):
         tgt = acc[b // 4]
         out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(H[4]), 8 * (b % 4), tgt))
     out += ["v_mov_b32 %s, %s" % (lo(d), acc[0]), "v_mov_b32 %s, %s" % (hi(d), acc[1])]
+    return out
+
+
+def h_ldx_map(z, d, sr):
+    """Load from an LDS-resident array-map value: r_src is (by pointer provenance) a lookup
+    result of one map, i.e. NULL or dev_base + k*value_size + c.  s[10:11] = dev_base - off,
+    s13 = map bytes - z (last valid byte offset), s14 = the map's LDS byte address.  Lanes whose
+    address leaves the map (NULL, out of range) fault MEM; the rest read the LDS copy (aligned
+    by construction: the host only selects this family when the access is)."""
+    u0, u1, t = v(H[0]), v(H[1]), v(H[2])
+    out = ["v_sub_co_u32 %s, vcc, %s, s10" % (u0, lo(sr)),
+           "v_mov_b32 %s, s11" % t,
+           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (u1, hi(sr), t),
+           "v_cmp_ge_u32_e64 %s, s13, %s" % (sp(S_MASK), u0),
+           "v_cmp_eq_u32_e64 vcc, 0, %s" % u1,
+           "s_and_b64 %s, %s, vcc" % (sp(S_MASK), sp(S_MASK)),
+           "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), sp(S_MASK)),
+           "s_cbranch_scc0 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:",
+           "v_add_u32 %s, s14, %s" % (u0, u0)]
+    if z == 8:
+        out.append("ds_read2_b32 %s, %s offset1:1" % (pair(d), u0))
+    else:
+        out += ["%s %s, %s" % (DS_R[z], lo(d), u0), "v_mov_b32 %s, 0" % hi(d)]
     return out
 
 
@@ -423,7 +463,7 @@ def store_bytes(a0, vals, z):
 def h_stx_gen(z, d, sr):
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(d)),
-           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(S_R_CHECK)
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(".Lr_check")
     out += ["v_mov_b32 %s, %s" % (v(H[2]), lo(sr)), "v_mov_b32 %s, %s" % (v(H[3]), hi(sr))]
     return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
 
@@ -434,7 +474,7 @@ def h_st_gen(z, d):
     out = ["s_ashr_i32 %s, s15, 31" % s(S_T3),
            "v_mov_b32 %s, s15" % v(H[2]), "v_mov_b32 %s, %s" % (v(H[3]), s(S_T3)),
            "v_lshl_add_u64 %s, %s, 0, %s" % (vp(a0), vp(H[2]), pair(d)),
-           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(S_R_CHECK)
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(".Lr_check")
     out += ["v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3])]
     return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
 
@@ -484,28 +524,29 @@ def handler_body(name, d, sr):
         return h_st_stk(int(name[5:])), False
     if name.startswith("LDXGEN"):
         return h_ldx_gen(int(name[6:]), d, sr), False
+    if name.startswith("LDXMAP"):
+        return h_ldx_map(int(name[6:]), d, sr), False
     if name.startswith("STXGEN"):
         return h_stx_gen(int(name[6:]), d, sr), False
     if name.startswith("STGEN"):
         return h_st_gen(int(name[5:]), d), False
     if name == "EXIT":
-        return ["s_setpc_b64 %s" % sp(S_R_EXIT)], True
+        return goto(".Lr_exit"), True
     if name == "FAULT":
         return ["s_mov_b32 %s, s14" % s(S_CODE), "s_mov_b64 %s, exec" % sp(S_MASK)] + \
-            call(S_R_FAULT) + ["s_endpgm"], True
+            call(".Lr_fault") + ["s_endpgm"], True
     if name == "NOP":
         return [], False
     if name == "LOOKUPSTK":
         return h_lookup_stk(), False
     if name == "LOOKUPGEN":
-        return call(S_R_LOOKUP), False
+        return call(".Lr_lookup"), False
     raise ValueError(name)
 
 
 # ---------------------------------------------------------------- shared routines
 def routines():
     L = []
-    q0, q1, r0_, r1_ = R[4], R[5], R[6], R[7]
 
     # --- schedule: pick the parked group of the first live lane
     L += [".Lr_schedule:",
@@ -524,17 +565,15 @@ def routines():
           "s_mov_b64 exec, %s" % sp(S_MASK),
           "v_mov_b32 v%d, s13" % V_T,
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK))] + dispatch(12)
-    # EXIT: value r0
+    # EXIT: value r0.  Stores are not waited for (the next group's vmcnt wait or the end of
+    # the program retires them).
     L += [".Lr_exit:",
-          "v_mov_b32 %s, 8" % v(R[8]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_RET)),
-          "global_store_dwordx2 %s, v[0:1], off" % vp(R[10]),
+          "v_lshlrev_b32 %s, 3, v%d" % (v(R[10]), V_GID),
+          "global_store_dwordx2 %s, v[0:1], %s" % (v(R[10]), sp(S_RET)),
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lex_nofault",
-          "v_mov_b32 %s, 1" % v(R[8]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_FAULTS)),
           "v_mov_b32 %s, 0" % v(R[8]),
-          "global_store_byte %s, %s, off" % (vp(R[10]), v(R[8])),
+          "global_store_byte v%d, %s, %s" % (V_GID, v(R[8]), sp(S_FAULTS)),
           ".Lex_nofault:",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lex_nohist",
@@ -545,37 +584,30 @@ def routines():
           "v_lshlrev_b32 %s, 2, %s" % (v(R[8]), v(R[8])),
           "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
           ".Lex_nohist:",
-          "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE)),
-          "s_waitcnt vmcnt(0) lgkmcnt(0)",
-          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+          "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE))] + goto(".Lr_schedule")
     # FAULT: lanes s[mask], code s[S_CODE]; returns via s[link] unless no lane remains
     L += [".Lr_fault:",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
           "s_mov_b64 exec, %s" % sp(S_MASK),
-          "v_mov_b32 %s, 8" % v(R[8]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_RET)),
+          "v_lshlrev_b32 %s, 3, v%d" % (v(R[10]), V_GID),
           "v_mov_b32 %s, 0" % v(R[8]),
           "v_mov_b32 %s, 0" % v(R[9]),
-          "global_store_dwordx2 %s, %s, off" % (vp(R[10]), vp(R[8])),
+          "global_store_dwordx2 %s, %s, %s" % (v(R[10]), vp(R[8]), sp(S_RET)),
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lfl_nofault",
-          "v_mov_b32 %s, 1" % v(R[8]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(R[10]), sp(S_JUNK), V_GID, v(R[8]), sp(S_FAULTS)),
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
-          "global_store_byte %s, %s, off" % (vp(R[10]), v(R[8])),
+          "global_store_byte v%d, %s, %s" % (V_GID, v(R[8]), sp(S_FAULTS)),
           ".Lfl_nofault:",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfl_nohist",
           "v_mov_b32 %s, 1024" % v(R[8]),
           "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
           ".Lfl_nohist:",
-          "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_andn2_b64 %s, %s, %s" % (sp(S_ALIVE), sp(S_ALIVE), sp(S_MASK)),
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
           "s_cbranch_execz .Lfl_none",
           "s_setpc_b64 %s" % sp(S_LINK),
-          ".Lfl_none:",
-          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+          ".Lfl_none:"] + goto(".Lr_schedule")
     # UDIVMOD64: n = R[0:1], d = R[2:3] (non-zero) -> q = R[4:5], r = R[6:7]; clobbers R[8:9]
     n, dd, q, r = vp(R[0]), vp(R[2]), vp(R[4]), vp(R[6])
     L += [".Lr_udiv:",
@@ -601,9 +633,7 @@ def routines():
           "s_setpc_b64 %s" % sp(S_LINK)]
     # CHECK: address H[0:1], size s[S_T0], write s[S_T1]; lanes outside every region fault
     # (MEM, or MAP_WRITE for a store into a map value); returns with exec = good lanes.
-    a = vp(H[0])
-    ok = sp(S_SAVE)           # accumulated ok mask
-    u = vp(R[0])
+    ok = sp(S_OK)             # accumulated ok mask (the fault routine leaves it alone)
     L += [".Lr_check:",
           "s_mov_b64 %s, 0" % ok,
           # packet: u = a - pkt; u_hi == 0 && len >= size && u_lo <= len - size
@@ -628,27 +658,24 @@ def routines():
           "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_T3), v(R[0])),
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
-          # maps: for m in table
+          # maps: for m in table (dp_map records of 32 B -> s[64:71])
           "s_mov_b32 %s, 0" % s(S_T2),
           ".Lck_map_loop:",
           "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
           "s_cbranch_scc1 .Lck_map_done",
-          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
-          "s_load_dwordx4 s[80:83], %s, %s" % (sp(S_MAPS), s(S_T3)),
-          "s_add_u32 %s, %s, 16" % (s(S_T3), s(S_T3)),
-          "s_load_dwordx2 s[84:85], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx8 s[%d:%d], %s, %s" % (S_REC, S_REC + 7, sp(S_MAPS), s(S_T3)),
           "s_waitcnt lgkmcnt(0)",
-          # s[82:83] = dev_base, s84 = value_size, s85 = max_entries
-          "s_mul_i32 %s, s84, s85" % s(S_T3),
-          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_T3), s(S_T0)),
-          "v_mov_b32 %s, s83" % v(R[3]),
-          "v_sub_co_u32 %s, vcc, %s, s82" % (v(R[0]), v(H[0])),
+          # s[66:67] = dev_base, s68 = value_size, s69 = max_entries
+          "s_mul_i32 %s, s68, s69" % s(S_BYTES),
+          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_BYTES), s(S_T0)),
+          "v_mov_b32 %s, s67" % v(R[3]),
+          "v_sub_co_u32 %s, vcc, %s, s66" % (v(R[0]), v(H[0])),
           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[3])),
           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
           "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_T3), v(R[0])),
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-          "s_mul_i32 s86, s84, s85",
-          "s_cmp_ge_u32 s86, %s" % s(S_T0),
+          "s_cmp_ge_u32 %s, %s" % (s(S_BYTES), s(S_T0)),
           "s_cselect_b64 %s, %s, 0" % (sp(S_JUNK), sp(S_JUNK)),
           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
           "s_cmp_eq_u32 %s, 0" % s(S_T1),
@@ -658,11 +685,8 @@ def routines():
           "s_cbranch_scc1 .Lck_map_next",
           "s_mov_b64 %s, %s" % (sp(S_MASK), sp(S_JUNK)),
           "s_mov_b32 %s, 9" % s(S_CODE),
-          "s_mov_b64 s[86:87], %s" % sp(S_LINK),
-          "s_mov_b64 s[80:81], %s" % ok,
-          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_FAULT)),
-          "s_mov_b64 %s, s[86:87]" % sp(S_LINK),
-          "s_mov_b64 %s, s[80:81]" % ok,
+          "s_mov_b64 %s, %s" % (sp(S_SV0), sp(S_LINK))] + call(".Lr_fault") + [
+          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_SV0)),
           "s_branch .Lck_map_next",
           ".Lck_map_ok:",
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
@@ -673,48 +697,46 @@ def routines():
           "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), ok),
           "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
           "s_cbranch_scc1 .Lck_ret",
-          "s_mov_b32 %s, 3" % s(S_CODE),
-          "s_setpc_b64 %s" % sp(S_R_FAULT),   # tail call: returns to our caller
+          "s_mov_b32 %s, 3" % s(S_CODE)] + goto(".Lr_fault") + [   # tail call: returns to our caller
           ".Lck_ret:",
           "s_setpc_b64 %s" % sp(S_LINK)]
-    # LOOKUP (generic): r0 = lookup(r1, r2) for any r1/r2 (NULL -> NULL, unknown map -> BAD_MAP)
+    # LOOKUP (generic): r0 = lookup(r1, r2) for any r1/r2 (NULL -> NULL, unknown map -> BAD_MAP).
+    # Lanes with r1 == 0 or r2 == 0 get r0 = NULL and are parked at the next entry first, so a
+    # fault that retires every other lane leaves them resumable by the scheduler.
     L += [".Lr_lookup:",
-          "s_mov_b64 s[86:87], %s" % sp(S_LINK),
+          "s_mov_b64 %s, %s" % (sp(S_SV0), sp(S_LINK)),
           "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
-          # lanes with r1 == 0 or r2 == 0 keep r0 = NULL
+          "v_mov_b32 v%d, s12" % V_T,
           "v_cmp_ne_u64_e64 %s, v[2:3], 0" % sp(S_JUNK),
           "v_cmp_ne_u64_e64 vcc, v[4:5], 0",
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
-          "s_mov_b64 s[88:89], exec",
+          "s_mov_b64 %s, exec" % sp(S_SV1),
           "s_mov_b64 exec, %s" % sp(S_JUNK),
           "s_cbranch_execz .Llk_done",
           # which lanes name a known map
-          "s_mov_b64 s[90:91], 0",
+          "s_mov_b64 %s, 0" % sp(S_OK),
           "s_mov_b32 %s, 0" % s(S_T2),
           ".Llk_scan:",
           "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
           "s_cbranch_scc1 .Llk_scan_done",
-          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
-          "s_load_dwordx2 s[80:81], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx2 s[%d:%d], %s, %s" % (S_REC, S_REC + 1, sp(S_MAPS), s(S_T3)),
           "s_waitcnt lgkmcnt(0)",
-          "v_cmp_eq_u64_e64 vcc, v[2:3], s[80:81]",
-          "s_or_b64 s[90:91], s[90:91], vcc",
+          "v_cmp_eq_u64_e64 vcc, v[2:3], s[%d:%d]" % (S_REC, S_REC + 1),
+          "s_or_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
           "s_branch .Llk_scan",
           ".Llk_scan_done:",
-          "s_andn2_b64 %s, exec, s[90:91]" % sp(S_MASK),
+          "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), sp(S_OK)),
           "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
           "s_cbranch_scc1 .Llk_known",
           "s_mov_b32 %s, 10" % s(S_CODE),
-          "s_andn2_b64 s[88:89], s[88:89], %s" % sp(S_MASK),
-          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_FAULT)),
+          "s_andn2_b64 %s, %s, %s" % (sp(S_SV1), sp(S_SV1), sp(S_MASK))] + call(".Lr_fault") + [
           ".Llk_known:",
           # key = *(u32*)r2, region checked
           "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1]),
-          "s_mov_b32 %s, 4" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1),
-          "s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_R_CHECK)),
-          "s_and_b64 s[88:89], s[88:89], -1"]   # (check may have retired lanes: alive updated)
+          "s_mov_b32 %s, 4" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check")
     key = v(H[2])
     L += ["v_mov_b32 %s, 0" % key]
     for b in range(4):
@@ -724,37 +746,54 @@ def routines():
     L += ["s_mov_b32 %s, 0" % s(S_T2),
           ".Llk_map:",
           "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
-          "s_cbranch_scc1 .Llk_done_lanes",
-          "s_mul_i32 %s, %s, 24" % (s(S_T3), s(S_T2)),
-          "s_load_dwordx4 s[80:83], %s, %s" % (sp(S_MAPS), s(S_T3)),
-          "s_add_u32 %s, %s, 16" % (s(S_T3), s(S_T3)),
-          "s_load_dwordx2 s[84:85], %s, %s" % (sp(S_MAPS), s(S_T3)),
+          "s_cbranch_scc1 .Llk_done",
+          "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx8 s[%d:%d], %s, %s" % (S_REC, S_REC + 7, sp(S_MAPS), s(S_T3)),
           "s_waitcnt lgkmcnt(0)",
-          "v_cmp_eq_u64_e64 %s, v[2:3], s[80:81]" % sp(S_JUNK),
-          "v_cmp_gt_u32_e64 vcc, s85, %s" % key,
+          "v_cmp_eq_u64_e64 %s, v[2:3], s[64:65]" % sp(S_JUNK),
+          "v_cmp_gt_u32_e64 vcc, s69, %s" % key,
           "s_and_b64 vcc, vcc, %s" % sp(S_JUNK),
-          "v_mov_b32 %s, s84" % v(H[3]),
-          "v_mad_u64_u32 %s, %s, %s, %s, s[82:83]" % (vp(H[4]), sp(S_JUNK), key, v(H[3])),
+          "v_mov_b32 %s, s68" % v(H[3]),
+          "v_mad_u64_u32 %s, %s, %s, %s, s[66:67]" % (vp(H[4]), sp(S_JUNK), key, v(H[3])),
           "v_cndmask_b32 v0, v0, %s, vcc" % v(H[4]),
           "v_cndmask_b32 v1, v1, %s, vcc" % v(H[5]),
           "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
           "s_branch .Llk_map",
-          ".Llk_done_lanes:",
           ".Llk_done:",
-          "s_and_b64 exec, s[88:89], %s" % sp(S_ALIVE),
-          "s_mov_b64 %s, s[86:87]" % sp(S_LINK),
+          "s_and_b64 exec, %s, %s" % (sp(S_SV1), sp(S_ALIVE)),
+          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_SV0)),
           "s_cbranch_execz .Llk_sched",
           "s_setpc_b64 %s" % sp(S_LINK),
-          ".Llk_sched:",
-          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+          ".Llk_sched:"] + goto(".Lr_schedule")
+    # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
+    # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
+    # past the batch end masked off.  Clobbers s[64:68], m0, exec.
+    L += [".Lr_prefetch:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_NGROUPS)),
+          "s_cbranch_scc1 .Lpf_ret",
+          "s_lshl_b32 s66, %s, 6" % s(S_T0),
+          "s_sub_u32 s66, %s, s66" % s(S_COUNT),           # packets left from this group on
+          "s_mov_b32 s64, %s" % s(S_T0),
+          "s_mov_b32 s65, 0",
+          "s_lshl_b64 s[64:65], s[64:65], 12",
+          "s_add_u32 s64, s64, %s" % s(S_DATA),
+          "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
+          "s_mov_b32 s67, %s" % s(S_PKTLDS)]
+    for qq in range(4):
+        L += ["s_sub_i32 s68, s66, %d" % (16 * qq),
+              "s_max_i32 s68, s68, 0",
+              "s_min_u32 s68, s68, 16",
+              "s_lshl_b32 s68, s68, 6",
+              "v_cmp_gt_u32_e64 exec, s68, v%d" % V_L16,
+              "s_mov_b32 m0, s67",
+              "s_nop 0",
+              "global_load_lds_dwordx4 v%d, s[64:65]" % V_L16]
+        if qq < 3:
+            L += ["s_add_u32 s64, s64, 1024", "s_addc_u32 s65, s65, 0",
+                  "s_add_u32 s67, s67, 1024"]
+    L += [".Lpf_ret:",
+          "s_setpc_b64 %s" % sp(S_LINK)]
     return L
-
-
-def addr_of(label, sgpr, base_label):
-    """s[sgpr:sgpr+1] = absolute address of `label` (after base_label, which follows a getpc
-    into s[S_T0..]) — emitted right after 's_getpc_b64 s[sgpr:sgpr+1]' at base_label."""
-    return ["s_add_u32 %s, %s, %s-%s" % (s(sgpr), s(sgpr), label, base_label),
-            "s_addc_u32 %s, %s, 0" % (s(sgpr + 1), s(sgpr + 1))]
 
 
 def kernel(name, staged):
@@ -765,99 +804,140 @@ def kernel(name, staged):
           "s_lshr_b32 %s, %s, 6" % (s(S_WAVE), s(S_WAVE)),
           "s_load_dwordx16 s[%d:%d], s[0:1], 0x0" % (S_PROG, S_PROG + 15),
           "s_load_dwordx8 s[%d:%d], s[0:1], 0x40" % (S_COUNT, S_COUNT + 7),
+          "s_load_dword %s, s[0:1], 0x60" % s(S_GSTRIDE),
+          "s_load_dword %s, s[0:1], 0x64" % s(S_PKTLDS),
           "s_mov_b64 %s, src_shared_base" % sp(S_SHARED),
           "s_mov_b32 %s, 0x0c0c0001" % s(S_SEL16),
-          "s_mov_b32 %s, 0x00010203" % s(S_SEL32)]
-    # routine addresses (all routines follow the kernels' prologues in .text)
-    for lab, reg in ((".Lr_schedule", S_R_SCHED), (".Lr_diverge", S_R_DIVERGE),
-                     (".Lr_fault", S_R_FAULT), (".Lr_exit", S_R_EXIT), (".Lr_udiv", S_R_DIV),
-                     (".Lr_check", S_R_CHECK), (".Lr_lookup", S_R_LOOKUP)):
-        base = ".L%s_pc_%d" % (k, reg)
-        L += ["s_getpc_b64 %s" % sp(reg), "%s:" % base] + addr_of(lab, reg, base)
-    # lane constants
-    L += ["v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
+          "s_mov_b32 %s, 0x00010203" % s(S_SEL32),
+          # code base: routines are addressed relative to .Lcb
+          "s_getpc_b64 %s" % sp(S_CB),
+          ".L%s_pc:" % k,
+          "s_add_u32 %s, %s, .Lcb-.L%s_pc" % (s(S_CB), s(S_CB), k),
+          "s_addc_u32 %s, %s, 0" % (s(S_CB + 1), s(S_CB + 1)),
+          "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
           "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
+          "v_lshlrev_b32 v%d, 4, %s" % (V_L16, v(H[0])),
           "v_mov_b32 v%d, 1" % V_ONE,
-          "s_waitcnt lgkmcnt(0)"]
-    # S_STKSTRIDE = dp_launch.stack_stride, S_LDSBASE = dp_launch.lds_stack_base
-    # lane stack bottom = lds_base + (wave*64 + lane) * stride
-    L += ["s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
-          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),
-          "v_mul_lo_u32 %s, %s, %s" % (v(H[1]), v(H[1]), s(S_STKSTRIDE)),
-          "v_add_u32 v%d, %s, %s" % (V_STK, s(S_LDSBASE), v(H[1]))]
-    # zero the LDS verdict histogram (257 bins: lanes 0..255 of the 4 waves, bin 256 by wave 0)
-    L += ["s_lshl_b32 %s, %s, 8" % (s(S_T0), s(S_WAVE)),
-          "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[0])),
-          "v_add_u32 %s, %s, %s" % (v(H[2]), s(S_T0), v(H[2])),
-          "v_mov_b32 %s, 0" % v(H[3]),
-          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .L%s_hz" % k,
-          "v_mov_b32 %s, 1024" % v(H[2]),
-          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
-          ".L%s_hz:" % k,
-          "s_waitcnt lgkmcnt(0)",
-          "s_barrier"]
-    # groups of 64 packets: group = workgroup*4 + wave, stride = 4*numgroups
-    L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
-          "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
-          "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
-          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
-          "s_load_dword %s, s[0:1], 0x60" % s(S_GSTRIDE),
           "s_waitcnt lgkmcnt(0)",
           "s_mov_b32 s7, %s" % ("1" if staged else "0"),
-          "s_branch .Lgroup_check"]
+          "s_branch .Lprologue"]
     return L
 
 
 def common_group_code():
     """Shared by both kernels (mode in s7: 1 = staged 64-B packets)."""
-    L = [".Lgroup_done:",
-         "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_GSTRIDE)),
-         ".Lgroup_check:",
-         "s_mov_b64 exec, -1",
-         "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
-         "s_cbranch_scc0 .Lfinish",
-         "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
-         "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
-         "v_lshl_add_u32 v%d, %s, 6, %s" % (V_GID, s(S_GROUP), v(H[0])),
-         "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), V_GID),
-         "s_mov_b64 exec, %s" % sp(S_ALIVE),
-         # packet address / length
-         "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
-         "s_cbranch_scc0 .Lgs_offsets",
-         "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
-         "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
-                                                      v(H[1]), sp(S_DATA)),
-         "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
-         "s_branch .Lgs_addr_done",
-         ".Lgs_offsets:",
-         "v_mov_b32 %s, 8" % v(H[1]),
-         "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[2]), sp(S_JUNK), V_GID, v(H[1]), sp(S_OFFS)),
-         "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[2])),
-         "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[2])),
-         "s_waitcnt vmcnt(0)",
-         "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
-         "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
-         "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
-         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
-         "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
-         ".Lgs_addr_done:",
-         "s_cmp_eq_u32 s7, 1",
-         "s_cbranch_scc0 .Lgs_nostage"]
+    L = [".Lcb:",
+         ".Lprologue:"]
+    # lane stack bottom = lds_base + (wave*64 + lane) * stride
+    L += ["s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),          # tid
+          "v_mul_lo_u32 %s, %s, %s" % (v(H[4]), v(H[1]), s(S_STKSTRIDE)),
+          "v_add_u32 v%d, %s, %s" % (V_STK, s(S_LDSBASE), v(H[4]))]
+    # zero the LDS verdict histogram (257 bins: lanes 0..255 of the 4 waves, bin 256 by wave 0)
+    L += ["v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
+          "v_mov_b32 %s, 0" % v(H[3]),
+          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
+          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
+          "s_cbranch_scc0 .Lhz",
+          "v_mov_b32 %s, 1024" % v(H[2]),
+          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
+          ".Lhz:"]
+    # copy the LDS-resident array maps (dp_map.lds_off != ~0) into LDS: 256 lanes x 4 B
+    L += ["v_lshlrev_b32 %s, 2, %s" % (v(H[4]), v(H[1])),
+          "s_mov_b32 %s, 0" % s(S_T2),
+          ".Lmc_loop:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
+          "s_cbranch_scc1 .Lmc_done",
+          "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx8 s[%d:%d], %s, %s" % (S_REC, S_REC + 7, sp(S_MAPS), s(S_T3)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_cmp_eq_u32 s70, -1",
+          "s_cbranch_scc1 .Lmc_loop",
+          "s_mul_i32 %s, s68, s69" % s(S_T1),
+          "s_mov_b32 %s, 0" % s(S_T0),
+          ".Lmc_chunk:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_T1)),
+          "s_cbranch_scc1 .Lmc_loop",
+          "v_add_u32 %s, %s, %s" % (v(H[5]), s(S_T0), v(H[4])),
+          "v_cmp_gt_u32_e64 exec, %s, %s" % (s(S_T1), v(H[5])),
+          "global_load_dword %s, %s, s[66:67]" % (v(H[3]), v(H[5])),
+          "s_waitcnt vmcnt(0)",
+          "v_add_u32 %s, s70, %s" % (v(H[5]), v(H[5])),
+          "ds_write_b32 %s, %s" % (v(H[5]), v(H[3])),
+          "s_mov_b64 exec, -1",
+          "s_add_u32 %s, %s, 1024" % (s(S_T0), s(S_T0)),
+          "s_branch .Lmc_chunk",
+          ".Lmc_done:",
+          "s_waitcnt lgkmcnt(0)",
+          "s_barrier"]
+    # groups of 64 packets: group = workgroup*4 + wave, stride = total waves
+    L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
+          "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
+          "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
+          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
+          # this wave's packet buffer (staged kernel); first group's prefetch
+          "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
+          "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),
+          "s_cmp_eq_u32 s7, 1",
+          "s_cbranch_scc0 .Lgroup_check",
+          "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
+          "s_branch .Lgroup_check"]
+    L += [".Lgroup_done:",
+          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_GSTRIDE)),
+          ".Lgroup_check:",
+          "s_mov_b64 exec, -1",
+          "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
+          "s_cbranch_scc0 .Lfinish",
+          "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
+          "v_lshl_add_u32 v%d, %s, 6, %s" % (V_GID, s(S_GROUP), v(H[0])),
+          "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), V_GID),
+          "s_cmp_eq_u32 s7, 1",
+          "s_cbranch_scc0 .Lgs_general",
+          # staged: this group's packets are (or are being) DMA'd into the packet buffer
+          "s_waitcnt vmcnt(0)",
+          "v_lshlrev_b32 %s, 2, v%d" % (v(H[1]), V_L16),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_PKTLDS), v(H[1]))]
     for q in range(4):
-        L.append("global_load_dwordx4 v[%d:%d], v[%d:%d], off offset:%d" % (
-            PKT0 + 4 * q, PKT0 + 4 * q + 3, V_PKT, V_PKT + 1, 16 * q))
-    L.append(".Lgs_nostage:")
+        L.append("ds_read_b128 v[%d:%d], %s offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
+                                                          v(H[1]), 16 * q))
+    L += ["s_waitcnt lgkmcnt(0)",
+          "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_GSTRIDE))] + call(".Lr_prefetch") + [
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          "v_mov_b32 %s, 64" % v(H[1]),
+          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
+                                                       v(H[1]), sp(S_DATA)),
+          "v_mov_b32 v%d, 64" % V_LEN,
+          "s_branch .Lgs_init",
+          ".Lgs_general:",
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          # packet address / length
+          "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
+          "s_cbranch_scc0 .Lgs_offsets",
+          "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
+          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
+                                                       v(H[1]), sp(S_DATA)),
+          "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
+          "s_branch .Lgs_init",
+          ".Lgs_offsets:",
+          "v_mov_b32 %s, 8" % v(H[1]),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[2]), sp(S_JUNK), V_GID, v(H[1]), sp(S_OFFS)),
+          "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[2])),
+          "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[2])),
+          "s_waitcnt vmcnt(0)",
+          "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
+          "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
+          "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
+          "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
+          "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
+          ".Lgs_init:"]
     for r in range(22):
         L.append("v_mov_b32 v%d, 0" % r)
     L += ["v_mov_b32 v2, v%d" % V_PKT, "v_mov_b32 v3, v%d" % (V_PKT + 1),
           "v_add_u32 v20, %s, v%d" % (s(S_STKSTRIDE), V_STK),
           "v_mov_b32 v21, %s" % s(S_SHARED + 1),
           "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),
-          "v_mov_b32 v%d, %s" % (V_T, s(S_T0)),
-          "s_waitcnt vmcnt(0)",
-          "s_setpc_b64 %s" % sp(S_R_SCHED)]
+          "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
     # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
     L += [".Lfinish:",
           "s_mov_b64 exec, -1",
@@ -865,8 +945,7 @@ def common_group_code():
           "s_barrier",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfin_end",
-          "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
-          "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
+          "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
           "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # bin
           ".Lfin_bin:",
@@ -875,12 +954,10 @@ def common_group_code():
           "s_waitcnt lgkmcnt(0)",
           "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[3]),
           "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE),
-          "v_mov_b32 %s, 8" % v(H[4]),
-          "v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(R[0]), sp(S_JUNK), v(H[1]), v(H[4]), sp(S_HIST)),
-          "v_mov_b32 %s, 0" % v(H[4]),
+          "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(H[1])),
           "v_mov_b32 %s, %s" % (v(R[2]), v(H[3])),
           "v_mov_b32 %s, 0" % v(R[3]),
-          "global_atomic_add_x2 %s, %s, off" % (vp(R[0]), vp(R[2])),
+          "global_atomic_add_x2 %s, %s, %s" % (v(R[0]), vp(R[2]), sp(S_HIST)),
           "s_mov_b64 exec, %s" % sp(S_SAVE),
           # wave 0 also owns bin 256
           "s_cmp_eq_u32 %s, 0" % s(S_WAVE),

@@ -38,8 +38,10 @@ struct dp_map {
 	uint64_t dev_base;    // device address of the mirror (max_entries * value_size bytes)
 	uint32_t value_size;
 	uint32_t max_entries;
+	uint32_t lds_off;     // assembly interpreter: LDS byte address of the map's copy, or ~0u
+	uint32_t pad;
 };
-static_assert(sizeof(dp_map) == 24, "dp_map is 24 bytes");
+static_assert(sizeof(dp_map) == 32, "dp_map is 32 bytes");
 
 // Kernel arguments (passed by value).
 struct dp_launch {
@@ -60,6 +62,6 @@ struct dp_launch {
 	uint32_t stack_stride;    // LDS bytes per lane stack slice (S' in asm_runtime.cpp)
 	uint32_t lds_stack_base;  // LDS byte offset of the first stack slice (after the histogram)
 	uint32_t total_waves;     // persistent grid: waves in the launch (group stride)
-	uint32_t pad;
+	uint32_t lds_pkt_base;    // staged kernel: LDS byte offset of the per-wave packet buffers
 };
 static_assert(sizeof(dp_launch) == 104, "dp_launch layout is shared with the assembly kernels");

@@ -15,7 +15,8 @@
 
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
-hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode);
+hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
+			     uint32_t map_lds_bytes);
 int asm_available(int device);
 bool asm_program_needs_general(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
@@ -152,6 +153,15 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		m.dev_base = (uint64_t)(uintptr_t)mdev;
 		m.value_size = em->value_size;
 		m.max_entries = em->max_entries;
+		// Small array maps are copied into LDS by the assembly interpreter at kernel start
+		// (value loads through a lookup result then read LDS).  Budget: kMapLdsBudget bytes.
+		const uint64_t bytes = (uint64_t)em->value_size * em->max_entries;
+		m.lds_off = ~0u;
+		m.pad = 0;
+		if (bytes > 0 && bytes % 4 == 0 && nd->map_lds_bytes + bytes <= kMapLdsBudget) {
+			m.lds_off = kMapLdsBase + nd->map_lds_bytes;
+			nd->map_lds_bytes += (uint32_t)((bytes + 15) & ~15ull);
+		}
 		nd->table.push_back(m);
 	}
 	if (!nd->table.empty()) {
@@ -207,7 +217,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			return err;
 		L.prog = dp->d_asm[mode];
 		L.stack_stride = dp->asm_stride[mode];
-		e = launch_interp_asm(L, stream, dp->device, mode);
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes);
 	} else {
 		L.prog = dp->d_entries;
 		e = launch_interp_v0(L, stream);

@@ -65,6 +65,14 @@ struct ebpf_map {
 	uint8_t *array_storage() const;
 };
 
+// Assembly-interpreter LDS layout (per workgroup): verdict histogram [0, kHistLds), LDS-resident
+// array-map copies [kMapLdsBase, + map_lds_bytes), staged kernel only: 4 per-wave 4-KB packet
+// buffers, then the 256 per-lane stack slices.
+constexpr uint32_t kHistLds = 1040;
+constexpr uint32_t kMapLdsBase = kHistLds;
+constexpr uint32_t kMapLdsBudget = 8192;
+constexpr uint32_t kPktLdsPerWG = 4 * 4096;
+
 // Per (program, device): entries for each interpreter variant and the map table.
 struct dprog_device {
 	int device = -1;
@@ -73,6 +81,7 @@ struct dprog_device {
 	std::vector<dp_map> table;
 	uint32_t nentries = 0;
 	uint32_t nmaps = 0;
+	uint32_t map_lds_bytes = 0;      // LDS bytes taken by LDS-resident map copies (asm kernels)
 	dp_entry *d_asm[2] = {nullptr, nullptr}; // variant 0: lowered + linked, per mode
 	uint32_t asm_stride[2] = {0, 0};         // LDS stack bytes per lane, per mode
 	int asm_err[2] = {0, 0};

@@ -244,7 +244,26 @@ def prog_c5(seed=7, target=256):
     raise ValueError("cannot fit C5")
 
 
+def prog_c0():
+    """Floor: MOV r0, 2; EXIT (2 executed instructions) — measures staging + retirement."""
+    return assemble([I("mov_imm", R0, imm=2), I("exit")])
+
+
+def prog_chain(kind, n=200):
+    """Microbenchmarks: n straight-line instructions of one kind, then EXIT.
+    kind "nop": LE r0, 64 (a no-op in the reference); "alu": ADD64 r0, imm."""
+    body = [I("mov_imm", R0, imm=1)]
+    for k in range(n):
+        body.append(I("le", R0, imm=64) if kind == "nop" else I("add64_imm", R0, imm=k))
+    return assemble(body + [I("exit")])
+
+
 CONFIGS = {
+    "nop200": dict(desc="microbench: 200 no-op dispatches", prog=lambda: prog_chain("nop"),
+                   pkt="random"),
+    "alu200": dict(desc="microbench: 200 ADD64 dispatches", prog=lambda: prog_chain("alu"),
+                   pkt="random"),
+    "c0": dict(desc="2-insn floor (MOV r0; EXIT), 64 B packets", prog=prog_c0, pkt="random"),
     "c2": dict(desc="8-insn ALU-only, 64 B random packets", prog=prog_c2, pkt="random"),
     "c3": dict(desc="64-insn L2/L3 parse+classify, 64 B packets", prog=prog_c3, pkt="l2l3"),
     "c4": dict(desc="64-insn classify + array-map lookup, 64 B packets", prog=prog_c4,
