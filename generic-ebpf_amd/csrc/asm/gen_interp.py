@@ -17,9 +17,15 @@ Execution model (one lane = one packet, wavefront-lockstep dispatch):
   * lanes that disagree on a conditional jump are parked (v41 = their entry) and resumed after
     the running group retires; retirement writes r0, the fault code and an LDS histogram.
 """
+import os
 import sys
 
 NREG = 11
+# cache policy of the streaming accesses (experiments: EBPF_ASM_NT bit 0 = ret stores nt,
+# bit 1 = packet DMA loads nt)
+_NT = int(os.environ.get("EBPF_ASM_NT", "0"))
+ST_POLICY = " nt" if _NT & 1 else ""
+LD_POLICY = " nt" if _NT & 2 else ""
 # ---------------------------------------------------------------- register plan
 PKT0 = 22            # v22..v37 staged packet dwords (staged kernel)
 V_PKT = 38           # v[38:39] packet base address
@@ -30,7 +36,8 @@ V_GID = 43           # packet index within the launch
 V_L16 = 44           # lane * 16 (LDS-DMA staging offset)
 V_ONE = 45           # constant 1
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
-R = list(range(52, 64))              # routine temporaries
+R = list(range(52, 63))              # routine temporaries
+V_SEL = 63                           # v_perm selector 0x00010203 (byte swap)
 NVGPR = 64
 
 # SGPRs (next_free_sgpr 80 -> 8 waves per SIMD)
@@ -50,14 +57,10 @@ S_T0, S_T1, S_T2, S_T3 = 53, 54, 55, 56
 S_BYTES = 57         # check routine scratch
 S_SHARED = 58        # s[58:59] src_shared_base
 S_JUNK = 60          # s[60:61] scratch sdst
-S_JA = 62            # s[62:63] routine jump address
-S_SEL16, S_SEL32 = 72, 73
+S_OK = 62            # s[62:63] check: accumulated ok lanes
 S_REC = 64           # s[64:71] map record {handle, dev_base, value_size, max_entries, lds_off, pad}
-S_OK = 74            # s[74:75] check: accumulated ok lanes
-S_SV0 = 76           # s[76:77] saved link (lookup / check write path)
-S_SV1 = 78           # s[78:79] saved mask (lookup / check write path)
 S_WAVE = 3
-NSGPR = 80
+NSGPR = 72           # + VCC, XNACK, FLAT_SCRATCH = 78 <= 80 SGPRs: 8 waves per SIMD
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -152,17 +155,20 @@ def dispatch(next_reg=12):
             "s_setpc_b64 s[8:9]"]
 
 
-def raddr(label):
-    return ["s_add_u32 %s, %s, %s-.Lcb" % (s(S_JA), s(S_CB), label),
-            "s_addc_u32 %s, %s, 0" % (s(S_JA + 1), s(S_CB + 1))]
+def raddr(label, pair_):
+    return ["s_add_u32 %s, %s, %s-.Lcb" % (s(pair_), s(S_CB), label),
+            "s_addc_u32 %s, %s, 0" % (s(pair_ + 1), s(S_CB + 1))]
 
 
 def call(label):
-    return raddr(label) + ["s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_JA))]
+    """Call a routine: its address is formed in the link pair, which the swap then
+    overwrites with the return address (a routine that calls another saves its own link)."""
+    return raddr(label, S_LINK) + ["s_swappc_b64 %s, %s" % (sp(S_LINK), sp(S_LINK))]
 
 
 def goto(label):
-    return raddr(label) + ["s_setpc_b64 %s" % sp(S_JA)]
+    """Jump to a routine through the scratch pair (the link pair may be live: tail calls)."""
+    return raddr(label, S_JUNK) + ["s_setpc_b64 %s" % sp(S_JUNK)]
 
 
 def fault_mask(mask_sgpr_pair, code):
@@ -318,11 +324,12 @@ def h_cond(c, d, sr, imm):
 def h_bswap(w, d):
     D0, D1 = lo(d), hi(d)
     if w == 16:
-        return ["v_perm_b32 %s, 0, %s, %s" % (D0, D0, s(S_SEL16)), "v_mov_b32 %s, 0" % D1]
+        return ["v_perm_b32 %s, 0, %s, v%d" % (D0, D0, V_SEL),
+                "v_lshrrev_b32 %s, 16, %s" % (D0, D0), "v_mov_b32 %s, 0" % D1]
     if w == 32:
-        return ["v_perm_b32 %s, 0, %s, %s" % (D0, D0, s(S_SEL32)), "v_mov_b32 %s, 0" % D1]
-    return ["v_perm_b32 %s, 0, %s, %s" % (v(H[0]), D0, s(S_SEL32)),
-            "v_perm_b32 %s, 0, %s, %s" % (D0, D1, s(S_SEL32)),
+        return ["v_perm_b32 %s, 0, %s, v%d" % (D0, D0, V_SEL), "v_mov_b32 %s, 0" % D1]
+    return ["v_perm_b32 %s, 0, %s, v%d" % (v(H[0]), D0, V_SEL),
+            "v_perm_b32 %s, 0, %s, v%d" % (D0, D1, V_SEL),
             "v_mov_b32 %s, %s" % (D1, v(H[0]))]
 
 
@@ -540,7 +547,7 @@ def handler_body(name, d, sr):
     if name == "LOOKUPSTK":
         return h_lookup_stk(), False
     if name == "LOOKUPGEN":
-        return call(".Lr_lookup"), False
+        return goto(".Lr_lookup"), True
     raise ValueError(name)
 
 
@@ -569,7 +576,7 @@ def routines():
     # the program retires them).
     L += [".Lr_exit:",
           "v_lshlrev_b32 %s, 3, v%d" % (v(R[10]), V_GID),
-          "global_store_dwordx2 %s, v[0:1], %s" % (v(R[10]), sp(S_RET)),
+          "global_store_dwordx2 %s, v[0:1], %s%s" % (v(R[10]), sp(S_RET), ST_POLICY),
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lex_nofault",
           "v_mov_b32 %s, 0" % v(R[8]),
@@ -581,6 +588,22 @@ def routines():
           "v_mov_b32 %s, 0" % v(R[9]),
           "v_cmp_lt_u64_e64 vcc, v[0:1], %s" % vp(R[8]),
           "v_cndmask_b32 %s, %s, v0, vcc" % (v(R[8]), v(R[8])),
+          # one LDS atomic per wave when every exiting lane has the same verdict (the usual
+          # case); per-lane adds to one address would serialise
+          "v_readfirstlane_b32 %s, %s" % (s(S_BYTES), v(R[8])),
+          "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_MASK), s(S_BYTES), v(R[8])),
+          "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
+          "s_cbranch_scc0 .Lex_lanes",
+          "s_bcnt1_i32_b64 %s, exec" % s(S_CODE),
+          "s_lshl_b32 %s, %s, 2" % (s(S_BYTES), s(S_BYTES)),
+          "s_mov_b64 %s, exec" % sp(S_SAVE),
+          "s_mov_b64 exec, 1",
+          "v_mov_b32 %s, %s" % (v(R[8]), s(S_BYTES)),
+          "v_mov_b32 %s, %s" % (v(R[9]), s(S_CODE)),
+          "ds_add_u32 %s, %s" % (v(R[8]), v(R[9])),
+          "s_mov_b64 exec, %s" % sp(S_SAVE),
+          "s_branch .Lex_nohist",
+          ".Lex_lanes:",
           "v_lshlrev_b32 %s, 2, %s" % (v(R[8]), v(R[8])),
           "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
           ".Lex_nohist:",
@@ -598,10 +621,16 @@ def routines():
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
           "global_store_byte v%d, %s, %s" % (V_GID, v(R[8]), sp(S_FAULTS)),
           ".Lfl_nofault:",
+          # bin 256 (faulted) goes straight to the global histogram: faults are rare, and the
+          # LDS histogram then holds exactly 256 bins (1 KB)
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfl_nohist",
-          "v_mov_b32 %s, 1024" % v(R[8]),
-          "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
+          "s_bcnt1_i32_b64 %s, exec" % s(S_BYTES),
+          "v_mov_b32 %s, %s" % (v(R[8]), s(S_BYTES)),
+          "v_mov_b32 %s, 0" % v(R[9]),
+          "v_mov_b32 %s, 0" % v(R[10]),
+          "s_mov_b64 exec, 1",
+          "global_atomic_add_x2 %s, %s, %s offset:2048" % (v(R[10]), vp(R[8]), sp(S_HIST)),
           ".Lfl_nohist:",
           "s_andn2_b64 %s, %s, %s" % (sp(S_ALIVE), sp(S_ALIVE), sp(S_MASK)),
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
@@ -685,8 +714,8 @@ def routines():
           "s_cbranch_scc1 .Lck_map_next",
           "s_mov_b64 %s, %s" % (sp(S_MASK), sp(S_JUNK)),
           "s_mov_b32 %s, 9" % s(S_CODE),
-          "s_mov_b64 %s, %s" % (sp(S_SV0), sp(S_LINK))] + call(".Lr_fault") + [
-          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_SV0)),
+          "s_mov_b64 %s, %s" % (sp(S_REC + 6), sp(S_LINK))] + call(".Lr_fault") + [
+          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_REC + 6)),
           "s_branch .Lck_map_next",
           ".Lck_map_ok:",
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
@@ -700,20 +729,17 @@ def routines():
           "s_mov_b32 %s, 3" % s(S_CODE)] + goto(".Lr_fault") + [   # tail call: returns to our caller
           ".Lck_ret:",
           "s_setpc_b64 %s" % sp(S_LINK)]
-    # LOOKUP (generic): r0 = lookup(r1, r2) for any r1/r2 (NULL -> NULL, unknown map -> BAD_MAP).
-    # Lanes with r1 == 0 or r2 == 0 get r0 = NULL and are parked at the next entry first, so a
-    # fault that retires every other lane leaves them resumable by the scheduler.
+    # LOOKUP (generic, entered by goto, leaves by dispatch): r0 = lookup(r1, r2) for any r1/r2
+    # (NULL -> NULL, unknown map -> BAD_MAP).  Lanes with r1 == 0 or r2 == 0 get r0 = NULL and
+    # are parked at the next entry (the scheduler resumes them after the running lanes).
     L += [".Lr_lookup:",
-          "s_mov_b64 %s, %s" % (sp(S_SV0), sp(S_LINK)),
           "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
           "v_mov_b32 v%d, s12" % V_T,
           "v_cmp_ne_u64_e64 %s, v[2:3], 0" % sp(S_JUNK),
           "v_cmp_ne_u64_e64 vcc, v[4:5], 0",
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-          "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
-          "s_mov_b64 %s, exec" % sp(S_SV1),
-          "s_mov_b64 exec, %s" % sp(S_JUNK),
-          "s_cbranch_execz .Llk_done",
+          "s_and_b64 exec, %s, exec" % sp(S_JUNK),
+          "s_cbranch_execz .Llk_sched",
           # which lanes name a known map
           "s_mov_b64 %s, 0" % sp(S_OK),
           "s_mov_b32 %s, 0" % s(S_T2),
@@ -731,8 +757,7 @@ def routines():
           "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), sp(S_OK)),
           "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
           "s_cbranch_scc1 .Llk_known",
-          "s_mov_b32 %s, 10" % s(S_CODE),
-          "s_andn2_b64 %s, %s, %s" % (sp(S_SV1), sp(S_SV1), sp(S_MASK))] + call(".Lr_fault") + [
+          "s_mov_b32 %s, 10" % s(S_CODE)] + call(".Lr_fault") + [
           ".Llk_known:",
           # key = *(u32*)r2, region checked
           "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1]),
@@ -759,11 +784,7 @@ def routines():
           "v_cndmask_b32 v1, v1, %s, vcc" % v(H[5]),
           "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
           "s_branch .Llk_map",
-          ".Llk_done:",
-          "s_and_b64 exec, %s, %s" % (sp(S_SV1), sp(S_ALIVE)),
-          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_SV0)),
-          "s_cbranch_execz .Llk_sched",
-          "s_setpc_b64 %s" % sp(S_LINK),
+          ".Llk_done:"] + dispatch(12) + [
           ".Llk_sched:"] + goto(".Lr_schedule")
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
@@ -787,7 +808,7 @@ def routines():
               "v_cmp_gt_u32_e64 exec, s68, v%d" % V_L16,
               "s_mov_b32 m0, s67",
               "s_nop 0",
-              "global_load_lds_dwordx4 v%d, s[64:65]" % V_L16]
+              "global_load_lds_dwordx4 v%d, s[64:65]%s" % (V_L16, LD_POLICY)]
         if qq < 3:
             L += ["s_add_u32 s64, s64, 1024", "s_addc_u32 s65, s65, 0",
                   "s_add_u32 s67, s67, 1024"]
@@ -807,8 +828,7 @@ def kernel(name, staged):
           "s_load_dword %s, s[0:1], 0x60" % s(S_GSTRIDE),
           "s_load_dword %s, s[0:1], 0x64" % s(S_PKTLDS),
           "s_mov_b64 %s, src_shared_base" % sp(S_SHARED),
-          "s_mov_b32 %s, 0x0c0c0001" % s(S_SEL16),
-          "s_mov_b32 %s, 0x00010203" % s(S_SEL32),
+          "v_mov_b32 v%d, 0x00010203" % V_SEL,
           # code base: routines are addressed relative to .Lcb
           "s_getpc_b64 %s" % sp(S_CB),
           ".L%s_pc:" % k,
@@ -833,15 +853,10 @@ def common_group_code():
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),          # tid
           "v_mul_lo_u32 %s, %s, %s" % (v(H[4]), v(H[1]), s(S_STKSTRIDE)),
           "v_add_u32 v%d, %s, %s" % (V_STK, s(S_LDSBASE), v(H[4]))]
-    # zero the LDS verdict histogram (257 bins: lanes 0..255 of the 4 waves, bin 256 by wave 0)
+    # zero the LDS verdict histogram (bins 0..255, one per lane of the 4 waves)
     L += ["v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
           "v_mov_b32 %s, 0" % v(H[3]),
-          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lhz",
-          "v_mov_b32 %s, 1024" % v(H[2]),
-          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3])),
-          ".Lhz:"]
+          "ds_write_b32 %s, %s" % (v(H[2]), v(H[3]))]
     # copy the LDS-resident array maps (dp_map.lds_off != ~0) into LDS: 256 lanes x 4 B
     L += ["v_lshlrev_b32 %s, 2, %s" % (v(H[4]), v(H[1])),
           "s_mov_b32 %s, 0" % s(S_T2),
@@ -948,7 +963,6 @@ def common_group_code():
           "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
           "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # bin
-          ".Lfin_bin:",
           "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
           "ds_read_b32 %s, %s" % (v(H[3]), v(H[2])),
           "s_waitcnt lgkmcnt(0)",
@@ -958,14 +972,6 @@ def common_group_code():
           "v_mov_b32 %s, %s" % (v(R[2]), v(H[3])),
           "v_mov_b32 %s, 0" % v(R[3]),
           "global_atomic_add_x2 %s, %s, %s" % (v(R[0]), vp(R[2]), sp(S_HIST)),
-          "s_mov_b64 exec, %s" % sp(S_SAVE),
-          # wave 0 also owns bin 256
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lfin_end",
-          "s_mov_b32 %s, 1" % s(S_WAVE),       # run once more, lane 0 only, bin 256
-          "v_mov_b32 %s, 256" % v(H[1]),
-          "s_mov_b64 exec, 1",
-          "s_branch .Lfin_bin",
           ".Lfin_end:",
           "s_waitcnt vmcnt(0)",
           "s_endpgm"]
@@ -1016,6 +1022,7 @@ def kd(name, lds, vgprs, sgprs, kernarg, wgsize):
             ".amdhsa_next_free_sgpr %d" % sgprs,
             ".amdhsa_accum_offset %d" % vgprs,
             ".amdhsa_reserve_vcc 1",
+            ".amdhsa_reserve_xnack_mask 0",
             ".amdhsa_ieee_mode 0",
             ".amdhsa_dx10_clamp 0",
             ".end_amdhsa_kernel", ".text"]
@@ -1038,14 +1045,14 @@ def metadata(kernels):
                 "    .symbol: %s.kd" % name,
                 "    .vgpr_count: %d" % vgprs,
                 "    .wavefront_size: 64"]
-    out += ["amdhsa.target: amdgcn-amd-amdhsa--gfx950", "amdhsa.version:", "  - 1", "  - 2",
+    out += ["amdhsa.target: amdgcn-amd-amdhsa--gfx950:xnack-", "amdhsa.version:", "  - 1", "  - 2",
             "...", ".end_amdgpu_metadata"]
     return out
 
 
 def main():
     out_s, out_h = sys.argv[1], sys.argv[2]
-    A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text"]
+    A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950:xnack-"', ".amdhsa_code_object_version 5", ".text"]
     A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
     A += common_group_code() + routines()
     table = []

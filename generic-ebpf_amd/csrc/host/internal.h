@@ -68,7 +68,7 @@ struct ebpf_map {
 // Assembly-interpreter LDS layout (per workgroup): verdict histogram [0, kHistLds), LDS-resident
 // array-map copies [kMapLdsBase, + map_lds_bytes), staged kernel only: 4 per-wave 4-KB packet
 // buffers, then the 256 per-lane stack slices.
-constexpr uint32_t kHistLds = 1040;
+constexpr uint32_t kHistLds = 1024; // bins 0..255 (bin 256 is counted in global memory)
 constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
