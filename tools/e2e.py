@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""End-to-end (host memory in, host memory out) rate of ebpf_prog_run_batch: packets start in a
+host buffer (pinned, as a NIC ring or pcap buffer would be, or pageable), results land in a host
+array.  Includes H2D, kernel and D2H (chunked, double-buffered on two streams inside the library).
+Prints one JSON line per buffer kind."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import pkgload  # noqa: E402
+
+pkgload.load()
+from generic_ebpf_amd import native, workloads  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--packets", type=int, default=1 << 26)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    n = a.packets
+    lay = workloads.CONFIGS[a.config]["prog"]()
+    env = native.Env()
+    maps = []
+    if a.config == "c4":
+        m = native.Map(env, 256, 8)
+        m.fill(workloads.c4_map_values().tobytes())
+        maps.append(m)
+    prog = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    prog.prepare(0)
+    distinct = workloads.packets_l2l3(1 << 22, 64, seed=3)
+    for kind in ("pinned", "pageable"):
+        t = torch.empty(n * 64, dtype=torch.uint8, pin_memory=(kind == "pinned"))
+        host = t.numpy()
+        reps = (n + distinct.shape[0] - 1) // distinct.shape[0]
+        for r in range(reps):
+            lo = r * distinct.shape[0]
+            hi = min(n, lo + distinct.shape[0])
+            host[lo * 64:hi * 64] = distinct[: hi - lo].reshape(-1)
+        rt = torch.empty(n, dtype=torch.int64, pin_memory=(kind == "pinned"))
+        ret = rt.numpy().view(np.uint64)
+        st = native.BatchStats()
+        b = native.PktBatch(host.ctypes.data, None, n, 64, 0)
+        native._check(native.lib().ebpf_prog_run_batch(prog.ptr, native.ctypes.byref(b),
+                                                        ret.ctypes.data, None,
+                                                        native.ctypes.byref(st)), "warm")
+        best = None
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            native._check(native.lib().ebpf_prog_run_batch(prog.ptr, native.ctypes.byref(b),
+                                                            ret.ctypes.data, None,
+                                                            native.ctypes.byref(st)), "run")
+            el = time.perf_counter() - t0
+            if best is None or el < best[0]:
+                best = (el, st.kernel_ms, st.total_ms)
+        el, kms, tms = best
+        print(json.dumps({"e2e": kind, "config": a.config, "packets": n,
+                          "mpkt_s": round(n / el / 1e6, 1), "wall_ms": round(el * 1e3, 2),
+                          "kernel_ms_sum": round(kms, 2), "h2d_gb_s": round(n * 64 / el / 1e9, 2),
+                          "faulted": int(st.faulted)}), flush=True)
+        del t, rt
+    prog.destroy()
+    for m in maps:
+        m.destroy()
+    env.destroy()
+
+
+if __name__ == "__main__":
+    main()

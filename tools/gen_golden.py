@@ -7,7 +7,7 @@ compiles oracle/refgen/ref_harness.c against it (outputs only under oracle/_ref/
 case to a binary case file, runs the harness (every packet twice under two stack poisons), and
 keeps a case only if no packet read undefined state.
 
-Usage: python tools/gen_golden.py [--ref-lib-dir DIR] [--quick]
+Usage: python tools/gen_golden.py [--quick] [--rand N] [--pkts N]
 """
 import argparse
 import os
@@ -154,13 +154,15 @@ def workload_cases(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--rand", type=int, default=200, help="random-program cases")
+    ap.add_argument("--pkts", type=int, default=2048, help="packets per workload case")
     args = ap.parse_args()
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_ref/ref_harness"])
     os.makedirs(goldens.GOLDEN_DIR, exist_ok=True)
     groups = {
         "kat": kat_cases(),
-        "rand": rand_cases(40 if args.quick else 400, 1000),
-        "workloads": workload_cases(512 if args.quick else 4096),
+        "rand": rand_cases(40 if args.quick else args.rand, 1000),
+        "workloads": workload_cases(512 if args.quick else args.pkts),
     }
     with tempfile.TemporaryDirectory() as tmp:
         for gname, cases in groups.items():
