@@ -311,7 +311,8 @@ def h_cond(c, d, sr, imm):
         out.append("v_cmp_ne_u64_e64 vcc, %s, 0" % vp(H[0]))
     else:
         out.append("v_cmp_%s_e64 vcc, %s, %s" % (CMP[c], pair(d), srcop))
-    out += ["s_and_b64 %s, vcc, exec" % sp(S_MASK),
+    out += ["@CMPEND",
+            "s_and_b64 %s, vcc, exec" % sp(S_MASK),
             "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
             "s_cbranch_scc1 .Ltk_{uid}",
             "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
@@ -563,8 +564,15 @@ def routines():
           "v_readlane_b32 s6, v%d, %s" % (V_T, s(S_T0)),
           "v_cmp_eq_u32_e64 %s, s6, v%d" % (sp(S_MASK), V_T),
           "s_and_b64 exec, %s, %s" % (sp(S_MASK), sp(S_ALIVE)),
+          "s_bitcmp1_b32 s7, 1",
+          "s_cbranch_scc1 .Lsched_jit",
           "s_load_dwordx8 s[8:15], s[%d:%d], s6" % (S_PROG, S_PROG + 1),
           "s_waitcnt lgkmcnt(0)",
+          "s_setpc_b64 s[8:9]",
+          # compiled program: V_T is a code offset from .Lcb
+          ".Lsched_jit:",
+          "s_add_u32 s8, %s, s6" % s(S_CB),
+          "s_addc_u32 s9, %s, 0" % s(S_CB + 1),
           "s_setpc_b64 s[8:9]"]
     # --- diverge: taken lanes (s[mask]) park at the target, the rest continue
     L += [".Lr_diverge:",
@@ -784,7 +792,13 @@ def routines():
           "v_cndmask_b32 v1, v1, %s, vcc" % v(H[5]),
           "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
           "s_branch .Llk_map",
-          ".Llk_done:"] + dispatch(12) + [
+          ".Llk_done:",
+          "s_bitcmp1_b32 s7, 1",
+          "s_cbranch_scc1 .Llk_jit"] + dispatch(12) + [
+          ".Llk_jit:",     # compiled program: s12 = code offset of the next block
+          "s_add_u32 %s, %s, s12" % (s(S_JUNK), s(S_CB)),
+          "s_addc_u32 %s, %s, 0" % (s(S_JUNK + 1), s(S_CB + 1)),
+          "s_setpc_b64 %s" % sp(S_JUNK)] + [
           ".Llk_sched:"] + goto(".Lr_schedule")
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
@@ -817,8 +831,8 @@ def routines():
     return L
 
 
-def kernel(name, staged):
-    k = "K%s" % ("s" if staged else "g")
+def kernel(name, staged, jit=False):
+    k = "K%s%s" % ("s" if staged else "g", "j" if jit else "")
     L = [".globl %s" % name, ".p2align 8", ".type %s,@function" % name, "%s:" % name]
     # v0 = workitem id; wave index within the 256-lane workgroup
     L += ["v_readfirstlane_b32 %s, v0" % s(S_WAVE),
@@ -839,14 +853,15 @@ def kernel(name, staged):
           "v_lshlrev_b32 v%d, 4, %s" % (V_L16, v(H[0])),
           "v_mov_b32 v%d, 1" % V_ONE,
           "s_waitcnt lgkmcnt(0)",
-          "s_mov_b32 s7, %s" % ("1" if staged else "0"),
+          "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0)),
           "s_branch .Lprologue"]
     return L
 
 
 def common_group_code():
-    """Shared by both kernels (mode in s7: 1 = staged 64-B packets)."""
+    """Shared by all kernels (s7 bit 0: staged 64-B packets; bit 1: compiled program)."""
     L = [".Lcb:",
+         "ebpf_cb:",
          ".Lprologue:"]
     # lane stack bottom = lds_base + (wave*64 + lane) * stride
     L += ["s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
@@ -894,7 +909,7 @@ def common_group_code():
           # this wave's packet buffer (staged kernel); first group's prefetch
           "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
           "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),
-          "s_cmp_eq_u32 s7, 1",
+          "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgroup_check",
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
@@ -907,7 +922,7 @@ def common_group_code():
           "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
           "v_lshl_add_u32 v%d, %s, 6, %s" % (V_GID, s(S_GROUP), v(H[0])),
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), V_GID),
-          "s_cmp_eq_u32 s7, 1",
+          "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgs_general",
           # staged: this group's packets are (or are being) DMA'd into the packet buffer
           "s_waitcnt vmcnt(0)",
@@ -952,6 +967,8 @@ def common_group_code():
           "v_add_u32 v20, %s, v%d" % (s(S_STKSTRIDE), V_STK),
           "v_mov_b32 v21, %s" % s(S_SHARED + 1),
           "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),
+          "s_bitcmp1_b32 s7, 1",
+          "s_cselect_b32 %s, ebpf_jit_area-.Lcb, %s" % (s(S_T0), s(S_T0)),
           "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
     # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
     L += [".Lfinish:",
@@ -1050,43 +1067,156 @@ def metadata(kernels):
     return out
 
 
+JIT_AREA_BYTES = 512 * 1024
+ENTRY_SGPR_RE = None
+
+
+def entry_reads(lines):
+    """6-bit mask of the entry SGPRs s10..s15 a handler body reads (compiled programs set
+    exactly those before the copied body)."""
+    import re
+    global ENTRY_SGPR_RE
+    if ENTRY_SGPR_RE is None:
+        ENTRY_SGPR_RE = re.compile(r"(?<![\w\[:])s(1[0-5])(?![\w\]])|s\[(1[0-5]):(1[0-5])\]")
+    m = 0
+    for ln in lines:
+        code = ln.split("//")[0]
+        for x in ENTRY_SGPR_RE.finditer(code):
+            if x.group(1):
+                m |= 1 << (int(x.group(1)) - 10)
+            else:
+                for r in range(int(x.group(2)), int(x.group(3)) + 1):
+                    m |= 1 << (r - 10)
+    return m
+
+
+def jit_templates():
+    """Glue the host's copy-and-patch compiler stitches between copied handler bodies.  Never
+    executed in place.  Literals 0x5eed5eed and branch offsets are patched per use."""
+    L = [".p2align 2", "ebpf_jit_templates:"]
+    for r in range(10, 16):
+        L += [".Ljt_mov_s%d:" % r, "s_mov_b32 s%d, 0x5eed5eed" % r]
+    # conditional tail, short form: all lanes taken -> branch; none -> fall through; mixed ->
+    # park the taken lanes at the taken block (v41 = its code offset), continue not-taken
+    L += [".Ljt_cs:",
+          "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+          "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
+          ".Ljt_cs_br:",
+          "s_cbranch_scc1 .Ljt_cs_br",
+          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+          "s_cbranch_scc1 .Ljt_cs_end",
+          "s_mov_b64 %s, exec" % sp(S_SAVE),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          ".Ljt_cs_vt:",
+          "v_mov_b32 v%d, 0x5eed5eed" % V_T,
+          "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
+          ".Ljt_cs_end:"]
+    # long form (taken block beyond a 16-bit branch)
+    L += [".Ljt_cl:",
+          "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+          "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
+          "s_cbranch_scc0 .Ljt_cl_skip",
+          ".Ljt_cl_lit:",
+          "s_add_u32 %s, %s, 0x5eed5eed" % (s(S_JUNK), s(S_CB)),
+          "s_addc_u32 %s, %s, 0" % (s(S_JUNK + 1), s(S_CB + 1)),
+          "s_setpc_b64 %s" % sp(S_JUNK),
+          ".Ljt_cl_skip:",
+          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+          "s_cbranch_scc1 .Ljt_cl_end",
+          "s_mov_b64 %s, exec" % sp(S_SAVE),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          ".Ljt_cl_vt:",
+          "v_mov_b32 v%d, 0x5eed5eed" % V_T,
+          "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
+          ".Ljt_cl_end:"]
+    L += [".Ljt_wait:", "s_waitcnt lgkmcnt(0)",
+          ".Ljt_br:", "s_branch .Ljt_br",
+          ".Ljt_jl:",
+          "s_add_u32 %s, %s, 0x5eed5eed" % (s(S_JUNK), s(S_CB)),
+          "s_addc_u32 %s, %s, 0" % (s(S_JUNK + 1), s(S_CB + 1)),
+          "s_setpc_b64 %s" % sp(S_JUNK),
+          ".Ljt_jl_end:"]
+    # offsets from .Lcb, read by asm_jit.cpp (order = enum jt_index there)
+    names = [".Ljt_mov_s%d" % r for r in range(10, 16)] + [
+        ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
+        ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
+        ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", "ebpf_jit_area"]
+    L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
+    L += ["  .long %d" % JIT_AREA_BYTES]
+    return L
+
+
 def main():
     out_s, out_h = sys.argv[1], sys.argv[2]
     A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950:xnack-"', ".amdhsa_code_object_version 5", ".text"]
     A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
+    A += kernel("ebpf_jit_s64", True, True) + kernel("ebpf_jit_gen", False, True)
     A += common_group_code() + routines()
     table = []
+    meta = []
+    reads = []
+    conds = []
     hid = 0
     header = ["// generated by gen_interp.py — handler family ids for asm_runtime.cpp",
-              "#pragma once", "#define AH_NREGS %d" % NREG]
+              "#pragma once", "#include <stdint.h>", "#define AH_NREGS %d" % NREG]
     for name, arity in FAMILIES:
         header.append("#define AH_%s %d" % (name, hid))
         for d, sr in variants(arity):
             label = "h_%d" % hid
             uid = "%d" % hid
             body, own = handler_body(name, d, sr)
+            body = [ln.replace("{uid}", uid) for ln in body]
             A.append(".p2align 2")
             A.append("%s:" % label)
-            A += [ln.replace("{uid}", uid) for ln in body]
-            if not own:
-                A += dispatch(12)
+            is_cond = "@CMPEND" in body
+            if is_cond:
+                k = body.index("@CMPEND")
+                copy = body[:k]
+                A += copy + [".Lhe_%d:" % hid] + body[k + 1:]
+            else:
+                copy = body
+                A += body + [".Lhe_%d:" % hid]
+                if not own:
+                    A += dispatch(12)
+            m = entry_reads(copy)
+            if name == "LOOKUPGEN":
+                m |= 1 << 2      # the routine resumes at s12
+            reads.append(m)
+            # an LDS read whose result the interpreter's dispatch wait (lgkmcnt) covered
+            last_ds = max([i for i, ln in enumerate(copy) if ln.startswith("ds_read")] or [-1])
+            waits = [i for i, ln in enumerate(copy) if ln.startswith("s_waitcnt") and "lgkmcnt" in ln]
+            needw = last_ds >= 0 and not any(i > last_ds for i in waits)
+            conds.append((1 if is_cond else 0) | (2 if needw else 0))
             table.append(label)
+            meta.append("  .long %s-.Lcb, .Lhe_%d-%s" % (label, hid, label))
             hid += 1
     header.append("#define AH_COUNT %d" % hid)
+    header.append("// entry SGPRs (bit k = s(10+k)) each handler body reads")
+    header.append("static const uint8_t ah_reads[AH_COUNT] = {%s};" % ",".join(map(str, reads)))
+    header.append("// bit 0: conditional jump (copy the compare only); bit 1: body leaves an LDS read "
+                  "outstanding")
+    header.append("static const uint8_t ah_flags[AH_COUNT] = {%s};" % ",".join(map(str, conds)))
+    header.append("#define AH_JIT_AREA_BYTES %d" % JIT_AREA_BYTES)
     A += link_kernel()
     A += [".p2align 2", ".Lhandler_table:"]
     A += ["  .long %s-.Llink_base" % lab for lab in table]
+    # compiled-program support: handler body table, glue templates, the patch area
+    A += [".p2align 2", "ebpf_jit_meta:"] + meta
+    A += jit_templates()
+    A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
     kernarg = 104
-    A += kd("ebpf_interp_s64", 0, NVGPR, NSGPR, kernarg, 256)
-    A += kd("ebpf_interp_gen", 0, NVGPR, NSGPR, kernarg, 256)
-    A += kd("ebpf_asm_link", 0, 16, 16, 16, 64)
-    meta = metadata([("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR, 256),
-                   ("ebpf_interp_gen", kernarg, 0, NVGPR, NSGPR, 256),
-                   ("ebpf_asm_link", 16, 0, 16, 16, 64)])
+    ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR, 256),
+          ("ebpf_interp_gen", kernarg, 0, NVGPR, NSGPR, 256),
+          ("ebpf_jit_s64", kernarg, 0, NVGPR, NSGPR, 256),
+          ("ebpf_jit_gen", kernarg, 0, NVGPR, NSGPR, 256),
+          ("ebpf_asm_link", 16, 0, 16, 16, 64)]
+    for name, ka, lds, vg, sg, wg in ks:
+        A += kd(name, lds, vg, sg, ka, wg)
+    md = metadata(ks)
     with open(out_s, "w") as f:
         f.write("\n".join(("\t" + x if not (x.endswith(":") or x.startswith(".") or x.startswith(" ")) else x)
                           for x in A) + "\n")
-        f.write("\n".join(meta) + "\n")
+        f.write("\n".join(md) + "\n")
     with open(out_h, "w") as f:
         f.write("\n".join(header) + "\n")
 

@@ -1,0 +1,373 @@
+// asm_jit.cpp — copy-and-patch compilation of a translated program for gfx950.
+//
+// The interpreter (asm_runtime.cpp) pays one scalar dispatch per executed instruction: load the
+// 32-B entry, wait, jump.  Here the same lowered entries (asm_lower) become straight-line code:
+// for each entry, in depth-first order of the state tree (translate.cpp), the compiler emits
+//   s_mov_b32 s10..s15, <operand>       only the entry registers the handler body reads
+//   <handler body bytes>                copied from the assembled interpreter image
+//   s_waitcnt lgkmcnt(0)                if the body leaves an LDS read outstanding
+//   conditional tail / branch           see gen_interp.py jit_templates()
+// into the reserved area of a private copy of the code object (ebpf_jit_area), which is then
+// loaded as its own module.  Handler bodies reach the shared routines (fault, exit, udiv,
+// check, lookup, schedule) relative to .Lcb, whose offset is the same in every copy, so the
+// bytes need no relocation.  Divergence works as in the interpreter: lanes that take a branch
+// the rest of the wave does not are parked with v41 = the code offset of their block, and the
+// scheduler resumes them by jumping to .Lcb + v41 (s7 bit 1 selects that mode).
+//
+// The state graph is a tree, so every block is placed exactly once and each straight-line run
+// falls through; only taken branches (and shared fault entries) need jumps.
+#include <elf.h>
+#include <hip/hip_runtime.h>
+
+#include "asm_handlers.h"
+#include "internal.h"
+
+extern const unsigned char ebpf_asm_hsaco[];
+extern const size_t ebpf_asm_hsaco_len;
+
+int asm_lower(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+	      std::vector<dp_entry> &out, uint32_t *stack_stride, std::string *err);
+
+namespace {
+
+// Order of ebpf_jit_tmpl in gen_interp.py.
+enum jt_index {
+	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
+	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
+	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_AREA,
+	JT_AREA_BYTES,
+	JT_COUNT
+};
+
+struct jit_image {
+	bool ok = false;
+	std::string why;
+	size_t cb = 0;                          // file offset of .Lcb
+	std::vector<uint32_t> body_off, body_len; // per handler id, body offset from .Lcb, length
+	uint32_t t[JT_COUNT] = {};
+};
+
+bool
+find_symbols(const unsigned char *img, size_t len, const char *const *names, size_t nn,
+	     size_t *file_off)
+{
+	if (len < sizeof(Elf64_Ehdr))
+		return false;
+	const Elf64_Ehdr *eh = reinterpret_cast<const Elf64_Ehdr *>(img);
+	if (memcmp(eh->e_ident, ELFMAG, SELFMAG) != 0 || eh->e_ident[EI_CLASS] != ELFCLASS64 ||
+	    eh->e_shoff + (uint64_t)eh->e_shnum * sizeof(Elf64_Shdr) > len)
+		return false;
+	const Elf64_Shdr *sh = reinterpret_cast<const Elf64_Shdr *>(img + eh->e_shoff);
+	for (size_t i = 0; i < nn; i++)
+		file_off[i] = 0;
+	size_t found = 0;
+	for (int si = 0; si < eh->e_shnum; si++) {
+		if (sh[si].sh_type != SHT_SYMTAB || sh[si].sh_link >= eh->e_shnum)
+			continue;
+		const Elf64_Shdr &st = sh[si], &str = sh[st.sh_link];
+		if (st.sh_offset + st.sh_size > len || str.sh_offset + str.sh_size > len)
+			return false;
+		const Elf64_Sym *sym = reinterpret_cast<const Elf64_Sym *>(img + st.sh_offset);
+		const size_t ns = st.sh_size / sizeof(Elf64_Sym);
+		for (size_t k = 0; k < ns; k++) {
+			if (sym[k].st_name >= str.sh_size || sym[k].st_shndx == SHN_UNDEF ||
+			    sym[k].st_shndx >= eh->e_shnum)
+				continue;
+			const char *nm = reinterpret_cast<const char *>(img + str.sh_offset + sym[k].st_name);
+			for (size_t q = 0; q < nn; q++) {
+				if (file_off[q] || strcmp(nm, names[q]) != 0)
+					continue;
+				const Elf64_Shdr &sec = sh[sym[k].st_shndx];
+				file_off[q] = sec.sh_offset + (sym[k].st_value - sec.sh_addr);
+				found++;
+			}
+		}
+	}
+	return found == nn;
+}
+
+const jit_image &
+image_info()
+{
+	static jit_image info;
+	static std::once_flag once;
+	std::call_once(once, [] {
+		const char *names[] = {"ebpf_cb", "ebpf_jit_meta", "ebpf_jit_tmpl"};
+		size_t off[3];
+		if (!find_symbols(ebpf_asm_hsaco, ebpf_asm_hsaco_len, names, 3, off)) {
+			info.why = "code object lacks the compiled-program symbols";
+			return;
+		}
+		info.cb = off[0];
+		const unsigned char *meta = ebpf_asm_hsaco + off[1];
+		const unsigned char *tm = ebpf_asm_hsaco + off[2];
+		if (off[1] + 8ull * AH_COUNT > ebpf_asm_hsaco_len ||
+		    off[2] + 4ull * JT_COUNT > ebpf_asm_hsaco_len) {
+			info.why = "compiled-program tables out of range";
+			return;
+		}
+		info.body_off.resize(AH_COUNT);
+		info.body_len.resize(AH_COUNT);
+		for (int h = 0; h < AH_COUNT; h++) {
+			memcpy(&info.body_off[h], meta + 8 * h, 4);
+			memcpy(&info.body_len[h], meta + 8 * h + 4, 4);
+			if (info.cb + info.body_off[h] + info.body_len[h] > ebpf_asm_hsaco_len) {
+				info.why = "handler body out of range";
+				return;
+			}
+		}
+		memcpy(info.t, tm, sizeof(info.t));
+		if (info.t[JT_AREA_BYTES] != AH_JIT_AREA_BYTES ||
+		    info.cb + info.t[JT_AREA] + info.t[JT_AREA_BYTES] > ebpf_asm_hsaco_len) {
+			info.why = "compiled-program area out of range";
+			return;
+		}
+		info.ok = true;
+	});
+	return info;
+}
+
+inline bool
+is_terminal(uint32_t h)
+{
+	return h == (uint32_t)AH_EXIT || h == (uint32_t)AH_FAULT;
+}
+
+inline bool
+fits_simm16(int64_t bytes)
+{
+	const int64_t w = bytes / 4;
+	return (bytes % 4) == 0 && w >= -32768 && w <= 32767;
+}
+
+} // namespace
+
+// Compile the program for `mode` into a patched copy of the code object (*img) and return the
+// emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
+int
+asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
+	     uint32_t *stack_stride, std::string *err)
+{
+	const jit_image &I = image_info();
+	if (!I.ok) {
+		*err = I.why;
+		return ENOSYS;
+	}
+	std::vector<dp_entry> low;
+	int lerr = asm_lower(xl, mode, table, low, stack_stride, err);
+	if (lerr)
+		return lerr;
+	const size_t n = low.size();
+	const uint32_t *T = I.t;
+	auto tsize = [&](int a, int b) { return T[b] - T[a]; };
+	const uint32_t cs_len = tsize(JT_CS, JT_CS_END), cl_len = tsize(JT_CL, JT_CL_END);
+	const uint32_t jl_len = tsize(JT_JL, JT_JL_END);
+
+	// layout order: depth-first, not-taken successor falls through
+	std::vector<uint32_t> order;
+	order.reserve(n);
+	std::vector<char> placed(n, 0);
+	std::vector<uint32_t> stack{xl.start};
+	while (!stack.empty()) {
+		uint32_t cur = stack.back();
+		stack.pop_back();
+		while (cur < n && !placed[cur]) {
+			placed[cur] = 1;
+			order.push_back(cur);
+			const uint32_t h = (uint32_t)low[cur].handler;
+			if (is_terminal(h))
+				break;
+			if (ah_flags[h] & 1) {
+				const uint32_t tk = xl.entries[cur].target;
+				if (tk < n && !placed[tk])
+					stack.push_back(tk);
+			}
+			cur = xl.entries[cur].next;
+		}
+	}
+	// successor that must follow each block (UINT32_MAX: none)
+	auto succ = [&](uint32_t e) -> uint32_t {
+		const uint32_t h = (uint32_t)low[e].handler;
+		return is_terminal(h) ? UINT32_MAX : xl.entries[e].next;
+	};
+	std::vector<uint32_t> pos(n, 0), idx(n, UINT32_MAX);
+	for (size_t k = 0; k < order.size(); k++)
+		idx[order[k]] = (uint32_t)k;
+	std::vector<char> long_cond(n, 0), long_br(n, 0);
+	auto needs_branch = [&](uint32_t e) {
+		const uint32_t sx = succ(e);
+		if (sx == UINT32_MAX)
+			return false;
+		const uint32_t k = idx[e];
+		return !(k + 1 < order.size() && order[k + 1] == sx);
+	};
+	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
+		const uint32_t h = (uint32_t)low[e].handler;
+		uint32_t sz = 8u * (uint32_t)__builtin_popcount(ah_reads[h]);
+		*pre = sz;
+		sz += I.body_len[h];
+		if (ah_flags[h] & 2)
+			sz += 4;
+		*body_end = sz;
+		if (ah_flags[h] & 1)
+			sz += long_cond[e] ? cl_len : cs_len;
+		if (needs_branch(e))
+			sz += long_br[e] ? jl_len : 4;
+		return sz;
+	};
+	uint32_t total = 0;
+	for (int iter = 0; iter < 8; iter++) {
+		total = 0;
+		for (uint32_t e : order) {
+			uint32_t pre, be;
+			pos[e] = total;
+			total += block_size(e, &pre, &be);
+		}
+		bool changed = false;
+		for (uint32_t e : order) {
+			uint32_t pre, be;
+			block_size(e, &pre, &be);
+			const uint32_t h = (uint32_t)low[e].handler;
+			if ((ah_flags[h] & 1) && !long_cond[e]) {
+				const uint32_t br_at = pos[e] + be + (T[JT_CS_BR] - T[JT_CS]);
+				const uint32_t tk = xl.entries[e].target;
+				if (!fits_simm16((int64_t)pos[tk] - (int64_t)(br_at + 4))) {
+					long_cond[e] = 1;
+					changed = true;
+				}
+			}
+			if (needs_branch(e) && !long_br[e]) {
+				const uint32_t br_at = pos[e] + block_size(e, &pre, &be) - 4;
+				if (!fits_simm16((int64_t)pos[succ(e)] - (int64_t)(br_at + 4))) {
+					long_br[e] = 1;
+					changed = true;
+				}
+			}
+		}
+		if (!changed)
+			break;
+	}
+	if (total > (uint32_t)AH_JIT_AREA_BYTES) {
+		*err = "compiled program exceeds the code area";
+		return E2BIG;
+	}
+	for (uint32_t e = 0; e < n; e++)
+		if (!placed[e] && e == xl.start) {
+			*err = "internal error: start entry not placed";
+			return EINVAL;
+		}
+
+	// emit
+	std::vector<unsigned char> &img = *img_out;
+	img.assign(ebpf_asm_hsaco, ebpf_asm_hsaco + ebpf_asm_hsaco_len);
+	const size_t area = I.cb + T[JT_AREA];
+	const unsigned char *src = ebpf_asm_hsaco + I.cb;
+	auto code_off = [&](uint32_t e) { return T[JT_AREA] + pos[e]; }; // from .Lcb
+	auto put32 = [&](size_t at, uint32_t v) { memcpy(&img[area + at], &v, 4); };
+	auto copy_t = [&](size_t at, int a, uint32_t len) {
+		memcpy(&img[area + at], src + T[a], len);
+	};
+	auto patch_simm16 = [&](size_t at, uint32_t target) {
+		uint32_t w;
+		memcpy(&w, &img[area + at], 4);
+		const int32_t d = ((int32_t)target - (int32_t)(at + 4)) / 4;
+		w = (w & 0xffff0000u) | ((uint32_t)d & 0xffffu);
+		memcpy(&img[area + at], &w, 4);
+	};
+	for (uint32_t e : order) {
+		const dp_entry &o = low[e];
+		const uint32_t h = (uint32_t)o.handler;
+		uint32_t dw[8];
+		memcpy(dw, &o, 32);
+		size_t at = pos[e];
+		for (int r = 0; r < 6; r++) {
+			if (!(ah_reads[h] & (1u << r)))
+				continue;
+			uint32_t v = dw[2 + r];
+			if (r == 2) { // s12: code offset of the next block (LOOKUPGEN resumes there)
+				const uint32_t nx = xl.entries[e].next;
+				v = nx < n && placed[nx] ? code_off(nx) : 0;
+			}
+			copy_t(at, JT_MOV_S10 + r, 8);
+			put32(at + 4, v);
+			at += 8;
+		}
+		memcpy(&img[area + at], src + I.body_off[h], I.body_len[h]);
+		at += I.body_len[h];
+		if (ah_flags[h] & 2) {
+			copy_t(at, JT_WAIT, 4);
+			at += 4;
+		}
+		if (ah_flags[h] & 1) {
+			const uint32_t tk = xl.entries[e].target;
+			if (!long_cond[e]) {
+				copy_t(at, JT_CS, cs_len);
+				patch_simm16(at + (T[JT_CS_BR] - T[JT_CS]), pos[tk]);
+				put32(at + (T[JT_CS_VT] - T[JT_CS]) + 4, code_off(tk));
+				at += cs_len;
+			} else {
+				copy_t(at, JT_CL, cl_len);
+				put32(at + (T[JT_CL_LIT] - T[JT_CL]) + 4, code_off(tk));
+				put32(at + (T[JT_CL_VT] - T[JT_CL]) + 4, code_off(tk));
+				at += cl_len;
+			}
+		}
+		if (needs_branch(e)) {
+			const uint32_t sx = succ(e);
+			if (!long_br[e]) {
+				copy_t(at, JT_BR, 4);
+				patch_simm16(at, pos[sx]);
+				at += 4;
+			} else {
+				copy_t(at, JT_JL, jl_len);
+				put32(at + 4, code_off(sx));
+				at += jl_len;
+			}
+		}
+		uint32_t pre, be;
+		if (at != pos[e] + block_size(e, &pre, &be)) {
+			*err = "internal error: compiled block size mismatch";
+			return EINVAL;
+		}
+	}
+	if (code)
+		code->assign(img.begin() + area, img.begin() + area + total);
+	return 0;
+}
+
+// Build and load the compiled program for `mode`; on success *mod_out / *fn_out hold the
+// module and its kernel.
+int
+asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err)
+{
+	std::vector<unsigned char> img;
+	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err);
+	if (e)
+		return e;
+	if (hipSetDevice(device) != hipSuccess)
+		return EIO;
+	hipModule_t mod = nullptr;
+	if (hipModuleLoadData(&mod, img.data()) != hipSuccess) {
+		*err = "loading the compiled program failed";
+		return EIO;
+	}
+	hipFunction_t fn = nullptr;
+	if (hipModuleGetFunction(&fn, mod, mode == 1 ? "ebpf_jit_s64" : "ebpf_jit_gen") != hipSuccess) {
+		hipModuleUnload(mod);
+		*err = "compiled program kernel missing";
+		return EIO;
+	}
+	*mod_out = mod;
+	*fn_out = fn;
+	return 0;
+}
+
+void
+asm_jit_release(void *mod)
+{
+	if (mod)
+		hipModuleUnload(static_cast<hipModule_t>(mod));
+}

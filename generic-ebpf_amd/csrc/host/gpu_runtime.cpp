@@ -16,14 +16,34 @@
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
-			     uint32_t map_lds_bytes);
+			     uint32_t map_lds_bytes, void *fn);
 int asm_available(int device);
 bool asm_program_needs_general(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
+// asm_jit.cpp
+int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err);
+void asm_jit_release(void *mod);
+int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
+		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
+		 uint32_t *stack_stride, std::string *err);
 
 
 namespace {
+
+// Small array maps are copied into LDS by the assembly kernels at kernel start (value loads
+// through a lookup result then read LDS).  Budget: kMapLdsBudget bytes per program.
+uint32_t
+plan_map_lds(const struct ebpf_map *em, uint32_t *used)
+{
+	const uint64_t bytes = (uint64_t)em->value_size * em->max_entries;
+	if (bytes == 0 || bytes % 4 != 0 || *used + bytes > kMapLdsBudget)
+		return ~0u;
+	const uint32_t off = kMapLdsBase + *used;
+	*used += (uint32_t)((bytes + 15) & ~15ull);
+	return off;
+}
 
 thread_local std::string t_err;
 thread_local int t_dev = 0;
@@ -153,15 +173,8 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		m.dev_base = (uint64_t)(uintptr_t)mdev;
 		m.value_size = em->value_size;
 		m.max_entries = em->max_entries;
-		// Small array maps are copied into LDS by the assembly interpreter at kernel start
-		// (value loads through a lookup result then read LDS).  Budget: kMapLdsBudget bytes.
-		const uint64_t bytes = (uint64_t)em->value_size * em->max_entries;
-		m.lds_off = ~0u;
+		m.lds_off = plan_map_lds(em, &nd->map_lds_bytes);
 		m.pad = 0;
-		if (bytes > 0 && bytes % 4 == 0 && nd->map_lds_bytes + bytes <= kMapLdsBudget) {
-			m.lds_off = kMapLdsBase + nd->map_lds_bytes;
-			nd->map_lds_bytes += (uint32_t)((bytes + 15) & ~15ull);
-		}
 		nd->table.push_back(m);
 	}
 	if (!nd->table.empty()) {
@@ -176,6 +189,26 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 	nd->nmaps = (uint32_t)nd->table.size();
 	dp = std::move(nd);
 	*out = dp.get();
+	return 0;
+}
+
+// Compiled program for `mode`, built on first use.  Returns 0 with dp->jit_fn[mode] set, or
+// the build error (E2BIG: too large for the code area — the caller runs the interpreter).
+int
+jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
+{
+	std::lock_guard<std::mutex> g(ep->dlock);
+	if (dp->jit_fn[mode])
+		return 0;
+	if (dp->jit_err[mode])
+		return dp->jit_err[mode];
+	std::string msg;
+	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
+				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg);
+	if (err) {
+		dp->jit_err[mode] = err;
+		return fail(err, msg);
+	}
 	return 0;
 }
 
@@ -210,14 +243,26 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	if (err)
 		return err;
 	hipError_t e;
-	if (effective_variant(dp->device) == 0) {
+	const int variant = effective_variant(dp->device);
+	if (variant == 0 || variant == 2) {
 		const int mode =
 		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
-		if ((err = asm_entries(ep, dp, mode)))
-			return err;
-		L.prog = dp->d_asm[mode];
-		L.stack_stride = dp->asm_stride[mode];
-		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes);
+		// variant 0: the compiled program; a program too large for the code area runs on the
+		// assembly interpreter instead (still the device path)
+		if (variant == 0 && (err = jit_entries(ep, dp, mode)) == 0) {
+			L.prog = nullptr;
+			L.stack_stride = dp->jit_stride[mode];
+			e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes,
+					      dp->jit_fn[mode]);
+		} else {
+			if (variant == 0 && err != E2BIG)
+				return err;
+			if ((err = asm_entries(ep, dp, mode)))
+				return err;
+			L.prog = dp->d_asm[mode];
+			L.stack_stride = dp->asm_stride[mode];
+			e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, nullptr);
+		}
 	} else {
 		L.prog = dp->d_entries;
 		e = launch_interp_v0(L, stream);
@@ -291,6 +336,8 @@ prog_release_device_state(struct ebpf_prog *ep)
 			for (auto *a : dp->d_asm)
 				if (a)
 					hipFree(a);
+			for (auto *m : dp->jit_mod)
+				asm_jit_release(m);
 		}
 	}
 	ep->dev.clear();
@@ -323,8 +370,8 @@ ebpf_gpu_set_device(int device)
 EBPF_EXPORT int
 ebpf_gpu_set_variant(int variant)
 {
-	if (variant < 0 || variant > 1)
-		return fail(EINVAL, "variant must be 0 (default) or 1 (portable HIP)");
+	if (variant < 0 || variant > 2)
+		return fail(EINVAL, "variant must be 0 (compiled), 1 (portable HIP) or 2 (interpreter)");
 	g_variant.store(variant);
 	return 0;
 }
@@ -357,6 +404,42 @@ ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info)
 	info->nentries = (uint32_t)ep->xlated->entries.size();
 	info->nmaps = (uint32_t)ep->xlated->maps.size();
 	info->max_stack = ep->xlated->max_stack;
+	return 0;
+}
+
+EBPF_EXPORT int
+ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
+{
+	if (ep == nullptr || len == nullptr || (layout != 0 && layout != 1))
+		return fail(EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(ep->dlock);
+	int err = ensure_translated(ep);
+	if (err)
+		return err;
+	// host-side map table: device bases are unknown without a device (0 here; the real table
+	// differs only in those immediates)
+	std::vector<dp_map> table;
+	uint32_t used = 0;
+	for (struct ebpf_map *em : ep->xlated->maps) {
+		dp_map m;
+		memset(&m, 0, sizeof(m));
+		m.handle = (uint64_t)(uintptr_t)em;
+		m.value_size = em->value_size;
+		m.max_entries = em->max_entries;
+		m.lds_off = plan_map_lds(em, &used);
+		table.push_back(m);
+	}
+	std::vector<unsigned char> img, code;
+	uint32_t stride = 0;
+	std::string msg;
+	err = asm_jit_emit(*ep->xlated, layout, table, &img, &code, &stride, &msg);
+	if (err)
+		return fail(err, msg);
+	const size_t cap = *len;
+	*len = code.size();
+	if (buf == nullptr || cap < code.size())
+		return buf == nullptr ? 0 : fail(ENOSPC, "buffer too small");
+	memcpy(buf, code.data(), code.size());
 	return 0;
 }
 

@@ -85,6 +85,10 @@ struct dprog_device {
 	dp_entry *d_asm[2] = {nullptr, nullptr}; // variant 0: lowered + linked, per mode
 	uint32_t asm_stride[2] = {0, 0};         // LDS stack bytes per lane, per mode
 	int asm_err[2] = {0, 0};
+	void *jit_mod[2] = {nullptr, nullptr};   // variant 0: compiled program module, per mode
+	void *jit_fn[2] = {nullptr, nullptr};    // its kernel
+	uint32_t jit_stride[2] = {0, 0};
+	int jit_err[2] = {0, 0};                 // E2BIG etc.: run the interpreter instead
 };
 
 // Abstract value of a register (pointer provenance), computed by translate.cpp's dataflow pass

@@ -94,6 +94,7 @@ FUNCS = {
     "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_device_info": (_I, [_VP, _VP]),
+    "ebpf_prog_device_code": (_I, [_VP, _I, _VP, ctypes.POINTER(ctypes.c_size_t)]),
 }
 DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_hashtable",
                 "eht_map_lookup_elem", "eht_map_update_elem", "eht_map_delete_elem"]
@@ -246,6 +247,16 @@ class Prog:
                                          None if faults is None else faults.ctypes.data,
                                          ctypes.byref(st)), "ebpf_prog_run_batch")
         return ret, faults, st
+
+    def device_code(self, layout=1):
+        """The program compiled for variant 0 (raw gfx950 code bytes); works without a GPU."""
+        n = ctypes.c_size_t(0)
+        _check(lib().ebpf_prog_device_code(self.ptr, layout, None, ctypes.byref(n)),
+               "ebpf_prog_device_code")
+        buf = (ctypes.c_uint8 * max(1, n.value))()
+        _check(lib().ebpf_prog_device_code(self.ptr, layout, buf, ctypes.byref(n)),
+               "ebpf_prog_device_code")
+        return bytes(buf)[: n.value]
 
     def run_batch_dev(self, device, data_ptr, count, stride, ret_ptr, offsets_ptr=None,
                       faults_ptr=None, hist_ptr=None, stream=None):

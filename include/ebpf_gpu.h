@@ -96,9 +96,12 @@ int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_
 /* Select the device used by ebpf_prog_run_batch for the calling thread. */
 int ebpf_gpu_set_device(int device);
 
-/* Interpreter variant used by subsequent launches: 0 = the hand-written gfx950 assembly
- * interpreter (default; launches fail with ENOSYS if it cannot be loaded), 1 = the portable
- * HIP interpreter (correctness baseline). */
+/* Device path used by subsequent launches (all bit-identical):
+ *   0 = default: the program compiled to gfx950 code (copy-and-patch of the assembly
+ *       interpreter's handlers); a program too large for the code area runs on the assembly
+ *       interpreter.  Launches fail with ENOSYS if the code object cannot be loaded.
+ *   1 = the portable HIP interpreter (correctness baseline).
+ *   2 = the hand-written gfx950 assembly interpreter. */
 int ebpf_gpu_set_variant(int variant);
 
 /* Information about the translated device program. */
@@ -109,6 +112,12 @@ struct ebpf_dprog_info {
 	uint32_t max_stack;    /* deepest statically known stack access (bytes below r10) */
 };
 int ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info);
+
+/* Diagnostics: the program as compiled for variant 0, raw gfx950 instruction bytes, for packet
+ * `layout` 1 (fixed 64-B packets) or 0 (any stride / offsets).  Host only (no GPU needed; map
+ * base addresses are then 0).  *len: in = size of buf, out = bytes of code.  buf == NULL just
+ * sizes.  Returns 0, ENOSPC (buf too small), E2BIG (program too large to compile). */
+int ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len);
 
 /* Human-readable description of the last error on this thread ("" if none). */
 const char *ebpf_gpu_last_error(void);

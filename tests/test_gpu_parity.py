@@ -11,7 +11,7 @@ from helpers import device_run, make_maps, oracle_run
 pytestmark = pytest.mark.gpu
 
 CASES = [c for f in goldens.all_golden_files() for c in goldens.load(f)]
-VARIANTS = [0, 1]  # 0 = default (fastest available), 1 = portable HIP baseline
+VARIANTS = [0, 1, 2]  # 0 = compiled (default), 1 = portable HIP baseline, 2 = asm interpreter
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -98,9 +98,10 @@ def _tiled_case(name, base, tiles):
                         base.stride, None)
 
 
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("cfg,distinct,tiles", [("c2", 1 << 20, 1), ("c3", 1 << 20, 16),
                                                  ("c4", 1 << 20, 64)])
-def test_full_size_workloads(gpu, env, cfg, distinct, tiles):
+def test_full_size_workloads(gpu, env, cfg, distinct, tiles, variant):
     """BASELINE.json sizes (C2 1M, C3 16M, C4 64M packets): the device result for packet i must
     equal the oracle's for the distinct packet it tiles (size-independent property)."""
     from generic_ebpf_amd import workloads
@@ -114,19 +115,20 @@ def test_full_size_workloads(gpu, env, cfg, distinct, tiles):
     want, wf, _, _ = oracle_run(base, nthreads=8)
     assert not wf.any()
     full = _tiled_case(cfg, base, tiles)
-    got, gf, _ = device_run(gpu, env, full, 0)
+    got, gf, _ = device_run(gpu, env, full, variant)
     assert not gf.any()
     np.testing.assert_array_equal(got.reshape(tiles, distinct), np.broadcast_to(want, (tiles, distinct)))
 
 
-def test_c5_imix_vs_oracle(gpu, env):
+@pytest.mark.parametrize("variant", [0, 2])
+def test_c5_imix_vs_oracle(gpu, env, variant):
     from generic_ebpf_amd import workloads
     lay = workloads.prog_c5()
     n = 1 << 18
     data, offs, _ = workloads.packets_imix(n)
     c = goldens.Case("c5", lay.code, [], [], data, n, 0, offs)
     want, wf, _, _ = oracle_run(c, nthreads=8)
-    got, gf, _ = device_run(gpu, env, c, 0)
+    got, gf, _ = device_run(gpu, env, c, variant)
     np.testing.assert_array_equal(wf, gf)
     np.testing.assert_array_equal(want, got)
 

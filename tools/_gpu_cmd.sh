@@ -1,10 +1,14 @@
 set -o pipefail
-T=r1l
+T=r1n
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
 python3 -c "import __graft_entry__ as g; g.build()" > gpurun_out/$T/build.log 2>&1 || { tail -20 gpurun_out/$T/build.log; exit 1; }
-timeout -k 10 600 python3 tools/e2e.py > gpurun_out/$T/e2e.json 2> gpurun_out/$T/e2e.err || { tail -5 gpurun_out/$T/e2e.err; exit 1; }
-cat gpurun_out/$T/e2e.json
-timeout -k 10 600 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || { tail -5 gpurun_out/$T/bench.err; exit 1; }
-cat gpurun_out/$T/bench.json
-lscpu > gpurun_out/$T/lscpu.txt; nproc >> gpurun_out/$T/lscpu.txt
+VARIANTS=0 timeout -k 10 120 python3 tools/asm_smoke.py kat > gpurun_out/$T/smoke_kat.log 2>&1; rc=$?; tail -16 gpurun_out/$T/smoke_kat.log; [ $rc -eq 0 ] || exit $rc
+grep -q "^ok   kat_stdw_ldxb" gpurun_out/$T/smoke_kat.log || exit 3
+timeout -k 10 900 python3 -m pytest tests -x -q -m gpu > gpurun_out/$T/pytest_gpu.log 2>&1; rc=$?; tail -15 gpurun_out/$T/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+for v in 0 2; do
+for cfg in c0 c3 c4 c2 c5; do
+  timeout -k 10 300 python3 bench.py --config $cfg --variant $v --no-cpu-baseline > gpurun_out/$T/bench_${cfg}_$v.json 2> gpurun_out/$T/bench_$cfg.err || { tail -5 gpurun_out/$T/bench_$cfg.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" gpurun_out/$T/bench_${cfg}_$v.json "v$v $cfg"
+done
+done

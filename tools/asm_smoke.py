@@ -20,7 +20,7 @@ env = native.Env()
 names = sys.argv[1:] or ["kat", "workloads", "rand"]
 for g in names:
     for c in goldens.load(os.path.join(goldens.GOLDEN_DIR, g + ".npz")):
-        for variant in (0,):
+        for variant in [int(x) for x in os.environ.get("VARIANTS", "0").split(",")]:
             try:
                 ret, faults, after = device_run(native, env, c, variant)
             except Exception as e:  # noqa: BLE001
