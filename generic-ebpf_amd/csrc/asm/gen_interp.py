@@ -23,7 +23,7 @@ import sys
 NREG = 11
 # cache policy of the streaming accesses (experiments: EBPF_ASM_NT bit 0 = ret stores nt,
 # bit 1 = packet DMA loads nt)
-_NT = int(os.environ.get("EBPF_ASM_NT", "0"))
+_NT = int(os.environ.get("EBPF_ASM_NT", "1"))
 ST_POLICY = " nt" if _NT & 1 else ""
 LD_POLICY = " nt" if _NT & 2 else ""
 # ---------------------------------------------------------------- register plan
@@ -32,9 +32,9 @@ V_PKT = 38           # v[38:39] packet base address
 V_LEN = 40           # packet length (bytes)
 V_T = 41             # parked entry byte offset
 V_STK = 42           # lane stack bottom (LDS byte address)
-V_GID = 43           # packet index within the launch
-V_L16 = 44           # lane * 16 (LDS-DMA staging offset)
-V_ONE = 45           # constant 1
+V_L16 = 43           # lane * 16 (LDS-DMA staging offset)
+V_RET = 44           # v[44:45] r0 of the lanes that retired in the current group (stored at the
+                     # start of the next group: one full 512-B store per group)
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
 R = list(range(52, 63))              # routine temporaries
 V_SEL = 63                           # v_perm selector 0x00010203 (byte swap)
@@ -59,8 +59,9 @@ S_SHARED = 58        # s[58:59] src_shared_base
 S_JUNK = 60          # s[60:61] scratch sdst
 S_OK = 62            # s[62:63] check: accumulated ok lanes
 S_REC = 64           # s[64:71] map record {handle, dev_base, value_size, max_entries, lds_off, pad}
+S_PREVG = 72         # group whose results are still in V_RET (-1: none)
 S_WAVE = 3
-NSGPR = 72           # + VCC, XNACK, FLAT_SCRATCH = 78 <= 80 SGPRs: 8 waves per SIMD
+NSGPR = 73           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per SIMD
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -580,15 +581,16 @@ def routines():
           "s_mov_b64 exec, %s" % sp(S_MASK),
           "v_mov_b32 v%d, s13" % V_T,
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK))] + dispatch(12)
-    # EXIT: value r0.  Stores are not waited for (the next group's vmcnt wait or the end of
-    # the program retires them).
+    # EXIT: value r0 into V_RET (the group's results are stored together, see group code).
     L += [".Lr_exit:",
-          "v_lshlrev_b32 %s, 3, v%d" % (v(R[10]), V_GID),
-          "global_store_dwordx2 %s, v[0:1], %s%s" % (v(R[10]), sp(S_RET), ST_POLICY),
+          "v_mov_b32 v%d, v0" % V_RET,
+          "v_mov_b32 v%d, v1" % (V_RET + 1),
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lex_nofault",
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
           "v_mov_b32 %s, 0" % v(R[8]),
-          "global_store_byte v%d, %s, %s" % (V_GID, v(R[8]), sp(S_FAULTS)),
+          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
           ".Lex_nofault:",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lex_nohist",
@@ -613,21 +615,22 @@ def routines():
           "s_branch .Lex_nohist",
           ".Lex_lanes:",
           "v_lshlrev_b32 %s, 2, %s" % (v(R[8]), v(R[8])),
-          "ds_add_u32 %s, v%d" % (v(R[8]), V_ONE),
+          "v_mov_b32 %s, 1" % v(R[9]),
+          "ds_add_u32 %s, %s" % (v(R[8]), v(R[9])),
           ".Lex_nohist:",
           "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE))] + goto(".Lr_schedule")
     # FAULT: lanes s[mask], code s[S_CODE]; returns via s[link] unless no lane remains
     L += [".Lr_fault:",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
           "s_mov_b64 exec, %s" % sp(S_MASK),
-          "v_lshlrev_b32 %s, 3, v%d" % (v(R[10]), V_GID),
-          "v_mov_b32 %s, 0" % v(R[8]),
-          "v_mov_b32 %s, 0" % v(R[9]),
-          "global_store_dwordx2 %s, %s, %s" % (v(R[10]), vp(R[8]), sp(S_RET)),
+          "v_mov_b32 v%d, 0" % V_RET,
+          "v_mov_b32 v%d, 0" % (V_RET + 1),
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lfl_nofault",
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
-          "global_store_byte v%d, %s, %s" % (V_GID, v(R[8]), sp(S_FAULTS)),
+          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
           ".Lfl_nofault:",
           # bin 256 (faulted) goes straight to the global histogram: faults are rare, and the
           # LDS histogram then holds exactly 256 bins (1 KB)
@@ -819,7 +822,8 @@ def routines():
               "s_max_i32 s68, s68, 0",
               "s_min_u32 s68, s68, 16",
               "s_lshl_b32 s68, s68, 6",
-              "v_cmp_gt_u32_e64 exec, s68, v%d" % V_L16,
+              "v_cmp_gt_u32_e64 vcc, s68, v%d" % V_L16,
+              "s_mov_b64 exec, vcc",   # (a VALU write of EXEC would need 5 wait states here)
               "s_mov_b32 m0, s67",
               "s_nop 0",
               "global_load_lds_dwordx4 v%d, s[64:65]%s" % (V_L16, LD_POLICY)]
@@ -851,11 +855,27 @@ def kernel(name, staged, jit=False):
           "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[0]),
           "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[0]), v(H[0])),
           "v_lshlrev_b32 v%d, 4, %s" % (V_L16, v(H[0])),
-          "v_mov_b32 v%d, 1" % V_ONE,
+          "s_mov_b32 %s, -1" % s(S_PREVG),
           "s_waitcnt lgkmcnt(0)",
           "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0)),
           "s_branch .Lprologue"]
     return L
+
+
+def store_prev_results(tag):
+    """Store V_RET (r0 of every packet of group S_PREVG) as one 512-B write; clobbers exec."""
+    if os.environ.get("EBPF_ASM_NOSTORE"):   # experiment only: measures the read-side ceiling
+        return []
+    return ["s_cmp_eq_u32 %s, -1" % s(S_PREVG),
+            "s_cbranch_scc1 .Lsp_none_%s" % tag,
+            "v_lshrrev_b32 %s, 4, v%d" % (v(R[0]), V_L16),
+            "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[0]), s(S_PREVG), v(R[0])),
+            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_COUNT), v(R[0])),
+            "s_mov_b64 exec, vcc",
+            "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(R[0])),
+            "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RET, V_RET + 1, sp(S_RET),
+                                                       ST_POLICY),
+            ".Lsp_none_%s:" % tag]
 
 
 def common_group_code():
@@ -890,7 +910,8 @@ def common_group_code():
           "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_T1)),
           "s_cbranch_scc1 .Lmc_loop",
           "v_add_u32 %s, %s, %s" % (v(H[5]), s(S_T0), v(H[4])),
-          "v_cmp_gt_u32_e64 exec, %s, %s" % (s(S_T1), v(H[5])),
+          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T1), v(H[5])),
+          "s_mov_b64 exec, vcc",
           "global_load_dword %s, %s, s[66:67]" % (v(H[3]), v(H[5])),
           "s_waitcnt vmcnt(0)",
           "v_add_u32 %s, s70, %s" % (v(H[5]), v(H[5])),
@@ -920,8 +941,8 @@ def common_group_code():
           "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
           "s_cbranch_scc0 .Lfinish",
           "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
-          "v_lshl_add_u32 v%d, %s, 6, %s" % (V_GID, s(S_GROUP), v(H[0])),
-          "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), V_GID),
+          "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
+          "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
           "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgs_general",
           # staged: this group's packets are (or are being) DMA'd into the packet buffer
@@ -935,7 +956,7 @@ def common_group_code():
           "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_GSTRIDE))] + call(".Lr_prefetch") + [
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
           "v_mov_b32 %s, 64" % v(H[1]),
-          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
+          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
                                                        v(H[1]), sp(S_DATA)),
           "v_mov_b32 v%d, 64" % V_LEN,
           "s_branch .Lgs_init",
@@ -945,22 +966,24 @@ def common_group_code():
           "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
           "s_cbranch_scc0 .Lgs_offsets",
           "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
-          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), V_GID,
+          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
                                                        v(H[1]), sp(S_DATA)),
           "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
           "s_branch .Lgs_init",
           ".Lgs_offsets:",
           "v_mov_b32 %s, 8" % v(H[1]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[2]), sp(S_JUNK), V_GID, v(H[1]), sp(S_OFFS)),
-          "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[2])),
-          "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[2])),
+          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[4]), sp(S_JUNK), H[3], v(H[1]), sp(S_OFFS)),
+          "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[4])),
+          "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[4])),
           "s_waitcnt vmcnt(0)",
           "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
           "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
           "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
           "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
-          ".Lgs_init:"]
+          ".Lgs_init:"] + store_prev_results("g") + [
+          "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
+          "s_mov_b64 exec, %s" % sp(S_ALIVE)]
     for r in range(22):
         L.append("v_mov_b32 v%d, 0" % r)
     L += ["v_mov_b32 v2, v%d" % V_PKT, "v_mov_b32 v3, v%d" % (V_PKT + 1),
@@ -971,7 +994,7 @@ def common_group_code():
           "s_cselect_b32 %s, ebpf_jit_area-.Lcb, %s" % (s(S_T0), s(S_T0)),
           "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
     # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
-    L += [".Lfinish:",
+    L += [".Lfinish:"] + store_prev_results("f") + [
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_barrier",

@@ -203,9 +203,52 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		const uint32_t k = idx[e];
 		return !(k + 1 < order.size() && order[k + 1] == sx);
 	};
+	// Operand registers s10..s15 a block must set: the ones its body reads, minus those that
+	// provably already hold the value.  Values carry along a fall-through chain; a block that
+	// can be entered any other way (taken target, branch target, scheduler resume point after
+	// a lookup, the start) assumes nothing.
+	std::vector<uint8_t> pre_mask(n, 0);
+	{
+		std::vector<char> entry_point(n, 0);
+		entry_point[xl.start] = 1;
+		for (uint32_t e : order) {
+			const uint32_t h = (uint32_t)low[e].handler;
+			if (ah_flags[h] & 1)
+				entry_point[xl.entries[e].target] = 1;
+			if (h == (uint32_t)AH_LOOKUPGEN && xl.entries[e].next < n)
+				entry_point[xl.entries[e].next] = 1;
+			if (needs_branch(e))
+				entry_point[succ(e)] = 1;
+		}
+		bool known[6] = {};
+		uint32_t val[6] = {};
+		for (size_t k = 0; k < order.size(); k++) {
+			const uint32_t e = order[k];
+			const bool fall = k > 0 && succ(order[k - 1]) == e && !needs_branch(order[k - 1]);
+			if (!fall || entry_point[e])
+				for (bool &x : known)
+					x = false;
+			const uint32_t h = (uint32_t)low[e].handler;
+			uint32_t dw[8];
+			memcpy(dw, &low[e], 32);
+			uint8_t m = 0;
+			for (int r = 0; r < 6; r++) {
+				if (!(ah_reads[h] & (1u << r)))
+					continue;
+				if (r == 2 || !known[r] || val[r] != dw[2 + r]) {
+					m |= (uint8_t)(1u << r);
+					if (r != 2) {
+						known[r] = true;
+						val[r] = dw[2 + r];
+					}
+				}
+			}
+			pre_mask[e] = m;
+		}
+	}
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = 8u * (uint32_t)__builtin_popcount(ah_reads[h]);
+		uint32_t sz = 8u * (uint32_t)__builtin_popcount(pre_mask[e]);
 		*pre = sz;
 		sz += I.body_len[h];
 		if (ah_flags[h] & 2)
@@ -283,7 +326,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		memcpy(dw, &o, 32);
 		size_t at = pos[e];
 		for (int r = 0; r < 6; r++) {
-			if (!(ah_reads[h] & (1u << r)))
+			if (!(pre_mask[e] & (1u << r)))
 				continue;
 			uint32_t v = dw[2 + r];
 			if (r == 2) { // s12: code offset of the next block (LOOKUPGEN resumes there)
