@@ -33,12 +33,17 @@ V_LEN = 40           # packet length (bytes)
 V_T = 41             # parked entry byte offset
 V_STK = 42           # lane stack bottom (LDS byte address)
 V_L16 = 43           # lane * 16 (LDS-DMA staging offset)
-V_RET = 44           # v[44:45] r0 of the lanes that retired in the current group (stored at the
-                     # start of the next group: one full 512-B store per group)
+# v[44:45] (RETK == 1) or v[64:64+2*RETK]: r0 of the lanes that retired, per group of the
+# current superblock (stored together at the start of the next superblock)
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
 R = list(range(52, 63))              # routine temporaries
 V_SEL = 63                           # v_perm selector 0x00010203 (byte swap)
-NVGPR = 64
+# Results of RETK consecutive groups are kept in VGPRs and written as one RETK x 512-B burst
+# (RETK > 1 adds 2*RETK VGPRs at v64).  Each wave walks superblocks of RETK consecutive groups.
+RETK = int(os.environ.get("EBPF_ASM_RETK", "1"))
+assert RETK in (1, 2, 4, 8)
+V_RB = 44 if RETK == 1 else 64
+NVGPR = 64 if RETK == 1 else 64 + 2 * RETK
 
 # SGPRs (next_free_sgpr 80 -> 8 waves per SIMD)
 S_CB = 4             # s[4:5] code base (.Lcb): routines are reached at S_CB + (label - .Lcb)
@@ -582,9 +587,7 @@ def routines():
           "v_mov_b32 v%d, s13" % V_T,
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK))] + dispatch(12)
     # EXIT: value r0 into V_RET (the group's results are stored together, see group code).
-    L += [".Lr_exit:",
-          "v_mov_b32 v%d, v0" % V_RET,
-          "v_mov_b32 v%d, v1" % (V_RET + 1),
+    L += [".Lr_exit:"] + ret_slot_write("v0", "v1") + [
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lex_nofault",
           "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
@@ -623,8 +626,7 @@ def routines():
     L += [".Lr_fault:",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
           "s_mov_b64 exec, %s" % sp(S_MASK),
-          "v_mov_b32 v%d, 0" % V_RET,
-          "v_mov_b32 v%d, 0" % (V_RET + 1),
+          ] + ret_slot_write("0", "0") + [
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lfl_nofault",
           "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
@@ -637,10 +639,10 @@ def routines():
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfl_nohist",
           "s_bcnt1_i32_b64 %s, exec" % s(S_BYTES),
+          "s_mov_b64 exec, 1",     # lane 0 only (its operands set below, after the switch)
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_BYTES)),
           "v_mov_b32 %s, 0" % v(R[9]),
           "v_mov_b32 %s, 0" % v(R[10]),
-          "s_mov_b64 exec, 1",
           "global_atomic_add_x2 %s, %s, %s offset:2048" % (v(R[10]), vp(R[8]), sp(S_HIST)),
           ".Lfl_nohist:",
           "s_andn2_b64 %s, %s, %s" % (sp(S_ALIVE), sp(S_ALIVE), sp(S_MASK)),
@@ -862,20 +864,54 @@ def kernel(name, staged, jit=False):
     return L
 
 
-def store_prev_results(tag):
-    """Store V_RET (r0 of every packet of group S_PREVG) as one 512-B write; clobbers exec."""
+def ret_slot_write(x0, x1):
+    """r0 of the retiring lanes into this group's result slot (v[V_RB + 2k], k = group % RETK)."""
+    if RETK == 1:
+        return ["v_mov_b32 v%d, %s" % (V_RB, x0), "v_mov_b32 v%d, %s" % (V_RB + 1, x1)]
+    return ["s_and_b32 %s, %s, %d" % (s(S_BYTES), s(S_GROUP), RETK - 1),
+            "s_lshl_b32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
+            "s_set_gpr_idx_on %s, gpr_idx(DST)" % s(S_BYTES),
+            "v_mov_b32 v%d, %s" % (V_RB, x0),
+            "v_mov_b32 v%d, %s" % (V_RB + 1, x1),
+            "s_set_gpr_idx_off"]
+
+
+def store_prev_results(tag, final):
+    """Write the result slots of the superblock that group S_PREVG ends (at the start of the
+    next superblock, or at the end: `final`) as one burst of RETK x 512 B; clobbers exec."""
     if os.environ.get("EBPF_ASM_NOSTORE"):   # experiment only: measures the read-side ceiling
         return []
-    return ["s_cmp_eq_u32 %s, -1" % s(S_PREVG),
-            "s_cbranch_scc1 .Lsp_none_%s" % tag,
-            "v_lshrrev_b32 %s, 4, v%d" % (v(R[0]), V_L16),
-            "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[0]), s(S_PREVG), v(R[0])),
-            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_COUNT), v(R[0])),
-            "s_mov_b64 exec, vcc",
-            "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(R[0])),
-            "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RET, V_RET + 1, sp(S_RET),
-                                                       ST_POLICY),
-            ".Lsp_none_%s:" % tag]
+    L = ["s_cmp_eq_u32 %s, -1" % s(S_PREVG),
+         "s_cbranch_scc1 .Lsp_none_%s" % tag]
+    if not final and RETK > 1:
+        L += ["s_and_b32 %s, %s, %d" % (s(S_T0), s(S_PREVG), RETK - 1),
+              "s_cmp_lg_u32 %s, %d" % (s(S_T0), RETK - 1),
+              "s_cbranch_scc1 .Lsp_none_%s" % tag]
+    # R0 = byte offset of the superblock's first packet result for this lane; R1 = its index
+    # (all lanes: the current group's live mask says nothing about the stored groups)
+    L += ["s_mov_b64 exec, -1",
+          "s_andn2_b32 %s, %s, %d" % (s(S_T0), s(S_PREVG), RETK - 1),
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[1]), s(S_T0), v(R[1])),
+          "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(R[1]))]
+    for k in range(RETK):
+        if k:
+            L.append("v_add_u32 %s, 64, %s" % (v(R[1]), v(R[1])))
+        L += ["v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_COUNT), v(R[1])),
+              "s_mov_b64 exec, vcc",
+              "global_store_dwordx2 %s, v[%d:%d], %s offset:%d%s" % (
+                  v(R[0]), V_RB + 2 * k, V_RB + 2 * k + 1, sp(S_RET), 512 * k, ST_POLICY)]
+    L.append(".Lsp_none_%s:" % tag)
+    return L
+
+
+def next_group(dst):
+    """dst = the group after S_GROUP in this wave's sequence (superblocks of RETK groups;
+    S_GSTRIDE holds the jump to the next superblock's first group)."""
+    return ["s_and_b32 %s, %s, %d" % (s(dst), s(S_GROUP), RETK - 1),
+            "s_cmp_eq_u32 %s, %d" % (s(dst), RETK - 1),
+            "s_cselect_b32 %s, %s, 1" % (s(dst), s(S_GSTRIDE)),
+            "s_add_u32 %s, %s, %s" % (s(dst), s(dst), s(S_GROUP))]
 
 
 def common_group_code():
@@ -927,6 +963,10 @@ def common_group_code():
           "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
           "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
           "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
+          "s_mul_i32 %s, %s, %d" % (s(S_GROUP), s(S_GROUP), RETK),
+          # superblock jump: (total waves - 1) * RETK + 1
+          "s_mul_i32 %s, %s, %d" % (s(S_GSTRIDE), s(S_GSTRIDE), RETK),
+          "s_sub_u32 %s, %s, %d" % (s(S_GSTRIDE), s(S_GSTRIDE), RETK - 1),
           # this wave's packet buffer (staged kernel); first group's prefetch
           "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
           "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),
@@ -934,8 +974,8 @@ def common_group_code():
           "s_cbranch_scc0 .Lgroup_check",
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
-    L += [".Lgroup_done:",
-          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_GSTRIDE)),
+    L += [".Lgroup_done:"] + next_group(S_T0) + [
+          "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
           "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
@@ -952,8 +992,7 @@ def common_group_code():
     for q in range(4):
         L.append("ds_read_b128 v[%d:%d], %s offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
                                                           v(H[1]), 16 * q))
-    L += ["s_waitcnt lgkmcnt(0)",
-          "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_GSTRIDE))] + call(".Lr_prefetch") + [
+    L += ["s_waitcnt lgkmcnt(0)"] + next_group(S_T0) + call(".Lr_prefetch") + [
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
           "v_mov_b32 %s, 64" % v(H[1]),
           "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
@@ -981,7 +1020,7 @@ def common_group_code():
           "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
           "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
-          ".Lgs_init:"] + store_prev_results("g") + [
+          ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
           "s_mov_b64 exec, %s" % sp(S_ALIVE)]
     for r in range(22):
@@ -994,7 +1033,7 @@ def common_group_code():
           "s_cselect_b32 %s, ebpf_jit_area-.Lcb, %s" % (s(S_T0), s(S_T0)),
           "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
     # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
-    L += [".Lfinish:"] + store_prev_results("f") + [
+    L += [".Lfinish:"] + store_prev_results("f", True) + [
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_barrier",
@@ -1005,7 +1044,18 @@ def common_group_code():
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # bin
           "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
           "ds_read_b32 %s, %s" % (v(H[3]), v(H[2])),
+          "s_load_dwordx2 %s, s[0:1], 0x68" % sp(S_REC),               # dp_launch.hist_rows
           "s_waitcnt lgkmcnt(0)",
+          # rows: this workgroup's 256 counts as one 1-KB row (hot bins would otherwise
+          # serialise thousands of same-address atomics); ebpf_hist_reduce sums the rows
+          "s_cmp_eq_u64 %s, 0" % sp(S_REC),
+          "s_cbranch_scc1 .Lfin_atomic",
+          "s_lshl_b32 %s, s2, 10" % s(S_T1),
+          "s_add_u32 %s, %s, %s" % (s(S_REC), s(S_REC), s(S_T1)),
+          "s_addc_u32 %s, %s, 0" % (s(S_REC + 1), s(S_REC + 1)),
+          "global_store_dword %s, %s, %s" % (v(H[2]), v(H[3]), sp(S_REC)),
+          "s_branch .Lfin_end",
+          ".Lfin_atomic:",
           "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[3]),
           "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE),
           "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(H[1])),
@@ -1220,6 +1270,8 @@ def main():
                   "outstanding")
     header.append("static const uint8_t ah_flags[AH_COUNT] = {%s};" % ",".join(map(str, conds)))
     header.append("#define AH_JIT_AREA_BYTES %d" % JIT_AREA_BYTES)
+    header.append("#define AH_RET_GROUPS %d  // groups per result burst (superblock)" % RETK)
+    header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
     A += [".p2align 2", ".Lhandler_table:"]
     A += ["  .long %s-.Llink_base" % lab for lab in table]
@@ -1227,7 +1279,7 @@ def main():
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 104
+    kernarg = 112
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, NSGPR, 256),
           ("ebpf_jit_s64", kernarg, 0, NVGPR, NSGPR, 256),

@@ -63,5 +63,7 @@ struct dp_launch {
 	uint32_t lds_stack_base;  // LDS byte offset of the first stack slice (after the histogram)
 	uint32_t total_waves;     // persistent grid: waves in the launch (group stride)
 	uint32_t lds_pkt_base;    // staged kernel: LDS byte offset of the per-wave packet buffers
+	uint32_t *hist_rows;      // assembly kernels: per-workgroup u32[256] verdict counts (bins
+	                          // 0..255), summed into hist by ebpf_hist_reduce; NULL = atomics
 };
-static_assert(sizeof(dp_launch) == 104, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 112, "dp_launch layout is shared with the assembly kernels");

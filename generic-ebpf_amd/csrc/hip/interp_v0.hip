@@ -297,6 +297,37 @@ ebpf_interp_v0(dp_launch L)
 
 } // namespace
 
+namespace {
+
+// Verdict-histogram second stage for the assembly kernels: every workgroup wrote its 256 bin
+// counts as one u32 row; block b sums a contiguous slice of rows (thread t = bin t, so each row
+// read is one coalesced 1-KB load) and adds its partial sums to the caller's u64 histogram.
+__global__ void __launch_bounds__(256)
+ebpf_hist_reduce(const uint32_t *__restrict__ rows, uint32_t nrows, unsigned long long *hist)
+{
+	const uint32_t per = (nrows + gridDim.x - 1) / gridDim.x;
+	const uint32_t r0 = blockIdx.x * per;
+	const uint32_t r1 = r0 + per < nrows ? r0 + per : nrows;
+	unsigned long long acc = 0;
+	for (uint32_t r = r0; r < r1; r++)
+		acc += rows[(size_t)r * 256 + threadIdx.x];
+	if (acc)
+		atomicAdd(&hist[threadIdx.x], acc);
+}
+
+} // namespace
+
+hipError_t
+launch_hist_reduce(const uint32_t *rows, uint32_t nrows, unsigned long long *hist,
+		   hipStream_t stream)
+{
+	if (nrows == 0)
+		return hipSuccess;
+	const uint32_t blocks = nrows < 64 ? nrows : 64;
+	hipLaunchKernelGGL(ebpf_hist_reduce, dim3(blocks), dim3(256), 0, stream, rows, nrows, hist);
+	return hipGetLastError();
+}
+
 hipError_t
 launch_interp_v0(const dp_launch &L, hipStream_t stream)
 {

@@ -18,6 +18,7 @@ hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
 			     uint32_t map_lds_bytes, void *fn);
 int asm_available(int device);
+uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
@@ -43,6 +44,54 @@ plan_map_lds(const struct ebpf_map *em, uint32_t *used)
 	const uint32_t off = kMapLdsBase + *used;
 	*used += (uint32_t)((bytes + 15) & ~15ull);
 	return off;
+}
+
+// Per-device pool of histogram row buffers (asm kernels: one u32[256] row per workgroup).  A
+// buffer is reusable once the event recorded after its last use has completed, so concurrent
+// launches on different streams never share one.
+struct rows_slot {
+	void *p = nullptr;
+	hipEvent_t ev = nullptr;
+	bool busy = false; // between acquire and the event record of the launch using it
+};
+std::mutex g_rows_lock;
+std::vector<std::vector<rows_slot>> g_rows;
+
+int
+rows_acquire(int device, size_t bytes, rows_slot **out)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	if ((int)g_rows.size() <= device)
+		g_rows.resize(device + 1);
+	for (rows_slot &r : g_rows[device])
+		if (!r.busy && hipEventQuery(r.ev) == hipSuccess) {
+			r.busy = true;
+			*out = &r;
+			return 0;
+		}
+	if (g_rows[device].size() >= 64)
+		return ENOMEM;
+	g_rows[device].reserve(64); // slots must not move: callers keep pointers
+	rows_slot r;
+	if (hipMalloc(&r.p, bytes) != hipSuccess)
+		return ENOMEM;
+	if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+		hipFree(r.p);
+		return ENOMEM;
+	}
+	r.busy = true;
+	g_rows[device].push_back(r);
+	*out = &g_rows[device].back();
+	return 0;
+}
+
+void
+rows_release(rows_slot *r, hipStream_t stream, bool used)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	if (used)
+		hipEventRecord(r->ev, stream);
+	r->busy = false;
 }
 
 thread_local std::string t_err;
@@ -249,11 +298,11 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
 		// variant 0: the compiled program; a program too large for the code area runs on the
 		// assembly interpreter instead (still the device path)
+		void *fn = nullptr;
 		if (variant == 0 && (err = jit_entries(ep, dp, mode)) == 0) {
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];
-			e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes,
-					      dp->jit_fn[mode]);
+			fn = dp->jit_fn[mode];
 		} else {
 			if (variant == 0 && err != E2BIG)
 				return err;
@@ -261,8 +310,17 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 				return err;
 			L.prog = dp->d_asm[mode];
 			L.stack_stride = dp->asm_stride[mode];
-			e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, nullptr);
 		}
+		rows_slot *rows = nullptr;
+		if (L.hist) {
+			if ((err = rows_acquire(dp->device,
+						(size_t)asm_max_workgroups(dp->device) * 1024, &rows)))
+				return fail(err, "no histogram row buffer");
+			L.hist_rows = static_cast<uint32_t *>(rows->p);
+		}
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn);
+		if (rows)
+			rows_release(rows, stream, e == hipSuccess);
 	} else {
 		L.prog = dp->d_entries;
 		e = launch_interp_v0(L, stream);

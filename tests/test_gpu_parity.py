@@ -175,16 +175,19 @@ def test_device_resident_api_and_histogram(gpu, env):
             m.destroy()
 
 
-def test_empty_and_ragged_batches(gpu, env):
+@pytest.mark.parametrize("variant", [0, 2])
+def test_empty_and_ragged_batches(gpu, env, variant):
+    """Empty, sub-group and ragged batches; the last size gives every wave of the persistent
+    grid several groups and ends in a partial group."""
     from generic_ebpf_amd import workloads
     lay = workloads.prog_c3()
-    for n in (0, 1, 63, 65, 255, 257, 1000):
+    for n in (0, 1, 63, 65, 255, 257, 1000, 64 * 8192 * 2 + 37):
         pk = workloads.packets_l2l3(max(n, 1), 64)[:n]
         c = goldens.Case("c3", lay.code, [], [], pk.reshape(-1) if n else np.zeros(1, np.uint8),
                          n, 64, None)
-        got, gf, _ = device_run(gpu, env, c, 0)
+        got, gf, _ = device_run(gpu, env, c, variant)
         if n:
-            want, wf, _, _ = oracle_run(c)
+            want, wf, _, _ = oracle_run(c, nthreads=8)
             np.testing.assert_array_equal(want, got)
         else:
             assert got.size == 0
