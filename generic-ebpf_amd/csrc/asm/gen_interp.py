@@ -103,8 +103,6 @@ for w in (16, 32, 64):
 for c in CONDS:
     fam(c + "_I", 1)
 for z in SIZES:
-    fam("LDXPKTS%d" % z, 1)
-for z in SIZES:
     fam("LDXPKTG%d" % z, 1)
 for z in SIZES:
     fam("LDXSTK%d" % z, 1)
@@ -116,9 +114,13 @@ for z in SIZES:
     fam("STSTK%d" % z, 0)
 for n in ("EXIT", "FAULT", "NOP", "LOOKUPSTK", "LOOKUPGEN"):
     fam(n, 0)
+for z in SIZES:
+    fam("LDXPKC%d" % z, 3)      # staged packet load at a constant byte offset: (dst, offset)
 
 
 def variants(arity):
+    if arity == 3:
+        return [(d, o) for o in range(64) for d in range(NREG)]
     if arity == 2:
         return [(d, s) for d in range(NREG) for s in range(NREG)]
     if arity == 1:
@@ -362,6 +364,34 @@ def h_ldx_pkt_staged(z, d):
     return out
 
 
+def h_ldx_pkt_const(z, d, off):
+    """Staged packet load at a translation-time byte offset: the bytes are already in
+    v22..v37, so this is 1-2 VALU (bit-field extract / byte align), no indexing."""
+    if off + z > 64:
+        return []          # never selected: the lowering faults such loads statically
+    k, sh = off >> 2, off & 3
+    lo_, hi_ = "v%d" % (PKT0 + k), "v%d" % (PKT0 + k + 1) if k + 1 < 16 else None
+    D0, D1 = lo(d), hi(d)
+    if z == 1:
+        return ["v_bfe_u32 %s, %s, %d, 8" % (D0, lo_, 8 * sh), "v_mov_b32 %s, 0" % D1]
+    if z == 2:
+        if sh <= 2:
+            return ["v_bfe_u32 %s, %s, %d, 16" % (D0, lo_, 8 * sh), "v_mov_b32 %s, 0" % D1]
+        return ["v_alignbyte_b32 %s, %s, %s, 3" % (D0, hi_, lo_),
+                "v_bfe_u32 %s, %s, 0, 16" % (D0, D0), "v_mov_b32 %s, 0" % D1]
+    if z == 4:
+        if sh == 0:
+            return ["v_mov_b32 %s, %s" % (D0, lo_), "v_mov_b32 %s, 0" % D1]
+        return ["v_alignbyte_b32 %s, %s, %s, %d" % (D0, hi_, lo_, sh), "v_mov_b32 %s, 0" % D1]
+    if sh == 0:
+        if (PKT0 + k) % 2 == 0:
+            return ["v_mov_b64 %s, v[%d:%d]" % (pair(d), PKT0 + k, PKT0 + k + 1)]
+        return ["v_mov_b32 %s, %s" % (D0, lo_), "v_mov_b32 %s, %s" % (D1, hi_)]
+    h2 = "v%d" % (PKT0 + k + 2)
+    return ["v_alignbyte_b32 %s, %s, %s, %d" % (D0, hi_, lo_, sh),
+            "v_alignbyte_b32 %s, %s, %s, %d" % (D1, h2, hi_, sh)]
+
+
 LOADS = {1: "global_load_ubyte", 2: "global_load_ushort", 4: "global_load_dword",
          8: "global_load_dwordx2"}
 
@@ -526,8 +556,8 @@ def handler_body(name, d, sr):
             return h_cond(c, d, sr, False)
         if name == c + "_I":
             return h_cond(c, d, None, True)
-    if name.startswith("LDXPKTS"):
-        return h_ldx_pkt_staged(int(name[7:]), d), False
+    if name.startswith("LDXPKC"):
+        return h_ldx_pkt_const(int(name[6:]), d, sr), False
     if name.startswith("LDXPKTG"):
         return h_ldx_pkt_general(int(name[7:]), d), False
     if name.startswith("LDXSTK"):
@@ -1023,9 +1053,10 @@ def common_group_code():
           ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
           "s_mov_b64 exec, %s" % sp(S_ALIVE)]
-    for r in range(22):
-        L.append("v_mov_b32 v%d, 0" % r)
-    L += ["v_mov_b32 v2, v%d" % V_PKT, "v_mov_b32 v3, v%d" % (V_PKT + 1),
+    for r in range(0, 20, 2):
+        if r != 2:
+            L.append("v_mov_b64 v[%d:%d], 0" % (r, r + 1))
+    L += ["v_mov_b64 v[2:3], v[%d:%d]" % (V_PKT, V_PKT + 1),
           "v_add_u32 v20, %s, v%d" % (s(S_STKSTRIDE), V_STK),
           "v_mov_b32 v21, %s" % s(S_SHARED + 1),
           "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),

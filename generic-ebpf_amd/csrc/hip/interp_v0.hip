@@ -300,17 +300,23 @@ ebpf_interp_v0(dp_launch L)
 namespace {
 
 // Verdict-histogram second stage for the assembly kernels: every workgroup wrote its 256 bin
-// counts as one u32 row; block b sums a contiguous slice of rows (thread t = bin t, so each row
-// read is one coalesced 1-KB load) and adds its partial sums to the caller's u64 histogram.
+// counts as one u32 row; block b sums rows [16b, 16b+16) (thread t = bin t, so each row is one
+// coalesced 1-KB load, all 16 in flight at once) and adds the partial sums to the caller's u64
+// histogram.
+constexpr uint32_t kRowsPerBlock = 16;
+
 __global__ void __launch_bounds__(256)
 ebpf_hist_reduce(const uint32_t *__restrict__ rows, uint32_t nrows, unsigned long long *hist)
 {
-	const uint32_t per = (nrows + gridDim.x - 1) / gridDim.x;
-	const uint32_t r0 = blockIdx.x * per;
-	const uint32_t r1 = r0 + per < nrows ? r0 + per : nrows;
+	const uint32_t r0 = blockIdx.x * kRowsPerBlock;
+	uint32_t v[kRowsPerBlock];
+#pragma unroll
+	for (uint32_t k = 0; k < kRowsPerBlock; k++)
+		v[k] = r0 + k < nrows ? rows[(size_t)(r0 + k) * 256 + threadIdx.x] : 0u;
 	unsigned long long acc = 0;
-	for (uint32_t r = r0; r < r1; r++)
-		acc += rows[(size_t)r * 256 + threadIdx.x];
+#pragma unroll
+	for (uint32_t k = 0; k < kRowsPerBlock; k++)
+		acc += v[k];
 	if (acc)
 		atomicAdd(&hist[threadIdx.x], acc);
 }
@@ -323,7 +329,7 @@ launch_hist_reduce(const uint32_t *rows, uint32_t nrows, unsigned long long *his
 {
 	if (nrows == 0)
 		return hipSuccess;
-	const uint32_t blocks = nrows < 64 ? nrows : 64;
+	const uint32_t blocks = (nrows + kRowsPerBlock - 1) / kRowsPerBlock;
 	hipLaunchKernelGGL(ebpf_hist_reduce, dim3(blocks), dim3(256), 0, stream, rows, nrows, hist);
 	return hipGetLastError();
 }

@@ -16,7 +16,7 @@ for cfg in "$@"; do
   for p in "${PASSES[@]}"; do
     d=gpurun_out/$T/pmc_${cfg}_$i
     mkdir -p $d
-    timeout -k 10 300 rocprofv3 --pmc $p --kernel-trace --kernel-include-regex ebpf_interp \
+    timeout -k 10 300 rocprofv3 --pmc $p --kernel-trace --kernel-include-regex 'ebpf_(interp|jit)' \
       --output-format csv -d $d -o pmc -- python3 bench.py --config $cfg --no-cpu-baseline \
       --steps 3 --warmup 1 > $d/bench.json 2> $d/err.log || { tail -5 $d/err.log; exit 1; }
     i=$((i+1))

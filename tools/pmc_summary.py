@@ -19,7 +19,8 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "ebpf_interp" not in row.get("Kernel_Name", ""):
+                kn = row.get("Kernel_Name", "")
+                if "ebpf_interp" not in kn and "ebpf_jit" not in kn:
                     continue
                 vals[(row["Counter_Name"], row["Dispatch_Id"])].append(float(row["Counter_Value"]))
     per = defaultdict(list)
