@@ -21,9 +21,10 @@ import os
 import sys
 
 NREG = 11
-# cache policy of the streaming accesses (experiments: EBPF_ASM_NT bit 0 = ret stores nt,
-# bit 1 = packet DMA loads nt)
-_NT = int(os.environ.get("EBPF_ASM_NT", "1"))
+# cache policy of the streaming accesses (EBPF_ASM_NT bit 0 = ret stores nt, bit 1 = packet DMA
+# loads nt).  Both nt by default: the once-read packet stream with nt DMA reads 6.75 TB/s against
+# 6.06 TB/s default policy (tools/ubench/floor.hip, profiles/r01/ubench/)
+_NT = int(os.environ.get("EBPF_ASM_NT", "3"))
 ST_POLICY = " nt" if _NT & 1 else ""
 LD_POLICY = " nt" if _NT & 2 else ""
 # ---------------------------------------------------------------- register plan
@@ -40,7 +41,9 @@ R = list(range(52, 63))              # routine temporaries
 V_SEL = 63                           # v_perm selector 0x00010203 (byte swap)
 # Results of RETK consecutive groups are kept in VGPRs and written as one RETK x 512-B burst
 # (RETK > 1 adds 2*RETK VGPRs at v64).  Each wave walks superblocks of RETK consecutive groups.
-RETK = int(os.environ.get("EBPF_ASM_RETK", "1"))
+# Default 8: one aligned 4-KB result burst per wave reads+writes at 5.6-5.7 TB/s against
+# 5.1 TB/s for 512-B stores (floor.hip), worth the 6 instead of 8 waves per SIMD it costs.
+RETK = int(os.environ.get("EBPF_ASM_RETK", "8"))
 assert RETK in (1, 2, 4, 8)
 V_RB = 44 if RETK == 1 else 64
 NVGPR = 64 if RETK == 1 else 64 + 2 * RETK

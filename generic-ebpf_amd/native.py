@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libebpf.so")
+# EBPF_LIB: an alternative build of the same library (A/B experiments under tools/)
+LIB_PATH = os.environ.get("EBPF_LIB") or os.path.join(HERE, "lib", "libebpf.so")
 
 EBPF_TYPE_MAX = 64
 EBPF_NAME_MAX = 64
