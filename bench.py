@@ -33,8 +33,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c4", choices=sorted(workloads.CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default per config)")
     ap.add_argument("--variant", type=int, default=0, help="0 = default interpreter, 1 = HIP baseline")

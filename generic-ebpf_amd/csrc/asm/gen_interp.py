@@ -43,10 +43,21 @@ V_SEL = 63                           # v_perm selector 0x00010203 (byte swap)
 # (RETK > 1 adds 2*RETK VGPRs at v64).  Each wave walks superblocks of RETK consecutive groups.
 # Default 8: one aligned 4-KB result burst per wave reads+writes at 5.6-5.7 TB/s against
 # 5.1 TB/s for 512-B stores (floor.hip), worth the 6 instead of 8 waves per SIMD it costs.
-RETK = int(os.environ.get("EBPF_ASM_RETK", "8"))
-assert RETK in (1, 2, 4, 8)
-V_RB = 44 if RETK == 1 else 64
-NVGPR = 64 if RETK == 1 else 64 + 2 * RETK
+# Two code objects are generated: the staged (fixed 64-B) kernels use RETK_STAGED, the general
+# kernels (any stride / offsets: latency-bound per-packet loads, where the 8 waves per SIMD of
+# RETK = 1 matter more than the store burst) use RETK = 1.
+RETK_STAGED = int(os.environ.get("EBPF_ASM_RETK", "8"))
+assert RETK_STAGED in (1, 2, 4, 8)
+
+
+def set_retk(k):
+    global RETK, V_RB, NVGPR
+    RETK = k
+    V_RB = 44 if RETK == 1 else 64
+    NVGPR = 64 if RETK == 1 else 64 + 2 * RETK
+
+
+set_retk(RETK_STAGED)
 
 # SGPRs (next_free_sgpr 80 -> 8 waves per SIMD)
 S_CB = 4             # s[4:5] code base (.Lcb): routines are reached at S_CB + (label - .Lcb)
@@ -1254,7 +1265,23 @@ def jit_templates():
 
 
 def main():
-    out_s, out_h = sys.argv[1], sys.argv[2]
+    """gen_interp.py <staged.s> <general.s> <handlers.h>"""
+    out_s1, out_s0, out_h = sys.argv[1], sys.argv[2], sys.argv[3]
+    header = None
+    for out_s, k in ((out_s1, RETK_STAGED), (out_s0, 1)):
+        set_retk(k)
+        h = generate(out_s)
+        header = header or h
+        assert h[:-2] == header[:-2]   # identical but for the RETK-dependent lines
+    header = header[:-2] + ["#define AH_RET_GROUPS_STAGED %d  // groups per result burst, staged kernels"
+                            % RETK_STAGED,
+                            "#define AH_NVGPR_STAGED %d" % (64 if RETK_STAGED == 1 else 64 + 2 * RETK_STAGED),
+                            "#define AH_RET_GROUPS_GENERAL 1", "#define AH_NVGPR_GENERAL 64"]
+    with open(out_h, "w") as f:
+        f.write("\n".join(header) + "\n")
+
+
+def generate(out_s):
     A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950:xnack-"', ".amdhsa_code_object_version 5", ".text"]
     A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
     A += kernel("ebpf_jit_s64", True, True) + kernel("ebpf_jit_gen", False, True)
@@ -1266,9 +1293,14 @@ def main():
     hid = 0
     header = ["// generated by gen_interp.py — handler family ids for asm_runtime.cpp",
               "#pragma once", "#include <stdint.h>", "#define AH_NREGS %d" % NREG]
-    for name, arity in FAMILIES:
+    fam_of, dst_of, src_of = [], [], []
+    for fi, (name, arity) in enumerate(FAMILIES):
         header.append("#define AH_%s %d" % (name, hid))
+        header.append("#define AHF_%s %d" % (name, fi))
         for d, sr in variants(arity):
+            fam_of.append(fi)
+            dst_of.append(255 if d is None else d)
+            src_of.append(255 if sr is None else sr)
             label = "h_%d" % hid
             uid = "%d" % hid
             body, own = handler_body(name, d, sr)
@@ -1303,8 +1335,13 @@ def main():
     header.append("// bit 0: conditional jump (copy the compare only); bit 1: body leaves an LDS read "
                   "outstanding")
     header.append("static const uint8_t ah_flags[AH_COUNT] = {%s};" % ",".join(map(str, conds)))
+    header.append("// per handler: family (AHF_*), dst register, src register (LDXPKC: packet byte offset);")
+    header.append("// 255 = none.  Read by the optimising code generator (asm_cc.cpp)")
+    header.append("static const uint8_t ah_fam[AH_COUNT] = {%s};" % ",".join(map(str, fam_of)))
+    header.append("static const uint8_t ah_dst[AH_COUNT] = {%s};" % ",".join(map(str, dst_of)))
+    header.append("static const uint8_t ah_src[AH_COUNT] = {%s};" % ",".join(map(str, src_of)))
     header.append("#define AH_JIT_AREA_BYTES %d" % JIT_AREA_BYTES)
-    header.append("#define AH_RET_GROUPS %d  // groups per result burst (superblock)" % RETK)
+    header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
     A += [".p2align 2", ".Lhandler_table:"]
@@ -1326,8 +1363,7 @@ def main():
         f.write("\n".join(("\t" + x if not (x.endswith(":") or x.startswith(".") or x.startswith(" ")) else x)
                           for x in A) + "\n")
         f.write("\n".join(md) + "\n")
-    with open(out_h, "w") as f:
-        f.write("\n".join(header) + "\n")
+    return header
 
 
 if __name__ == "__main__":

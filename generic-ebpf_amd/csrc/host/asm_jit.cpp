@@ -19,11 +19,9 @@
 #include <elf.h>
 #include <hip/hip_runtime.h>
 
+#include "asm_cc.h"
 #include "asm_handlers.h"
 #include "internal.h"
-
-extern const unsigned char ebpf_asm_hsaco[];
-extern const size_t ebpf_asm_hsaco_len;
 
 int asm_lower(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	      std::vector<dp_entry> &out, uint32_t *stack_stride, std::string *err);
@@ -88,44 +86,45 @@ find_symbols(const unsigned char *img, size_t len, const char *const *names, siz
 }
 
 const jit_image &
-image_info()
+image_info(int mode)
 {
-	static jit_image info;
-	static std::once_flag once;
-	std::call_once(once, [] {
+	static jit_image info[2];
+	static std::once_flag once[2];
+	std::call_once(once[mode], [mode] {
+		jit_image &I = info[mode];
+		const unsigned char *img = asm_image(mode);
+		const size_t len = asm_image_len(mode);
 		const char *names[] = {"ebpf_cb", "ebpf_jit_meta", "ebpf_jit_tmpl"};
 		size_t off[3];
-		if (!find_symbols(ebpf_asm_hsaco, ebpf_asm_hsaco_len, names, 3, off)) {
-			info.why = "code object lacks the compiled-program symbols";
+		if (!find_symbols(img, len, names, 3, off)) {
+			I.why = "code object lacks the compiled-program symbols";
 			return;
 		}
-		info.cb = off[0];
-		const unsigned char *meta = ebpf_asm_hsaco + off[1];
-		const unsigned char *tm = ebpf_asm_hsaco + off[2];
-		if (off[1] + 8ull * AH_COUNT > ebpf_asm_hsaco_len ||
-		    off[2] + 4ull * JT_COUNT > ebpf_asm_hsaco_len) {
-			info.why = "compiled-program tables out of range";
+		I.cb = off[0];
+		const unsigned char *meta = img + off[1];
+		const unsigned char *tm = img + off[2];
+		if (off[1] + 8ull * AH_COUNT > len || off[2] + 4ull * JT_COUNT > len) {
+			I.why = "compiled-program tables out of range";
 			return;
 		}
-		info.body_off.resize(AH_COUNT);
-		info.body_len.resize(AH_COUNT);
+		I.body_off.resize(AH_COUNT);
+		I.body_len.resize(AH_COUNT);
 		for (int h = 0; h < AH_COUNT; h++) {
-			memcpy(&info.body_off[h], meta + 8 * h, 4);
-			memcpy(&info.body_len[h], meta + 8 * h + 4, 4);
-			if (info.cb + info.body_off[h] + info.body_len[h] > ebpf_asm_hsaco_len) {
-				info.why = "handler body out of range";
+			memcpy(&I.body_off[h], meta + 8 * h, 4);
+			memcpy(&I.body_len[h], meta + 8 * h + 4, 4);
+			if (I.cb + I.body_off[h] + I.body_len[h] > len) {
+				I.why = "handler body out of range";
 				return;
 			}
 		}
-		memcpy(info.t, tm, sizeof(info.t));
-		if (info.t[JT_AREA_BYTES] != AH_JIT_AREA_BYTES ||
-		    info.cb + info.t[JT_AREA] + info.t[JT_AREA_BYTES] > ebpf_asm_hsaco_len) {
-			info.why = "compiled-program area out of range";
+		memcpy(I.t, tm, sizeof(I.t));
+		if (I.t[JT_AREA_BYTES] != AH_JIT_AREA_BYTES || I.cb + I.t[JT_AREA] + I.t[JT_AREA_BYTES] > len) {
+			I.why = "compiled-program area out of range";
 			return;
 		}
-		info.ok = true;
+		I.ok = true;
 	});
-	return info;
+	return info[mode];
 }
 
 inline bool
@@ -150,7 +149,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
 	     uint32_t *stack_stride, std::string *err)
 {
-	const jit_image &I = image_info();
+	const jit_image &I = image_info(mode);
 	if (!I.ok) {
 		*err = I.why;
 		return ENOSYS;
@@ -203,23 +202,40 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		const uint32_t k = idx[e];
 		return !(k + 1 < order.size() && order[k + 1] == sx);
 	};
+	// blocks that can be entered other than by falling through from their layout predecessor:
+	// taken targets, branch targets, scheduler resume points after a lookup, the start
+	std::vector<char> entry_point(n, 0);
+	entry_point[xl.start] = 1;
+	for (uint32_t e : order) {
+		const uint32_t h = (uint32_t)low[e].handler;
+		if (ah_flags[h] & 1)
+			entry_point[xl.entries[e].target] = 1;
+		if (h == (uint32_t)AH_LOOKUPGEN && xl.entries[e].next < n)
+			entry_point[xl.entries[e].next] = 1;
+		if (needs_branch(e))
+			entry_point[succ(e)] = 1;
+	}
+	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
+	std::vector<cc_block> cb;
+	if (getenv("EBPF_JIT_NOCC") == nullptr)
+		cc_compile(xl, low, order, entry_point, mode, cb);
+	else
+		cb.assign(n, cc_block());
+	auto reads_of = [&](uint32_t e) -> uint8_t {
+		return cb[e].fast ? cb[e].reads : ah_reads[(uint32_t)low[e].handler];
+	};
+	auto sval_of = [&](uint32_t e, int r) -> uint32_t {
+		if (cb[e].fast)
+			return cb[e].sval[r];
+		uint32_t dw[8];
+		memcpy(dw, &low[e], 32);
+		return dw[2 + r];
+	};
 	// Operand registers s10..s15 a block must set: the ones its body reads, minus those that
 	// provably already hold the value.  Values carry along a fall-through chain; a block that
-	// can be entered any other way (taken target, branch target, scheduler resume point after
-	// a lookup, the start) assumes nothing.
+	// can be entered any other way assumes nothing.
 	std::vector<uint8_t> pre_mask(n, 0);
 	{
-		std::vector<char> entry_point(n, 0);
-		entry_point[xl.start] = 1;
-		for (uint32_t e : order) {
-			const uint32_t h = (uint32_t)low[e].handler;
-			if (ah_flags[h] & 1)
-				entry_point[xl.entries[e].target] = 1;
-			if (h == (uint32_t)AH_LOOKUPGEN && xl.entries[e].next < n)
-				entry_point[xl.entries[e].next] = 1;
-			if (needs_branch(e))
-				entry_point[succ(e)] = 1;
-		}
 		bool known[6] = {};
 		uint32_t val[6] = {};
 		for (size_t k = 0; k < order.size(); k++) {
@@ -228,31 +244,55 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			if (!fall || entry_point[e])
 				for (bool &x : known)
 					x = false;
-			const uint32_t h = (uint32_t)low[e].handler;
-			uint32_t dw[8];
-			memcpy(dw, &low[e], 32);
+			const uint8_t rd = reads_of(e);
 			uint8_t m = 0;
 			for (int r = 0; r < 6; r++) {
-				if (!(ah_reads[h] & (1u << r)))
+				if (!(rd & (1u << r)))
 					continue;
-				if (r == 2 || !known[r] || val[r] != dw[2 + r]) {
+				const uint32_t v = sval_of(e, r);
+				if (r == 2 || !known[r] || val[r] != v) {
 					m |= (uint8_t)(1u << r);
 					if (r != 2) {
 						known[r] = true;
-						val[r] = dw[2 + r];
+						val[r] = v;
 					}
 				}
 			}
 			pre_mask[e] = m;
 		}
 	}
+	// s_mov_b32 s(10+r), v: 4 bytes with an inline constant, else 8 (s12, the resume offset,
+	// is only known after layout: always the literal form)
+	auto inline_code = [](uint32_t v, uint32_t *code) {
+		const int32_t x = (int32_t)v;
+		if (x >= 0 && x <= 64) {
+			*code = 128 + (uint32_t)x;
+			return true;
+		}
+		if (x >= -16 && x < 0) {
+			*code = 192 + (uint32_t)(-x);
+			return true;
+		}
+		return false;
+	};
+	auto pre_len = [&](uint32_t e) {
+		uint32_t sz = 0, c;
+		for (int r = 0; r < 6; r++)
+			if (pre_mask[e] & (1u << r))
+				sz += (r != 2 && inline_code(sval_of(e, r), &c)) ? 4 : 8;
+		return sz;
+	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = 8u * (uint32_t)__builtin_popcount(pre_mask[e]);
+		uint32_t sz = pre_len(e);
 		*pre = sz;
-		sz += I.body_len[h];
-		if (ah_flags[h] & 2)
-			sz += 4;
+		if (cb[e].fast) {
+			sz += (uint32_t)cb[e].body.size();
+		} else {
+			sz += I.body_len[h];
+			if (ah_flags[h] & 2)
+				sz += 4;
+		}
 		*body_end = sz;
 		if (ah_flags[h] & 1)
 			sz += long_cond[e] ? cl_len : cs_len;
@@ -304,9 +344,9 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 
 	// emit
 	std::vector<unsigned char> &img = *img_out;
-	img.assign(ebpf_asm_hsaco, ebpf_asm_hsaco + ebpf_asm_hsaco_len);
+	img.assign(asm_image(mode), asm_image(mode) + asm_image_len(mode));
 	const size_t area = I.cb + T[JT_AREA];
-	const unsigned char *src = ebpf_asm_hsaco + I.cb;
+	const unsigned char *src = asm_image(mode) + I.cb;
 	auto code_off = [&](uint32_t e) { return T[JT_AREA] + pos[e]; }; // from .Lcb
 	auto put32 = [&](size_t at, uint32_t v) { memcpy(&img[area + at], &v, 4); };
 	auto copy_t = [&](size_t at, int a, uint32_t len) {
@@ -322,26 +362,36 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	for (uint32_t e : order) {
 		const dp_entry &o = low[e];
 		const uint32_t h = (uint32_t)o.handler;
-		uint32_t dw[8];
-		memcpy(dw, &o, 32);
 		size_t at = pos[e];
 		for (int r = 0; r < 6; r++) {
 			if (!(pre_mask[e] & (1u << r)))
 				continue;
-			uint32_t v = dw[2 + r];
+			uint32_t v = sval_of(e, r);
 			if (r == 2) { // s12: code offset of the next block (LOOKUPGEN resumes there)
 				const uint32_t nx = xl.entries[e].next;
 				v = nx < n && placed[nx] ? code_off(nx) : 0;
+			}
+			uint32_t ic;
+			if (r != 2 && inline_code(v, &ic)) { // s_mov_b32 s(10+r), <inline constant>
+				put32(at, 0xbe800000u | ((uint32_t)(10 + r) << 16) | ic);
+				at += 4;
+				continue;
 			}
 			copy_t(at, JT_MOV_S10 + r, 8);
 			put32(at + 4, v);
 			at += 8;
 		}
-		memcpy(&img[area + at], src + I.body_off[h], I.body_len[h]);
-		at += I.body_len[h];
-		if (ah_flags[h] & 2) {
-			copy_t(at, JT_WAIT, 4);
-			at += 4;
+		if (cb[e].fast) {
+			if (!cb[e].body.empty())
+				memcpy(&img[area + at], cb[e].body.data(), cb[e].body.size());
+			at += cb[e].body.size();
+		} else {
+			memcpy(&img[area + at], src + I.body_off[h], I.body_len[h]);
+			at += I.body_len[h];
+			if (ah_flags[h] & 2) {
+				copy_t(at, JT_WAIT, 4);
+				at += 4;
+			}
 		}
 		if (ah_flags[h] & 1) {
 			const uint32_t tk = xl.entries[e].target;

@@ -73,6 +73,13 @@ constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 
+// The assembly interpreter's two code objects (build/asm_image.cpp): mode 1 = staged 64-B
+// kernels, mode 0 = general kernels.
+extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[];
+extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len;
+inline const unsigned char *asm_image(int mode) { return mode == 1 ? ebpf_asm_hsaco_m1 : ebpf_asm_hsaco_m0; }
+inline size_t asm_image_len(int mode) { return mode == 1 ? ebpf_asm_hsaco_m1_len : ebpf_asm_hsaco_m0_len; }
+
 // Per (program, device): entries for each interpreter variant and the map table.
 struct dprog_device {
 	int device = -1;

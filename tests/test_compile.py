@@ -19,6 +19,20 @@ def _decode(code):
     return r.stdout, r.stderr
 
 
+def _encodings(code):
+    """Re-encode the disassembly: llvm-mc's encoding of every decoded instruction, concatenated
+    (must reproduce `code` exactly when every instruction decodes as what was encoded)."""
+    hexs = " ".join("0x%02x" % b for b in code)
+    r = subprocess.run([LLVM_MC, "--disassemble", "-show-encoding", "-triple=amdgcn-amd-amdhsa",
+                        "-mcpu=gfx950"], input=hexs, capture_output=True, text=True, timeout=60)
+    out = bytearray()
+    for ln in r.stdout.splitlines():
+        if "encoding: [" in ln:
+            enc = ln.split("encoding: [")[1].split("]")[0]
+            out += bytes(int(x, 16) for x in enc.split(","))
+    return bytes(out), r.stdout
+
+
 def _progs(native, env):
     from generic_ebpf_amd import workloads
     out = []
@@ -76,3 +90,79 @@ def test_device_code_rejects_bad_layout(native, env):
                           "device_code")
     finally:
         p.destroy()
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+def test_optimised_c4_instruction_forms(native, env):
+    """Spot-check the encodings of the optimising code generator (asm_cc.cpp) on the classifier:
+    the decoded instructions are exactly the forms it means to emit."""
+    from generic_ebpf_amd import workloads
+    m = native.Map(env, 256, 8)
+    try:
+        lay = workloads.prog_c4()
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle]))
+        try:
+            text, err = _decode(p.device_code(1))
+        finally:
+            p.destroy()
+    finally:
+        m.destroy()
+    lines = [ln.strip() for ln in text.splitlines() if ln.strip() and not ln.strip().startswith(".")]
+    want = [
+        # LDXH r2, [r1+12]; BE16 r2  ->  one byte-select from the staged packet dwords 3/4
+        "s_mov_b32 s13, 0xc0c0001", "v_perm_b32 v4, v26, v25, s13",
+        # JEQ r2, 0x86dd with r2 < 2^16: one 32-bit compare, constant as a literal
+        "v_cmp_eq_u32_e32 vcc, 0x86dd, v4",
+        # LDXB r3, [r1+23]
+        "v_bfe_u32 v6, v27, 24, 8",
+        # LDXW r4, [r1+26]; BE32 r4
+        "s_mov_b32 s13, 0x2030405", "v_perm_b32 v8, v29, v28, s13",
+        # r8 = 0; r8 |= r4; r8 <<= 32; r8 |= r5  ->  moves
+        "v_mov_b32_e32 v16, v8", "v_mov_b32_e32 v17, v16", "v_mov_b32_e32 v16, 0",
+        "v_or_b32_e32 v16, v10, v16",
+        # MUL64 r8, 0x1e3779b1: two quarter-rate multiplies
+        "s_mov_b32 s13, 0x1e3779b1", "v_mul_lo_u32 v48, v17, s13",
+        "v_mad_u64_u32 v[46:47], s[60:61], v16, s13, 0", "v_add_u32_e32 v17, v47, v48",
+        "v_mov_b32_e32 v16, v46",
+        # XOR64 r8, imm with a zero high word: low half only
+        "v_xor_b32_e32 v16, 0x5bd1e995, v16",
+        # r2 = r10 - 4
+        "v_mov_b64_e32 v[4:5], v[20:21]", "v_lshl_add_u64 v[4:5], -4, 0, v[4:5]",
+    ]
+    for w in want:
+        assert w in lines, (w, "\n".join(lines[:80]))
+
+
+def _count_valu(native, env, code, layout, nocc):
+    if nocc:
+        os.environ["EBPF_JIT_NOCC"] = "1"
+    try:
+        p = native.Prog(env, code)
+        try:
+            dc = p.device_code(layout)
+        finally:
+            p.destroy()
+    finally:
+        os.environ.pop("EBPF_JIT_NOCC", None)
+    out, _ = _decode(dc)
+    return sum(1 for ln in out.splitlines() if ln.strip().startswith("v_")), len(dc)
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+def test_optimised_code_is_smaller(native, env):
+    """The known-bits code generator must not emit more vector instructions than the
+    handler-copy baseline, and must remove a good share of them on the classifier (C4)."""
+    from generic_ebpf_amd import workloads
+    m = native.Map(env, 256, 8)
+    try:
+        for cfg in ("c2", "c3", "c4", "c5"):
+            lay = workloads.CONFIGS[cfg]["prog"]()
+            code = native.patch_relocs(lay.code, lay.relocs, [m.handle] if cfg == "c4" else [])
+            for layout in (1, 0):
+                opt, _ = _count_valu(native, env, code, layout, False)
+                base, _ = _count_valu(native, env, code, layout, True)
+                assert opt <= base, (cfg, layout, opt, base)
+                if cfg == "c4" and layout == 1:
+                    assert opt <= 0.8 * base, (opt, base)
+    finally:
+        m.destroy()
