@@ -651,6 +651,7 @@ def routines():
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_MASK), s(S_BYTES), v(R[8])),
           "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
           "s_cbranch_scc0 .Lex_lanes",
+          ".Lex_uniform:",
           "s_bcnt1_i32_b64 %s, exec" % s(S_CODE),
           "s_lshl_b32 %s, %s, 2" % (s(S_BYTES), s(S_BYTES)),
           "s_mov_b64 %s, exec" % sp(S_SAVE),
@@ -666,6 +667,19 @@ def routines():
           "ds_add_u32 %s, %s" % (v(R[8]), v(R[9])),
           ".Lex_nohist:",
           "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE))] + goto(".Lr_schedule")
+    # EXIT with r0 known at compile time (compiled programs): v[44:45] = r0 and S_BYTES = its
+    # verdict bin are set by the caller, so the verdict needs no per-lane work
+    L += [".Lr_exit_k:",
+          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
+          "s_cbranch_scc1 .Lexk_nofault",
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
+          "v_mov_b32 %s, 0" % v(R[8]),
+          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
+          ".Lexk_nofault:",
+          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
+          "s_cbranch_scc1 .Lex_nohist",
+          "s_branch .Lex_uniform"]
     # FAULT: lanes s[mask], code s[S_CODE]; returns via s[link] unless no lane remains
     L += [".Lr_fault:",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
@@ -908,15 +922,25 @@ def kernel(name, staged, jit=False):
     return L
 
 
+V_RES = 44   # v[44:45]: r0 of the lanes that retired in the running group
+
+
 def ret_slot_write(x0, x1):
-    """r0 of the retiring lanes into this group's result slot (v[V_RB + 2k], k = group % RETK)."""
+    """r0 of the retiring lanes into v[44:45]; a superblock kernel (RETK > 1) moves the whole
+    group's results into its slot v[V_RB + 2k], k = group % RETK, once when the group is done
+    (slot_commit), not at every exit."""
+    return ["v_mov_b32 v%d, %s" % (V_RES, x0), "v_mov_b32 v%d, %s" % (V_RES + 1, x1)]
+
+
+def slot_commit():
     if RETK == 1:
-        return ["v_mov_b32 v%d, %s" % (V_RB, x0), "v_mov_b32 v%d, %s" % (V_RB + 1, x1)]
-    return ["s_and_b32 %s, %s, %d" % (s(S_BYTES), s(S_GROUP), RETK - 1),
+        return []
+    return ["s_mov_b64 exec, -1",
+            "s_and_b32 %s, %s, %d" % (s(S_BYTES), s(S_GROUP), RETK - 1),
             "s_lshl_b32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
             "s_set_gpr_idx_on %s, gpr_idx(DST)" % s(S_BYTES),
-            "v_mov_b32 v%d, %s" % (V_RB, x0),
-            "v_mov_b32 v%d, %s" % (V_RB + 1, x1),
+            "v_mov_b32 v%d, v%d" % (V_RB, V_RES),
+            "v_mov_b32 v%d, v%d" % (V_RB + 1, V_RES + 1),
             "s_set_gpr_idx_off"]
 
 
@@ -1018,7 +1042,7 @@ def common_group_code():
           "s_cbranch_scc0 .Lgroup_check",
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
-    L += [".Lgroup_done:"] + next_group(S_T0) + [
+    L += [".Lgroup_done:"] + slot_commit() + next_group(S_T0) + [
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
@@ -1036,7 +1060,28 @@ def common_group_code():
     for q in range(4):
         L.append("ds_read_b128 v[%d:%d], %s offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
                                                           v(H[1]), 16 * q))
-    L += ["s_waitcnt lgkmcnt(0)"] + next_group(S_T0) + call(".Lr_prefetch") + [
+    # next group's DMA: a full group (the common case) inline, with exec = all lanes and the
+    # instruction offset stepping both the global and the LDS address (M0 set once); a partial
+    # group through the masking routine
+    L += ["s_waitcnt lgkmcnt(0)"] + next_group(S_T0) + [
+          "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),        # full groups
+          "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
+          "s_cbranch_scc0 .Lgs_pf_slow",
+          "s_lshr_b32 s65, %s, 20" % s(S_T0),
+          "s_lshl_b32 s64, %s, 12" % s(S_T0),
+          "s_add_u32 s64, s64, %s" % s(S_DATA),
+          "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
+          "s_mov_b64 exec, -1",
+          "s_mov_b32 m0, %s" % s(S_PKTLDS),
+          "s_nop 0"] + [
+          "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
+          for qq in range(4)] + [
+          "s_branch .Lgs_pf_done",
+          ".Lgs_pf_slow:"] + call(".Lr_prefetch") + [
+          ".Lgs_pf_done:",
+          # a compiled program computes the packet address itself if it needs it
+          "s_bitcmp1_b32 s7, 1",
+          "s_cbranch_scc1 .Lgs_init",
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
           "v_mov_b32 %s, 64" % v(H[1]),
           "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
@@ -1066,7 +1111,13 @@ def common_group_code():
           "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
           ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
-          "s_mov_b64 exec, %s" % sp(S_ALIVE)]
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          # a compiled program (s7 bit 1) starts at the head of its code area and sets up the
+          # registers it reads itself (packet address, r1, r10, zeroes: asm_cc.cpp prologue)
+          "s_bitcmp1_b32 s7, 1",
+          "s_cbranch_scc0 .Lgs_interp"] + goto("ebpf_jit_area") + [
+          ".Lgs_interp:"]
+    # r0, r2..r9 start at zero
     for r in range(0, 20, 2):
         if r != 2:
             L.append("v_mov_b64 v[%d:%d], 0" % (r, r + 1))
@@ -1074,8 +1125,6 @@ def common_group_code():
           "v_add_u32 v20, %s, v%d" % (s(S_STKSTRIDE), V_STK),
           "v_mov_b32 v21, %s" % s(S_SHARED + 1),
           "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),
-          "s_bitcmp1_b32 s7, 1",
-          "s_cselect_b32 %s, ebpf_jit_area-.Lcb, %s" % (s(S_T0), s(S_T0)),
           "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
     # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
     L += [".Lfinish:"] + store_prev_results("f", True) + [
@@ -1214,15 +1263,15 @@ def jit_templates():
     L = [".p2align 2", "ebpf_jit_templates:"]
     for r in range(10, 16):
         L += [".Ljt_mov_s%d:" % r, "s_mov_b32 s%d, 0x5eed5eed" % r]
-    # conditional tail, short form: all lanes taken -> branch; none -> fall through; mixed ->
-    # park the taken lanes at the taken block (v41 = its code offset), continue not-taken
+    # conditional tail, short form: no lane taken -> fall through (the common uniform case costs
+    # two scalar instructions); all taken -> branch; mixed -> park the taken lanes at the taken
+    # block (v41 = its code offset), continue with the rest
     L += [".Ljt_cs:",
           "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+          "s_cbranch_scc0 .Ljt_cs_end",
           "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
           ".Ljt_cs_br:",
           "s_cbranch_scc1 .Ljt_cs_br",
-          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
-          "s_cbranch_scc1 .Ljt_cs_end",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
           "s_mov_b64 exec, %s" % sp(S_MASK),
           ".Ljt_cs_vt:",
@@ -1232,6 +1281,7 @@ def jit_templates():
     # long form (taken block beyond a 16-bit branch)
     L += [".Ljt_cl:",
           "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+          "s_cbranch_scc0 .Ljt_cl_end",
           "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
           "s_cbranch_scc0 .Ljt_cl_skip",
           ".Ljt_cl_lit:",
@@ -1239,8 +1289,6 @@ def jit_templates():
           "s_addc_u32 %s, %s, 0" % (s(S_JUNK + 1), s(S_CB + 1)),
           "s_setpc_b64 %s" % sp(S_JUNK),
           ".Ljt_cl_skip:",
-          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
-          "s_cbranch_scc1 .Ljt_cl_end",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
           "s_mov_b64 exec, %s" % sp(S_MASK),
           ".Ljt_cl_vt:",
@@ -1258,7 +1306,7 @@ def jit_templates():
     names = [".Ljt_mov_s%d" % r for r in range(10, 16)] + [
         ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
-        ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", "ebpf_jit_area"]
+        ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
     return L

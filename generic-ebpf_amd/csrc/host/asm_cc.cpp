@@ -1,33 +1,46 @@
 // asm_cc.cpp — optimising gfx950 code generation for compiled programs (variant 0).
 //
-// asm_jit.cpp lays a lowered program (asm_lower) out as straight-line code and, for each entry,
-// used to copy the interpreter's handler body verbatim.  Handler bodies are written for any
-// register contents, so they pay for 64-bit generality everywhere: a 32-bit result re-zeroes
-// its high half, a 64-bit multiply by a 32-bit constant multiplies by a zero high word, a
-// compare of a loaded byte is a 64-bit compare against an SGPR pair set by two scalar moves.
+// asm_jit.cpp lays a lowered program (asm_lower) out as straight-line code; for each entry it
+// can copy the interpreter's handler body verbatim.  Handler bodies are written for any register
+// contents, so they pay for 64-bit generality everywhere: a 32-bit result re-zeroes its high
+// half, a 64-bit multiply by a 32-bit constant multiplies by a zero high word, a compare of a
+// loaded byte is a 64-bit compare against an SGPR pair set by two scalar moves, a map lookup
+// re-reads its key from the stack and re-checks the result's range at every use.
 //
-// Here a forward dataflow over the state tree tracks, for every eBPF register, whether it holds
-// a known constant and how many of its leading bits are known zero (the translator's tree gives
-// every entry exactly one predecessor, so the facts are exact per path; taken/not-taken edges of
-// compares against constants refine them).  With those facts the hot families are emitted as
-// hand-encoded gfx950 instructions instead of the generic body:
+// Here two forward passes and one backward pass over the state tree (the translator gives every
+// entry one predecessor, so facts are exact per path) compile the hot families to hand-encoded
+// gfx950 instructions instead:
+//   facts (forward): per eBPF register, a known constant, the number of known leading zero bits,
+//     non-NULL-ness, and for a map lookup result the map and the register holding its index;
+//     per stack word, the register whose low bytes it holds (store-to-load forwarding);
+//     compares against constants refine the facts on their taken / fall-through edges;
+//   liveness (backward): pure operations (ALU, byte swaps, staged packet and stack loads,
+//     lookups with a statically resolved map) whose result no path reads emit nothing, and the
+//     group's register zeroing covers only the registers the program reads before writing;
+//   emission (forward):
 //   * constants fold (both operands known: a move of the result);
 //   * high halves known zero are neither recomputed nor re-zeroed;
 //   * 64-bit AND/OR/XOR/shift by constants become 32-bit operations where a half is unchanged
 //     or zero, shifts by >= 32 become moves;
-//   * MUL by a constant drops the partial products of known-zero words (3 → 2 or 1 quarter-rate
-//     multiplies), multiplies by powers of two become shifts;
+//   * MUL by a constant drops the partial products of known-zero words, multiplies by powers
+//     of two become shifts;
 //   * compares of values below 2^32 against constants below 2^32 are single VOPC e32
-//     instructions with the constant as a literal (no scalar moves); statically decided
-//     compares become VCC = EXEC or 0;
+//     instructions with the constant as a literal; statically decided compares (including
+//     NULL checks of lookups that cannot fail) become VCC = EXEC or 0;
 //   * a staged packet load followed by BE16/BE32 of the same register is one v_perm_b32 that
-//     picks the bytes in network order straight from the staged packet registers.
-// Everything else (memory through pointers, lookups, division, exits, faults) still copies the
-// interpreter's handler body, so semantics there are unchanged by construction.
+//     picks the bytes in network order straight from the staged packet registers;
+//   * stack stores/loads at known offsets are single LDS instructions with the offset folded in;
+//     a load of a word stored from a register that is unchanged since reads the register;
+//   * an array-map lookup whose key comes from a register proven below max_entries cannot
+//     return NULL: r0 = base + key * value_size (one v_mad_u64_u32, or nothing if r0 is only
+//     dereferenced), and loads through it read the workgroup's LDS copy of the map at
+//     lds_off + key * value_size + off with no range check.
+// Everything else (memory through unknown pointers, generic lookups, division, generic exits,
+// faults) still copies the interpreter's handler body, so semantics there are unchanged.
 //
-// Encodings: VOP1/VOP2/VOPC (e32, literal allowed in src0), VOP3 (no literal on gfx9), SOP1.
-// Field layouts and opcodes were taken from llvm-mc -show-encoding for gfx950;
-// tests/test_compile.py disassembles the generated code to check them.
+// Encodings: VOP1/VOP2/VOPC (e32, literal allowed in src0), VOP3 (no literal on gfx9), SOP1,
+// SOP2, DS.  Field layouts and opcodes are from llvm-mc -show-encoding for gfx950;
+// tests/test_compile.py checks decoded forms.
 #include "asm_handlers.h"
 #include "internal.h"
 
@@ -41,27 +54,34 @@ enum : uint32_t {
 };
 // VOP2 opcodes (bits 30:25)
 enum : uint32_t {
-	V2_CNDMASK = 0x00, V2_LSHRREV_B32 = 0x10, V2_ASHRREV_I32 = 0x11, V2_LSHLREV_B32 = 0x12,
-	V2_AND = 0x13, V2_OR = 0x14, V2_XOR = 0x15, V2_ADD_CO = 0x19, V2_SUB_CO = 0x1a,
-	V2_ADDC_CO = 0x1c, V2_SUBB_CO = 0x1d, V2_ADD_U32 = 0x34, V2_SUB_U32 = 0x35, V2_SUBREV_U32 = 0x36,
+	V2_LSHRREV_B32 = 0x10, V2_LSHLREV_B32 = 0x12, V2_AND = 0x13, V2_OR = 0x14, V2_XOR = 0x15,
+	V2_ADD_U32 = 0x34, V2_SUB_U32 = 0x35, V2_SUBREV_U32 = 0x36,
 };
 // VOP1 opcodes (bits 16:9)
-enum : uint32_t { V1_MOV_B32 = 0x01, V1_NOT_B32 = 0x2b, V1_MOV_B64 = 0x38 };
+enum : uint32_t { V1_MOV_B32 = 0x01, V1_MOV_B64 = 0x38 };
 // VOP3 opcodes (bits 25:16)
 enum : uint32_t {
-	V3_BFE_U32 = 0x1c8, V3_ALIGNBYTE = 0x1cf, V3_MAD_U64_U32 = 0x1e8, V3_PERM_B32 = 0x1ed,
-	V3_ADD3_U32 = 0x1ff, V3_LSHL_ADD_U64 = 0x208, V3_MUL_LO_U32 = 0x285, V3_LSHLREV_B64 = 0x28f,
-	V3_LSHRREV_B64 = 0x290,
+	V3_MAD_U32_U24 = 0x1c3, V3_BFE_U32 = 0x1c8, V3_ALIGNBYTE = 0x1cf, V3_MAD_U64_U32 = 0x1e8,
+	V3_PERM_B32 = 0x1ed, V3_ADD3_U32 = 0x1ff, V3_LSHL_ADD_U64 = 0x208, V3_MUL_LO_U32 = 0x285,
+	V3_LSHLREV_B64 = 0x28f, V3_LSHRREV_B64 = 0x290,
+};
+// DS opcodes (bits 24:17)
+enum : uint32_t {
+	DS_WRITE_B32 = 0x0d, DS_WRITE2_B32 = 0x0e, DS_WRITE_B8 = 0x1e, DS_WRITE_B16 = 0x1f,
+	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c,
 };
 // VOPC compare codes: base + {lt 1, eq 2, le 3, gt 4, ne 5, ge 6}
-enum : uint32_t { VC_I32 = 0xc0, VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
+enum : uint32_t { VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
 enum { P_LT = 1, P_EQ = 2, P_LE = 3, P_GT = 4, P_NE = 5, P_GE = 6 };
+const uint32_t S_WAITCNT_LGKM0 = 0xbf8cc07fu;
 const int S_JUNK = 60; // s[60:61]: carry-out sink of v_mad_u64_u32 (gen_interp.py S_JUNK)
-const int T0 = 46, T1 = 47, T2 = 48, T3 = 49; // handler temporaries (gen_interp.py H)
-const int PKT0 = 22;                          // staged packet dwords v22..v37
+const int S_BYTES = 57, S_CB = 4;              // gen_interp.py S_BYTES, S_CB
+const int T0 = 46, T1 = 47, T2 = 48, T3 = 49;  // handler temporaries (gen_interp.py H)
+const int PKT0 = 22;                           // staged packet dwords v22..v37
+const int V_STK = 42;                          // lane stack bottom (LDS byte address)
+const int V_RES = 44;                          // v[44:45]: r0 of retiring lanes
 const int V_SEL = 63;                          // v63 = 0x00010203 (byte reversal selector)
 
-// a source operand: 9-bit code, plus the literal when code == SRC_LIT
 struct opnd {
 	uint32_t code;
 	uint32_t lit = 0;
@@ -87,7 +107,7 @@ vreg(int n)
 	return opnd{VGPR0 + (uint32_t)n};
 }
 
-// 32-bit constant for an e32 src0: inline constant or literal
+// 32-bit constant for an e32 src0 / SOP source: inline constant or literal
 opnd
 k32(uint32_t v)
 {
@@ -130,15 +150,33 @@ struct enc {
 		w((0x34u << 26) | (op << 16) | ((uint32_t)sdst << 8) | (uint32_t)vdst);
 		w(s0 | (s1 << 9) | (s2 << 18));
 	}
-	// s_mov_b64 vcc, exec | 0
-	void vcc_all(bool all) { w(0xbe800000u | (SRC_VCC << 16) | (0x01u << 8) | (all ? SRC_EXEC : 128u)); }
+	void ds(uint32_t op, int addr, int data0, int data1, int vdst, uint32_t off0, uint32_t off1 = 0)
+	{
+		w((0x36u << 26) | (op << 17) | (off1 << 8) | off0);
+		w((uint32_t)addr | ((uint32_t)data0 << 8) | ((uint32_t)data1 << 16) | ((uint32_t)vdst << 24));
+	}
+	void sop1(uint32_t op, int sdst, opnd s0)
+	{
+		w(0xbe800000u | ((uint32_t)sdst << 16) | (op << 8) | s0.code);
+		lit(s0);
+	}
+	void sop2(uint32_t op, int sdst, opnd s0, opnd s1)
+	{
+		w(0x80000000u | (op << 23) | ((uint32_t)sdst << 16) | (s1.code << 8) | s0.code);
+		lit(s0);
+		lit(s1);
+	}
+	void wait_lgkm() { w(S_WAITCNT_LGKM0); }
 };
 
 // ---------------------------------------------------------------- facts
 struct rf {
-	bool c = false;  // known constant
+	bool c = false;   // known constant
 	uint64_t v = 0;
-	uint8_t lz = 0;  // known leading zero bits (64 if c && v == 0)
+	uint8_t lz = 0;   // known leading zero bits (64 if c && v == 0)
+	bool nz = false;  // known non-zero (a lookup that cannot fail)
+	int8_t mp = -1;   // >= 0: a pointer to map mp's value number u32(r[mreg]) (+0)
+	int8_t mreg = -1;
 };
 
 inline int
@@ -154,6 +192,7 @@ kconst(uint64_t v)
 	r.c = true;
 	r.v = v;
 	r.lz = (uint8_t)clz64(v);
+	r.nz = v != 0;
 	return r;
 }
 
@@ -171,8 +210,68 @@ bits_of(const rf &r)
 	return 64 - r.lz;
 }
 
+// a stack word whose bytes are the low `size` bytes of register `reg` (unchanged since)
+struct sslot {
+	uint32_t off; // LDS offset from the lane's stack bottom (the lowered operand)
+	uint8_t size;
+	int8_t reg;
+};
+
 struct facts {
 	rf r[AH_NREGS];
+	bool pv[AH_NREGS] = {}; // the register's VGPRs hold its value (false: a dead write skipped)
+	sslot st[8];
+	uint8_t nst = 0;
+
+	void def(int d, const rf &v, bool phys = true)
+	{
+		r[d] = v;
+		pv[d] = phys;
+		uint8_t k = 0;
+		for (uint8_t i = 0; i < nst; i++)
+			if (st[i].reg != d)
+				st[k++] = st[i];
+		nst = k;
+		for (int q = 0; q < AH_NREGS; q++)
+			if (q != d && r[q].mreg == d) {
+				r[q].mp = -1;
+				r[q].mreg = -1;
+			}
+	}
+	void store(uint32_t off, int size, int reg)
+	{
+		uint8_t k = 0;
+		for (uint8_t i = 0; i < nst; i++)
+			if (st[i].off + st[i].size <= off || off + (uint32_t)size <= st[i].off)
+				st[k++] = st[i];
+		nst = k;
+		if (reg >= 0 && nst < 8)
+			st[nst++] = sslot{off, (uint8_t)size, (int8_t)reg};
+	}
+	bool nofwd = false;
+	const sslot *slot(uint32_t off, int size) const
+	{
+		if (nofwd)
+			return nullptr;
+		for (uint8_t i = 0; i < nst; i++)
+			if (st[i].off == off && st[i].size >= size)
+				return &st[i];
+		return nullptr;
+	}
+};
+
+// EBPF_CC_OFF (debugging / A-B): bit 0 no dead-code removal, 1 zero every register at the start,
+// 2 no stack forwarding, 3 no lookup specialisation, 4 no static branches, 5 no known-r0 exits
+unsigned
+cc_off()
+{
+	const char *e = getenv("EBPF_CC_OFF");
+	return e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
+}
+
+struct mapinfo {
+	uint64_t dev_base;
+	uint32_t value_size, max_entries, lds_off;
 };
 
 // ---------------------------------------------------------------- per-entry emission
@@ -180,31 +279,29 @@ struct emitter {
 	cc_block &blk;
 	enc E;
 	facts &f;
-	int next_s = 0; // constant SGPR allocation: s10/s11 (pair), s13, s14, s15
+	const std::vector<mapinfo> &maps;
+	uint16_t used = 0; // registers this entry's code reads
 
-	emitter(cc_block &b, facts &fa) : blk(b), E{b.body}, f(fa) {}
+	emitter(cc_block &b, facts &fa, const std::vector<mapinfo> &m) : blk(b), E{b.body}, f(fa), maps(m) {}
 
 	static int L(int r) { return 2 * r; }
 	static int Hi(int r) { return 2 * r + 1; }
 	bool hz(int r) const { return f.r[r].lz >= 32; }
+	void use(int r) { used |= (uint16_t)(1u << r); }
 
 	// an SGPR holding the 32-bit constant v for this body (s13, s14, s15)
 	uint32_t sconst(uint32_t v)
 	{
 		static const int regs[3] = {13, 14, 15};
-		for (int i = 0; i < 3; i++) {
-			const int r = regs[i];
+		for (int r : regs)
 			if ((blk.reads & (1u << (r - 10))) && blk.sval[r - 10] == v)
 				return (uint32_t)r;
-		}
-		for (int i = 0; i < 3; i++) {
-			const int r = regs[i];
+		for (int r : regs)
 			if (!(blk.reads & (1u << (r - 10)))) {
 				blk.reads |= (uint8_t)(1u << (r - 10));
 				blk.sval[r - 10] = v;
 				return (uint32_t)r;
 			}
-		}
 		return UINT32_MAX; // never: no body needs four constants
 	}
 	// the SGPR pair s[10:11] holding the 64-bit constant v
@@ -215,7 +312,6 @@ struct emitter {
 		blk.sval[1] = (uint32_t)(v >> 32);
 		return 10;
 	}
-	// VOP3 source for a 32-bit constant
 	uint32_t c3(uint32_t v)
 	{
 		uint32_t c;
@@ -223,7 +319,6 @@ struct emitter {
 			return c;
 		return sconst(v);
 	}
-	// VOP3 / VOPC source for a 64-bit constant
 	uint32_t c64(uint64_t v)
 	{
 		uint32_t c;
@@ -233,60 +328,76 @@ struct emitter {
 	}
 
 	void mov32(int vd, uint32_t v) { E.vop1(V1_MOV_B32, vd, k32(v)); }
+	// hi(d) = 0 after a write of lo(d) (d's previous value read or not)
 	void hi0(int d)
 	{
-		if (!hz(d))
+		if (!(f.pv[d] && hz(d)))
 			mov32(Hi(d), 0);
 	}
-	// d = v (a constant), skipping halves already known to hold it
+	// d = v (a constant), skipping halves the registers already hold
 	void mov64(int d, uint64_t v)
 	{
 		const rf &o = f.r[d];
+		const bool pv = f.pv[d];
 		const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-		if (!(o.c && (uint32_t)o.v == lo))
+		if (!(pv && o.c && (uint32_t)o.v == lo))
 			mov32(L(d), lo);
-		if (!((o.c && (uint32_t)(o.v >> 32) == hi) || (hi == 0 && hz(d))))
+		if (!(pv && ((o.c && (uint32_t)(o.v >> 32) == hi) || (hi == 0 && hz(d)))))
 			mov32(Hi(d), hi);
-		f.r[d] = kconst(v);
+		f.def(d, kconst(v));
 	}
 	// d = s (registers)
 	void copy64(int d, int s)
 	{
-		if (d == s)
+		if (d == s) {
+			use(s);
 			return;
+		}
 		if (f.r[s].c) {
 			mov64(d, f.r[s].v);
 			return;
 		}
+		use(s);
 		if (hz(s)) {
 			E.vop1(V1_MOV_B32, L(d), vreg(L(s)));
 			hi0(d);
 		} else {
 			E.vop1(V1_MOV_B64, L(d), vreg(L(s)));
 		}
-		f.r[d] = f.r[s];
+		rf v = f.r[s];
+		v.mp = -1; // (keep it simple: provenance stays with the original)
+		v.mreg = -1;
+		f.def(d, v);
 	}
 
 	// ---- ALU64 with a constant operand (d op= K)
 	void add64i(int d, uint64_t K)
 	{
-		rf &x = f.r[d];
-		if (K == 0)
+		const rf x = f.r[d];
+		if (K == 0) {
+			use(d); // (a no-op passes d's value through)
 			return;
+		}
 		if (x.c) {
 			mov64(d, x.v + K);
 			return;
 		}
+		use(d);
 		E.vop3(V3_LSHL_ADD_U64, L(d), c64(K), 128, VGPR0 + L(d));
-		x = (int64_t)K >= 0 ? kbits(std::max(bits_of(x), 64 - clz64(K)) + 1) : rf();
+		f.def(d, (int64_t)K >= 0 ? kbits(std::max(bits_of(x), 64 - clz64(K)) + 1) : rf());
 	}
 	void or64i(int d, uint64_t K)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (x.c) {
 			mov64(d, x.v | K);
 			return;
 		}
+		if (K == 0) {
+			use(d);
+			return;
+		}
+		use(d);
 		const uint32_t lo = (uint32_t)K, hi = (uint32_t)(K >> 32);
 		if (lo)
 			E.vop2(V2_OR, L(d), k32(lo), L(d));
@@ -294,29 +405,45 @@ struct emitter {
 			mov32(Hi(d), hi);
 		else if (hi)
 			E.vop2(V2_OR, Hi(d), k32(hi), Hi(d));
-		x = kbits(std::max(bits_of(x), 64 - clz64(K)));
+		rf v = kbits(std::max(bits_of(x), 64 - clz64(K)));
+		v.nz = true;
+		f.def(d, v);
 	}
 	void xor64i(int d, uint64_t K)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (x.c) {
 			mov64(d, x.v ^ K);
 			return;
 		}
+		if (K == 0) {
+			use(d);
+			return;
+		}
+		use(d);
 		const uint32_t lo = (uint32_t)K, hi = (uint32_t)(K >> 32);
 		if (lo)
 			E.vop2(V2_XOR, L(d), k32(lo), L(d));
 		if (hi)
 			E.vop2(V2_XOR, Hi(d), k32(hi), Hi(d));
-		x = kbits(std::max(bits_of(x), 64 - clz64(K)));
+		f.def(d, kbits(std::max(bits_of(x), 64 - clz64(K))));
 	}
 	void and64i(int d, uint64_t K)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (x.c) {
 			mov64(d, x.v & K);
 			return;
 		}
+		if (K == ~0ull) {
+			use(d);
+			return;
+		}
+		if (K == 0) {
+			mov64(d, 0);
+			return;
+		}
+		use(d);
 		const uint32_t lo = (uint32_t)K, hi = (uint32_t)(K >> 32);
 		if (lo == 0)
 			mov32(L(d), 0);
@@ -326,18 +453,21 @@ struct emitter {
 			hi0(d);
 		else if (hi != 0xffffffffu && !hz(d))
 			E.vop2(V2_AND, Hi(d), k32(hi), Hi(d));
-		x = kbits(std::min(bits_of(x), 64 - clz64(K)));
+		f.def(d, kbits(std::min(bits_of(x), 64 - clz64(K))));
 	}
 	void lsh64i(int d, uint32_t c)
 	{
 		c &= 63;
-		rf &x = f.r[d];
-		if (c == 0)
+		const rf x = f.r[d];
+		if (c == 0) {
+			use(d);
 			return;
+		}
 		if (x.c) {
 			mov64(d, x.v << c);
 			return;
 		}
+		use(d);
 		const int nb = std::min(64, bits_of(x) + (int)c);
 		if (c >= 32) {
 			if (c == 32)
@@ -350,14 +480,16 @@ struct emitter {
 		} else {
 			E.vop3(V3_LSHLREV_B64, L(d), 128 + c, VGPR0 + L(d), 0);
 		}
-		x = kbits(nb);
+		f.def(d, kbits(nb));
 	}
 	void rsh64i(int d, uint32_t c)
 	{
 		c &= 63;
-		rf &x = f.r[d];
-		if (c == 0)
+		const rf x = f.r[d];
+		if (c == 0) {
+			use(d);
 			return;
+		}
 		if (x.c) {
 			mov64(d, x.v >> c);
 			return;
@@ -367,22 +499,23 @@ struct emitter {
 			mov64(d, 0);
 			return;
 		}
+		use(d);
 		if (c >= 32) {
 			if (c == 32)
 				E.vop1(V1_MOV_B32, L(d), vreg(Hi(d)));
 			else
 				E.vop2(V2_LSHRREV_B32, L(d), opnd{128 + (c - 32)}, Hi(d));
-			hi0(d);
+			mov32(Hi(d), 0);
 		} else if (hz(d)) {
 			E.vop2(V2_LSHRREV_B32, L(d), opnd{128 + c}, L(d));
 		} else {
 			E.vop3(V3_LSHRREV_B64, L(d), 128 + c, VGPR0 + L(d), 0);
 		}
-		f.r[d] = kbits(nb);
+		f.def(d, kbits(nb));
 	}
 	void mul64i(int d, uint64_t K)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (x.c) {
 			mov64(d, x.v * K);
 			return;
@@ -391,12 +524,15 @@ struct emitter {
 			mov64(d, 0);
 			return;
 		}
-		if (K == 1)
+		if (K == 1) {
+			use(d);
 			return;
+		}
 		if ((K & (K - 1)) == 0) {
 			lsh64i(d, (uint32_t)__builtin_ctzll(K));
 			return;
 		}
+		use(d);
 		const int nb = std::min(64, bits_of(x) + 64 - clz64(K));
 		const uint32_t lo = (uint32_t)K, hi = (uint32_t)(K >> 32);
 		const uint32_t klo = c3(lo);
@@ -421,13 +557,13 @@ struct emitter {
 			E.vop3(V3_ADD3_U32, Hi(d), VGPR0 + T1, VGPR0 + T2, VGPR0 + T3);
 			E.vop1(V1_MOV_B32, L(d), vreg(T0));
 		}
-		x = kbits(nb);
+		f.def(d, kbits(nb));
 	}
 
 	// ---- ALU32 (lo op= k; hi = 0)
 	bool alu32i(int fam, int d, uint32_t k)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		const uint32_t a = (uint32_t)x.v;
 		const int ab = std::min(32, bits_of(x));
 		if (x.c || fam == AHF_A32I_MOV) {
@@ -491,8 +627,9 @@ struct emitter {
 		default:
 			return false;
 		}
+		use(d);
 		hi0(d);
-		x = kbits(nb);
+		f.def(d, kbits(nb));
 		return true;
 	}
 	bool alu32r(int fam, int d, int s)
@@ -503,7 +640,7 @@ struct emitter {
 						   AHF_A32I_MOV};
 			return alu32i(to_i[fam - AHF_A32R_ADD], d, (uint32_t)f.r[s].v);
 		}
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		const int ab = std::min(32, bits_of(x)), sb = std::min(32, bits_of(f.r[s]));
 		int nb = 32;
 		switch (fam) {
@@ -518,21 +655,24 @@ struct emitter {
 		case AHF_A32R_MOV: E.vop1(V1_MOV_B32, L(d), vreg(L(s))); nb = sb; break;
 		default: return false;
 		}
+		use(s);
+		if (fam != AHF_A32R_MOV)
+			use(d);
 		if (d == s && (fam == AHF_A32R_SUB || fam == AHF_A32R_XOR))
 			nb = 0;
 		hi0(d);
-		x = kbits(nb);
+		f.def(d, kbits(nb));
 		return true;
 	}
 	bool alu64r(int fam, int d, int s)
 	{
 		const rf xs = f.r[s];
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (d == s) {
 			switch (fam) {
 			case AHF_A64R_ADD: lsh64i(d, 1); return true;
 			case AHF_A64R_SUB: case AHF_A64R_XOR: mov64(d, 0); return true;
-			case AHF_A64R_OR: case AHF_A64R_AND: return true;
+			case AHF_A64R_OR: case AHF_A64R_AND: use(d); return true;
 			default: return false;
 			}
 		}
@@ -555,25 +695,31 @@ struct emitter {
 		}
 		switch (fam) {
 		case AHF_A64R_ADD:
+			use(d);
+			use(s);
 			E.vop3(V3_LSHL_ADD_U64, L(d), VGPR0 + L(s), 128, VGPR0 + L(d));
-			x = kbits(std::min(64, std::max(bits_of(x), bits_of(xs)) + 1));
+			f.def(d, kbits(std::min(64, std::max(bits_of(x), bits_of(xs)) + 1)));
 			return true;
 		case AHF_A64R_OR:
 		case AHF_A64R_XOR: {
+			use(d);
+			use(s);
 			const uint32_t op = fam == AHF_A64R_OR ? V2_OR : V2_XOR;
 			E.vop2(op, L(d), vreg(L(s)), L(d));
 			if (!hz(s))
 				E.vop2(op, Hi(d), vreg(Hi(s)), Hi(d));
-			x = kbits(std::max(bits_of(x), bits_of(xs)));
+			f.def(d, kbits(std::max(bits_of(x), bits_of(xs))));
 			return true;
 		}
 		case AHF_A64R_AND:
+			use(d);
+			use(s);
 			E.vop2(V2_AND, L(d), vreg(L(s)), L(d));
 			if (hz(s))
 				hi0(d);
 			else if (!hz(d))
 				E.vop2(V2_AND, Hi(d), vreg(Hi(s)), Hi(d));
-			x = kbits(std::min(bits_of(x), bits_of(xs)));
+			f.def(d, kbits(std::min(bits_of(x), bits_of(xs))));
 			return true;
 		default:
 			return false;
@@ -583,15 +729,16 @@ struct emitter {
 	// ---- byte swaps (BE16/BE32 zero-extend; LE is lowered to AND)
 	bool bswap(int fam, int d)
 	{
-		rf &x = f.r[d];
+		const rf x = f.r[d];
 		if (fam == AHF_BSWAP16) {
 			if (x.c) {
 				mov64(d, __builtin_bswap16((uint16_t)x.v));
 				return true;
 			}
+			use(d);
 			E.vop3(V3_PERM_B32, L(d), 128, VGPR0 + L(d), sconst(0x0c0c0001u));
 			hi0(d);
-			x = kbits(16);
+			f.def(d, kbits(16));
 			return true;
 		}
 		if (fam == AHF_BSWAP32) {
@@ -599,9 +746,10 @@ struct emitter {
 				mov64(d, __builtin_bswap32((uint32_t)x.v));
 				return true;
 			}
+			use(d);
 			E.vop3(V3_PERM_B32, L(d), 128, VGPR0 + L(d), VGPR0 + V_SEL);
 			hi0(d);
-			x = kbits(32);
+			f.def(d, kbits(32));
 			return true;
 		}
 		return false;
@@ -624,7 +772,7 @@ struct emitter {
 			const uint32_t sc = sel == 0x00010203u ? VGPR0 + V_SEL : sconst(sel);
 			E.vop3(V3_PERM_B32, L(d), VGPR0 + nx, VGPR0 + lo, sc);
 			hi0(d);
-			f.r[d] = kbits(8 * std::min(z, swap_bytes));
+			f.def(d, kbits(8 * std::min(z, swap_bytes)));
 			return;
 		}
 		if (z == 1) {
@@ -651,11 +799,126 @@ struct emitter {
 				E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + lo + 1, VGPR0 + lo, 128 + sh);
 				E.vop3(V3_ALIGNBYTE, Hi(d), VGPR0 + lo + 2, VGPR0 + lo + 1, 128 + sh);
 			}
-			f.r[d] = rf();
+			f.def(d, rf());
 			return;
 		}
 		hi0(d);
-		f.r[d] = kbits(8 * z);
+		f.def(d, kbits(8 * z));
+	}
+
+	// ---- stack accesses at a known LDS offset `o` from the lane's stack bottom
+	void stxstk(int z, int r, uint32_t o)
+	{
+		use(r);
+		if (z == 8)
+			E.ds(DS_WRITE2_B32, V_STK, L(r), Hi(r), 0, o / 4, o / 4 + 1);
+		else
+			E.ds(z == 4 ? DS_WRITE_B32 : z == 2 ? DS_WRITE_B16 : DS_WRITE_B8, V_STK, L(r), 0, 0, o);
+		f.store(o, z, r);
+	}
+	// low z bytes of register s into d
+	void low_bytes(int d, int s, int z)
+	{
+		if (z == 8) {
+			copy64(d, s);
+			return;
+		}
+		const rf xs = f.r[s];
+		if (xs.c) {
+			mov64(d, z == 4 ? (uint32_t)xs.v : xs.v & ((1ull << (8 * z)) - 1));
+			return;
+		}
+		use(s);
+		const int sb = std::min(bits_of(xs), 8 * z);
+		if (bits_of(xs) <= 8 * z)
+			E.vop1(V1_MOV_B32, L(d), vreg(L(s)));
+		else if (z == 4)
+			E.vop1(V1_MOV_B32, L(d), vreg(L(s)));
+		else
+			E.vop2(V2_AND, L(d), k32(z == 1 ? 0xffu : 0xffffu), L(s));
+		hi0(d);
+		f.def(d, kbits(sb));
+	}
+	void ldxstk(int z, int d, uint32_t o)
+	{
+		if (const sslot *sl = f.slot(o, z)) {
+			low_bytes(d, sl->reg, z);
+			return;
+		}
+		if (z == 8) {
+			E.ds(DS_READ2_B32, V_STK, 0, 0, L(d), o / 4, o / 4 + 1);
+			E.wait_lgkm();
+			f.def(d, rf());
+			return;
+		}
+		E.ds(z == 4 ? DS_READ_B32 : z == 2 ? DS_READ_U16 : DS_READ_U8, V_STK, 0, 0, L(d), o);
+		E.wait_lgkm();
+		hi0(d);
+		f.def(d, kbits(8 * z));
+	}
+
+	// ---- array-map lookup resolved to map `mi` with the key at stack offset `o`: specialised
+	// when the key is a register proven below max_entries (the lookup cannot return NULL)
+	bool lookup_stk(int mi, uint32_t o)
+	{
+		if (mi < 0)
+			return false;
+		const mapinfo &m = maps[mi];
+		const sslot *sl = f.slot(o, 4);
+		if (!sl)
+			return false;
+		const int R = sl->reg;
+		const rf xr = f.r[R];
+		const uint64_t kmax = xr.c ? (uint32_t)xr.v : (bits_of(xr) >= 32 ? 0xffffffffull : (1ull << bits_of(xr)) - 1);
+		if (kmax >= m.max_entries || m.max_entries > (1u << 24))
+			return false;
+		use(R);
+		E.vop3(V3_MAD_U64_U32, L(0), VGPR0 + L(R), c3(m.value_size), spair(m.dev_base), S_JUNK);
+		rf v;
+		v.nz = true;
+		v.mp = (int8_t)mi;
+		v.mreg = (int8_t)R;
+		f.def(0, v);
+		return true;
+	}
+	// LDXMAP through a pointer with known map and index register: the LDS copy, no check
+	bool ldxmap(int z, int d, int s, uint64_t imm)
+	{
+		const rf xs = f.r[s];
+		if (xs.mp < 0 || xs.mreg < 0 || !xs.nz)
+			return false;
+		const mapinfo &m = maps[xs.mp];
+		if (m.lds_off == ~0u)
+			return false;
+		const int64_t c = (int64_t)(m.dev_base - imm); // the access offset within the value
+		if (c < 0 || c + z > (int64_t)m.value_size)
+			return false;
+		const int R = xs.mreg;
+		use(R);
+		const uint32_t base = m.lds_off + (uint32_t)c;
+		E.vop3(V3_MAD_U32_U24, T0, VGPR0 + L(R), c3(m.value_size), c3(base));
+		if (z == 8) {
+			E.ds(DS_READ2_B32, T0, 0, 0, L(d), 0, 1);
+			E.wait_lgkm();
+			f.def(d, rf());
+			return true;
+		}
+		E.ds(z == 4 ? DS_READ_B32 : z == 2 ? DS_READ_U16 : DS_READ_U8, T0, 0, 0, L(d), 0);
+		E.wait_lgkm();
+		hi0(d);
+		f.def(d, kbits(8 * z));
+		return true;
+	}
+
+	// ---- EXIT with r0 known: result and verdict bin set here, then .Lr_exit_k (gen_interp.py)
+	void exit_known(uint64_t r0, uint32_t exitk_off)
+	{
+		mov32(V_RES, (uint32_t)r0);
+		mov32(V_RES + 1, (uint32_t)(r0 >> 32));
+		E.sop1(0x00, S_BYTES, k32(r0 < 255 ? (uint32_t)r0 : 255u));   // s_mov_b32
+		E.sop2(0x00, S_JUNK, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, exitk_off}); // s_add_u32
+		E.sop2(0x04, S_JUNK + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});     // s_addc_u32
+		E.sop1(0x1d, 0, opnd{(uint32_t)S_JUNK});                           // s_setpc_b64
 	}
 
 	// ---- conditional jumps: VCC = lanes taking the branch (the caller appends the tail)
@@ -677,7 +940,6 @@ struct emitter {
 		default: return (a & b) != 0;
 		}
 	}
-	// predicate of `d c x`, and of `x c' d` (operands swapped)
 	static int pred(int c) { static const int p[] = {P_EQ, P_NE, P_GT, P_GE, P_LT, P_LE, P_GT, P_GE, P_LT, P_LE}; return p[c]; }
 	static int swapped(int p)
 	{
@@ -689,17 +951,32 @@ struct emitter {
 		default: return p;
 		}
 	}
+	// a compare decided at compile time: no code, the layout falls through or jumps
+	unsigned off = 0;
+	void decided(bool taken)
+	{
+		if (off & 16) { // s_mov_b64 vcc, exec | 0
+			E.sop1(0x01, (int)SRC_VCC, opnd{taken ? SRC_EXEC : 128u});
+			return;
+		}
+		blk.sdir = taken ? 1 : 0;
+	}
 	void cond_imm(int c, int d, uint64_t K)
 	{
 		const rf &x = f.r[d];
 		if (x.c) {
-			E.vcc_all(eval(c, x.v, K));
+			decided(eval(c, x.v, K));
 			return;
 		}
+		if (K == 0 && x.nz && (c == 0 || c == 1)) { // NULL check of a lookup that cannot fail
+			decided(c == 1);
+			return;
+		}
+		use(d);
 		if (c == 10) { // JSET
 			const uint32_t lo = (uint32_t)K, hi = hz(d) ? 0u : (uint32_t)(K >> 32);
 			if (!lo && !hi) {
-				E.vcc_all(false);
+				decided(false);
 				return;
 			}
 			if (!hi) {
@@ -720,12 +997,12 @@ struct emitter {
 				switch (c) {
 				case 0: r = false; break;
 				case 1: r = true; break;
-				case 2: case 3: r = false; break;       // d > K (unsigned): K >= 2^32 > d
+				case 2: case 3: r = false; break;
 				case 4: case 5: r = true; break;
-				case 6: case 7: r = kneg; break;        // d > K (signed)
-				default: r = !kneg; break;              // d < K (signed)
+				case 6: case 7: r = kneg; break;
+				default: r = !kneg; break;
 				}
-				E.vcc_all(r);
+				decided(r);
 				return;
 			}
 			E.vopc(VC_U32 + swapped(pred(c)), k32((uint32_t)K), L(d));
@@ -740,6 +1017,8 @@ struct emitter {
 			cond_imm(c, d, f.r[s].v);
 			return;
 		}
+		use(d);
+		use(s);
 		if (c == 10) {
 			E.vop2(V2_AND, T0, vreg(L(s)), L(d));
 			if (hz(d) || hz(s)) {
@@ -758,13 +1037,18 @@ struct emitter {
 	}
 };
 
-// registers a copied handler body may write
+bool
+is_cond_fam(int fam)
+{
+	return (fam >= AHF_JEQ_R && fam <= AHF_JSET_R) || (fam >= AHF_JEQ_I && fam <= AHF_JSET_I);
+}
+
+// the register a copied handler body writes (-1: none)
 int
 written_reg(int fam, int d)
 {
 	switch (fam) {
-	case AHF_LOOKUPSTK:
-	case AHF_LOOKUPGEN:
+	case AHF_LOOKUPSTK: case AHF_LOOKUPGEN:
 		return 0;
 	case AHF_EXIT: case AHF_FAULT: case AHF_NOP:
 	case AHF_STXGEN1: case AHF_STXGEN2: case AHF_STXGEN4: case AHF_STXGEN8:
@@ -773,11 +1057,27 @@ written_reg(int fam, int d)
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8:
 		return -1;
 	default:
-		if (fam >= AHF_JEQ_R && fam <= AHF_JSET_R)
-			return -1;
-		if (fam >= AHF_JEQ_I && fam <= AHF_JSET_I)
+		if (is_cond_fam(fam))
 			return -1;
 		return d < AH_NREGS ? d : -1;
+	}
+}
+
+// registers a copied handler body reads
+uint16_t
+copied_uses(int fam, int d, int s)
+{
+	auto m = [](int r) -> uint16_t { return r < AH_NREGS ? (uint16_t)(1u << r) : 0; };
+	switch (fam) {
+	case AHF_EXIT: return 1;
+	case AHF_LOOKUPGEN: return (1u << 1) | (1u << 2);
+	case AHF_FAULT: case AHF_NOP: case AHF_LOOKUPSTK: return 0;
+	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8: return 0;
+	case AHF_LDXPKTG1: case AHF_LDXPKTG2: case AHF_LDXPKTG4: case AHF_LDXPKTG8: return 0;
+	case AHF_LDXSTK1: case AHF_LDXSTK2: case AHF_LDXSTK4: case AHF_LDXSTK8: return 0;
+	case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: return 0;
+	case AHF_A64I_MOV: return 0;
+	default: return m(d) | m(s); // (LDX*: s = the address; ST*: d = base, s = value; ALU: both)
 	}
 }
 
@@ -798,6 +1098,30 @@ copied_result(int fam)
 	}
 }
 
+// operations with no effect besides writing their destination register (no fault, no memory
+// write): skipped when the destination is dead
+bool
+pure_fam(int fam, bool specialised_map_load)
+{
+	if (fam >= AHF_A64R_ADD && fam <= AHF_A64R_MOD)
+		return fam != AHF_A64R_DIV && fam != AHF_A64R_MOD;
+	if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
+		return fam != AHF_A32R_DIV && fam != AHF_A32R_MOD;
+	if ((fam >= AHF_A64I_ADD && fam <= AHF_A64I_MOV) || (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD))
+		return true; // immediate divisors are never zero here (the translator faults them)
+	switch (fam) {
+	case AHF_BSWAP16: case AHF_BSWAP32: case AHF_BSWAP64:
+	case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8:
+	case AHF_LDXSTK1: case AHF_LDXSTK2: case AHF_LDXSTK4: case AHF_LDXSTK8:
+	case AHF_LOOKUPSTK:
+		return true;
+	case AHF_LDXMAP1: case AHF_LDXMAP2: case AHF_LDXMAP4: case AHF_LDXMAP8:
+		return specialised_map_load;
+	default:
+		return false;
+	}
+}
+
 // refine facts on the taken (taken = true) or fall-through edge of `d c K`
 void
 refine(facts &fa, int c, int d, uint64_t K, bool taken)
@@ -805,15 +1129,23 @@ refine(facts &fa, int c, int d, uint64_t K, bool taken)
 	rf &x = fa.r[d];
 	if (x.c)
 		return;
-	// equality
 	if ((c == 0 && taken) || (c == 1 && !taken)) {
-		x = kconst(K);
+		const bool keep_map = K != 0 && x.mp >= 0;
+		rf k = kconst(K);
+		if (keep_map) {
+			k.mp = x.mp;
+			k.mreg = x.mreg;
+		}
+		x = k;
 		return;
 	}
-	// unsigned upper bounds: d <= B
+	if (K == 0 && ((c == 1 && taken) || (c == 0 && !taken))) { // d != 0
+		x.nz = true;
+		return;
+	}
 	uint64_t B;
 	bool ub = false;
-	if ((c == 5 && taken) || (c == 2 && !taken)) { // d <= K
+	if ((c == 5 && taken) || (c == 2 && !taken)) { // d <= K (unsigned)
 		B = K;
 		ub = true;
 	} else if (((c == 4 && taken) || (c == 3 && !taken)) && K) { // d < K
@@ -830,13 +1162,38 @@ refine(facts &fa, int c, int d, uint64_t K, bool taken)
 } // namespace
 
 void
+cc_prologue(int mode, uint16_t live, bool needs_pkt, std::vector<uint8_t> &out)
+{
+	enc P{out};
+	const int V_PKT = 38, V_LEN = 40, H1 = 47, H3 = 49, S_DATA = 24;
+	if (mode == 1 && (needs_pkt || (live & (1u << 1)))) {
+		// staged kernel: packet address = data + index * 64 (index in v49, gen_interp.py H[3])
+		P.vop1(V1_MOV_B32, H1, opnd{128 + 64});
+		P.vop3(V3_MAD_U64_U32, V_PKT, VGPR0 + H3, VGPR0 + H1, S_DATA, S_JUNK);
+		P.vop1(V1_MOV_B32, V_LEN, opnd{128 + 64});
+	}
+	if (live & (1u << 1))
+		P.vop1(V1_MOV_B64, 2, vreg(V_PKT));
+	if (live & (1u << 10)) {
+		const int S_STKSTRIDE = 42, S_SHARED_HI = 59;
+		P.vop2(V2_ADD_U32, 20, opnd{(uint32_t)S_STKSTRIDE}, V_STK);
+		P.vop1(V1_MOV_B32, 21, opnd{(uint32_t)S_SHARED_HI});
+	}
+	for (int r = 0; r < AH_NREGS; r++)
+		if (r != 1 && r != 10 && (live & (1u << r)))
+			P.vop1(V1_MOV_B64, 2 * r, opnd{128});
+}
+
+void
 cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
-	   const std::vector<char> &entry_point, int mode, std::vector<cc_block> &out)
+	   const std::vector<char> &entry_point, int mode, uint32_t exitk_off,
+	   const std::vector<dp_map> &table, std::vector<cc_block> &out)
 {
 	const size_t n = low.size();
-	out.assign(n, cc_block());
-	// predecessors (the tree gives one; shared fault entries and anything unexpected get none of
-	// the facts)
+	std::vector<mapinfo> maps(table.size());
+	for (size_t i = 0; i < table.size(); i++)
+		maps[i] = mapinfo{table[i].dev_base, table[i].value_size, table[i].max_entries, table[i].lds_off};
+	// predecessors (the tree gives one; shared fault entries get no facts)
 	std::vector<uint32_t> npred(n, 0);
 	for (uint32_t e : order) {
 		const uint32_t h = (uint32_t)low[e].handler;
@@ -848,111 +1205,226 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 		if ((ah_flags[h] & 1) && xl.entries[e].target < n)
 			npred[xl.entries[e].target]++;
 	}
-	std::vector<facts> in(n);
-	std::vector<char> have(n, 0);
-	{
-		facts f0; // the kernels zero r0, r2..r9 per group; r1 = packet, r10 = stack (unknown)
-		for (int r = 0; r < AH_NREGS; r++)
-			f0.r[r] = (r == 1 || r == 10) ? rf() : kconst(0);
+	std::vector<uint16_t> uses(n, 0), live_out(n, 0xffff);
+	std::vector<int8_t> defreg(n, -1);
+	std::vector<char> pure(n, 0);
+	uint16_t live_start = 0x7ff;
+	const unsigned off = cc_off();
+
+	for (int pass = 0; pass < 2; pass++) {
+		const bool final_pass = pass == 1;
+		out.assign(n, cc_block());
+		std::vector<facts> in(n);
+		std::vector<char> have(n, 0);
 		if (xl.start < n) {
+			facts f0; // r0, r2..r9 are zero at the start (the kernel, or the prologue below)
+			for (int r = 0; r < AH_NREGS; r++) {
+				f0.r[r] = (r == 1 || r == 10) ? rf() : kconst(0);
+				f0.pv[r] = (live_start & (1u << r)) != 0;
+			}
 			in[xl.start] = f0;
 			have[xl.start] = 1;
 		}
-	}
-	std::vector<char> fused(n, 0); // a BSWAP folded into the preceding packet load
-	for (size_t k = 0; k < order.size(); k++) {
-		const uint32_t e = order[k];
-		// exact facts need the one predecessor (the start state: none)
-		const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u);
-		facts f = valid ? in[e] : facts();
-		cc_block &blk = out[e];
-		const uint32_t h = (uint32_t)low[e].handler;
-		const int fam = ah_fam[h], d = ah_dst[h], s = ah_src[h];
-		const uint64_t K = low[e].imm;
-		emitter em(blk, f);
-		bool ok = true;
-		switch (fam) {
-		case AHF_NOP: break;
-		case AHF_A64I_MOV: em.mov64(d, K); break;
-		case AHF_A64I_ADD: em.add64i(d, K); break;
-		case AHF_A64I_OR: em.or64i(d, K); break;
-		case AHF_A64I_XOR: em.xor64i(d, K); break;
-		case AHF_A64I_AND: em.and64i(d, K); break;
-		case AHF_A64I_LSH: em.lsh64i(d, (uint32_t)K); break;
-		case AHF_A64I_RSH: em.rsh64i(d, (uint32_t)K); break;
-		case AHF_A64I_MUL: em.mul64i(d, K); break;
-		case AHF_BSWAP16:
-		case AHF_BSWAP32:
-			if (fused[e])
+		std::vector<char> fused(n, 0); // a BSWAP folded into the preceding packet load
+		for (size_t k = 0; k < order.size(); k++) {
+			const uint32_t e = order[k];
+			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u);
+			facts f = valid ? in[e] : facts();
+			if (!valid)
+				for (bool &p : f.pv)
+					p = true;
+			cc_block &blk = out[e];
+			const uint32_t h = (uint32_t)low[e].handler;
+			const int fam = ah_fam[h], d = ah_dst[h], s = ah_src[h];
+			const uint64_t K = low[e].imm;
+			uint32_t aux0, aux1;
+			memcpy(&aux0, reinterpret_cast<const uint8_t *>(&low[e]) + 24, 4);
+			memcpy(&aux1, reinterpret_cast<const uint8_t *>(&low[e]) + 28, 4);
+			f.nofwd = (off & 4) != 0;
+			const facts before = f;
+			emitter em(blk, f, maps);
+			em.off = off;
+			bool ok = true, spec_map = false;
+			switch (fam) {
+			case AHF_NOP: break;
+			case AHF_EXIT:
+				if (f.r[0].c && !(off & 32))
+					em.exit_known(f.r[0].v, exitk_off);
+				else
+					ok = false;
 				break;
-			ok = em.bswap(fam, d);
-			break;
-		case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: {
-			const int z = 1 << (fam - AHF_LDXPKC1);
-			int swap = 0;
+			case AHF_A64I_MOV: em.mov64(d, K); break;
+			case AHF_A64I_ADD: em.add64i(d, K); break;
+			case AHF_A64I_OR: em.or64i(d, K); break;
+			case AHF_A64I_XOR: em.xor64i(d, K); break;
+			case AHF_A64I_AND: em.and64i(d, K); break;
+			case AHF_A64I_LSH: em.lsh64i(d, (uint32_t)K); break;
+			case AHF_A64I_RSH: em.rsh64i(d, (uint32_t)K); break;
+			case AHF_A64I_MUL: em.mul64i(d, K); break;
+			case AHF_BSWAP16:
+			case AHF_BSWAP32:
+				if (fused[e]) {
+					em.use(d); // the value the fused load produced
+					break;
+				}
+				ok = em.bswap(fam, d);
+				break;
+			case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: {
+				const int z = 1 << (fam - AHF_LDXPKC1);
+				int swap = 0;
+				const uint32_t nx = xl.entries[e].next;
+				if (mode == 1 && z <= 4 && nx < n && k + 1 < order.size() && order[k + 1] == nx &&
+				    !entry_point[nx] && npred[nx] == 1) {
+					const uint32_t h2 = (uint32_t)low[nx].handler;
+					const int f2 = ah_fam[h2];
+					if ((f2 == AHF_BSWAP16 || f2 == AHF_BSWAP32) && ah_dst[h2] == d) {
+						swap = f2 == AHF_BSWAP16 ? 2 : 4;
+						fused[nx] = 1;
+					}
+				}
+				em.ldxpkc(d, z, s, swap);
+				break;
+			}
+			case AHF_STXSTK1: case AHF_STXSTK2: case AHF_STXSTK4: case AHF_STXSTK8:
+				if (K + 8 <= 255 * 4)
+					em.stxstk(1 << (fam - AHF_STXSTK1), d, (uint32_t)K);
+				else
+					ok = false;
+				break;
+			case AHF_LDXSTK1: case AHF_LDXSTK2: case AHF_LDXSTK4: case AHF_LDXSTK8:
+				if (K + 8 <= 255 * 4)
+					em.ldxstk(1 << (fam - AHF_LDXSTK1), d, (uint32_t)K);
+				else
+					ok = false;
+				break;
+			case AHF_LOOKUPSTK: {
+				int mi = -1;
+				for (size_t t = 0; t < maps.size(); t++)
+					if (maps[t].dev_base == K && maps[t].max_entries == low[e].target &&
+					    maps[t].value_size == aux1)
+						mi = (int)t;
+				ok = !(off & 8) && em.lookup_stk(mi, aux0);
+				break;
+			}
+			case AHF_LDXMAP1: case AHF_LDXMAP2: case AHF_LDXMAP4: case AHF_LDXMAP8:
+				ok = spec_map = em.ldxmap(1 << (fam - AHF_LDXMAP1), d, s, K);
+				break;
+			default:
+				if (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD)
+					ok = em.alu32i(fam, d, (uint32_t)K);
+				else if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
+					ok = em.alu32r(fam, d, s);
+				else if (fam >= AHF_A64R_ADD && fam <= AHF_A64R_MOD)
+					ok = em.alu64r(fam, d, s);
+				else if (fam >= AHF_JEQ_I && fam <= AHF_JSET_I)
+					em.cond_imm(fam - AHF_JEQ_I, d, K);
+				else if (fam >= AHF_JEQ_R && fam <= AHF_JSET_R)
+					em.cond_reg(fam - AHF_JEQ_R, d, s);
+				else
+					ok = false;
+			}
+			const int wr = written_reg(fam, d);
+			if (ok) {
+				blk.fast = true;
+			} else {
+				// the interpreter's body; the facts of what it writes are lost
+				f = before;
+				blk.fast = false;
+				blk.body.clear();
+				blk.reads = 0;
+				em.used = copied_uses(fam, d, s);
+				if (wr >= 0)
+					f.def(wr, copied_result(fam));
+				// stores through unknown pointers may hit the stack
+				if (fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8)
+					f.nst = 0;
+				if (fam >= AHF_STGEN1 && fam <= AHF_STGEN8)
+					f.nst = 0;
+				if (fam >= AHF_STSTK1 && fam <= AHF_STSTK8)
+					f.store(aux0, 1 << (fam - AHF_STSTK1), -1);
+			}
+			if (!final_pass) {
+				uses[e] = em.used;
+				defreg[e] = (int8_t)wr;
+				pure[e] = (char)(pure_fam(fam, spec_map) && wr >= 0);
+			} else if (!(off & 1) && pure[e] && wr >= 0 && !(live_out[e] & (1u << wr))) {
+				// dead: no code, the register's VGPRs do not hold the (unused) value
+				blk.fast = true;
+				blk.body.clear();
+				blk.reads = 0;
+				f.pv[wr] = false;
+			}
+			// successors
+			if (fam == AHF_EXIT || fam == AHF_FAULT)
+				continue;
 			const uint32_t nx = xl.entries[e].next;
-			if (mode == 1 && z <= 4 && nx < n && k + 1 < order.size() && order[k + 1] == nx &&
-			    !entry_point[nx] && npred[nx] == 1) {
-				const uint32_t h2 = (uint32_t)low[nx].handler;
-				const int f2 = ah_fam[h2];
-				if ((f2 == AHF_BSWAP16 || f2 == AHF_BSWAP32) && ah_dst[h2] == d) {
-					swap = f2 == AHF_BSWAP16 ? 2 : 4;
-					fused[nx] = 1;
+			const bool is_cond = (ah_flags[h] & 1) != 0;
+			auto give = [&](uint32_t to, const facts &fo) {
+				if (to >= n)
+					return;
+				in[to] = fo;
+				have[to] = 1;
+			};
+			if (is_cond) {
+				const uint32_t tk = xl.entries[e].target;
+				const int c = fam >= AHF_JEQ_I ? fam - AHF_JEQ_I : fam - AHF_JEQ_R;
+				const bool cimm = fam >= AHF_JEQ_I || f.r[s].c;
+				const uint64_t cv = fam >= AHF_JEQ_I ? K : f.r[s].v;
+				facts ft = f, fn = f;
+				if (cimm && d < AH_NREGS) {
+					refine(ft, c, d, cv, true);
+					refine(fn, c, d, cv, false);
+				}
+				give(tk, ft);
+				give(nx, fn);
+			} else {
+				give(nx, f);
+			}
+		}
+		if (final_pass) {
+			// the group set-up the kernel leaves to compiled programs: the packet address
+			// (staged mode; the generic memory routines and r1 read it), r1, r10 and the
+			// zeroing of r0, r2..r9 — each only if something reads it
+			bool needs_pkt = (live_start & (1u << 1)) != 0;
+			for (uint32_t e : order) {
+				const int fam = ah_fam[(uint32_t)low[e].handler];
+				if (!out[e].fast &&
+				    ((fam >= AHF_LDXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
+				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN))
+					needs_pkt = true;
+			}
+			if (xl.start < n)
+				cc_prologue(mode, live_start, needs_pkt, out[xl.start].prologue);
+			break;
+		}
+		// liveness (backward over the tree: children come after their parent in `order`)
+		std::vector<uint16_t> live_in(n, 0);
+		for (size_t k = order.size(); k-- > 0;) {
+			const uint32_t e = order[k];
+			const uint32_t h = (uint32_t)low[e].handler;
+			const int fam = ah_fam[h];
+			uint16_t lo = 0;
+			if (fam != AHF_EXIT && fam != AHF_FAULT) {
+				const uint32_t nx = xl.entries[e].next;
+				if (nx < n)
+					lo |= npred[nx] == 1 ? live_in[nx] : 0x7ff;
+				if ((ah_flags[h] & 1) && xl.entries[e].target < n) {
+					const uint32_t tk = xl.entries[e].target;
+					lo |= npred[tk] == 1 ? live_in[tk] : 0x7ff;
 				}
 			}
-			em.ldxpkc(d, z, s, swap);
-			break;
-		}
-		default:
-			if (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD)
-				ok = em.alu32i(fam, d, (uint32_t)K);
-			else if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
-				ok = em.alu32r(fam, d, s);
-			else if (fam >= AHF_A64R_ADD && fam <= AHF_A64R_MOD)
-				ok = em.alu64r(fam, d, s);
-			else if (fam >= AHF_JEQ_I && fam <= AHF_JSET_I)
-				em.cond_imm(fam - AHF_JEQ_I, d, K);
-			else if (fam >= AHF_JEQ_R && fam <= AHF_JSET_R)
-				em.cond_reg(fam - AHF_JEQ_R, d, s);
+			live_out[e] = lo;
+			uint16_t li = lo;
+			if (defreg[e] >= 0 && !(uses[e] & (1u << defreg[e])))
+				li &= (uint16_t)~(1u << defreg[e]);
+			if (pure[e] && defreg[e] >= 0 && !(lo & (1u << defreg[e])))
+				li = lo; // a dead pure operation reads nothing
 			else
-				ok = false;
+				li |= uses[e];
+			live_in[e] = li;
 		}
-		if (ok) {
-			blk.fast = true;
-		} else {
-			// the interpreter's body; the facts of what it writes are lost
-			blk.fast = false;
-			blk.body.clear();
-			blk.reads = 0;
-			const int wr = written_reg(fam, d);
-			if (wr >= 0)
-				f.r[wr] = copied_result(fam);
-		}
-		// successors
-		if (fam == AHF_EXIT || fam == AHF_FAULT)
-			continue;
-		const uint32_t nx = xl.entries[e].next;
-		const bool is_cond = (ah_flags[h] & 1) != 0;
-		auto give = [&](uint32_t to, const facts &fo) {
-			if (to >= n)
-				return;
-			in[to] = fo;
-			have[to] = 1;
-		};
-		if (is_cond) {
-			const uint32_t tk = xl.entries[e].target;
-			const int c = fam >= AHF_JEQ_I ? fam - AHF_JEQ_I : fam - AHF_JEQ_R;
-			const bool cimm = fam >= AHF_JEQ_I || f.r[s].c;
-			const uint64_t cv = fam >= AHF_JEQ_I ? K : f.r[s].v;
-			facts ft = f, fn = f;
-			if (cimm && d < AH_NREGS) {
-				refine(ft, c, d, cv, true);
-				refine(fn, c, d, cv, false);
-			}
-			give(tk, ft);
-			give(nx, fn);
-		} else {
-			give(nx, f);
-		}
+		live_start = xl.start < n ? live_in[xl.start] : 0x7ff;
+		if (off & 3)
+			live_start = 0x7ff;
 	}
 }

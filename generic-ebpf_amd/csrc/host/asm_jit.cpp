@@ -33,7 +33,7 @@ enum jt_index {
 	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
-	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_AREA,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_AREA,
 	JT_AREA_BYTES,
 	JT_COUNT
 };
@@ -218,9 +218,11 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
 	if (getenv("EBPF_JIT_NOCC") == nullptr)
-		cc_compile(xl, low, order, entry_point, mode, cb);
-	else
-		cb.assign(n, cc_block());
+		cc_compile(xl, low, order, entry_point, mode, T[JT_EXITK], table, cb);
+	else {
+		cb.assign(n, cc_block()); // every body copied: full group set-up
+		cc_prologue(mode, 0x7ff, true, cb[xl.start].prologue);
+	}
 	auto reads_of = [&](uint32_t e) -> uint8_t {
 		return cb[e].fast ? cb[e].reads : ah_reads[(uint32_t)low[e].handler];
 	};
@@ -284,7 +286,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = pre_len(e);
+		uint32_t sz = (uint32_t)cb[e].prologue.size() + pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
 			sz += (uint32_t)cb[e].body.size();
@@ -294,8 +296,12 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				sz += 4;
 		}
 		*body_end = sz;
-		if (ah_flags[h] & 1)
-			sz += long_cond[e] ? cl_len : cs_len;
+		if (ah_flags[h] & 1) {
+			if (cb[e].sdir < 0)
+				sz += long_cond[e] ? cl_len : cs_len;
+			else if (cb[e].sdir == 1)
+				sz += long_cond[e] ? jl_len : 4; // always taken: a jump
+		}
 		if (needs_branch(e))
 			sz += long_br[e] ? jl_len : 4;
 		return sz;
@@ -313,8 +319,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			uint32_t pre, be;
 			block_size(e, &pre, &be);
 			const uint32_t h = (uint32_t)low[e].handler;
-			if ((ah_flags[h] & 1) && !long_cond[e]) {
-				const uint32_t br_at = pos[e] + be + (T[JT_CS_BR] - T[JT_CS]);
+			if ((ah_flags[h] & 1) && !long_cond[e] && cb[e].sdir != 0) {
+				const uint32_t br_at = pos[e] + be + (cb[e].sdir == 1 ? 0 : T[JT_CS_BR] - T[JT_CS]);
 				const uint32_t tk = xl.entries[e].target;
 				if (!fits_simm16((int64_t)pos[tk] - (int64_t)(br_at + 4))) {
 					long_cond[e] = 1;
@@ -363,6 +369,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		const dp_entry &o = low[e];
 		const uint32_t h = (uint32_t)o.handler;
 		size_t at = pos[e];
+		if (!cb[e].prologue.empty()) {
+			memcpy(&img[area + at], cb[e].prologue.data(), cb[e].prologue.size());
+			at += cb[e].prologue.size();
+		}
 		for (int r = 0; r < 6; r++) {
 			if (!(pre_mask[e] & (1u << r)))
 				continue;
@@ -393,7 +403,18 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				at += 4;
 			}
 		}
-		if (ah_flags[h] & 1) {
+		if ((ah_flags[h] & 1) && cb[e].sdir == 1) { // statically taken by every lane
+			const uint32_t tk = xl.entries[e].target;
+			if (!long_cond[e]) {
+				copy_t(at, JT_BR, 4);
+				patch_simm16(at, pos[tk]);
+				at += 4;
+			} else {
+				copy_t(at, JT_JL, jl_len);
+				put32(at + 4, code_off(tk));
+				at += jl_len;
+			}
+		} else if ((ah_flags[h] & 1) && cb[e].sdir < 0) {
 			const uint32_t tk = xl.entries[e].target;
 			if (!long_cond[e]) {
 				copy_t(at, JT_CS, cs_len);

@@ -126,11 +126,19 @@ def test_optimised_c4_instruction_forms(native, env):
         "v_mov_b32_e32 v16, v46",
         # XOR64 r8, imm with a zero high word: low half only
         "v_xor_b32_e32 v16, 0x5bd1e995, v16",
-        # r2 = r10 - 4
-        "v_mov_b64_e32 v[4:5], v[20:21]", "v_lshl_add_u64 v[4:5], -4, 0, v[4:5]",
+        # STXW [r10-4] = r6: one LDS store, offset folded
+        "ds_write_b32 v42, v12",
+        # lookup(map, key = r6 < 256 = max_entries) cannot fail: its NULL check is gone and the
+        # value load reads the LDS copy of the map at lds_off + key * 8
+        "v_mad_u32_u24 v46, v12, 8, s13", "ds_read2_b32 v[12:13], v46 offset1:1",
     ]
     for w in want:
         assert w in lines, (w, "\n".join(lines[:80]))
+    # dead code: r1 = map handle (LDDW) and r2 = r10 - 4 are only the statically resolved
+    # lookup's arguments
+    assert "v_mov_b64_e32 v[4:5], v[20:21]" not in lines
+    assert not any(ln.startswith("v_mov_b32_e32 v2,") or ln.startswith("v_mov_b32_e32 v3,")
+                   for ln in lines)
 
 
 def _count_valu(native, env, code, layout, nocc):

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""In-process A/B timing of compiled programs on one GPU: the boxes differ by several percent in
+HBM throughput, so relative costs (C4 over the c0 floor, optimiser on/off) are measured by
+alternating the candidates inside one process, many rounds, and reporting the median kernel time.
+
+  python3 tools/ab_inproc.py c0 c4 c4:nocc c3 ...     (":nocc" = compiled with EBPF_JIT_NOCC=1)
+  python3 tools/ab_inproc.py ab/k4.so@c0 ab/k4.so@c4 ab/k8.so@c4   (a build of the library per
+                                                                   candidate, all in one process)
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import pkgload  # noqa: E402
+
+pkgload.load()
+from generic_ebpf_amd import native, workloads  # noqa: E402
+
+
+def main():
+    import torch
+    names = sys.argv[1:] or ["c0", "c4"]
+    rounds, launches = 7, 20
+    dev = torch.device("cuda", 0)
+    n = 1 << 26
+    pk = workloads.packets_l2l3(1 << 22, 64, seed=3)
+    d_l2 = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(16)
+    rnd = workloads.packets_random(1 << 22, 64, seed=2)
+    d_rnd = torch.from_numpy(rnd.reshape(-1)).to(dev).repeat(16)
+    d_ret = torch.empty(n, dtype=torch.int64, device=dev)
+    d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+    cands = []
+    libs = {}
+
+    def select(path):
+        # one CDLL per library build (RTLD_LOCAL: each resolves its own symbols)
+        if path not in libs:
+            native._lib = None
+            native.LIB_PATH = path
+            libs[path] = native.lib()
+        native._lib = libs[path]
+
+    default_lib = native.LIB_PATH
+    envs = {}
+    for nm in names:
+        path, _, spec = nm.rpartition("@")
+        path = os.path.join(ROOT, path) if path else default_lib
+        select(path)
+        if path not in envs:
+            envs[path] = (native.Env(), {})
+        env, maps = envs[path]
+        cfg, _, opt = spec.partition(":")
+        lay = workloads.CONFIGS[cfg]["prog"]()
+        handles = []
+        if cfg == "c4":
+            if "c4" not in maps:
+                m = native.Map(env, 256, 8)
+                m.fill(workloads.c4_map_values().tobytes())
+                maps["c4"] = m
+            handles = [maps["c4"].handle]
+        if opt == "nocc":
+            os.environ["EBPF_JIT_NOCC"] = "1"
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, handles))
+        p.prepare(0)
+        data = d_rnd if cfg in ("c0", "c2") else d_l2
+        # the program is compiled at its first launch
+        p.run_batch_dev(0, data.data_ptr(), 64, 64, d_ret.data_ptr(), None, None, None,
+                        stream.cuda_stream)
+        torch.cuda.synchronize()
+        os.environ.pop("EBPF_JIT_NOCC", None)
+        cands.append((nm, p, data, path))
+    times = {nm: [] for nm in names}
+
+    def launch(p, data, path):
+        select(path)
+        p.run_batch_dev(0, data.data_ptr(), n, 64, d_ret.data_ptr(), None, None, d_hist.data_ptr(),
+                        stream.cuda_stream)
+
+    for nm, p, data, path in cands:  # warm
+        for _ in range(3):
+            launch(p, data, path)
+    torch.cuda.synchronize()
+    for r in range(rounds):
+        for nm, p, data, path in cands:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(launches):
+                launch(p, data, path)
+            b.record(stream)
+            torch.cuda.synchronize()
+            times[nm].append(a.elapsed_time(b) / launches)
+    base = float(np.median(times[names[0]]))
+    for nm in names:
+        t = float(np.median(times[nm]))
+        print("%-10s %.4f ms  %.1f Gpkt/s  frac %.4f  x%.3f of %s   (min %.4f max %.4f)" % (
+            nm, t, n / t / 1e6, n * 64 / (t * 1e-3) / 8e12, t / base, names[0],
+            min(times[nm]), max(times[nm])), flush=True)
+
+
+if __name__ == "__main__":
+    main()
