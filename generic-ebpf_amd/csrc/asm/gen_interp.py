@@ -81,6 +81,11 @@ S_REC = 64           # s[64:71] map record {handle, dev_base, value_size, max_en
 S_PREVG = 72         # group whose results are still in V_RET (-1: none)
 S_WAVE = 3
 NSGPR = 73           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per SIMD
+# staged image: s[74:75] .. s[96:97] hold the taken-lane masks of a structured compiled program's
+# pending branches (asm_jit.cpp; 12 levels); 98 SGPRs still allow the image's 6 waves per SIMD
+S_JOIN = 74
+JOIN_LEVELS = 12
+NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -666,7 +671,12 @@ def routines():
           "v_mov_b32 %s, 1" % v(R[9]),
           "ds_add_u32 %s, %s" % (v(R[8]), v(R[9])),
           ".Lex_nohist:",
-          "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE))] + goto(".Lr_schedule")
+          "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE)),
+          # structured compiled programs (s7 bit 2) call the exit and continue themselves
+          "s_bitcmp1_b32 s7, 2",
+          "s_cbranch_scc0 .Lex_sched",
+          "s_setpc_b64 %s" % sp(S_LINK),
+          ".Lex_sched:"] + goto(".Lr_schedule")
     # EXIT with r0 known at compile time (compiled programs): v[44:45] = r0 and S_BYTES = its
     # verdict bin are set by the caller, so the verdict needs no per-lane work
     L += [".Lr_exit_k:",
@@ -707,7 +717,12 @@ def routines():
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK)),
           "s_cbranch_execz .Lfl_none",
           "s_setpc_b64 %s" % sp(S_LINK),
-          ".Lfl_none:"] + goto(".Lr_schedule")
+          ".Lfl_none:",
+          # structured compiled programs continue with no lane (their join restores the rest)
+          "s_bitcmp1_b32 s7, 2",
+          "s_cbranch_scc0 .Lfl_sched",
+          "s_setpc_b64 %s" % sp(S_LINK),
+          ".Lfl_sched:"] + goto(".Lr_schedule")
     # UDIVMOD64: n = R[0:1], d = R[2:3] (non-zero) -> q = R[4:5], r = R[6:7]; clobbers R[8:9]
     n, dd, q, r = vp(R[0]), vp(R[2]), vp(R[4]), vp(R[6])
     L += [".Lr_udiv:",
@@ -1306,7 +1321,8 @@ def jit_templates():
     names = [".Ljt_mov_s%d" % r for r in range(10, 16)] + [
         ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
-        ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", "ebpf_jit_area"]
+        ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", ".Lr_exit", ".Lr_fault",
+        ".Lgroup_done", "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
     return L
@@ -1316,9 +1332,9 @@ def main():
     """gen_interp.py <staged.s> <general.s> <handlers.h>"""
     out_s1, out_s0, out_h = sys.argv[1], sys.argv[2], sys.argv[3]
     header = None
-    for out_s, k in ((out_s1, RETK_STAGED), (out_s0, 1)):
+    for out_s, k, staged in ((out_s1, RETK_STAGED, True), (out_s0, 1, False)):
         set_retk(k)
-        h = generate(out_s)
+        h = generate(out_s, staged)
         header = header or h
         assert h[:-2] == header[:-2]   # identical but for the RETK-dependent lines
     header = header[:-2] + ["#define AH_RET_GROUPS_STAGED %d  // groups per result burst, staged kernels"
@@ -1329,7 +1345,7 @@ def main():
         f.write("\n".join(header) + "\n")
 
 
-def generate(out_s):
+def generate(out_s, staged_image):
     A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950:xnack-"', ".amdhsa_code_object_version 5", ".text"]
     A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
     A += kernel("ebpf_jit_s64", True, True) + kernel("ebpf_jit_gen", False, True)
@@ -1389,6 +1405,8 @@ def generate(out_s):
     header.append("static const uint8_t ah_dst[AH_COUNT] = {%s};" % ",".join(map(str, dst_of)))
     header.append("static const uint8_t ah_src[AH_COUNT] = {%s};" % ",".join(map(str, src_of)))
     header.append("#define AH_JIT_AREA_BYTES %d" % JIT_AREA_BYTES)
+    header.append("#define AH_S_JOIN %d  // structured programs: taken-lane masks s[74:75]..  (staged image)" % S_JOIN)
+    header.append("#define AH_JOIN_LEVELS %d" % JOIN_LEVELS)
     header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
@@ -1399,10 +1417,11 @@ def generate(out_s):
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
     kernarg = 112
-    ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR, 256),
-          ("ebpf_interp_gen", kernarg, 0, NVGPR, NSGPR, 256),
-          ("ebpf_jit_s64", kernarg, 0, NVGPR, NSGPR, 256),
-          ("ebpf_jit_gen", kernarg, 0, NVGPR, NSGPR, 256),
+    nsg = NSGPR_STAGED if staged_image else NSGPR
+    ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
+          ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),
+          ("ebpf_jit_s64", kernarg, 0, NVGPR, nsg, 256),
+          ("ebpf_jit_gen", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_asm_link", 16, 0, 16, 16, 64)]
     for name, ka, lds, vg, sg, wg in ks:
         A += kd(name, lds, vg, sg, ka, wg)

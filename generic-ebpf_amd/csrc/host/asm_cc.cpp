@@ -911,14 +911,35 @@ struct emitter {
 	}
 
 	// ---- EXIT with r0 known: result and verdict bin set here, then .Lr_exit_k (gen_interp.py)
-	void exit_known(uint64_t r0, uint32_t exitk_off)
+	void exit_known(uint64_t r0, uint32_t exitk_off, bool call)
 	{
 		mov32(V_RES, (uint32_t)r0);
 		mov32(V_RES + 1, (uint32_t)(r0 >> 32));
 		E.sop1(0x00, S_BYTES, k32(r0 < 255 ? (uint32_t)r0 : 255u));   // s_mov_b32
+		if (call) {
+			call_routine(exitk_off, 0);
+			return;
+		}
 		E.sop2(0x00, S_JUNK, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, exitk_off}); // s_add_u32
 		E.sop2(0x04, S_JUNK + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});     // s_addc_u32
 		E.sop1(0x1d, 0, opnd{(uint32_t)S_JUNK});                           // s_setpc_b64
+	}
+	// call a routine that returns (structured programs): the link pair s[50:51]
+	void call_routine(uint32_t off, uint16_t reads)
+	{
+		const int S_LINK = 50;
+		used |= reads;
+		E.sop2(0x00, S_LINK, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, off});     // s_add_u32
+		E.sop2(0x04, S_LINK + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});     // s_addc_u32
+		E.sop1(0x1e, S_LINK, opnd{(uint32_t)S_LINK});                      // s_swappc_b64
+	}
+	// FAULT entry (structured): fault every running lane with `code`
+	void fault(uint32_t code, uint32_t fault_off)
+	{
+		const int S_MASK = 48, S_CODE = 52;
+		E.sop1(0x00, S_CODE, k32(code));            // s_mov_b32 s52, code
+		E.sop1(0x01, S_MASK, opnd{SRC_EXEC});       // s_mov_b64 s[48:49], exec
+		call_routine(fault_off, 0);
 	}
 
 	// ---- conditional jumps: VCC = lanes taking the branch (the caller appends the tail)
@@ -1162,9 +1183,11 @@ refine(facts &fa, int c, int d, uint64_t K, bool taken)
 } // namespace
 
 void
-cc_prologue(int mode, uint16_t live, bool needs_pkt, std::vector<uint8_t> &out)
+cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vector<uint8_t> &out)
 {
 	enc P{out};
+	if (structured)
+		P.sop2(0x0e, 7, opnd{7}, opnd{128 + 4}); // s_or_b32 s7, s7, 4
 	const int V_PKT = 38, V_LEN = 40, H1 = 47, H3 = 49, S_DATA = 24;
 	if (mode == 1 && (needs_pkt || (live & (1u << 1)))) {
 		// staged kernel: packet address = data + index * 64 (index in v49, gen_interp.py H[3])
@@ -1186,7 +1209,7 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, std::vector<uint8_t> &out)
 
 void
 cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
-	   const std::vector<char> &entry_point, int mode, uint32_t exitk_off,
+	   const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 	   const std::vector<dp_map> &table, std::vector<cc_block> &out)
 {
 	const size_t n = low.size();
@@ -1209,7 +1232,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	std::vector<int8_t> defreg(n, -1);
 	std::vector<char> pure(n, 0);
 	uint16_t live_start = 0x7ff;
-	const unsigned off = cc_off();
+	const unsigned off = cc_off() | (structured ? 16u : 0u); // structured: compares leave VCC
 
 	for (int pass = 0; pass < 2; pass++) {
 		const bool final_pass = pass == 1;
@@ -1249,7 +1272,15 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			case AHF_NOP: break;
 			case AHF_EXIT:
 				if (f.r[0].c && !(off & 32))
-					em.exit_known(f.r[0].v, exitk_off);
+					em.exit_known(f.r[0].v, rt.exit_k, structured);
+				else if (structured)
+					em.call_routine(rt.exit, 1);
+				else
+					ok = false;
+				break;
+			case AHF_FAULT:
+				if (structured)
+					em.fault(aux0, rt.fault);
 				else
 					ok = false;
 				break;
@@ -1394,7 +1425,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					needs_pkt = true;
 			}
 			if (xl.start < n)
-				cc_prologue(mode, live_start, needs_pkt, out[xl.start].prologue);
+				cc_prologue(mode, live_start, needs_pkt, structured, out[xl.start].prologue);
 			break;
 		}
 		// liveness (backward over the tree: children come after their parent in `order`)

@@ -22,15 +22,25 @@ struct cc_block {
 	int8_t sdir = -1; // conditional decided at compile time: 0 never taken, 1 always taken
 };
 
+// Offsets from .Lcb of the interpreter routines compiled code calls or jumps to.
+struct cc_routines {
+	uint32_t exit_k; // EXIT with r0 known (v[44:45], s57 = verdict bin set by the caller)
+	uint32_t exit;   // EXIT (r0 in v[0:1])
+	uint32_t fault;  // fault the lanes s[48:49] with code s52
+};
+
 // low: the lowered entries (asm_lower); order: the layout order (depth-first, parents first);
 // entry_point[e]: e can be entered other than by falling through from its layout predecessor.
-// mode 1 = staged 64-B packets (packet loads read v22..v37).  exitk_off: offset of the
-// .Lr_exit_k routine from .Lcb (EXIT with a known r0).  table: the program's maps.
+// mode 1 = staged 64-B packets (packet loads read v22..v37).  structured: the program runs with
+// structured control flow (asm_jit.cpp): exits and faults are calls that return, compares
+// always leave VCC.  table: the program's maps.
 void cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
-		const std::vector<char> &entry_point, int mode, uint32_t exitk_off,
+		const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 		const std::vector<dp_map> &table, std::vector<cc_block> &out);
 
 // The group set-up a compiled program does itself (the kernel jumps straight to it): the packet
 // address (staged mode), r1 = packet, r10 = stack top, zeroes for r0, r2..r9 — the registers in
 // `live` (bit r), the packet address also if `needs_pkt` (generic memory routines read it).
-void cc_prologue(int mode, uint16_t live, bool needs_pkt, std::vector<uint8_t> &out);
+// structured: also mark the wave's group as structured (s7 bit 2, read by the exit and fault
+// routines).
+void cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vector<uint8_t> &out);

@@ -33,7 +33,7 @@ enum jt_index {
 	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
-	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_AREA,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_GDONE, JT_AREA,
 	JT_AREA_BYTES,
 	JT_COUNT
 };
@@ -215,13 +215,66 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		if (needs_branch(e))
 			entry_point[succ(e)] = 1;
 	}
+	// Structured control flow (staged programs without generic lookups): every conditional
+	// splits exec into its fall-through lanes, which run first, and its taken lanes, whose mask
+	// waits in s[74 + 2d] (d = branches pending on the path) and which run when the fall-through
+	// subtree is done (the join at the head of the taken block).  A leaf (EXIT / FAULT) calls
+	// its routine and continues at the innermost pending join (or ends the group).  No lane is
+	// parked and nothing is scheduled; the interpreter's v41 parking remains for the rest.
+	const uint32_t GROUP_END = UINT32_MAX;
+	std::vector<uint32_t> cont(n, GROUP_END); // where a path through the entry continues
+	std::vector<int> jdepth(n, 0);            // pending branches (join masks in use)
+	std::vector<int> join_of(n, -1);          // entry e is the taken block of conditional k
+	bool structured = mode == 1 && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
+			  getenv("EBPF_JIT_NOCC") == nullptr;
+	for (uint32_t e : order) {
+		const uint32_t h = (uint32_t)low[e].handler;
+		if (h == (uint32_t)AH_LOOKUPGEN)
+			structured = false;
+	}
+	if (structured) {
+		std::vector<char> seen(n, 0);
+		seen[xl.start] = 1;
+		for (uint32_t e : order) {
+			if (!seen[e]) { // more than the tree: no structure
+				structured = false;
+				break;
+			}
+			const uint32_t h = (uint32_t)low[e].handler;
+			if (is_terminal(h))
+				continue;
+			const uint32_t nx = xl.entries[e].next;
+			if (ah_flags[h] & 1) {
+				const uint32_t tk = xl.entries[e].target;
+				if (jdepth[e] >= AH_JOIN_LEVELS || nx >= n || tk >= n || seen[nx] || seen[tk]) {
+					structured = false;
+					break;
+				}
+				jdepth[nx] = jdepth[e] + 1;
+				cont[nx] = tk;
+				jdepth[tk] = jdepth[e];
+				cont[tk] = cont[e];
+				join_of[tk] = (int)e;
+				seen[nx] = seen[tk] = 1;
+			} else if (nx < n) {
+				if (seen[nx]) {
+					structured = false;
+					break;
+				}
+				jdepth[nx] = jdepth[e];
+				cont[nx] = cont[e];
+				seen[nx] = 1;
+			}
+		}
+	}
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
 	if (getenv("EBPF_JIT_NOCC") == nullptr)
-		cc_compile(xl, low, order, entry_point, mode, T[JT_EXITK], table, cb);
+		cc_compile(xl, low, order, entry_point, mode, structured,
+			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT]}, table, cb);
 	else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
-		cc_prologue(mode, 0x7ff, true, cb[xl.start].prologue);
+		cc_prologue(mode, 0x7ff, true, false, cb[xl.start].prologue);
 	}
 	auto reads_of = [&](uint32_t e) -> uint8_t {
 		return cb[e].fast ? cb[e].reads : ah_reads[(uint32_t)low[e].handler];
@@ -284,9 +337,23 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				sz += (r != 2 && inline_code(sval_of(e, r), &c)) ? 4 : 8;
 		return sz;
 	};
+	// structured-mode glue (SALU, encoded here): join head, conditional split, leaf continuation
+	std::vector<char> long_join(n, 0), long_leaf(n, 0);
+	const uint32_t LJ = 16; // s_add_u32 (8) + s_addc_u32 + s_setpc_b64: a jump anywhere
+	auto join_len = [&](uint32_t e) -> uint32_t {
+		return (structured && join_of[e] >= 0) ? (long_join[e] ? 8 + LJ : 8) : 0;
+	};
+	auto leaf_jumps = [&](uint32_t e) -> bool { // a leaf whose continuation is not next in layout
+		const uint32_t h = (uint32_t)low[e].handler;
+		if (!structured || !is_terminal(h))
+			return false;
+		const uint32_t k = idx[e];
+		const uint32_t nxt = k + 1 < order.size() ? order[k + 1] : GROUP_END;
+		return cont[e] != nxt;
+	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = (uint32_t)cb[e].prologue.size() + pre_len(e);
+		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() + pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
 			sz += (uint32_t)cb[e].body.size();
@@ -296,7 +363,9 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				sz += 4;
 		}
 		*body_end = sz;
-		if (ah_flags[h] & 1) {
+		if (structured && (ah_flags[h] & 1)) {
+			sz += long_cond[e] ? 12 + LJ : 12;
+		} else if (ah_flags[h] & 1) {
 			if (cb[e].sdir < 0)
 				sz += long_cond[e] ? cl_len : cs_len;
 			else if (cb[e].sdir == 1)
@@ -304,8 +373,13 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		}
 		if (needs_branch(e))
 			sz += long_br[e] ? jl_len : 4;
+		if (leaf_jumps(e))
+			sz += long_leaf[e] ? LJ : 4;
 		return sz;
 	};
+	// position of a continuation (GROUP_END: the block after the last one)
+	uint32_t end_pos = 0;
+	auto cont_pos = [&](uint32_t c) { return c == GROUP_END ? end_pos : pos[c]; };
 	uint32_t total = 0;
 	for (int iter = 0; iter < 8; iter++) {
 		total = 0;
@@ -314,12 +388,34 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			pos[e] = total;
 			total += block_size(e, &pre, &be);
 		}
+		end_pos = total;
+		if (structured)
+			total += LJ; // the group end: jump to .Lgroup_done
 		bool changed = false;
 		for (uint32_t e : order) {
 			uint32_t pre, be;
 			block_size(e, &pre, &be);
 			const uint32_t h = (uint32_t)low[e].handler;
-			if ((ah_flags[h] & 1) && !long_cond[e] && cb[e].sdir != 0) {
+			if (structured) {
+				if (join_of[e] >= 0 && !long_join[e] &&
+				    !fits_simm16((int64_t)cont_pos(cont[e]) - (int64_t)(pos[e] + 8))) {
+					long_join[e] = 1;
+					changed = true;
+				}
+				if ((ah_flags[h] & 1) && !long_cond[e] &&
+				    !fits_simm16((int64_t)pos[xl.entries[e].target] - (int64_t)(pos[e] + be + 12))) {
+					long_cond[e] = 1;
+					changed = true;
+				}
+				if (leaf_jumps(e) && !long_leaf[e]) {
+					const uint32_t br_at = pos[e] + block_size(e, &pre, &be) - 4;
+					if (!fits_simm16((int64_t)cont_pos(cont[e]) - (int64_t)(br_at + 4))) {
+						long_leaf[e] = 1;
+						changed = true;
+					}
+				}
+			}
+			if (!structured && (ah_flags[h] & 1) && !long_cond[e] && cb[e].sdir != 0) {
 				const uint32_t br_at = pos[e] + be + (cb[e].sdir == 1 ? 0 : T[JT_CS_BR] - T[JT_CS]);
 				const uint32_t tk = xl.entries[e].target;
 				if (!fits_simm16((int64_t)pos[tk] - (int64_t)(br_at + 4))) {
@@ -369,6 +465,31 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		const dp_entry &o = low[e];
 		const uint32_t h = (uint32_t)o.handler;
 		size_t at = pos[e];
+		// (a long jump: s_add_u32 s60, s4, off; s_addc_u32 s61, s5, 0; s_setpc_b64 s[60:61])
+		auto long_jump = [&](size_t a, uint32_t target_pos) {
+			put32(a, 0x80000000u | (60u << 16) | (255u << 8) | 4u);
+			put32(a + 4, T[JT_AREA] + target_pos);
+			put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
+			put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
+		};
+		auto sopp = [&](size_t a, uint32_t op, uint32_t target_pos) { // s_branch / s_cbranch_*
+			const int32_t d = ((int32_t)target_pos - (int32_t)(a + 4)) / 4;
+			put32(a, 0xbf800000u | (op << 16) | ((uint32_t)d & 0xffffu));
+		};
+		const uint32_t OP_BRANCH = 0x02, OP_EXECZ = 0x08, OP_EXECNZ = 0x09;
+		if (structured && join_of[e] >= 0) {
+			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[join_of[e]];
+			put32(at, 0xbe800000u | (126u << 16) | (0x01u << 8) | sk); // s_mov_b64 exec, s[Tk]
+			at += 4;
+			if (!long_join[e]) {
+				sopp(at, OP_EXECZ, cont_pos(cont[e]));
+				at += 4;
+			} else {
+				put32(at, 0xbf800000u | (OP_EXECNZ << 16) | (LJ / 4));
+				long_jump(at + 4, cont_pos(cont[e]));
+				at += 4 + LJ;
+			}
+		}
 		if (!cb[e].prologue.empty()) {
 			memcpy(&img[area + at], cb[e].prologue.data(), cb[e].prologue.size());
 			at += cb[e].prologue.size();
@@ -403,7 +524,22 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				at += 4;
 			}
 		}
-		if ((ah_flags[h] & 1) && cb[e].sdir == 1) { // statically taken by every lane
+		if (structured && (ah_flags[h] & 1)) {
+			// s_and_b64 s[Tk], vcc, exec; s_andn2_b64 exec, exec, vcc; s_cbranch_execz join
+			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[e];
+			put32(at, 0x80000000u | (0x0du << 23) | (sk << 16) | (126u << 8) | 106u);
+			put32(at + 4, 0x80000000u | (0x13u << 23) | (126u << 16) | (106u << 8) | 126u);
+			at += 8;
+			const uint32_t tk = xl.entries[e].target;
+			if (!long_cond[e]) {
+				sopp(at, OP_EXECZ, pos[tk]);
+				at += 4;
+			} else {
+				put32(at, 0xbf800000u | (OP_EXECNZ << 16) | (LJ / 4));
+				long_jump(at + 4, pos[tk]);
+				at += 4 + LJ;
+			}
+		} else if ((ah_flags[h] & 1) && cb[e].sdir == 1) { // statically taken by every lane
 			const uint32_t tk = xl.entries[e].target;
 			if (!long_cond[e]) {
 				copy_t(at, JT_BR, 4);
@@ -440,11 +576,27 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				at += jl_len;
 			}
 		}
+		if (leaf_jumps(e)) {
+			if (!long_leaf[e]) {
+				sopp(at, OP_BRANCH, cont_pos(cont[e]));
+				at += 4;
+			} else {
+				long_jump(at, cont_pos(cont[e]));
+				at += LJ;
+			}
+		}
 		uint32_t pre, be;
 		if (at != pos[e] + block_size(e, &pre, &be)) {
 			*err = "internal error: compiled block size mismatch";
 			return EINVAL;
 		}
+	}
+	if (structured) { // group end: every path has exited
+		const size_t a = end_pos;
+		put32(a, 0x80000000u | (60u << 16) | (255u << 8) | 4u);
+		put32(a + 4, T[JT_GDONE]);
+		put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
+		put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
 	}
 	if (code)
 		code->assign(img.begin() + area, img.begin() + area + total);
