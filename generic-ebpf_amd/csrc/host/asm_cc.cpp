@@ -249,6 +249,7 @@ struct facts {
 			st[nst++] = sslot{off, (uint8_t)size, (int8_t)reg};
 	}
 	bool nofwd = false;
+	bool t2zero = false; // v48 (T2) holds 0 in this path's lanes (the multiply addend's low word)
 	const sslot *slot(uint32_t off, int size) const
 	{
 		if (nofwd)
@@ -536,27 +537,28 @@ struct emitter {
 		const int nb = std::min(64, bits_of(x) + 64 - clz64(K));
 		const uint32_t lo = (uint32_t)K, hi = (uint32_t)(K >> 32);
 		const uint32_t klo = c3(lo);
+		// d * K mod 2^64 = lo(d) * lo(K) + ((hi(d) * lo(K) + lo(d) * hi(K)) << 32): the cross
+		// terms (low words only) go into the high word of the addend v[48:49] = {0, cross} of
+		// one v_mad_u64_u32 that writes d in place
 		if (hz(d) && hi == 0) {
-			// d < 2^32: the full 64-bit product of two 32-bit words
-			E.vop3(V3_MAD_U64_U32, T0, VGPR0 + L(d), klo, 128, S_JUNK);
-			E.vop1(V1_MOV_B64, L(d), vreg(T0));
-		} else if (hi == 0) {
-			E.vop3(V3_MUL_LO_U32, T2, VGPR0 + Hi(d), klo, 0);
-			E.vop3(V3_MAD_U64_U32, T0, VGPR0 + L(d), klo, 128, S_JUNK);
-			E.vop2(V2_ADD_U32, Hi(d), vreg(T1), T2);
-			E.vop1(V1_MOV_B32, L(d), vreg(T0));
-		} else if (hz(d)) {
-			E.vop3(V3_MUL_LO_U32, T2, VGPR0 + L(d), c3(hi), 0);
-			E.vop3(V3_MAD_U64_U32, T0, VGPR0 + L(d), klo, 128, S_JUNK);
-			E.vop2(V2_ADD_U32, Hi(d), vreg(T1), T2);
-			E.vop1(V1_MOV_B32, L(d), vreg(T0));
-		} else {
-			E.vop3(V3_MUL_LO_U32, T2, VGPR0 + L(d), c3(hi), 0);
-			E.vop3(V3_MUL_LO_U32, T3, VGPR0 + Hi(d), klo, 0);
-			E.vop3(V3_MAD_U64_U32, T0, VGPR0 + L(d), klo, 128, S_JUNK);
-			E.vop3(V3_ADD3_U32, Hi(d), VGPR0 + T1, VGPR0 + T2, VGPR0 + T3);
-			E.vop1(V1_MOV_B32, L(d), vreg(T0));
+			E.vop3(V3_MAD_U64_U32, L(d), VGPR0 + L(d), klo, 128, S_JUNK);
+			f.def(d, kbits(nb));
+			return;
 		}
+		if (!f.t2zero) {
+			mov32(T2, 0);
+			f.t2zero = true;
+		}
+		if (hi == 0) {
+			E.vop3(V3_MUL_LO_U32, T3, VGPR0 + Hi(d), klo, 0);
+		} else if (hz(d)) {
+			E.vop3(V3_MUL_LO_U32, T3, VGPR0 + L(d), c3(hi), 0);
+		} else {
+			E.vop3(V3_MUL_LO_U32, T3, VGPR0 + Hi(d), klo, 0);
+			E.vop3(V3_MUL_LO_U32, T1, VGPR0 + L(d), c3(hi), 0);
+			E.vop2(V2_ADD_U32, T3, vreg(T3), T1);
+		}
+		E.vop3(V3_MAD_U64_U32, L(d), VGPR0 + L(d), klo, VGPR0 + T2, S_JUNK);
 		f.def(d, kbits(nb));
 	}
 
@@ -1360,6 +1362,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			} else {
 				// the interpreter's body; the facts of what it writes are lost
 				f = before;
+				f.t2zero = false; // (handler bodies use v46..v51 freely)
 				blk.fast = false;
 				blk.body.clear();
 				blk.reads = 0;
@@ -1384,6 +1387,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				blk.body.clear();
 				blk.reads = 0;
 				f.pv[wr] = false;
+				f.t2zero = before.t2zero; // (its code, which may have zeroed v48, is gone)
 			}
 			// successors
 			if (fam == AHF_EXIT || fam == AHF_FAULT)

@@ -120,10 +120,10 @@ def test_optimised_c4_instruction_forms(native, env):
         # r8 = 0; r8 |= r4; r8 <<= 32; r8 |= r5  ->  moves
         "v_mov_b32_e32 v16, v8", "v_mov_b32_e32 v17, v16", "v_mov_b32_e32 v16, 0",
         "v_or_b32_e32 v16, v10, v16",
-        # MUL64 r8, 0x1e3779b1: two quarter-rate multiplies
-        "s_mov_b32 s13, 0x1e3779b1", "v_mul_lo_u32 v48, v17, s13",
-        "v_mad_u64_u32 v[46:47], s[60:61], v16, s13, 0", "v_add_u32_e32 v17, v47, v48",
-        "v_mov_b32_e32 v16, v46",
+        # MUL64 r8, 0x1e3779b1: the cross term into the addend {0, hi*K}, one in-place
+        # v_mad_u64_u32 (v48 = 0 is kept for the rest of the path)
+        "s_mov_b32 s13, 0x1e3779b1", "v_mov_b32_e32 v48, 0", "v_mul_lo_u32 v49, v17, s13",
+        "v_mad_u64_u32 v[16:17], s[60:61], v16, s13, v[48:49]",
         # XOR64 r8, imm with a zero high word: low half only
         "v_xor_b32_e32 v16, 0x5bd1e995, v16",
         # STXW [r10-4] = r6: one LDS store, offset folded
