@@ -1190,6 +1190,14 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vecto
 	enc P{out};
 	if (structured)
 		P.sop2(0x0e, 7, opnd{7}, opnd{128 + 4}); // s_or_b32 s7, s7, 4
+	// diagnostics only (EBPF_CC_PAD_SALU / _VALU = n): n filler instructions per group, to
+	// measure which issue port bounds a compiled program
+	if (const char *ps = getenv("EBPF_CC_PAD_SALU"))
+		for (int i = atoi(ps); i > 0; i--)
+			P.sop2(0x00, 60, opnd{60}, opnd{128 + 1}); // s_add_u32 s60, s60, 1
+	if (const char *pv = getenv("EBPF_CC_PAD_VALU"))
+		for (int i = atoi(pv); i > 0; i--)
+			P.vop2(V2_ADD_U32, 51, opnd{128 + 1}, 51); // v_add_u32 v51, 1, v51
 	const int V_PKT = 38, V_LEN = 40, H1 = 47, H3 = 49, S_DATA = 24;
 	if (mode == 1 && (needs_pkt || (live & (1u << 1)))) {
 		// staged kernel: packet address = data + index * 64 (index in v49, gen_interp.py H[3])

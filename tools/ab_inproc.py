@@ -25,11 +25,11 @@ def main():
     names = sys.argv[1:] or ["c0", "c4"]
     rounds, launches = 7, 20
     dev = torch.device("cuda", 0)
-    n = 1 << 26
+    n = int(os.environ.get("AB_PACKETS", 1 << 26))
     pk = workloads.packets_l2l3(1 << 22, 64, seed=3)
-    d_l2 = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(16)
+    d_l2 = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(max(1, n >> 22))
     rnd = workloads.packets_random(1 << 22, 64, seed=2)
-    d_rnd = torch.from_numpy(rnd.reshape(-1)).to(dev).repeat(16)
+    d_rnd = torch.from_numpy(rnd.reshape(-1)).to(dev).repeat(max(1, n >> 22))
     d_ret = torch.empty(n, dtype=torch.int64, device=dev)
     d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
@@ -64,14 +64,22 @@ def main():
             handles = [maps["c4"].handle]
         if opt == "nocc":
             os.environ["EBPF_JIT_NOCC"] = "1"
+        if opt.startswith("salu") or opt.startswith("valu"):   # issue-port probes
+            os.environ["EBPF_CC_PAD_" + opt[:4].upper()] = opt[4:]
         p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, handles))
         p.prepare(0)
         data = d_rnd if cfg in ("c0", "c2") else d_l2
+        if opt == "l2":      # the same program over the other packet buffer (placement check)
+            data = d_l2
+        elif opt == "rnd":
+            data = d_rnd
         # the program is compiled at its first launch
         p.run_batch_dev(0, data.data_ptr(), 64, 64, d_ret.data_ptr(), None, None, None,
                         stream.cuda_stream)
         torch.cuda.synchronize()
         os.environ.pop("EBPF_JIT_NOCC", None)
+        os.environ.pop("EBPF_CC_PAD_SALU", None)
+        os.environ.pop("EBPF_CC_PAD_VALU", None)
         cands.append((nm, p, data, path))
     times = {nm: [] for nm in names}
 
