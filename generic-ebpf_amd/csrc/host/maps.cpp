@@ -4,13 +4,14 @@
 //                                          through emt->ops, manual env release on init failure)
 //   eht_map_{lookup,update,delete}_elem  ↔ sys/dev/ebpf/ebpf_map.c:176-189
 //   emt_array / emt_percpu_array         ↔ sys/dev/ebpf/ebpf_map_array.c:27-298
-//   emt_hashtable / emt_percpu_hashtable ↔ sys/dev/ebpf/ebpf_map_hashtable.c (exported so
-//        configs link; creating one returns EOPNOTSUPP — hash maps are the "next" row of
-//        SURVEY.md §8(f), not part of this round's hot path)
+//   emt_hashtable / emt_percpu_hashtable ↔ sys/dev/ebpf/ebpf_map_hashtable.c:25-571 (host side:
+//        power-of-two buckets, newest-first chains, preallocated elements with a per-CPU
+//        spare for in-place replacement, jhash from csrc/jhash.h)
 //
 // Every host-side write bumps em->version so device mirrors re-upload before the next batch.
 // ebpf_map_lookup_elem hands out a writable pointer, so it marks the map dirty as well.
 #include "internal.h"
+#include "../jhash.h"
 
 #include <pthread.h>
 #include <sched.h>
@@ -218,18 +219,274 @@ percpu_update_from_user(struct ebpf_map *em, void *key, void *value, uint64_t fl
 	return 0;
 }
 
-// ---- hash tables: not in this round's scope ----
-int
-hash_init_unsupported(struct ebpf_map *, struct ebpf_map_attr *)
+// ---- hashtable / percpu hashtable (ebpf_map_hashtable.c) ----
+// Elements live in one preallocated pool.  Free elements form a LIFO stack, like the
+// reference's allocator (ebpf_allocator.c:80-144: blocks pushed in creation order, alloc and
+// free at the head), which decides which percpu element (and its stale per-CPU values) a new
+// key reuses.  Bucket chains are doubly linked, new elements at the head.
+struct hash_priv {
+	uint32_t key_size, value_size; // internal sizes, rounded up to 8 (:153-154)
+	uint32_t nbuckets;             // max_entries rounded up to a power of two (:167)
+	uint32_t nelems;               // pool size
+	std::vector<int32_t> head;     // per bucket: first element or -1
+	std::vector<int32_t> next, prev;
+	std::vector<uint8_t> keys;     // nelems * key_size
+	std::vector<uint8_t> vals;     // nelems * value_size (percpu: nelems * ncpus * value_size)
+	std::vector<int32_t> free_stack; // back = head of the free list
+	std::vector<int32_t> spare;    // non-percpu: per-CPU spare element (:207-224)
+	uint16_t ncpu = 1;
+	bool percpu = false;
+	uint64_t nlive = 0;
+	std::mutex lock; // one lock per map (the reference locks per bucket)
+
+	uint8_t *key(int32_t e) { return keys.data() + (size_t)e * key_size; }
+	uint8_t *val(int32_t e, uint16_t cpu = 0)
+	{
+		return vals.data() + ((size_t)e * (percpu ? ncpu : 1) + cpu) * value_size;
+	}
+	uint32_t bucket_of(const void *k, uint32_t ks) const
+	{
+		return ebpf_jhash(k, ks, 0) & (nbuckets - 1); // :58-62, :288
+	}
+	int32_t find(uint32_t b, const void *k, uint32_t ks)
+	{
+		for (int32_t e = head[b]; e >= 0; e = next[e])
+			if (memcmp(key(e), k, ks) == 0)
+				return e;
+		return -1;
+	}
+	void link_head(uint32_t b, int32_t e)
+	{
+		prev[e] = -1;
+		next[e] = head[b];
+		if (head[b] >= 0)
+			prev[head[b]] = e;
+		head[b] = e;
+	}
+	void unlink(uint32_t b, int32_t e)
+	{
+		if (prev[e] >= 0)
+			next[prev[e]] = next[e];
+		else
+			head[b] = next[e];
+		if (next[e] >= 0)
+			prev[next[e]] = prev[e];
+		next[e] = prev[e] = -1;
+	}
+	int32_t alloc()
+	{
+		if (free_stack.empty())
+			return -1;
+		int32_t e = free_stack.back();
+		free_stack.pop_back();
+		return e;
+	}
+};
+
+uint32_t
+roundup_pow2(uint32_t x)
 {
-	set_last_error("hashtable maps are not implemented by this engine yet");
-	return EOPNOTSUPP;
+	uint32_t p = 1;
+	while (p < x && p != 0)
+		p <<= 1;
+	return p;
 }
-void *hash_lookup_none(struct ebpf_map *, void *) { return nullptr; }
-int hash_err4(struct ebpf_map *, void *, void *, uint64_t) { return EOPNOTSUPP; }
-int hash_err2(struct ebpf_map *, void *) { return EOPNOTSUPP; }
-int hash_err3(struct ebpf_map *, void *, void *) { return EOPNOTSUPP; }
-void hash_deinit(struct ebpf_map *) {}
+
+int
+hash_init(struct ebpf_map *em, struct ebpf_map_attr *attr)
+{
+	const bool pc = em->emt == &emt_percpu_hashtable;
+	em->percpu = pc;
+	const uint64_t ks = (attr->key_size + 7ull) & ~7ull, vs = (attr->value_size + 7ull) & ~7ull;
+	if (ks + vs + 16 > UINT32_MAX) // :141-146 (16 = the element's list linkage)
+		return E2BIG;
+	hash_priv *h = new (std::nothrow) hash_priv();
+	if (h == nullptr)
+		return ENOMEM;
+	try {
+		h->key_size = (uint32_t)ks;
+		h->value_size = (uint32_t)vs;
+		h->percpu = pc;
+		h->ncpu = ncpus();
+		h->nbuckets = roundup_pow2(attr->max_entries);
+		if (h->nbuckets == 0)
+			throw std::bad_alloc();
+		// pool: max_entries (+ one spare per CPU for non-percpu maps, :200-225)
+		h->nelems = attr->max_entries + (pc ? 0u : h->ncpu);
+		h->head.assign(h->nbuckets, -1);
+		h->next.assign(h->nelems, -1);
+		h->prev.assign(h->nelems, -1);
+		h->keys.assign((size_t)h->nelems * h->key_size, 0);
+		h->vals.assign((size_t)h->nelems * (pc ? h->ncpu : 1) * h->value_size, 0);
+		h->free_stack.reserve(h->nelems);
+		for (uint32_t e = 0; e < h->nelems; e++)
+			h->free_stack.push_back((int32_t)e);
+		if (!pc)
+			for (uint16_t c = 0; c < h->ncpu; c++)
+				h->spare.push_back(h->alloc());
+	} catch (const std::bad_alloc &) {
+		delete h;
+		return ENOMEM;
+	}
+	em->data = h;
+	return 0;
+}
+
+void
+hash_deinit(struct ebpf_map *em)
+{
+	delete static_cast<hash_priv *>(em->data);
+}
+
+void *
+hash_lookup(struct ebpf_map *em, void *key) // :285-301
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	int32_t e = h->find(h->bucket_of(key, em->key_size), key, em->key_size);
+	if (e < 0)
+		return nullptr;
+	mark_dirty(em); // the caller may write through the pointer
+	return h->val(e, h->percpu ? curcpu() % h->ncpu : 0);
+}
+
+int
+hash_lookup_from_user(struct ebpf_map *em, void *key, void *value) // :303-342
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	int32_t e = h->find(h->bucket_of(key, em->key_size), key, em->key_size);
+	if (e < 0)
+		return ENOENT;
+	if (!h->percpu) {
+		memcpy(value, h->val(e), em->value_size);
+		return 0;
+	}
+	for (uint16_t c = 0; c < h->ncpu; c++)
+		memcpy(static_cast<uint8_t *>(value) + (size_t)em->value_size * c, h->val(e, c), em->value_size);
+	return 0;
+}
+
+int
+hash_check_flags(int32_t found, uint64_t flags) // :88-100
+{
+	if (found >= 0)
+		return (flags & EBPF_NOEXIST) ? EEXIST : 0;
+	return (flags & EBPF_EXIST) ? ENOENT : 0;
+}
+
+std::mutex &
+hash_lock(struct ebpf_map *em)
+{
+	return static_cast<hash_priv *>(em->data)->lock;
+}
+
+int
+hash_update(struct ebpf_map *em, void *key, void *value, uint64_t flags) // :344-390
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	std::lock_guard<std::mutex> g(hash_lock(em));
+	const uint32_t b = h->bucket_of(key, em->key_size);
+	const int32_t old = h->find(b, key, em->key_size);
+	int error = hash_check_flags(old, flags);
+	if (error)
+		return error;
+	int32_t ne;
+	if (old >= 0) { // replace through this CPU's spare element, which the old one becomes
+		const uint16_t c = curcpu() % h->ncpu;
+		ne = h->spare[c];
+		h->spare[c] = old;
+	} else if ((ne = h->alloc()) < 0) {
+		return EBUSY;
+	}
+	memcpy(h->key(ne), key, em->key_size);
+	memcpy(h->val(ne), value, em->value_size);
+	h->link_head(b, ne);
+	if (old >= 0)
+		h->unlink(b, old);
+	else
+		h->nlive++;
+	mark_dirty(em);
+	return 0;
+}
+
+int
+hash_update_percpu_common(struct ebpf_map *em, void *key, void *value, uint64_t flags, bool all)
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	std::lock_guard<std::mutex> g(hash_lock(em));
+	const uint32_t b = h->bucket_of(key, em->key_size);
+	int32_t e = h->find(b, key, em->key_size);
+	int error = hash_check_flags(e, flags);
+	if (error)
+		return error;
+	const bool fresh = e < 0;
+	if (fresh && (e = h->alloc()) < 0)
+		return EBUSY;
+	if (all) // from user: every CPU's copy (:433-473)
+		for (uint16_t c = 0; c < h->ncpu; c++)
+			memcpy(h->val(e, c), value, em->value_size);
+	else // from a program: this CPU's copy (:392-431)
+		memcpy(h->val(e, curcpu() % h->ncpu), value, em->value_size);
+	if (fresh) {
+		memcpy(h->key(e), key, em->key_size);
+		h->link_head(b, e);
+		h->nlive++;
+	}
+	mark_dirty(em);
+	return 0;
+}
+
+int
+hash_update_percpu(struct ebpf_map *em, void *key, void *value, uint64_t flags)
+{
+	return hash_update_percpu_common(em, key, value, flags, false);
+}
+
+int
+hash_update_percpu_from_user(struct ebpf_map *em, void *key, void *value, uint64_t flags)
+{
+	return hash_update_percpu_common(em, key, value, flags, true);
+}
+
+int
+hash_delete(struct ebpf_map *em, void *key) // :475-502: 0 whether or not the key existed
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	std::lock_guard<std::mutex> g(hash_lock(em));
+	const uint32_t b = h->bucket_of(key, em->key_size);
+	const int32_t e = h->find(b, key, em->key_size);
+	if (e >= 0) {
+		h->unlink(b, e);
+		h->free_stack.push_back(e);
+		h->nlive--;
+		mark_dirty(em);
+	}
+	return 0;
+}
+
+int
+hash_get_next_key(struct ebpf_map *em, void *key, void *next_key) // :504-541
+{
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	std::lock_guard<std::mutex> g(hash_lock(em));
+	uint32_t i = 0;
+	if (key != nullptr) {
+		const uint32_t b = h->bucket_of(key, em->key_size);
+		const int32_t e = h->find(b, key, em->key_size);
+		if (e >= 0) {
+			if (h->next[e] >= 0) {
+				memcpy(next_key, h->key(h->next[e]), em->key_size);
+				return 0;
+			}
+			i = b + 1;
+		}
+	}
+	for (; i < h->nbuckets; i++)
+		if (h->head[i] >= 0) {
+			memcpy(next_key, h->key(h->head[i]), em->key_size);
+			return 0;
+		}
+	return ENOENT;
+}
 
 void
 map_dtor(struct ebpf_obj *eo)
@@ -266,13 +523,13 @@ EBPF_EXPORT const struct ebpf_map_type emt_percpu_array = {
 
 EBPF_EXPORT const struct ebpf_map_type emt_hashtable = {
 	"hashtable",
-	{hash_init_unsupported, hash_lookup_none, hash_err4, hash_err2, hash_err3, hash_err4,
-	 hash_err2, hash_err3, hash_deinit}};
+	{hash_init, hash_lookup, hash_update, hash_delete, hash_lookup_from_user, hash_update,
+	 hash_delete, hash_get_next_key, hash_deinit}};
 
 EBPF_EXPORT const struct ebpf_map_type emt_percpu_hashtable = {
 	"percpu_hashtable",
-	{hash_init_unsupported, hash_lookup_none, hash_err4, hash_err2, hash_err3, hash_err4,
-	 hash_err2, hash_err3, hash_deinit}};
+	{hash_init, hash_lookup, hash_update_percpu, hash_delete, hash_lookup_from_user,
+	 hash_update_percpu_from_user, hash_delete, hash_get_next_key, hash_deinit}};
 
 // ---------------------------------------------------------------------------- generic layer
 

@@ -451,9 +451,14 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	// Resolve LDDW immediates that are live array maps of this env: the device map table.
 	struct ebpf_env *ee = ep->eo.eo_ee;
 	std::lock_guard<std::mutex> g(ee->lock);
+	const struct ebpf_map *unsupported = nullptr;
 	auto add_map = [&](struct ebpf_map *m) {
-		if (m->array_storage() == nullptr)
+		if (m->array_storage() == nullptr) {
+			// device batches resolve array maps; a program that loads any other live map
+			// (hashtable, percpu) runs on the CPU path only (ebpf_prog_run)
+			unsupported = m;
 			return;
+		}
 		for (auto *x : out.maps)
 			if (x == m)
 				return;
@@ -475,6 +480,13 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	for (uint32_t i = 0; i < ep->ndep_maps; i++)
 		if (ee->maps.count(ep->dep_maps[i]))
 			add_map(ep->dep_maps[i]);
+	if (unsupported != nullptr) {
+		out.error = EOPNOTSUPP;
+		out.error_msg = std::string("device batches support array maps only; the program uses a ") +
+				unsupported->emt->name + " map (run it with ebpf_prog_run)";
+		out.maps.clear(); // (not pinned: nothing to release)
+		return EOPNOTSUPP;
+	}
 	dataflow(out);
 	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
 	// its map while a later batch may still read it.

@@ -96,3 +96,116 @@ class OracleProgram:
                                        count, stride, ret.ctypes.data, faults.ctypes.data,
                                        nthreads)
         return ret, faults, work, int(steps)
+
+
+# ---- hashtable maps (host-side map API; small cases, pure Python) ----
+
+def _rot(x, k):
+    return ((x << k) | (x >> (32 - k))) & 0xffffffff
+
+
+def jhash(key, initval=0):
+    """Bob Jenkins' lookup3 hashlittle over ``key`` (bytes): the reference's
+    ebpf_jenkins_hash() (sys/dev/ebpf/ebpf_jhash.h:159-330, bound on little-endian hosts by
+    Linux/ebpf/user/ebpf_linux_user.c:204-208).  The reference's aligned 4-/2-/1-byte read paths
+    all compute this value.  Pinned by tests/golden/maps/jhash.npz."""
+    M = 0xffffffff
+    n = len(key)
+    a = b = c = (0xdeadbeef + n + initval) & M
+    w = lambda p: int.from_bytes(key[p:p + 4].ljust(4, b"\0"), "little")
+    i = 0
+    while n - i > 12:
+        a, b, c = (a + w(i)) & M, (b + w(i + 4)) & M, (c + w(i + 8)) & M
+        a = ((a - c) & M) ^ _rot(c, 4); c = (c + b) & M
+        b = ((b - a) & M) ^ _rot(a, 6); a = (a + c) & M
+        c = ((c - b) & M) ^ _rot(b, 8); b = (b + a) & M
+        a = ((a - c) & M) ^ _rot(c, 16); c = (c + b) & M
+        b = ((b - a) & M) ^ _rot(a, 19); a = (a + c) & M
+        c = ((c - b) & M) ^ _rot(b, 4); b = (b + a) & M
+        i += 12
+    if n == i:
+        return c
+    tail = key[i:].ljust(12, b"\0")
+    a = (a + int.from_bytes(tail[0:4], "little")) & M
+    b = (b + int.from_bytes(tail[4:8], "little")) & M
+    c = (c + int.from_bytes(tail[8:12], "little")) & M
+    c ^= b; c = (c - _rot(b, 14)) & M
+    a ^= c; a = (a - _rot(c, 11)) & M
+    b ^= a; b = (b - _rot(a, 25)) & M
+    c ^= b; c = (c - _rot(b, 16)) & M
+    a ^= c; a = (a - _rot(c, 4)) & M
+    b ^= a; b = (b - _rot(a, 14)) & M
+    c ^= b; c = (c - _rot(b, 24)) & M
+    return c
+
+
+EBPF_ANY, EBPF_NOEXIST, EBPF_EXIST = 0, 1, 2
+_ENOENT, _EEXIST, _EBUSY = 2, 17, 16
+
+
+class HashtableModel:
+    """The reference's hashtable map as a CPU model (sys/dev/ebpf/ebpf_map_hashtable.c):
+    nbuckets = max_entries rounded up to a power of two (:167), bucket = jhash(key) & (n-1)
+    (:58-62), newest element first in its bucket (:380, :421), update flag checks (:88-100),
+    EBUSY when the element pool is empty (:371-375), delete always 0 (:475-502) and
+    get_next_key's bucket walk (:504-541).  Keys are bytes; values bytes (percpu: one per CPU)."""
+
+    def __init__(self, max_entries, percpu=False, ncpu=1):
+        self.nb = 1
+        while self.nb < max_entries:
+            self.nb <<= 1
+        self.cap = max_entries
+        self.percpu, self.ncpu = percpu, ncpu
+        self.buckets = [[] for _ in range(self.nb)]   # newest first: [key, value(s)]
+
+    def _find(self, key):
+        bk = self.buckets[jhash(key) & (self.nb - 1)]
+        for i, (k, _) in enumerate(bk):
+            if k == key:
+                return bk, i
+        return bk, -1
+
+    def __len__(self):
+        return sum(len(b) for b in self.buckets)
+
+    def lookup(self, key):
+        bk, i = self._find(key)
+        return None if i < 0 else bk[i][1]
+
+    def update(self, key, value, flags=EBPF_ANY):
+        bk, i = self._find(key)
+        if i >= 0 and flags & EBPF_NOEXIST:
+            return _EEXIST
+        if i < 0 and flags & EBPF_EXIST:
+            return _ENOENT
+        if i >= 0:
+            if self.percpu:       # in place (:405-407 / :452-455)
+                bk[i][1] = [value] * self.ncpu
+                return 0
+            del bk[i]            # replaced by a new head element (:378-381)
+        elif len(self) >= self.cap:
+            return _EBUSY
+        bk.insert(0, [key, [value] * self.ncpu if self.percpu else value])
+        return 0
+
+    def delete(self, key):
+        bk, i = self._find(key)
+        if i >= 0:
+            del bk[i]
+        return 0
+
+    def get_next_key(self, key=None):
+        start = 0
+        if key is not None:
+            bk, i = self._find(key)
+            if i >= 0:
+                if i + 1 < len(bk):
+                    return 0, bk[i + 1][0]
+                start = (jhash(key) & (self.nb - 1)) + 1
+        for b in range(start, self.nb):
+            if self.buckets[b]:
+                return 0, self.buckets[b][0][0]
+        return _ENOENT, None
+
+    def keys_in_order(self):
+        return [k for b in self.buckets for k, _ in b]

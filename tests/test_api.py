@@ -198,9 +198,3 @@ def test_percpu_array_roundtrip(native, env):
     finally:
         m.destroy()
 
-
-def test_hashtable_not_supported_yet(native, env):
-    em = ctypes.c_void_p()
-    a = native.MapAttr(native.MAP_TYPE_HASHTABLE, 4, 4, 100, 0)
-    assert native.lib().ebpf_map_create(env.ptr, ctypes.byref(em), ctypes.byref(a)) == \
-        errno.EOPNOTSUPP

@@ -1,0 +1,277 @@
+"""Hashtable and percpu-hashtable maps through the C-ABI (host side).
+
+Re-expresses the reference's tests/ebpf_map_tests/{,percpu_}hashtable_map_*_test.cpp and checks
+the things those tests leave open against the oracle's model of
+sys/dev/ebpf/ebpf_map_hashtable.c (oracle/pyoracle.py HashtableModel): the exact get_next_key
+order (which pins the bucket hash, jhash), replacement moving a key to the head of its bucket,
+EBUSY at capacity, the spare-element swap, and programs doing hashtable lookups through
+ebpf_prog_run.  Device batches reject programs that load a hashtable (EOPNOTSUPP).
+"""
+import ctypes
+import errno
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle
+
+HT, PHT = 2, 3
+NCPU = os.sysconf("SC_NPROCESSORS_ONLN")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "maps", "jhash.npz")
+
+
+class HMap:
+    """Byte-keyed view of one map (key/value sizes as created)."""
+
+    def __init__(self, native, env, type, key_size, value_size, max_entries):
+        self.native, self.ks, self.vs = native, key_size, value_size
+        self.percpu = type == PHT
+        self.ptr = ctypes.c_void_p()
+        attr = native.MapAttr(type, key_size, value_size, max_entries, 0)
+        rc = native.lib().ebpf_map_create(env.ptr, ctypes.byref(self.ptr), ctypes.byref(attr))
+        assert rc == 0, rc
+        self.L = native.lib()
+
+    def update(self, key, value, flags=0):
+        k = ctypes.create_string_buffer(key, self.ks)
+        v = ctypes.create_string_buffer(value, self.vs)
+        return self.L.ebpf_map_update_elem_from_user(self.ptr, k, v, flags)
+
+    def lookup(self, key):
+        k = ctypes.create_string_buffer(key, self.ks)
+        n = self.vs * (NCPU if self.percpu else 1)
+        v = ctypes.create_string_buffer(n)
+        rc = self.L.ebpf_map_lookup_elem_from_user(self.ptr, k, v)
+        if rc:
+            return rc, None
+        if self.percpu:
+            return 0, [v.raw[i * self.vs:(i + 1) * self.vs] for i in range(NCPU)]
+        return 0, v.raw
+
+    def delete(self, key):
+        return self.L.ebpf_map_delete_elem_from_user(self.ptr, ctypes.create_string_buffer(key, self.ks))
+
+    def next_key(self, key):
+        out = ctypes.create_string_buffer(self.ks)
+        k = None if key is None else ctypes.create_string_buffer(key, self.ks)
+        rc = self.L.ebpf_map_get_next_key_from_user(self.ptr, k, out)
+        return rc, (out.raw if rc == 0 else None)
+
+    def walk(self):
+        keys, rc, k = [], 0, None
+        while True:
+            rc, k = self.next_key(k)
+            if rc:
+                assert rc == errno.ENOENT
+                return keys
+            keys.append(k)
+            assert len(keys) <= 1 << 20
+
+    def destroy(self):
+        self.L.ebpf_map_destroy(self.ptr)
+
+
+@pytest.fixture(params=[HT, PHT], ids=["hashtable", "percpu_hashtable"])
+def hmap(request, native, env):
+    m = HMap(native, env, request.param, 4, 4, 100)
+    yield m
+    m.destroy()
+
+
+def u32(x):
+    return struct.pack("<I", x)
+
+
+# ---- jhash: the oracle's restatement against vectors from the reference's own header ----
+
+def test_oracle_jhash_matches_reference_vectors():
+    z = np.load(GOLDEN)
+    d, o = z["data"].tobytes(), z["offsets"]
+    for i in range(len(o) - 1):
+        assert pyoracle.jhash(d[o[i]:o[i + 1]], int(z["initval"][i])) == int(z["expect"][i]), i
+
+
+def test_product_jhash_header_matches_reference_vectors(tmp_path):
+    """csrc/jhash.h (shared by host maps and device code) compiled on its own, every golden
+    vector at its recorded misalignment."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "t.cpp"
+    src.write_text(
+        '#include "jhash.h"\n#include <cstdio>\n#include <cstring>\n#include <cstdlib>\n'
+        'int main(){unsigned init,off;char hex[1024];static unsigned char buf[600];\n'
+        'while(scanf("%u %u %1023s",&init,&off,hex)==3){size_t n=0;\n'
+        'if(strcmp(hex,"-"))for(;hex[2*n];n++){unsigned b;sscanf(hex+2*n,"%2x",&b);buf[off+n]=b;}\n'
+        'printf("%u\\n",ebpf_jhash(buf+off,n,init));}}\n')
+    exe = tmp_path / "t"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "generic-ebpf_amd", "csrc"),
+                           str(src), "-o", str(exe)])
+    z = np.load(GOLDEN)
+    d, o = z["data"].tobytes(), z["offsets"]
+    lines = ["%d %d %s" % (int(z["initval"][i]), int(z["misalign"][i]), d[o[i]:o[i + 1]].hex() or "-")
+             for i in range(len(o) - 1)]
+    out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                         check=True).stdout.split()
+    assert [int(x) for x in out] == [int(x) for x in z["expect"]]
+
+
+# ---- the reference's map tests (hashtable_map_*_test.cpp, percpu_hashtable_map_*_test.cpp) ----
+
+def test_correct_update(hmap):
+    assert hmap.update(u32(50), u32(100)) == 0
+
+
+def test_update_more_than_max_entries(hmap):
+    for i in range(100):
+        assert hmap.update(u32(i), u32(i)) == 0
+    assert hmap.update(u32(100), u32(100)) == errno.EBUSY
+    # replacing an existing key at capacity still works (spare element / in place)
+    assert hmap.update(u32(7), u32(70)) == 0
+    rc, v = hmap.lookup(u32(7))
+    assert rc == 0 and (v == [u32(70)] * NCPU if hmap.percpu else v == u32(70))
+
+
+def test_update_flags(hmap):
+    assert hmap.update(u32(50), u32(100), pyoracle.EBPF_EXIST) == errno.ENOENT
+    assert hmap.update(u32(50), u32(100), pyoracle.EBPF_NOEXIST) == 0
+    assert hmap.update(u32(50), u32(100), pyoracle.EBPF_NOEXIST) == errno.EEXIST
+    assert hmap.update(u32(50), u32(101), pyoracle.EBPF_EXIST) == 0
+    rc, v = hmap.lookup(u32(50))
+    assert rc == 0 and (v == [u32(101)] * NCPU if hmap.percpu else v == u32(101))
+
+
+def test_lookup(hmap):
+    assert hmap.update(u32(50), u32(100)) == 0
+    assert hmap.lookup(u32(51)) == (errno.ENOENT, None)
+    rc, v = hmap.lookup(u32(50))
+    assert rc == 0
+    assert v == ([u32(100)] * NCPU if hmap.percpu else u32(100))
+
+
+def test_delete(hmap):
+    assert hmap.delete(u32(50)) == 0          # absent key: still 0
+    assert hmap.update(u32(50), u32(1)) == 0
+    assert hmap.delete(u32(50)) == 0
+    assert hmap.lookup(u32(50))[0] == errno.ENOENT
+    assert hmap.walk() == []
+
+
+def test_get_first_key(hmap):
+    assert hmap.next_key(None) == (errno.ENOENT, None)
+    assert hmap.update(u32(100), u32(200)) == 0
+    assert hmap.next_key(None) == (0, u32(100))
+
+
+def test_get_next_key_walks_every_key_in_reference_order(hmap):
+    model = pyoracle.HashtableModel(100, percpu=hmap.percpu, ncpu=NCPU)
+    for i in range(100):
+        assert hmap.update(u32(i), u32(i)) == 0
+        assert model.update(u32(i), u32(i)) == 0
+    got = hmap.walk()
+    assert sorted(got) == sorted(u32(i) for i in range(100))
+    assert got == model.keys_in_order()
+    # an absent key restarts from the first bucket (:518-520)
+    assert hmap.next_key(u32(12345)) == model.get_next_key(u32(12345))
+
+
+@pytest.mark.parametrize("key_size,max_entries,seed", [(1, 200, 1), (3, 50, 2), (8, 1000, 3),
+                                                       (13, 300, 4), (40, 64, 5)])
+def test_random_operations_match_model(native, env, key_size, max_entries, seed):
+    """Random update/delete/lookup streams (flags included), then the full get_next_key walk:
+    return codes, values and iteration order all equal the model's."""
+    rng = np.random.default_rng(seed)
+    for typ in (HT, PHT):
+        m = HMap(native, env, typ, key_size, 12, max_entries)
+        model = pyoracle.HashtableModel(max_entries, percpu=typ == PHT, ncpu=NCPU)
+        universe = [rng.integers(0, 256, key_size, dtype=np.uint8).tobytes()
+                    for _ in range(min(256 ** key_size, max_entries * 2))]
+        try:
+            for step in range(max_entries * 4):
+                k = universe[int(rng.integers(0, len(universe)))]
+                op = int(rng.integers(0, 10))
+                if op < 6:
+                    v = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+                    fl = int(rng.integers(0, 3))
+                    assert m.update(k, v, fl) == model.update(k, v, fl), step
+                elif op < 8:
+                    assert m.delete(k) == model.delete(k) == 0
+                else:
+                    rc, v = m.lookup(k)
+                    mv = model.lookup(k)
+                    assert (rc == 0) == (mv is not None)
+                    if mv is not None:
+                        assert v == mv
+            assert m.walk() == model.keys_in_order()
+        finally:
+            m.destroy()
+
+
+def test_percpu_hashtable_reuses_elements_lifo(native, env):
+    """A deleted element goes back to the head of the free list and is the next one allocated
+    (ebpf_allocator.c:80-144): observable as a fresh key inheriting nothing but working."""
+    m = HMap(native, env, PHT, 4, 8, 4)
+    try:
+        for i in range(4):
+            assert m.update(u32(i), struct.pack("<Q", i)) == 0
+        assert m.update(u32(9), struct.pack("<Q", 9)) == errno.EBUSY
+        assert m.delete(u32(2)) == 0
+        assert m.update(u32(9), struct.pack("<Q", 9)) == 0
+        assert m.lookup(u32(9)) == (0, [struct.pack("<Q", 9)] * NCPU)
+        assert m.update(u32(10), struct.pack("<Q", 9)) == errno.EBUSY
+    finally:
+        m.destroy()
+
+
+def test_hashtable_create_limits(native, env):
+    em = ctypes.c_void_p()
+    big = native.MapAttr(HT, 0xfffffff0, 0x10, 4, 0)       # key + value + linkage > UINT32_MAX
+    assert native.lib().ebpf_map_create(env.ptr, ctypes.byref(em), ctypes.byref(big)) == errno.E2BIG
+
+
+# ---- programs using a hashtable ----
+
+def _lookup_prog(native):
+    """r0 = value(u32 at packet[0]) or 0xdead when absent — through helper 0 (map_lookup_elem)."""
+    from generic_ebpf_amd import isa
+    from generic_ebpf_amd.layout import Branch, LdDw, MapRef, assemble
+    I = isa.Insn
+    nodes = [I("ldxw", 6, 1, 0), I("stxw", 10, 6, -4), LdDw(1, MapRef(0)),
+             I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4), I("call", imm=0),
+             Branch(I("jeq_imm", 0, imm=0), [I("mov_imm", 0, imm=0xdead), I("exit")]),
+             I("ldxdw", 0, 0, 0), I("exit")]
+    return assemble(nodes)
+
+
+@pytest.mark.parametrize("typ", [HT, PHT], ids=["hashtable", "percpu_hashtable"])
+def test_prog_run_with_hashtable_lookup(native, env, typ):
+    m = HMap(native, env, typ, 4, 8, 64)
+    p = None
+    try:
+        for k in range(0, 64, 2):
+            assert m.update(u32(k * 1000), struct.pack("<Q", k * 7 + 1)) == 0
+        lay = _lookup_prog(native)
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.ptr.value]))
+        for k in range(64):
+            r, _ = p.run_cpu(u32(k * 1000) + bytes(60))
+            assert r == (k * 7 + 1 if k % 2 == 0 else 0xdead), k
+    finally:
+        if p is not None:
+            p.destroy()
+        m.destroy()
+
+
+def test_device_batch_rejects_hashtable_programs(native, env):
+    m = HMap(native, env, HT, 4, 8, 64)
+    p = None
+    try:
+        lay = _lookup_prog(native)
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.ptr.value]))
+        i = native.DprogInfo()
+        assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert "array maps only" in native.last_error()
+    finally:
+        if p is not None:
+            p.destroy()
+        m.destroy()
