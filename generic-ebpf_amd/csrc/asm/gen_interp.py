@@ -135,6 +135,7 @@ for n in ("EXIT", "FAULT", "NOP", "LOOKUPSTK", "LOOKUPGEN"):
     fam(n, 0)
 for z in SIZES:
     fam("LDXPKC%d" % z, 3)      # staged packet load at a constant byte offset: (dst, offset)
+fam("HLOOKUP", 0)              # hashtable lookup, map known at translation time (s14 = record offset)
 
 
 def variants(arity):
@@ -557,6 +558,146 @@ def h_lookup_stk():
             "v_cndmask_b32 v1, 0, %s, vcc" % v(H[3])]
 
 
+def _hl_word(dst, off, n):
+    """dst = the little-endian key word at byte offset s[off] of the key at H[0:1], bytes at or
+    past the key size (S_T0) read as 0 (jhash's zero-padded tail; the device table stores keys
+    zero-padded the same way).  Clobbers R[8:10], H[3:5], S_BYTES, vcc."""
+    t = [v(R[10]), v(H[3]), v(H[4]), v(H[5])]
+    out = ["v_add_co_u32 %s, vcc, %s, %s" % (v(R[8]), s(off), v(H[0])),
+           "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[9]), v(H[1]))]
+    for j in range(4):
+        out += ["s_add_u32 %s, %s, %d" % (s(S_BYTES), s(off), j + 1),
+                "s_cmp_le_u32 %s, %s" % (s(S_BYTES), s(S_T0)),
+                "s_cbranch_scc0 .Lhw_z%d_%d" % (n, j),
+                "flat_load_ubyte %s, %s offset:%d" % (t[j], vp(R[8]), j),
+                "s_branch .Lhw_d%d_%d" % (n, j),
+                ".Lhw_z%d_%d:" % (n, j),
+                "v_mov_b32 %s, 0" % t[j],
+                ".Lhw_d%d_%d:" % (n, j)]
+    out += ["s_waitcnt vmcnt(0) lgkmcnt(0)",
+            "v_lshl_or_b32 %s, %s, 8, %s" % (dst, t[1], t[0]),
+            "v_lshl_or_b32 %s, %s, 16, %s" % (dst, t[2], dst),
+            "v_lshl_or_b32 %s, %s, 24, %s" % (dst, t[3], dst)]
+    return out
+
+
+def _rot(d, x, k):
+    """d = rotl32(x, k)"""
+    return ["v_alignbit_b32 %s, %s, %s, %d" % (d, x, x, 32 - k)]
+
+
+def hlookup_routine():
+    """HLOOKUP (called): r0 = hashtable_map_lookup_elem(map, r2) for the map whose dp_map record
+    is at byte offset s14 of the map table (ebpf_map.c:77-84 -> ebpf_map_hashtable.c:285-301).
+    The key (key_size bytes at r2, anywhere a program may read) is region-checked like a load,
+    hashed with jhash (ebpf_jhash.h hashlittle, initval 0) and probed linearly in the device
+    table (dprog.h dp_map): a lane stops at its key (r0 = the slot's value) or at an empty slot
+    (r0 = NULL).  r2 == 0 gives NULL with no access, as the reference's NULL-key check.
+    Uses s[8:9] (return address), s[10:11] (entry exec), R[*], H[*]; compiled programs treat
+    s10..s11 as clobbered after it."""
+    a, b, c = v(R[0]), v(R[1]), v(R[2])
+    t = v(R[3])
+    L = [".Lr_hlookup:",
+         "s_mov_b64 s[8:9], %s" % sp(S_LINK),
+         "s_mov_b64 s[10:11], exec",
+         "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
+         "v_cmp_ne_u64_e64 vcc, 0, v[4:5]",
+         "s_and_b64 exec, exec, vcc",              # NULL keys: r0 = NULL, nothing read
+         "s_cbranch_execz .Lhl_ret",
+         "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+         "s_waitcnt lgkmcnt(0)",
+         "s_and_b32 %s, s71, 0xffff" % s(S_T0),    # key size
+         "s_mov_b32 %s, 0" % s(S_T1),
+         "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1])] + call(".Lr_check") + [
+         # exec = the lanes whose key is readable (the others retired with a fault); a
+         # structured compiled program may come back with none
+         "s_cbranch_execz .Lhl_ret",
+         "s_mov_b64 %s, exec" % sp(S_MASK),
+         "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+         "s_waitcnt lgkmcnt(0)",
+         "s_and_b32 %s, s71, 0xffff" % s(S_T0),             # key size
+         "s_bfe_u32 %s, s71, 0x50010" % s(S_T1),            # log2 slot stride (5 bits at 16)
+         "s_sub_u32 s69, s69, 1",                            # slot mask
+         "s_add_u32 s70, %s, 15" % s(S_T0),
+         "s_and_b32 s70, s70, -8",                           # value offset 8 + round8(key size)
+         # jhash: a = b = c = 0xdeadbeef + length (+ initval 0)
+         "s_add_u32 %s, %s, 0xdeadbeef" % (s(S_JUNK), s(S_T0)),
+         "v_mov_b32 %s, %s" % (a, s(S_JUNK)), "v_mov_b32 %s, %s" % (b, s(S_JUNK)),
+         "v_mov_b32 %s, %s" % (c, s(S_JUNK)),
+         "s_mov_b32 %s, 0" % s(S_T2),                       # byte offset
+         "s_mov_b32 %s, %s" % (s(S_T3), s(S_T0)),           # bytes left
+         ".Lhh_loop:",
+         "s_cmp_le_u32 %s, 12" % s(S_T3),
+         "s_cbranch_scc1 .Lhh_tail"]
+    n = [0]
+
+    def add_words():
+        out = []
+        for x in (a, b, c):
+            out += _hl_word(t, S_T2, n[0])
+            n[0] += 1
+            out += ["v_add_u32 %s, %s, %s" % (x, x, t), "s_add_u32 %s, %s, 4" % (s(S_T2), s(S_T2))]
+        return out
+    L += add_words()
+    for (x, y, z, k) in ((a, c, b, 4), (b, a, c, 6), (c, b, a, 8), (a, c, b, 16), (b, a, c, 19),
+                         (c, b, a, 4)):
+        # x -= y; x ^= rot(y, k); y += z
+        L += ["v_sub_u32 %s, %s, %s" % (x, x, y)] + _rot(t, y, k) + \
+             ["v_xor_b32 %s, %s, %s" % (x, x, t), "v_add_u32 %s, %s, %s" % (y, y, z)]
+    L += ["s_sub_u32 %s, %s, 12" % (s(S_T3), s(S_T3)),
+          "s_branch .Lhh_loop",
+          ".Lhh_tail:"]
+    L += add_words()
+    for (x, y, k) in ((c, b, 14), (a, c, 11), (b, a, 25), (c, b, 16), (a, c, 4), (b, a, 14), (c, b, 24)):
+        # x ^= y; x -= rot(y, k)
+        L += ["v_xor_b32 %s, %s, %s" % (x, x, y)] + _rot(t, y, k) + ["v_sub_u32 %s, %s, %s" % (x, x, t)]
+    # probe: slot i = hash & mask, then i + 1, ... until the key or an empty slot
+    idx, sa, hd = v(R[3]), vp(R[4]), vp(R[6])
+    L += ["v_and_b32 %s, s69, %s" % (idx, c),
+          "s_mov_b64 %s, exec" % sp(S_OK),                  # lanes still probing
+          ".Lhp_loop:",
+          "v_mov_b32 %s, %s" % (v(R[4]), idx),
+          "v_mov_b32 %s, 0" % v(R[5]),
+          "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
+          "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
+          "global_load_dwordx2 %s, %s, off" % (hd, sa),
+          "s_waitcnt vmcnt(0)",
+          "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),          # empty slot: not found
+          "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
+          "s_and_b64 exec, exec, %s" % sp(S_OK),
+          "v_cmp_eq_u32_e64 vcc, %s, %s" % (v(R[7]), c),    # stored hash matches: compare keys
+          "s_and_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lhp_next",
+          "s_mov_b32 %s, 0" % s(S_T2),
+          ".Lhc_loop:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_T0)),
+          "s_cbranch_scc1 .Lhc_found"] + _hl_word(v(R[6]), S_T2, 99) + [
+          "v_add_co_u32 %s, vcc, %s, %s" % (v(R[8]), s(S_T2), v(R[4])),
+          "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[9]), v(R[5])),
+          "global_load_dword %s, %s, off offset:8" % (v(R[7]), vp(R[8])),
+          "s_waitcnt vmcnt(0)",
+          "v_cmp_ne_u32_e64 vcc, %s, %s" % (v(R[6]), v(R[7])),
+          "s_andn2_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lhp_next",
+          "s_add_u32 %s, %s, 4" % (s(S_T2), s(S_T2)),
+          "s_branch .Lhc_loop",
+          ".Lhc_found:",
+          "v_add_co_u32 v0, vcc, s70, %s" % v(R[4]),
+          "v_addc_co_u32 v1, vcc, 0, %s, vcc" % v(R[5]),
+          "s_andn2_b64 %s, %s, exec" % (sp(S_OK), sp(S_OK)),
+          ".Lhp_next:",
+          "s_mov_b64 exec, %s" % sp(S_OK),
+          "s_cbranch_execz .Lhl_ret",
+          "v_add_u32 %s, 1, %s" % (idx, idx),
+          "v_and_b32 %s, s69, %s" % (idx, idx),
+          "s_branch .Lhp_loop",
+          ".Lhl_ret:",
+          # every lane that entered and did not fault (S_ALIVE lost the faulted ones)
+          "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
+          "s_setpc_b64 s[8:9]"]
+    return L
+
+
 # ---------------------------------------------------------------- handler emission
 def handler_body(name, d, sr):
     """Returns (lines, has_dispatch)."""
@@ -604,6 +745,8 @@ def handler_body(name, d, sr):
         return h_lookup_stk(), False
     if name == "LOOKUPGEN":
         return goto(".Lr_lookup"), True
+    if name == "HLOOKUP":
+        return call(".Lr_hlookup"), False
     raise ValueError(name)
 
 
@@ -781,6 +924,8 @@ def routines():
           "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
           "s_load_dwordx8 s[%d:%d], %s, %s" % (S_REC, S_REC + 7, sp(S_MAPS), s(S_T3)),
           "s_waitcnt lgkmcnt(0)",
+          "s_bitcmp1_b32 s71, 31",                 # hashtable record: its own rule below
+          "s_cbranch_scc1 .Lck_hash",
           # s[66:67] = dev_base, s68 = value_size, s69 = max_entries
           "s_mul_i32 %s, s68, s69" % s(S_BYTES),
           "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_BYTES), s(S_T0)),
@@ -792,6 +937,7 @@ def routines():
           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
           "s_cmp_ge_u32 %s, %s" % (s(S_BYTES), s(S_T0)),
           "s_cselect_b64 %s, %s, 0" % (sp(S_JUNK), sp(S_JUNK)),
+          ".Lck_map_tail:",
           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
           "s_cmp_eq_u32 %s, 0" % s(S_T1),
           "s_cbranch_scc1 .Lck_map_ok",
@@ -808,6 +954,29 @@ def routines():
           ".Lck_map_next:",
           "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
           "s_branch .Lck_map_loop",
+          # hashtable table (dprog.h dp_map): only [value, value + value_size) of a slot:
+          # u = a - base < slots << lg, and (u mod stride) - value_off <= value_size - size
+          ".Lck_hash:",
+          "s_mov_b32 s64, s69",
+          "s_mov_b32 s65, 0",
+          "s_bfe_u32 s70, s71, 0x50010",
+          "s_lshl_b64 s[64:65], s[64:65], s70",
+          "v_mov_b32 %s, s67" % v(R[3]),
+          "v_sub_co_u32 %s, vcc, %s, s66" % (v(R[0]), v(H[0])),
+          "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[3])),
+          "v_cmp_gt_u64_e64 %s, s[64:65], %s" % (sp(S_JUNK), vp(R[0])),
+          "s_lshl_b32 %s, 1, s70" % s(S_BYTES),
+          "s_sub_u32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
+          "v_and_b32 %s, %s, %s" % (v(R[2]), s(S_BYTES), v(R[0])),
+          "s_and_b32 %s, s71, 0xffff" % s(S_T3),
+          "s_add_u32 %s, %s, 15" % (s(S_T3), s(S_T3)),
+          "s_and_b32 %s, %s, -8" % (s(S_T3), s(S_T3)),
+          "v_subrev_u32 %s, %s, %s" % (v(R[2]), s(S_T3), v(R[2])),
+          "s_sub_u32 %s, s68, %s" % (s(S_BYTES), s(S_T0)),
+          "s_cselect_b64 %s, 0, %s" % (sp(S_JUNK), sp(S_JUNK)),  # (scc: size > value_size)
+          "v_cmp_ge_u32_e64 vcc, %s, %s" % (s(S_BYTES), v(R[2])),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_branch .Lck_map_tail",
           ".Lck_map_done:",
           "s_andn2_b64 %s, exec, %s" % (sp(S_MASK), ok),
           "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
@@ -878,6 +1047,7 @@ def routines():
           "s_addc_u32 %s, %s, 0" % (s(S_JUNK + 1), s(S_CB + 1)),
           "s_setpc_b64 %s" % sp(S_JUNK)] + [
           ".Llk_sched:"] + goto(".Lr_schedule")
+    L += hlookup_routine()
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
     # past the batch end masked off.  Clobbers s[64:68], m0, exec.
@@ -1384,6 +1554,8 @@ def generate(out_s, staged_image):
             m = entry_reads(copy)
             if name == "LOOKUPGEN":
                 m |= 1 << 2      # the routine resumes at s12
+            if name == "HLOOKUP":
+                m |= 1 << 4      # the routine reads the map record offset from s14
             reads.append(m)
             # an LDS read whose result the interpreter's dispatch wait (lgkmcnt) covered
             last_ds = max([i for i, ln in enumerate(copy) if ln.startswith("ds_read")] or [-1])

@@ -32,15 +32,37 @@ struct dp_entry {
 };
 static_assert(sizeof(dp_entry) == 32, "dp_entry is 32 bytes");
 
-// One array map visible to device programs (resolved LDDW handle → device mirror).
+// One map visible to device programs (resolved LDDW handle → device mirror).
+//
+// Array maps: the mirror is the value array (max_entries * value_size bytes), flags = 0.
+// Hashtable maps (flags & DP_MAP_HASH): the mirror is a read-only open-addressing snapshot of
+// the host table, rebuilt on upload: max_entries holds the slot count (a power of two, at least
+// twice the map's max_entries, so every probe sequence reaches an empty slot), flags holds the
+// key size and log2 of the slot stride.  Slot layout (stride a power of two):
+//   u32 used (1) | u32 jhash(key) | key, zero-padded to dp_hash_key_bytes | value[value_size]
+// A key hashes to slot jhash(key, key_size, 0) & (slots - 1), then linear probing.  Programs
+// may read [value, value + value_size) through a lookup result; anything else in the table
+// faults like any stray address.
 struct dp_map {
 	uint64_t handle;      // the value programs load with LDDW: the host struct ebpf_map*
-	uint64_t dev_base;    // device address of the mirror (max_entries * value_size bytes)
+	uint64_t dev_base;    // device address of the mirror
 	uint32_t value_size;
-	uint32_t max_entries;
+	uint32_t max_entries; // hashtable: slot count
 	uint32_t lds_off;     // assembly interpreter: LDS byte address of the map's copy, or ~0u
-	uint32_t pad;
+	uint32_t flags;       // DP_MAP_HASH | log2(stride) << 16 | key_size (hashtable), else 0
 };
+#define DP_MAP_HASH 0x80000000u
+#define DP_HASH_MAX_KEY 256u
+#if defined(__HIPCC__)
+#define DP_FN __host__ __device__ static inline
+#else
+#define DP_FN static inline
+#endif
+DP_FN uint32_t dp_hash_key_size(uint32_t flags) { return flags & 0xffffu; }
+DP_FN uint32_t dp_hash_stride_log2(uint32_t flags) { return (flags >> 16) & 0x1fu; }
+DP_FN uint32_t dp_hash_key_bytes(uint32_t key_size) { return (key_size + 7u) & ~7u; }
+// offset of the value in a slot
+DP_FN uint32_t dp_hash_value_off(uint32_t key_size) { return 8u + dp_hash_key_bytes(key_size); }
 static_assert(sizeof(dp_map) == 32, "dp_map is 32 bytes");
 
 // Kernel arguments (passed by value).

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../dprog.h"
+#include "../jhash.h"
 
 namespace {
 
@@ -46,8 +47,18 @@ check(const regions &rg, const dp_launch &L, uint64_t a, uint32_t size, bool wri
 	if (a - rg.stk_lo <= (uint64_t)(kStack - size))
 		return F_NONE;
 	for (uint32_t m = 0; m < L.nmaps; m++) {
-		uint64_t bytes = (uint64_t)L.maps[m].value_size * L.maps[m].max_entries;
-		if (bytes >= size && a - L.maps[m].dev_base <= bytes - size)
+		const dp_map &mp = L.maps[m];
+		if (mp.flags & DP_MAP_HASH) { // only the value of an occupied-or-not slot
+			const uint32_t lg = dp_hash_stride_log2(mp.flags);
+			const uint64_t off = a - mp.dev_base;
+			const uint64_t vo = dp_hash_value_off(dp_hash_key_size(mp.flags));
+			const uint64_t so = off & ((1ull << lg) - 1);
+			if (off < ((uint64_t)mp.max_entries << lg) && so >= vo && so - vo + size <= mp.value_size)
+				return write ? F_MAP_WRITE : F_NONE;
+			continue;
+		}
+		uint64_t bytes = (uint64_t)mp.value_size * mp.max_entries;
+		if (bytes >= size && a - mp.dev_base <= bytes - size)
 			return write ? F_MAP_WRITE : F_NONE;
 	}
 	return F_MEM;
@@ -167,15 +178,41 @@ ebpf_interp_v0(dp_launch L)
 					active = false;
 					continue;
 				}
-				int f = check(rg, L, r2, 4, false);
+				const dp_map &mp = L.maps[mi];
+				const uint32_t ks = (mp.flags & DP_MAP_HASH) ? dp_hash_key_size(mp.flags) : 4;
+				int f = check(rg, L, r2, ks, false);
 				if (f) {
 					fault = f;
 					active = false;
 					continue;
 				}
-				uint32_t key = (uint32_t)load_bytes(r2, 4);
-				if (key < L.maps[mi].max_entries)
-					res = L.maps[mi].dev_base + (uint64_t)L.maps[mi].value_size * key;
+				if (mp.flags & DP_MAP_HASH) {
+					// hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301) over the
+					// device table: linear probing from jhash(key) to the key or an empty slot
+					const uint8_t *kp = reinterpret_cast<const uint8_t *>(r2);
+					const uint32_t hv = ebpf_jhash(kp, ks, 0);
+					const uint32_t lg = dp_hash_stride_log2(mp.flags), mask = mp.max_entries - 1;
+					for (uint32_t i = hv & mask;; i = (i + 1) & mask) {
+						const uint8_t *slot =
+						    reinterpret_cast<const uint8_t *>(mp.dev_base + ((uint64_t)i << lg));
+						const uint32_t *hdr = reinterpret_cast<const uint32_t *>(slot);
+						if (hdr[0] == 0)
+							break;
+						if (hdr[1] != hv)
+							continue;
+						uint32_t b = 0;
+						while (b < ks && slot[8 + b] == kp[b])
+							b++;
+						if (b == ks) {
+							res = (uint64_t)(uintptr_t)(slot + dp_hash_value_off(ks));
+							break;
+						}
+					}
+				} else {
+					uint32_t key = (uint32_t)load_bytes(r2, 4);
+					if (key < mp.max_entries)
+						res = mp.dev_base + (uint64_t)mp.value_size * key;
+				}
 			}
 			R[0][tid] = res;
 			continue;

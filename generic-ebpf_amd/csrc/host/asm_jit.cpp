@@ -314,6 +314,9 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				}
 			}
 			pre_mask[e] = m;
+			if (ah_fam[(uint32_t)low[e].handler] == AHF_HLOOKUP) // (its routine uses s10/s11)
+				for (bool &x : known)
+					x = false;
 		}
 	}
 	// s_mov_b32 s(10+r), v: 4 bytes with an inline constant, else 8 (s12, the resume offset,

@@ -38,12 +38,29 @@ namespace {
 uint32_t
 plan_map_lds(const struct ebpf_map *em, uint32_t *used)
 {
+	if (em->is_hashtable())
+		return ~0u;
 	const uint64_t bytes = (uint64_t)em->value_size * em->max_entries;
 	if (bytes == 0 || bytes % 4 != 0 || *used + bytes > kMapLdsBudget)
 		return ~0u;
 	const uint32_t off = kMapLdsBase + *used;
 	*used += (uint32_t)((bytes + 15) & ~15ull);
 	return off;
+}
+
+// The dp_map record of one map (dev_base filled in by the caller).
+dp_map
+map_record(const struct ebpf_map *em, uint32_t *lds_used)
+{
+	const map_device_layout l = map_device_layout_of(em);
+	dp_map m;
+	memset(&m, 0, sizeof(m));
+	m.handle = (uint64_t)(uintptr_t)em;
+	m.value_size = em->value_size;
+	m.max_entries = l.slots;
+	m.lds_off = plan_map_lds(em, lds_used);
+	m.flags = l.flags;
+	return m;
 }
 
 // Per-device pool of histogram row buffers (asm kernels: one u32[256] row per workgroup).  A
@@ -154,7 +171,7 @@ ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 		em->mirrors.resize(device + 1);
 	map_mirror &m = em->mirrors[device];
 	if (m.dev == nullptr) {
-		hipError_t e = hipMalloc(&m.dev, (size_t)em->value_size * em->max_entries);
+		hipError_t e = hipMalloc(&m.dev, map_device_layout_of(em).bytes);
 		if (e != hipSuccess)
 			return hip_fail(e, "hipMalloc(map mirror)");
 		m.version = ~0ull;
@@ -171,9 +188,19 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 		map_mirror &m = em->mirrors[device];
 		uint64_t v = em->version.load();
 		if (m.version != v) {
-			hipError_t e = hipMemcpyAsync(m.dev, em->array_storage(),
-						      (size_t)em->value_size * em->max_entries,
-						      hipMemcpyHostToDevice, stream);
+			hipError_t e;
+			if (em->is_hashtable()) {
+				// a fresh snapshot of the table; the staging copy must outlive the transfer
+				map_device_image(em, m.image);
+				e = hipMemcpyAsync(m.dev, m.image.data(), m.image.size(), hipMemcpyHostToDevice,
+						   stream);
+				if (e == hipSuccess)
+					e = hipStreamSynchronize(stream);
+			} else {
+				e = hipMemcpyAsync(m.dev, em->array_storage(),
+						   (size_t)em->value_size * em->max_entries,
+						   hipMemcpyHostToDevice, stream);
+			}
 			if (e != hipSuccess)
 				return hip_fail(e, "hipMemcpyAsync(map mirror)");
 			m.version = v;
@@ -217,13 +244,8 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		err = ensure_map_mirror(em, device, &mdev);
 		if (err)
 			return err;
-		dp_map m;
-		m.handle = (uint64_t)(uintptr_t)em;
+		dp_map m = map_record(em, &nd->map_lds_bytes);
 		m.dev_base = (uint64_t)(uintptr_t)mdev;
-		m.value_size = em->value_size;
-		m.max_entries = em->max_entries;
-		m.lds_off = plan_map_lds(em, &nd->map_lds_bytes);
-		m.pad = 0;
 		nd->table.push_back(m);
 	}
 	if (!nd->table.empty()) {
@@ -478,15 +500,8 @@ ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 	// differs only in those immediates)
 	std::vector<dp_map> table;
 	uint32_t used = 0;
-	for (struct ebpf_map *em : ep->xlated->maps) {
-		dp_map m;
-		memset(&m, 0, sizeof(m));
-		m.handle = (uint64_t)(uintptr_t)em;
-		m.value_size = em->value_size;
-		m.max_entries = em->max_entries;
-		m.lds_off = plan_map_lds(em, &used);
-		table.push_back(m);
-	}
+	for (struct ebpf_map *em : ep->xlated->maps)
+		table.push_back(map_record(em, &used));
 	std::vector<unsigned char> img, code;
 	uint32_t stride = 0;
 	std::string msg;

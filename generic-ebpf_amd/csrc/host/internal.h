@@ -47,7 +47,20 @@ struct ebpf_obj {
 struct map_mirror {
 	void *dev = nullptr;
 	uint64_t version = ~0ull; // host version last uploaded
+	std::vector<uint8_t> image; // hashtable: host staging copy of the device table
 };
+
+// The device mirror of a map (maps.cpp).  Array maps mirror their value array; non-percpu
+// hashtables mirror a read-only open-addressing table (dprog.h dp_map).  `bytes == 0` means the
+// map type has no device form (percpu maps, hashtable keys over DP_HASH_MAX_KEY).
+struct map_device_layout {
+	size_t bytes = 0;
+	uint32_t slots = 0; // dp_map.max_entries
+	uint32_t flags = 0; // dp_map.flags
+};
+map_device_layout map_device_layout_of(const struct ebpf_map *em);
+// Hashtable: fill `out` (layout.bytes) with the current table, under the map's lock.
+void map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out);
 
 struct ebpf_map {
 	struct ebpf_obj eo; // must stay first (callers cast to struct ebpf_obj *)
@@ -63,6 +76,7 @@ struct ebpf_map {
 	std::vector<map_mirror> mirrors;  // indexed by device
 	// array-map storage (for device mirroring); null for other map types
 	uint8_t *array_storage() const;
+	bool is_hashtable() const;
 };
 
 // Assembly-interpreter LDS layout (per workgroup): verdict histogram [0, kHistLds), LDS-resident

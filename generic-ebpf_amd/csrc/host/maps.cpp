@@ -511,6 +511,64 @@ ebpf_map::array_storage() const
 	return static_cast<array_priv *>(data)->array;
 }
 
+bool
+ebpf_map::is_hashtable() const
+{
+	return emt == &emt_hashtable;
+}
+
+map_device_layout
+map_device_layout_of(const struct ebpf_map *em)
+{
+	map_device_layout l;
+	if (em->emt == &emt_array) {
+		l.bytes = (size_t)em->value_size * em->max_entries;
+		l.slots = em->max_entries;
+		return l;
+	}
+	if (em->emt != &emt_hashtable || em->key_size == 0 || em->key_size > DP_HASH_MAX_KEY)
+		return l;
+	uint64_t need = dp_hash_value_off(em->key_size) + (uint64_t)em->value_size, stride = 16;
+	uint32_t lg = 4;
+	while (stride < need) {
+		stride <<= 1;
+		lg++;
+	}
+	uint64_t slots = 16;
+	while (slots < 2ull * em->max_entries)
+		slots <<= 1;
+	if (lg > 31 || slots > (1ull << 31) || slots * stride > (1ull << 36))
+		return l;
+	l.bytes = (size_t)(slots * stride);
+	l.slots = (uint32_t)slots;
+	l.flags = DP_MAP_HASH | (lg << 16) | em->key_size;
+	return l;
+}
+
+void
+map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out)
+{
+	const map_device_layout l = map_device_layout_of(em);
+	hash_priv *h = static_cast<hash_priv *>(em->data);
+	std::lock_guard<std::mutex> g(hash_lock(em));
+	out.assign(l.bytes, 0);
+	const uint32_t lg = dp_hash_stride_log2(l.flags), mask = l.slots - 1;
+	const uint32_t voff = dp_hash_value_off(em->key_size);
+	for (uint32_t b = 0; b < h->nbuckets; b++)
+		for (int32_t e = h->head[b]; e >= 0; e = h->next[e]) {
+			const uint32_t hv = ebpf_jhash(h->key(e), em->key_size, 0);
+			uint32_t i = hv & mask;
+			while (out[((size_t)i << lg)] != 0)
+				i = (i + 1) & mask;
+			uint8_t *slot = out.data() + ((size_t)i << lg);
+			const uint32_t used = 1;
+			memcpy(slot, &used, 4);
+			memcpy(slot + 4, &hv, 4);
+			memcpy(slot + 8, h->key(e), em->key_size);
+			memcpy(slot + voff, h->val(e), em->value_size);
+		}
+}
+
 EBPF_EXPORT const struct ebpf_map_type emt_array = {
 	"array",
 	{array_init, array_lookup, array_update, array_delete, array_lookup_from_user, array_update,

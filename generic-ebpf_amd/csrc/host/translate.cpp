@@ -448,14 +448,14 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	if (err)
 		return err;
 
-	// Resolve LDDW immediates that are live array maps of this env: the device map table.
+	// Resolve LDDW immediates that are live maps of this env: the device map table.
 	struct ebpf_env *ee = ep->eo.eo_ee;
 	std::lock_guard<std::mutex> g(ee->lock);
 	const struct ebpf_map *unsupported = nullptr;
 	auto add_map = [&](struct ebpf_map *m) {
-		if (m->array_storage() == nullptr) {
-			// device batches resolve array maps; a program that loads any other live map
-			// (hashtable, percpu) runs on the CPU path only (ebpf_prog_run)
+		if (map_device_layout_of(m).bytes == 0) {
+			// device batches resolve array and hashtable maps; a program that loads any
+			// other live map (percpu) runs on the CPU path only (ebpf_prog_run)
 			unsupported = m;
 			return;
 		}
@@ -482,12 +482,28 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 			add_map(ep->dep_maps[i]);
 	if (unsupported != nullptr) {
 		out.error = EOPNOTSUPP;
-		out.error_msg = std::string("device batches support array maps only; the program uses a ") +
+		out.error_msg = std::string("device batches support array and hashtable maps only; the "
+					    "program uses a ") +
 				unsupported->emt->name + " map (run it with ebpf_prog_run)";
 		out.maps.clear(); // (not pinned: nothing to release)
 		return EOPNOTSUPP;
 	}
 	dataflow(out);
+	// A hashtable lookup runs a probe specialised for its map, so every lookup of a program
+	// that uses a hashtable must name its map statically (r1 a known constant).
+	bool any_hash = false;
+	for (struct ebpf_map *m : out.maps)
+		any_hash |= m->is_hashtable();
+	if (any_hash)
+		for (size_t i = 0; i < out.entries.size(); i++)
+			if (out.entries[i].kind == DK_CALL_LOOKUP && out.annot[i].reached &&
+			    out.annot[i].in[1].kind != AV_CONST) {
+				out.error = EOPNOTSUPP;
+				out.error_msg = "device batches with hashtable maps need every lookup's map "
+						"known at translation time (r1 loaded by LDDW on all paths)";
+				out.maps.clear();
+				return EOPNOTSUPP;
+			}
 	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
 	// its map while a later batch may still read it.
 	for (struct ebpf_map *m : out.maps)

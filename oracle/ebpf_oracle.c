@@ -41,10 +41,16 @@ check_access(const struct region_env *re, uint64_t addr, uint64_t size, int writ
 	if (addr >= re->stk_lo && end <= re->stk_hi)
 		return 0;
 	for (uint32_t m = 0; m < re->p->nmaps; m++) {
-		uint64_t lo = (uint64_t)(uintptr_t)re->p->maps[m].data;
-		uint64_t hi = lo + (uint64_t)re->p->maps[m].value_size * re->p->maps[m].max_entries;
-		if (addr >= lo && end <= hi)
-			return write ? F_MAP_WRITE : 0;
+		const struct oracle_map *mp = &re->p->maps[m];
+		uint64_t lo = (uint64_t)(uintptr_t)mp->data;
+		uint64_t hi = lo + (uint64_t)mp->value_size * mp->max_entries;
+		if (!(addr >= lo && end <= hi))
+			continue;
+		/* a hashtable value is its own allocation (a hash_elem, ebpf_map_hashtable.c:30-36):
+		 * an access that leaves it reads stray memory, which stops the packet like any other */
+		if (mp->kind == ORACLE_MAP_HASH && (addr - lo) / mp->value_size != (end - 1 - lo) / mp->value_size)
+			continue;
+		return write ? F_MAP_WRITE : 0;
 	}
 	return F_MEM;
 }
@@ -123,7 +129,8 @@ uses_src(uint8_t op)
 	return 0;
 }
 
-/* ebpf_map_lookup_elem (ebpf_map.c:77-84) → array_map_lookup_elem (ebpf_map_array.c:115-124) */
+/* ebpf_map_lookup_elem (ebpf_map.c:77-84) → array_map_lookup_elem (ebpf_map_array.c:115-124)
+ * or hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301) */
 static inline uint64_t
 helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
 {
@@ -138,6 +145,23 @@ helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_
 		}
 	if (m == NULL) {
 		*fault = F_BAD_MAP;
+		return 0;
+	}
+	if (m->kind == ORACLE_MAP_HASH) {
+		/* hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301): the element whose key
+		 * equals the key_size bytes at r2 (how the reference finds it — bucket, chain — does
+		 * not change which value that is) */
+		if (checked) {
+			int f = check_access(re, r2, m->key_size, 0);
+			if (f) {
+				*fault = f;
+				return 0;
+			}
+		}
+		const void *key = (const void *)(uintptr_t)r2;
+		for (uint32_t i = 0; i < m->max_entries; i++)
+			if (memcmp(m->keys + (uint64_t)m->key_size * i, key, m->key_size) == 0)
+				return (uint64_t)(uintptr_t)(m->data + (uint64_t)m->value_size * i);
 		return 0;
 	}
 	if (checked) {

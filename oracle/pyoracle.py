@@ -17,7 +17,18 @@ HELPER_UNSET, HELPER_MAP_LOOKUP, HELPER_OTHER = 0, 1, 2
 
 class _Map(ctypes.Structure):
     _fields_ = [("handle", ctypes.c_uint64), ("data", ctypes.c_void_p),
-                ("value_size", ctypes.c_uint32), ("max_entries", ctypes.c_uint32)]
+                ("value_size", ctypes.c_uint32), ("max_entries", ctypes.c_uint32),
+                ("kind", ctypes.c_uint32), ("key_size", ctypes.c_uint32),
+                ("keys", ctypes.c_void_p)]
+
+
+class HashSpec:
+    """A hashtable map for the oracle: ``items`` = [(key bytes, value bytes)] (live entries)."""
+
+    def __init__(self, key_size, value_size, items):
+        self.key_size, self.value_size = key_size, value_size
+        self.items = [(bytes(k), bytes(v)) for k, v in items]
+        assert all(len(k) == key_size and len(v) == value_size for k, v in self.items)
 
 
 class _Prog(ctypes.Structure):
@@ -64,14 +75,25 @@ class OracleProgram:
             b[slot * 8 + 4: slot * 8 + 8] = (h & 0xffffffff).to_bytes(4, "little")
             b[slot * 8 + 12: slot * 8 + 16] = (h >> 32).to_bytes(4, "little")
         self.code = np.frombuffer(bytes(b), dtype=np.uint8).copy()
-        self.map_data = [np.ascontiguousarray(np.frombuffer(bytes(d), dtype=np.uint8)).copy()
-                         for (_, _, d) in maps]
+        u8 = lambda d: np.ascontiguousarray(np.frombuffer(bytes(d) or b"\0", dtype=np.uint8)).copy()
+        self.map_data, self.map_keys = [], []
         self.maps_arr = (_Map * max(1, len(maps)))()
-        for k, (vs, me, _) in enumerate(maps):
+        for k, m in enumerate(maps):
             self.maps_arr[k].handle = oracle_handle(k)
+            if isinstance(m, HashSpec):
+                self.map_data.append(u8(b"".join(v for _, v in m.items)))
+                self.map_keys.append(u8(b"".join(kk for kk, _ in m.items)))
+                self.maps_arr[k].kind = 1
+                self.maps_arr[k].key_size = m.key_size
+                self.maps_arr[k].keys = self.map_keys[-1].ctypes.data
+                self.maps_arr[k].value_size = m.value_size
+                self.maps_arr[k].max_entries = len(m.items)
+            else:
+                vs, me, d = m
+                self.map_data.append(u8(d))
+                self.maps_arr[k].value_size = vs
+                self.maps_arr[k].max_entries = me
             self.maps_arr[k].data = self.map_data[k].ctypes.data
-            self.maps_arr[k].value_size = vs
-            self.maps_arr[k].max_entries = me
         self.p = _Prog()
         self.p.insns = self.code.ctypes.data
         self.p.nslots = len(self.code) // 8

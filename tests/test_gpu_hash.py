@@ -1,0 +1,137 @@
+"""Device hashtable lookups (read-only device table, dprog.h dp_map) against the oracle's
+hashtable_map_lookup_elem restatement: every device variant, the staged and the general kernels,
+key sizes 1..40, keys on the stack or in the packet, NULL keys, faults, two hashtables in one
+program, table refresh after host updates, and a large table with long probe chains."""
+import numpy as np
+import pytest
+
+import hashprogs
+import pyoracle
+from test_maps_hash import HCASES, hcase
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [0, 1, 2]   # compiled, portable HIP, asm interpreter
+
+
+def run_device(native, env, lay, specs, data, count, stride, offsets=None, variant=0, max_entries=64):
+    maps = [hashprogs.NativeHash(native, env, s.key_size, s.value_size, max_entries, s.items)
+            for s in specs]
+    p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        native.set_variant(variant)
+        d = np.ascontiguousarray(data.copy())
+        ret, faults, _ = p.run_batch(d, count, stride, offsets)
+        return ret, faults
+    finally:
+        native.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("stride", [64, 80])
+def test_hash_cases_vs_oracle(gpu, env, variant, stride):
+    bad = []
+    for k in range(len(HCASES)):
+        rng = np.random.default_rng(300 + k)
+        lay, specs, pk = hcase(k, rng, n=4096, size=stride)
+        want, wf, _ = hashprogs.oracle(lay, specs, pk.reshape(-1), len(pk), stride)
+        got, gf = run_device(gpu, env, lay, specs, pk.reshape(-1), len(pk), stride, variant=variant)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad.append((k, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_hash_map_write_faults(gpu, env, variant):
+    rng = np.random.default_rng(5)
+    items, keys = hashprogs.make_table(rng, 4, 8, 40)
+    lay = hashprogs.lookup_program(4, "stack", 0, store=True)
+    specs = [pyoracle.HashSpec(4, 8, items)]
+    pk = hashprogs.packets_with_keys(rng, 2048, 64, keys, 0, 4)
+    want, wf, _ = hashprogs.oracle(lay, specs, pk.reshape(-1), len(pk), 64)
+    got, gf = run_device(gpu, env, lay, specs, pk.reshape(-1), len(pk), 64, variant=variant)
+    assert (wf == 9).any() and (want == 0xdead).any()
+    assert np.array_equal(want, got) and np.array_equal(wf, gf)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_hash_offsets_batch(gpu, env, variant):
+    """Ragged packets (CSR offsets): keys in the packet, some packets too short for the key."""
+    rng = np.random.default_rng(9)
+    items, keys = hashprogs.make_table(rng, 6, 8, 200)
+    lay = hashprogs.lookup_program(6, "packet", 10)
+    n = 3000
+    lens = rng.integers(8, 120, n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    for i in range(n):
+        if lens[i] >= 16:
+            k = keys[int(rng.integers(0, len(keys)))]
+            data[int(offs[i]) + 10:int(offs[i]) + 16] = np.frombuffer(k, dtype=np.uint8)
+    specs = [pyoracle.HashSpec(6, 8, items)]
+    want, wf, _ = hashprogs.oracle(lay, specs, data, n, 0, offs)
+    got, gf = run_device(gpu, env, lay, specs, data, n, 0, offs, variant=variant, max_entries=256)
+    assert wf.any() and (want == 0xdead).any()
+    assert np.array_equal(want, got) and np.array_equal(wf, gf)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_hash_table_refresh_after_updates(gpu, env, variant):
+    """Host updates, deletes and replacements between batches reach the device table."""
+    rng = np.random.default_rng(11)
+    items, keys = hashprogs.make_table(rng, 4, 8, 50)
+    lay = hashprogs.lookup_program(4, "stack", 0)
+    pk = hashprogs.packets_with_keys(rng, 4096, 64, keys, 0, 4)
+    m = hashprogs.NativeHash(gpu, env, 4, 8, 100, items)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle]))
+    try:
+        gpu.set_variant(variant)
+        live = dict(items)
+        for rnd in range(4):
+            d = np.ascontiguousarray(pk.reshape(-1).copy())
+            got, gf, _ = p.run_batch(d, len(pk), 64)
+            want, wf, _ = hashprogs.oracle(lay, [pyoracle.HashSpec(4, 8, list(live.items()))],
+                                           pk.reshape(-1), len(pk), 64)
+            assert np.array_equal(want, got) and np.array_equal(wf, gf), rnd
+            for k in list(live)[:10]:
+                m.delete(k)
+                del live[k]
+            for k in keys[50 + 10 * rnd:60 + 10 * rnd]:
+                v = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+                m.update(k, v)
+                live[k] = v
+            k0 = next(iter(live))
+            live[k0] = b"\x01" * 8
+            m.update(k0, live[k0])
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_hash_large_table(gpu, env, variant):
+    """200k entries of 8-byte keys (a 512k-slot device table), 1M packets, half hits."""
+    rng = np.random.default_rng(13)
+    n_items = 200_000
+    keys = np.unique(rng.integers(0, 2**63, 2 * n_items + 1000, dtype=np.uint64))[:2 * n_items]
+    rng.shuffle(keys)
+    kb = keys.view(np.uint8).reshape(-1, 8)
+    vals = rng.integers(0, 2**63, n_items, dtype=np.uint64)
+    items = [(kb[i].tobytes(), vals[i].tobytes()) for i in range(n_items)]
+    lay = hashprogs.lookup_program(8, "packet", 16)
+    n = 1 << 20
+    pk = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    pk[:, 16:24] = kb[rng.integers(0, len(kb), n)]
+    # expected: a numpy join instead of the oracle's linear scan (same semantics, fast)
+    lut = dict(zip(keys[:n_items].tolist(), vals.tolist()))
+    pkeys = pk[:, 16:24].copy().view(np.uint64).reshape(-1)
+    want = np.array([lut.get(k, 0xdead) for k in pkeys.tolist()], dtype=np.uint64)
+    got, gf = run_device(gpu, env, lay, [pyoracle.HashSpec(8, 8, items)], pk.reshape(-1), n, 64,
+                         variant=variant, max_entries=n_items)
+    assert not gf.any()
+    assert np.array_equal(want, got)

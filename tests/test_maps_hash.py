@@ -262,16 +262,97 @@ def test_prog_run_with_hashtable_lookup(native, env, typ):
         m.destroy()
 
 
-def test_device_batch_rejects_hashtable_programs(native, env):
-    m = HMap(native, env, HT, 4, 8, 64)
-    p = None
+def test_device_translation_of_hashtable_programs(native, env):
+    """Hashtable lookups with a statically known map translate for the device (both code
+    layouts compile); percpu hashtables and lookups whose map is only known at run time do not
+    (EOPNOTSUPP, the program still runs through ebpf_prog_run)."""
+    from generic_ebpf_amd import isa
+    from generic_ebpf_amd.layout import Branch, LdDw, MapRef, assemble
+    I = isa.Insn
+    ht = HMap(native, env, HT, 4, 8, 64)
+    pht = HMap(native, env, PHT, 4, 8, 64)
+    progs = []
     try:
         lay = _lookup_prog(native)
-        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.ptr.value]))
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [ht.ptr.value]))
+        progs.append(p)
         i = native.DprogInfo()
-        assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
-        assert "array maps only" in native.last_error()
+        assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == 0
+        assert i.nmaps == 1
+        for layout in (0, 1):
+            assert len(p.device_code(layout)) > 0
+        p2 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [pht.ptr.value]))
+        progs.append(p2)
+        assert native.lib().ebpf_prog_device_info(p2.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert "percpu_hashtable" in native.last_error()
+        # r1 = the hashtable's handle plus a packet byte: not resolvable at translation time
+        nodes = [I("ldxw", 6, 1, 0), I("stxw", 10, 6, -4), I("ldxb", 7, 1, 4), LdDw(1, MapRef(0)),
+                 I("add64_reg", 1, 7), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                 I("call", imm=0), I("exit")]
+        lay3 = assemble(nodes)
+        p3 = native.Prog(env, native.patch_relocs(lay3.code, lay3.relocs, [ht.ptr.value]))
+        progs.append(p3)
+        assert native.lib().ebpf_prog_device_info(p3.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert "known at translation time" in native.last_error()
     finally:
-        if p is not None:
+        for p in progs:
             p.destroy()
-        m.destroy()
+        ht.destroy()
+        pht.destroy()
+
+
+# ---- the oracle's hashtable lookups against the CPU path (ebpf_prog_run over the host table) ----
+
+HCASES = [  # (ks, vs, key source, key offset, read (size, off), store, second map)
+    (4, 8, "stack", 0, (8, 0), False, None),
+    (1, 8, "stack", 5, (4, 4), False, None),
+    (3, 16, "packet", 7, (8, 8), False, None),
+    (8, 8, "stack", 2, (2, 6), False, None),
+    (13, 12, "packet", 20, (4, 8), False, None),
+    (16, 8, "stack", 16, (8, 0), False, (4, 40)),
+    (40, 24, "stack", 0, (8, 16), False, None),
+    (4, 8, "stack", 0, (8, 4), False, None),      # crosses the value end: fault
+    (4, 8, "null", 0, (8, 0), False, None),       # NULL key: r0 = NULL
+    (8, 8, "packet", 60, (8, 0), False, None),    # key runs off the packet: fault
+]
+
+
+def hcase(k, rng, n=128, size=64):
+    import hashprogs
+    ks, vs, src, off, read, store, second = HCASES[k]
+    items, keys = hashprogs.make_table(rng, ks, vs, 40)
+    lay = hashprogs.lookup_program(ks, src, off, read=read, store=store, second=second)
+    specs = [pyoracle.HashSpec(ks, vs, items)]
+    if second:
+        items2, keys2 = hashprogs.make_table(rng, second[0], 8, 30)
+        specs.append(pyoracle.HashSpec(second[0], 8, items2))
+    pk = hashprogs.packets_with_keys(rng, n, size, keys, min(off, size - ks), ks)
+    if second:
+        pk2 = hashprogs.packets_with_keys(rng, n, size, keys2, second[1], second[0])
+        pk[:, second[1]:second[1] + second[0]] = pk2[:, second[1]:second[1] + second[0]]
+    return lay, specs, pk
+
+
+@pytest.mark.parametrize("k", range(len(HCASES)))
+def test_oracle_hash_lookups_match_cpu_path(native, env, k):
+    import hashprogs
+    rng = np.random.default_rng(100 + k)
+    lay, specs, pk = hcase(k, rng)
+    want, wf, _ = hashprogs.oracle(lay, specs, pk.reshape(-1), len(pk), pk.shape[1])
+    maps = [hashprogs.NativeHash(native, env, s.key_size, s.value_size, 64, s.items) for s in specs]
+    p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        for i in range(len(pk)):
+            if wf[i]:
+                continue      # (the reference's behaviour there is a crash or a stray read)
+            r, _ = p.run_cpu(pk[i].tobytes())
+            assert r == int(want[i]), (i, hex(r), hex(int(want[i])))
+        if HCASES[k][2] != "null" and k != 7 and k != 9:
+            assert not wf.any()
+            assert (want != 0xdead).any() and (want == 0xdead).any()   # hits and misses
+        if k in (7, 9):
+            assert wf.any()
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
