@@ -43,7 +43,9 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 26, "c5": 1 << 22}
+DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
+                   "c4": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26}
+C4H_SLOT_BYTES = 32  # device table slot: u32 used | u32 hash | 4-B key (8-B padded) | 8-B value
 DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
 
 
@@ -53,6 +55,10 @@ def build_inputs(cfg, n, rank):
     maps = []
     if cfg == "c4":
         maps = [(8, 256, workloads.c4_map_values().tobytes())]
+    if cfg == "c4h":   # ("hash", key_size, value_size, max_entries, keys, values)
+        universe, keys, values = workloads.c4h_table()
+        maps = [("hash", 4, 8, len(keys), keys, values)]
+        return lay, maps, workloads.packets_c4h(min(n, DISTINCT), universe, seed=4 + 1000 * rank), None
     if cfg == "c5":
         data, offs, _ = workloads.packets_imix(n, seed=5 + rank)
         return lay, maps, data, offs
@@ -73,6 +79,8 @@ def cpu_baseline(cfg, lay, maps, pk, offs, budget_s):
     else:
         n = min(pk.shape[0], 1 << 20)
         data, offsets = pk[:n].reshape(-1), None
+    maps = [pyoracle.HashSpec(m[1], m[2], keys=m[4], values=m[5]) if m[0] == "hash" else m
+            for m in maps]
     op = pyoracle.OracleProgram(lay.code, lay.relocs, maps, checked=False)
     op.run(data, n, 64, offsets, nthreads=threads)  # warm
     t0 = time.perf_counter()
@@ -107,9 +115,15 @@ def main():
     lay, maps_spec, pk, offs = build_inputs(cfg, n, rank)
     env = native.Env()
     maps = []
-    for vs, me, d in maps_spec:
-        m = native.Map(env, me, vs)
-        m.fill(d)
+    for spec in maps_spec:
+        if spec[0] == "hash":
+            _, ks, vs, me, keys, values = spec
+            m = native.HashMap(env, ks, vs, me)
+            m.fill(keys, values)
+        else:
+            vs, me, d = spec
+            m = native.Map(env, me, vs)
+            m.fill(d)
         maps.append(m)
     prog = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
     native.set_variant(a.variant)
@@ -123,6 +137,10 @@ def main():
         del base
         d_offs = None
         bytes_per_launch = n * 64
+        if cfg == "c4h":  # + one table slot per packet that reaches the lookup (IPv4, not ICMP)
+            et = (pk[:, 12].astype(np.uint32) << 8) | pk[:, 13]
+            reach = float(np.mean((et == 0x0800) & (pk[:, 23] != 1)))
+            bytes_per_launch = int(n * 64 + round(n * reach) * C4H_SLOT_BYTES)
     else:
         d_pk = torch.from_numpy(pk).to(dev)
         d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)

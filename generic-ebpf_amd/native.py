@@ -200,6 +200,51 @@ class Map:
         lib().ebpf_map_destroy(self.ptr)
 
 
+class HashMap:
+    """A hashtable (or percpu hashtable) map with byte-string keys (ebpf_map_hashtable.c)."""
+
+    def __init__(self, env, key_size, value_size, max_entries, percpu=False):
+        self.env = env
+        self.key_size, self.value_size, self.max_entries = key_size, value_size, max_entries
+        t = MAP_TYPE_PERCPU_HASHTABLE if percpu else MAP_TYPE_HASHTABLE
+        attr = MapAttr(t, key_size, value_size, max_entries, 0)
+        self.ptr = ctypes.c_void_p()
+        _check(lib().ebpf_map_create(env.ptr, ctypes.byref(self.ptr), ctypes.byref(attr)),
+               "ebpf_map_create")
+
+    @property
+    def handle(self):
+        return self.ptr.value
+
+    def update(self, key, value_bytes, flags=EBPF_ANY):
+        k = ctypes.create_string_buffer(bytes(key), self.key_size)
+        v = ctypes.create_string_buffer(bytes(value_bytes), self.value_size)
+        return lib().ebpf_map_update_elem_from_user(self.ptr, k, v, flags)
+
+    def fill(self, keys, values):
+        """keys: uint8 [n, key_size]; values: uint8 [n, value_size] (EBPF_ANY updates)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, self.key_size)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1, self.value_size)
+        f = lib().ebpf_map_update_elem_from_user
+        kp, vp = keys.ctypes.data, values.ctypes.data
+        for i in range(len(keys)):
+            _check(f(self.ptr, kp + i * self.key_size, vp + i * self.value_size, EBPF_ANY),
+                   "map update")
+
+    def lookup(self, key):
+        k = ctypes.create_string_buffer(bytes(key), self.key_size)
+        v = ctypes.create_string_buffer(self.value_size)
+        err = lib().ebpf_map_lookup_elem_from_user(self.ptr, k, v)
+        return err, v.raw
+
+    def delete(self, key):
+        k = ctypes.create_string_buffer(bytes(key), self.key_size)
+        return lib().ebpf_map_delete_elem_from_user(self.ptr, k)
+
+    def destroy(self):
+        lib().ebpf_map_destroy(self.ptr)
+
+
 def patch_relocs(code, relocs, handles):
     b = bytearray(code)
     for slot, k in relocs:

@@ -4,6 +4,8 @@
   C3  64-insn L2/L3 parse + classify (VALE-BPF style) over structured 64-B packets
   C4  C3 + one array-map lookup per packet (array map, 256 x 8 B)
   C5  256-insn branch-heavy filter over mixed 64-1500 B packets (offsets array)
+  C4H C3 + one hashtable lookup per packet keyed by the IPv4 destination address (a 1M-entry
+      route/flow table, half the packets' addresses present) — the §8(f) hashtable row
 
 Programs are laid out with the stepping-aware assembler (layout.py) so the reference
 interpreter executes them as written; "N-insn" = N executed instructions on the main path,
@@ -105,7 +107,7 @@ def prog_c2():
     return assemble(nodes)
 
 
-def _classify_program(with_lookup, pad, reset):
+def _classify_program(with_lookup, pad, reset, hash_key=False):
     """Ethernet → IPv4 (TCP/UDP main path) | IPv6 | ICMP | other.  The flow hash and the
     verdict arithmetic run first and the ACL decisions sit at the end of the path, so nearly
     every IPv4 packet executes the full main path (no early-exit shortcut)."""
@@ -141,7 +143,16 @@ def _classify_program(with_lookup, pad, reset):
     pads = [I("xor64_imm", R8, imm=0x5bd1e995 ^ (k * 0x1f1f)) if k % 2 == 0 else
             I("mul64_imm", R8, imm=0x27d4eb2d) for k in range(pad)]
     lookup = []
-    if with_lookup:
+    if with_lookup and hash_key:   # key: the destination address (r5, host order)
+        lookup = [
+            I("stxw", R10, R5, -4),
+            LdDw(R1, MapRef(0)),
+            I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+            I("call", imm=0),
+            Branch(I("jeq_imm", R0, imm=0), _exit_with(2)),
+            I("ldxdw", R6, R0, 0), I("xor64_reg", R8, R6),
+        ]
+    elif with_lookup:
         lookup = [
             I("mov_reg", R6, R9), I("and_imm", R6, imm=0xff),
             I("stxw", R10, R6, -4),
@@ -166,11 +177,11 @@ def _classify_program(with_lookup, pad, reset):
     return assemble(head + pads + lookup + verdict, reset_stride=reset)
 
 
-def _fit(with_lookup, target, exact=True):
+def _fit(with_lookup, target, exact=True, hash_key=False):
     """Smallest padding whose main path executes ``target`` instructions (JA resets included)."""
     for reset in (8, 7, 9, 6, 10):
         for pad in range(0, 64):
-            lay = _classify_program(with_lookup, pad, reset)
+            lay = _classify_program(with_lookup, pad, reset, hash_key)
             if lay.main_path_steps == target or (not exact and lay.main_path_steps >= target):
                 return lay
             if lay.main_path_steps > target:
@@ -188,6 +199,36 @@ def prog_c4():
     path (64) plus STXW key, LDDW map, r2 = r10-4 (3 insns), CALL, NULL check, LDXDW value and
     XOR into the hash — 75 executed instructions on the main path."""
     return _fit(True, 75, exact=False)
+
+
+def prog_c4h():
+    """C3 + one hashtable lookup keyed by the IPv4 destination address (STXW key, LDDW map,
+    r2 = r10-4, CALL, NULL check, LDXDW value, XOR): the C4 path shape on a hashtable."""
+    return _fit(True, 73, exact=False, hash_key=True)
+
+
+C4H_ENTRIES = 1 << 20
+
+
+def c4h_table(seed=12, entries=C4H_ENTRIES):
+    """(universe u32[2*entries] distinct addresses, keys u8[entries,4], values u8[entries,8]):
+    the map holds the first half of the universe; keys are the addresses in host order (the
+    program's BE32 of the packet bytes), stored little-endian like the STXW that builds them."""
+    g = _rng(seed)
+    u = np.unique(g.integers(0, 2**32, int(entries * 2.2), dtype=np.uint64))
+    u = u[g.permutation(len(u))][:2 * entries].astype(np.uint32)
+    keys = u[:entries].view(np.uint8).reshape(-1, 4)
+    values = g.integers(0, 2**63, entries, dtype=np.uint64).view(np.uint8).reshape(-1, 8)
+    return u, keys, values
+
+
+def packets_c4h(n, universe, seed=4):
+    """C3/C4 packets whose IPv4 destination address is drawn from ``universe``."""
+    p = packets_l2l3(n, 64, seed)
+    a = universe[_rng(seed + 100).integers(0, len(universe), n)]
+    for b in range(4):
+        p[:, 30 + b] = (a >> (24 - 8 * b)) & 0xff
+    return p
 
 
 def c4_map_values(seed=11, entries=256):
@@ -270,4 +311,6 @@ CONFIGS = {
                pkt="l2l3"),
     "c5": dict(desc="256-insn branch-heavy filter, IMIX 64-1500 B packets", prog=prog_c5,
                pkt="imix"),
+    "c4h": dict(desc="64-insn classify + hashtable lookup (1M-entry table keyed by IPv4 dst), "
+                     "64 B packets", prog=prog_c4h, pkt="c4h"),
 }

@@ -129,6 +129,63 @@ uses_src(uint8_t op)
 	return 0;
 }
 
+static inline uint32_t
+rot32(uint32_t x, int k)
+{
+	return (x << k) | (x >> (32 - k));
+}
+
+uint32_t
+oracle_jhash(const void *key, uint32_t length, uint32_t initval)
+{
+	const uint8_t *k = (const uint8_t *)key;
+	uint32_t a, b, c;
+	a = b = c = 0xdeadbeefu + length + initval;
+#define W(p) ((uint32_t)(p)[0] | (uint32_t)(p)[1] << 8 | (uint32_t)(p)[2] << 16 | (uint32_t)(p)[3] << 24)
+	while (length > 12) {
+		a += W(k);
+		b += W(k + 4);
+		c += W(k + 8);
+		a -= c; a ^= rot32(c, 4);  c += b;
+		b -= a; b ^= rot32(a, 6);  a += c;
+		c -= b; c ^= rot32(b, 8);  b += a;
+		a -= c; a ^= rot32(c, 16); c += b;
+		b -= a; b ^= rot32(a, 19); a += c;
+		c -= b; c ^= rot32(b, 4);  b += a;
+		length -= 12;
+		k += 12;
+	}
+	if (length == 0)
+		return c;
+	uint8_t t[12] = {0};
+	memcpy(t, k, length);
+	a += W(t);
+	b += W(t + 4);
+	c += W(t + 8);
+#undef W
+	c ^= b; c -= rot32(b, 14);
+	a ^= c; a -= rot32(c, 11);
+	b ^= a; b -= rot32(a, 25);
+	c ^= b; c -= rot32(b, 16);
+	a ^= c; a -= rot32(c, 4);
+	b ^= a; b -= rot32(a, 14);
+	c ^= b; c -= rot32(b, 24);
+	return c;
+}
+
+void
+oracle_hash_build(struct oracle_map *m)
+{
+	for (uint32_t b = 0; b < m->nbuckets; b++)
+		m->bucket_head[b] = -1;
+	for (uint32_t i = 0; i < m->max_entries; i++) {
+		uint32_t b = oracle_jhash(m->keys + (uint64_t)m->key_size * i, m->key_size, 0) &
+			     (m->nbuckets - 1);
+		m->bucket_next[i] = m->bucket_head[b];
+		m->bucket_head[b] = (int32_t)i;
+	}
+}
+
 /* ebpf_map_lookup_elem (ebpf_map.c:77-84) → array_map_lookup_elem (ebpf_map_array.c:115-124)
  * or hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301) */
 static inline uint64_t
@@ -159,6 +216,13 @@ helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_
 			}
 		}
 		const void *key = (const void *)(uintptr_t)r2;
+		if (m->nbuckets) {
+			uint32_t b = oracle_jhash(key, m->key_size, 0) & (m->nbuckets - 1);
+			for (int32_t i = m->bucket_head[b]; i >= 0; i = m->bucket_next[i])
+				if (memcmp(m->keys + (uint64_t)m->key_size * i, key, m->key_size) == 0)
+					return (uint64_t)(uintptr_t)(m->data + (uint64_t)m->value_size * i);
+			return 0;
+		}
 		for (uint32_t i = 0; i < m->max_entries; i++)
 			if (memcmp(m->keys + (uint64_t)m->key_size * i, key, m->key_size) == 0)
 				return (uint64_t)(uintptr_t)(m->data + (uint64_t)m->value_size * i);

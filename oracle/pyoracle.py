@@ -19,16 +19,31 @@ class _Map(ctypes.Structure):
     _fields_ = [("handle", ctypes.c_uint64), ("data", ctypes.c_void_p),
                 ("value_size", ctypes.c_uint32), ("max_entries", ctypes.c_uint32),
                 ("kind", ctypes.c_uint32), ("key_size", ctypes.c_uint32),
-                ("keys", ctypes.c_void_p)]
+                ("keys", ctypes.c_void_p), ("nbuckets", ctypes.c_uint32),
+                ("bucket_head", ctypes.c_void_p), ("bucket_next", ctypes.c_void_p)]
 
 
 class HashSpec:
-    """A hashtable map for the oracle: ``items`` = [(key bytes, value bytes)] (live entries)."""
+    """A hashtable map for the oracle: ``items`` = [(key bytes, value bytes)] (live entries), or
+    ``keys``/``values`` as uint8 arrays [n, key_size] / [n, value_size] (large tables)."""
 
-    def __init__(self, key_size, value_size, items):
+    def __init__(self, key_size, value_size, items=None, keys=None, values=None):
         self.key_size, self.value_size = key_size, value_size
-        self.items = [(bytes(k), bytes(v)) for k, v in items]
-        assert all(len(k) == key_size and len(v) == value_size for k, v in self.items)
+        if items is not None:
+            items = [(bytes(k), bytes(v)) for k, v in items]
+            assert all(len(k) == key_size and len(v) == value_size for k, v in items)
+            keys = np.frombuffer(b"".join(k for k, _ in items), dtype=np.uint8)
+            values = np.frombuffer(b"".join(v for _, v in items), dtype=np.uint8)
+        self.keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint8).reshape(-1, key_size))
+        self.values = np.ascontiguousarray(np.asarray(values, dtype=np.uint8).reshape(-1, value_size))
+        assert len(self.keys) == len(self.values)
+
+    @property
+    def items(self):
+        return [(self.keys[i].tobytes(), self.values[i].tobytes()) for i in range(len(self.keys))]
+
+    def __len__(self):
+        return len(self.keys)
 
 
 class _Prog(ctypes.Structure):
@@ -55,6 +70,10 @@ def lib():
         _lib.oracle_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]
+        _lib.oracle_hash_build.restype = None
+        _lib.oracle_hash_build.argtypes = [ctypes.c_void_p]
+        _lib.oracle_jhash.restype = ctypes.c_uint32
+        _lib.oracle_jhash.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
     return _lib
 
 
@@ -76,18 +95,29 @@ class OracleProgram:
             b[slot * 8 + 12: slot * 8 + 16] = (h >> 32).to_bytes(4, "little")
         self.code = np.frombuffer(bytes(b), dtype=np.uint8).copy()
         u8 = lambda d: np.ascontiguousarray(np.frombuffer(bytes(d) or b"\0", dtype=np.uint8)).copy()
-        self.map_data, self.map_keys = [], []
+        self.map_data, self.map_keys, self.map_index = [], [], []
         self.maps_arr = (_Map * max(1, len(maps)))()
         for k, m in enumerate(maps):
             self.maps_arr[k].handle = oracle_handle(k)
             if isinstance(m, HashSpec):
-                self.map_data.append(u8(b"".join(v for _, v in m.items)))
-                self.map_keys.append(u8(b"".join(kk for kk, _ in m.items)))
+                self.map_data.append(u8(m.values.tobytes()))
+                self.map_keys.append(u8(m.keys.tobytes()))
                 self.maps_arr[k].kind = 1
                 self.maps_arr[k].key_size = m.key_size
                 self.maps_arr[k].keys = self.map_keys[-1].ctypes.data
                 self.maps_arr[k].value_size = m.value_size
-                self.maps_arr[k].max_entries = len(m.items)
+                self.maps_arr[k].max_entries = len(m)
+                # the reference's bucket index (nbuckets = entries rounded up to a power of two)
+                nb = 1
+                while nb < max(1, len(m)):
+                    nb <<= 1
+                head = np.zeros(nb, dtype=np.int32)
+                nxt = np.zeros(max(1, len(m)), dtype=np.int32)
+                self.map_index.append((head, nxt))
+                self.maps_arr[k].nbuckets = nb
+                self.maps_arr[k].bucket_head = head.ctypes.data
+                self.maps_arr[k].bucket_next = nxt.ctypes.data
+                lib().oracle_hash_build(ctypes.byref(self.maps_arr[k]))
             else:
                 vs, me, d = m
                 self.map_data.append(u8(d))

@@ -135,3 +135,32 @@ def test_hash_large_table(gpu, env, variant):
                          variant=variant, max_entries=n_items)
     assert not gf.any()
     assert np.array_equal(want, got)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_c4h_full_size(gpu, env, variant):
+    """The C4H bench workload at its full size (64M packets tiled from 1M distinct over the
+    1M-entry table): device result of packet i == the oracle's for the distinct packet it tiles."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4h()
+    universe, keys, values = workloads.c4h_table()
+    distinct, tiles = 1 << 20, 64
+    pk = workloads.packets_c4h(distinct, universe)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [pyoracle.HashSpec(4, 8, keys=keys, values=values)])
+    want, wf, _, _ = op.run(pk.reshape(-1), distinct, 64, None, nthreads=8)
+    assert not wf.any()
+    assert (want == 2).any()      # misses take the NULL branch (exit 2) ...
+    m = gpu.HashMap(env, 4, 8, len(keys))
+    m.fill(keys, values)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle]))
+    try:
+        gpu.set_variant(variant)
+        data = np.tile(pk.reshape(-1), tiles)
+        got, gf, _ = p.run_batch(data, distinct * tiles, 64)
+        assert not gf.any()
+        np.testing.assert_array_equal(got.reshape(tiles, distinct),
+                                      np.broadcast_to(want, (tiles, distinct)))
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()

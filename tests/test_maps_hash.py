@@ -94,6 +94,15 @@ def test_oracle_jhash_matches_reference_vectors():
         assert pyoracle.jhash(d[o[i]:o[i + 1]], int(z["initval"][i])) == int(z["expect"][i]), i
 
 
+def test_oracle_c_jhash_matches_reference_vectors():
+    z = np.load(GOLDEN)
+    d, o = z["data"].tobytes(), z["offsets"]
+    L = pyoracle.lib()
+    for i in range(len(o) - 1):
+        k = d[o[i]:o[i + 1]]
+        assert L.oracle_jhash(k, len(k), int(z["initval"][i])) == int(z["expect"][i]), i
+
+
 def test_product_jhash_header_matches_reference_vectors(tmp_path):
     """csrc/jhash.h (shared by host maps and device code) compiled on its own, every golden
     vector at its recorded misalignment."""
