@@ -136,6 +136,8 @@ for n in ("EXIT", "FAULT", "NOP", "LOOKUPSTK", "LOOKUPGEN"):
 for z in SIZES:
     fam("LDXPKC%d" % z, 3)      # staged packet load at a constant byte offset: (dst, offset)
 fam("HLOOKUP", 0)              # hashtable lookup, map known at translation time (s14 = record offset)
+for z in SIZES:
+    fam("LDXHV%d" % z, 2)       # load from a hashtable value (lookup result), in range by provenance
 
 
 def variants(arity):
@@ -511,6 +513,26 @@ def h_ldx_map(z, d, sr):
     return out
 
 
+def h_ldx_hv(z, d, sr):
+    """Load from a hashtable value: r_src is (by pointer provenance) a lookup result of a
+    hashtable map, i.e. NULL or a slot's value address, and the translator proved
+    [off, off + z) inside the value (s14 = off, naturally aligned).  NULL lanes fault MEM;
+    the rest do one global load (no region walk)."""
+    ld = {1: "global_load_ubyte", 2: "global_load_ushort", 4: "global_load_dword",
+          8: "global_load_dwordx2"}[z]
+    a = vp(H[0])
+    out = ["v_cmp_eq_u64_e64 %s, 0, %s" % (sp(S_MASK), pair(sr)),
+           "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+           "s_cbranch_scc0 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:",
+           "v_add_co_u32 %s, vcc, s14, %s" % (v(H[0]), lo(sr)),
+           "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(H[1]), hi(sr))]
+    if z == 8:
+        out += ["%s %s, %s, off" % (ld, pair(d), a)]
+    else:
+        out += ["%s %s, %s, off" % (ld, lo(d), a), "v_mov_b32 %s, 0" % hi(d)]
+    return out + ["s_waitcnt vmcnt(0)"]
+
+
 def store_bytes(a0, vals, z):
     out = []
     for b in range(z):
@@ -631,12 +653,14 @@ def hlookup_routine():
          "s_cbranch_scc1 .Lhh_tail"]
     n = [0]
 
-    def add_words():
+    def add_words(keep=False):
         out = []
-        for x in (a, b, c):
+        for i, x in enumerate((a, b, c)):
             out += _hl_word(t, S_T2, n[0])
             n[0] += 1
             out += ["v_add_u32 %s, %s, %s" % (x, x, t), "s_add_u32 %s, %s, 4" % (s(S_T2), s(S_T2))]
+            if keep and i < 2:   # keys of <= 8 bytes: the tail's first two words are the key
+                out.append("v_mov_b32 %s, %s" % (v(H[2]) if i == 0 else v(R[5]), t))
         return out
     L += add_words()
     for (x, y, z, k) in ((a, c, b, 4), (b, a, c, 6), (c, b, a, 8), (a, c, b, 16), (b, a, c, 19),
@@ -647,12 +671,43 @@ def hlookup_routine():
     L += ["s_sub_u32 %s, %s, 12" % (s(S_T3), s(S_T3)),
           "s_branch .Lhh_loop",
           ".Lhh_tail:"]
-    L += add_words()
+    L += add_words(keep=True)
     for (x, y, k) in ((c, b, 14), (a, c, 11), (b, a, 25), (c, b, 16), (a, c, 4), (b, a, 14), (c, b, 24)):
         # x ^= y; x -= rot(y, k)
         L += ["v_xor_b32 %s, %s, %s" % (x, x, y)] + _rot(t, y, k) + ["v_sub_u32 %s, %s, %s" % (x, x, t)]
     # probe: slot i = hash & mask, then i + 1, ... until the key or an empty slot
     idx, sa, hd = v(R[3]), vp(R[4]), vp(R[6])
+    # keys of up to 8 bytes: one 16-byte load per slot (used, hash, key) compared in registers
+    k0, k1 = v(H[2]), v(H[3])
+    L += ["s_cmp_le_u32 %s, 8" % s(S_T0),
+          "s_cbranch_scc0 .Lhp_general",
+          "v_mov_b32 %s, %s" % (k1, v(R[5])),
+          "v_and_b32 %s, s69, %s" % (idx, c),
+          "s_mov_b64 %s, exec" % sp(S_OK),
+          ".Lhq_loop:",
+          "v_mov_b32 %s, %s" % (v(R[4]), idx),
+          "v_mov_b32 %s, 0" % v(R[5]),
+          "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
+          "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
+          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa),
+          "s_waitcnt vmcnt(0)",
+          "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),           # empty slot: not found
+          "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
+          "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[7]), c),
+          "v_cmp_eq_u32_e64 vcc, %s, %s" % (v(R[8]), k0),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "v_cmp_eq_u32_e64 vcc, %s, %s" % (v(R[9]), k1),
+          "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+          "s_and_b64 exec, %s, %s" % (sp(S_JUNK), sp(S_OK)),  # found here
+          "v_add_co_u32 v0, vcc, s70, %s" % v(R[4]),
+          "v_addc_co_u32 v1, vcc, 0, %s, vcc" % v(R[5]),
+          "s_andn2_b64 %s, %s, exec" % (sp(S_OK), sp(S_OK)),
+          "s_mov_b64 exec, %s" % sp(S_OK),
+          "s_cbranch_execz .Lhl_ret",
+          "v_add_u32 %s, 1, %s" % (idx, idx),
+          "v_and_b32 %s, s69, %s" % (idx, idx),
+          "s_branch .Lhq_loop",
+          ".Lhp_general:"]
     L += ["v_and_b32 %s, s69, %s" % (idx, c),
           "s_mov_b64 %s, exec" % sp(S_OK),                  # lanes still probing
           ".Lhp_loop:",
@@ -730,6 +785,8 @@ def handler_body(name, d, sr):
         return h_ldx_gen(int(name[6:]), d, sr), False
     if name.startswith("LDXMAP"):
         return h_ldx_map(int(name[6:]), d, sr), False
+    if name.startswith("LDXHV"):
+        return h_ldx_hv(int(name[5:]), d, sr), False
     if name.startswith("STXGEN"):
         return h_stx_gen(int(name[6:]), d, sr), False
     if name.startswith("STGEN"):

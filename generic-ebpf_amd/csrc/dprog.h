@@ -37,7 +37,7 @@ static_assert(sizeof(dp_entry) == 32, "dp_entry is 32 bytes");
 // Array maps: the mirror is the value array (max_entries * value_size bytes), flags = 0.
 // Hashtable maps (flags & DP_MAP_HASH): the mirror is a read-only open-addressing snapshot of
 // the host table, rebuilt on upload: max_entries holds the slot count (a power of two, at least
-// twice the map's max_entries, so every probe sequence reaches an empty slot), flags holds the
+// four times the map's max_entries, so every probe sequence reaches an empty slot), flags holds the
 // key size and log2 of the slot stride.  Slot layout (stride a power of two):
 //   u32 used (1) | u32 jhash(key) | key, zero-padded to dp_hash_key_bytes | value[value_size]
 // A key hashes to slot jhash(key, key_size, 0) & (slots - 1), then linear probing.  Programs

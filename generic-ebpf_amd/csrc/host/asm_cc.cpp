@@ -1110,9 +1110,9 @@ rf
 copied_result(int fam)
 {
 	switch (fam) {
-	case AHF_LDXGEN1: case AHF_LDXMAP1: case AHF_LDXPKTG1: case AHF_LDXSTK1: return kbits(8);
-	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: return kbits(16);
-	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: return kbits(32);
+	case AHF_LDXGEN1: case AHF_LDXMAP1: case AHF_LDXPKTG1: case AHF_LDXSTK1: case AHF_LDXHV1: return kbits(8);
+	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: case AHF_LDXHV2: return kbits(16);
+	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: case AHF_LDXHV4: return kbits(32);
 	default:
 		if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
 			return kbits(32);

@@ -534,8 +534,10 @@ map_device_layout_of(const struct ebpf_map *em)
 		stride <<= 1;
 		lg++;
 	}
+	// at most a quarter full: linear probing then ends within a slot or two almost always
+	// (an unsuccessful search probes (1 + 1/(1-a)^2)/2 = 1.4 slots on average at a = 1/4)
 	uint64_t slots = 16;
-	while (slots < 2ull * em->max_entries)
+	while (slots < 4ull * em->max_entries)
 		slots <<= 1;
 	if (lg > 31 || slots > (1ull << 31) || slots * stride > (1ull << 36))
 		return l;
