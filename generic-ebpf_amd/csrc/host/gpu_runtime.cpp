@@ -472,6 +472,18 @@ ebpf_prog_prepare_device(struct ebpf_prog *ep, int device)
 }
 
 EBPF_EXPORT int
+ebpf_prog_set_semantics(struct ebpf_prog *ep, int semantics)
+{
+	if (ep == nullptr || (semantics != EBPF_SEM_REFERENCE && semantics != EBPF_SEM_STANDARD))
+		return fail(EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(ep->dlock);
+	if (ep->xlated && ep->semantics.load() != semantics)
+		return fail(EBUSY, "the program was already translated with other semantics");
+	ep->semantics.store(semantics);
+	return 0;
+}
+
+EBPF_EXPORT int
 ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info)
 {
 	if (ep == nullptr || info == nullptr)

@@ -154,6 +154,7 @@ struct ebpf_prog {
 	uint32_t prog_len;
 	struct ebpf_inst *prog;
 	struct ebpf_map *dep_maps[EBPF_PROG_MAX_ATTACHED_MAPS];
+	std::atomic<int> semantics{EBPF_SEM_REFERENCE}; // ebpf_prog_set_semantics
 	// GPU backend state
 	std::mutex dlock;
 	std::unique_ptr<dprog_host> xlated;            // translation (device independent)

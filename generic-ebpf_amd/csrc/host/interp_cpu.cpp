@@ -11,6 +11,10 @@
 // access, CALL through the env helper table (:282-284), abort on an invalid opcode (:367-369).
 // Instead of a 90-way switch it dispatches through a table of handlers indexed by opcode,
 // built once.
+//
+// EBPF_SEM_STANDARD programs (ebpf_prog_set_semantics) run on a second table: sequential pc,
+// MOV64 / NEG / NEG64 / ARSH with their standard meaning, DIV/MOD by zero defined (0 / dst
+// unchanged) and the JMP32 class.  Same dispatch loop with `inst = prog + pc++`.
 #include "internal.h"
 
 #include <stdio.h>
@@ -128,6 +132,47 @@ J(jsler, (int64_t)D(v, i) <= (int64_t)S(v, i))
 J(jslei, (int64_t)D(v, i) <= (int64_t)SX(i))
 H(call, v.reg[0] = v.helpers[i.imm]->fn(v.reg[1], v.reg[2], v.reg[3], v.reg[4], v.reg[5]))
 bool exit_(cpu_vm &, const struct ebpf_inst &) { return false; }
+// standard semantics (where they differ from the reference's)
+H(mov64r_std, D(v, i) = S(v, i))
+H(mov64i_std, D(v, i) = SX(i))
+H(neg32_std, D(v, i) = (uint32_t)(0u - (uint32_t)D(v, i)))
+H(neg64_std, D(v, i) = 0 - D(v, i))
+H(arsh32r_std, D(v, i) = (uint32_t)((int32_t)(uint32_t)D(v, i) >> (S(v, i) & 31)))
+H(arsh32i_std, D(v, i) = (uint32_t)((int32_t)(uint32_t)D(v, i) >> (U(i) & 31)))
+H(arsh64r_std, D(v, i) = (uint64_t)((int64_t)D(v, i) >> (S(v, i) & 63)))
+H(arsh64i_std, D(v, i) = (uint64_t)((int64_t)D(v, i) >> (SX(i) & 63)))
+H(div32r_std, D(v, i) = (uint32_t)S(v, i) ? (uint32_t)D(v, i) / (uint32_t)S(v, i) : 0)
+H(div32i_std, D(v, i) = U(i) ? (uint32_t)D(v, i) / U(i) : 0)
+H(mod32r_std, D(v, i) = (uint32_t)S(v, i) ? (uint32_t)D(v, i) % (uint32_t)S(v, i) : (uint32_t)D(v, i))
+H(mod32i_std, D(v, i) = U(i) ? (uint32_t)D(v, i) % U(i) : (uint32_t)D(v, i))
+H(div64r_std, D(v, i) = S(v, i) ? D(v, i) / S(v, i) : 0)
+H(div64i_std, D(v, i) = SX(i) ? D(v, i) / SX(i) : 0)
+H(mod64r_std, if (S(v, i)) D(v, i) %= S(v, i))
+H(mod64i_std, if (SX(i)) D(v, i) %= SX(i))
+inline uint32_t D32(cpu_vm &v, const struct ebpf_inst &i) { return (uint32_t)v.reg[i.dst]; }
+inline uint32_t S32(cpu_vm &v, const struct ebpf_inst &i) { return (uint32_t)v.reg[i.src]; }
+J(jeq32r, D32(v, i) == S32(v, i))
+J(jeq32i, D32(v, i) == U(i))
+J(jgt32r, D32(v, i) > S32(v, i))
+J(jgt32i, D32(v, i) > U(i))
+J(jge32r, D32(v, i) >= S32(v, i))
+J(jge32i, D32(v, i) >= U(i))
+J(jset32r, (D32(v, i) & S32(v, i)) != 0)
+J(jset32i, (D32(v, i) & U(i)) != 0)
+J(jne32r, D32(v, i) != S32(v, i))
+J(jne32i, D32(v, i) != U(i))
+J(jsgt32r, (int32_t)D32(v, i) > (int32_t)S32(v, i))
+J(jsgt32i, (int32_t)D32(v, i) > (int32_t)U(i))
+J(jsge32r, (int32_t)D32(v, i) >= (int32_t)S32(v, i))
+J(jsge32i, (int32_t)D32(v, i) >= (int32_t)U(i))
+J(jlt32r, D32(v, i) < S32(v, i))
+J(jlt32i, D32(v, i) < U(i))
+J(jle32r, D32(v, i) <= S32(v, i))
+J(jle32i, D32(v, i) <= U(i))
+J(jslt32r, (int32_t)D32(v, i) < (int32_t)S32(v, i))
+J(jslt32i, (int32_t)D32(v, i) < (int32_t)U(i))
+J(jsle32r, (int32_t)D32(v, i) <= (int32_t)S32(v, i))
+J(jsle32i, (int32_t)D32(v, i) <= (int32_t)U(i))
 bool invalid(cpu_vm &v, const struct ebpf_inst &)
 {
 	fprintf(stderr, "Invalid instruction at PC %u\n", v.pc);
@@ -167,6 +212,27 @@ struct table {
 
 const table k_table;
 
+struct std_table : table {
+	std_table()
+	{
+		const struct { uint8_t op; handler_fn fn; } ops[] = {
+		    {0xbf, mov64r_std}, {0xb7, mov64i_std}, {0x84, neg32_std}, {0x87, neg64_std},
+		    {0xcc, arsh32r_std}, {0xc4, arsh32i_std}, {0xcf, arsh64r_std}, {0xc7, arsh64i_std},
+		    {0x3c, div32r_std}, {0x34, div32i_std}, {0x9c, mod32r_std}, {0x94, mod32i_std},
+		    {0x3f, div64r_std}, {0x37, div64i_std}, {0x9f, mod64r_std}, {0x97, mod64i_std},
+		    {0x16, jeq32i}, {0x1e, jeq32r}, {0x26, jgt32i}, {0x2e, jgt32r}, {0x36, jge32i},
+		    {0x3e, jge32r}, {0x46, jset32i}, {0x4e, jset32r}, {0x56, jne32i}, {0x5e, jne32r},
+		    {0x66, jsgt32i}, {0x6e, jsgt32r}, {0x76, jsge32i}, {0x7e, jsge32r}, {0xa6, jlt32i},
+		    {0xae, jlt32r}, {0xb6, jle32i}, {0xbe, jle32r}, {0xc6, jslt32i}, {0xce, jslt32r},
+		    {0xd6, jsle32i}, {0xde, jsle32r},
+		};
+		for (const auto &o : ops)
+			f[o.op] = o.fn;
+	}
+};
+
+const std_table k_std_table;
+
 } // namespace
 
 EBPF_EXPORT uint64_t
@@ -180,6 +246,16 @@ ebpf_prog_run(void *ctx, struct ebpf_prog *ep)
 	v.helpers = ep->eo.eo_ee->ec->helper_types;
 	v.inst = ep->prog;
 	v.pc = 0;
+	if (ep->semantics.load(std::memory_order_relaxed) == EBPF_SEM_STANDARD) {
+		const uint32_t nslots = ep->prog_len / sizeof(struct ebpf_inst);
+		for (;;) {
+			if (v.pc >= nslots) // (a verifier would have refused the program)
+				invalid(v, *ep->prog);
+			v.inst = ep->prog + v.pc++;
+			if (!k_std_table.f[v.inst->opcode](v, *v.inst))
+				return v.reg[0];
+		}
+	}
 	for (;;) {
 		v.inst = v.inst + v.pc++;
 		if (!k_table.f[v.inst->opcode](v, *v.inst))

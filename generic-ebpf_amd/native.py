@@ -22,6 +22,7 @@ EBPF_NAME_MAX = 64
 EBPF_HIST_BINS = 257
 
 MAP_TYPE_ARRAY, MAP_TYPE_PERCPU_ARRAY, MAP_TYPE_HASHTABLE, MAP_TYPE_PERCPU_HASHTABLE = range(4)
+SEM_REFERENCE, SEM_STANDARD = 0, 1
 HELPER_LOOKUP, HELPER_UPDATE, HELPER_DELETE = range(3)
 EBPF_ANY, EBPF_NOEXIST, EBPF_EXIST = 0, 1, 2
 
@@ -96,6 +97,7 @@ FUNCS = {
     "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_device_info": (_I, [_VP, _VP]),
     "ebpf_prog_device_code": (_I, [_VP, _I, _VP, ctypes.POINTER(ctypes.c_size_t)]),
+    "ebpf_prog_set_semantics": (_I, [_VP, _I]),
 }
 DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_hashtable",
                 "eht_map_lookup_elem", "eht_map_update_elem", "eht_map_delete_elem"]
@@ -270,6 +272,10 @@ class Prog:
         i = DprogInfo()
         _check(lib().ebpf_prog_device_info(self.ptr, ctypes.byref(i)), "ebpf_prog_device_info")
         return i
+
+    def set_semantics(self, semantics):
+        """SEM_REFERENCE (default) or SEM_STANDARD (ebpf_gpu.h ebpf_prog_set_semantics)."""
+        _check(lib().ebpf_prog_set_semantics(self.ptr, semantics), "ebpf_prog_set_semantics")
 
     def prepare(self, device=0):
         _check(lib().ebpf_prog_prepare_device(self.ptr, device), "ebpf_prog_prepare_device")

@@ -104,6 +104,21 @@ int ebpf_gpu_set_device(int device);
  *   2 = the hand-written gfx950 assembly interpreter. */
 int ebpf_gpu_set_variant(int variant);
 
+/* Instruction semantics of a program (extension: the reference has only the first).
+ *   EBPF_SEM_REFERENCE (default): the reference interpreter's, quirks included
+ *       (ebpf_interpreter.c:23-372: cumulative stepping, MOV64 adds, NEG ignores dst, NEG64 is
+ *       dst - imm, logical ARSH, DIV/MOD by zero faults).
+ *   EBPF_SEM_STANDARD: standard eBPF as compilers emit it: sequential pc (a jump goes to
+ *       pc + 1 + off), MOV64 moves (imm sign-extended), NEG/NEG64 negate dst, arithmetic ARSH,
+ *       DIV by zero gives 0 and MOD by zero leaves dst (32-bit ops: truncated), and the JMP32
+ *       class (opcode class 0x06, compares of the low 32 bits).  Device batches accept
+ *       loop-free programs (EOPNOTSUPP otherwise); ebpf_prog_run runs any.
+ * Applies to ebpf_prog_run and to device batches.  Returns 0, EINVAL (bad argument) or EBUSY
+ * (the program was already translated for a device). */
+#define EBPF_SEM_REFERENCE 0
+#define EBPF_SEM_STANDARD 1
+int ebpf_prog_set_semantics(struct ebpf_prog *ep, int semantics);
+
 /* Information about the translated device program. */
 struct ebpf_dprog_info {
 	uint32_t nslots;       /* prog_len / 8 */

@@ -242,7 +242,7 @@ helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_
 }
 
 static inline uint64_t
-run_one(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
+run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
 	uint64_t *steps_out)
 {
 	uint64_t reg[11];
@@ -466,6 +466,261 @@ done:
 	return r0;
 }
 
+/* Standard eBPF (ISA v3 without the v4 extensions), the semantics compilers target and the
+ * Linux interpreter implements: sequential pc (a taken jump goes to pc + 1 + off), MOV64 moves
+ * (imm sign-extended), NEG/NEG64 negate dst, arithmetic ARSH, DIV by zero = 0, MOD by zero =
+ * dst (32-bit: truncated), the JMP32 class comparing the low 32 bits.  Everything else (memory
+ * regions, helpers, LDDW, byte swaps, masked shift counts, fault codes) as in run_ref.
+ * No reference implementation exists to pin this against: it is pinned
+ * by hand-computed known-answer tests (tests/test_standard.py).  A program still running after
+ * 1M instructions is stopped with F_LOOP. */
+static uint64_t
+run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
+	uint64_t *steps_out)
+{
+	uint64_t reg[11];
+	uint8_t stack[STACK_BYTES];
+	struct region_env re;
+	uint64_t pc = 0, steps = 0, r0 = 0;
+	int fault = F_NONE;
+
+	if (checked)
+		memset(stack, p->stack_init, sizeof(stack));
+	for (int i = 0; i < 11; i++)
+		reg[i] = p->reg_init;
+	reg[1] = (uint64_t)(uintptr_t)pkt;
+	reg[10] = (uint64_t)(uintptr_t)(stack + STACK_BYTES);
+	re.pkt_lo = (uint64_t)(uintptr_t)pkt;
+	re.pkt_hi = re.pkt_lo + len;
+	re.stk_lo = (uint64_t)(uintptr_t)stack;
+	re.stk_hi = re.stk_lo + STACK_BYTES;
+	re.p = p;
+
+	for (;;) {
+		if (pc >= p->nslots) {
+			fault = F_SLOT;
+			break;
+		}
+		if (++steps > 1000000) {
+			fault = F_LOOP;
+			break;
+		}
+		const uint8_t *ip = p->insns + pc * 8;
+		uint8_t op = ip[0];
+		uint8_t d = ip[1] & 0x0f, s = ip[1] >> 4;
+		int16_t off;
+		int32_t imm;
+		memcpy(&off, ip + 2, 2);
+		memcpy(&imm, ip + 4, 4);
+		pc++;
+		const int jmp32 = (op & 7) == 6;
+		if (!(valid_op(op) || (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 &&
+				       op != 0x86 && op != 0x96))) {
+			fault = F_BAD_OPCODE;
+			break;
+		}
+		if (jmp32) { /* same register rules as the 64-bit compare */
+			if (d >= 11 || ((op & 0x08) && s >= 11)) {
+				fault = F_BAD_REG;
+				break;
+			}
+		} else if ((uses_dst(op) && d >= 11) || (uses_src(op) && s >= 11)) {
+			fault = F_BAD_REG;
+			break;
+		}
+		uint64_t D = d < 11 ? reg[d] : 0, S = s < 11 ? reg[s] : 0;
+		uint32_t D32 = (uint32_t)D, S32 = (uint32_t)S, I32 = (uint32_t)imm;
+		uint64_t IS = (uint64_t)(int64_t)imm;
+		int taken = -1;
+		int msize = 0;
+		if (jmp32) {
+			const uint32_t B = (op & 0x08) ? S32 : I32;
+			switch (op & 0xf0) {
+			case 0x10: taken = D32 == B; break;
+			case 0x20: taken = D32 > B; break;
+			case 0x30: taken = D32 >= B; break;
+			case 0x40: taken = (D32 & B) != 0; break;
+			case 0x50: taken = D32 != B; break;
+			case 0x60: taken = (int32_t)D32 > (int32_t)B; break;
+			case 0x70: taken = (int32_t)D32 >= (int32_t)B; break;
+			case 0xa0: taken = D32 < B; break;
+			case 0xb0: taken = D32 <= B; break;
+			case 0xc0: taken = (int32_t)D32 < (int32_t)B; break;
+			case 0xd0: taken = (int32_t)D32 <= (int32_t)B; break;
+			}
+		} else switch (op) {
+		/* where standard eBPF differs from the reference */
+		case 0x84: reg[d] = (uint32_t)(0u - D32); break;
+		case 0x87: reg[d] = 0 - D; break;
+		case 0xbf: reg[d] = S; break;
+		case 0xb7: reg[d] = IS; break;
+		case 0xcc: reg[d] = (uint32_t)((int32_t)D32 >> (S32 & 31)); break;
+		case 0xc4: reg[d] = (uint32_t)((int32_t)D32 >> (I32 & 31)); break;
+		case 0xcf: reg[d] = (uint64_t)((int64_t)D >> (S & 63)); break;
+		case 0xc7: reg[d] = (uint64_t)((int64_t)D >> (IS & 63)); break;
+		case 0x3c: reg[d] = S32 ? D32 / S32 : 0; break;
+		case 0x34: reg[d] = I32 ? D32 / I32 : 0; break;
+		case 0x9c: reg[d] = S32 ? D32 % S32 : D32; break;
+		case 0x94: reg[d] = I32 ? D32 % I32 : D32; break;
+		case 0x3f: reg[d] = S ? D / S : 0; break;
+		case 0x37: reg[d] = IS ? D / IS : 0; break;
+		case 0x9f: reg[d] = S ? D % S : D; break;
+		case 0x97: reg[d] = IS ? D % IS : D; break;
+		/* the same as the reference */
+		case 0x0c: reg[d] = (uint32_t)(D32 + S32); break;
+		case 0x04: reg[d] = (uint32_t)(D32 + I32); break;
+		case 0x1c: reg[d] = (uint32_t)(D32 - S32); break;
+		case 0x14: reg[d] = (uint32_t)(D32 - I32); break;
+		case 0x2c: reg[d] = (uint32_t)(D32 * S32); break;
+		case 0x24: reg[d] = (uint32_t)(D32 * I32); break;
+		case 0x4c: reg[d] = D32 | S32; break;
+		case 0x44: reg[d] = D32 | I32; break;
+		case 0x5c: reg[d] = D32 & S32; break;
+		case 0x54: reg[d] = D32 & I32; break;
+		case 0x6c: reg[d] = (uint32_t)(D32 << (S32 & 31)); break;
+		case 0x64: reg[d] = (uint32_t)(D32 << (I32 & 31)); break;
+		case 0x7c: reg[d] = D32 >> (S32 & 31); break;
+		case 0x74: reg[d] = D32 >> (I32 & 31); break;
+		case 0xac: reg[d] = D32 ^ S32; break;
+		case 0xa4: reg[d] = D32 ^ I32; break;
+		case 0xbc: reg[d] = S32; break;
+		case 0xb4: reg[d] = I32; break;
+		case 0xd4:
+			if (imm == 16) reg[d] = (uint16_t)D;
+			else if (imm == 32) reg[d] = D32;
+			break;
+		case 0xdc:
+			if (imm == 16) reg[d] = bs16((uint16_t)D);
+			else if (imm == 32) reg[d] = __builtin_bswap32(D32);
+			else if (imm == 64) reg[d] = __builtin_bswap64(D);
+			break;
+		case 0x0f: reg[d] = D + S; break;
+		case 0x07: reg[d] = D + IS; break;
+		case 0x1f: reg[d] = D - S; break;
+		case 0x17: reg[d] = D - IS; break;
+		case 0x2f: reg[d] = D * S; break;
+		case 0x27: reg[d] = D * IS; break;
+		case 0x4f: reg[d] = D | S; break;
+		case 0x47: reg[d] = D | IS; break;
+		case 0x5f: reg[d] = D & S; break;
+		case 0x57: reg[d] = D & IS; break;
+		case 0x6f: reg[d] = D << (S & 63); break;
+		case 0x67: reg[d] = D << (IS & 63); break;
+		case 0x7f: reg[d] = D >> (S & 63); break;
+		case 0x77: reg[d] = D >> (IS & 63); break;
+		case 0xaf: reg[d] = D ^ S; break;
+		case 0xa7: reg[d] = D ^ IS; break;
+		case 0x05: taken = 1; break;
+		case 0x1d: taken = D == S; break;
+		case 0x15: taken = D == IS; break;
+		case 0x2d: taken = D > S; break;
+		case 0x25: taken = D > IS; break;
+		case 0x3d: taken = D >= S; break;
+		case 0x35: taken = D >= IS; break;
+		case 0x4d: taken = (D & S) != 0; break;
+		case 0x45: taken = (D & IS) != 0; break;
+		case 0x5d: taken = D != S; break;
+		case 0x55: taken = D != IS; break;
+		case 0x6d: taken = (int64_t)D > (int64_t)S; break;
+		case 0x65: taken = (int64_t)D > (int64_t)IS; break;
+		case 0x7d: taken = (int64_t)D >= (int64_t)S; break;
+		case 0x75: taken = (int64_t)D >= (int64_t)IS; break;
+		case 0xad: taken = D < S; break;
+		case 0xa5: taken = D < IS; break;
+		case 0xbd: taken = D <= S; break;
+		case 0xb5: taken = D <= IS; break;
+		case 0xcd: taken = (int64_t)D < (int64_t)S; break;
+		case 0xc5: taken = (int64_t)D < (int64_t)IS; break;
+		case 0xdd: taken = (int64_t)D <= (int64_t)S; break;
+		case 0xd5: taken = (int64_t)D <= (int64_t)IS; break;
+		case 0x85:
+			if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
+				fault = F_HELPER;
+				break;
+			}
+			if (p->helper_kind[imm] != ORACLE_HELPER_MAP_LOOKUP) {
+				fault = F_HELPER_UNSUPPORTED;
+				break;
+			}
+			reg[0] = helper_map_lookup(&re, checked, reg[1], reg[2], &fault);
+			break;
+		case 0x95: r0 = reg[0]; goto done;
+		case 0x71: msize = 1; goto ldx;
+		case 0x69: msize = 2; goto ldx;
+		case 0x61: msize = 4; goto ldx;
+		case 0x79: msize = 8;
+		ldx: {
+			uint64_t a = S + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 0)))
+				break;
+			reg[d] = load_n(a, msize);
+			break;
+		}
+		case 0x18:
+			if (pc >= p->nslots) { fault = F_SLOT; break; }
+			{
+				int32_t hi;
+				memcpy(&hi, p->insns + pc * 8 + 4, 4);
+				reg[d] = (uint64_t)I32 | ((uint64_t)(uint32_t)hi << 32);
+			}
+			pc++;
+			break;
+		case 0x73: msize = 1; goto stx;
+		case 0x6b: msize = 2; goto stx;
+		case 0x63: msize = 4; goto stx;
+		case 0x7b: msize = 8;
+		stx: {
+			uint64_t a = D + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 1)))
+				break;
+			store_n(a, msize, S);
+			break;
+		}
+		case 0x72: msize = 1; goto st;
+		case 0x6a: msize = 2; goto st;
+		case 0x62: msize = 4; goto st;
+		case 0x7a: msize = 8;
+		st: {
+			uint64_t a = D + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 1)))
+				break;
+			store_n(a, msize, IS);
+			break;
+		}
+		default:
+			fault = F_BAD_OPCODE;
+			break;
+		}
+		if (fault)
+			break;
+		if (taken > 0) {
+			int64_t npc = (int64_t)pc + off;
+			if (npc < 0) {
+				fault = F_SLOT;
+				break;
+			}
+			pc = (uint64_t)npc;
+		}
+	}
+done:
+	if (fault)
+		r0 = 0;
+	if (fault_out)
+		*fault_out = (uint8_t)fault;
+	if (steps_out)
+		*steps_out = steps;
+	return r0;
+}
+
+static inline uint64_t
+run_one(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
+	uint64_t *steps_out)
+{
+	if (p->semantics == 1)
+		return run_std(p, checked, pkt, len, fault_out, steps_out);
+	return run_ref(p, checked, pkt, len, fault_out, steps_out);
+}
+
 /* Raw mode: the reference's own cost model — one switch per instruction, operands read inside
  * each case, raw pointer memory access, no fault checks (valid programs only; used for the
  * timed CPU baseline).  Same semantics as run_one(checked=0) on valid programs. */
@@ -615,6 +870,8 @@ oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fau
 {
 	if (p->checked)
 		return run_one(p, 1, pkt, len, fault, steps);
+	if (p->semantics == 1)
+		return run_std(p, 0, pkt, len, fault, steps);
 	uint64_t st = 0;
 	uint64_t r = run_raw(p, pkt, &st);
 	if (fault)

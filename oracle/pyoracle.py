@@ -50,7 +50,8 @@ class _Prog(ctypes.Structure):
     _fields_ = [("insns", ctypes.c_void_p), ("nslots", ctypes.c_uint64),
                 ("helper_kind", ctypes.c_uint8 * 64), ("maps", ctypes.c_void_p),
                 ("nmaps", ctypes.c_uint32), ("reg_init", ctypes.c_uint64),
-                ("stack_init", ctypes.c_uint8), ("checked", ctypes.c_uint8)]
+                ("stack_init", ctypes.c_uint8), ("checked", ctypes.c_uint8),
+                ("semantics", ctypes.c_uint8)]
 
 
 _lib = None
@@ -87,7 +88,7 @@ class OracleProgram:
     [(slot, map_index)] are patched with oracle handles here."""
 
     def __init__(self, code, relocs=(), maps=(), helper_kinds=None, checked=True,
-                 reg_init=0, stack_init=0):
+                 reg_init=0, stack_init=0, semantics=0):
         b = bytearray(code)
         for slot, k in relocs:
             h = oracle_handle(k)
@@ -135,6 +136,7 @@ class OracleProgram:
         self.p.reg_init = reg_init
         self.p.stack_init = stack_init
         self.p.checked = 1 if checked else 0
+        self.p.semantics = semantics
 
     def run(self, data, count, stride=0, offsets=None, nthreads=1):
         """Runs in place on a COPY of ``data``; returns (ret u64[count], faults u8[count],

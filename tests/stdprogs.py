@@ -1,0 +1,191 @@
+"""Standard-eBPF test programs (EBPF_SEM_STANDARD): a sequential assembler with labels, the
+hand-computed known-answer programs, and a seeded generator of loop-free programs."""
+import numpy as np
+
+from generic_ebpf_amd import isa
+
+E = isa.encode
+O = isa.OPS
+JMP32 = {"jeq": 0x16, "jgt": 0x26, "jge": 0x36, "jset": 0x46, "jne": 0x56, "jsgt": 0x66,
+         "jsge": 0x76, "jlt": 0xa6, "jle": 0xb6, "jslt": 0xc6, "jsle": 0xd6}
+JMP64 = {k: v - 1 for k, v in JMP32.items()}   # class 5 twins
+
+
+def asm(items):
+    """items: (op, dst, src, off, imm) tuples (op a name or byte; off may be a label name),
+    ("label", name), ("lddw", dst, value) or ("lddw_map", dst, k).  Returns (code, relocs)."""
+    slots, labels, fix = [], {}, []
+    relocs = []
+    for it in items:
+        if it[0] == "label":
+            labels[it[1]] = len(slots)
+        elif it[0] == "lddw":
+            v = it[2] & 0xffffffffffffffff
+            slots += [E(0x18, it[1], 0, 0, isa.s32(v)), E(0, 0, 0, 0, isa.s32(v >> 32))]
+        elif it[0] == "lddw_map":
+            relocs.append((len(slots), it[2]))
+            slots += [E(0x18, it[1], 0, 0, 0), E(0, 0, 0, 0, 0)]
+        else:
+            op, d, s, off, imm = it
+            op = O[op] if isinstance(op, str) else op
+            if isinstance(off, str):
+                fix.append((len(slots), off))
+                off = 0
+            slots.append([op, d, s, off, imm])
+    out = []
+    for i, x in enumerate(slots):
+        if isinstance(x, list):
+            for at, lab in fix:
+                if at == i:
+                    x[3] = labels[lab] - (i + 1)
+            out.append(E(*x))
+        else:
+            out.append(x)
+    return b"".join(out), relocs
+
+
+def I(op, d=0, s=0, off=0, imm=0):
+    return (op, d, s, off, imm)
+
+
+# (name, items, packet bytes (64), expected r0) — every expectation worked out by hand from the
+# standard semantics (comments), not computed by any of the implementations under test
+PKT = bytes(range(64))
+KATS = [
+    ("mov64_imm_moves", [I("mov64_imm", 0, imm=5), I("mov64_imm", 0, imm=7), I("exit")], 7),
+    ("mov64_imm_sign_extends", [I("mov64_imm", 0, imm=-1), I("exit")], 0xffffffffffffffff),
+    ("mov64_reg_moves", [I("mov64_imm", 2, imm=3), I("mov64_imm", 0, imm=100),
+                         I("mov64_reg", 0, 2), I("exit")], 3),
+    ("neg64", [I("mov64_imm", 0, imm=5), I("neg64", 0), I("exit")], (-5) & (2**64 - 1)),
+    ("neg32", [I("mov64_imm", 0, imm=5), I("neg", 0), I("exit")], 0xfffffffb),
+    ("neg32_of_big", [("lddw", 0, 0x1_0000_0001), I("neg", 0), I("exit")], 0xffffffff),
+    ("arsh64_imm", [I("mov64_imm", 0, imm=-16), I("arsh64_imm", 0, imm=2), I("exit")],
+     (-4) & (2**64 - 1)),
+    ("arsh64_reg_63", [I("mov64_imm", 0, imm=-2), I("mov64_imm", 2, imm=63),
+                       I("arsh64_reg", 0, 2), I("exit")], 2**64 - 1),
+    ("arsh32_imm", [I("mov_imm", 0, imm=isa.s32(0x80000000)), I("arsh_imm", 0, imm=4), I("exit")],
+     0xf8000000),
+    ("arsh32_reg_positive", [I("mov_imm", 0, imm=0x40000000), I("mov64_imm", 3, imm=30),
+                             I("arsh_reg", 0, 3), I("exit")], 1),
+    ("arsh32_truncates_upper", [("lddw", 0, 0xffff_ffff_0000_0100), I("arsh_imm", 0, imm=4),
+                                I("exit")], 0x10),
+    ("div64_reg_by_zero_is_zero", [I("mov64_imm", 0, imm=10), I("mov64_imm", 2, imm=0),
+                                   I("div64_reg", 0, 2), I("exit")], 0),
+    ("mod64_reg_by_zero_keeps_dst", [I("mov64_imm", 0, imm=10), I("mov64_imm", 2, imm=0),
+                                     I("mod64_reg", 0, 2), I("exit")], 10),
+    ("mod32_reg_by_zero_truncates", [("lddw", 0, 0x1_0000_0007), I("mov64_imm", 2, imm=0),
+                                     I("mod_reg", 0, 2), I("exit")], 7),
+    ("div32_imm_zero", [I("mov64_imm", 0, imm=9), I("div_imm", 0, imm=0), I("exit")], 0),
+    ("mod64_imm_zero", [I("mov64_imm", 0, imm=9), I("mod64_imm", 0, imm=0), I("exit")], 9),
+    ("div32_reg_by_upper_only_is_zero", [I("mov64_imm", 0, imm=9), ("lddw", 2, 0x1_0000_0000),
+                                         I("div_reg", 0, 2), I("exit")], 0),
+    ("div64_normal", [I("mov64_imm", 0, imm=100), I("mov64_imm", 2, imm=7),
+                      I("div64_reg", 0, 2), I("exit")], 14),
+    ("ja_sequential", [I("mov64_imm", 0, imm=1), I("ja", off="L"), I("mov64_imm", 0, imm=2),
+                       ("label", "L"), I("exit")], 1),
+    ("jeq_taken_skips", [I("mov64_imm", 0, imm=0), I("mov64_imm", 2, imm=5),
+                         I("jeq_imm", 2, imm=5, off="L"), I("mov64_imm", 0, imm=9),
+                         ("label", "L"), I("exit")], 0),
+    ("jeq_not_taken", [I("mov64_imm", 0, imm=0), I("mov64_imm", 2, imm=4),
+                       I("jeq_imm", 2, imm=5, off="L"), I("mov64_imm", 0, imm=9),
+                       ("label", "L"), I("exit")], 9),
+    ("jmp32_eq_low_word", [I("mov64_imm", 0, imm=0), ("lddw", 2, 0x1_0000_0005),
+                           I(JMP32["jeq"], 2, imm=5, off="A"), I("add64_imm", 0, imm=1),
+                           ("label", "A"), I("jeq_imm", 2, imm=5, off="B"),
+                           I("add64_imm", 0, imm=2), ("label", "B"), I("exit")], 2),
+    ("jmp32_signed", [I("mov64_imm", 0, imm=0), I("mov_imm", 2, imm=-1),
+                      I(JMP32["jsgt"], 2, imm=0, off="A"), I("add64_imm", 0, imm=1),
+                      ("label", "A"), I(JMP32["jgt"], 2, imm=0, off="B"),
+                      I("add64_imm", 0, imm=2), ("label", "B"), I("exit")], 1),
+    ("jmp32_reg_unsigned", [I("mov64_imm", 0, imm=0), ("lddw", 2, 0x5_0000_0003),
+                            ("lddw", 3, 0x1_0000_0004), I(JMP32["jlt"] | 8, 2, 3, off="A"),
+                            I("add64_imm", 0, imm=1), ("label", "A"),
+                            I(JMP64["jlt"] | 8, 2, 3, off="B"), I("add64_imm", 0, imm=2),
+                            ("label", "B"), I("exit")], 2),
+    ("jmp32_jset", [I("mov64_imm", 0, imm=0), ("lddw", 2, 0x1_0000_0000),
+                    I(JMP32["jset"], 2, imm=-1, off="A"), I("add64_imm", 0, imm=1),
+                    ("label", "A"), I("exit")], 1),
+    ("lddw_full", [("lddw", 0, 0x1122334455667788), I("exit")], 0x1122334455667788),
+    ("stack_roundtrip", [("lddw", 2, 0x1122334455667788), I("stxdw", 10, 2, -8),
+                         I("ldxw", 0, 10, -8), I("exit")], 0x55667788),
+    ("ctx_copy_and_load", [I("mov64_reg", 6, 1), I("mov64_imm", 1, imm=0),
+                           I("ldxb", 0, 6, 3), I("exit")], 3),
+    ("packet_be16", [I("ldxh", 0, 1, 12), I("be", 0, imm=16), I("exit")], 0x0c0d),
+    ("pointer_arith_clang_style", [I("mov64_reg", 2, 1), I("add64_imm", 2, imm=8),
+                                   I("ldxdw", 0, 2, 0), I("exit")], 0x0f0e0d0c0b0a0908),
+    ("shift_masks", [I("mov64_imm", 0, imm=1), I("mov64_imm", 2, imm=65),
+                     I("lsh64_reg", 0, 2), I("exit")], 2),
+    ("alu32_zero_extends", [I("mov64_imm", 0, imm=-1), I("add_imm", 0, imm=1), I("exit")], 0),
+    ("loop_free_diamond", [I("ldxb", 2, 1, 5), I("mov64_imm", 0, imm=10),
+                           I("jgt_imm", 2, imm=4, off="T"), I("mov64_imm", 0, imm=20),
+                           I("ja", off="J"), ("label", "T"), I("mov64_imm", 0, imm=30),
+                           ("label", "J"), I("add64_imm", 0, imm=1), I("exit")], 31),
+]
+
+
+def gen_program(seed, length=40, with_map=False):
+    """A loop-free standard program: r6 = ctx, r0-r5/r7-r9 seeded with immediates, then
+    `length` random ALU32/ALU64 ops (every opcode, divisors possibly zero), byte swaps, packet
+    loads in range, stack stores/loads, forward JMP/JMP32 branches, an optional hashless array
+    lookup; EXIT with r0."""
+    g = np.random.default_rng(seed)
+    regs = [0, 1, 2, 3, 4, 5, 7, 8, 9]
+    items = [I("mov64_reg", 6, 1)]
+    for r in regs:
+        items.append(I("mov64_imm", r, imm=int(g.integers(-2**31, 2**31))))
+    for k in range(1, 9):      # every stack slot the program may read is defined on all paths
+        items.append(I("stxdw", 10, regs[k], -8 * k))
+    alu = ["add", "sub", "mul", "div", "or", "and", "lsh", "rsh", "mod", "xor", "mov", "arsh"]
+    pending = []   # (label, position to place it)
+    nlab = 0
+    stored = []
+    for k in range(length):
+        for lab, at in list(pending):
+            if at == k:
+                items.append(("label", lab))
+                pending.remove((lab, at))
+        c = g.random()
+        d = int(g.choice(regs))
+        if c < 0.55:
+            name = alu[int(g.integers(0, len(alu)))]
+            w64 = g.random() < 0.6
+            if g.random() < 0.5:
+                imm = int(g.integers(-40, 40)) if g.random() < 0.5 else int(g.integers(-2**31, 2**31))
+                items.append(I(name + ("64_imm" if w64 else "_imm"), d, imm=imm))
+            else:
+                items.append(I(name + ("64_reg" if w64 else "_reg"), d, int(g.choice(regs))))
+        elif c < 0.6:
+            items.append(I("neg64" if g.random() < 0.5 else "neg", d))
+        elif c < 0.65:
+            items.append(I("be" if g.random() < 0.5 else "le", d, imm=int(g.choice([16, 32, 64]))))
+        elif c < 0.75:
+            z = int(g.choice([1, 2, 4, 8]))
+            op = {1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[z]
+            items.append(I(op, d, 6, int(g.integers(0, 64 - z + 1))))
+        elif c < 0.82:
+            so = -8 * int(g.integers(1, 9))
+            items.append(I("stxdw", 10, int(g.choice(regs)), so))
+            stored.append(so)
+        elif c < 0.86:
+            items.append(I("ldxdw", d, 10, -8 * int(g.integers(1, 9))))
+        elif k < length - 2:
+            lab = "L%d" % nlab
+            nlab += 1
+            conds = list(JMP32)
+            cn = conds[int(g.integers(0, len(conds)))]
+            tab = JMP32 if g.random() < 0.5 else JMP64
+            op = tab[cn] + (8 if g.random() < 0.5 else 0)
+            if op & 8:
+                items.append(I(op, d, int(g.choice(regs)), lab))
+            else:
+                items.append(I(op, d, 0, lab, int(g.integers(-50, 50))))
+            pending.append((lab, int(g.integers(k + 1, length + 1))))
+    if with_map:
+        items += [I("mov64_reg", 7, 0), I("and64_imm", 7, imm=15), I("stxw", 10, 7, -4),
+                  ("lddw_map", 1, 0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                  I("call", imm=0), I("jeq_imm", 0, imm=0, off="M"),
+                  I("ldxdw", 0, 0, 0), ("label", "M")]
+    for lab, at in pending:
+        items.append(("label", lab))
+    items.append(I("exit"))
+    return asm(items)
