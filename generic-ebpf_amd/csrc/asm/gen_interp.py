@@ -138,6 +138,21 @@ for z in SIZES:
 fam("HLOOKUP", 0)              # hashtable lookup, map known at translation time (s14 = record offset)
 for z in SIZES:
     fam("LDXHV%d" % z, 2)       # load from a hashtable value (lookup result), in range by provenance
+# standard-eBPF semantics (ebpf_prog_set_semantics): the operations whose meaning differs from
+# the reference's, and the JMP32 class
+fam("MOV64R", 2)
+fam("NEG64", 1)
+fam("NEG32", 1)
+fam("ARSH64I", 1)
+fam("ARSH64R", 2)
+fam("ARSH32I", 1)
+fam("ARSH32R", 2)
+for o in ("DIV64Z", "MOD64Z", "DIV32Z", "MOD32Z"):
+    fam(o, 2)                  # register divisor; zero gives 0 (DIV) or dst (MOD)
+for c in CONDS:
+    fam("J32" + c[1:] + "_R", 2)
+for c in CONDS:
+    fam("J32" + c[1:] + "_I", 1)
 
 
 def variants(arity):
@@ -298,9 +313,11 @@ def h_alu32i(op, d):
     return body[op] + ["v_mov_b32 %s, 0" % D1]
 
 
-def divmod_body(d, sr, imm, op, bits):
+def divmod_body(d, sr, imm, op, bits, zero_ok=False):
     """Operands to R[0:1] (n) and R[2:3] (den); lanes with den == 0 fault DIV_ZERO (the
-    reference raises SIGFPE); quotient / remainder from the shared restoring divider."""
+    reference raises SIGFPE), or with zero_ok (standard eBPF) get 0 (DIV) or n (MOD: the
+    divider's remainder for a zero divisor is n); quotient / remainder from the shared
+    restoring divider."""
     n0, n1, d0, d1 = v(R[0]), v(R[1]), v(R[2]), v(R[3])
     out = ["v_mov_b32 %s, %s" % (n0, lo(d))]
     out.append("v_mov_b32 %s, %s" % (n1, hi(d) if bits == 64 else "0"))
@@ -309,7 +326,7 @@ def divmod_body(d, sr, imm, op, bits):
     else:
         out += ["v_mov_b32 %s, %s" % (d0, lo(sr)),
                 "v_mov_b32 %s, %s" % (d1, hi(sr) if bits == 64 else "0")]
-    if not imm:  # immediate divisors are never 0 here (the translator faults them statically)
+    if not imm and not zero_ok:  # (immediate zero divisors are resolved by the translator)
         out += ["v_cmp_eq_u64_e64 %s, %s, 0" % (sp(S_MASK), vp(R[2])),
                 "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
                 "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
@@ -318,6 +335,10 @@ def divmod_body(d, sr, imm, op, bits):
         out.append(".Ldz_{uid}:")
     out += call(".Lr_udiv")
     q0, q1, r0, r1 = v(R[4]), v(R[5]), v(R[6]), v(R[7])
+    if zero_ok and op == "DIV":
+        out += ["v_cmp_eq_u64_e64 vcc, 0, %s" % vp(R[2]),
+                "v_cndmask_b32_e64 %s, %s, 0, vcc" % (q0, q0),
+                "v_cndmask_b32_e64 %s, %s, 0, vcc" % (q1, q1)]
     src = (q0, q1) if op == "DIV" else (r0, r1)
     out += ["v_mov_b32 %s, %s" % (lo(d), src[0]),
             "v_mov_b32 %s, %s" % (hi(d), src[1] if bits == 64 else "0")]
@@ -350,6 +371,44 @@ def h_cond(c, d, sr, imm):
             ] + goto(".Lr_diverge") + [
             ".Ltk_{uid}:"] + dispatch(13) + [".Lnt_{uid}:"] + dispatch(12)
     return out, True   # (body, has own dispatch)
+
+
+CMP32 = {"JEQ": "eq_u32", "JNE": "ne_u32", "JGT": "gt_u32", "JGE": "ge_u32", "JLT": "lt_u32",
+         "JLE": "le_u32", "JSGT": "gt_i32", "JSGE": "ge_i32", "JSLT": "lt_i32", "JSLE": "le_i32"}
+
+
+def h_cond32(c, d, sr, imm):
+    """JMP32: the compare of the low 32 bits (s10 = u32(imm) for the immediate form)."""
+    srcop = "s10" if imm else lo(sr)
+    if c == "JSET":
+        out = ["v_and_b32 %s, %s, %s" % (v(H[0]), srcop, lo(d)),
+               "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[0])]
+    else:
+        out = ["v_cmp_%s_e64 vcc, %s, %s" % (CMP32[c], lo(d), srcop)]
+    body, own = h_cond(c, d, sr, imm)
+    return out + body[body.index("@CMPEND"):], own
+
+
+def h_std(name, d, sr):
+    """Standard-eBPF operations (ebpf_gpu.h EBPF_SEM_STANDARD)."""
+    D0, D1 = lo(d), hi(d)
+    if name == "MOV64R":
+        return ["v_mov_b64 %s, %s" % (pair(d), pair(sr))]
+    if name == "NEG64":
+        return ["v_sub_co_u32 %s, vcc, 0, %s" % (D0, D0),
+                "v_subb_co_u32 %s, vcc, 0, %s, vcc" % (D1, D1)]
+    if name == "NEG32":
+        return ["v_sub_u32 %s, 0, %s" % (D0, D0), "v_mov_b32 %s, 0" % D1]
+    if name == "ARSH64I":
+        return ["v_ashrrev_i64 %s, s10, %s" % (pair(d), pair(d))]
+    if name == "ARSH64R":
+        return ["v_ashrrev_i64 %s, %s, %s" % (pair(d), lo(sr), pair(d))]
+    if name == "ARSH32I":
+        return ["v_ashrrev_i32 %s, s10, %s" % (D0, D0), "v_mov_b32 %s, 0" % D1]
+    if name == "ARSH32R":
+        return ["v_ashrrev_i32 %s, %s, %s" % (D0, lo(sr), D0), "v_mov_b32 %s, 0" % D1]
+    op, bits = name[:3], int(name[3:5])
+    return divmod_body(d, sr, None, op, bits, zero_ok=True)
 
 
 def h_bswap(w, d):
@@ -787,6 +846,12 @@ def handler_body(name, d, sr):
         return h_ldx_map(int(name[6:]), d, sr), False
     if name.startswith("LDXHV"):
         return h_ldx_hv(int(name[5:]), d, sr), False
+    if name in ("MOV64R", "NEG64", "NEG32", "ARSH64I", "ARSH64R", "ARSH32I", "ARSH32R",
+                "DIV64Z", "MOD64Z", "DIV32Z", "MOD32Z"):
+        return h_std(name, d, sr), False
+    if name.startswith("J32"):
+        c = "J" + name[3:-2]
+        return h_cond32(c, d, sr, name.endswith("_I"))
     if name.startswith("STXGEN"):
         return h_stx_gen(int(name[6:]), d, sr), False
     if name.startswith("STGEN"):

@@ -17,7 +17,22 @@ enum dp_kind : uint16_t {
 	// 0x00..0xff: the eBPF opcode itself (ALU, ALU64, LDX, ST, STX, LDDW, cond jumps, EXIT)
 	DK_FAULT = 0x100,       // terminal: aux = ebpf_fault code
 	DK_CALL_LOOKUP = 0x101, // r0 = map_lookup_elem(r1, r2)  (ebpf_map.c:77-84)
+	// standard-eBPF semantics (EBPF_SEM_STANDARD) where they differ from the reference's;
+	// MOV64_IMM becomes an LDDW entry (dst = sext(imm)), and JMP32 entries keep their opcode
+	// (class 0x06)
+	DK_MOV64R = 0x102,  // dst = src
+	DK_NEG64 = 0x103,   // dst = -dst
+	DK_NEG32 = 0x104,   // dst = u32(-dst)
+	DK_ARSH64I = 0x105, // dst = (s64)dst >> imm   (imm already masked to 63)
+	DK_ARSH64R = 0x106, // dst = (s64)dst >> (src & 63)
+	DK_ARSH32I = 0x107, // dst = u32((s32)dst >> imm)
+	DK_ARSH32R = 0x108, // dst = u32((s32)dst >> (src & 31))
+	DK_DIV64Z = 0x109,  // dst = src ? dst / src : 0
+	DK_MOD64Z = 0x10a,  // dst = src ? dst % src : dst
+	DK_DIV32Z = 0x10b,  // 32-bit forms, results zero-extended
+	DK_MOD32Z = 0x10c,
 };
+#define DP_CLS_JMP32 6
 
 struct dp_entry {
 	uint64_t handler; // asm interpreter: absolute handler address (patched per device)

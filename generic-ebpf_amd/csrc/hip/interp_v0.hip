@@ -217,6 +217,37 @@ ebpf_interp_v0(dp_launch L)
 			R[0][tid] = res;
 			continue;
 		}
+		if (k >= DK_MOV64R && k <= DK_MOD32Z) { // standard-eBPF operations
+			const uint64_t d = R[e.dst][tid], s = R[e.src][tid];
+			const uint32_t d32 = (uint32_t)d, s32 = (uint32_t)s;
+			uint64_t r;
+			switch (k) {
+			case DK_MOV64R: r = s; break;
+			case DK_NEG64: r = 0 - d; break;
+			case DK_NEG32: r = (uint32_t)(0u - d32); break;
+			case DK_ARSH64I: r = (uint64_t)((int64_t)d >> (e.imm & 63)); break;
+			case DK_ARSH64R: r = (uint64_t)((int64_t)d >> (s & 63)); break;
+			case DK_ARSH32I: r = (uint32_t)((int32_t)d32 >> (e.imm & 31)); break;
+			case DK_ARSH32R: r = (uint32_t)((int32_t)d32 >> (s32 & 31)); break;
+			case DK_DIV64Z: r = s ? d / s : 0; break;
+			case DK_MOD64Z: r = s ? d % s : d; break;
+			case DK_DIV32Z: r = s32 ? d32 / s32 : 0; break;
+			default: r = s32 ? d32 % s32 : d32; break;
+			}
+			R[e.dst][tid] = r;
+			continue;
+		}
+		if (cls == DP_CLS_JMP32) { // standard eBPF: compares of the low 32 bits
+			const uint32_t d = (uint32_t)R[e.dst][tid];
+			const uint32_t s = (k & 0x08) ? (uint32_t)R[e.src][tid] : (uint32_t)e.imm;
+			const bool sg = (k & 0xf0) == 0x60 || (k & 0xf0) == 0x70 || (k & 0xf0) == 0xc0 ||
+					(k & 0xf0) == 0xd0;
+			const uint64_t dx = sg ? (uint64_t)(int64_t)(int32_t)d : d;
+			const uint64_t sx = sg ? (uint64_t)(int64_t)(int32_t)s : s;
+			if (cond_taken(k, dx, sx))
+				T = e.target;
+			continue;
+		}
 		if (cls == 0x5) { // conditional jumps (JA and CALL/EXIT handled above / folded)
 			const uint64_t d = R[e.dst][tid];
 			const uint64_t s = (k & 0x08) ? R[e.src][tid] : e.imm;

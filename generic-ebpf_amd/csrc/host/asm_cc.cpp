@@ -71,7 +71,7 @@ enum : uint32_t {
 	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c,
 };
 // VOPC compare codes: base + {lt 1, eq 2, le 3, gt 4, ne 5, ge 6}
-enum : uint32_t { VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
+enum : uint32_t { VC_I32 = 0xc0, VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
 enum { P_LT = 1, P_EQ = 2, P_LE = 3, P_GT = 4, P_NE = 5, P_GE = 6 };
 const uint32_t S_WAITCNT_LGKM0 = 0xbf8cc07fu;
 const int S_JUNK = 60; // s[60:61]: carry-out sink of v_mad_u64_u32 (gen_interp.py S_JUNK)
@@ -1058,12 +1058,64 @@ struct emitter {
 		}
 		E.vopc((c >= 6 ? VC_I64 : VC_U64) + pred(c), vreg(L(d)), L(s));
 	}
+	// JMP32: compares of the low words
+	static bool eval32(int c, uint32_t a, uint32_t b)
+	{
+		switch (c) {
+		case 0: return a == b;
+		case 1: return a != b;
+		case 2: return a > b;
+		case 3: return a >= b;
+		case 4: return a < b;
+		case 5: return a <= b;
+		case 6: return (int32_t)a > (int32_t)b;
+		case 7: return (int32_t)a >= (int32_t)b;
+		case 8: return (int32_t)a < (int32_t)b;
+		case 9: return (int32_t)a <= (int32_t)b;
+		default: return (a & b) != 0;
+		}
+	}
+	void cond32_imm(int c, int d, uint32_t K)
+	{
+		const rf &x = f.r[d];
+		if (x.c) {
+			decided(eval32(c, (uint32_t)x.v, K));
+			return;
+		}
+		use(d);
+		if (c == 10) {
+			if (!K) {
+				decided(false);
+				return;
+			}
+			E.vop2(V2_AND, T0, k32(K), L(d));
+			E.vopc(VC_U32 + P_NE, opnd{128}, T0);
+			return;
+		}
+		E.vopc((c >= 6 ? VC_I32 : VC_U32) + swapped(pred(c)), k32(K), L(d));
+	}
+	void cond32_reg(int c, int d, int s)
+	{
+		if (f.r[s].c) {
+			cond32_imm(c, d, (uint32_t)f.r[s].v);
+			return;
+		}
+		use(d);
+		use(s);
+		if (c == 10) {
+			E.vop2(V2_AND, T0, vreg(L(s)), L(d));
+			E.vopc(VC_U32 + P_NE, opnd{128}, T0);
+			return;
+		}
+		E.vopc((c >= 6 ? VC_I32 : VC_U32) + pred(c), vreg(L(d)), L(s));
+	}
 };
 
 bool
 is_cond_fam(int fam)
 {
-	return (fam >= AHF_JEQ_R && fam <= AHF_JSET_R) || (fam >= AHF_JEQ_I && fam <= AHF_JSET_I);
+	return (fam >= AHF_JEQ_R && fam <= AHF_JSET_R) || (fam >= AHF_JEQ_I && fam <= AHF_JSET_I) ||
+	       (fam >= AHF_J32EQ_R && fam <= AHF_J32SET_R) || (fam >= AHF_J32EQ_I && fam <= AHF_J32SET_I);
 }
 
 // the register a copied handler body writes (-1: none)
@@ -1362,6 +1414,12 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					em.cond_imm(fam - AHF_JEQ_I, d, K);
 				else if (fam >= AHF_JEQ_R && fam <= AHF_JSET_R)
 					em.cond_reg(fam - AHF_JEQ_R, d, s);
+				else if (fam >= AHF_J32EQ_I && fam <= AHF_J32SET_I)
+					em.cond32_imm(fam - AHF_J32EQ_I, d, (uint32_t)K);
+				else if (fam >= AHF_J32EQ_R && fam <= AHF_J32SET_R)
+					em.cond32_reg(fam - AHF_J32EQ_R, d, s);
+				else if (fam == AHF_MOV64R)
+					em.copy64(d, s);
 				else
 					ok = false;
 			}
@@ -1411,11 +1469,12 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			};
 			if (is_cond) {
 				const uint32_t tk = xl.entries[e].target;
+				const bool c64 = fam <= AHF_JSET_I; // (JMP32 edges refine nothing)
 				const int c = fam >= AHF_JEQ_I ? fam - AHF_JEQ_I : fam - AHF_JEQ_R;
 				const bool cimm = fam >= AHF_JEQ_I || f.r[s].c;
 				const uint64_t cv = fam >= AHF_JEQ_I ? K : f.r[s].v;
 				facts ft = f, fn = f;
-				if (cimm && d < AH_NREGS) {
+				if (c64 && cimm && d < AH_NREGS) {
 					refine(ft, c, d, cv, true);
 					refine(fn, c, d, cv, false);
 				}

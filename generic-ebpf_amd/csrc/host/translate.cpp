@@ -67,9 +67,11 @@ struct Translator {
 	uint32_t fault_id[EBPF_FAULT_MAX];
 	std::vector<std::pair<uint32_t, uint64_t>> pending; // (entry, state) to fill
 	bool overflow = false;
+	bool std_mode = false; // EBPF_SEM_STANDARD: sequential pc, the state is the slot alone
 
-	Translator(const struct ebpf_inst *c, uint64_t n, const struct ebpf_config *e, dprog_host &o)
-	    : code(c), nslots(n), ec(e), out(o)
+	Translator(const struct ebpf_inst *c, uint64_t n, const struct ebpf_config *e, dprog_host &o,
+		   bool std_sem)
+	    : code(c), nslots(n), ec(e), out(o), std_mode(std_sem)
 	{
 		for (auto &f : fault_id)
 			f = UINT32_MAX;
@@ -117,6 +119,16 @@ struct Translator {
 				break;
 			}
 			const struct ebpf_inst &in = code[idx];
+			if (std_mode && in.opcode == EBPF_OP_JA && hops <= nslots + 2) {
+				aliases.push_back(key(idx, pc));
+				const uint64_t nidx = idx + 1 + (uint64_t)(int64_t)in.offset;
+				if (nidx == idx) {
+					id = fault(EBPF_FAULT_LOOP);
+					break;
+				}
+				idx = nidx;
+				continue;
+			}
 			if (in.opcode == EBPF_OP_JA && hops <= nslots + 2) {
 				uint32_t np = pc + (uint32_t)(int32_t)in.offset;
 				uint64_t nidx = idx + np;
@@ -144,6 +156,65 @@ struct Translator {
 		return id;
 	}
 
+	// Standard semantics: entries for the operations whose meaning differs from the reference's
+	// (returns true when `e` is complete; its successor is the next slot).
+	bool std_rewrite(dp_entry &e, const struct ebpf_inst &in)
+	{
+		const uint8_t op = in.opcode;
+		const uint64_t sx = (uint64_t)(int64_t)in.imm, zx = (uint64_t)(uint32_t)in.imm;
+		switch (op) {
+		case EBPF_OP_MOV64_IMM: e.kind = EBPF_OP_LDDW; e.imm = sx; return true;
+		case EBPF_OP_MOV64_REG: e.kind = DK_MOV64R; return true;
+		case EBPF_OP_NEG64: e.kind = DK_NEG64; return true;
+		case EBPF_OP_NEG: e.kind = DK_NEG32; return true;
+		case EBPF_OP_ARSH64_IMM: e.kind = DK_ARSH64I; e.imm = sx & 63; return true;
+		case EBPF_OP_ARSH64_REG: e.kind = DK_ARSH64R; return true;
+		case EBPF_OP_ARSH_IMM: e.kind = DK_ARSH32I; e.imm = zx & 31; return true;
+		case EBPF_OP_ARSH_REG: e.kind = DK_ARSH32R; return true;
+		case EBPF_OP_DIV64_REG: e.kind = DK_DIV64Z; return true;
+		case EBPF_OP_MOD64_REG: e.kind = DK_MOD64Z; return true;
+		case EBPF_OP_DIV_REG: e.kind = DK_DIV32Z; return true;
+		case EBPF_OP_MOD_REG: e.kind = DK_MOD32Z; return true;
+		case EBPF_OP_DIV64_IMM: // by a zero immediate: dst = 0
+			if (sx != 0)
+				return false;
+			e.kind = EBPF_OP_LDDW;
+			e.imm = 0;
+			return true;
+		case EBPF_OP_MOD64_IMM: // by a zero immediate: dst unchanged (dst += 0)
+			if (sx != 0)
+				return false;
+			e.kind = EBPF_OP_ADD64_IMM;
+			e.imm = 0;
+			return true;
+		case EBPF_OP_DIV_IMM: // 32-bit: dst = 0
+			if (zx != 0)
+				return false;
+			e.kind = EBPF_OP_MOV_IMM;
+			e.imm = 0;
+			return true;
+		case EBPF_OP_MOD_IMM: // 32-bit: dst = u32(dst)
+			if (zx != 0)
+				return false;
+			e.kind = EBPF_OP_MOV_REG;
+			e.src = e.dst;
+			return true;
+		default:
+			return false;
+		}
+	}
+
+	static bool valid_jmp32(uint8_t op)
+	{
+		switch (op & 0xf0) {
+		case 0x10: case 0x20: case 0x30: case 0x40: case 0x50: case 0x60: case 0x70:
+		case 0xa0: case 0xb0: case 0xc0: case 0xd0:
+			return true;
+		default:
+			return false;
+		}
+	}
+
 	// Fill one entry; returns the fallthrough successor if it was newly created (so the
 	// caller continues the straight-line run), else UINT32_MAX.
 	void fill(uint32_t id, uint64_t idx, uint32_t pc, std::vector<uint64_t> &deferred_taken,
@@ -158,11 +229,14 @@ struct Translator {
 			x.kind = DK_FAULT;
 			x.aux = (uint16_t)c;
 		};
-		if (!valid_op(op)) {
+		const bool jmp32 = std_mode && (op & 7) == DP_CLS_JMP32;
+		if (jmp32 ? !valid_jmp32(op) : !valid_op(op)) {
 			make_fault(EBPF_FAULT_BAD_OPCODE);
 			return;
 		}
-		if ((uses_dst(op) && in.dst >= EBPF_REG_MAX) || (uses_src(op) && in.src >= EBPF_REG_MAX)) {
+		if (jmp32 ? (in.dst >= EBPF_REG_MAX || ((op & 0x08) && in.src >= EBPF_REG_MAX))
+			  : ((uses_dst(op) && in.dst >= EBPF_REG_MAX) ||
+			     (uses_src(op) && in.src >= EBPF_REG_MAX))) {
 			make_fault(EBPF_FAULT_BAD_REG);
 			return;
 		}
@@ -173,8 +247,18 @@ struct Translator {
 		uint8_t cls = op & 7;
 		uint64_t sx = (uint64_t)(int64_t)in.imm;
 		uint64_t zx = (uint64_t)(uint32_t)in.imm;
-		uint64_t next_idx = idx + pc;
-		uint32_t next_pc = pc + 1;
+		uint64_t next_idx = std_mode ? idx + 1 : idx + pc;
+		uint32_t next_pc = std_mode ? 0 : pc + 1;
+		if (std_mode && std_rewrite(e, in)) {
+			bool created;
+			uint32_t n = get(next_idx, next_pc, &created);
+			out.entries[id].next = n;
+			if (created)
+				*next_new = n;
+			return;
+		}
+		if (jmp32)
+			cls = EBPF_CLS_JMP; // (a conditional jump; the entry keeps its class-6 opcode)
 		switch (cls) {
 		case EBPF_CLS_ALU: {
 			uint8_t alu = op & 0xf0;
@@ -206,8 +290,8 @@ struct Translator {
 				return;
 			}
 			e.imm = zx | ((uint64_t)(uint32_t)code[idx + 1].imm << 32);
-			next_idx = idx + pc + 1;
-			next_pc = pc + 2;
+			next_idx = std_mode ? idx + 2 : idx + pc + 1;
+			next_pc = std_mode ? 0 : pc + 2;
 			break;
 		case EBPF_CLS_ST:
 			e.imm = sx;
@@ -237,11 +321,11 @@ struct Translator {
 				e.kind = DK_CALL_LOOKUP;
 				break;
 			}
-			e.imm = sx;
+			e.imm = jmp32 ? zx : sx;
 			{
 				uint32_t np = pc + (uint32_t)(int32_t)in.offset;
-				uint64_t tidx = idx + np;
-				uint32_t tpc = np + 1;
+				uint64_t tidx = std_mode ? idx + 1 + (uint64_t)(int64_t)in.offset : idx + np;
+				uint32_t tpc = std_mode ? 0 : np + 1;
 				if (tidx == idx && tpc == pc) {
 					uint32_t f = fault(EBPF_FAULT_LOOP); // may grow entries: no `e` after this
 					out.entries[id].target = f;
@@ -332,6 +416,14 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 	const uint16_t k = e.kind;
 	if (k == DK_FAULT || k == EBPF_OP_EXIT)
 		return;
+	if (k == DK_MOV64R) {
+		r[e.dst] = r[e.src];
+		return;
+	}
+	if (k >= DK_NEG64 && k <= DK_MOD32Z) {
+		r[e.dst] = av();
+		return;
+	}
 	if (k == DK_CALL_LOOKUP) {
 		av res;
 		if (r[1].kind == AV_CONST)
@@ -342,7 +434,7 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		return;
 	}
 	const uint8_t cls = k & 7;
-	if (cls == EBPF_CLS_JMP || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
+	if (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32 || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
 		return;
 	if (cls == EBPF_CLS_LDX) {
 		r[e.dst] = av();
@@ -409,7 +501,7 @@ dataflow(dprog_host &out)
 			r[i] = out.annot[id].in[i];
 		transfer(e, out, r);
 		uint32_t succ[2] = {e.next, UINT32_MAX};
-		if ((e.kind & 7) == EBPF_CLS_JMP && e.kind != DK_CALL_LOOKUP)
+		if (e.kind < 0x100 && ((e.kind & 7) == EBPF_CLS_JMP || (e.kind & 7) == DP_CLS_JMP32))
 			succ[1] = e.target;
 		for (uint32_t sx : succ) {
 			if (sx == UINT32_MAX || sx >= n)
@@ -436,6 +528,50 @@ dataflow(dprog_host &out)
 	}
 }
 
+// Any cycle in the entry graph (standard semantics only: the reference's state graph is a tree).
+bool
+has_cycle(const dprog_host &x)
+{
+	const size_t n = x.entries.size();
+	std::vector<uint8_t> color(n, 0); // 0 new, 1 on the stack, 2 done
+	std::vector<std::pair<uint32_t, int>> st;
+	auto succ = [&](uint32_t e, int k) -> uint32_t {
+		const dp_entry &d = x.entries[e];
+		if (d.kind == DK_FAULT || d.kind == EBPF_OP_EXIT)
+			return UINT32_MAX;
+		if (k == 0)
+			return d.next;
+		const uint8_t cls = d.kind & 7;
+		if (d.kind < 0x100 && (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32))
+			return d.target;
+		return UINT32_MAX;
+	};
+	for (uint32_t r = 0; r < n; r++) {
+		if (color[r])
+			continue;
+		st.push_back({r, 0});
+		color[r] = 1;
+		while (!st.empty()) {
+			auto &top = st.back();
+			if (top.second >= 2) {
+				color[top.first] = 2;
+				st.pop_back();
+				continue;
+			}
+			const uint32_t s = succ(top.first, top.second++);
+			if (s >= n)
+				continue;
+			if (color[s] == 1)
+				return true;
+			if (color[s] == 0) {
+				color[s] = 1;
+				st.push_back({s, 0});
+			}
+		}
+	}
+	return false;
+}
+
 } // namespace
 
 int
@@ -443,10 +579,17 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 {
 	const struct ebpf_inst *code = ep->prog;
 	uint64_t nslots = ep->prog_len / sizeof(struct ebpf_inst);
-	Translator t(code, nslots, ep->eo.eo_ee->ec, out);
+	const bool std_sem = ep->semantics.load() == EBPF_SEM_STANDARD;
+	Translator t(code, nslots, ep->eo.eo_ee->ec, out, std_sem);
 	int err = t.run();
 	if (err)
 		return err;
+	if (std_sem && has_cycle(out)) {
+		out.error = EOPNOTSUPP;
+		out.error_msg = "device batches run loop-free standard-eBPF programs only (the program "
+				"has a backward jump cycle; run it with ebpf_prog_run)";
+		return EOPNOTSUPP;
+	}
 
 	// Resolve LDDW immediates that are live maps of this env: the device map table.
 	struct ebpf_env *ee = ep->eo.eo_ee;

@@ -1,0 +1,82 @@
+"""Standard-eBPF semantics on the device (every variant, staged and general kernels) against the
+oracle's standard restatement: the hand-computed known answers, random loop-free programs with
+every ALU op / JMP32 / stack / packet access / array lookup, and one program at full size."""
+import numpy as np
+import pytest
+
+import pyoracle
+import stdprogs
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [0, 1, 2]
+
+
+def run_device(native, env, code, rel, specs, data, count, stride, variant, offsets=None):
+    maps = []
+    for vs, me, d in specs:
+        m = native.Map(env, me, vs)
+        m.fill(d)
+        maps.append(m)
+    p = native.Prog(env, native.patch_relocs(code, rel, [m.handle for m in maps]))
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        native.set_variant(variant)
+        d = np.ascontiguousarray(data.copy())
+        ret, faults, _ = p.run_batch(d, count, stride, offsets)
+        return ret, faults
+    finally:
+        native.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("stride", [64, 96])
+def test_known_answers_on_device(gpu, env, variant, stride):
+    bad = []
+    for name, items, want in stdprogs.KATS:
+        code, rel = stdprogs.asm(items)
+        pk = np.zeros((256, stride), dtype=np.uint8)
+        pk[:, :64] = np.frombuffer(stdprogs.PKT, dtype=np.uint8)
+        got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), 256, stride, variant)
+        if gf.any() or not (got == want).all():
+            bad.append((name, hex(int(got[0])), hex(want), int(gf[0])))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_random_programs_vs_oracle(gpu, env, variant):
+    bad = []
+    for seed in range(80):
+        g = np.random.default_rng(seed)
+        with_map = seed % 3 == 0
+        code, rel = stdprogs.gen_program(5000 + seed, length=20 + seed % 60, with_map=with_map)
+        specs = []
+        if with_map:
+            specs = [(8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
+        stride = 64 if seed % 2 == 0 else 72
+        n = 2048
+        pk = g.integers(0, 256, (n, stride), dtype=np.uint8)
+        want, wf, _, _ = pyoracle.OracleProgram(code, rel, specs, semantics=1).run(
+            pk.reshape(-1), n, stride)
+        got, gf = run_device(gpu, env, code, rel, specs, pk.reshape(-1), n, stride, variant)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad.append((seed, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_full_size_random_program(gpu, env, variant):
+    """16M packets tiled from 256k distinct: result i equals the oracle's for its distinct packet."""
+    code, rel = stdprogs.gen_program(777, length=60)
+    distinct, tiles = 1 << 18, 64
+    pk = np.random.default_rng(4).integers(0, 256, (distinct, 64), dtype=np.uint8)
+    want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(
+        pk.reshape(-1), distinct, 64, nthreads=8)
+    assert not wf.any()
+    got, gf = run_device(gpu, env, code, rel, [], np.tile(pk.reshape(-1), tiles), distinct * tiles,
+                         64, variant)
+    assert not gf.any()
+    np.testing.assert_array_equal(got.reshape(tiles, distinct), np.broadcast_to(want, (tiles, distinct)))

@@ -93,3 +93,36 @@ def test_random_programs_oracle_vs_cpu_path(native, env, seed):
         p.destroy()
         for m in maps:
             m.destroy()
+
+
+@pytest.mark.parametrize("seed", range(0, 60, 7))
+def test_device_translation_compiles(native, env, seed):
+    """Standard programs translate for the device and compile in both packet layouts."""
+    code, rel = stdprogs.gen_program(1000 + seed, length=30 + seed % 40)
+    p = native.Prog(env, code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        p.info()
+        for layout in (0, 1):
+            assert len(p.device_code(layout)) > 0
+    finally:
+        p.destroy()
+
+
+def test_device_rejects_loops_cpu_runs_them(native, env):
+    """A bounded loop (r0 = 0; r2 = 5; do r0 += r2 while --r2 != 0): 15 on the CPU path; the
+    device refuses programs with cycles (EOPNOTSUPP)."""
+    I = stdprogs.I
+    code, _ = stdprogs.asm([I("mov64_imm", 0, imm=0), I("mov64_imm", 2, imm=5), ("label", "L"),
+                            I("add64_reg", 0, 2), I("sub64_imm", 2, imm=1),
+                            I("jne_imm", 2, imm=0, off="L"), I("exit")])
+    p = native.Prog(env, code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        assert p.run_cpu(stdprogs.PKT)[0] == 15
+        i = native.DprogInfo()
+        import ctypes
+        assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert "loop-free" in native.last_error()
+    finally:
+        p.destroy()
