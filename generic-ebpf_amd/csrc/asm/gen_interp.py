@@ -50,6 +50,9 @@ RETK_STAGED = int(os.environ.get("EBPF_ASM_RETK", "8"))
 assert RETK_STAGED in (1, 2, 4, 8)
 
 
+STAGED_IMAGE = True   # set per generated image (generate())
+
+
 def set_retk(k):
     global RETK, V_RB, NVGPR
     RETK = k
@@ -86,6 +89,9 @@ NSGPR = 73           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per 
 S_JOIN = 74
 JOIN_LEVELS = 12
 NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
+# general image with the join SGPRs too (structured compiled programs in the general kernels;
+# 98 SGPRs allow 7 instead of 8 waves per SIMD there)
+GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -446,10 +452,34 @@ def h_ldx_pkt_staged(z, d):
 
 
 def h_ldx_pkt_const(z, d, off):
-    """Staged packet load at a translation-time byte offset: the bytes are already in
-    v22..v37, so this is 1-2 VALU (bit-field extract / byte align), no indexing."""
+    """Packet load at a translation-time byte offset from the packet bytes held in v22..v37,
+    so 1-2 VALU (bit-field extract / byte align), no indexing.  Staged kernels: every packet is
+    exactly 64 bytes.  General kernels (header staging, s7 bit 3): lanes whose packet is shorter
+    than off + z fault MEM, lanes shorter than 64 bytes (not staged) load from memory."""
     if off + z > 64:
         return []          # never selected: the lowering faults such loads statically
+    if not STAGED_IMAGE:
+        out = ["v_cmp_gt_u32_e64 %s, %d, v%d" % (sp(S_MASK), off + z, V_LEN),
+               "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+               "s_cbranch_scc0 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:"]
+        out += _pkc_extract(z, d, off)
+        ld = {1: "global_load_ubyte", 2: "global_load_ushort", 4: "global_load_dword",
+              8: "global_load_dwordx2"}[z]
+        out += ["v_cmp_gt_u32_e64 %s, 64, v%d" % (sp(S_MASK), V_LEN),
+                "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+                "s_cbranch_scc0 .Lst_{uid}",
+                "s_mov_b64 %s, exec" % sp(S_JUNK),
+                "s_mov_b64 exec, %s" % sp(S_MASK),
+                "%s %s, v[%d:%d], off offset:%d" % (ld, pair(d) if z == 8 else lo(d), V_PKT,
+                                                    V_PKT + 1, off),
+                "s_waitcnt vmcnt(0)"]
+        if z < 8:
+            out.append("v_mov_b32 %s, 0" % hi(d))
+        return out + ["s_mov_b64 exec, %s" % sp(S_JUNK), ".Lst_{uid}:"]
+    return _pkc_extract(z, d, off)
+
+
+def _pkc_extract(z, d, off):
     k, sh = off >> 2, off & 3
     lo_, hi_ = "v%d" % (PKT0 + k), "v%d" % (PKT0 + k + 1) if k + 1 < 16 else None
     D0, D1 = lo(d), hi(d)
@@ -1224,8 +1254,13 @@ def kernel(name, staged, jit=False):
           "v_lshlrev_b32 v%d, 4, %s" % (V_L16, v(H[0])),
           "s_mov_b32 %s, -1" % s(S_PREVG),
           "s_waitcnt lgkmcnt(0)",
-          "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0)),
-          "s_branch .Lprologue"]
+          "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0))]
+    if not staged:   # header staging requested by the host (dp_launch.lds_pkt_base bit 31)
+        L += ["s_bitcmp1_b32 %s, 31" % s(S_PKTLDS),
+              "s_cbranch_scc0 .L%s_nogs" % k,
+              "s_or_b32 s7, s7, 8",
+              ".L%s_nogs:" % k]
+    L += ["s_branch .Lprologue"]
     return L
 
 
@@ -1404,7 +1439,7 @@ def common_group_code():
           "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
                                                        v(H[1]), sp(S_DATA)),
           "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
-          "s_branch .Lgs_init",
+          "s_branch .Lgs_gstage",
           ".Lgs_offsets:",
           "v_mov_b32 %s, 8" % v(H[1]),
           "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[4]), sp(S_JUNK), H[3], v(H[1]), sp(S_OFFS)),
@@ -1416,6 +1451,20 @@ def common_group_code():
           "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
           "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
           "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
+          # general kernels with header staging: the first 64 bytes of every packet at least
+          # that long into v22..v37 (what the staged kernels' LDS DMA provides)
+          ".Lgs_gstage:",
+          "s_bitcmp1_b32 s7, 3",
+          "s_cbranch_scc0 .Lgs_init",
+          "v_cmp_lt_u32_e64 vcc, 63, v%d" % V_LEN,
+          "s_and_b64 exec, %s, vcc" % sp(S_ALIVE),
+          "s_cbranch_execz .Lgs_gs_done"] + [
+          "global_load_dwordx4 v[%d:%d], v[%d:%d], off offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
+                                                                     V_PKT, V_PKT + 1, 16 * q)
+          for q in range(4)] + [
+          "s_waitcnt vmcnt(0)",
+          ".Lgs_gs_done:",
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
           ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
@@ -1638,6 +1687,8 @@ def main():
 
 
 def generate(out_s, staged_image):
+    global STAGED_IMAGE
+    STAGED_IMAGE = staged_image
     A = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950:xnack-"', ".amdhsa_code_object_version 5", ".text"]
     A += kernel("ebpf_interp_s64", True) + kernel("ebpf_interp_gen", False)
     A += kernel("ebpf_jit_s64", True, True) + kernel("ebpf_jit_gen", False, True)
@@ -1701,6 +1752,7 @@ def generate(out_s, staged_image):
     header.append("#define AH_JIT_AREA_BYTES %d" % JIT_AREA_BYTES)
     header.append("#define AH_S_JOIN %d  // structured programs: taken-lane masks s[74:75]..  (staged image)" % S_JOIN)
     header.append("#define AH_JOIN_LEVELS %d" % JOIN_LEVELS)
+    header.append("#define AH_GEN_JOIN %d  // the general image holds the join SGPRs too" % GEN_JOIN)
     header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
@@ -1711,7 +1763,7 @@ def generate(out_s, staged_image):
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
     kernarg = 112
-    nsg = NSGPR_STAGED if staged_image else NSGPR
+    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_jit_s64", kernarg, 0, NVGPR, nsg, 256),

@@ -1364,6 +1364,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = em.bswap(fam, d);
 				break;
 			case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: {
+				if (mode == 0) { // general kernels: the handler's length checks (copied)
+					ok = false;
+					break;
+				}
 				const int z = 1 << (fam - AHF_LDXPKC1);
 				int swap = 0;
 				const uint32_t nx = xl.entries[e].next;
@@ -1447,7 +1451,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			if (!final_pass) {
 				uses[e] = em.used;
 				defreg[e] = (int8_t)wr;
-				pure[e] = (char)(pure_fam(fam, spec_map) && wr >= 0);
+				pure[e] = (char)(pure_fam(fam, spec_map) && wr >= 0 &&
+						 !(mode == 0 && fam >= AHF_LDXPKC1 && fam <= AHF_LDXPKC8));
 			} else if (!(off & 1) && pure[e] && wr >= 0 && !(live_out[e] & (1u << wr))) {
 				// dead: no code, the register's VGPRs do not hold the (unused) value
 				blk.fast = true;

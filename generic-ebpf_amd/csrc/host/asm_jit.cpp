@@ -225,7 +225,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<uint32_t> cont(n, GROUP_END); // where a path through the entry continues
 	std::vector<int> jdepth(n, 0);            // pending branches (join masks in use)
 	std::vector<int> join_of(n, -1);          // entry e is the taken block of conditional k
-	bool structured = mode == 1 && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
+	bool structured = (mode == 1 || AH_GEN_JOIN) && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
 			  getenv("EBPF_JIT_NOCC") == nullptr;
 	for (uint32_t e : order) {
 		const uint32_t h = (uint32_t)low[e].handler;

@@ -20,6 +20,7 @@ hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device,
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
+bool asm_program_gstage(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 // asm_jit.cpp
@@ -155,8 +156,10 @@ ensure_translated(struct ebpf_prog *ep)
 	int err = translate_program(ep, *x);
 	if (err && x->error == 0)
 		x->error = err;
-	if (!x->error)
+	if (!x->error) {
 		x->asm_needs_general = asm_program_needs_general(*x);
+		x->asm_gstage = asm_program_gstage(*x);
+	}
 	ep->xlated = std::move(x);
 	if (ep->xlated->error)
 		return fail(ep->xlated->error, ep->xlated->error_msg);
@@ -333,6 +336,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.prog = dp->d_asm[mode];
 			L.stack_stride = dp->asm_stride[mode];
 		}
+		L.lds_pkt_base = (mode == 0 && ep->xlated->asm_gstage) ? 0x80000000u : 0;
 		rows_slot *rows = nullptr;
 		if (L.hist) {
 			if ((err = rows_acquire(dp->device,

@@ -142,6 +142,7 @@ struct dprog_host {
 	std::vector<struct ebpf_map *> maps; // referenced array maps, in dp_map table order
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
+	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
 	uint32_t max_stack = 0;
 	int error = 0;
 	std::string error_msg;

@@ -191,3 +191,35 @@ def test_empty_and_ragged_batches(gpu, env, variant):
             np.testing.assert_array_equal(want, got)
         else:
             assert got.size == 0
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_general_kernels_header_staging(gpu, env, variant):
+    """General kernels stage the first 64 bytes of each packet for constant-offset loads: ragged
+    packets of 1..140 bytes (CSR offsets) and a 40-byte stride, so some lanes are unstaged
+    (shorter than 64 B) and some loads run past the packet (MEM faults).  C3 and random
+    programs against the oracle."""
+    from generic_ebpf_amd import randprog, workloads
+    g = np.random.default_rng(31)
+    progs = [(workloads.prog_c3(), [])]
+    for k in range(30):
+        vs = 8
+        lay = randprog.random_program(70000 + k, length=int(g.integers(10, 60)), nmaps=1,
+                                      map_value_size=vs)
+        progs.append((lay, [(vs, 16, g.integers(0, 256, vs * 16, dtype=np.uint8).tobytes())]))
+    n = 3000
+    lens = g.integers(1, 141, n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    base = workloads.packets_l2l3(n, 160)
+    data = np.concatenate([base[i, :lens[i]] for i in range(n)])
+    bad = []
+    for i, (lay, maps) in enumerate(progs):
+        for stride, o in ((0, offs), (40, None)):
+            d = data if o is not None else base[:, :40].reshape(-1).copy()
+            c = goldens.Case("gs%d" % i, lay.code, lay.relocs, maps, d, n, stride, o)
+            want, wf, wd, _ = oracle_run(c)
+            got, gf, gd = device_run(gpu, env, c, variant)
+            if not (np.array_equal(want, got) and np.array_equal(wf, gf) and np.array_equal(wd, gd)):
+                bad.append((i, stride, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
+    assert not bad, bad
