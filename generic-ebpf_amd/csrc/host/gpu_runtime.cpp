@@ -186,27 +186,30 @@ ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 int
 sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 {
+	const uint16_t cpu = map_current_cpu();
 	for (struct ebpf_map *em : ep->xlated->maps) {
 		std::lock_guard<std::mutex> g(em->mirror_lock);
 		map_mirror &m = em->mirrors[device];
 		uint64_t v = em->version.load();
-		if (m.version != v) {
+		const uint16_t c = em->percpu ? cpu : 0;
+		if (m.version != v || m.cpu != c) {
 			hipError_t e;
 			if (em->is_hashtable()) {
 				// a fresh snapshot of the table; the staging copy must outlive the transfer
-				map_device_image(em, m.image);
+				map_device_image(em, m.image, c);
 				e = hipMemcpyAsync(m.dev, m.image.data(), m.image.size(), hipMemcpyHostToDevice,
 						   stream);
 				if (e == hipSuccess)
 					e = hipStreamSynchronize(stream);
 			} else {
-				e = hipMemcpyAsync(m.dev, em->array_storage(),
+				e = hipMemcpyAsync(m.dev, map_array_image(em, c),
 						   (size_t)em->value_size * em->max_entries,
 						   hipMemcpyHostToDevice, stream);
 			}
 			if (e != hipSuccess)
 				return hip_fail(e, "hipMemcpyAsync(map mirror)");
 			m.version = v;
+			m.cpu = c;
 		}
 	}
 	return 0;

@@ -47,20 +47,28 @@ struct ebpf_obj {
 struct map_mirror {
 	void *dev = nullptr;
 	uint64_t version = ~0ull; // host version last uploaded
+	uint16_t cpu = 0;         // percpu maps: the CPU whose copy was uploaded
 	std::vector<uint8_t> image; // hashtable: host staging copy of the device table
 };
 
-// The device mirror of a map (maps.cpp).  Array maps mirror their value array; non-percpu
-// hashtables mirror a read-only open-addressing table (dprog.h dp_map).  `bytes == 0` means the
-// map type has no device form (percpu maps, hashtable keys over DP_HASH_MAX_KEY).
+// The device mirror of a map (maps.cpp).  Array maps mirror their value array, hashtables a
+// read-only open-addressing table (dprog.h dp_map).  Percpu maps mirror the copy of the CPU the
+// batch is submitted from: a device batch behaves like the caller's own loop over
+// ebpf_prog_run on its current CPU.  `bytes == 0` means no device form (hashtable keys over
+// DP_HASH_MAX_KEY).
 struct map_device_layout {
 	size_t bytes = 0;
 	uint32_t slots = 0; // dp_map.max_entries
 	uint32_t flags = 0; // dp_map.flags
 };
 map_device_layout map_device_layout_of(const struct ebpf_map *em);
-// Hashtable: fill `out` (layout.bytes) with the current table, under the map's lock.
-void map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out);
+// Hashtable: fill `out` (layout.bytes) with the current table (percpu: `cpu`'s values), under
+// the map's lock.
+void map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out, uint16_t cpu);
+// Array / percpu array: the value array to mirror (percpu: `cpu`'s copy).
+const uint8_t *map_array_image(struct ebpf_map *em, uint16_t cpu);
+// The CPU the calling thread runs on, as the percpu maps index it (ebpf_linux_user.c:83-112).
+uint16_t map_current_cpu();
 
 struct ebpf_map {
 	struct ebpf_obj eo; // must stay first (callers cast to struct ebpf_obj *)
@@ -76,7 +84,7 @@ struct ebpf_map {
 	std::vector<map_mirror> mirrors;  // indexed by device
 	// array-map storage (for device mirroring); null for other map types
 	uint8_t *array_storage() const;
-	bool is_hashtable() const;
+	bool is_hashtable() const; // hashtable or percpu hashtable
 };
 
 // Assembly-interpreter LDS layout (per workgroup): verdict histogram [0, kHistLds), LDS-resident

@@ -178,7 +178,8 @@ percpu_lookup(struct ebpf_map *em, void *key)
 	uint32_t k = *static_cast<uint32_t *>(key);
 	if (k >= em->max_entries)
 		return nullptr;
-	return static_cast<array_priv *>(em->data)[curcpu()].array + (uint64_t)em->value_size * k;
+	mark_dirty(em); // the caller may write through the pointer
+	return static_cast<array_priv *>(em->data)[curcpu() % ncpus()].array + (uint64_t)em->value_size * k;
 }
 
 int
@@ -201,8 +202,9 @@ percpu_update(struct ebpf_map *em, void *key, void *value, uint64_t flags)
 	if (error != 0)
 		return error;
 	uint32_t k = *static_cast<uint32_t *>(key);
-	memcpy(static_cast<array_priv *>(em->data)[curcpu()].array + (uint64_t)em->value_size * k,
+	memcpy(static_cast<array_priv *>(em->data)[curcpu() % ncpus()].array + (uint64_t)em->value_size * k,
 	       value, em->value_size);
+	mark_dirty(em);
 	return 0;
 }
 
@@ -216,6 +218,7 @@ percpu_update_from_user(struct ebpf_map *em, void *key, void *value, uint64_t fl
 	array_priv *ma = static_cast<array_priv *>(em->data);
 	for (uint16_t i = 0; i < ncpus(); i++)
 		memcpy(ma[i].array + (uint64_t)em->value_size * k, value, em->value_size);
+	mark_dirty(em);
 	return 0;
 }
 
@@ -514,19 +517,35 @@ ebpf_map::array_storage() const
 bool
 ebpf_map::is_hashtable() const
 {
-	return emt == &emt_hashtable;
+	return emt == &emt_hashtable || emt == &emt_percpu_hashtable;
+}
+
+uint16_t
+map_current_cpu()
+{
+	return (uint16_t)(curcpu() % ncpus());
+}
+
+const uint8_t *
+map_array_image(struct ebpf_map *em, uint16_t cpu)
+{
+	if (em->emt == &emt_array)
+		return static_cast<array_priv *>(em->data)->array;
+	if (em->emt == &emt_percpu_array)
+		return static_cast<array_priv *>(em->data)[cpu % ncpus()].array;
+	return nullptr;
 }
 
 map_device_layout
 map_device_layout_of(const struct ebpf_map *em)
 {
 	map_device_layout l;
-	if (em->emt == &emt_array) {
+	if (em->emt == &emt_array || em->emt == &emt_percpu_array) {
 		l.bytes = (size_t)em->value_size * em->max_entries;
 		l.slots = em->max_entries;
 		return l;
 	}
-	if (em->emt != &emt_hashtable || em->key_size == 0 || em->key_size > DP_HASH_MAX_KEY)
+	if (!em->is_hashtable() || em->key_size == 0 || em->key_size > DP_HASH_MAX_KEY)
 		return l;
 	uint64_t need = dp_hash_value_off(em->key_size) + (uint64_t)em->value_size, stride = 16;
 	uint32_t lg = 4;
@@ -548,7 +567,7 @@ map_device_layout_of(const struct ebpf_map *em)
 }
 
 void
-map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out)
+map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out, uint16_t cpu)
 {
 	const map_device_layout l = map_device_layout_of(em);
 	hash_priv *h = static_cast<hash_priv *>(em->data);
@@ -567,7 +586,7 @@ map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out)
 			memcpy(slot, &used, 4);
 			memcpy(slot + 4, &hv, 4);
 			memcpy(slot + 8, h->key(e), em->key_size);
-			memcpy(slot + voff, h->val(e), em->value_size);
+			memcpy(slot + voff, h->val(e, h->percpu ? cpu % h->ncpu : 0), em->value_size);
 		}
 }
 

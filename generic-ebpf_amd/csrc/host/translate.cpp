@@ -597,8 +597,8 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	const struct ebpf_map *unsupported = nullptr;
 	auto add_map = [&](struct ebpf_map *m) {
 		if (map_device_layout_of(m).bytes == 0) {
-			// device batches resolve array and hashtable maps; a program that loads any
-			// other live map (percpu) runs on the CPU path only (ebpf_prog_run)
+			// device batches resolve array and hashtable maps (percpu ones included); a
+			// map with no device form runs on the CPU path only (ebpf_prog_run)
 			unsupported = m;
 			return;
 		}
@@ -625,9 +625,9 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 			add_map(ep->dep_maps[i]);
 	if (unsupported != nullptr) {
 		out.error = EOPNOTSUPP;
-		out.error_msg = std::string("device batches support array and hashtable maps only; the "
-					    "program uses a ") +
-				unsupported->emt->name + " map (run it with ebpf_prog_run)";
+		out.error_msg = std::string("the program uses a ") + unsupported->emt->name +
+				" map with no device form (hashtable keys over 256 bytes; run it with "
+				"ebpf_prog_run)";
 		out.maps.clear(); // (not pinned: nothing to release)
 		return EOPNOTSUPP;
 	}

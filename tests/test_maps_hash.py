@@ -273,14 +273,15 @@ def test_prog_run_with_hashtable_lookup(native, env, typ):
 
 def test_device_translation_of_hashtable_programs(native, env):
     """Hashtable lookups with a statically known map translate for the device (both code
-    layouts compile); percpu hashtables and lookups whose map is only known at run time do not
-    (EOPNOTSUPP, the program still runs through ebpf_prog_run)."""
+    layouts compile), percpu hashtables included; keys longer than 256 bytes and lookups whose
+    map is only known at run time do not (EOPNOTSUPP, the program still runs through
+    ebpf_prog_run)."""
     from generic_ebpf_amd import isa
     from generic_ebpf_amd.layout import Branch, LdDw, MapRef, assemble
     I = isa.Insn
     ht = HMap(native, env, HT, 4, 8, 64)
     pht = HMap(native, env, PHT, 4, 8, 64)
-    progs = []
+    progs, extra = [], []
     try:
         lay = _lookup_prog(native)
         p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [ht.ptr.value]))
@@ -292,8 +293,13 @@ def test_device_translation_of_hashtable_programs(native, env):
             assert len(p.device_code(layout)) > 0
         p2 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [pht.ptr.value]))
         progs.append(p2)
-        assert native.lib().ebpf_prog_device_info(p2.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
-        assert "percpu_hashtable" in native.last_error()
+        assert native.lib().ebpf_prog_device_info(p2.ptr, ctypes.byref(i)) == 0   # percpu: the caller's CPU copy
+        big = HMap(native, env, HT, 300, 8, 4)      # keys too long for the device table
+        extra.append(big)
+        p4 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [big.ptr.value]))
+        progs.append(p4)
+        assert native.lib().ebpf_prog_device_info(p4.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert "no device form" in native.last_error()
         # r1 = the hashtable's handle plus a packet byte: not resolvable at translation time
         nodes = [I("ldxw", 6, 1, 0), I("stxw", 10, 6, -4), I("ldxb", 7, 1, 4), LdDw(1, MapRef(0)),
                  I("add64_reg", 1, 7), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
@@ -308,6 +314,8 @@ def test_device_translation_of_hashtable_programs(native, env):
             p.destroy()
         ht.destroy()
         pht.destroy()
+        for m in extra:
+            m.destroy()
 
 
 # ---- the oracle's hashtable lookups against the CPU path (ebpf_prog_run over the host table) ----
