@@ -92,6 +92,9 @@ NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
 # general image with the join SGPRs too (structured compiled programs in the general kernels;
 # 98 SGPRs allow 7 instead of 8 waves per SIMD there)
 GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
+# general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
+# hoist plan); 16 cost the general kernels 8 -> 6 waves per SIMD
+GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -1675,13 +1678,17 @@ def main():
     header = None
     for out_s, k, staged in ((out_s1, RETK_STAGED, True), (out_s0, 1, False)):
         set_retk(k)
+        if not staged:
+            global NVGPR
+            NVGPR += GEN_HOIST_REGS
         h = generate(out_s, staged)
         header = header or h
         assert h[:-2] == header[:-2]   # identical but for the RETK-dependent lines
     header = header[:-2] + ["#define AH_RET_GROUPS_STAGED %d  // groups per result burst, staged kernels"
                             % RETK_STAGED,
                             "#define AH_NVGPR_STAGED %d" % (64 if RETK_STAGED == 1 else 64 + 2 * RETK_STAGED),
-                            "#define AH_RET_GROUPS_GENERAL 1", "#define AH_NVGPR_GENERAL 64"]
+                            "#define AH_RET_GROUPS_GENERAL 1",
+                            "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS)]
     with open(out_h, "w") as f:
         f.write("\n".join(header) + "\n")
 
@@ -1753,6 +1760,8 @@ def generate(out_s, staged_image):
     header.append("#define AH_S_JOIN %d  // structured programs: taken-lane masks s[74:75]..  (staged image)" % S_JOIN)
     header.append("#define AH_JOIN_LEVELS %d" % JOIN_LEVELS)
     header.append("#define AH_GEN_JOIN %d  // the general image holds the join SGPRs too" % GEN_JOIN)
+    header.append("#define AH_GEN_HOIST_BASE 64  // general image: spare VGPRs for hoisted loads")
+    header.append("#define AH_GEN_HOIST_REGS %d" % GEN_HOIST_REGS)
     header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()

@@ -19,6 +19,7 @@ struct cc_block {
 	uint32_t sval[6] = {};
 	std::vector<uint8_t> body;
 	std::vector<uint8_t> prologue;
+	std::vector<uint8_t> hoist; // general kernels: packet loads issued ahead for this straight run
 	int8_t sdir = -1; // conditional decided at compile time: 0 never taken, 1 always taken
 };
 

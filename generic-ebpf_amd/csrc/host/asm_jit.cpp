@@ -356,7 +356,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() + pre_len(e);
+		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() + (uint32_t)cb[e].hoist.size() +
+			      pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
 			sz += (uint32_t)cb[e].body.size();
@@ -496,6 +497,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		if (!cb[e].prologue.empty()) {
 			memcpy(&img[area + at], cb[e].prologue.data(), cb[e].prologue.size());
 			at += cb[e].prologue.size();
+		}
+		if (!cb[e].hoist.empty()) {
+			memcpy(&img[area + at], cb[e].hoist.data(), cb[e].hoist.size());
+			at += cb[e].hoist.size();
 		}
 		for (int r = 0; r < 6; r++) {
 			if (!(pre_mask[e] & (1u << r)))

@@ -68,6 +68,8 @@ def main():
             handles = [maps["c4"].handle]
         if opt == "nocc":
             os.environ["EBPF_JIT_NOCC"] = "1"
+        if opt == "nohoist":
+            os.environ["EBPF_CC_NOHOIST"] = "1"
         if opt.startswith("salu") or opt.startswith("valu"):   # issue-port probes
             os.environ["EBPF_CC_PAD_" + opt[:4].upper()] = opt[4:]
         p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, handles))
@@ -87,6 +89,7 @@ def main():
                             stream.cuda_stream)
         torch.cuda.synchronize()
         os.environ.pop("EBPF_JIT_NOCC", None)
+        os.environ.pop("EBPF_CC_NOHOIST", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
         cands.append((nm, p, data, path))
