@@ -1666,7 +1666,7 @@ def jit_templates():
         ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
         ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", ".Lr_exit", ".Lr_fault",
-        ".Lgroup_done", "ebpf_jit_area"]
+        ".Lr_hlookup", ".Lgroup_done", "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
     return L

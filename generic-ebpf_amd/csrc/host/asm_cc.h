@@ -28,6 +28,7 @@ struct cc_routines {
 	uint32_t exit_k; // EXIT with r0 known (v[44:45], s57 = verdict bin set by the caller)
 	uint32_t exit;   // EXIT (r0 in v[0:1])
 	uint32_t fault;  // fault the lanes s[48:49] with code s52
+	uint32_t hlookup; // HLOOKUP: r0 = hashtable lookup (record offset s14, key at r2)
 };
 
 // low: the lowered entries (asm_lower); order: the layout order (depth-first, parents first);

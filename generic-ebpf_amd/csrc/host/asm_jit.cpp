@@ -33,7 +33,7 @@ enum jt_index {
 	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
-	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_GDONE, JT_AREA,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE, JT_AREA,
 	JT_AREA_BYTES,
 	JT_COUNT
 };
@@ -271,7 +271,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<cc_block> cb;
 	if (getenv("EBPF_JIT_NOCC") == nullptr)
 		cc_compile(xl, low, order, entry_point, mode, structured,
-			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT]}, table, cb);
+			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, cb);
 	else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
 		cc_prologue(mode, 0x7ff, true, false, cb[xl.start].prologue);

@@ -164,3 +164,33 @@ def test_c4h_full_size(gpu, env, variant):
         gpu.set_variant(0)
         p.destroy()
         m.destroy()
+
+
+def test_hash_cases_specialised_lookup(gpu, env, monkeypatch):
+    """The code generator's inline hashtable probe (opt-in, EBPF_CC_HSPEC=1) on every case with
+    a key of at most 8 bytes in the frame, and the C4H program, against the oracle."""
+    monkeypatch.setenv("EBPF_CC_HSPEC", "1")
+    bad = []
+    for k in range(len(HCASES)):
+        rng = np.random.default_rng(900 + k)
+        lay, specs, pk = hcase(k, rng, n=4096, size=64)
+        want, wf, _ = hashprogs.oracle(lay, specs, pk.reshape(-1), len(pk), 64)
+        got, gf = run_device(gpu, env, lay, specs, pk.reshape(-1), len(pk), 64, variant=0)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad.append(k)
+    assert not bad, bad
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4h()
+    universe, keys, values = workloads.c4h_table(entries=1 << 16)
+    pk = workloads.packets_c4h(1 << 18, universe)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [pyoracle.HashSpec(4, 8, keys=keys, values=values)])
+    want, wf, _, _ = op.run(pk.reshape(-1), len(pk), 64, None, nthreads=8)
+    m = gpu.HashMap(env, 4, 8, len(keys))
+    m.fill(keys, values)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle]))
+    try:
+        got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), len(pk), 64)
+        assert not gf.any() and np.array_equal(want, got)
+    finally:
+        p.destroy()
+        m.destroy()

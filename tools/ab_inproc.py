@@ -60,6 +60,15 @@ def main():
         cfg, _, opt = spec.partition(":")
         lay = workloads.CONFIGS[cfg]["prog"]()
         handles = []
+        if cfg == "c4h":
+            if "c4h" not in maps:
+                universe, hk, hv = workloads.c4h_table()
+                hm = native.HashMap(env, 4, 8, len(hk))
+                hm.fill(hk, hv)
+                maps["c4h"] = hm
+                maps["c4h_pk"] = torch.from_numpy(
+                    workloads.packets_c4h(1 << 22, universe).reshape(-1)).to(dev).repeat(max(1, n >> 22))
+            handles = [maps["c4h"].handle]
         if cfg == "c4":
             if "c4" not in maps:
                 m = native.Map(env, 256, 8)
@@ -70,11 +79,15 @@ def main():
             os.environ["EBPF_JIT_NOCC"] = "1"
         if opt == "nohoist":
             os.environ["EBPF_CC_NOHOIST"] = "1"
+        if opt.startswith("off"):
+            os.environ["EBPF_CC_OFF"] = opt[3:]
         if opt.startswith("salu") or opt.startswith("valu"):   # issue-port probes
             os.environ["EBPF_CC_PAD_" + opt[:4].upper()] = opt[4:]
         p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, handles))
         p.prepare(0)
         data = d_rnd if cfg in ("c0", "c2") else d_l2
+        if cfg == "c4h":
+            data = maps["c4h_pk"]
         if opt == "l2":      # the same program over the other packet buffer (placement check)
             data = d_l2
         elif opt == "rnd":
@@ -90,6 +103,7 @@ def main():
         torch.cuda.synchronize()
         os.environ.pop("EBPF_JIT_NOCC", None)
         os.environ.pop("EBPF_CC_NOHOIST", None)
+        os.environ.pop("EBPF_CC_OFF", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
         cands.append((nm, p, data, path))
