@@ -27,6 +27,12 @@ NREG = 11
 _NT = int(os.environ.get("EBPF_ASM_NT", "3"))
 ST_POLICY = " nt" if _NT & 1 else ""
 LD_POLICY = " nt" if _NT & 2 else ""
+# explicit cache-policy strings (A/B probes of the gfx950 sc0/sc1/nt bits), "+"-separated,
+# e.g. EBPF_ASM_LDPOL=sc1+nt ("none" = no bits)
+for _v, _n in (("EBPF_ASM_STPOL", "ST_POLICY"), ("EBPF_ASM_LDPOL", "LD_POLICY")):
+    if os.environ.get(_v):
+        _p = os.environ[_v].replace("+", " ")
+        globals()[_n] = "" if _p == "none" else " " + _p
 # ---------------------------------------------------------------- register plan
 PKT0 = 22            # v22..v37 staged packet dwords (staged kernel)
 V_PKT = 38           # v[38:39] packet base address
@@ -934,16 +940,9 @@ def routines():
           "v_mov_b32 v%d, s13" % V_T,
           "s_andn2_b64 exec, %s, %s" % (sp(S_SAVE), sp(S_MASK))] + dispatch(12)
     # EXIT: value r0 into V_RET (the group's results are stored together, see group code).
+    # (the fault byte of every lane is zeroed when its group starts, and the LDS histogram is
+    # kept whether or not the launch asked for one, so an exit does neither check)
     L += [".Lr_exit:"] + ret_slot_write("v0", "v1") + [
-          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
-          "s_cbranch_scc1 .Lex_nofault",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
-          "v_mov_b32 %s, 0" % v(R[8]),
-          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
-          ".Lex_nofault:",
-          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
-          "s_cbranch_scc1 .Lex_nohist",
           "v_mov_b32 %s, 255" % v(R[8]),
           "v_mov_b32 %s, 0" % v(R[9]),
           "v_cmp_lt_u64_e64 vcc, v[0:1], %s" % vp(R[8]),
@@ -954,6 +953,9 @@ def routines():
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_MASK), s(S_BYTES), v(R[8])),
           "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
           "s_cbranch_scc0 .Lex_lanes",
+          # EXIT with r0 known at compile time (compiled programs): v[44:45] = r0 and S_BYTES =
+          # its verdict bin are set by the caller, so the verdict needs no per-lane work
+          ".Lr_exit_k:",
           ".Lex_uniform:",
           "s_bcnt1_i32_b64 %s, exec" % s(S_CODE),
           "s_lshl_b32 %s, %s, 2" % (s(S_BYTES), s(S_BYTES)),
@@ -975,19 +977,6 @@ def routines():
           "s_cbranch_scc0 .Lex_sched",
           "s_setpc_b64 %s" % sp(S_LINK),
           ".Lex_sched:"] + goto(".Lr_schedule")
-    # EXIT with r0 known at compile time (compiled programs): v[44:45] = r0 and S_BYTES = its
-    # verdict bin are set by the caller, so the verdict needs no per-lane work
-    L += [".Lr_exit_k:",
-          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
-          "s_cbranch_scc1 .Lexk_nofault",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
-          "v_mov_b32 %s, 0" % v(R[8]),
-          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
-          ".Lexk_nofault:",
-          "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
-          "s_cbranch_scc1 .Lex_nohist",
-          "s_branch .Lex_uniform"]
     # FAULT: lanes s[mask], code s[S_CODE]; returns via s[link] unless no lane remains
     L += [".Lr_fault:",
           "s_mov_b64 %s, exec" % sp(S_SAVE),
@@ -1471,6 +1460,14 @@ def common_group_code():
           ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          # fault code 0 for the whole group up front (a faulting lane overwrites its byte)
+          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
+          "s_cbranch_scc1 .Lgs_nofz",
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
+          "v_mov_b32 %s, 0" % v(R[8]),
+          "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
+          ".Lgs_nofz:",
           # a compiled program (s7 bit 1) starts at the head of its code area and sets up the
           # registers it reads itself (packet address, r1, r10, zeroes: asm_cc.cpp prologue)
           "s_bitcmp1_b32 s7, 1",

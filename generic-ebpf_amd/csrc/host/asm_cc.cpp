@@ -1068,11 +1068,23 @@ struct emitter {
 	{
 		mov32(V_RES, (uint32_t)r0);
 		mov32(V_RES + 1, (uint32_t)(r0 >> 32));
-		E.sop1(0x00, S_BYTES, k32(r0 < 255 ? (uint32_t)r0 : 255u));   // s_mov_b32
 		if (call) {
-			call_routine(exitk_off, 0);
+			// structured programs: the verdict count inline (.Lr_exit_k's work): one LDS add
+			// of popcount(exec) to bin min(r0, 255); the exiting lanes leave the alive mask
+			const int S_CODE = 52, S_SAVE = 18, S_ALIVE = 16, R8 = 60, R9 = 61;
+			const uint32_t bin = r0 < 255 ? (uint32_t)r0 : 255u;
+			E.sop1(0x0d, S_CODE, opnd{SRC_EXEC});                         // s_bcnt1_i32_b64
+			E.sop1(0x01, S_SAVE, opnd{SRC_EXEC});                         // s_mov_b64
+			E.sop1(0x01, 126, opnd{128 + 1});                              // exec = lane 0
+			E.vop1(V1_MOV_B32, R8, opnd{(uint32_t)S_CODE});
+			E.vop1(V1_MOV_B32, R9, k32(bin * 4));
+			E.ds(0x00, R9, R8, 0, 0, 0);                                   // ds_add_u32
+			E.sop1(0x01, 126, opnd{(uint32_t)S_SAVE});
+			E.sop2(0x13, S_ALIVE, opnd{(uint32_t)S_ALIVE}, opnd{SRC_EXEC}); // s_andn2_b64
+			(void)exitk_off;
 			return;
 		}
+		E.sop1(0x00, S_BYTES, k32(r0 < 255 ? (uint32_t)r0 : 255u));   // s_mov_b32
 		E.sop2(0x00, S_JUNK, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, exitk_off}); // s_add_u32
 		E.sop2(0x04, S_JUNK + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});     // s_addc_u32
 		E.sop1(0x1d, 0, opnd{(uint32_t)S_JUNK});                           // s_setpc_b64
