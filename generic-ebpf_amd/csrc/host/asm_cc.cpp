@@ -1071,16 +1071,16 @@ struct emitter {
 		if (call) {
 			// structured programs: the verdict count inline (.Lr_exit_k's work): one LDS add
 			// of popcount(exec) to bin min(r0, 255); the exiting lanes leave the alive mask
-			const int S_CODE = 52, S_SAVE = 18, S_ALIVE = 16, R8 = 60, R9 = 61;
+			// (lane 0's V_L16 = 0 addresses the bin through the instruction offset; the alive
+			// mask is not read again before the group ends in a structured program)
+			const int S_CODE = 52, S_SAVE = 18, R8 = 60, V_L16 = 43;
 			const uint32_t bin = r0 < 255 ? (uint32_t)r0 : 255u;
 			E.sop1(0x0d, S_CODE, opnd{SRC_EXEC});                         // s_bcnt1_i32_b64
 			E.sop1(0x01, S_SAVE, opnd{SRC_EXEC});                         // s_mov_b64
 			E.sop1(0x01, 126, opnd{128 + 1});                              // exec = lane 0
 			E.vop1(V1_MOV_B32, R8, opnd{(uint32_t)S_CODE});
-			E.vop1(V1_MOV_B32, R9, k32(bin * 4));
-			E.ds(0x00, R9, R8, 0, 0, 0);                                   // ds_add_u32
+			E.ds(0x00, V_L16, R8, 0, 0, (bin * 4) & 0xff, (bin * 4) >> 8);  // ds_add_u32
 			E.sop1(0x01, 126, opnd{(uint32_t)S_SAVE});
-			E.sop2(0x13, S_ALIVE, opnd{(uint32_t)S_ALIVE}, opnd{SRC_EXEC}); // s_andn2_b64
 			(void)exitk_off;
 			return;
 		}
