@@ -563,9 +563,12 @@ struct emitter {
 	}
 
 	// ---- ALU32 (lo op= k; hi = 0)
-	bool alu32i(int fam, int d, uint32_t k)
+	// src >= 0: the operand is u32(r[src]) instead of r[d] (a 32-bit MOV d = src fused into
+	// this operation by the caller)
+	bool alu32i(int fam, int d, uint32_t k, int src = -1)
 	{
-		const rf x = f.r[d];
+		const int sr = src >= 0 ? src : d;
+		const rf x = f.r[sr];
 		const uint32_t a = (uint32_t)x.v;
 		const int ab = std::min(32, bits_of(x));
 		if (x.c || fam == AHF_A32I_MOV) {
@@ -586,50 +589,53 @@ struct emitter {
 			return true;
 		}
 		int nb = 32;
+		const size_t at = blk.body.size();
 		switch (fam) {
 		case AHF_A32I_ADD:
 			if (k)
-				E.vop2(V2_ADD_U32, L(d), k32(k), L(d));
+				E.vop2(V2_ADD_U32, L(d), k32(k), L(sr));
 			nb = k ? std::min(32, std::max(ab, 32 - __builtin_clz(k)) + 1) : ab;
 			break;
 		case AHF_A32I_SUB:
 			if (k)
-				E.vop2(V2_SUBREV_U32, L(d), k32(k), L(d));
+				E.vop2(V2_SUBREV_U32, L(d), k32(k), L(sr));
 			nb = k ? 32 : ab;
 			break;
 		case AHF_A32I_MUL:
-			E.vop3(V3_MUL_LO_U32, L(d), VGPR0 + L(d), c3(k), 0);
+			E.vop3(V3_MUL_LO_U32, L(d), VGPR0 + L(sr), c3(k), 0);
 			nb = k ? std::min(32, ab + 32 - __builtin_clz(k)) : 0;
 			break;
 		case AHF_A32I_OR:
 			if (k)
-				E.vop2(V2_OR, L(d), k32(k), L(d));
+				E.vop2(V2_OR, L(d), k32(k), L(sr));
 			nb = std::max(ab, k ? 32 - __builtin_clz(k) : 0);
 			break;
 		case AHF_A32I_AND:
 			if (k != 0xffffffffu)
-				E.vop2(V2_AND, L(d), k32(k), L(d));
+				E.vop2(V2_AND, L(d), k32(k), L(sr));
 			nb = std::min(ab, k ? 32 - __builtin_clz(k) : 0);
 			break;
 		case AHF_A32I_XOR:
 			if (k)
-				E.vop2(V2_XOR, L(d), k32(k), L(d));
+				E.vop2(V2_XOR, L(d), k32(k), L(sr));
 			nb = std::max(ab, k ? 32 - __builtin_clz(k) : 0);
 			break;
 		case AHF_A32I_LSH:
 			if (k & 31)
-				E.vop2(V2_LSHLREV_B32, L(d), opnd{128 + (k & 31)}, L(d));
+				E.vop2(V2_LSHLREV_B32, L(d), opnd{128 + (k & 31)}, L(sr));
 			nb = std::min(32, ab + (int)(k & 31));
 			break;
 		case AHF_A32I_RSH:
 			if (k & 31)
-				E.vop2(V2_LSHRREV_B32, L(d), opnd{128 + (k & 31)}, L(d));
+				E.vop2(V2_LSHRREV_B32, L(d), opnd{128 + (k & 31)}, L(sr));
 			nb = std::max(0, ab - (int)(k & 31));
 			break;
 		default:
 			return false;
 		}
-		use(d);
+		if (sr != d && blk.body.size() == at) // (an identity operation: the fused copy alone)
+			E.vop1(V1_MOV_B32, L(d), vreg(L(sr)));
+		use(sr);
 		hi0(d);
 		f.def(d, kbits(nb));
 		return true;
@@ -1550,6 +1556,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			have[xl.start] = 1;
 		}
 		std::vector<char> fused(n, 0); // a BSWAP folded into the preceding packet load
+		std::vector<int8_t> movfuse_src(n, -1);  // this entry reads a fused MOV's source
+		std::vector<int16_t> movfuse_fam(n, -1); // ... as this 32-bit operation
 		for (size_t k = 0; k < order.size(); k++) {
 			const uint32_t e = order[k];
 			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u);
@@ -1568,6 +1576,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			const facts before = f;
 			emitter em(blk, f, maps);
 			em.off = off;
+			bool break_mov = false;
 			// issue packet load x into its ring slot, for the lanes whose packet holds it
 			auto issue = [&](enc &Hq, uint32_t x) {
 				const int S_JUNK_ = 60, V_LEN = 40, V_PKT = 38;
@@ -1587,13 +1596,42 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					issue(Hq, x);
 			}
 			bool ok = true, spec_map = false;
-			if (hoist_tmp[e] >= 0) {
+			// a 32-bit MOV d = s whose only successor operates on d with an immediate: the
+			// successor reads s directly and the MOV emits nothing (one VALU move saved)
+			if (fam == AHF_A32R_MOV && d != s && d < AH_NREGS && s < AH_NREGS && !(off & 1)) {
+				const uint32_t nx = xl.entries[e].next;
+				if (nx < n && k + 1 < order.size() && order[k + 1] == nx && !entry_point[nx] &&
+				    npred[nx] == 1 && hoist_tmp[nx] < 0) {
+					const uint32_t h2 = (uint32_t)low[nx].handler;
+					const int f2 = ah_fam[h2];
+					const uint32_t K2 = (uint32_t)low[nx].imm;
+					int as32 = -1;
+					if (ah_dst[h2] == d && f2 >= AHF_A32I_ADD && f2 <= AHF_A32I_RSH && f2 != AHF_A32I_MUL)
+						as32 = f2; // (ADD, SUB, OR, AND, XOR, LSH, RSH: see alu32i)
+					else if (ah_dst[h2] == d && f2 == AHF_A64I_RSH && K2 < 32)
+						as32 = AHF_A32I_RSH; // (u32 >> c)
+					else if (ah_dst[h2] == d && f2 == AHF_A64I_LSH && K2 < 32 &&
+						 std::min(32, bits_of(f.r[s])) + (int)K2 <= 32)
+						as32 = AHF_A32I_LSH; // (the result still fits 32 bits)
+					if (as32 >= 0 && as32 != AHF_A32I_MUL && as32 != AHF_A32I_MOV) {
+						movfuse_src[nx] = (int8_t)s;
+						movfuse_fam[nx] = (int16_t)as32;
+						em.use(s);
+						break_mov = true;
+					}
+				}
+			}
+			if (break_mov) {
+				// (nothing emitted; d keeps its old facts until the fused operation defines it)
+			} else if (movfuse_src[e] >= 0) {
+				ok = em.alu32i(movfuse_fam[e], d, (uint32_t)K, movfuse_src[e]);
+			} else if (hoist_tmp[e] >= 0) {
 				em.ldx_hoisted(d, 1 << (fam - AHF_LDXPKTG1), (uint32_t)K, hoist_tmp[e], hoist_later[e],
 					       rt.fault);
 				if (hoist_next[e] != UINT32_MAX)
 					issue(em.E, hoist_next[e]);
 			}
-			switch (hoist_tmp[e] >= 0 ? -1 : fam) {
+			switch ((hoist_tmp[e] >= 0 || break_mov || movfuse_src[e] >= 0) ? -1 : fam) {
 			case -1: break;
 			case AHF_NOP: break;
 			case AHF_EXIT:
