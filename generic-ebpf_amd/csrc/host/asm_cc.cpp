@@ -1095,6 +1095,27 @@ struct emitter {
 		E.sop2(0x04, S_JUNK + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});     // s_addc_u32
 		E.sop1(0x1d, 0, opnd{(uint32_t)S_JUNK});                           // s_setpc_b64
 	}
+	// EXIT with r0 in registers (structured programs), inline: r0 into the result slot and one
+	// LDS histogram add per lane at bin min(r0, 255) (what .Lr_exit does, without the call,
+	// the return and the uniform-verdict test)
+	void exit_inline()
+	{
+		const int R8 = 60, R9 = 61;
+		use(0);
+		E.vop1(V1_MOV_B32, V_RES, vreg(0));
+		E.vop1(V1_MOV_B32, V_RES + 1, vreg(1));
+		int bin = 0; // v0 holds the bin if r0 < 256
+		if (f.r[0].lz < 56) {
+			E.vop1(V1_MOV_B32, R8, k32(255));
+			E.vop1(V1_MOV_B32, R9, opnd{128});
+			E.vopc(VC_U64 + P_LT, vreg(0), R8);            // vcc = r0 < 255
+			E.vop2(0x00, R8, vreg(R8), 0);                 // v_cndmask_b32 v60, v60, v0, vcc
+			bin = R8;
+		}
+		E.vop2(V2_LSHLREV_B32, R8, opnd{128 + 2}, bin);
+		E.vop1(V1_MOV_B32, R9, opnd{128 + 1});
+		E.ds(0x00, R8, R9, 0, 0, 0);                        // ds_add_u32
+	}
 	// call a routine that returns (structured programs): the link pair s[50:51]
 	void call_routine(uint32_t off, uint16_t reads)
 	{
@@ -1637,6 +1658,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			case AHF_EXIT:
 				if (f.r[0].c && !(off & 32))
 					em.exit_known(f.r[0].v, rt.exit_k, structured);
+				else if (structured && getenv("EBPF_CC_EXITCALL") == nullptr)
+					em.exit_inline();
 				else if (structured)
 					em.call_routine(rt.exit, 1);
 				else
