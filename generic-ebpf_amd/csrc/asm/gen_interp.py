@@ -706,6 +706,38 @@ def _rot(d, x, k):
     return ["v_alignbit_b32 %s, %s, %s, %d" % (d, x, x, 32 - k)]
 
 
+def dma_next_full(tmp, save):
+    """LDS DMA of this wave's next group (a full one) into its packet buffer, as the group
+    set-up issues it; sets s7 bit 5.  Clobbers s[64:65], `tmp`, the SGPR pair `save`, m0."""
+    return ["s_or_b32 s7, s7, 32"] + next_group(tmp) + [
+            "s_lshr_b32 s65, %s, 20" % s(tmp),
+            "s_lshl_b32 s64, %s, 12" % s(tmp),
+            "s_add_u32 s64, s64, %s" % s(S_DATA),
+            "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
+            "s_mov_b64 %s, exec" % sp(save),
+            "s_mov_b64 exec, -1",
+            "s_mov_b32 m0, %s" % s(S_PKTLDS),
+            "s_nop 0"] + [
+            "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
+            for qq in range(4)] + [
+            "s_mov_b64 exec, %s" % sp(save)]
+
+
+def probe_wait(tag):
+    """Wait for the hashtable probe load just issued.  When the group set-up deferred the next
+    group's DMA (s7 bits 5:4 = 01), issue it now, behind the probe, and wait for the probe
+    alone (vmcnt(4): loads retire in issue order), so the probe's latency no longer includes
+    the 4-KB DMA's.  Uses s[64:65], s68 (not read by the probe loops), S_JUNK, m0."""
+    return ["s_and_b32 s68, s7, 48",
+            "s_cmp_eq_u32 s68, 16",
+            "s_cbranch_scc0 .L%s_w0" % tag] + dma_next_full(68, S_JUNK) + [
+            "s_waitcnt vmcnt(4)",
+            "s_branch .L%s_wd" % tag,
+            ".L%s_w0:" % tag,
+            "s_waitcnt vmcnt(0)",
+            ".L%s_wd:" % tag]
+
+
 def hlookup_routine():
     """HLOOKUP (called): r0 = hashtable_map_lookup_elem(map, r2) for the map whose dp_map record
     is at byte offset s14 of the map table (ebpf_map.c:77-84 -> ebpf_map_hashtable.c:285-301).
@@ -787,8 +819,7 @@ def hlookup_routine():
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
           "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
-          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa),
-          "s_waitcnt vmcnt(0)",
+          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa)] + probe_wait("hq") + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),           # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[7]), c),
@@ -813,8 +844,7 @@ def hlookup_routine():
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
           "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
-          "global_load_dwordx2 %s, %s, off" % (hd, sa),
-          "s_waitcnt vmcnt(0)",
+          "global_load_dwordx2 %s, %s, off" % (hd, sa)] + probe_wait("hp") + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),          # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "s_and_b64 exec, exec, %s" % sp(S_OK),
@@ -1192,6 +1222,12 @@ def routines():
           "s_setpc_b64 %s" % sp(S_JUNK)] + [
           ".Llk_sched:"] + goto(".Lr_schedule")
     L += hlookup_routine()
+    # DMA_NEXT (staged kernel, deferred mode s7 bit 4): issue the LDS DMA of this wave's next
+    # group now, once per group (sets bit 5).  The group set-up defers only a full next group,
+    # so this is always the 4-instruction full-group DMA.  Preserves exec, S_T*, s[66:71];
+    # clobbers s[64:65], S_CODE, S_SAVE, m0.
+    L += [".Lr_dma_next:"] + dma_next_full(S_CODE, S_SAVE) + [
+          "s_setpc_b64 %s" % sp(S_LINK)]
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
     # past the batch end masked off.  Clobbers s[64:68], m0, exec.
@@ -1376,7 +1412,11 @@ def common_group_code():
           "s_cbranch_scc0 .Lgroup_check",
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
-    L += [".Lgroup_done:"] + slot_commit() + next_group(S_T0) + [
+    L += [".Lgroup_done:",
+          "s_and_b32 %s, s7, 48" % s(S_BYTES),
+          "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
+          "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
+          ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
@@ -1397,10 +1437,18 @@ def common_group_code():
     # next group's DMA: a full group (the common case) inline, with exec = all lanes and the
     # instruction offset stepping both the global and the LDS address (M0 set once); a partial
     # group through the masking routine
-    L += ["s_waitcnt lgkmcnt(0)"] + next_group(S_T0) + [
+    # (s7 bit 4: a program that probes memory issues this DMA itself right after its first
+    # probe, so the two latencies overlap — see .Lr_dma_next; bit 5: issued for this group)
+    L += ["s_waitcnt lgkmcnt(0)",
+          "s_or_b32 s7, s7, 32"] + next_group(S_T0) + [
           "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),        # full groups
           "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
           "s_cbranch_scc0 .Lgs_pf_slow",
+          "s_bitcmp1_b32 s7, 4",                                   # deferred: left to .Lr_dma_next
+          "s_cbranch_scc0 .Lgs_pf_now",
+          "s_and_b32 s7, s7, ~32",
+          "s_branch .Lgs_pf_done",
+          ".Lgs_pf_now:",
           "s_lshr_b32 s65, %s, 20" % s(S_T0),
           "s_lshl_b32 s64, %s, 12" % s(S_T0),
           "s_add_u32 s64, s64, %s" % s(S_DATA),

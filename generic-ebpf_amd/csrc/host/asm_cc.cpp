@@ -1836,8 +1836,23 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN))
 					needs_pkt = true;
 			}
-			if (xl.start < n)
+			if (xl.start < n) {
 				cc_prologue(mode, live_start, needs_pkt, structured, out[xl.start].prologue);
+				// staged kernel, hashtable probes through the routine: the group set-up
+				// can leave the next group's packet DMA to the first probe (s7 bit 4,
+				// gen_interp.py probe_wait), so a probe does not also wait for the DMA.
+				// Opt-in (EBPF_CC_DEFER_DMA=1): measured 2.2% slower on C4H, the probe's own
+				// latency (a random line out of a 128-MB table) dominates, not the DMA's
+				const char *dd = getenv("EBPF_CC_DEFER_DMA");
+				bool probes = false;
+				for (uint32_t e : order)
+					if (ah_fam[(uint32_t)low[e].handler] == AHF_HLOOKUP && !out[e].fast)
+						probes = true;
+				if (mode == 1 && probes && dd && atoi(dd) != 0) {
+					enc P{out[xl.start].prologue};
+					P.sop2(0x0e, 7, opnd{7}, opnd{128 + 16}); // s_or_b32 s7, s7, 16
+				}
+			}
 			break;
 		}
 		// liveness (backward over the tree: children come after their parent in `order`)

@@ -166,10 +166,12 @@ def test_c4h_full_size(gpu, env, variant):
         m.destroy()
 
 
-def test_hash_cases_specialised_lookup(gpu, env, monkeypatch):
-    """The code generator's inline hashtable probe (opt-in, EBPF_CC_HSPEC=1) on every case with
-    a key of at most 8 bytes in the frame, and the C4H program, against the oracle."""
-    monkeypatch.setenv("EBPF_CC_HSPEC", "1")
+@pytest.mark.parametrize("knob", ["EBPF_CC_HSPEC", "EBPF_CC_DEFER_DMA"])
+def test_hash_cases_specialised_lookup(gpu, env, monkeypatch, knob):
+    """The code generator's opt-in hashtable paths against the oracle, on every case with a key
+    of at most 8 bytes in the frame and on the C4H program: the inline probe (EBPF_CC_HSPEC=1)
+    and the next group's packet DMA issued behind the first probe (EBPF_CC_DEFER_DMA=1)."""
+    monkeypatch.setenv(knob, "1")
     bad = []
     for k in range(len(HCASES)):
         rng = np.random.default_rng(900 + k)

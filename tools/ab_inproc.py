@@ -79,6 +79,8 @@ def main():
             os.environ["EBPF_JIT_NOCC"] = "1"
         if opt == "nohoist":
             os.environ["EBPF_CC_NOHOIST"] = "1"
+        if opt == "defer":
+            os.environ["EBPF_CC_DEFER_DMA"] = "1"
         if opt.startswith("off"):
             os.environ["EBPF_CC_OFF"] = opt[3:]
         if opt.startswith("salu") or opt.startswith("valu"):   # issue-port probes
@@ -104,6 +106,7 @@ def main():
         os.environ.pop("EBPF_JIT_NOCC", None)
         os.environ.pop("EBPF_CC_NOHOIST", None)
         os.environ.pop("EBPF_CC_OFF", None)
+        os.environ.pop("EBPF_CC_DEFER_DMA", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
         cands.append((nm, p, data, path))
