@@ -88,8 +88,11 @@ S_JUNK = 60          # s[60:61] scratch sdst
 S_OK = 62            # s[62:63] check: accumulated ok lanes
 S_REC = 64           # s[64:71] map record {handle, dev_base, value_size, max_entries, lds_off, pad}
 S_PREVG = 72         # group whose results are still in V_RET (-1: none)
+S_KMASK = 73         # superblock size - 1 of this launch (K' <= RETK, a power of two; host-chosen,
+                     # dp_launch.total_waves bits 28..29 = log2 K'): small batches use shorter
+                     # superblocks so that every wave gets work
 S_WAVE = 3
-NSGPR = 73           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per SIMD
+NSGPR = 74           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per SIMD
 # staged image: s[74:75] .. s[96:97] hold the taken-lane masks of a structured compiled program's
 # pending branches (asm_jit.cpp; 12 levels); 98 SGPRs still allow the image's 6 waves per SIMD
 S_JOIN = 74
@@ -1306,7 +1309,7 @@ def slot_commit():
     if RETK == 1:
         return []
     return ["s_mov_b64 exec, -1",
-            "s_and_b32 %s, %s, %d" % (s(S_BYTES), s(S_GROUP), RETK - 1),
+            "s_and_b32 %s, %s, %s" % (s(S_BYTES), s(S_GROUP), s(S_KMASK)),
             "s_lshl_b32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
             "s_set_gpr_idx_on %s, gpr_idx(DST)" % s(S_BYTES),
             "v_mov_b32 v%d, v%d" % (V_RB, V_RES),
@@ -1322,19 +1325,21 @@ def store_prev_results(tag, final):
     L = ["s_cmp_eq_u32 %s, -1" % s(S_PREVG),
          "s_cbranch_scc1 .Lsp_none_%s" % tag]
     if not final and RETK > 1:
-        L += ["s_and_b32 %s, %s, %d" % (s(S_T0), s(S_PREVG), RETK - 1),
-              "s_cmp_lg_u32 %s, %d" % (s(S_T0), RETK - 1),
+        L += ["s_and_b32 %s, %s, %s" % (s(S_T0), s(S_PREVG), s(S_KMASK)),
+              "s_cmp_lg_u32 %s, %s" % (s(S_T0), s(S_KMASK)),
               "s_cbranch_scc1 .Lsp_none_%s" % tag]
     # R0 = byte offset of the superblock's first packet result for this lane; R1 = its index
     # (all lanes: the current group's live mask says nothing about the stored groups)
     L += ["s_mov_b64 exec, -1",
-          "s_andn2_b32 %s, %s, %d" % (s(S_T0), s(S_PREVG), RETK - 1),
+          "s_andn2_b32 %s, %s, %s" % (s(S_T0), s(S_PREVG), s(S_KMASK)),
           "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),
           "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[1]), s(S_T0), v(R[1])),
           "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(R[1]))]
     for k in range(RETK):
         if k:
-            L.append("v_add_u32 %s, 64, %s" % (v(R[1]), v(R[1])))
+            L += ["s_cmp_lt_u32 %s, %d" % (s(S_KMASK), k),        # past this launch's K'
+                  "s_cbranch_scc1 .Lsp_none_%s" % tag,
+                  "v_add_u32 %s, 64, %s" % (v(R[1]), v(R[1]))]
         L += ["v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_COUNT), v(R[1])),
               "s_mov_b64 exec, vcc",
               "global_store_dwordx2 %s, v[%d:%d], %s offset:%d%s" % (
@@ -1346,8 +1351,8 @@ def store_prev_results(tag, final):
 def next_group(dst):
     """dst = the group after S_GROUP in this wave's sequence (superblocks of RETK groups;
     S_GSTRIDE holds the jump to the next superblock's first group)."""
-    return ["s_and_b32 %s, %s, %d" % (s(dst), s(S_GROUP), RETK - 1),
-            "s_cmp_eq_u32 %s, %d" % (s(dst), RETK - 1),
+    return ["s_and_b32 %s, %s, %s" % (s(dst), s(S_GROUP), s(S_KMASK)),
+            "s_cmp_eq_u32 %s, %s" % (s(dst), s(S_KMASK)),
             "s_cselect_b32 %s, %s, 1" % (s(dst), s(S_GSTRIDE)),
             "s_add_u32 %s, %s, %s" % (s(dst), s(dst), s(S_GROUP))]
 
@@ -1401,10 +1406,15 @@ def common_group_code():
           "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
           "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
           "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
-          "s_mul_i32 %s, %s, %d" % (s(S_GROUP), s(S_GROUP), RETK),
-          # superblock jump: (total waves - 1) * RETK + 1
-          "s_mul_i32 %s, %s, %d" % (s(S_GSTRIDE), s(S_GSTRIDE), RETK),
-          "s_sub_u32 %s, %s, %d" % (s(S_GSTRIDE), s(S_GSTRIDE), RETK - 1),
+          # K' = superblock size of this launch (total_waves bits 28..29 = log2 K')
+          "s_lshr_b32 %s, %s, 28" % (s(S_T1), s(S_GSTRIDE)),
+          "s_and_b32 %s, %s, 0xffff" % (s(S_GSTRIDE), s(S_GSTRIDE)),
+          "s_lshl_b32 %s, 1, %s" % (s(S_KMASK), s(S_T1)),
+          "s_sub_u32 %s, %s, 1" % (s(S_KMASK), s(S_KMASK)),
+          "s_lshl_b32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_T1)),
+          # superblock jump: (total waves - 1) * K' + 1
+          "s_lshl_b32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_T1)),
+          "s_sub_u32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_KMASK)),
           # this wave's packet buffer (staged kernel); first group's prefetch
           "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
           "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),

@@ -98,7 +98,8 @@ struct dp_launch {
 	// assembly interpreter only:
 	uint32_t stack_stride;    // LDS bytes per lane stack slice (S' in asm_runtime.cpp)
 	uint32_t lds_stack_base;  // LDS byte offset of the first stack slice (after the histogram)
-	uint32_t total_waves;     // persistent grid: waves in the launch (group stride)
+	uint32_t total_waves;     // persistent grid: waves in the launch (group stride); bits
+	                          // 28..29: log2 of the superblock size (staged kernels)
 	uint32_t lds_pkt_base;    // staged kernel: LDS byte offset of the per-wave packet buffers
 	uint32_t *hist_rows;      // assembly kernels: per-workgroup u32[256] verdict counts (bins
 	                          // 0..255), summed into hist by ebpf_hist_reduce; NULL = atomics

@@ -16,7 +16,7 @@
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
-			     uint32_t map_lds_bytes, void *fn);
+			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
@@ -347,7 +347,13 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 				return fail(err, "no histogram row buffer");
 			L.hist_rows = static_cast<uint32_t *>(rows->p);
 		}
-		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn);
+		// a program that probes hashtables is bound by their latency and wants every wave;
+		// the others stream packets (asm_runtime.cpp, occupancy)
+		bool probes = false;
+		for (const dp_map &m : dp->table)
+			probes = probes || (m.flags & DP_MAP_HASH) != 0;
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
+				      (mode == 1 && !probes) ? 4u : 0u);
 		if (rows)
 			rows_release(rows, stream, e == hipSuccess);
 	} else {

@@ -193,6 +193,23 @@ def test_empty_and_ragged_batches(gpu, env, variant):
             assert got.size == 0
 
 
+@pytest.mark.parametrize("superblock", [1, 2, 4, 8])
+def test_superblock_sizes(gpu, env, superblock, monkeypatch):
+    """Staged kernels walk superblocks of K' groups whose results go out as one burst; the host
+    picks K' per launch (small batches: shorter superblocks).  Every K' on ragged batches that
+    end inside a superblock and inside a group, with the histogram."""
+    from generic_ebpf_amd import workloads
+    monkeypatch.setenv("EBPF_SUPERBLOCK", str(superblock))
+    lay = workloads.prog_c3()
+    for n in (1, 64 * 5 + 3, 64 * 6144 * superblock + 64 * 3 + 17):
+        pk = workloads.packets_l2l3(n, 64)
+        c = goldens.Case("c3", lay.code, [], [], pk.reshape(-1), n, 64, None)
+        got, gf, _ = device_run(gpu, env, c, 0)
+        want, wf, _, _ = oracle_run(c, nthreads=8)
+        np.testing.assert_array_equal(want, got)
+        np.testing.assert_array_equal(wf, gf)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_general_kernels_header_staging(gpu, env, variant):
     """General kernels stage the first 64 bytes of each packet for constant-offset loads: ragged

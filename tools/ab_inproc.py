@@ -27,9 +27,9 @@ def main():
     dev = torch.device("cuda", 0)
     n = int(os.environ.get("AB_PACKETS", 1 << 26))
     pk = workloads.packets_l2l3(1 << 22, 64, seed=3)
-    d_l2 = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(max(1, n >> 22))
+    d_l2 = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(-(-n >> 22))
     rnd = workloads.packets_random(1 << 22, 64, seed=2)
-    d_rnd = torch.from_numpy(rnd.reshape(-1)).to(dev).repeat(max(1, n >> 22))
+    d_rnd = torch.from_numpy(rnd.reshape(-1)).to(dev).repeat(-(-n >> 22))
     d_ret = torch.empty(n, dtype=torch.int64, device=dev)
     n5 = min(n, 1 << 22)
     imix, imix_offs, _ = workloads.packets_imix(n5, seed=5)
@@ -67,7 +67,7 @@ def main():
                 hm.fill(hk, hv)
                 maps["c4h"] = hm
                 maps["c4h_pk"] = torch.from_numpy(
-                    workloads.packets_c4h(1 << 22, universe).reshape(-1)).to(dev).repeat(max(1, n >> 22))
+                    workloads.packets_c4h(1 << 22, universe).reshape(-1)).to(dev).repeat(-(-n >> 22))
             handles = [maps["c4h"].handle]
         if cfg == "c4":
             if "c4" not in maps:
@@ -109,11 +109,21 @@ def main():
         os.environ.pop("EBPF_CC_DEFER_DMA", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
-        cands.append((nm, p, data, path))
+        launch_env = {}
+        if opt.startswith("wg"):   # workgroups per CU cap at launch (occupancy / tail probe)
+            launch_env["EBPF_WG_PER_CU"] = opt[2:]
+        if opt.startswith("sb"):   # superblock size at launch
+            launch_env["EBPF_SUPERBLOCK"] = opt[2:]
+        cands.append((nm, p, data, path, launch_env))
     times = {nm: [] for nm in names}
 
-    def launch(p, data, path):
+    def launch(p, data, path, launch_env):
         select(path)
+        for k in ("EBPF_WG_PER_CU", "EBPF_SUPERBLOCK"):
+            if k in launch_env:
+                os.environ[k] = launch_env[k]
+            else:
+                os.environ.pop(k, None)
         if data is d_imix:
             p.run_batch_dev(0, data.data_ptr(), n5, 0, d_ret.data_ptr(), d_imix_offs.data_ptr(), None,
                             d_hist.data_ptr(), stream.cuda_stream)
@@ -121,16 +131,16 @@ def main():
         p.run_batch_dev(0, data.data_ptr(), n, 64, d_ret.data_ptr(), None, None, d_hist.data_ptr(),
                         stream.cuda_stream)
 
-    for nm, p, data, path in cands:  # warm
+    for nm, p, data, path, le in cands:  # warm
         for _ in range(3):
-            launch(p, data, path)
+            launch(p, data, path, le)
     torch.cuda.synchronize()
     for r in range(rounds):
-        for nm, p, data, path in cands:
+        for nm, p, data, path, le in cands:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
             for _ in range(launches):
-                launch(p, data, path)
+                launch(p, data, path, le)
             b.record(stream)
             torch.cuda.synchronize()
             times[nm].append(a.elapsed_time(b) / launches)
