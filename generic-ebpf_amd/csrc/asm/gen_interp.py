@@ -822,7 +822,11 @@ def hlookup_routine():
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
           "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
-          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa)] + probe_wait("hq") + [
+          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa),
+          # the slot's first 8 value bytes (value offset 16 for keys of <= 8 bytes), same line:
+          # lanes that meet their key here keep them in v[50:51] for the code generator's
+          # forwarded value loads (asm_cc.cpp AHF_LDXHV)
+          "global_load_dwordx2 %s, %s, off offset:16" % (vp(H[4]), sa)] + probe_wait("hq") + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),           # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[7]), c),

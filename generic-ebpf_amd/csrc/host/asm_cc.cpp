@@ -177,6 +177,8 @@ struct rf {
 	bool nz = false;  // known non-zero (a lookup that cannot fail)
 	int8_t mp = -1;   // >= 0: a pointer to map mp's value number u32(r[mreg]) (+0)
 	int8_t mreg = -1;
+	int8_t hfwd = -1; // >= 0: a hashtable lookup result whose value's first 8 bytes register
+	                  // hfwd's VGPRs hold (loaded with the probe, see AHF_HLOOKUP)
 };
 
 inline int
@@ -232,11 +234,14 @@ struct facts {
 			if (st[i].reg != d)
 				st[k++] = st[i];
 		nst = k;
-		for (int q = 0; q < AH_NREGS; q++)
+		for (int q = 0; q < AH_NREGS; q++) {
 			if (q != d && r[q].mreg == d) {
 				r[q].mp = -1;
 				r[q].mreg = -1;
 			}
+			if (r[q].hfwd == d)
+				r[q].hfwd = -1;
+		}
 	}
 	void store(uint32_t off, int size, int reg)
 	{
@@ -1040,6 +1045,30 @@ struct emitter {
 		f.t2zero = false;
 		return true;
 	}
+	// LDXHV through a non-NULL hashtable lookup result whose value's first 8 bytes were
+	// loaded with the probe into register D's VGPRs: an extract, no memory access
+	bool ldxhv_fwd(int z, int d, int s, int32_t o)
+	{
+		const rf xs = f.r[s];
+		if (xs.hfwd < 0 || !xs.nz || o < 0 || o + z > 8 || (o % z) != 0)
+			return false;
+		const int D = xs.hfwd;
+		use(s);
+		use(D);
+		if (z == 8) {
+			if (d != D)
+				E.vop1(V1_MOV_B64, L(d), vreg(L(D)));
+		} else if (z == 4) {
+			E.vop1(V1_MOV_B32, L(d), vreg(L(D) + o / 4));
+		} else {
+			E.vop3(V3_BFE_U32, L(d), VGPR0 + L(D) + (uint32_t)(o / 4), 128 + 8 * (uint32_t)(o % 4),
+			       128 + 8 * (uint32_t)z);
+		}
+		if (z < 8)
+			mov32(Hi(d), 0);
+		f.def(d, z == 8 ? rf() : kbits(8 * z));
+		return true;
+	}
 	// LDXMAP through a pointer with known map and index register: the LDS copy, no check
 	bool ldxmap(int z, int d, int s, uint64_t imm)
 	{
@@ -1740,8 +1769,34 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				     (table[mi].flags & DP_MAP_HASH) &&
 				     em.hlookup_stk(mi, aux0, aux1 - 1, (int)dp_hash_key_size(table[mi].flags),
 						    table[mi].flags, rt.hlookup);
+				// the generic routine, whose probe of a key of <= 8 bytes also loads the
+				// slot's first 8 value bytes (v[50:51], gen_interp.py hlookup_routine): they
+				// are kept in a register D dead from here on, so that loads through the
+				// result (LDXHV) become register extracts (one memory round trip less)
+				if (!ok && final_pass && mi < (int)table.size() && (table[mi].flags & DP_MAP_HASH) &&
+				    dp_hash_key_size(table[mi].flags) <= 8 && getenv("EBPF_CC_NOHFWD") == nullptr) {
+					int D = -1;
+					for (int r = 9; r >= 2 && D < 0; r--)
+						if (!(live_out[e] & (1u << r)))
+							D = r;
+					if (D >= 0) {
+						blk.reads |= (uint8_t)(1u << 4); // s14 = the map record offset
+						blk.sval[4] = aux0;
+						em.use(2);
+						em.call_routine(rt.hlookup, 0);
+						em.E.vop1(V1_MOV_B64, 2 * D, vreg(50));
+						f.def(0, rf());
+						f.def(D, rf());
+						f.r[0].hfwd = (int8_t)D;
+						f.t2zero = false;
+						ok = true;
+					}
+				}
 				break;
 			}
+			case AHF_LDXHV1: case AHF_LDXHV2: case AHF_LDXHV4: case AHF_LDXHV8:
+				ok = em.ldxhv_fwd(1 << (fam - AHF_LDXHV1), d, s, (int32_t)aux0);
+				break;
 			default:
 				if (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD)
 					ok = em.alu32i(fam, d, (uint32_t)K);

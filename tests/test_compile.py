@@ -174,3 +174,33 @@ def test_optimised_code_is_smaller(native, env):
                     assert opt <= 0.8 * base, (opt, base)
     finally:
         m.destroy()
+
+
+def test_hash_value_loads_forwarded(native, env):
+    """C4H: the hashtable probe routine also loads the slot's first value bytes; the code
+    generator keeps them in a dead register so the load through the non-NULL lookup result is a
+    register move (EBPF_CC_NOHFWD=1 turns it off: one more global load)."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4h()
+    m = native.HashMap(env, 4, 8, 64)
+    try:
+        code = native.patch_relocs(lay.code, lay.relocs, [m.handle])
+        p = native.Prog(env, code)
+        dc = p.device_code(1)
+        p.destroy()
+        os.environ["EBPF_CC_NOHFWD"] = "1"
+        try:
+            p = native.Prog(env, code)
+            dc_off = p.device_code(1)
+            p.destroy()
+        finally:
+            os.environ.pop("EBPF_CC_NOHFWD", None)
+        assert dc != dc_off
+        if os.path.exists(LLVM_MC):
+            out, err = _decode(dc)
+            out_off, _ = _decode(dc_off)
+            assert "invalid" not in err.lower()
+            loads = lambda s: sum(1 for ln in s.splitlines() if "global_load" in ln)
+            assert loads(out) == loads(out_off) - 1
+    finally:
+        m.destroy()

@@ -79,6 +79,8 @@ def main():
             os.environ["EBPF_JIT_NOCC"] = "1"
         if opt == "nohoist":
             os.environ["EBPF_CC_NOHOIST"] = "1"
+        if opt == "nohfwd":
+            os.environ["EBPF_CC_NOHFWD"] = "1"
         if opt == "defer":
             os.environ["EBPF_CC_DEFER_DMA"] = "1"
         if opt.startswith("off"):
@@ -107,6 +109,7 @@ def main():
         os.environ.pop("EBPF_CC_NOHOIST", None)
         os.environ.pop("EBPF_CC_OFF", None)
         os.environ.pop("EBPF_CC_DEFER_DMA", None)
+        os.environ.pop("EBPF_CC_NOHFWD", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
         launch_env = {}
