@@ -127,7 +127,7 @@ void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int c
 	       LDNT, MAP, wpc, ms, npk / ms / 1e6, npk * (ST == 2 ? 64.0 : 72.0) / ms / 1e6);
 }
 
-int main() {
+int main(int argc, char **argv) {
 	const uint64_t npk = 1ull << 26;
 	const uint32_t ngroups = npk / 64;
 	uint8_t *in;
@@ -136,6 +136,23 @@ int main() {
 	(void)hipMalloc(&out, npk * 8);
 	(void)hipMemset(in, 1, npk * 64);
 	const int cus = 256;
+	if (argc > 1 && argv[1][0] == 'o') {
+		// occupancy x prefetch depth, with a little per-group work (the staged kernel at 4
+		// workgroups per CU, round 1)
+		for (int rep = 0; rep < 2; rep++) {
+			run<1, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 16);
+			run<2, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 16);
+			run<3, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 12);
+			run<2, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 12);
+			run<1, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 20);
+			run<2, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 20);
+			run<1, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 24);
+			run<1, 8, 2, 1, 0, 16>(in, out, ngroups, npk, cus, 16);
+			run<2, 8, 2, 1, 0, 16>(in, out, ngroups, npk, cus, 16);
+		}
+		return 0;
+	}
 	run<1, 8, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 24);
 	run<1, 8, 0, 1, 0, 16>(in, out, ngroups, npk, cus, 24);
 	run<1, 8, 0, 1, 0, 32>(in, out, ngroups, npk, cus, 24);
