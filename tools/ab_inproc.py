@@ -61,14 +61,17 @@ def main():
         lay = workloads.CONFIGS[cfg]["prog"]()
         handles = []
         if cfg == "c4h":
-            if "c4h" not in maps:
-                universe, hk, hv = workloads.c4h_table()
+            # ":eNN" = a table of 2^NN entries instead of the bench's 1M (footprint probe)
+            ent = 1 << int(opt[1:]) if opt.startswith("e") else workloads.C4H_ENTRIES
+            key = "c4h%d" % ent
+            if key not in maps:
+                universe, hk, hv = workloads.c4h_table(entries=ent)
                 hm = native.HashMap(env, 4, 8, len(hk))
                 hm.fill(hk, hv)
-                maps["c4h"] = hm
-                maps["c4h_pk"] = torch.from_numpy(
+                maps[key] = hm
+                maps[key + "_pk"] = torch.from_numpy(
                     workloads.packets_c4h(1 << 22, universe).reshape(-1)).to(dev).repeat(-(-n >> 22))
-            handles = [maps["c4h"].handle]
+            handles = [maps[key].handle]
         if cfg == "c4":
             if "c4" not in maps:
                 m = native.Map(env, 256, 8)
@@ -91,7 +94,7 @@ def main():
         p.prepare(0)
         data = d_rnd if cfg in ("c0", "c2") else d_l2
         if cfg == "c4h":
-            data = maps["c4h_pk"]
+            data = maps["c4h%d_pk" % (1 << int(opt[1:]) if opt.startswith("e") else workloads.C4H_ENTRIES)]
         if opt == "l2":      # the same program over the other packet buffer (placement check)
             data = d_l2
         elif opt == "rnd":
