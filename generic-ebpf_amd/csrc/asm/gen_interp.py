@@ -92,7 +92,8 @@ S_KMASK = 73         # superblock size - 1 of this launch (K' <= RETK, a power o
                      # dp_launch.total_waves bits 28..29 = log2 K'): small batches use shorter
                      # superblocks so that every wave gets work
 S_WAVE = 3
-NSGPR = 74           # + VCC, XNACK, FLAT_SCRATCH = 79 <= 80 SGPRs: 8 waves per SIMD
+NSGPR = 76           # + VCC, XNACK, FLAT_SCRATCH; s[74:75]: compiled programs' short-lane mask
+                     # in the general image (asm_cc.cpp ldxpkc_general)
 # staged image: s[74:75] .. s[96:97] hold the taken-lane masks of a structured compiled program's
 # pending branches (asm_jit.cpp; 12 levels); 98 SGPRs still allow the image's 6 waves per SIMD
 S_JOIN = 74

@@ -770,6 +770,50 @@ struct emitter {
 
 	// ---- staged packet load at constant offset `off`, size z; swap_bytes = 0, 2 or 4 (a fused
 	// BE16 / BE32 of the loaded register)
+	// General kernels with header staging: the packet load at constant offset off < 64 from the
+	// staged header registers, like the handler (h_ldx_pkt_const) but with its two per-load lane
+	// compares replaced by one per-group mask: s[74:75] = lanes whose packet is shorter than 64
+	// bytes (set by the prologue).  Only such lanes can fault (off + z > len) or need the load
+	// from memory; when none is running the load is the extract alone.
+	void ldxpkc_general(int d, int z, int off, uint32_t fault_off)
+	{
+		const int S_SHORT = 74, S_MASK = 48, S_CODE = 52, S_JUNK_ = 60, V_LEN = 40, V_PKT = 38;
+		static const uint32_t gop[4] = {0x10, 0x12, 0x14, 0x15};
+		const int zi = z == 1 ? 0 : z == 2 ? 1 : z == 4 ? 2 : 3;
+		auto patch = [&](size_t at) { // branch at byte `at` jumps to here
+			const uint32_t rel = (uint32_t)((blk.body.size() - at - 4) / 4);
+			blk.body[at] = (uint8_t)(rel & 0xff);
+			blk.body[at + 1] = (uint8_t)((rel >> 8) & 0xff);
+		};
+		E.sop2(0x0d, S_MASK, opnd{(uint32_t)S_SHORT}, opnd{SRC_EXEC});   // s_and_b64 (scc)
+		const size_t to_fast = blk.body.size();
+		E.w(0xbf840000u);                                                 // s_cbranch_scc0 fast
+		E.vopc(VC_U32 + P_GT, k32((uint32_t)(off + z)), V_LEN);          // vcc = off+z > len
+		E.sop2(0x0d, S_MASK, opnd{SRC_VCC}, opnd{SRC_EXEC});
+		E.w(0xbf840000u | 5u);                                           // s_cbranch_scc0 +5
+		E.sop1(0x00, S_CODE, opnd{128 + 3});                             // s_mov_b32 s52, 3 (MEM)
+		call_routine(fault_off, 0);                                      // (4 dwords)
+		const facts f0 = f; // (both paths emit the same extract from the same facts)
+		ldxpkc(d, z, off, 0);
+		E.sop2(0x0d, S_MASK, opnd{(uint32_t)S_SHORT}, opnd{SRC_EXEC});
+		const size_t to_end1 = blk.body.size();
+		E.w(0xbf840000u);                                                 // s_cbranch_scc0 end
+		E.sop1(0x01, S_JUNK_, opnd{SRC_EXEC});                           // s_mov_b64 s60, exec
+		E.sop1(0x01, 126, opnd{(uint32_t)S_MASK});                       // exec = short lanes
+		E.w(0xdc008000u | (gop[zi] << 18) | (uint32_t)off);              // global_load_*
+		E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)L(d) << 24));
+		E.w(0xbf8c0f70u);                                                 // s_waitcnt vmcnt(0)
+		if (z < 8)
+			mov32(Hi(d), 0);
+		E.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});                      // exec back
+		const size_t to_end2 = blk.body.size();
+		E.w(0xbf820000u);                                                 // s_branch end
+		patch(to_fast);
+		f = f0;
+		ldxpkc(d, z, off, 0);
+		patch(to_end1);
+		patch(to_end2);
+	}
 	void ldxpkc(int d, int z, int off, int swap_bytes)
 	{
 		const int k = off >> 2, sh = off & 3;
@@ -1403,9 +1447,12 @@ rf
 copied_result(int fam)
 {
 	switch (fam) {
-	case AHF_LDXGEN1: case AHF_LDXMAP1: case AHF_LDXPKTG1: case AHF_LDXSTK1: case AHF_LDXHV1: return kbits(8);
-	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: case AHF_LDXHV2: return kbits(16);
-	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: case AHF_LDXHV4: return kbits(32);
+	case AHF_LDXGEN1: case AHF_LDXMAP1: case AHF_LDXPKTG1: case AHF_LDXSTK1: case AHF_LDXHV1:
+	case AHF_LDXPKC1: return kbits(8);
+	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: case AHF_LDXHV2:
+	case AHF_LDXPKC2: return kbits(16);
+	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: case AHF_LDXHV4:
+	case AHF_LDXPKC4: return kbits(32);
 	default:
 		if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
 			return kbits(32);
@@ -1590,6 +1637,11 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	std::vector<char> pure(n, 0);
 	uint16_t live_start = 0x7ff;
 	const unsigned off = cc_off() | (structured ? 16u : 0u); // structured: compares leave VCC
+	// general kernels (parking scheduler, no join SGPRs): s[74:75] is free for the short-lane
+	// mask of the inline header loads (ldxpkc_general)
+	const bool gen_short_mask = mode == 0 && !structured && !AH_GEN_JOIN &&
+				    getenv("EBPF_CC_NOSHORT") == nullptr;
+	bool uses_short_mask = false;
 
 	for (int pass = 0; pass < 2; pass++) {
 		const bool final_pass = pass == 1;
@@ -1717,8 +1769,12 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = em.bswap(fam, d);
 				break;
 			case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: {
-				if (mode == 0) { // general kernels: the handler's length checks (copied)
-					ok = false;
+				if (mode == 0) { // general kernels: length checks against the short-lane mask
+					ok = gen_short_mask && s + (1 << (fam - AHF_LDXPKC1)) <= 64;
+					if (ok) {
+						em.ldxpkc_general(d, 1 << (fam - AHF_LDXPKC1), s, rt.fault);
+						uses_short_mask = true;
+					}
 					break;
 				}
 				const int z = 1 << (fam - AHF_LDXPKC1);
@@ -1893,6 +1949,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			}
 			if (xl.start < n) {
 				cc_prologue(mode, live_start, needs_pkt, structured, out[xl.start].prologue);
+				if (uses_short_mask) { // s[74:75] = lanes whose packet is shorter than 64 B
+					enc P{out[xl.start].prologue};
+					P.vop3(VC_U32 + P_GT, 74, 128 + 64, VGPR0 + 40, 0);
+				}
 				// staged kernel, hashtable probes through the routine: the group set-up
 				// can leave the next group's packet DMA to the first probe (s7 bit 4,
 				// gen_interp.py probe_wait), so a probe does not also wait for the DMA.

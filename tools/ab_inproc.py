@@ -82,6 +82,8 @@ def main():
             os.environ["EBPF_JIT_NOCC"] = "1"
         if opt == "nohoist":
             os.environ["EBPF_CC_NOHOIST"] = "1"
+        if opt == "noshort":
+            os.environ["EBPF_CC_NOSHORT"] = "1"
         if opt == "nohfwd":
             os.environ["EBPF_CC_NOHFWD"] = "1"
         if opt == "defer":
@@ -113,6 +115,7 @@ def main():
         os.environ.pop("EBPF_CC_OFF", None)
         os.environ.pop("EBPF_CC_DEFER_DMA", None)
         os.environ.pop("EBPF_CC_NOHFWD", None)
+        os.environ.pop("EBPF_CC_NOSHORT", None)
         os.environ.pop("EBPF_CC_PAD_SALU", None)
         os.environ.pop("EBPF_CC_PAD_VALU", None)
         launch_env = {}
