@@ -20,5 +20,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
     python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 > $O/prof_bench.json 2> $O/prof.err \
   || { tail -5 $O/prof.err; exit 1; }
 step pmc
-T=${TAG:-final}/pmc bash tools/pmc.sh c4 c4h c3 c0 || exit 1
+T=${TAG:-final}/pmc bash tools/pmc.sh ${PMC_CFGS:-c4 c4h c3 c0} || exit 1
 echo "== done ($(date +%T))"
