@@ -7,7 +7,11 @@ lookup per packet over 64M x 64 B synthetic packets per GPU) plus the per-step v
 histogram all-reduce (RCCL) when N > 1.  Packets are synthetic (seeded generator) and resident
 in HBM before timing starts.  Multi-GPU: one process per GPU (torch.distributed.run), each
 rank runs its own 64M-packet shard (weak scaling), the only collective is the 257-bin
-histogram all-reduce.
+histogram all-reduce, issued asynchronously so that it runs under the next step's kernel.
+
+roofline.kernel_ms is the interpreter kernel alone: HIP events that the library records on the
+launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so it compares
+with the kernel's average in a rocprofv3 --kernel-trace --stats summary.
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for the fields).
 """
@@ -40,6 +44,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="0 = default interpreter, 1 = HIP baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
+                    help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args()
 
 
@@ -147,31 +153,65 @@ def main():
         sizes = np.diff(offs)
         bytes_per_launch = int(sizes.sum()) + 8 * (n + 1)
     d_ret = torch.empty(n, dtype=torch.int64, device=dev)
-    d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream()
+    # two histogram buffers: the all-reduce of step i (N > 1) overlaps the launch of step i + 1
+    hists = [torch.zeros(257, dtype=torch.int64, device=dev) for _ in range(2)]
+    red = shard.OverlappedHistReduce(hists)
 
-    def step(ev=None):
-        d_hist.zero_()
-        if ev is not None:
-            ev[0].record(stream)
+    def launch(h, stream):
+        h.zero_()
         prog.run_batch_dev(local, d_pk.data_ptr(), n, 64, d_ret.data_ptr(),
                            None if d_offs is None else d_offs.data_ptr(), None,
-                           d_hist.data_ptr(), stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
-        shard.reduce_hist(d_hist)
+                           h.data_ptr(), stream.cuda_stream)
 
-    for _ in range(a.warmup):
-        step()
+    # HIP graphs (one per histogram buffer): the zeroing memset, the interpreter and the
+    # histogram reduce replay as one submission, with no per-step host launch gaps
+    graphs = None
+    if a.launch == "graph":
+        launch(hists[0], torch.cuda.current_stream())  # map mirrors and program uploaded
+        torch.cuda.synchronize()
+        try:
+            graphs = []
+            for h in hists:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    launch(h, torch.cuda.current_stream())
+                graphs.append(g)
+        except Exception as e:  # capture unsupported: eager launches, said in the bench line
+            print("graph capture failed (%s); eager launches" % e, file=sys.stderr)
+            graphs = None
+            torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+
+    def step(i, ev=None):
+        b = red.acquire(i)
+        if graphs is not None:  # events around the replay (histogram memset and reduce in it)
+            if ev is not None:
+                ev[0].record(stream)
+            graphs[b].replay()
+            if ev is not None:
+                ev[1].record(stream)
+        else:
+            if ev is not None:  # the library records them around the interpreter kernel alone
+                native.time_next_launch(ev[0].cuda_event, ev[1].cuda_event)
+            launch(hists[b], stream)
+        red.issue(b)
+
+    for i in range(a.warmup):
+        step(i)
+    red.finish()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(a.steps)]
+    for e0, e1 in evs:  # torch creates its events at their first record
+        e0.record(stream)
+        e1.record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(evs[i])
+        step(i, evs[i])
+    d_hist = red.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -187,6 +227,8 @@ def main():
 
     hist = d_hist.cpu().numpy()
     faulted = int(hist[256])
+    if int(hist.sum()) != n * world:  # every packet lands in exactly one bin of the last step
+        raise SystemExit("verdict histogram counts %d packets, expected %d" % (int(hist.sum()), n * world))
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     info = prog.info()
     if rank == 0:
@@ -207,7 +249,8 @@ def main():
                        "packets_per_gpu": n, "packet_bytes": 64 if offs is None else "IMIX",
                        "main_path_insns": lay.main_path_steps, "prog_slots": lay.nslots,
                        "dprog_entries": info.nentries, "variant": a.variant,
-                       "parallelism": "dp%d" % world, "faulted_packets": faulted},
+                       "parallelism": "dp%d" % world,
+                       "launch": "graph" if graphs is not None else "eager", "faulted_packets": faulted},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 4),

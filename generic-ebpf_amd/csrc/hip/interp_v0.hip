@@ -371,8 +371,7 @@ namespace {
 // counts as one u32 row; block b sums rows [16b, 16b+16) (thread t = bin t, so each row is one
 // coalesced 1-KB load, all 16 in flight at once) and adds the partial sums to the caller's u64
 // histogram.
-constexpr uint32_t kRowsPerBlock = 16;
-
+template <uint32_t kRowsPerBlock>
 __global__ void __launch_bounds__(256)
 ebpf_hist_reduce(const uint32_t *__restrict__ rows, uint32_t nrows, unsigned long long *hist)
 {
@@ -389,6 +388,16 @@ ebpf_hist_reduce(const uint32_t *__restrict__ rows, uint32_t nrows, unsigned lon
 		atomicAdd(&hist[threadIdx.x], acc);
 }
 
+template <uint32_t R>
+hipError_t
+launch_hist_reduce_r(const uint32_t *rows, uint32_t nrows, unsigned long long *hist,
+		     hipStream_t stream)
+{
+	const uint32_t blocks = (nrows + R - 1) / R;
+	hipLaunchKernelGGL(ebpf_hist_reduce<R>, dim3(blocks), dim3(256), 0, stream, rows, nrows, hist);
+	return hipGetLastError();
+}
+
 } // namespace
 
 hipError_t
@@ -397,9 +406,16 @@ launch_hist_reduce(const uint32_t *rows, uint32_t nrows, unsigned long long *his
 {
 	if (nrows == 0)
 		return hipSuccess;
-	const uint32_t blocks = (nrows + kRowsPerBlock - 1) / kRowsPerBlock;
-	hipLaunchKernelGGL(ebpf_hist_reduce, dim3(blocks), dim3(256), 0, stream, rows, nrows, hist);
-	return hipGetLastError();
+	// rows per block: fewer blocks means fewer atomics per bin (A/B probe EBPF_HIST_ROWS)
+	static const int rows_per_block = [] {
+		const char *e = getenv("EBPF_HIST_ROWS");
+		return e ? atoi(e) : 16;
+	}();
+	if (rows_per_block >= 64)
+		return launch_hist_reduce_r<64>(rows, nrows, hist, stream);
+	if (rows_per_block >= 32)
+		return launch_hist_reduce_r<32>(rows, nrows, hist, stream);
+	return launch_hist_reduce_r<16>(rows, nrows, hist, stream);
 }
 
 hipError_t

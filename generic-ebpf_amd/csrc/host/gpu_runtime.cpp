@@ -16,7 +16,8 @@
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
-			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap);
+			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap,
+			     hipEvent_t ev_start, hipEvent_t ev_stop);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
@@ -66,14 +67,18 @@ map_record(const struct ebpf_map *em, uint32_t *lds_used)
 
 // Per-device pool of histogram row buffers (asm kernels: one u32[256] row per workgroup).  A
 // buffer is reusable once the event recorded after its last use has completed, so concurrent
-// launches on different streams never share one.
+// launches on different streams never share one.  When all 64 buffers are queued on the GPU, the
+// caller waits for the oldest one's use to finish (back-pressure on a host that queues far
+// ahead, e.g. a loop of asynchronous launches) rather than failing.
 struct rows_slot {
 	void *p = nullptr;
 	hipEvent_t ev = nullptr;
+	uint64_t seq = 0; // order of the last use (the smallest is the oldest)
 	bool busy = false; // between acquire and the event record of the launch using it
 };
 std::mutex g_rows_lock;
 std::vector<std::vector<rows_slot>> g_rows;
+uint64_t g_rows_seq = 0;
 
 int
 rows_acquire(int device, size_t bytes, rows_slot **out)
@@ -81,25 +86,37 @@ rows_acquire(int device, size_t bytes, rows_slot **out)
 	std::lock_guard<std::mutex> g(g_rows_lock);
 	if ((int)g_rows.size() <= device)
 		g_rows.resize(device + 1);
-	for (rows_slot &r : g_rows[device])
+	std::vector<rows_slot> &pool = g_rows[device];
+	for (rows_slot &r : pool)
 		if (!r.busy && hipEventQuery(r.ev) == hipSuccess) {
 			r.busy = true;
 			*out = &r;
 			return 0;
 		}
-	if (g_rows[device].size() >= 64)
-		return ENOMEM;
-	g_rows[device].reserve(64); // slots must not move: callers keep pointers
-	rows_slot r;
-	if (hipMalloc(&r.p, bytes) != hipSuccess)
-		return ENOMEM;
-	if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
-		hipFree(r.p);
-		return ENOMEM;
+	if (pool.size() < 64) {
+		pool.reserve(64); // slots must not move: callers keep pointers
+		rows_slot r;
+		if (hipMalloc(&r.p, bytes) != hipSuccess)
+			return ENOMEM;
+		if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+			hipFree(r.p);
+			return ENOMEM;
+		}
+		r.busy = true;
+		pool.push_back(r);
+		*out = &pool.back();
+		return 0;
 	}
-	r.busy = true;
-	g_rows[device].push_back(r);
-	*out = &g_rows[device].back();
+	rows_slot *old = nullptr;
+	for (rows_slot &r : pool)
+		if (!r.busy && (!old || r.seq < old->seq))
+			old = &r;
+	if (!old)
+		return ENOMEM; // 64 launches mid-submission on the host at once
+	if (hipEventSynchronize(old->ev) != hipSuccess)
+		return EIO;
+	old->busy = true;
+	*out = old;
 	return 0;
 }
 
@@ -107,13 +124,16 @@ void
 rows_release(rows_slot *r, hipStream_t stream, bool used)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
-	if (used)
+	if (used) {
 		hipEventRecord(r->ev, stream);
+		r->seq = ++g_rows_seq;
+	}
 	r->busy = false;
 }
 
 thread_local std::string t_err;
 thread_local int t_dev = 0;
+thread_local hipEvent_t t_time_ev[2] = {nullptr, nullptr}; // ebpf_gpu_time_next_launch
 std::atomic<int> g_variant{0};
 
 int
@@ -309,7 +329,8 @@ asm_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 }
 
 int
-launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream)
+launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
+       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr)
 {
 	dp_launch L = L0;
 	L.maps = dp->d_maps;
@@ -353,12 +374,16 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-				      (mode == 1 && !probes) ? 4u : 0u);
+				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop);
 		if (rows)
 			rows_release(rows, stream, e == hipSuccess);
 	} else {
 		L.prog = dp->d_entries;
-		e = launch_interp_v0(L, stream);
+		if (ev_start)
+			hipEventRecord(ev_start, stream);
+		e = launch_interp_v0(L, stream); // (one kernel: its histogram is added in-kernel)
+		if (ev_stop)
+			hipEventRecord(ev_stop, stream);
 	}
 	if (e != hipSuccess)
 		return hip_fail(e, "kernel launch");
@@ -461,6 +486,16 @@ ebpf_gpu_set_device(int device)
 }
 
 EBPF_EXPORT int
+ebpf_gpu_time_next_launch(void *start_event, void *stop_event)
+{
+	if ((start_event == nullptr) != (stop_event == nullptr))
+		return fail(EINVAL, "start_event and stop_event must both be set or both be NULL");
+	t_time_ev[0] = static_cast<hipEvent_t>(start_event);
+	t_time_ev[1] = static_cast<hipEvent_t>(stop_event);
+	return 0;
+}
+
+EBPF_EXPORT int
 ebpf_gpu_set_variant(int variant)
 {
 	if (variant < 0 || variant > 2)
@@ -545,6 +580,9 @@ EBPF_EXPORT int
 ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
 			uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev, void *stream)
 {
+	// the measurement hook is consumed by this call, whatever it returns
+	hipEvent_t ev_start = t_time_ev[0], ev_stop = t_time_ev[1];
+	t_time_ev[0] = t_time_ev[1] = nullptr;
 	if (ep == nullptr || ret_dev == nullptr)
 		return fail(EINVAL, "prog or ret is NULL");
 	int err = validate_batch(batch);
@@ -554,8 +592,13 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	err = prepare(ep, device, &dp);
 	if (err)
 		return err;
-	if (batch->count == 0)
+	if (batch->count == 0) {
+		if (ev_start) { // no kernel: an empty interval
+			hipEventRecord(ev_start, static_cast<hipStream_t>(stream));
+			hipEventRecord(ev_stop, static_cast<hipStream_t>(stream));
+		}
 		return 0;
+	}
 	hipError_t e = hipSetDevice(device);
 	if (e != hipSuccess)
 		return hip_fail(e, "hipSetDevice");
@@ -569,7 +612,7 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	L.hist = reinterpret_cast<unsigned long long *>(hist_dev);
 	L.count = batch->count;
 	L.stride = batch->stride;
-	return launch(ep, dp, L, static_cast<hipStream_t>(stream));
+	return launch(ep, dp, L, static_cast<hipStream_t>(stream), ev_start, ev_stop);
 }
 
 EBPF_EXPORT int

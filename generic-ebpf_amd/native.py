@@ -91,7 +91,7 @@ FUNCS = {
     "ebpf_map_destroy": (None, [_VP]),
     # ebpf_gpu.h
     "ebpf_gpu_device_count": (_I, []), "ebpf_gpu_set_device": (_I, [_I]),
-    "ebpf_gpu_set_variant": (_I, [_I]), "ebpf_gpu_last_error": (ctypes.c_char_p, []),
+    "ebpf_gpu_set_variant": (_I, [_I]), "ebpf_gpu_time_next_launch": (_I, [_VP, _VP]), "ebpf_gpu_last_error": (ctypes.c_char_p, []),
     "ebpf_prog_prepare_device": (_I, [_VP, _I]),
     "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
@@ -111,6 +111,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError("native library not built: %s (run __graft_entry__.build())" % LIB_PATH)
+        # torch (when installed) bundles its own HIP runtime under the same soname: loaded
+        # first, it is the one the library binds to as well.  Loaded the other way round, a
+        # process gets two HIP runtimes and whichever initialises second sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in FUNCS.items():
             f = getattr(L, name)
@@ -321,6 +328,12 @@ class Prog:
 
 def gpu_count():
     return lib().ebpf_gpu_device_count()
+
+
+def time_next_launch(start_event, stop_event):
+    """The calling thread's next run_batch_dev records these hipEvent_t handles (ints, or None
+    to cancel) around the interpreter kernel alone (include/ebpf_gpu.h)."""
+    _check(lib().ebpf_gpu_time_next_launch(start_event, stop_event), "ebpf_gpu_time_next_launch")
 
 
 def set_variant(v):

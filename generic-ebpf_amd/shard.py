@@ -17,3 +17,44 @@ def reduce_hist(hist, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
     return hist
+
+
+class OverlappedHistReduce:
+    """Per-step histogram all-reduce overlapped with the next step's launch.
+
+    Step i accumulates into buffer ``i % 2``; its all-reduce is issued asynchronously (on the
+    collective's own stream, after the step's kernel) and is only waited for before step i + 2
+    zeroes that buffer again, so the all-reduce of step i runs under the kernel of step i + 1
+    instead of between them.  ``finish()`` waits for every pending reduce and returns the
+    buffer of the last step.  Without a process group the reduces are no-ops."""
+
+    def __init__(self, bufs, group=None):
+        import torch.distributed as dist
+        self.bufs = bufs
+        self.group = group
+        self.work = [None] * len(bufs)
+        self.last = None
+        self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def acquire(self, i):
+        """Buffer for step ``i`` (its previous reduce waited for)."""
+        b = i % len(self.bufs)
+        if self.work[b] is not None:
+            self.work[b].wait()
+            self.work[b] = None
+        return b
+
+    def issue(self, b):
+        """Start the all-reduce of buffer ``b`` (after the step that filled it)."""
+        import torch.distributed as dist
+        if self.active:
+            self.work[b] = dist.all_reduce(self.bufs[b], op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=True)
+        self.last = b
+
+    def finish(self):
+        for b, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[b] = None
+        return None if self.last is None else self.bufs[self.last]

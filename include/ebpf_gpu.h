@@ -104,6 +104,13 @@ int ebpf_gpu_set_device(int device);
  *   2 = the hand-written gfx950 assembly interpreter. */
 int ebpf_gpu_set_variant(int variant);
 
+/* Measurement hook (extension): the calling thread's next ebpf_prog_run_batch_dev records
+ * `start_event` just before the interpreter kernel and `stop_event` just after it, on the launch
+ * stream, so that hipEventElapsedTime gives the interpreter kernel's own duration (the verdict
+ * histogram's second-stage reduce comes after `stop_event`).  Both are hipEvent_t of the HIP
+ * runtime the library runs on; NULL, NULL cancels.  Returns 0, or EINVAL if only one is NULL. */
+int ebpf_gpu_time_next_launch(void *start_event, void *stop_event);
+
 /* Instruction semantics of a program (extension: the reference has only the first).
  *   EBPF_SEM_REFERENCE (default): the reference interpreter's, quirks included
  *       (ebpf_interpreter.c:23-372: cumulative stepping, MOV64 adds, NEG ignores dst, NEG64 is

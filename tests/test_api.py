@@ -198,3 +198,11 @@ def test_percpu_array_roundtrip(native, env):
     finally:
         m.destroy()
 
+
+
+def test_time_next_launch_argument_checks(native):
+    """ebpf_gpu_time_next_launch (include/ebpf_gpu.h): both events or neither; no HIP call."""
+    L = native.lib()
+    assert L.ebpf_gpu_time_next_launch(ctypes.c_void_p(16), None) == errno.EINVAL
+    assert L.ebpf_gpu_time_next_launch(None, ctypes.c_void_p(16)) == errno.EINVAL
+    assert L.ebpf_gpu_time_next_launch(None, None) == 0

@@ -175,6 +175,49 @@ def test_device_resident_api_and_histogram(gpu, env):
             m.destroy()
 
 
+def test_deep_async_queue_with_histogram(gpu, env):
+    """More queued launches than the 64 histogram row buffers, with no synchronisation in
+    between (a bench loop of many steps): every launch succeeds and the accumulated histogram
+    counts every packet of every launch."""
+    import torch
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4()
+    n = 1 << 20
+    pk = workloads.packets_l2l3(n, 64)
+    vals = workloads.c4_map_values()
+    case = goldens.Case("c4", lay.code, lay.relocs, [(8, 256, vals.tobytes())], pk, n, 64, None)
+    want, _, _, _ = oracle_run(case, nthreads=8)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream()
+        launches = 200
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(launches)]
+        for e0, e1 in evs:  # created at their first record
+            e0.record(st)
+            e1.record(st)
+        for e0, e1 in evs:  # every launch timed by the library's kernel events
+            gpu.time_next_launch(e0.cuda_event, e1.cuda_event)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, None,
+                            d_hist.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+        assert all(0.0 < m < 100.0 for m in ms), ms[:4]
+        np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+        h = np.zeros(257, dtype=np.int64)
+        np.add.at(h, np.minimum(want, 255).astype(np.int64), launches)
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
 @pytest.mark.parametrize("variant", [0, 2])
 def test_empty_and_ragged_batches(gpu, env, variant):
     """Empty, sub-group and ragged batches; the last size gives every wave of the persistent

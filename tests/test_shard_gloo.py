@@ -62,3 +62,56 @@ def test_shard_bounds_cover():
             spans = [shard.shard_bounds(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _overlap_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import pkgload
+    pkgload.load()
+    from generic_ebpf_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bufs = [torch.zeros(257, dtype=torch.int64) for _ in range(2)]
+    red = shard.OverlappedHistReduce(bufs)
+    steps = 7
+    for i in range(steps):   # bench.py's step: acquire, zero + fill, issue
+        b = red.acquire(i)
+        bufs[b].zero_()
+        bufs[b][(i * 3 + rank) % 256] += 10 + i
+        bufs[b][256] += rank
+        red.issue(b)
+    h = red.finish()
+    if rank == 0:
+        np.save(out, h.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_reduce_last_step(tmp_path):
+    """The double-buffered asynchronous reduce returns the last step's summed histogram."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "h.npy")
+    mp.spawn(_overlap_worker, args=(2, port, out), nprocs=2, join=True)
+    want = np.zeros(257, dtype=np.int64)
+    last = 6
+    for r in range(2):
+        want[(last * 3 + r) % 256] += 10 + last
+        want[256] += r
+    np.testing.assert_array_equal(np.load(out), want)
+
+
+def test_overlapped_reduce_single_process():
+    from generic_ebpf_amd import shard
+    bufs = [torch.zeros(257, dtype=torch.int64) for _ in range(2)]
+    red = shard.OverlappedHistReduce(bufs)
+    assert red.finish() is None
+    for i in range(3):
+        b = red.acquire(i)
+        bufs[b].fill_(i)
+        red.issue(b)
+    assert int(red.finish()[0]) == 2
