@@ -17,7 +17,8 @@ hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v
 // asm_runtime.cpp
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
 			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap,
-			     hipEvent_t ev_start, hipEvent_t ev_stop);
+			     hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist,
+			     bool hist_overwrite);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
@@ -66,38 +67,61 @@ map_record(const struct ebpf_map *em, uint32_t *lds_used)
 }
 
 // Per-device pool of histogram row buffers (asm kernels: one u32[256] row per workgroup).  A
-// buffer is reusable once the event recorded after its last use has completed, so concurrent
-// launches on different streams never share one.  When all 64 buffers are queued on the GPU, the
-// caller waits for the oldest one's use to finish (back-pressure on a host that queues far
-// ahead, e.g. a loop of asynchronous launches) rather than failing.
+// buffer whose last use has completed (its event) is taken as is.  Otherwise the pool grows to
+// kRowsPool buffers, so that launches on that many streams run concurrently; past that, a launch
+// takes the least recently used buffer and makes its stream wait (on the GPU, no host block) for
+// that buffer's last use, unless that use was on the same stream, whose order already implies
+// the wait (the per-thread default stream excepted: one handle, many streams; a destroyed
+// stream's handle is safe to see again since hipStreamDestroy finishes its work first).  A loop
+// of asynchronous launches on one stream thus never allocates nor waits in its steady state.
 struct rows_slot {
 	void *p = nullptr;
 	hipEvent_t ev = nullptr;
-	uint64_t seq = 0; // order of the last use (the smallest is the oldest)
+	uint64_t seq = 0; // order of the last use (the smallest is the least recent)
+	hipStream_t stream = nullptr; // stream of the last use
 	bool busy = false; // between acquire and the event record of the launch using it
 };
 std::mutex g_rows_lock;
 std::vector<std::vector<rows_slot>> g_rows;
 uint64_t g_rows_seq = 0;
+constexpr size_t kRowsPool = 4;
+constexpr size_t kRowsMax = 64; // buffers busy on the host at once (concurrent callers)
+
+// Each buffer is `bytes` of rows followed by kRowsScratch bytes: 257 u64 whose bin 256 takes the
+// interpreter's fault count (the second stage moves it out and re-zeroes it).
+constexpr size_t kRowsScratch = 4096;
 
 int
-rows_acquire(int device, size_t bytes, rows_slot **out)
+rows_acquire(int device, size_t bytes, hipStream_t stream, rows_slot **out)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
 	if ((int)g_rows.size() <= device)
 		g_rows.resize(device + 1);
 	std::vector<rows_slot> &pool = g_rows[device];
-	for (rows_slot &r : pool)
-		if (!r.busy && hipEventQuery(r.ev) == hipSuccess) {
-			r.busy = true;
-			*out = &r;
-			return 0;
-		}
-	if (pool.size() < 64) {
-		pool.reserve(64); // slots must not move: callers keep pointers
+	rows_slot *lru = nullptr;
+	size_t idle = 0;
+	for (rows_slot &r : pool) {
+		if (r.busy)
+			continue;
+		idle++;
+		if (!lru || r.seq < lru->seq)
+			lru = &r;
+	}
+	if (lru && hipEventQuery(lru->ev) == hipSuccess) { // the least recent use is done
+		lru->busy = true;
+		*out = lru;
+		return 0;
+	}
+	if ((idle < kRowsPool || !lru) && pool.size() < kRowsMax) {
+		pool.reserve(kRowsMax); // slots must not move: callers keep pointers
 		rows_slot r;
-		if (hipMalloc(&r.p, bytes) != hipSuccess)
+		if (hipMalloc(&r.p, bytes + kRowsScratch) != hipSuccess)
 			return ENOMEM;
+		if (hipMemsetAsync(static_cast<char *>(r.p) + bytes, 0, kRowsScratch, stream) !=
+		    hipSuccess) {
+			hipFree(r.p);
+			return ENOMEM;
+		}
 		if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
 			hipFree(r.p);
 			return ENOMEM;
@@ -107,16 +131,13 @@ rows_acquire(int device, size_t bytes, rows_slot **out)
 		*out = &pool.back();
 		return 0;
 	}
-	rows_slot *old = nullptr;
-	for (rows_slot &r : pool)
-		if (!r.busy && (!old || r.seq < old->seq))
-			old = &r;
-	if (!old)
-		return ENOMEM; // 64 launches mid-submission on the host at once
-	if (hipEventSynchronize(old->ev) != hipSuccess)
+	if (!lru)
+		return ENOMEM; // kRowsMax launches mid-submission on the host at once
+	if ((lru->stream != stream || stream == hipStreamPerThread) &&
+	    hipStreamWaitEvent(stream, lru->ev, 0) != hipSuccess)
 		return EIO;
-	old->busy = true;
-	*out = old;
+	lru->busy = true;
+	*out = lru;
 	return 0;
 }
 
@@ -127,6 +148,7 @@ rows_release(rows_slot *r, hipStream_t stream, bool used)
 	if (used) {
 		hipEventRecord(r->ev, stream);
 		r->seq = ++g_rows_seq;
+		r->stream = stream;
 	}
 	r->busy = false;
 }
@@ -330,7 +352,7 @@ asm_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 
 int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
-       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr)
+       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false)
 {
 	dp_launch L = L0;
 	L.maps = dp->d_maps;
@@ -362,11 +384,15 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		}
 		L.lds_pkt_base = (mode == 0 && ep->xlated->asm_gstage) ? 0x80000000u : 0;
 		rows_slot *rows = nullptr;
+		unsigned long long *user_hist = L.hist;
 		if (L.hist) {
-			if ((err = rows_acquire(dp->device,
-						(size_t)asm_max_workgroups(dp->device) * 1024, &rows)))
+			const size_t rows_bytes = (size_t)asm_max_workgroups(dp->device) * 1024;
+			if ((err = rows_acquire(dp->device, rows_bytes, stream, &rows)))
 				return fail(err, "no histogram row buffer");
 			L.hist_rows = static_cast<uint32_t *>(rows->p);
+			// faults (bin 256) go to the buffer's scratch; the second stage moves them
+			L.hist = reinterpret_cast<unsigned long long *>(static_cast<char *>(rows->p) +
+									rows_bytes);
 		}
 		// a program that probes hashtables is bound by their latency and wants every wave;
 		// the others stream packets (asm_runtime.cpp, occupancy)
@@ -374,11 +400,16 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop);
+				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop, user_hist,
+				      hist_overwrite);
 		if (rows)
 			rows_release(rows, stream, e == hipSuccess);
 	} else {
 		L.prog = dp->d_entries;
+		if (hist_overwrite && L.hist &&
+		    (e = hipMemsetAsync(L.hist, 0, EBPF_HIST_BINS * sizeof(uint64_t), stream)) !=
+			hipSuccess)
+			return hip_fail(e, "hipMemsetAsync(hist)");
 		if (ev_start)
 			hipEventRecord(ev_start, stream);
 		e = launch_interp_v0(L, stream); // (one kernel: its histogram is added in-kernel)
@@ -391,12 +422,13 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 }
 
 int
-validate_batch(const struct ebpf_pkt_batch *b)
+validate_batch(const struct ebpf_pkt_batch *b, uint32_t allowed_flags = 0)
 {
 	if (b == nullptr || (b->data == nullptr && b->count != 0))
 		return fail(EINVAL, "batch or batch->data is NULL");
-	if (b->flags != 0)
-		return fail(EINVAL, "batch->flags must be 0");
+	if (b->flags & ~allowed_flags)
+		return fail(EINVAL, allowed_flags ? "batch->flags: unknown bits"
+						  : "batch->flags must be 0");
 	if (b->offsets == nullptr && b->stride == 0 && b->count != 0)
 		return fail(EINVAL, "fixed-stride batch with stride 0");
 	return 0;
@@ -585,9 +617,10 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	t_time_ev[0] = t_time_ev[1] = nullptr;
 	if (ep == nullptr || ret_dev == nullptr)
 		return fail(EINVAL, "prog or ret is NULL");
-	int err = validate_batch(batch);
+	int err = validate_batch(batch, EBPF_BATCH_HIST_OVERWRITE);
 	if (err)
 		return err;
+	const bool overwrite = (batch->flags & EBPF_BATCH_HIST_OVERWRITE) != 0;
 	dprog_device *dp;
 	err = prepare(ep, device, &dp);
 	if (err)
@@ -596,6 +629,12 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 		if (ev_start) { // no kernel: an empty interval
 			hipEventRecord(ev_start, static_cast<hipStream_t>(stream));
 			hipEventRecord(ev_stop, static_cast<hipStream_t>(stream));
+		}
+		if (overwrite && hist_dev) {
+			hipError_t e = hipMemsetAsync(hist_dev, 0, EBPF_HIST_BINS * sizeof(uint64_t),
+						      static_cast<hipStream_t>(stream));
+			if (e != hipSuccess)
+				return hip_fail(e, "hipMemsetAsync(hist)");
 		}
 		return 0;
 	}
@@ -612,7 +651,7 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	L.hist = reinterpret_cast<unsigned long long *>(hist_dev);
 	L.count = batch->count;
 	L.stride = batch->stride;
-	return launch(ep, dp, L, static_cast<hipStream_t>(stream), ev_start, ev_stop);
+	return launch(ep, dp, L, static_cast<hipStream_t>(stream), ev_start, ev_stop, overwrite);
 }
 
 EBPF_EXPORT int

@@ -105,6 +105,9 @@ DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_ha
 _lib = None
 
 
+BATCH_HIST_OVERWRITE = 0x1  # include/ebpf_gpu.h EBPF_BATCH_HIST_OVERWRITE
+
+
 def lib():
     """Load lib/libebpf.so (raises OSError if it has not been built)."""
     global _lib
@@ -318,9 +321,11 @@ class Prog:
         return bytes(buf)[: n.value]
 
     def run_batch_dev(self, device, data_ptr, count, stride, ret_ptr, offsets_ptr=None,
-                      faults_ptr=None, hist_ptr=None, stream=None):
-        """Device pointers (ints); asynchronous on ``stream`` (hipStream_t as int or None)."""
-        b = PktBatch(data_ptr, offsets_ptr, count, stride, 0)
+                      faults_ptr=None, hist_ptr=None, stream=None, hist_overwrite=False):
+        """Device pointers (ints); asynchronous on ``stream`` (hipStream_t as int or None).
+        ``hist_overwrite``: the histogram is set to this batch's counts instead of added to."""
+        b = PktBatch(data_ptr, offsets_ptr, count, stride,
+                     BATCH_HIST_OVERWRITE if hist_overwrite else 0)
         _check(lib().ebpf_prog_run_batch_dev(self.ptr, device, ctypes.byref(b), ret_ptr,
                                              faults_ptr, hist_ptr, stream),
                "ebpf_prog_run_batch_dev")

@@ -55,8 +55,12 @@ struct ebpf_pkt_batch {
 	const uint64_t *offsets;
 	uint64_t count;
 	uint32_t stride;
-	uint32_t flags; /* reserved, must be 0 */
+	uint32_t flags; /* 0, or EBPF_BATCH_HIST_OVERWRITE (ebpf_prog_run_batch_dev only) */
 };
+
+/* ebpf_prog_run_batch_dev: hist_dev receives this batch's counts instead of having them added,
+ * so the caller need not zero it before each launch. */
+#define EBPF_BATCH_HIST_OVERWRITE 0x1u
 
 /* Verdict histogram: bin min(r0, 255) for packets that reached EXIT, bin 256 = faulted. */
 #define EBPF_HIST_BINS 257
@@ -88,7 +92,8 @@ int ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch
 /* Device-resident batch: every pointer (batch->data, batch->offsets, ret_dev, faults_dev,
  * hist_dev) is device memory on `device`.  Enqueued on `stream` (hipStream_t, NULL = default
  * stream) and returns without synchronising.  faults_dev / hist_dev may be NULL; hist_dev is
- * EBPF_HIST_BINS u64 counters that the kernel ADDS to (zero it yourself). */
+ * EBPF_HIST_BINS u64 counters that the kernel ADDS to (zero it yourself), or, with
+ * EBPF_BATCH_HIST_OVERWRITE in batch->flags, sets to this batch's counts. */
 int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
 			    uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev,
 			    void *stream);

@@ -206,3 +206,21 @@ def test_time_next_launch_argument_checks(native):
     assert L.ebpf_gpu_time_next_launch(ctypes.c_void_p(16), None) == errno.EINVAL
     assert L.ebpf_gpu_time_next_launch(None, ctypes.c_void_p(16)) == errno.EINVAL
     assert L.ebpf_gpu_time_next_launch(None, None) == 0
+
+
+def test_batch_flags_validation(native, env):
+    """batch->flags: only EBPF_BATCH_HIST_OVERWRITE, and only on the device entry point; the
+    check comes before any device work, so it holds without a GPU."""
+    from generic_ebpf_amd import isa
+    code = isa.encode(isa.OPS["mov_imm"], 0, imm=1) + isa.encode(isa.OPS["exit"])
+    p = native.Prog(env, code)
+    try:
+        L = native.lib()
+        bad = native.PktBatch(16, None, 1, 64, 0x2)
+        assert L.ebpf_prog_run_batch_dev(p.ptr, 0, ctypes.byref(bad), 16, None, None,
+                                         None) == errno.EINVAL
+        host = native.PktBatch(16, None, 1, 64, native.BATCH_HIST_OVERWRITE)
+        ret = (ctypes.c_uint64 * 1)()
+        assert L.ebpf_prog_run_batch(p.ptr, ctypes.byref(host), ret, None, None) == errno.EINVAL
+    finally:
+        p.destroy()

@@ -218,6 +218,54 @@ def test_deep_async_queue_with_histogram(gpu, env):
             m.destroy()
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_histogram_overwrite_with_faults(gpu, env, variant):
+    """EBPF_BATCH_HIST_OVERWRITE: the histogram (faulted bin 256 included) is set to each
+    launch's counts over a garbage-filled buffer, launch after launch (the fault count's scratch
+    is left zero for the next launch), in add mode the counts accumulate, and an empty batch
+    zeroes it."""
+    import torch
+    from generic_ebpf_amd import isa, layout, workloads
+    I = isa.Insn
+    # r0 = pkt[0]; faults (division by zero) where pkt[1] & 3 == 0
+    code = layout.assemble([I("ldxb", 0, 1, 0), I("ldxb", 2, 1, 1), I("and_imm", 2, imm=3),
+                            I("div64_reg", 0, 2), I("exit")]).code
+    n = 64 * 4096 + 77
+    pk = workloads.packets_random(n, 64, seed=31)
+    c = goldens.Case("ovw", code, [], [], pk.reshape(-1), n, 64, None)
+    want, wf, _, _ = oracle_run(c, nthreads=8)
+    h = np.zeros(257, dtype=np.int64)
+    ok = wf == 0
+    np.add.at(h, np.minimum(want[ok], 255).astype(np.int64), 1)
+    h[256] = int((~ok).sum())
+    assert h[256] > 0
+    gpu.set_variant(variant)
+    p = gpu.Prog(env, code)
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_hist = torch.full((257,), 12345, dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        for _ in range(3):
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, None,
+                            d_hist.data_ptr(), st, hist_overwrite=True)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+        for _ in range(2):  # add mode on top
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, None,
+                            d_hist.data_ptr(), st)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), 3 * h)
+        p.run_batch_dev(0, d_pk.data_ptr(), 0, 64, d_ret.data_ptr(), None, None,
+                        d_hist.data_ptr(), st, hist_overwrite=True)
+        torch.cuda.synchronize()
+        assert not d_hist.cpu().numpy().any()
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+
+
 @pytest.mark.parametrize("variant", [0, 2])
 def test_empty_and_ragged_batches(gpu, env, variant):
     """Empty, sub-group and ragged batches; the last size gives every wave of the persistent
