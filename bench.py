@@ -11,7 +11,8 @@ histogram all-reduce, issued asynchronously so that it runs under the next step'
 
 roofline.kernel_ms is the interpreter kernel alone: HIP events that the library records on the
 launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so it compares
-with the kernel's average in a rocprofv3 --kernel-trace --stats summary.
+with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 5th timed step
+carries the events (--time-every): each event pair costs a launch gap.
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for the fields).
 """
@@ -44,6 +45,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="0 = default interpreter, 1 = HIP baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--time-every", type=int, default=5,
+                    help="event-time the kernel of every k-th timed step (default 5: a pair of events per step costs C2 7 us of its 21-us step; profiles/r01/te)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args()
@@ -199,8 +202,9 @@ def main():
         step(i)
     red.finish()
     torch.cuda.synchronize()
+    timed = list(range(0, a.steps, max(1, a.time_every)))  # steps whose kernel is event-timed
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
+           for _ in timed]
     for e0, e1 in evs:  # torch creates its events at their first record
         e0.record(stream)
         e1.record(stream)
@@ -208,8 +212,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    k = 0
     for i in range(a.steps):
-        step(i, evs[i])
+        if k < len(timed) and timed[k] == i:
+            step(i, evs[k])
+            k += 1
+        else:
+            step(i)
     d_hist = red.finish()
     torch.cuda.synchronize()
     if world > 1:
@@ -253,6 +262,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                         "kernel_ms_samples": len(evs),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
         }

@@ -19,6 +19,7 @@ step rocprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- \
     python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 > $O/prof_bench.json 2> $O/prof.err \
   || { tail -5 $O/prof.err; exit 1; }
+[ -n "${SKIP_PMC:-}" ] && { echo "== done, no pmc ($(date +%T))"; exit 0; }
 step pmc
 T=${TAG:-final}/pmc bash tools/pmc.sh ${PMC_CFGS:-c4 c4h c3 c0} || exit 1
 echo "== done ($(date +%T))"
