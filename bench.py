@@ -115,7 +115,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        # nccl (= RCCL) on the node; EBPF_BENCH_BACKEND=gloo rehearses N > 1 on one GPU
+        dist.init_process_group(os.environ.get("EBPF_BENCH_BACKEND", "nccl"))
+    if world > 1 and os.environ.get("EBPF_BENCH_BACKEND") == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = a.config
