@@ -1,25 +1,41 @@
 #!/usr/bin/env python3
 """Device-resident batch eBPF throughput on MI355X (BASELINE.json metric).
 
-One step = one launch of the interpreter over the rank's whole device-resident batch (the
-workload named by --config; default C4: the 64-insn VALE-BPF-style classify + one array-map
-lookup per packet over 64M x 64 B synthetic packets per GPU) plus the per-step verdict
-histogram all-reduce (RCCL) when N > 1.  Packets are synthetic (seeded generator) and resident
-in HBM before timing starts.  Multi-GPU: one process per GPU (torch.distributed.run), each
-rank runs its own 64M-packet shard (weak scaling), the only collective is the 257-bin
-histogram all-reduce, issued asynchronously so that it runs under the next step's kernel.
+One step = one launch of the engine over the rank's whole device-resident shard of the batch
+(the workload named by --config; default C4: the 64-insn VALE-BPF-style classify + one
+array-map lookup per packet over 64M x 64 B synthetic packets) plus, when N > 1, the per-step
+verdict histogram all-reduce (RCCL).  Packets are synthetic (seeded generator) and resident in
+HBM before timing starts.
 
-roofline.kernel_ms is the interpreter kernel alone: HIP events that the library records on the
+Multi-GPU (one process per GPU, torch.distributed.run): by default the config's batch is
+SHARDED (--scaling strong: C4's 64M packets split in contiguous shards over the N ranks,
+shard.shard_bounds, as BASELINE config 4 states); --scaling weak gives every rank a batch of
+the config's size.  The only collective is the 257-bin histogram all-reduce, issued
+asynchronously so that it runs under the next step's kernel.
+
+After the timed loop the LAST timed launch is verified: its per-packet results (the whole
+shard, on the GPU) and the reduced verdict histogram are compared with the CPU oracle
+(oracle/, the restatement of the reference interpreter) on the distinct packets the shard
+tiles; any mismatch prints the line with "verified": false and exits 1.
+
+roofline.kernel_ms is the engine's kernel alone: HIP events that the library records on the
 launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so it compares
 with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 5th timed step
-carries the events (--time-every): each event pair costs a launch gap.
+carries the events (--time-every).  roofline.traffic is measured by THIS run: two child passes
+of this script under rocprofv3 --pmc (FETCH_SIZE, then WRITE_SIZE) on the same workload, after
+the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).
 
-Prints ONE JSON line on rank 0 (see README / DESIGN.md for the fields).
+Prints ONE JSON line on rank 0.
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -33,23 +49,35 @@ pkg = pkgload.load()
 from generic_ebpf_amd import native, shard, workloads  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "Mpkt/s device-resident (64-insn filter, 64B pkts); achieved HBM GB/s vs peak"
+# Round-1 calibration in the build container, C4, 1 thread: the genuine reference libebpf.so
+# 9.1 Mpkt/s, this oracle (port) 7.6 Mpkt/s
+PORT_VS_REFERENCE = round(7.6 / 9.1, 3)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c4", choices=sorted(workloads.CONFIGS))
-    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default per config)")
-    ap.add_argument("--variant", type=int, default=0, help="0 = default interpreter, 1 = HIP baseline")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    ap.add_argument("--packets", type=int, default=0,
+                    help="packets of the whole batch (strong) or per GPU (weak); default per config")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the batch is sharded over the ranks (default); weak: each rank its own batch")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="0 = compiled (default), 1 = portable HIP, 2 = assembly interpreter")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU baseline budget (half all-threads, half one pinned thread)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle check (PMC child passes)")
+    ap.add_argument("--no-pmc", action="store_true", help="no rocprofv3 --pmc passes for roofline.traffic")
+    ap.add_argument("--pmc-dir", default="", help="where the PMC passes write (default: a temp dir)")
     ap.add_argument("--time-every", type=int, default=5,
                     help="event-time the kernel of every k-th timed step (default 5: a pair of events per step costs C2 7 us of its 21-us step; profiles/r01/te)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
@@ -58,52 +86,231 @@ C4H_SLOT_BYTES = 32  # device table slot: u32 used | u32 hash | 4-B key (8-B pad
 DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
 
 
-def build_inputs(cfg, n, rank):
-    """Host-side synthetic inputs for one rank: (layout, maps spec, packets u8, offsets|None)."""
-    lay = workloads.CONFIGS[cfg]["prog"]()
+class Workload:
+    """The rank's part [lo, hi) of the global batch.  Fixed-size configs: global packet g is
+    distinct[g % D] (D distinct packets generated once, the same on every rank).  C5: an
+    IMIX stream generated in blocks, so a shard is the same bytes whatever N."""
+
+    def __init__(self, cfg, lo, hi, total):
+        self.cfg, self.lo, self.hi = cfg, lo, hi
+        self.n = hi - lo
+        self.lay = workloads.CONFIGS[cfg]["prog"]()
+        self.maps = []
+        self.offs = None
+        if cfg == "c5":
+            self.pk, self.offs, _ = workloads.packets_imix_range(lo, hi, seed=5)
+            self.D = self.n
+            return
+        self.D = min(total, DISTINCT)
+        if cfg == "c4":
+            self.maps = [(8, 256, workloads.c4_map_values().tobytes())]
+        if cfg == "c4h":  # ("hash", key_size, value_size, max_entries, keys, values)
+            universe, keys, values = workloads.c4h_table()
+            self.maps = [("hash", 4, 8, len(keys), keys, values)]
+            self.pk = workloads.packets_c4h(self.D, universe, seed=4)
+            return
+        rnd = cfg in ("c0", "c2", "nop200", "alu200")
+        gen = workloads.packets_random if rnd else workloads.packets_l2l3
+        self.pk = gen(self.D, 64, seed=2 if rnd else 3)
+
+    def device_packets(self, torch, dev):
+        """(packets on dev, offsets on dev or None) for this shard."""
+        if self.offs is not None:
+            return (torch.from_numpy(self.pk).to(dev),
+                    torch.from_numpy(self.offs.view(np.int64)).to(dev))
+        base = torch.from_numpy(self.pk).to(dev)           # D x 64
+        s = self.lo % self.D
+        if s:
+            base = torch.cat([base[s:], base[:s]])
+        reps = (self.n + self.D - 1) // self.D
+        d_pk = (base.repeat(reps, 1)[: self.n] if reps > 1 else base[: self.n]).contiguous()
+        return d_pk.reshape(-1), None
+
+    def algorithmic_bytes(self):
+        if self.offs is not None:  # every packet byte + the offsets array
+            return int(np.diff(self.offs).sum()) + 8 * (self.n + 1)
+        b = self.n * 64
+        if self.cfg == "c4h":  # + one table slot per packet that reaches the lookup (IPv4, not ICMP)
+            pk = self.pk
+            et = (pk[:, 12].astype(np.uint32) << 8) | pk[:, 13]
+            reach = float(np.mean((et == 0x0800) & (pk[:, 23] != 1)))
+            b += int(round(self.n * reach) * C4H_SLOT_BYTES)
+        return b
+
+    def oracle_maps(self):
+        import pyoracle
+        return [pyoracle.HashSpec(m[1], m[2], keys=m[4], values=m[5]) if m[0] == "hash" else m
+                for m in self.maps]
+
+
+def make_maps(env, spec):
     maps = []
-    if cfg == "c4":
-        maps = [(8, 256, workloads.c4_map_values().tobytes())]
-    if cfg == "c4h":   # ("hash", key_size, value_size, max_entries, keys, values)
-        universe, keys, values = workloads.c4h_table()
-        maps = [("hash", 4, 8, len(keys), keys, values)]
-        return lay, maps, workloads.packets_c4h(min(n, DISTINCT), universe, seed=4 + 1000 * rank), None
-    if cfg == "c5":
-        data, offs, _ = workloads.packets_imix(n, seed=5 + rank)
-        return lay, maps, data, offs
-    d = min(n, DISTINCT)
-    rnd = cfg in ("c0", "c2", "nop200", "alu200")
-    gen = workloads.packets_random if rnd else workloads.packets_l2l3
-    return lay, maps, gen(d, 64, seed=(2 if rnd else 3) + 1000 * rank), None
+    for s in spec:
+        if s[0] == "hash":
+            _, ks, vs, me, keys, values = s
+            m = native.HashMap(env, ks, vs, me)
+            m.fill(keys, values)
+        else:
+            vs, me, d = s
+            m = native.Map(env, me, vs)
+            m.fill(d)
+        maps.append(m)
+    return maps
 
 
-def cpu_baseline(cfg, lay, maps, pk, offs, budget_s):
-    """Oracle (the CPU restatement of the reference interpreter, raw-pointer mode like the
-    reference) on a bounded sample of the same workload, all host threads up to 16."""
+def oracle_threads():
+    """Host threads for the oracle: the CPU share this process may use (OMP_NUM_THREADS is set
+    to the box's share on the GPU pool; else the affinity mask)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(aff, int(env))) if env.isdigit() and int(env) > 0 else aff
+
+
+def verify(w, torch, d_ret, d_hist_total, world, dev):
+    """Compare the last launch's results on the device with the oracle.  Returns (ok, info)."""
     import pyoracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    if offs is not None:
-        n = min(len(offs) - 1, 1 << 18)
-        data, offsets = pk[: int(offs[n])], offs[: n + 1]
+    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=True)
+    thr = oracle_threads()
+    if w.offs is not None:
+        want, wf, _, _ = op.run(w.pk, w.n, 0, w.offs, nthreads=thr)
     else:
-        n = min(pk.shape[0], 1 << 20)
-        data, offsets = pk[:n].reshape(-1), None
-    maps = [pyoracle.HashSpec(m[1], m[2], keys=m[4], values=m[5]) if m[0] == "hash" else m
-            for m in maps]
-    op = pyoracle.OracleProgram(lay.code, lay.relocs, maps, checked=False)
-    op.run(data, n, 64, offsets, nthreads=threads)  # warm
-    t0 = time.perf_counter()
-    passes = 0
-    while True:
-        op.run(data, n, 64, offsets, nthreads=threads)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(n * passes / el / 1e6, 2), "unit": "Mpkt/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d passes over %d %s packets (%s), %d host threads, %.1f s" % (
-                passes, n, cfg.upper(), "IMIX" if offsets is not None else "64 B", threads, el)}
+        want, wf, _, _ = op.run(w.pk, w.D, 64, None, nthreads=thr)
+    # per-packet results: the shard tiles want[] starting at lo % D
+    wt = torch.from_numpy(want.view(np.int64)).to(dev)
+    s = w.lo % w.D
+    if s:
+        wt = torch.cat([wt[s:], wt[:s]])
+    got = d_ret[: w.n]
+    k, r = divmod(w.n, w.D)
+    bad = 0
+    if k:
+        bad += int((got[: k * w.D].view(k, w.D) != wt.unsqueeze(0)).sum())
+    if r:
+        bad += int((got[k * w.D:] != wt[:r]).sum())
+    # histogram of the shard: bin min(r0, 255), faulted packets in bin 256
+    cnt = np.full(w.D, k, dtype=np.int64)
+    cnt[(s + np.arange(r)) % w.D] += 1
+    bins = np.where(wf != 0, 256, np.minimum(want, 255)).astype(np.int64)
+    exp = np.bincount(bins, weights=cnt, minlength=257).astype(np.int64)
+    exp_t = torch.from_numpy(exp).to(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(exp_t)
+        b = torch.tensor([bad], dtype=torch.int64, device=dev)
+        dist.all_reduce(b)
+        bad = int(b[0])
+    hist_bad = int((d_hist_total != exp_t).sum())
+    info = {"verified": bad == 0 and hist_bad == 0, "ret_mismatches": bad,
+            "hist_mismatched_bins": hist_bad,
+            "oracle_packets": int(w.n if w.offs is not None else w.D)}
+    return info["verified"], info
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(w, budget_s):
+    """The oracle (the CPU restatement of the reference interpreter in raw-pointer mode, the
+    reference's cost model) on a bounded sample of the same workload, run in place on
+    preallocated buffers: (i) every thread of this process's CPU share, contiguous shards
+    (OpenMP static schedule); (ii) one thread pinned to one core."""
+    import pyoracle
+    if w.offs is not None:
+        n = min(w.n, 1 << 18)
+        data = np.ascontiguousarray(w.pk[: int(w.offs[n])])
+        offsets = np.ascontiguousarray(w.offs[: n + 1], dtype=np.uint64)
+        stride = 0
+    else:
+        n = min(w.D, 1 << 20)
+        data = np.ascontiguousarray(w.pk[:n].reshape(-1))
+        offsets, stride = None, 64
+    # no configured program stores to packet bytes, so passes over the same buffer are identical
+    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=False)
+    ret = np.zeros(n, dtype=np.uint64)
+
+    def timed(threads, seconds):
+        op.run_inplace(data, n, stride, offsets, ret, None, threads)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            op.run_inplace(data, n, stride, offsets, ret, None, threads)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return n * passes / el / 1e6, passes, el
+
+    thr = oracle_threads()
+    multi, mp, mel = timed(thr, budget_s / 2)
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    try:
+        os.sched_setaffinity(0, {core})
+        single, sp, sel = timed(1, budget_s / 2)
+    finally:
+        os.sched_setaffinity(0, old)
+    return {"value": round(multi, 2), "unit": "Mpkt/s", "cores": thr, "kind": "port",
+            "single_thread_value": round(single, 2), "single_thread_core": core,
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "port_vs_reference": PORT_VS_REFERENCE,
+            "sample": "%d %s packets (%s) run in place: %d passes on %d threads in %.1f s; "
+                      "%d passes on 1 thread pinned to CPU %d in %.1f s" % (
+                          n, w.cfg.upper(), "IMIX" if offsets is not None else "64 B",
+                          mp, thr, mel, sp, core, sel)}
+
+
+def pmc_traffic(a, w, total, layout):
+    """HBM bytes per launch of the engine's kernel, from two rocprofv3 --pmc child passes of
+    this script on the same workload (each counter group in a run of its own, kernel trace
+    only besides --pmc: MI355X_MICROARCH.md, HBM/rocprofv3).  FETCH_SIZE/WRITE_SIZE are KiB;
+    gfx950's FETCH_SIZE reports half of a 16-B/lane streaming read, so the staged kernels'
+    packet DMA (layout 1) gets its other half added back."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    out = a.pmc_dir or tempfile.mkdtemp(prefix="ebpf_pmc_")
+    child = [sys.executable, os.path.abspath(__file__), "--config", a.config, "--packets",
+             str(total), "--steps", "2", "--warmup", "1", "--variant", str(a.variant),
+             "--no-cpu-baseline", "--no-pmc", "--no-verify"]
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out, "pmc_%s_%s" % (a.config, counter))
+        os.makedirs(d, exist_ok=True)
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "--kernel-trace",
+               "--kernel-include-regex", "ebpf_(interp|jit)", "--output-format", "csv",
+               "-d", d, "-o", "pmc", "--"] + child
+        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
+        if r.returncode != 0:
+            return None, "%s pass exited %d: %s" % (counter, r.returncode,
+                                                     r.stderr.decode(errors="replace")[-300:])
+        per = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    kn = row.get("Kernel_Name", "")
+                    if row.get("Counter_Name") != counter or not (
+                            "ebpf_interp" in kn or "ebpf_jit" in kn):
+                        continue
+                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+        if not per:
+            return None, "%s pass recorded no engine dispatch" % counter
+        vals[counter] = sum(per.values()) / len(per) * 1024.0
+    fetch = vals["FETCH_SIZE"]
+    note = "FETCH_SIZE + WRITE_SIZE per launch, this run"
+    if layout == 1:
+        fetch += w.n * 64 / 2.0
+        note += "; staged 64-B packet DMA: half its bytes added (gfx950 16-B/lane undercount)"
+    return {"bytes": fetch + vals["WRITE_SIZE"], "fetch_reported": vals["FETCH_SIZE"],
+            "write": vals["WRITE_SIZE"], "note": note}, None
 
 
 def main():
@@ -122,83 +329,67 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = a.config
-    n = a.packets or DEFAULT_PACKETS[cfg]
+    size = a.packets or DEFAULT_PACKETS[cfg]
+    if a.scaling == "strong":
+        total = size
+        lo, hi = shard.shard_bounds(total, rank, world)
+    else:
+        total = size * world
+        lo, hi = rank * size, (rank + 1) * size
+    w = Workload(cfg, lo, hi, size if a.scaling == "weak" else total)
+    n = w.n
 
-    lay, maps_spec, pk, offs = build_inputs(cfg, n, rank)
     env = native.Env()
-    maps = []
-    for spec in maps_spec:
-        if spec[0] == "hash":
-            _, ks, vs, me, keys, values = spec
-            m = native.HashMap(env, ks, vs, me)
-            m.fill(keys, values)
-        else:
-            vs, me, d = spec
-            m = native.Map(env, me, vs)
-            m.fill(d)
-        maps.append(m)
-    prog = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    maps = make_maps(env, w.maps)
+    prog = native.Prog(env, native.patch_relocs(w.lay.code, w.lay.relocs, [m.handle for m in maps]))
     native.set_variant(a.variant)
     prog.prepare(local)
 
-    # device-resident inputs
-    if offs is None:
-        base = torch.from_numpy(pk.reshape(-1)).to(dev)
-        reps = (n + pk.shape[0] - 1) // pk.shape[0]
-        d_pk = base.repeat(reps)[: n * 64].contiguous()
-        del base
-        d_offs = None
-        bytes_per_launch = n * 64
-        if cfg == "c4h":  # + one table slot per packet that reaches the lookup (IPv4, not ICMP)
-            et = (pk[:, 12].astype(np.uint32) << 8) | pk[:, 13]
-            reach = float(np.mean((et == 0x0800) & (pk[:, 23] != 1)))
-            bytes_per_launch = int(n * 64 + round(n * reach) * C4H_SLOT_BYTES)
-    else:
-        d_pk = torch.from_numpy(pk).to(dev)
-        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-        sizes = np.diff(offs)
-        bytes_per_launch = int(sizes.sum()) + 8 * (n + 1)
-    d_ret = torch.empty(n, dtype=torch.int64, device=dev)
+    d_pk, d_offs = w.device_packets(torch, dev)
+    bytes_per_launch = w.algorithmic_bytes()
+    d_ret = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     # two histogram buffers: the all-reduce of step i (N > 1) overlaps the launch of step i + 1
     hists = [torch.zeros(257, dtype=torch.int64, device=dev) for _ in range(2)]
     red = shard.OverlappedHistReduce(hists)
-
-    def launch(h, stream):  # the launch sets h to this batch's counts (no memset first)
-        prog.run_batch_dev(local, d_pk.data_ptr(), n, 64, d_ret.data_ptr(),
+    stream = torch.cuda.current_stream()
+    # the launch sets its histogram to this batch's counts (no memset first)
+    launch = prog.launcher(local, d_pk.data_ptr(), n, 64, d_ret.data_ptr(),
                            None if d_offs is None else d_offs.data_ptr(), None,
-                           h.data_ptr(), stream.cuda_stream, hist_overwrite=True)
+                           stream.cuda_stream, hist_overwrite=True)
+    hptr = [h.data_ptr() for h in hists]
 
-    # HIP graphs (one per histogram buffer): the zeroing memset, the interpreter and the
-    # histogram reduce replay as one submission, with no per-step host launch gaps
+    # HIP graphs (one per histogram buffer): the launch replays as one submission
     graphs = None
     if a.launch == "graph":
-        launch(hists[0], torch.cuda.current_stream())  # map mirrors and program uploaded
+        launch(hptr[0])  # map mirrors uploaded, program compiled
         torch.cuda.synchronize()
         try:
             graphs = []
-            for h in hists:
+            for p in hptr:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    launch(h, torch.cuda.current_stream())
+                    prog.run_batch_dev(local, d_pk.data_ptr(), n, 64, d_ret.data_ptr(),
+                                       None if d_offs is None else d_offs.data_ptr(), None, p,
+                                       torch.cuda.current_stream().cuda_stream,
+                                       hist_overwrite=True)
                 graphs.append(g)
         except Exception as e:  # capture unsupported: eager launches, said in the bench line
             print("graph capture failed (%s); eager launches" % e, file=sys.stderr)
             graphs = None
             torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
 
     def step(i, ev=None):
         b = red.acquire(i)
-        if graphs is not None:  # events around the replay (histogram reduce in it)
+        if graphs is not None:  # events around the replay
             if ev is not None:
                 ev[0].record(stream)
             graphs[b].replay()
             if ev is not None:
                 ev[1].record(stream)
         else:
-            if ev is not None:  # the library records them around the interpreter kernel alone
+            if ev is not None:  # the library records them around the engine's kernel alone
                 native.time_next_launch(ev[0].cuda_event, ev[1].cuda_event)
-            launch(hists[b], stream)
+            launch(hptr[b])
         red.issue(b)
 
     for i in range(a.warmup):
@@ -233,39 +424,49 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     ms_per_step = el * 1e3 / a.steps
-    total_pkts = n * world * a.steps
-    value = total_pkts / el / 1e6
+    value = total * a.steps / el / 1e6
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    exec_name, layout, translate_ms, build_ms = prog.exec_info(local)
 
     hist = d_hist.cpu().numpy()
     faulted = int(hist[256])
-    if int(hist.sum()) != n * world:  # every packet lands in exactly one bin of the last step
-        raise SystemExit("verdict histogram counts %d packets, expected %d" % (int(hist.sum()), n * world))
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    info = prog.info()
+    vinfo = {"verified": None}
+    ok = True
+    if not a.no_verify:  # the last timed launch against the oracle (outside the timing)
+        ok, vinfo = verify(w, torch, d_ret, d_hist, world, dev)
+    elif int(hist.sum()) != total:
+        ok = False
+        vinfo = {"verified": False, "hist_total": int(hist.sum())}
+
     if rank == 0:
         cpu = None
         if not a.no_cpu_baseline and world == 1:
-            maps_for_oracle = maps_spec
-            cpu = cpu_baseline(cfg, lay, maps_for_oracle, pk, offs, a.cpu_seconds)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg)
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            cpu = cpu_baseline(w, a.cpu_seconds)
+        traffic, pmc_note = None, "not collected (N > 1)" if world > 1 else "disabled (--no-pmc)"
+        if not a.no_pmc and world == 1:
+            t, err = pmc_traffic(a, w, total, layout)
+            traffic, pmc_note = (t["bytes"], t["note"]) if t else (None, err)
         out = {
-            "metric": "Mpkt/s device-resident (64-insn filter, 64B pkts); achieved HBM GB/s vs peak",
+            "metric": METRIC,
             "value": round(value, 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "verified": vinfo.get("verified"),
             "config": {"workload": cfg, "desc": workloads.CONFIGS[cfg]["desc"],
-                       "packets_per_gpu": n, "packet_bytes": 64 if offs is None else "IMIX",
-                       "main_path_insns": lay.main_path_steps, "prog_slots": lay.nslots,
-                       "dprog_entries": info.nentries, "variant": a.variant,
+                       "packets_total": total, "packets_per_gpu": n,
+                       "packet_bytes": 64 if w.offs is None else "IMIX",
+                       "main_path_insns": w.lay.main_path_steps, "prog_slots": w.lay.nslots,
+                       "dprog_entries": prog.info().nentries, "variant": a.variant,
+                       "exec": exec_name, "kernel_layout": "staged64" if layout == 1 else "general",
+                       "translate_ms": round(translate_ms, 3), "build_ms": round(build_ms, 3),
                        "parallelism": "dp%d" % world,
-                       "launch": "graph" if graphs is not None else "eager", "faulted_packets": faulted},
+                       "launch": "graph" if graphs is not None else "eager",
+                       "faulted_packets": faulted},
+            "check": vinfo,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": traffic, "kernel_ms": round(kern_ms, 4),
-                         "kernel_ms_samples": len(evs),
+                         "traffic": traffic, "traffic_note": pmc_note,
+                         "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": len(evs),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
         }
@@ -276,6 +477,8 @@ def main():
     env.destroy()
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

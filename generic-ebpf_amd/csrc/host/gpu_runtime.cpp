@@ -18,7 +18,7 @@ hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
 			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap,
 			     hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist,
-			     bool hist_overwrite);
+			     bool hist_overwrite, bool *enqueued);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
@@ -70,10 +70,8 @@ map_record(const struct ebpf_map *em, uint32_t *lds_used)
 // buffer whose last use has completed (its event) is taken as is.  Otherwise the pool grows to
 // kRowsPool buffers, so that launches on that many streams run concurrently; past that, a launch
 // takes the least recently used buffer and makes its stream wait (on the GPU, no host block) for
-// that buffer's last use, unless that use was on the same stream, whose order already implies
-// the wait (the per-thread default stream excepted: one handle, many streams; a destroyed
-// stream's handle is safe to see again since hipStreamDestroy finishes its work first).  A loop
-// of asynchronous launches on one stream thus never allocates nor waits in its steady state.
+// that buffer's last use — always, also when that use was on the same stream (a stream handle
+// can be recycled while work from its previous life is still in flight).
 struct rows_slot {
 	void *p = nullptr;
 	hipEvent_t ev = nullptr;
@@ -133,20 +131,27 @@ rows_acquire(int device, size_t bytes, hipStream_t stream, rows_slot **out)
 	}
 	if (!lru)
 		return ENOMEM; // kRowsMax launches mid-submission on the host at once
-	if ((lru->stream != stream || stream == hipStreamPerThread) &&
-	    hipStreamWaitEvent(stream, lru->ev, 0) != hipSuccess)
+	if (hipStreamWaitEvent(stream, lru->ev, 0) != hipSuccess)
 		return EIO;
 	lru->busy = true;
 	*out = lru;
 	return 0;
 }
 
+// `enqueued`: some kernel of the launch reached the stream (whatever the launch returned), so
+// the buffer's next user must wait for it.  `failed`: the launch stopped part way, so the fault
+// scratch may hold a count the second stage never moved: it is re-zeroed on the same stream; a
+// buffer that cannot be made clean again is left busy (never reused).
 void
-rows_release(rows_slot *r, hipStream_t stream, bool used)
+rows_release(rows_slot *r, hipStream_t stream, bool enqueued, bool failed, size_t rows_bytes)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
-	if (used) {
-		hipEventRecord(r->ev, stream);
+	if (enqueued) {
+		if (failed && hipMemsetAsync(static_cast<char *>(r->p) + rows_bytes, 0, kRowsScratch,
+					     stream) != hipSuccess)
+			return;
+		if (hipEventRecord(r->ev, stream) != hipSuccess)
+			return;
 		r->seq = ++g_rows_seq;
 		r->stream = stream;
 	}
@@ -195,7 +200,10 @@ ensure_translated(struct ebpf_prog *ep)
 	if (ep->xlated)
 		return ep->xlated->error;
 	auto x = std::make_unique<dprog_host>();
+	const auto t0 = std::chrono::steady_clock::now();
 	int err = translate_program(ep, *x);
+	x->translate_ms =
+	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err && x->error == 0)
 		x->error = err;
 	if (!x->error) {
@@ -322,8 +330,11 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	if (dp->jit_err[mode])
 		return dp->jit_err[mode];
 	std::string msg;
+	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
 				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg);
+	dp->build_ms[mode] =
+	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
 		dp->jit_err[mode] = err;
 		return fail(err, msg);
@@ -341,8 +352,11 @@ asm_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	if (dp->asm_err[mode])
 		return dp->asm_err[mode];
 	std::string msg;
+	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_build_entries(dp->device, *ep->xlated, mode, dp->table, &dp->d_asm[mode],
 				    &dp->asm_stride[mode], &msg);
+	dp->build_ms[mode] =
+	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
 		dp->asm_err[mode] = err;
 		return fail(err, msg);
@@ -382,11 +396,14 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.prog = dp->d_asm[mode];
 			L.stack_stride = dp->asm_stride[mode];
 		}
+		dp->last_exec = fn ? EBPF_EXEC_COMPILED : EBPF_EXEC_INTERPRETER;
+		dp->last_layout = mode;
 		L.lds_pkt_base = (mode == 0 && ep->xlated->asm_gstage) ? 0x80000000u : 0;
 		rows_slot *rows = nullptr;
 		unsigned long long *user_hist = L.hist;
+		size_t rows_bytes = 0;
 		if (L.hist) {
-			const size_t rows_bytes = (size_t)asm_max_workgroups(dp->device) * 1024;
+			rows_bytes = (size_t)asm_max_workgroups(dp->device) * 1024;
 			if ((err = rows_acquire(dp->device, rows_bytes, stream, &rows)))
 				return fail(err, "no histogram row buffer");
 			L.hist_rows = static_cast<uint32_t *>(rows->p);
@@ -399,13 +416,16 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		bool probes = false;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
+		bool enqueued = false;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
 				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop, user_hist,
-				      hist_overwrite);
+				      hist_overwrite, &enqueued);
 		if (rows)
-			rows_release(rows, stream, e == hipSuccess);
+			rows_release(rows, stream, enqueued, e != hipSuccess, rows_bytes);
 	} else {
 		L.prog = dp->d_entries;
+		dp->last_exec = EBPF_EXEC_HIP;
+		dp->last_layout = 0;
 		if (hist_overwrite && L.hist &&
 		    (e = hipMemsetAsync(L.hist, 0, EBPF_HIST_BINS * sizeof(uint64_t), stream)) !=
 			hipSuccess)
@@ -580,6 +600,27 @@ ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info)
 }
 
 EBPF_EXPORT int
+ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *info)
+{
+	if (ep == nullptr || info == nullptr)
+		return fail(EINVAL, "NULL argument");
+	std::lock_guard<std::mutex> g(ep->dlock);
+	memset(info, 0, sizeof(*info));
+	info->exec = -1;
+	info->layout = -1;
+	if (ep->xlated)
+		info->translate_ms = ep->xlated->translate_ms;
+	if (device < 0 || device >= (int)ep->dev.size() || !ep->dev[device])
+		return 0;
+	const dprog_device &dp = *ep->dev[device];
+	info->exec = dp.last_exec;
+	info->layout = dp.last_layout;
+	if (dp.last_layout >= 0 && dp.last_exec != EBPF_EXEC_HIP)
+		info->build_ms = dp.build_ms[dp.last_layout];
+	return 0;
+}
+
+EBPF_EXPORT int
 ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 {
 	if (ep == nullptr || len == nullptr || (layout != 0 && layout != 1))
@@ -689,17 +730,26 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 	const uint64_t n = batch->count;
 	// Chunked, double-buffered: chunk k's H2D overlaps chunk k-1's kernel and D2H.
 	const uint64_t chunk = batch->offsets ? (1ull << 20) : (1ull << 22);
-	hipMemsetAsync(S.d_hist, 0, EBPF_HIST_BINS * sizeof(unsigned long long), S.stream[0]);
-	hipStreamSynchronize(S.stream[0]);
+	if ((e = hipMemsetAsync(S.d_hist, 0, EBPF_HIST_BINS * sizeof(unsigned long long),
+				S.stream[0])) != hipSuccess ||
+	    (e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
+		return hip_fail(e, "hipMemsetAsync(hist)");
 	float kernel_ms = 0;
 	bool timed[2] = {false, false};
-	auto collect = [&](int b) {
+	// on any error: drain both streams (buffers stay valid for the copies in flight)
+	auto drain = [&](int rc) {
+		hipStreamSynchronize(S.stream[0]);
+		hipStreamSynchronize(S.stream[1]);
+		return rc;
+	};
+	auto collect = [&](int b) -> hipError_t {
 		if (!timed[b])
-			return;
+			return hipSuccess;
 		float ms = 0;
-		hipEventElapsedTime(&ms, S.ev[2 * b], S.ev[2 * b + 1]);
+		hipError_t te = hipEventElapsedTime(&ms, S.ev[2 * b], S.ev[2 * b + 1]);
 		kernel_ms += ms;
 		timed[b] = false;
+		return te;
 	};
 	for (uint64_t c0 = 0, k = 0; c0 < n; c0 += chunk, k++) {
 		const int b = (int)(k & 1);
@@ -713,21 +763,25 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 			byte0 = c0 * batch->stride;
 			byte1 = (c0 + cn) * batch->stride;
 		}
-		hipStreamSynchronize(st); // buffers of chunk k-2 are free again
-		collect(b);
+		// buffers of chunk k-2 are free again
+		if ((e = hipStreamSynchronize(st)) != hipSuccess || (e = collect(b)) != hipSuccess)
+			return drain(hip_fail(e, "batch chunk"));
 		if ((err = stage_alloc(&S.d_data[b], &S.data_cap[b], byte1 - byte0 + 16)))
-			return err;
+			return drain(err);
 		const size_t small = cn * 9 + (batch->offsets ? (cn + 1) * 8 : 0) + 64;
 		if ((err = stage_alloc(&S.d_small[b], &S.small_cap[b], small)))
-			return err;
+			return drain(err);
 		uint8_t *sm = static_cast<uint8_t *>(S.d_small[b]);
 		uint64_t *d_ret = reinterpret_cast<uint64_t *>(sm);
 		uint64_t *d_offs = batch->offsets ? reinterpret_cast<uint64_t *>(sm + cn * 8) : nullptr;
 		uint8_t *d_faults = sm + cn * 8 + (batch->offsets ? (cn + 1) * 8 : 0);
 		const uint8_t *src = static_cast<const uint8_t *>(batch->data) + byte0;
-		hipMemcpyAsync(S.d_data[b], src, byte1 - byte0, hipMemcpyHostToDevice, st);
-		if (d_offs)
-			hipMemcpyAsync(d_offs, batch->offsets + c0, (cn + 1) * 8, hipMemcpyHostToDevice, st);
+		if ((e = hipMemcpyAsync(S.d_data[b], src, byte1 - byte0, hipMemcpyHostToDevice, st)) !=
+		    hipSuccess)
+			return drain(hip_fail(e, "hipMemcpyAsync(packets H2D)"));
+		if (d_offs && (e = hipMemcpyAsync(d_offs, batch->offsets + c0, (cn + 1) * 8,
+						  hipMemcpyHostToDevice, st)) != hipSuccess)
+			return drain(hip_fail(e, "hipMemcpyAsync(offsets H2D)"));
 		dp_launch L;
 		memset(&L, 0, sizeof(L));
 		L.data = static_cast<uint8_t *>(S.d_data[b]);
@@ -738,28 +792,31 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 		L.hist = S.d_hist;
 		L.count = cn;
 		L.stride = batch->stride;
-		hipEventRecord(S.ev[2 * b], st);
+		if ((e = hipEventRecord(S.ev[2 * b], st)) != hipSuccess)
+			return drain(hip_fail(e, "hipEventRecord"));
 		if ((err = launch(ep, dp, L, st)))
-			return err;
-		hipEventRecord(S.ev[2 * b + 1], st);
-		hipMemcpyAsync(ret + c0, d_ret, cn * 8, hipMemcpyDeviceToHost, st);
-		if (faults)
-			hipMemcpyAsync(faults + c0, d_faults, cn, hipMemcpyDeviceToHost, st);
-		if (copy_back)
-			hipMemcpyAsync(const_cast<uint8_t *>(src), S.d_data[b], byte1 - byte0,
-				       hipMemcpyDeviceToHost, st);
+			return drain(err);
+		if ((e = hipEventRecord(S.ev[2 * b + 1], st)) != hipSuccess)
+			return drain(hip_fail(e, "hipEventRecord"));
 		timed[b] = true;
+		if ((e = hipMemcpyAsync(ret + c0, d_ret, cn * 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
+			return drain(hip_fail(e, "hipMemcpyAsync(results D2H)"));
+		if (faults && (e = hipMemcpyAsync(faults + c0, d_faults, cn, hipMemcpyDeviceToHost, st)) !=
+				  hipSuccess)
+			return drain(hip_fail(e, "hipMemcpyAsync(faults D2H)"));
+		if (copy_back && (e = hipMemcpyAsync(const_cast<uint8_t *>(src), S.d_data[b],
+						     byte1 - byte0, hipMemcpyDeviceToHost, st)) !=
+				     hipSuccess)
+			return drain(hip_fail(e, "hipMemcpyAsync(packets D2H)"));
 	}
 	for (int i = 0; i < 2; i++) {
-		hipStreamSynchronize(S.stream[i]);
-		collect(i);
+		if ((e = hipStreamSynchronize(S.stream[i])) != hipSuccess || (e = collect(i)) != hipSuccess)
+			return drain(hip_fail(e, "batch"));
 	}
-	e = hipGetLastError();
-	if (e != hipSuccess)
-		return hip_fail(e, "batch");
+	unsigned long long h[EBPF_HIST_BINS];
+	if (stats && (e = hipMemcpy(h, S.d_hist, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess)
+		return hip_fail(e, "hipMemcpy(hist)");
 	if (stats) {
-		unsigned long long h[EBPF_HIST_BINS];
-		hipMemcpy(h, S.d_hist, sizeof(h), hipMemcpyDeviceToHost);
 		stats->packets = n;
 		stats->faulted = h[256];
 		for (int i = 0; i < EBPF_HIST_BINS; i++)

@@ -118,6 +118,9 @@ struct dprog_device {
 	void *jit_fn[2] = {nullptr, nullptr};    // its kernel
 	uint32_t jit_stride[2] = {0, 0};
 	int jit_err[2] = {0, 0};                 // E2BIG etc.: run the interpreter instead
+	double build_ms[2] = {0, 0};             // compile (variant 0) or lower + link time, per mode
+	int last_exec = -1;                      // ebpf_dexec_info.exec of the last launch
+	int last_layout = -1;                    // its mode
 };
 
 // Abstract value of a register (pointer provenance), computed by translate.cpp's dataflow pass
@@ -152,6 +155,7 @@ struct dprog_host {
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
 	uint32_t max_stack = 0;
+	double translate_ms = 0;             // host time of translate_program
 	int error = 0;
 	std::string error_msg;
 };

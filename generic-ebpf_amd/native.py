@@ -68,6 +68,14 @@ class BatchStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double)]
 
 
+class DexecInfo(ctypes.Structure):
+    _fields_ = [("exec", ctypes.c_int32), ("layout", ctypes.c_int32),
+                ("translate_ms", ctypes.c_double), ("build_ms", ctypes.c_double)]
+
+
+EXEC_NAMES = {0: "compiled", 1: "hip", 2: "interpreter"}
+
+
 class DprogInfo(ctypes.Structure):
     _fields_ = [("nslots", ctypes.c_uint32), ("nentries", ctypes.c_uint32),
                 ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
@@ -96,6 +104,7 @@ FUNCS = {
     "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_device_info": (_I, [_VP, _VP]),
+    "ebpf_prog_device_exec": (_I, [_VP, _I, _VP]),
     "ebpf_prog_device_code": (_I, [_VP, _I, _VP, ctypes.POINTER(ctypes.c_size_t)]),
     "ebpf_prog_set_semantics": (_I, [_VP, _I]),
 }
@@ -283,6 +292,14 @@ class Prog:
         _check(lib().ebpf_prog_device_info(self.ptr, ctypes.byref(i)), "ebpf_prog_device_info")
         return i
 
+    def exec_info(self, device=0):
+        """What the last launch on ``device`` ran (ebpf_prog_device_exec): (exec name or None,
+        layout, translate ms, build ms)."""
+        i = DexecInfo()
+        _check(lib().ebpf_prog_device_exec(self.ptr, device, ctypes.byref(i)),
+               "ebpf_prog_device_exec")
+        return EXEC_NAMES.get(i.exec), i.layout, i.translate_ms, i.build_ms
+
     def set_semantics(self, semantics):
         """SEM_REFERENCE (default) or SEM_STANDARD (ebpf_gpu.h ebpf_prog_set_semantics)."""
         _check(lib().ebpf_prog_set_semantics(self.ptr, semantics), "ebpf_prog_set_semantics")
@@ -329,6 +346,25 @@ class Prog:
         _check(lib().ebpf_prog_run_batch_dev(self.ptr, device, ctypes.byref(b), ret_ptr,
                                              faults_ptr, hist_ptr, stream),
                "ebpf_prog_run_batch_dev")
+
+
+    def launcher(self, device, data_ptr, count, stride, ret_ptr, offsets_ptr=None,
+                 faults_ptr=None, stream=None, hist_overwrite=False):
+        """A prebound ebpf_prog_run_batch_dev for a bench loop: returns ``launch(hist_ptr)``
+        whose only per-call work is the C call itself (batch descriptor and argument
+        conversion done once here).  Raises EbpfError on a non-zero return."""
+        b = PktBatch(data_ptr, offsets_ptr, count, stride,
+                     BATCH_HIST_OVERWRITE if hist_overwrite else 0)
+        f = lib().ebpf_prog_run_batch_dev
+        args = (self.ptr, device, ctypes.byref(b), ret_ptr, faults_ptr)
+        st = stream
+
+        def launch(hist_ptr):
+            rc = f(*args, hist_ptr, st)
+            if rc:
+                raise EbpfError(rc, "ebpf_prog_run_batch_dev")
+        launch.batch = b  # keeps the descriptor alive with the closure
+        return launch
 
 
 def gpu_count():

@@ -95,6 +95,29 @@ def packets_imix(n, seed=5):
     return data, offsets, sizes
 
 
+IMIX_BLOCK = 1 << 16
+
+
+def packets_imix_range(lo, hi, seed=5):
+    """Packets [lo, hi) of an endless IMIX stream generated in blocks of IMIX_BLOCK packets
+    (block b from seed (seed, b)), so that any shard of a batch is reproducible on its own:
+    the shards of [0, n) concatenate to the packets of [0, n) whatever the shard count.
+    Returns (data, offsets rebased to 0, sizes) as packets_imix."""
+    parts, sizes = [], []
+    for b in range(lo // IMIX_BLOCK, (hi + IMIX_BLOCK - 1) // IMIX_BLOCK):
+        d, o, s = packets_imix(IMIX_BLOCK, seed=(seed, b))
+        a = max(lo, b * IMIX_BLOCK) - b * IMIX_BLOCK
+        e = min(hi, (b + 1) * IMIX_BLOCK) - b * IMIX_BLOCK
+        parts.append(d[int(o[a]):int(o[e])])
+        sizes.append(s[a:e])
+    sizes = np.concatenate(sizes) if sizes else np.zeros(0, np.uint32)
+    padded = ((sizes.astype(np.uint64) + 63) // 64) * 64
+    offsets = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    np.cumsum(padded, out=offsets[1:])
+    data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return data, offsets, sizes
+
+
 # --------------------------------------------------------------------------- programs
 
 def prog_c2():

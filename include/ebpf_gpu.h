@@ -140,6 +140,20 @@ struct ebpf_dprog_info {
 };
 int ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info);
 
+/* What ran, and what it cost to get there (extension; measurement and diagnostics). */
+#define EBPF_EXEC_COMPILED 0     /* the program compiled to gfx950 code (variant 0) */
+#define EBPF_EXEC_HIP 1          /* the portable HIP interpreter (variant 1) */
+#define EBPF_EXEC_INTERPRETER 2  /* the gfx950 assembly interpreter (variant 2, or variant 0 on a
+                                    program too large for the code area) */
+struct ebpf_dexec_info {
+	int32_t exec;          /* EBPF_EXEC_* of the last launch on `device`; -1 = none yet */
+	int32_t layout;        /* its kernel: 1 = staged fixed 64-B packets, 0 = general; -1 = none */
+	double translate_ms;   /* host time of the state-tree translation (once per program) */
+	double build_ms;       /* compile (COMPILED) or lower + link (INTERPRETER) time for that
+	                          kernel on that device, paid at its first launch; 0 for HIP */
+};
+int ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *info);
+
 /* Diagnostics: the program as compiled for variant 0, raw gfx950 instruction bytes, for packet
  * `layout` 1 (fixed 64-B packets) or 0 (any stride / offsets).  Host only (no GPU needed; map
  * base addresses are then 0).  *len: in = size of buf, out = bytes of code.  buf == NULL just

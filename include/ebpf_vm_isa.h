@@ -7,10 +7,10 @@
  *   - class / source / size / mode / ALU-op / JMP-op fields ↔ :46-105
  *   - EBPF_OP_* opcode values   ↔ :145-238 (90 opcodes dispatched by ebpf_interpreter.c:40-369)
  *
+ *   - construction macros       ↔ :107-143, bug for bug (see the block comment there)
+ *
  * Every opcode below is spelled out as its final byte value so the table doubles as the
- * device decoder's reference.  The reference's convenience macros (EBPF_ALU_IMM, EBPF_STX,
- * EBPF_LDDW, ... at :107-143) are intentionally not provided: several of them do not compile
- * or encode the wrong class ("ISA definitions").
+ * device decoder's reference.
  */
 #ifndef EBPF_AMD_VM_ISA_H
 #define EBPF_AMD_VM_ISA_H
@@ -98,6 +98,57 @@ enum ebpf_registers {
 #define EBPF_JLE  0xb0
 #define EBPF_JSLT 0xc0
 #define EBPF_JSLE 0xd0
+
+/* ---- instruction construction macros (sys/sys/ebpf_vm_isa.h:107-143) ----
+ * Brace initializers for struct ebpf_inst {opcode, dst, src, offset, imm}.  They reproduce the
+ * reference's encodings exactly, defects included, so that a program built with them means the
+ * same bytes against either header:
+ *   - EBPF_ALU_REG / EBPF_ALU64_REG set the IMMEDIATE source bit (SRC_IMM, :109-110, :113-114):
+ *     the instruction executes as "dst op imm" with imm = 0, src only recorded in the byte;
+ *   - EBPF_LD / EBPF_LDX / EBPF_ST / EBPF_STX name EBPF_SRC_MEM, which neither header defines,
+ *     and EBPF_STX would encode class ST (:119-126);
+ *   - EBPF_LDDW names the undefined EBPF_DW (:127-129);
+ *   - EBPF_PSEUDO_MAP_LD has no comma between its two initializers (:130-133);
+ *   - EBPF_JMP_JA puts a variable named `imm` into the offset field and ignores `ofs` (:134-135).
+ * The ones the reference can compile compile here to the same bytes
+ * (tests/test_isa_macros.py builds a program with them and runs it). */
+#define EBPF_ALU_IMM(op, dst, imm) \
+	{ (EBPF_CLS_ALU | EBPF_SRC_IMM | op), dst, 0, 0, imm }
+#define EBPF_ALU_REG(op, dst, src) \
+	{ (EBPF_CLS_ALU | EBPF_SRC_IMM | op), dst, src, 0, 0 }
+#define EBPF_ALU64_IMM(op, dst, imm) \
+	{ (EBPF_CLS_ALU64 | EBPF_SRC_IMM | op), dst, 0, 0, imm }
+#define EBPF_ALU64_REG(op, dst, src) \
+	{ (EBPF_CLS_ALU64 | EBPF_SRC_IMM | op), dst, src, 0, 0 }
+#define EBPF_LE(dst, size) \
+	{ (EBPF_CLS_ALU | EBPF_TO_LE | EBPF_END), dst, 0, 0, size }
+#define EBPF_BE(dst, size) \
+	{ (EBPF_CLS_ALU | EBPF_TO_BE | EBPF_END), dst, 0, 0, size }
+#define EBPF_LD(size, dst, src, ofs) \
+	{ (EBPF_CLS_LD | EBPF_SRC_MEM | size), dst, src, ofs, 0 }
+#define EBPF_LDX(size, dst, src, ofs) \
+	{ (EBPF_CLS_LDX | EBPF_SRC_MEM | size), dst, src, ofs, 0 }
+#define EBPF_ST(size, dst, src, ofs) \
+	{ (EBPF_CLS_ST | EBPF_SRC_MEM | size), dst, src, ofs, 0 }
+#define EBPF_STX(size, dst, src, ofs) \
+	{ (EBPF_CLS_ST | EBPF_SRC_MEM | size), dst, src, ofs, 0 }
+#define EBPF_LDDW(dst, imm) \
+	{ (EBPF_CLS_LD | EBPF_SRC_IMM | EBPF_DW), dst, 0, 0, (uint32_t)imm }, \
+	{ 0, 0, 0, 0, ((uint64_t)imm) >> 32 }
+#define EBPF_PSEUDO_MAP_LD(dst, imm) \
+	{ (EBPF_CLS_LD | EBPF_SRC_IMM | EBPF_DW), dst, \
+		EBPF_PSEUDO_MAP_DESC, 0, (uint32_t)imm } \
+	{ 0, 0, 0, 0, 0 }
+#define EBPF_JMP_JA(ofs) \
+	{ (EBPF_CLS_JMP | EBPF_JA ), 0, 0, imm, 0 }
+#define EBPF_JMP_IMM(op, dst, ofs, imm) \
+	{ (EBPF_CLS_JMP | EBPF_SRC_IMM | op), dst, 0, ofs, imm }
+#define EBPF_JMP_REG(op, dst, src, ofs) \
+	{ (EBPF_CLS_JMP | EBPF_SRC_REG | op), dst, src, ofs, 0 }
+#define EBPF_JMP_CALL(id) \
+	{ (EBPF_CLS_JMP | EBPF_CALL), 0, 0, 0, id }
+#define EBPF_JMP_EXIT \
+	{ (EBPF_CLS_JMP | EBPF_EXIT), 0, 0, 0, 0 }
 
 /* ---- the 90 opcodes the reference interpreter dispatches (ebpf_interpreter.c:41-366) ---- */
 /* ALU (32-bit) */

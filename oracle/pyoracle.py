@@ -151,6 +151,17 @@ class OracleProgram:
                                        nthreads)
         return ret, faults, work, int(steps)
 
+    def run_inplace(self, data, count, stride, offsets, ret, faults=None, nthreads=1):
+        """Timed form for bench.py's cpu_baseline: runs on ``data`` itself (packet stores land
+        in it) into caller-preallocated ``ret`` (u64[count]) / ``faults`` (u8[count] or None);
+        no copy, no allocation.  ``offsets`` must already be a contiguous u64 array or None.
+        Returns the executed-instruction count."""
+        return int(lib().oracle_run_batch(ctypes.addressof(self.p), data.ctypes.data,
+                                          None if offsets is None else offsets.ctypes.data,
+                                          count, stride, ret.ctypes.data,
+                                          None if faults is None else faults.ctypes.data,
+                                          nthreads))
+
 
 # ---- hashtable maps (host-side map API; small cases, pure Python) ----
 

@@ -331,3 +331,79 @@ def test_general_kernels_header_staging(gpu, env, variant):
             if not (np.array_equal(want, got) and np.array_equal(wf, gf) and np.array_equal(wd, gd)):
                 bad.append((i, stride, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("cfg", ["c4", "c3"])
+def test_one_launch_full_size_overwrite(gpu, env, cfg):
+    """The launch bench.py times: ONE device-resident ebpf_prog_run_batch_dev over the full
+    BASELINE batch (C4: 64M x 64 B = 4 GiB; C3: 16M) with EBPF_BATCH_HIST_OVERWRITE on a
+    garbage-filled histogram.  Every packet's result must equal the oracle's for the distinct
+    packet it tiles (4M distinct packets, the bench's tiling), and the histogram the tiled
+    oracle histogram."""
+    import torch
+    from generic_ebpf_amd import workloads
+    D = 1 << 22
+    n = {"c4": 1 << 26, "c3": 1 << 24}[cfg]
+    lay = workloads.CONFIGS[cfg]["prog"]()
+    pk = workloads.packets_l2l3(D, 64)
+    maps_spec = [(8, 256, workloads.c4_map_values().tobytes())] if cfg == "c4" else []
+    base = goldens.Case(cfg, lay.code, lay.relocs, maps_spec, pk, D, 64, None)
+    want, wf, _, _ = oracle_run(base, nthreads=16)
+    assert not wf.any()
+    maps = make_maps(gpu, env, base)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev).repeat(n // D)
+        d_ret = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        d_hist = torch.full((257,), 987654321, dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, None,
+                        d_hist.data_ptr(), st, hist_overwrite=True)
+        torch.cuda.synchronize()
+        wt = torch.from_numpy(want.view(np.int64)).to(dev)
+        bad = int((d_ret.view(n // D, D) != wt.unsqueeze(0)).sum())
+        assert bad == 0, "%d of %d packets differ from the oracle" % (bad, n)
+        h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257) * (n // D)
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+def test_many_streams_separate_histograms(gpu, env):
+    """More concurrent streams (8) than the library's 4 pooled histogram row buffers, each
+    launching into its own histogram with no synchronisation between launches: the row buffers
+    are handed across streams with GPU-side waits, and every histogram must come out exact."""
+    import torch
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4()
+    n = 1 << 20
+    pk = workloads.packets_l2l3(n, 64, seed=41)
+    vals = workloads.c4_map_values()
+    case = goldens.Case("c4", lay.code, lay.relocs, [(8, 256, vals.tobytes())], pk, n, 64, None)
+    want, _, _, _ = oracle_run(case, nthreads=8)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        nst, rounds = 8, 6
+        streams = [torch.cuda.Stream() for _ in range(nst)]
+        rets = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(nst)]
+        hists = [torch.zeros(257, dtype=torch.int64, device=dev) for _ in range(nst)]
+        torch.cuda.synchronize()
+        for r in range(rounds):
+            for s, d_ret, h in zip(streams, rets, hists):
+                p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, None,
+                                h.data_ptr(), s.cuda_stream, hist_overwrite=(r == 0))
+        torch.cuda.synchronize()
+        exp = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257) * rounds
+        for d_ret, h in zip(rets, hists):
+            np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+            np.testing.assert_array_equal(h.cpu().numpy(), exp)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
