@@ -8,8 +8,10 @@
 // executes eBPF on the CPU — without a GPU the entry points return ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <thread>
 
 #include "internal.h"
 
@@ -454,7 +456,8 @@ validate_batch(const struct ebpf_pkt_batch *b, uint32_t allowed_flags = 0)
 	return 0;
 }
 
-// Per-thread staging for the host-buffer entry point.
+// Staging buffers of the host-buffer entry points: per device, a pool of sets (two streams, two
+// chunk buffers, a histogram), one set per call in flight on that device, reused across calls.
 struct staging {
 	int device = -1;
 	hipStream_t stream[2] = {nullptr, nullptr};
@@ -464,9 +467,44 @@ struct staging {
 	void *d_small[2] = {nullptr, nullptr}; // ret | faults | offsets, per chunk
 	size_t small_cap[2] = {0, 0};
 	unsigned long long *d_hist = nullptr;
-	~staging() {}
 };
-thread_local staging t_stage;
+std::mutex g_stage_lock;
+std::vector<std::vector<staging *>> g_stage_free; // per device
+
+int
+staging_acquire(int device, staging **out)
+{
+	{
+		std::lock_guard<std::mutex> g(g_stage_lock);
+		if ((int)g_stage_free.size() <= device)
+			g_stage_free.resize(device + 1);
+		if (!g_stage_free[device].empty()) {
+			*out = g_stage_free[device].back();
+			g_stage_free[device].pop_back();
+			return 0;
+		}
+	}
+	auto S = std::make_unique<staging>();
+	S->device = device;
+	hipError_t e = hipSetDevice(device);
+	for (int i = 0; i < 2 && e == hipSuccess; i++)
+		e = hipStreamCreateWithFlags(&S->stream[i], hipStreamNonBlocking);
+	for (int i = 0; i < 4 && e == hipSuccess; i++)
+		e = hipEventCreate(&S->ev[i]);
+	if (e == hipSuccess)
+		e = hipMalloc(&S->d_hist, EBPF_HIST_BINS * sizeof(unsigned long long));
+	if (e != hipSuccess)
+		return hip_fail(e, "staging set-up"); // (a set that failed half way is not pooled)
+	*out = S.release();
+	return 0;
+}
+
+void
+staging_release(staging *S)
+{
+	std::lock_guard<std::mutex> g(g_stage_lock);
+	g_stage_free[S->device].push_back(S);
+}
 
 int
 stage_alloc(void **p, size_t *cap, size_t need)
@@ -695,46 +733,28 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	return launch(ep, dp, L, static_cast<hipStream_t>(stream), ev_start, ev_stop, overwrite);
 }
 
-EBPF_EXPORT int
-ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, uint64_t *ret,
-		    uint8_t *faults, struct ebpf_batch_stats *stats)
+namespace {
+
+// Packets [lo, hi) of a host-buffer batch on `device` with staging set S: chunked,
+// double-buffered H2D -> kernel -> D2H on S's two streams.  Results go to ret[lo..hi) (and
+// faults[lo..hi)); the shard's verdict histogram is left in S.d_hist (zeroed first) and the
+// interpreter kernels' device time is added to *kernel_ms.  Synchronous.
+int
+run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
+	       const struct ebpf_pkt_batch *batch, uint64_t lo, uint64_t hi, uint64_t *ret,
+	       uint8_t *faults, double *kernel_ms)
 {
-	if (ep == nullptr || ret == nullptr)
-		return fail(EINVAL, "prog or ret is NULL");
-	int err = validate_batch(batch);
-	if (err)
-		return err;
-	auto t0 = std::chrono::steady_clock::now();
-	const int device = t_dev;
-	dprog_device *dp;
-	err = prepare(ep, device, &dp);
-	if (err)
-		return err;
-	staging &S = t_stage;
-	hipError_t e = hipSetDevice(device);
+	hipError_t e = hipSetDevice(S.device);
 	if (e != hipSuccess)
 		return hip_fail(e, "hipSetDevice");
-	if (S.device != device) {
-		for (int i = 0; i < 2; i++) {
-			if (hipStreamCreateWithFlags(&S.stream[i], hipStreamNonBlocking) != hipSuccess)
-				return fail(EIO, "hipStreamCreate");
-		}
-		for (auto &ev : S.ev)
-			if (hipEventCreate(&ev) != hipSuccess)
-				return fail(EIO, "hipEventCreate");
-		if (hipMalloc(&S.d_hist, EBPF_HIST_BINS * sizeof(unsigned long long)) != hipSuccess)
-			return fail(ENOMEM, "hipMalloc(hist)");
-		S.device = device;
-	}
 	const bool copy_back = ep->xlated->writes_memory;
-	const uint64_t n = batch->count;
 	// Chunked, double-buffered: chunk k's H2D overlaps chunk k-1's kernel and D2H.
 	const uint64_t chunk = batch->offsets ? (1ull << 20) : (1ull << 22);
 	if ((e = hipMemsetAsync(S.d_hist, 0, EBPF_HIST_BINS * sizeof(unsigned long long),
 				S.stream[0])) != hipSuccess ||
 	    (e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
 		return hip_fail(e, "hipMemsetAsync(hist)");
-	float kernel_ms = 0;
+	int err;
 	bool timed[2] = {false, false};
 	// on any error: drain both streams (buffers stay valid for the copies in flight)
 	auto drain = [&](int rc) {
@@ -747,14 +767,14 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 			return hipSuccess;
 		float ms = 0;
 		hipError_t te = hipEventElapsedTime(&ms, S.ev[2 * b], S.ev[2 * b + 1]);
-		kernel_ms += ms;
+		*kernel_ms += ms;
 		timed[b] = false;
 		return te;
 	};
-	for (uint64_t c0 = 0, k = 0; c0 < n; c0 += chunk, k++) {
+	for (uint64_t c0 = lo, k = 0; c0 < hi; c0 += chunk, k++) {
 		const int b = (int)(k & 1);
 		hipStream_t st = S.stream[b];
-		const uint64_t cn = (n - c0 < chunk) ? n - c0 : chunk;
+		const uint64_t cn = (hi - c0 < chunk) ? hi - c0 : chunk;
 		uint64_t byte0, byte1;
 		if (batch->offsets) {
 			byte0 = batch->offsets[c0];
@@ -813,17 +833,157 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 		if ((e = hipStreamSynchronize(S.stream[i])) != hipSuccess || (e = collect(i)) != hipSuccess)
 			return drain(hip_fail(e, "batch"));
 	}
-	unsigned long long h[EBPF_HIST_BINS];
-	if (stats && (e = hipMemcpy(h, S.d_hist, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess)
-		return hip_fail(e, "hipMemcpy(hist)");
-	if (stats) {
-		stats->packets = n;
-		stats->faulted = h[256];
-		for (int i = 0; i < EBPF_HIST_BINS; i++)
-			stats->hist[i] = h[i];
-		stats->kernel_ms = kernel_ms;
-		stats->total_ms =
-		    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	return 0;
+}
+
+int
+fill_stats(struct ebpf_batch_stats *stats, uint64_t n, const unsigned long long *h, double kernel_ms,
+	   std::chrono::steady_clock::time_point t0)
+{
+	stats->packets = n;
+	stats->faulted = h[256];
+	for (int i = 0; i < EBPF_HIST_BINS; i++)
+		stats->hist[i] = h[i];
+	stats->kernel_ms = kernel_ms;
+	stats->total_ms =
+	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	return 0;
+}
+
+int
+check_devices(int ndev, const int *devices, bool distinct)
+{
+	if (ndev < 1 || devices == nullptr)
+		return fail(EINVAL, "ndev < 1 or devices is NULL");
+	const int have = device_count();
+	for (int d = 0; d < ndev; d++) {
+		if (devices[d] < 0 || devices[d] >= have)
+			return fail(ENODEV, "no such GPU device");
+		for (int d2 = 0; distinct && d2 < d; d2++)
+			if (devices[d2] == devices[d])
+				return fail(EINVAL, "a device appears twice in the list");
 	}
+	return 0;
+}
+
+} // namespace (host-buffer helpers)
+
+int rccl_hist_allreduce(int ndev, const int *devices, uint64_t *const *hist, hipStream_t *streams,
+			std::string *msg);
+
+EBPF_EXPORT int
+ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, uint64_t *ret,
+		    uint8_t *faults, struct ebpf_batch_stats *stats)
+{
+	if (ep == nullptr || ret == nullptr)
+		return fail(EINVAL, "prog or ret is NULL");
+	int err = validate_batch(batch);
+	if (err)
+		return err;
+	auto t0 = std::chrono::steady_clock::now();
+	const int device = t_dev;
+	dprog_device *dp;
+	if ((err = prepare(ep, device, &dp)))
+		return err;
+	staging *S;
+	if ((err = staging_acquire(device, &S)))
+		return err;
+	double kernel_ms = 0;
+	err = run_host_shard(ep, dp, *S, batch, 0, batch->count, ret, faults, &kernel_ms);
+	unsigned long long h[EBPF_HIST_BINS];
+	hipError_t e;
+	if (!err && stats &&
+	    (e = hipMemcpy(h, S->d_hist, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess)
+		err = hip_fail(e, "hipMemcpy(hist)");
+	staging_release(S);
+	if (!err && stats)
+		fill_stats(stats, batch->count, h, kernel_ms, t0);
+	return err;
+}
+
+EBPF_EXPORT int
+ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
+			  const struct ebpf_pkt_batch *batch, uint64_t *ret, uint8_t *faults,
+			  struct ebpf_batch_stats *stats)
+{
+	if (ep == nullptr || ret == nullptr)
+		return fail(EINVAL, "prog or ret is NULL");
+	int err = validate_batch(batch);
+	if (err || (err = check_devices(ndev, devices, false)))
+		return err;
+	auto t0 = std::chrono::steady_clock::now();
+	std::vector<dprog_device *> dps(ndev);
+	std::vector<staging *> S(ndev, nullptr);
+	for (int d = 0; d < ndev && !err; d++)
+		if (!(err = prepare(ep, devices[d], &dps[d])))
+			err = staging_acquire(devices[d], &S[d]);
+	std::vector<int> rc(ndev, 0);
+	std::vector<std::string> msg(ndev);
+	std::vector<double> kms(ndev, 0.0);
+	std::vector<unsigned long long> h((size_t)ndev * EBPF_HIST_BINS, 0);
+	if (!err) {
+		// one host thread per shard: contiguous shards [d*n/N, (d+1)*n/N) (shard.shard_bounds)
+		std::vector<std::thread> th;
+		const uint64_t n = batch->count, base = n / ndev, extra = n % ndev;
+		for (int d = 0; d < ndev; d++) {
+			const uint64_t lo = d * base + std::min<uint64_t>(d, extra);
+			const uint64_t hi = lo + base + ((uint64_t)d < extra ? 1 : 0);
+			th.emplace_back([&, d, lo, hi] {
+				rc[d] = run_host_shard(ep, dps[d], *S[d], batch, lo, hi, ret, faults, &kms[d]);
+				hipError_t e;
+				if (!rc[d] && (e = hipMemcpy(&h[(size_t)d * EBPF_HIST_BINS], S[d]->d_hist,
+							     EBPF_HIST_BINS * 8, hipMemcpyDeviceToHost)) !=
+						  hipSuccess)
+					rc[d] = hip_fail(e, "hipMemcpy(hist)");
+				msg[d] = t_err;
+			});
+		}
+		for (auto &t : th)
+			t.join();
+		for (int d = 0; d < ndev && !err; d++)
+			if ((err = rc[d]))
+				fail(err, msg[d]);
+	}
+	for (staging *s : S)
+		if (s)
+			staging_release(s);
+	if (err || !stats)
+		return err;
+	// the results came back over PCIe anyway: the per-shard histograms are summed here
+	unsigned long long sum[EBPF_HIST_BINS] = {0};
+	double kmax = 0;
+	for (int d = 0; d < ndev; d++) {
+		for (int i = 0; i < EBPF_HIST_BINS; i++)
+			sum[i] += h[(size_t)d * EBPF_HIST_BINS + i];
+		kmax = std::max(kmax, kms[d]);
+	}
+	return fill_stats(stats, batch->count, sum, kmax, t0);
+}
+
+EBPF_EXPORT int
+ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices,
+			      const struct ebpf_pkt_batch *shards, uint64_t *const *ret_dev,
+			      uint8_t *const *faults_dev, uint64_t *const *hist_dev,
+			      void *const *streams)
+{
+	if (ep == nullptr || shards == nullptr || ret_dev == nullptr)
+		return fail(EINVAL, "prog, shards or ret_dev is NULL");
+	int err = check_devices(ndev, devices, true);
+	if (err)
+		return err;
+	std::vector<hipStream_t> st(ndev);
+	for (int d = 0; d < ndev; d++) {
+		st[d] = streams ? static_cast<hipStream_t>(streams[d]) : nullptr;
+		if ((err = ebpf_prog_run_batch_dev(ep, devices[d], &shards[d], ret_dev[d],
+						   faults_dev ? faults_dev[d] : nullptr,
+						   hist_dev ? hist_dev[d] : nullptr, st[d])))
+			return err;
+	}
+	const char *force = getenv("EBPF_FORCE_RCCL"); // (tests: the collective on one GPU)
+	if (hist_dev == nullptr || (ndev == 1 && !(force && *force == '1')))
+		return 0;
+	std::string msg;
+	if ((err = rccl_hist_allreduce(ndev, devices, hist_dev, st.data(), &msg)))
+		return fail(err, msg);
 	return 0;
 }

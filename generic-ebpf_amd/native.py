@@ -103,6 +103,8 @@ FUNCS = {
     "ebpf_prog_prepare_device": (_I, [_VP, _I]),
     "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_run_batch_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
+    "ebpf_prog_run_batch_multi": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP]),
+    "ebpf_prog_run_batch_multi_dev": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP]),
     "ebpf_prog_device_info": (_I, [_VP, _VP]),
     "ebpf_prog_device_exec": (_I, [_VP, _I, _VP]),
     "ebpf_prog_device_code": (_I, [_VP, _I, _VP, ctypes.POINTER(ctypes.c_size_t)]),
@@ -326,6 +328,37 @@ class Prog:
                                          None if faults is None else faults.ctypes.data,
                                          ctypes.byref(st)), "ebpf_prog_run_batch")
         return ret, faults, st
+
+    def run_batch_multi(self, devices, data, count, stride=0, offsets=None, want_faults=True):
+        """ebpf_prog_run_batch_multi: host buffers sharded over ``devices`` (a list of device
+        indices, repeats allowed).  Returns (ret, faults, stats) like run_batch."""
+        assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
+        ret = np.zeros(count, dtype=np.uint64)
+        faults = np.zeros(count, dtype=np.uint8) if want_faults else None
+        offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        b = PktBatch(data.ctypes.data, None if offs is None else offs.ctypes.data, count,
+                     stride, 0)
+        devs = (ctypes.c_int * len(devices))(*devices)
+        st = BatchStats()
+        _check(lib().ebpf_prog_run_batch_multi(self.ptr, len(devices), devs, ctypes.byref(b),
+                                               ret.ctypes.data,
+                                               None if faults is None else faults.ctypes.data,
+                                               ctypes.byref(st)), "ebpf_prog_run_batch_multi")
+        return ret, faults, st
+
+    def run_batch_multi_dev(self, devices, shards, rets, faults=None, hists=None, streams=None,
+                            hist_overwrite=False):
+        """ebpf_prog_run_batch_multi_dev.  ``shards``: [(data_ptr, count, stride, offsets_ptr)]
+        per device; ``rets`` / ``faults`` / ``hists`` / ``streams``: per-device pointers (ints)."""
+        n = len(devices)
+        arr = (PktBatch * n)()
+        for d, (dp, cnt, stride, op) in enumerate(shards):
+            arr[d] = PktBatch(dp, op, cnt, stride, BATCH_HIST_OVERWRITE if hist_overwrite else 0)
+        P = ctypes.c_void_p * n
+        _check(lib().ebpf_prog_run_batch_multi_dev(
+            self.ptr, n, (ctypes.c_int * n)(*devices), arr, P(*rets),
+            None if faults is None else P(*faults), None if hists is None else P(*hists),
+            None if streams is None else P(*streams)), "ebpf_prog_run_batch_multi_dev")
 
     def device_code(self, layout=1):
         """The program compiled for variant 0 (raw gfx950 code bytes); works without a GPU."""

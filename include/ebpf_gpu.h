@@ -98,6 +98,29 @@ int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_
 			    uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev,
 			    void *stream);
 
+/* One batch sharded over several GPUs of this process (packets are independent,
+ * maps are read-only during a batch, so the batch splits into contiguous shards
+ * [d*n/N, (d+1)*n/N) with no data exchange; bytecode and map mirrors are replicated per device).
+ *
+ * ebpf_prog_run_batch_multi: host buffers, as ebpf_prog_run_batch; one host thread per device
+ *   runs its shard's chunked H2D -> kernel -> D2H pipeline.  `devices` may repeat a device (two
+ *   shards then share it).  stats->hist is the sum of the shards' histograms, stats->kernel_ms
+ *   the slowest shard's device time.
+ * ebpf_prog_run_batch_multi_dev: device-resident, asynchronous: shards[d], ret_dev[d],
+ *   faults_dev[d] (optional), hist_dev[d] (optional) live on devices[d] (distinct devices) and
+ *   each launch is enqueued on streams[d] (NULL array = default streams).  With hist_dev, each
+ *   hist_dev[d] then holds the SUM over all devices: one RCCL all-reduce (uint64, sum) over the
+ *   devices' streams, the path's only collective.  Returns ENOSYS if ndev > 1 and RCCL
+ *   (librccl.so.1) cannot be loaded.
+ * Both return 0 or an errno (ENODEV: a device index out of range; EINVAL: bad arguments). */
+int ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
+			      const struct ebpf_pkt_batch *batch, uint64_t *ret, uint8_t *faults,
+			      struct ebpf_batch_stats *stats);
+int ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices,
+				  const struct ebpf_pkt_batch *shards, uint64_t *const *ret_dev,
+				  uint8_t *const *faults_dev, uint64_t *const *hist_dev,
+				  void *const *streams);
+
 /* Select the device used by ebpf_prog_run_batch for the calling thread. */
 int ebpf_gpu_set_device(int device);
 

@@ -1,0 +1,135 @@
+"""Multi-GPU sharding of one batch.
+
+* In the library: ebpf_prog_run_batch_multi (host buffers, one thread per shard; a device may
+  repeat, which is how one GPU box exercises N shards) and ebpf_prog_run_batch_multi_dev
+  (device-resident, RCCL all-reduce of the verdict histograms).
+* Across processes (the bench's layout): 2 ranks on cuda:0 with gloo, the concatenated
+  shard results and the summed histogram equal ONE launch over the whole batch
+  (tests/shard_worker.py)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import goldens
+from helpers import make_maps, oracle_run
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _c4_case(n, seed=3):
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4()
+    pk = workloads.packets_l2l3(n, 64, seed=seed)
+    return goldens.Case("c4", lay.code, lay.relocs,
+                        [(8, 256, workloads.c4_map_values().tobytes())], pk.reshape(-1), n, 64, None)
+
+
+def test_multi_rejects_bad_devices(env):
+    """No GPU here: every device index is out of range (ENODEV); bad lists are EINVAL."""
+    import errno
+    from generic_ebpf_amd import native
+    c = _c4_case(64)
+    maps = make_maps(native, env, c)
+    p = native.Prog(env, native.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        with pytest.raises(native.EbpfError) as ei:
+            p.run_batch_multi([], np.ascontiguousarray(c.data), 64, 64)
+        assert ei.value.code == errno.EINVAL
+        if native.gpu_count() == 0:
+            with pytest.raises(native.EbpfError) as ei:
+                p.run_batch_multi([0], np.ascontiguousarray(c.data), 64, 64)
+            assert ei.value.code == errno.ENODEV
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [1, 2, 3])
+def test_run_batch_multi_host_buffers(gpu, env, ndev):
+    """Shards on one GPU (repeated device index): results, faults and the summed histogram equal
+    the oracle's; a ragged count leaves uneven shards."""
+    n = (1 << 20) + 37
+    c = _c4_case(n)
+    want, wf, _, _ = oracle_run(c, nthreads=16)
+    maps = make_maps(gpu, env, c)
+    p = gpu.Prog(env, gpu.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        ret, faults, st = p.run_batch_multi([0] * ndev, np.ascontiguousarray(c.data), n, 64)
+        np.testing.assert_array_equal(ret, want)
+        np.testing.assert_array_equal(faults, wf)
+        h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
+        np.testing.assert_array_equal(np.array(st.hist[:], dtype=np.int64), h)
+        assert st.packets == n and st.faulted == 0
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+def test_run_batch_multi_imix(gpu, env):
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c5()
+    n = 1 << 16
+    data, offs, _ = workloads.packets_imix(n, seed=9)
+    c = goldens.Case("c5", lay.code, [], [], data, n, 0, offs)
+    want, wf, _, _ = oracle_run(c, nthreads=16)
+    p = gpu.Prog(env, c.code)
+    try:
+        ret, faults, st = p.run_batch_multi([0, 0], np.ascontiguousarray(data), n, 0, offs)
+        np.testing.assert_array_equal(ret, want)
+        np.testing.assert_array_equal(faults, wf)
+    finally:
+        p.destroy()
+
+
+@pytest.mark.gpu
+def test_run_batch_multi_dev_rccl(gpu, env, monkeypatch):
+    """Device-resident multi launch through the RCCL all-reduce (forced at one device: the
+    communicator, the grouped all-reduce and the dlopen of RCCL all run), histogram exact;
+    a repeated device is refused."""
+    import errno
+    import torch
+    monkeypatch.setenv("EBPF_FORCE_RCCL", "1")
+    n = 1 << 20
+    c = _c4_case(n, seed=21)
+    want, _, _, _ = oracle_run(c, nthreads=16)
+    maps = make_maps(gpu, env, c)
+    p = gpu.Prog(env, gpu.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(c.data).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_hist = torch.full((257,), 5, dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        p.run_batch_multi_dev([0], [(d_pk.data_ptr(), n, 64, None)], [d_ret.data_ptr()],
+                              hists=[d_hist.data_ptr()], streams=[st], hist_overwrite=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+        h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+        with pytest.raises(gpu.EbpfError) as ei:
+            p.run_batch_multi_dev([0, 0], [(d_pk.data_ptr(), n, 64, None)] * 2,
+                                  [d_ret.data_ptr()] * 2)
+        assert ei.value.code == errno.EINVAL
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,total", [("c4", (1 << 22) + 4099), ("c5", 200001)])
+def test_two_ranks_gloo_equal_one_launch(gpu, cfg, total):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29611 + (cfg == "c5")),
+           os.path.join(ROOT, "tests", "shard_worker.py"), cfg, str(total)]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout.decode()[-2000:], r.stderr.decode()[-3000:])
+    assert '"hist_equal": true' in r.stdout.decode()
