@@ -58,6 +58,13 @@ assert RETK_STAGED in (1, 2, 4, 8)
 
 STAGED_IMAGE = True   # set per generated image (generate())
 
+# Launch-private verdict partials (dp_launch.hist_rows, shared with asm_runtime.cpp): 8 replicas
+# of EBPF_HIST_BINS u64 (bin 256 of replica 0 = the fault count), then the u32 arrival tickets:
+# one per replica and a top one, each on a 64-B line of its own.
+HIST_REPLICAS = 8
+HIST_REPLICA_BYTES = 257 * 8
+HIST_TICKET_OFF = HIST_REPLICAS * HIST_REPLICA_BYTES
+
 
 def set_retk(k):
     global RETK, V_RB, NVGPR
@@ -1545,7 +1552,14 @@ def common_group_code():
           "v_mov_b32 v21, %s" % s(S_SHARED + 1),
           "s_lshl_b32 %s, %s, 5" % (s(S_T0), s(S_START)),
           "v_mov_b32 v%d, %s" % (V_T, s(S_T0))] + goto(".Lr_schedule")
-    # finish: flush the LDS histogram (u32 per workgroup) into the u64 global histogram
+    # finish: this workgroup's LDS histogram (u32 bins) goes into the launch's u64 partial
+    # histograms with device-scope atomics, one replica per (workgroup & 7) so that the adds to
+    # a hot bin spread over 8 lines; the workgroup whose ticket add returns nwg - 1 arrived last
+    # and moves the 8 replicas (read-and-zero swaps) plus the fault count into the caller's
+    # histogram (stored, or added), then re-arms the ticket.  One kernel per launch: no
+    # second-stage reduce (hand-off form: 8-B agent atomics on both sides, MI355X_MICROARCH.md
+    # "Valid forms")
+    HR = HIST_REPLICA_BYTES
     L += [".Lfinish:"] + store_prev_results("f", True) + [
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
@@ -1558,16 +1572,105 @@ def common_group_code():
           "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
           "ds_read_b32 %s, %s" % (v(H[3]), v(H[2])),
           "s_load_dwordx2 %s, s[0:1], 0x68" % sp(S_REC),               # dp_launch.hist_rows
+          "s_load_dwordx4 s[68:71], s[0:1], 0x70",     # hist_user, hist_flags, nwg
           "s_waitcnt lgkmcnt(0)",
-          # rows: this workgroup's 256 counts as one 1-KB row (hot bins would otherwise
-          # serialise thousands of same-address atomics); ebpf_hist_reduce sums the rows
           "s_cmp_eq_u64 %s, 0" % sp(S_REC),
           "s_cbranch_scc1 .Lfin_atomic",
-          "s_lshl_b32 %s, s2, 10" % s(S_T1),
-          "s_add_u32 %s, %s, %s" % (s(S_REC), s(S_REC), s(S_T1)),
-          "s_addc_u32 %s, %s, 0" % (s(S_REC + 1), s(S_REC + 1)),
-          "global_store_dword %s, %s, %s" % (v(H[2]), v(H[3]), sp(S_REC)),
+          "s_and_b32 %s, s2, 7" % s(S_T1),
+          "s_mul_i32 %s, %s, %d" % (s(S_T1), s(S_T1), HR),
+          "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(H[1])),
+          "v_add_u32 %s, %s, %s" % (v(R[0]), s(S_T1), v(R[0])),
+          "v_mov_b32 %s, %s" % (v(R[2]), v(H[3])),
+          "v_mov_b32 %s, 0" % v(R[3]),
+          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[3]),
+          "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE),
+          "s_cbranch_execz .Lfin_noadd",
+          "global_atomic_add_x2 %s, %s, %s" % (v(R[0]), vp(R[2]), sp(S_REC)),
+          ".Lfin_noadd:",
+          "s_mov_b64 exec, -1",
+          "s_waitcnt vmcnt(0)",          # this wave's adds (and its fault counts) performed
+          "s_barrier",                   # ... and every wave's
+          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
+          "s_cbranch_scc0 .Lfin_flag",
+          # two-level ticket (one hot word would serialise every workgroup's arrival): the
+          # workgroups of replica r = wg & 7 count on ticket r; the last of them (its add
+          # returns n_r - 1, n_r = (nwg - 1 - r) / 8 + 1) re-arms ticket r and counts on the
+          # top ticket, whose last arrival (min(nwg, 8) - 1) is the launch's last workgroup
+          "s_mov_b64 exec, 1",
+          "s_and_b32 %s, s2, 7" % s(S_T1),
+          "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_T1)),
+          "s_add_u32 %s, %s, %d" % (s(S_T0), s(S_T0), HIST_TICKET_OFF),
+          "v_mov_b32 %s, %s" % (v(R[4]), s(S_T0)),
+          "v_mov_b32 %s, 1" % v(R[5]),
+          "global_atomic_add %s, %s, %s, %s sc0" % (v(R[6]), v(R[4]), v(R[5]), sp(S_REC)),
+          "s_sub_u32 %s, s71, 1" % s(S_T3),
+          "s_sub_u32 %s, %s, %s" % (s(S_T3), s(S_T3), s(S_T1)),
+          "s_lshr_b32 %s, %s, 3" % (s(S_T3), s(S_T3)),        # n_r - 1
+          "s_waitcnt vmcnt(0)",
+          "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[6])),
+          "s_cmp_eq_u32 %s, %s" % (s(S_T2), s(S_T3)),
+          "s_cselect_b32 %s, 1, 0" % s(S_T2),
+          "s_cbranch_scc0 .Lfin_setflag",
+          "v_mov_b32 %s, 0" % v(R[10]),
+          "global_atomic_swap %s, %s, %s, %s sc0" % (v(R[8]), v(R[4]), v(R[10]), sp(S_REC)),
+          "v_mov_b32 %s, %d" % (v(R[9]), HIST_TICKET_OFF + 64 * HIST_REPLICAS),
+          "global_atomic_add %s, %s, %s, %s sc0" % (v(R[6]), v(R[9]), v(R[5]), sp(S_REC)),
+          "s_min_u32 %s, s71, %d" % (s(S_T3), HIST_REPLICAS),
+          "s_sub_u32 %s, %s, 1" % (s(S_T3), s(S_T3)),
+          "s_waitcnt vmcnt(0)",
+          "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[6])),
+          "s_cmp_eq_u32 %s, %s" % (s(S_T2), s(S_T3)),
+          "s_cselect_b32 %s, 1, 0" % s(S_T2),
+          ".Lfin_setflag:",
+          "v_mov_b32 %s, %s" % (v(R[7]), s(S_T2)),
+          "v_mov_b32 %s, 0" % v(R[8]),
+          # LDS word 0 (bin 0, read by every wave before the barrier above) tells the others
+          "ds_write_b32 %s, %s" % (v(R[8]), v(R[7])),
+          "s_mov_b64 exec, -1",
+          "s_waitcnt lgkmcnt(0)",
+          ".Lfin_flag:",
+          "s_barrier",
+          "v_mov_b32 %s, 0" % v(R[8]),
+          "ds_read_b32 %s, %s" % (v(R[7]), v(R[8])),
+          "s_waitcnt lgkmcnt(0)",
+          "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[7])),
+          "s_cmp_eq_u32 %s, 0" % s(S_T2),
+          "s_cbranch_scc1 .Lfin_end",
+          # the last workgroup: wave w moves bins 64w..64w+63 (v0..v15 results, v16..v23
+          # addresses, v[24:25] = 0: the eBPF registers and staged packet are dead here)
+          "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(H[1])),
+          "v_mov_b32 v24, 0",
+          "v_mov_b32 v25, 0"]
+    for r in range(HIST_REPLICAS):
+        L += ["v_add_u32 v%d, %d, %s" % (16 + r, r * HR, v(R[0])),
+              "global_atomic_swap_x2 v[%d:%d], v%d, v[24:25], %s sc0" % (2 * r, 2 * r + 1, 16 + r,
+                                                                       sp(S_REC))]
+    L += ["s_waitcnt vmcnt(0)"]
+    for r in range(1, HIST_REPLICAS):
+        L += ["v_lshl_add_u64 v[0:1], v[%d:%d], 0, v[0:1]" % (2 * r, 2 * r + 1)]
+    L += ["s_bitcmp1_b32 s70, 0",                   # hist_flags bit 0: store (overwrite)
+          "s_cbranch_scc0 .Lfin_add",
+          "global_store_dwordx2 %s, v[0:1], s[68:69]" % v(R[0]),
+          "s_branch .Lfin_faults",
+          ".Lfin_add:",
+          "global_atomic_add_x2 %s, v[0:1], s[68:69]" % v(R[0]),
+          ".Lfin_faults:",
+          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
+          "s_cbranch_scc0 .Lfin_end",
+          "s_mov_b64 exec, 1",                       # bin 256 (replica 0 only) and the ticket
+          "v_mov_b32 v16, 2048",
+          "global_atomic_swap_x2 v[2:3], v16, v[24:25], %s sc0" % sp(S_REC),
+          "v_mov_b32 v17, %d" % (HIST_TICKET_OFF + 64 * HIST_REPLICAS),   # the top ticket
+          "global_atomic_swap v18, v17, v24, %s sc0" % sp(S_REC),
+          "s_waitcnt vmcnt(0)",
+          "s_bitcmp1_b32 s70, 0",
+          "s_cbranch_scc0 .Lfin_fadd",
+          "global_store_dwordx2 v16, v[2:3], s[68:69]",
           "s_branch .Lfin_end",
+          ".Lfin_fadd:",
+          "global_atomic_add_x2 v16, v[2:3], s[68:69]",
+          "s_branch .Lfin_end",
+          # no partial buffer (variant-free fallback used by nothing today): per-bin atomics
           ".Lfin_atomic:",
           "v_cmp_ne_u32_e64 vcc, 0, %s" % v(H[3]),
           "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE),
@@ -1831,7 +1934,7 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 112
+    kernarg = 128
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),

@@ -101,7 +101,21 @@ struct dp_launch {
 	uint32_t total_waves;     // persistent grid: waves in the launch (group stride); bits
 	                          // 28..29: log2 of the superblock size (staged kernels)
 	uint32_t lds_pkt_base;    // staged kernel: LDS byte offset of the per-wave packet buffers
-	uint32_t *hist_rows;      // assembly kernels: per-workgroup u32[256] verdict counts (bins
-	                          // 0..255), summed into hist by ebpf_hist_reduce; NULL = atomics
+	uint32_t *hist_rows;      // assembly kernels: the launch's private verdict partials
+	                          // (DP_HIST_* layout below; hist points at it too, so faults count
+	                          // into replica 0's bin 256); NULL = per-bin atomics into hist
+	unsigned long long *hist_user; // the caller's histogram: the last workgroup stores (flags
+	                          // bit 0) or adds the reduced partials there
+	uint32_t hist_flags;      // bit 0: store instead of add (EBPF_BATCH_HIST_OVERWRITE)
+	uint32_t nwg;             // workgroups in this launch (the ticket's arrival count)
 };
-static_assert(sizeof(dp_launch) == 112, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 128, "dp_launch layout is shared with the assembly kernels");
+
+// Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
+// EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B
+// lines of their own (one per replica, then the top one).  All zero between launches: the last
+// workgroup swaps every word back to 0.
+#define DP_HIST_REPLICAS 8u
+#define DP_HIST_REPLICA_BYTES (257u * 8u)
+#define DP_HIST_TICKET_OFF (DP_HIST_REPLICAS * DP_HIST_REPLICA_BYTES)
+#define DP_HIST_PARTIAL_BYTES (DP_HIST_TICKET_OFF + 64u * (DP_HIST_REPLICAS + 1u))

@@ -367,77 +367,7 @@ ebpf_interp_v0(dp_launch L)
 
 namespace {
 
-// Verdict-histogram second stage for the assembly kernels: every workgroup wrote its 256 bin
-// counts as one u32 row (1 KB).  Bins per block of the second stage: block b sums bins [4b, 4b+4) over every row (thread t
-// reads rows t, t+256, ...: one 16-B load per row), so each bin has one writer and the result
-// can be stored (EBPF_BATCH_HIST_OVERWRITE) or added without contention.
-constexpr uint32_t kBinsPerBlock = 4;
-
-__global__ void __launch_bounds__(256)
-ebpf_hist_reduce(const uint32_t *__restrict__ rows, uint32_t nrows, unsigned long long *hist,
-		 unsigned long long *fault_scratch, uint32_t overwrite)
-{
-	const uint32_t bin0 = blockIdx.x * kBinsPerBlock;
-	unsigned long long acc[kBinsPerBlock] = {0, 0, 0, 0};
-	for (uint32_t r0 = threadIdx.x; r0 < nrows; r0 += 4 * 256) {
-		uint4 q[4]; // four rows in flight per thread before the first add
-#pragma unroll
-		for (uint32_t k = 0; k < 4; k++) {
-			const uint32_t r = r0 + k * 256;
-			q[k] = r < nrows ? *reinterpret_cast<const uint4 *>(rows + (size_t)r * 256 + bin0)
-					 : make_uint4(0, 0, 0, 0);
-		}
-#pragma unroll
-		for (uint32_t k = 0; k < 4; k++) {
-			acc[0] += q[k].x;
-			acc[1] += q[k].y;
-			acc[2] += q[k].z;
-			acc[3] += q[k].w;
-		}
-	}
-	__shared__ unsigned long long part[4][kBinsPerBlock];
-#pragma unroll
-	for (uint32_t k = 0; k < kBinsPerBlock; k++)
-		for (int d = 32; d > 0; d >>= 1)
-			acc[k] += __shfl_down(acc[k], d, 64);
-	const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-	if (lane == 0)
-#pragma unroll
-		for (uint32_t k = 0; k < kBinsPerBlock; k++)
-			part[wave][k] = acc[k];
-	__syncthreads();
-	if (threadIdx.x < kBinsPerBlock) {
-		const uint32_t k = threadIdx.x;
-		const unsigned long long v = part[0][k] + part[1][k] + part[2][k] + part[3][k];
-		if (overwrite)
-			hist[bin0 + k] = v;
-		else if (v)
-			atomicAdd(&hist[bin0 + k], v);
-	}
-	// bin 256 (faulted): the interpreter added it to fault_scratch[256]; move it over and leave
-	// the scratch zero for the row buffer's next use
-	if (fault_scratch && blockIdx.x == 0 && threadIdx.x == 0) {
-		const unsigned long long f = fault_scratch[256];
-		if (overwrite)
-			hist[256] = f;
-		else if (f)
-			atomicAdd(&hist[256], f);
-		fault_scratch[256] = 0;
-	}
-}
-
 } // namespace
-
-hipError_t
-launch_hist_reduce(const uint32_t *rows, uint32_t nrows, unsigned long long *hist,
-		   unsigned long long *fault_scratch, bool overwrite, hipStream_t stream)
-{
-	if (nrows == 0 && !overwrite && !fault_scratch)
-		return hipSuccess;
-	hipLaunchKernelGGL(ebpf_hist_reduce, dim3(256 / kBinsPerBlock), dim3(256), 0, stream, rows,
-			   nrows, hist, fault_scratch, overwrite ? 1u : 0u);
-	return hipGetLastError();
-}
 
 hipError_t
 launch_interp_v0(const dp_launch &L, hipStream_t stream)

@@ -8,6 +8,8 @@
 // executes eBPF on the CPU — without a GPU the entry points return ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -20,7 +22,7 @@ hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
 			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap,
 			     hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist,
-			     bool hist_overwrite, bool *enqueued);
+			     bool hist_overwrite);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
@@ -68,96 +70,78 @@ map_record(const struct ebpf_map *em, uint32_t *lds_used)
 	return m;
 }
 
-// Per-device pool of histogram row buffers (asm kernels: one u32[256] row per workgroup).  A
-// buffer whose last use has completed (its event) is taken as is.  Otherwise the pool grows to
-// kRowsPool buffers, so that launches on that many streams run concurrently; past that, a launch
-// takes the least recently used buffer and makes its stream wait (on the GPU, no host block) for
-// that buffer's last use — always, also when that use was on the same stream (a stream handle
-// can be recycled while work from its previous life is still in flight).
+// Verdict-partial buffers of the assembly kernels (dprog.h DP_HIST_*), one per STREAM and
+// device: launches on one stream run in order and each kernel leaves its buffer zero, so a
+// stream reuses its own buffer with no event and no wait.  Streams are told apart by
+// hipStreamGetId where the HIP runtime has it (ROCm >= 7.1: a stream handle can be recycled
+// while work from its previous life is still in flight, an id is never reused), else by handle.
+// At most kRowsMax streams per device own a buffer; past that the least recently used stream's
+// buffer moves to the new stream, which first waits (on the GPU) for everything the old stream
+// has submitted — or, if that stream no longer exists, the device drains.
 struct rows_slot {
 	void *p = nullptr;
-	hipEvent_t ev = nullptr;
-	uint64_t seq = 0; // order of the last use (the smallest is the least recent)
-	hipStream_t stream = nullptr; // stream of the last use
-	bool busy = false; // between acquire and the event record of the launch using it
+	unsigned long long sid = 0; // owning stream's id
+	hipStream_t stream = nullptr;
+	uint64_t last = 0;          // order of the last use
 };
 std::mutex g_rows_lock;
-std::vector<std::vector<rows_slot>> g_rows;
-uint64_t g_rows_seq = 0;
-constexpr size_t kRowsPool = 4;
-constexpr size_t kRowsMax = 64; // buffers busy on the host at once (concurrent callers)
-
-// Each buffer is `bytes` of rows followed by kRowsScratch bytes: 257 u64 whose bin 256 takes the
-// interpreter's fault count (the second stage moves it out and re-zeroes it).
-constexpr size_t kRowsScratch = 4096;
+std::vector<std::vector<rows_slot>> g_rows; // per device
+uint64_t g_rows_tick = 0;
+constexpr size_t kRowsMax = 64;
 
 int
-rows_acquire(int device, size_t bytes, hipStream_t stream, rows_slot **out)
+rows_acquire(int device, hipStream_t stream, void **out)
 {
+	// (resolved at run time: torch bundles a HIP runtime older than the one this is built on)
+	using get_id_fn = hipError_t (*)(hipStream_t, unsigned long long *);
+	static const get_id_fn get_id =
+	    reinterpret_cast<get_id_fn>(dlsym(RTLD_DEFAULT, "hipStreamGetId"));
+	unsigned long long sid = (unsigned long long)(uintptr_t)stream;
+	if (get_id && get_id(stream, &sid) != hipSuccess)
+		return EIO;
 	std::lock_guard<std::mutex> g(g_rows_lock);
 	if ((int)g_rows.size() <= device)
 		g_rows.resize(device + 1);
 	std::vector<rows_slot> &pool = g_rows[device];
 	rows_slot *lru = nullptr;
-	size_t idle = 0;
 	for (rows_slot &r : pool) {
-		if (r.busy)
-			continue;
-		idle++;
-		if (!lru || r.seq < lru->seq)
+		if (r.sid == sid) {
+			r.stream = stream;
+			r.last = ++g_rows_tick;
+			*out = r.p;
+			return 0;
+		}
+		if (!lru || r.last < lru->last)
 			lru = &r;
 	}
-	if (lru && hipEventQuery(lru->ev) == hipSuccess) { // the least recent use is done
-		lru->busy = true;
-		*out = lru;
-		return 0;
-	}
-	if ((idle < kRowsPool || !lru) && pool.size() < kRowsMax) {
-		pool.reserve(kRowsMax); // slots must not move: callers keep pointers
+	if (pool.size() < kRowsMax) {
 		rows_slot r;
-		if (hipMalloc(&r.p, bytes + kRowsScratch) != hipSuccess)
+		if (hipMalloc(&r.p, DP_HIST_PARTIAL_BYTES) != hipSuccess)
 			return ENOMEM;
-		if (hipMemsetAsync(static_cast<char *>(r.p) + bytes, 0, kRowsScratch, stream) !=
-		    hipSuccess) {
+		if (hipMemsetAsync(r.p, 0, DP_HIST_PARTIAL_BYTES, stream) != hipSuccess) {
 			hipFree(r.p);
 			return ENOMEM;
 		}
-		if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
-			hipFree(r.p);
-			return ENOMEM;
-		}
-		r.busy = true;
+		r.sid = sid;
+		r.stream = stream;
+		r.last = ++g_rows_tick;
 		pool.push_back(r);
-		*out = &pool.back();
+		*out = r.p;
 		return 0;
 	}
-	if (!lru)
-		return ENOMEM; // kRowsMax launches mid-submission on the host at once
-	if (hipStreamWaitEvent(stream, lru->ev, 0) != hipSuccess)
+	hipEvent_t ev;
+	if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+		return ENOMEM;
+	hipError_t e = hipEventRecord(ev, lru->stream);
+	e = (e == hipSuccess) ? hipStreamWaitEvent(stream, ev, 0) : hipDeviceSynchronize();
+	hipEventDestroy(ev);
+	if (e != hipSuccess)
 		return EIO;
-	lru->busy = true;
-	*out = lru;
+	lru->sid = sid;
+	lru->stream = stream;
+	lru->last = ++g_rows_tick;
+	*out = lru->p;
 	return 0;
-}
-
-// `enqueued`: some kernel of the launch reached the stream (whatever the launch returned), so
-// the buffer's next user must wait for it.  `failed`: the launch stopped part way, so the fault
-// scratch may hold a count the second stage never moved: it is re-zeroed on the same stream; a
-// buffer that cannot be made clean again is left busy (never reused).
-void
-rows_release(rows_slot *r, hipStream_t stream, bool enqueued, bool failed, size_t rows_bytes)
-{
-	std::lock_guard<std::mutex> g(g_rows_lock);
-	if (enqueued) {
-		if (failed && hipMemsetAsync(static_cast<char *>(r->p) + rows_bytes, 0, kRowsScratch,
-					     stream) != hipSuccess)
-			return;
-		if (hipEventRecord(r->ev, stream) != hipSuccess)
-			return;
-		r->seq = ++g_rows_seq;
-		r->stream = stream;
-	}
-	r->busy = false;
 }
 
 thread_local std::string t_err;
@@ -401,29 +385,30 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		dp->last_exec = fn ? EBPF_EXEC_COMPILED : EBPF_EXEC_INTERPRETER;
 		dp->last_layout = mode;
 		L.lds_pkt_base = (mode == 0 && ep->xlated->asm_gstage) ? 0x80000000u : 0;
-		rows_slot *rows = nullptr;
 		unsigned long long *user_hist = L.hist;
-		size_t rows_bytes = 0;
 		if (L.hist) {
-			rows_bytes = (size_t)asm_max_workgroups(dp->device) * 1024;
-			if ((err = rows_acquire(dp->device, rows_bytes, stream, &rows)))
-				return fail(err, "no histogram row buffer");
-			L.hist_rows = static_cast<uint32_t *>(rows->p);
-			// faults (bin 256) go to the buffer's scratch; the second stage moves them
-			L.hist = reinterpret_cast<unsigned long long *>(static_cast<char *>(rows->p) +
-									rows_bytes);
+			void *part = nullptr;
+			if ((err = rows_acquire(dp->device, stream, &part)))
+				return fail(err, "no verdict-partial buffer");
+			// faults (bin 256) count into replica 0 of the partials; the kernel's last
+			// workgroup moves everything into the caller's histogram (user_hist)
+			L.hist_rows = static_cast<uint32_t *>(part);
+			L.hist = static_cast<unsigned long long *>(part);
 		}
 		// a program that probes hashtables is bound by their latency and wants every wave;
 		// the others stream packets (asm_runtime.cpp, occupancy)
 		bool probes = false;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
-		bool enqueued = false;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
 				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop, user_hist,
-				      hist_overwrite, &enqueued);
-		if (rows)
-			rows_release(rows, stream, enqueued, e != hipSuccess, rows_bytes);
+				      hist_overwrite);
+		if (e == hipSuccess && getenv("EBPF_AB_EVENT")) { // (A/B probe: per-launch marker cost)
+			static thread_local hipEvent_t ab_ev = nullptr;
+			if (!ab_ev)
+				hipEventCreateWithFlags(&ab_ev, hipEventDisableTiming);
+			hipEventRecord(ab_ev, stream);
+		}
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;
