@@ -20,7 +20,7 @@ tiles; any mismatch prints the line with "verified": false and exits 1.
 
 roofline.kernel_ms is the engine's kernel alone: HIP events that the library records on the
 launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so it compares
-with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 5th timed step
+with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 10th timed step
 carries the events (--time-every).  roofline.traffic is measured by THIS run: two child passes
 of this script under rocprofv3 --pmc (FETCH_SIZE, then WRITE_SIZE) on the same workload, after
 the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).
@@ -73,8 +73,8 @@ def parse(argv=None):
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle check (PMC child passes)")
     ap.add_argument("--no-pmc", action="store_true", help="no rocprofv3 --pmc passes for roofline.traffic")
     ap.add_argument("--pmc-dir", default="", help="where the PMC passes write (default: a temp dir)")
-    ap.add_argument("--time-every", type=int, default=5,
-                    help="event-time the kernel of every k-th timed step (default 5: a pair of events per step costs C2 7 us of its 21-us step; profiles/r01/te)")
+    ap.add_argument("--time-every", type=int, default=10,
+                    help="event-time the kernel of every k-th timed step (default 10: each event pair is a GPU-side marker, C2 steps with a pair every 5th step took 14.2 us against 12.9 us with none; profiles/r02/ab_event)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)

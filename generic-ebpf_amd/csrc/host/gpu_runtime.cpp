@@ -403,12 +403,6 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
 				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop, user_hist,
 				      hist_overwrite);
-		if (e == hipSuccess && getenv("EBPF_AB_EVENT")) { // (A/B probe: per-launch marker cost)
-			static thread_local hipEvent_t ab_ev = nullptr;
-			if (!ab_ev)
-				hipEventCreateWithFlags(&ab_ev, hipEventDisableTiming);
-			hipEventRecord(ab_ev, stream);
-		}
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;
