@@ -162,6 +162,7 @@ for n in ("EXIT", "FAULT", "NOP", "LOOKUPSTK", "LOOKUPGEN"):
 for z in SIZES:
     fam("LDXPKC%d" % z, 3)      # staged packet load at a constant byte offset: (dst, offset)
 fam("HLOOKUP", 0)              # hashtable lookup, map known at translation time (s14 = record offset)
+fam("UPDATE", 0)               # map_update_elem, map known (s14 = record offset, s15 = entry index)
 for z in SIZES:
     fam("LDXHV%d" % z, 2)       # load from a hashtable value (lookup result), in range by provenance
 # standard-eBPF semantics (ebpf_prog_set_semantics): the operations whose meaning differs from
@@ -896,6 +897,134 @@ def hlookup_routine():
     return L
 
 
+def update_routine():
+    """UPDATE (called): r0 = map_update_elem(map, r2, r3, r4) for the map whose dp_map record is
+    at byte offset s14 of the map table (ebpf_map.c:101-108 -> ebpf_map_array.c:185-211), with
+    the device-batch semantics (ebpf_gpu.h "Map writes in a device batch"): the return code is
+    the reference's (EINVAL for a NULL key / value or flags > EBPF_EXIST, EEXIST for
+    EBPF_NOEXIST, EINVAL for a key >= max_entries, else 0) and the write itself goes to the
+    launch's log (dp_launch.upd_log: {u64 packet, u32 entry | map << 20, u32 key, value}),
+    applied after the batch in packet order.  Key and value are region-checked like loads.  A
+    hashtable faults HELPER_UNSUPPORTED.  Uses s[8:9] (return address), s[10:11] (entry exec),
+    R[*], H[*]; compiled programs treat s10..s11 as clobbered after it."""
+    key = v(H[2])
+    L = [".Lr_update:",
+         "s_mov_b64 s[8:9], %s" % sp(S_LINK),
+         "s_mov_b64 s[10:11], exec",
+         "v_mov_b32 v0, 22", "v_mov_b32 v1, 0",
+         # NULL key / value or flags > EBPF_EXIST: EINVAL, nothing read (ebpf_map.c:101-107)
+         "v_cmp_ne_u64_e64 %s, 0, v[4:5]" % sp(S_JUNK),
+         "v_cmp_ne_u64_e64 vcc, 0, v[6:7]",
+         "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+         "v_cmp_ge_u64_e64 vcc, 2, v[8:9]",
+         "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+         "s_and_b64 exec, exec, %s" % sp(S_JUNK),
+         "s_cbranch_execz .Lup_ret",
+         "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+         "s_waitcnt lgkmcnt(0)",
+         "s_bitcmp1_b32 s71, 31",                       # a hashtable: no device form
+         "s_cbranch_scc0 .Lup_array",
+         "s_mov_b64 %s, exec" % sp(S_MASK),
+         "s_mov_b32 %s, 6" % s(S_CODE)] + call(".Lr_fault") + [
+         "s_branch .Lup_ret",
+         ".Lup_array:",
+         # EBPF_NOEXIST: every key of an array exists -> EEXIST (ebpf_map_array.c:188-189)
+         "v_and_b32 %s, 1, v8" % v(R[0]),
+         "v_cmp_ne_u32_e64 vcc, 0, %s" % v(R[0]),
+         "s_mov_b64 %s, exec" % sp(S_MASK),
+         "s_and_b64 exec, exec, vcc",
+         "v_mov_b32 v0, 17",
+         "s_andn2_b64 exec, %s, vcc" % sp(S_MASK),
+         "s_cbranch_execz .Lup_ret",
+         # the key: 4 bytes at r2, region-checked like a load
+         "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1]),
+         "s_mov_b32 %s, 4" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check") + [
+         "s_cbranch_execz .Lup_ret",
+         "v_mov_b32 %s, 0" % key]
+    for b in range(4):
+        L += ["flat_load_ubyte %s, %s offset:%d" % (v(H[3]), vp(H[0]), b),
+              "s_waitcnt vmcnt(0) lgkmcnt(0)",
+              "v_lshl_or_b32 %s, %s, %d, %s" % (key, v(H[3]), 8 * b, key)]
+    L += ["s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "v_cmp_gt_u32_e64 vcc, s69, %s" % key,          # key >= max_entries: EINVAL
+          "s_and_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lup_ret",
+          # the value: value_size bytes at r3, region-checked
+          "v_mov_b32 %s, v6" % v(H[0]), "v_mov_b32 %s, v7" % v(H[1]),
+          "s_mov_b32 %s, s68" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check") + [
+          "s_cbranch_execz .Lup_ret",
+          "v_mov_b32 v0, 0",
+          # a log slot per lane: one atomic add on the log's counter for the wave
+          "s_load_dwordx4 s[64:67], s[0:1], 0x80",         # upd_log, upd_cap, upd_stride
+          "s_load_dwordx2 s[68:69], s[0:1], 0x90",         # pkt_base
+          "s_waitcnt lgkmcnt(0)",
+          "s_bcnt1_i32_b64 %s, exec" % s(S_T0),
+          "v_mbcnt_lo_u32_b32 %s, exec_lo, 0" % v(R[0]),
+          "v_mbcnt_hi_u32_b32 %s, exec_hi, %s" % (v(R[0]), v(R[0])),
+          "s_mov_b64 %s, exec" % sp(S_MASK),
+          "s_ff1_i32_b64 %s, exec" % s(S_T1),
+          "s_lshl_b64 exec, 1, %s" % s(S_T1),
+          "v_mov_b32 %s, %s" % (v(R[1]), s(S_T0)),
+          "v_mov_b32 %s, 0" % v(R[2]),
+          "global_atomic_add %s, %s, %s, s[64:65] sc0" % (v(R[3]), v(R[2]), v(R[1])),
+          "s_waitcnt vmcnt(0)",
+          "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[3])),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "v_add_u32 %s, %s, %s" % (v(R[0]), s(S_T2), v(R[0])),      # this lane's slot
+          # (the host sizes the log for the program's most updates per path; a full log is a
+          # library bug: MEM fault, loudly, rather than a lost write)
+          "v_cmp_gt_u32_e64 vcc, s66, %s" % v(R[0]),
+          "s_andn2_b64 %s, exec, vcc" % sp(S_MASK),
+          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+          "s_cbranch_scc1 .Lup_room",
+          "s_mov_b32 %s, 3" % s(S_CODE)] + call(".Lr_fault") + [
+          "s_cbranch_execz .Lup_ret",
+          "s_load_dwordx4 s[64:67], s[0:1], 0x80",
+          "s_load_dwordx2 s[68:69], s[0:1], 0x90",
+          "s_waitcnt lgkmcnt(0)",
+          ".Lup_room:",
+          # the record: log + 64 + slot * stride
+          "s_add_u32 s64, s64, 64",
+          "s_addc_u32 s65, s65, 0",
+          "v_mov_b32 %s, s67" % v(R[1]),
+          "v_mad_u64_u32 %s, %s, %s, %s, s[64:65]" % (vp(R[4]), sp(S_JUNK), v(R[0]), v(R[1])),
+          # packet index (pkt_base = this launch's first packet in its batch)
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[2]), V_L16),
+          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[2]), s(S_GROUP), v(R[2])),
+          "v_mov_b32 %s, s69" % v(R[3]),
+          "v_add_co_u32 %s, vcc, s68, %s" % (v(R[2]), v(R[2])),
+          "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[3]), v(R[3])),
+          "global_store_dwordx2 %s, %s, off" % (vp(R[4]), vp(R[2])),
+          "s_lshr_b32 %s, s14, 5" % s(S_T0),                  # map index
+          "s_lshl_b32 %s, %s, 20" % (s(S_T0), s(S_T0)),
+          "s_or_b32 %s, %s, s15" % (s(S_T0), s(S_T0)),        # | entry index
+          "v_mov_b32 %s, %s" % (v(R[6]), s(S_T0)),
+          "v_mov_b32 %s, %s" % (v(R[7]), key),
+          "global_store_dwordx2 %s, %s, off offset:8" % (vp(R[4]), vp(R[6])),
+          # the value, byte by byte (r3 may point at the stack, the packet or a map value)
+          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_mov_b32 %s, 0" % s(S_T0),
+          ".Lup_copy:",
+          "s_cmp_ge_u32 %s, s68" % s(S_T0),
+          "s_cbranch_scc1 .Lup_ret",
+          "v_add_co_u32 %s, vcc, %s, v6" % (v(H[0]), s(S_T0)),
+          "v_addc_co_u32 %s, vcc, 0, v7, vcc" % v(H[1]),
+          "flat_load_ubyte %s, %s" % (v(H[3]), vp(H[0])),
+          "v_add_co_u32 %s, vcc, %s, %s" % (v(H[4]), s(S_T0), v(R[4])),
+          "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(H[5]), v(R[5])),
+          "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          "global_store_byte %s, %s, off offset:16" % (vp(H[4]), v(H[3])),
+          "s_add_u32 %s, %s, 1" % (s(S_T0), s(S_T0)),
+          "s_branch .Lup_copy",
+          ".Lup_ret:",
+          # every lane that entered and did not fault (S_ALIVE lost the faulted ones)
+          "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
+          "s_setpc_b64 s[8:9]"]
+    return L
+
+
 # ---------------------------------------------------------------- handler emission
 def handler_body(name, d, sr):
     """Returns (lines, has_dispatch)."""
@@ -953,6 +1082,8 @@ def handler_body(name, d, sr):
         return goto(".Lr_lookup"), True
     if name == "HLOOKUP":
         return call(".Lr_hlookup"), False
+    if name == "UPDATE":
+        return call(".Lr_update"), False
     raise ValueError(name)
 
 
@@ -1237,6 +1368,7 @@ def routines():
           "s_setpc_b64 %s" % sp(S_JUNK)] + [
           ".Llk_sched:"] + goto(".Lr_schedule")
     L += hlookup_routine()
+    L += update_routine()
     # DMA_NEXT (staged kernel, deferred mode s7 bit 4): issue the LDS DMA of this wave's next
     # group now, once per group (sets bit 5).  The group set-up defers only a full next group,
     # so this is always the 4-instruction full-group DMA.  Preserves exec, S_T*, s[66:71];
@@ -1899,6 +2031,8 @@ def generate(out_s, staged_image):
                 m |= 1 << 2      # the routine resumes at s12
             if name == "HLOOKUP":
                 m |= 1 << 4      # the routine reads the map record offset from s14
+            if name == "UPDATE":
+                m |= (1 << 4) | (1 << 5)   # map record offset (s14), entry index (s15)
             reads.append(m)
             # an LDS read whose result the interpreter's dispatch wait (lgkmcnt) covered
             last_ds = max([i for i, ln in enumerate(copy) if ln.startswith("ds_read")] or [-1])
@@ -1934,7 +2068,7 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 128
+    kernarg = 152
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),

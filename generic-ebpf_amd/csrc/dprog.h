@@ -31,6 +31,9 @@ enum dp_kind : uint16_t {
 	DK_MOD64Z = 0x10a,  // dst = src ? dst % src : dst
 	DK_DIV32Z = 0x10b,  // 32-bit forms, results zero-extended
 	DK_MOD32Z = 0x10c,
+	// map-writing helpers (device-batch semantics, ebpf_gpu.h "Map writes in a device batch");
+	// the map is a translation-time constant: aux = its index in the dp_map table
+	DK_CALL_UPDATE = 0x10d, // r0 = map_update_elem(map, r2, r3, r4) (ebpf_map.c:101-108)
 };
 #define DP_CLS_JMP32 6
 
@@ -108,8 +111,14 @@ struct dp_launch {
 	                          // bit 0) or adds the reduced partials there
 	uint32_t hist_flags;      // bit 0: store instead of add (EBPF_BATCH_HIST_OVERWRITE)
 	uint32_t nwg;             // workgroups in this launch (the ticket's arrival count)
+	// map writes (DK_CALL_UPDATE): the batch's log, u32 record count at +0, records from +64:
+	// {u64 packet index, u32 entry | map << 20, u32 key, value[value_size]}, upd_stride apart
+	uint8_t *upd_log;
+	uint32_t upd_cap;         // records the log holds
+	uint32_t upd_stride;
+	uint64_t pkt_base;        // index of this launch's first packet in its batch
 };
-static_assert(sizeof(dp_launch) == 128, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 152, "dp_launch layout is shared with the assembly kernels");
 
 // Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
 // EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B

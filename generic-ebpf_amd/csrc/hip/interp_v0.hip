@@ -217,6 +217,52 @@ ebpf_interp_v0(dp_launch L)
 			R[0][tid] = res;
 			continue;
 		}
+		if (k == DK_CALL_UPDATE) {
+			// map_update_elem (ebpf_map.c:101-108 -> ebpf_map_array.c:185-211) with the device
+			// batch's deferred write (map_writes.hip): the reference's return code, the write
+			// logged for after the batch
+			const uint64_t r2 = R[2][tid], r3 = R[3][tid], r4 = R[4][tid];
+			uint64_t res = 22; // EINVAL: NULL key / value, flags > EBPF_EXIST
+			if (r2 != 0 && r3 != 0 && r4 <= 2) {
+				const dp_map &mp = L.maps[e.aux];
+				if (mp.flags & DP_MAP_HASH) {
+					fault = F_HELPER_UNSUPPORTED;
+					active = false;
+					continue;
+				}
+				if (r4 & 1) {
+					res = 17; // EEXIST (EBPF_NOEXIST)
+				} else {
+					int f = check(rg, L, r2, 4, false);
+					const uint32_t key = f ? 0 : (uint32_t)load_bytes(r2, 4);
+					if (!f && key < mp.max_entries)
+						f = check(rg, L, r3, mp.value_size, false);
+					if (f) {
+						fault = f;
+						active = false;
+						continue;
+					}
+					if (key < mp.max_entries) {
+						const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t *>(L.upd_log), 1u);
+						if (slot >= L.upd_cap) {
+							fault = F_MEM; // (the host sizes the log: never)
+							active = false;
+							continue;
+						}
+						uint8_t *rec = L.upd_log + 64 + (uint64_t)slot * L.upd_stride;
+						*reinterpret_cast<uint64_t *>(rec) = L.pkt_base + gid;
+						*reinterpret_cast<uint32_t *>(rec + 8) = t | ((uint32_t)e.aux << 20);
+						*reinterpret_cast<uint32_t *>(rec + 12) = key;
+						const uint8_t *v = reinterpret_cast<const uint8_t *>(r3);
+						for (uint32_t b = 0; b < mp.value_size; b++)
+							rec[16 + b] = v[b];
+						res = 0;
+					}
+				}
+			}
+			R[0][tid] = res;
+			continue;
+		}
 		if (k >= DK_MOV64R && k <= DK_MOD32Z) { // standard-eBPF operations
 			const uint64_t d = R[e.dst][tid], s = R[e.src][tid];
 			const uint32_t d32 = (uint32_t)d, s32 = (uint32_t)s;

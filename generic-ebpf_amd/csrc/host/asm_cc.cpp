@@ -1408,7 +1408,7 @@ int
 written_reg(int fam, int d)
 {
 	switch (fam) {
-	case AHF_LOOKUPSTK: case AHF_LOOKUPGEN: case AHF_HLOOKUP:
+	case AHF_LOOKUPSTK: case AHF_LOOKUPGEN: case AHF_HLOOKUP: case AHF_UPDATE:
 		return 0;
 	case AHF_EXIT: case AHF_FAULT: case AHF_NOP:
 	case AHF_STXGEN1: case AHF_STXGEN2: case AHF_STXGEN4: case AHF_STXGEN8:
@@ -1432,6 +1432,7 @@ copied_uses(int fam, int d, int s)
 	case AHF_EXIT: return 1;
 	case AHF_LOOKUPGEN: return (1u << 1) | (1u << 2);
 	case AHF_HLOOKUP: return 1u << 2;
+	case AHF_UPDATE: return (1u << 2) | (1u << 3) | (1u << 4);
 	case AHF_FAULT: case AHF_NOP: case AHF_LOOKUPSTK: return 0;
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8: return 0;
 	case AHF_LDXPKTG1: case AHF_LDXPKTG2: case AHF_LDXPKTG4: case AHF_LDXPKTG8: return 0;

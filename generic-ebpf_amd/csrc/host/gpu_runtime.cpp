@@ -16,6 +16,7 @@
 #include <thread>
 
 #include "internal.h"
+#include "map_writes.h"
 
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
@@ -83,14 +84,21 @@ struct rows_slot {
 	unsigned long long sid = 0; // owning stream's id
 	hipStream_t stream = nullptr;
 	uint64_t last = 0;          // order of the last use
+	// map-writing programs (map_writes.hip): the stream's write log and winner words, grown on
+	// demand (the kernels leave the log's counter and every winner word zero)
+	void *log = nullptr;
+	size_t log_bytes = 0;
+	void *win = nullptr;
+	size_t win_bytes = 0;
 };
 std::mutex g_rows_lock;
-std::vector<std::vector<rows_slot>> g_rows; // per device
+std::vector<std::vector<rows_slot>> g_rows; // per device (capacity kRowsMax: slots never move)
 uint64_t g_rows_tick = 0;
 constexpr size_t kRowsMax = 64;
 
+// The stream's slot (under g_rows_lock), created or taken over as described above.
 int
-rows_acquire(int device, hipStream_t stream, void **out)
+slot_for(int device, hipStream_t stream, rows_slot **out)
 {
 	// (resolved at run time: torch bundles a HIP runtime older than the one this is built on)
 	using get_id_fn = hipError_t (*)(hipStream_t, unsigned long long *);
@@ -99,7 +107,6 @@ rows_acquire(int device, hipStream_t stream, void **out)
 	unsigned long long sid = (unsigned long long)(uintptr_t)stream;
 	if (get_id && get_id(stream, &sid) != hipSuccess)
 		return EIO;
-	std::lock_guard<std::mutex> g(g_rows_lock);
 	if ((int)g_rows.size() <= device)
 		g_rows.resize(device + 1);
 	std::vector<rows_slot> &pool = g_rows[device];
@@ -108,13 +115,14 @@ rows_acquire(int device, hipStream_t stream, void **out)
 		if (r.sid == sid) {
 			r.stream = stream;
 			r.last = ++g_rows_tick;
-			*out = r.p;
+			*out = &r;
 			return 0;
 		}
 		if (!lru || r.last < lru->last)
 			lru = &r;
 	}
 	if (pool.size() < kRowsMax) {
+		pool.reserve(kRowsMax);
 		rows_slot r;
 		if (hipMalloc(&r.p, DP_HIST_PARTIAL_BYTES) != hipSuccess)
 			return ENOMEM;
@@ -126,7 +134,7 @@ rows_acquire(int device, hipStream_t stream, void **out)
 		r.stream = stream;
 		r.last = ++g_rows_tick;
 		pool.push_back(r);
-		*out = r.p;
+		*out = &pool.back();
 		return 0;
 	}
 	hipEvent_t ev;
@@ -140,7 +148,58 @@ rows_acquire(int device, hipStream_t stream, void **out)
 	lru->sid = sid;
 	lru->stream = stream;
 	lru->last = ++g_rows_tick;
-	*out = lru->p;
+	*out = lru;
+	return 0;
+}
+
+int
+rows_acquire(int device, hipStream_t stream, void **out)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		*out = r->p;
+	return err;
+}
+
+// grow a zero-initialised buffer (synchronous: hipFree waits for the device)
+int
+grow_zeroed(void **p, size_t *have, size_t need)
+{
+	if (*have >= need)
+		return 0;
+	if (*p)
+		hipFree(*p);
+	*p = nullptr;
+	*have = 0;
+	if (hipMalloc(p, need) != hipSuccess)
+		return ENOMEM;
+	if (hipMemset(*p, 0, need) != hipSuccess) {
+		hipFree(*p);
+		*p = nullptr;
+		return ENOMEM;
+	}
+	*have = need;
+	return 0;
+}
+
+// The stream's map-write log (>= log_bytes) and winner words (>= win_bytes).
+int
+upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, uint8_t **log,
+	    unsigned long long **win)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		err = grow_zeroed(&r->log, &r->log_bytes, log_bytes);
+	if (!err)
+		err = grow_zeroed(&r->win, &r->win_bytes, win_bytes);
+	if (err)
+		return err;
+	*log = static_cast<uint8_t *>(r->log);
+	*win = static_cast<unsigned long long *>(r->win);
 	return 0;
 }
 
@@ -203,6 +262,13 @@ ensure_translated(struct ebpf_prog *ep)
 }
 
 int
+ensure_translated_locked(struct ebpf_prog *ep)
+{
+	std::lock_guard<std::mutex> g(ep->dlock);
+	return ensure_translated(ep);
+}
+
+int
 ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 {
 	std::lock_guard<std::mutex> g(em->mirror_lock);
@@ -224,6 +290,10 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 {
 	const uint16_t cpu = map_current_cpu();
 	for (struct ebpf_map *em : ep->xlated->maps) {
+		// a batch on another device wrote the map: its writes reach the host copy first
+		const int dd = em->dev_dirty.load(std::memory_order_acquire);
+		if (dd >= 0 && dd != device)
+			map_pull_device_writes(em);
 		std::lock_guard<std::mutex> g(em->mirror_lock);
 		map_mirror &m = em->mirrors[device];
 		uint64_t v = em->version.load();
@@ -300,6 +370,28 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 			return hip_fail(e, "hipMemcpy(map table)");
 	}
 	nd->nmaps = (uint32_t)nd->table.size();
+	if (ep->xlated->max_updates) {
+		// map writes: the apply step's view of the table (map_writes.h), winner words for
+		// every key of every written map, the log record size
+		std::vector<upd_map> um(nd->table.size());
+		uint32_t vmax = 8;
+		for (size_t t = 0; t < nd->table.size(); t++) {
+			um[t].dev_base = nd->table[t].dev_base;
+			um[t].value_size = nd->table[t].value_size;
+			um[t].max_entries = nd->table[t].max_entries;
+			um[t].win_off = nd->win_words;
+			if (std::find(ep->xlated->upd_maps.begin(), ep->xlated->upd_maps.end(), (uint16_t)t) !=
+			    ep->xlated->upd_maps.end()) {
+				nd->win_words += nd->table[t].max_entries;
+				vmax = std::max(vmax, nd->table[t].value_size);
+			}
+		}
+		nd->upd_stride = 16 + ((vmax + 7) & ~7u);
+		if ((e = hipMalloc(&nd->d_upd, um.size() * sizeof(upd_map))) != hipSuccess ||
+		    (e = hipMemcpy(nd->d_upd, um.data(), um.size() * sizeof(upd_map),
+				   hipMemcpyHostToDevice)) != hipSuccess)
+			return hip_fail(e, "map-write table");
+	}
 	dp = std::move(nd);
 	*out = dp.get();
 	return 0;
@@ -350,9 +442,47 @@ asm_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	return 0;
 }
 
+// A device batch's map writes (map_writes.hip): the log its launches share, and where in the
+// batch a launch starts.  The caller that passes a plan applies the log itself after the last
+// launch (the host-buffer path: every chunk of one batch reads the maps as they were at its start).
+struct upd_plan {
+	uint8_t *log = nullptr;
+	unsigned long long *win = nullptr;
+	uint32_t cap = 0;
+	uint64_t pkt_base = 0;
+};
+
+// Log capacity for `count` packets of a map-writing program (records, and bytes).
+int
+upd_size(const struct ebpf_prog *ep, const dprog_device *dp, uint64_t count, uint32_t *cap,
+	 size_t *bytes)
+{
+	const uint64_t rec = count * ep->xlated->max_updates;
+	if (rec > UINT32_MAX)
+		return fail(E2BIG, "map-writing program: more than 2^32 writes in one batch");
+	*cap = (uint32_t)rec;
+	*bytes = 64 + rec * dp->upd_stride;
+	return 0;
+}
+
+// After the batch: the logged writes land in the mirrors (packet order), and the written maps
+// remember that this device's mirror is newer than their host copy.
+int
+upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
+{
+	hipError_t e = launch_map_writes(P.log, P.cap, dp->upd_stride,
+					 static_cast<const upd_map *>(dp->d_upd), P.win, stream);
+	if (e != hipSuccess)
+		return hip_fail(e, "map writes");
+	for (uint16_t t : ep->xlated->upd_maps)
+		map_mark_device_write(ep->xlated->maps[t], dp->device, static_cast<void *>(stream));
+	return 0;
+}
+
 int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
-       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false)
+       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false,
+       const upd_plan *plan = nullptr)
 {
 	dp_launch L = L0;
 	L.maps = dp->d_maps;
@@ -363,6 +493,21 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	if (err)
 		return err;
 	hipError_t e;
+	upd_plan own;
+	if (ep->xlated->max_updates) {
+		if (plan == nullptr) { // this launch is the whole batch: its own log, applied below
+			size_t bytes;
+			if ((err = upd_size(ep, dp, L0.count, &own.cap, &bytes)) ||
+			    (err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &own.log,
+					       &own.win)))
+				return fail(err, "map-write log");
+		}
+		const upd_plan &P = plan ? *plan : own;
+		L.upd_log = P.log;
+		L.upd_cap = P.cap;
+		L.upd_stride = dp->upd_stride;
+		L.pkt_base = P.pkt_base;
+	}
 	const int variant = effective_variant(dp->device);
 	if (variant == 0 || variant == 2) {
 		const int mode =
@@ -419,6 +564,8 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	}
 	if (e != hipSuccess)
 		return hip_fail(e, "kernel launch");
+	if (ep->xlated->max_updates && plan == nullptr)
+		return upd_apply(ep, dp, own, stream);
 	return 0;
 }
 
@@ -520,6 +667,8 @@ prog_release_device_state(struct ebpf_prog *ep)
 				hipFree(dp->d_entries);
 			if (dp->d_maps)
 				hipFree(dp->d_maps);
+			if (dp->d_upd)
+				hipFree(dp->d_upd);
 			for (auto *a : dp->d_asm)
 				if (a)
 					hipFree(a);
@@ -533,10 +682,53 @@ prog_release_device_state(struct ebpf_prog *ep)
 void
 map_release_device_state(struct ebpf_map *em)
 {
+	if (em->wb_event) {
+		hipEventSynchronize(static_cast<hipEvent_t>(em->wb_event));
+		hipEventDestroy(static_cast<hipEvent_t>(em->wb_event));
+		em->wb_event = nullptr;
+	}
 	for (size_t d = 0; d < em->mirrors.size(); d++)
 		if (em->mirrors[d].dev && hipSetDevice((int)d) == hipSuccess)
 			hipFree(em->mirrors[d].dev);
 	em->mirrors.clear();
+}
+
+// The device's mirror now holds the batch's writes: it is the newest copy.  The version moves on
+// so that other devices re-upload (after pulling these writes, sync_map_mirrors) while this
+// device keeps its mirror.
+void
+map_mark_device_write(struct ebpf_map *em, int device, void *stream)
+{
+	std::lock_guard<std::mutex> g(em->mirror_lock);
+	if (em->wb_event == nullptr) {
+		hipEvent_t ev;
+		if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+			return;
+		em->wb_event = ev;
+	}
+	hipEventRecord(static_cast<hipEvent_t>(em->wb_event), static_cast<hipStream_t>(stream));
+	const uint64_t v = em->version.fetch_add(1) + 1;
+	if ((int)em->mirrors.size() > device)
+		em->mirrors[device].version = v;
+	em->dev_dirty.store(device, std::memory_order_release);
+}
+
+void
+map_pull_device_writes(struct ebpf_map *em)
+{
+	if (em->dev_dirty.load(std::memory_order_acquire) < 0)
+		return;
+	std::lock_guard<std::mutex> g(em->mirror_lock);
+	const int d = em->dev_dirty.load(std::memory_order_acquire);
+	if (d < 0 || d >= (int)em->mirrors.size())
+		return;
+	const map_mirror &m = em->mirrors[d];
+	hipEventSynchronize(static_cast<hipEvent_t>(em->wb_event));
+	// array / percpu array: the mirror is the (submitting CPU's) value array
+	uint8_t *dst = const_cast<uint8_t *>(map_array_image(em, em->percpu ? m.cpu : 0));
+	if (dst && m.dev)
+		hipMemcpy(dst, m.dev, (size_t)em->value_size * em->max_entries, hipMemcpyDeviceToHost);
+	em->dev_dirty.store(-1, std::memory_order_release);
 }
 
 EBPF_EXPORT int
@@ -734,6 +926,16 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	    (e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
 		return hip_fail(e, "hipMemsetAsync(hist)");
 	int err;
+	// a map-writing program: one log for the whole shard, applied after its last chunk (every
+	// chunk reads the maps as they were when the batch started)
+	upd_plan plan;
+	if (ep->xlated->max_updates) {
+		size_t bytes;
+		if ((err = upd_size(ep, dp, hi - lo, &plan.cap, &bytes)) ||
+		    (err = upd_acquire(S.device, S.stream[0], bytes, dp->win_words * 8, &plan.log,
+				       &plan.win)))
+			return fail(err, "map-write log");
+	}
 	bool timed[2] = {false, false};
 	// on any error: drain both streams (buffers stay valid for the copies in flight)
 	auto drain = [&](int rc) {
@@ -793,7 +995,8 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 		L.stride = batch->stride;
 		if ((e = hipEventRecord(S.ev[2 * b], st)) != hipSuccess)
 			return drain(hip_fail(e, "hipEventRecord"));
-		if ((err = launch(ep, dp, L, st)))
+		plan.pkt_base = c0;
+		if ((err = launch(ep, dp, L, st, nullptr, nullptr, false, &plan)))
 			return drain(err);
 		if ((e = hipEventRecord(S.ev[2 * b + 1], st)) != hipSuccess)
 			return drain(hip_fail(e, "hipEventRecord"));
@@ -811,6 +1014,12 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	for (int i = 0; i < 2; i++) {
 		if ((e = hipStreamSynchronize(S.stream[i])) != hipSuccess || (e = collect(i)) != hipSuccess)
 			return drain(hip_fail(e, "batch"));
+	}
+	if (ep->xlated->max_updates && hi > lo) {
+		if ((err = upd_apply(ep, dp, plan, S.stream[0])))
+			return drain(err);
+		if ((e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
+			return hip_fail(e, "map writes");
 	}
 	return 0;
 }
@@ -891,6 +1100,9 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 	if (err || (err = check_devices(ndev, devices, false)))
 		return err;
 	auto t0 = std::chrono::steady_clock::now();
+	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
+		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
+					"land in packet order in one mirror)");
 	std::vector<dprog_device *> dps(ndev);
 	std::vector<staging *> S(ndev, nullptr);
 	for (int d = 0; d < ndev && !err; d++)
@@ -950,6 +1162,9 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 	int err = check_devices(ndev, devices, true);
 	if (err)
 		return err;
+	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
+		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
+					"land in packet order in one mirror)");
 	std::vector<hipStream_t> st(ndev);
 	for (int d = 0; d < ndev; d++) {
 		st[d] = streams ? static_cast<hipStream_t>(streams[d]) : nullptr;

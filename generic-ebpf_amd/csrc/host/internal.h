@@ -82,6 +82,10 @@ struct ebpf_map {
 	std::atomic<uint64_t> version{0}; // bumped on every host-side write
 	std::mutex mirror_lock;
 	std::vector<map_mirror> mirrors;  // indexed by device
+	// a device batch wrote the map (map_update_elem): that device's mirror is newer than the
+	// host copy until map_pull_device_writes copies it back (after wb_event, a hipEvent_t)
+	std::atomic<int> dev_dirty{-1};
+	void *wb_event = nullptr;
 	// array-map storage (for device mirroring); null for other map types
 	uint8_t *array_storage() const;
 	bool is_hashtable() const; // hashtable or percpu hashtable
@@ -119,6 +123,9 @@ struct dprog_device {
 	uint32_t jit_stride[2] = {0, 0};
 	int jit_err[2] = {0, 0};                 // E2BIG etc.: run the interpreter instead
 	double build_ms[2] = {0, 0};             // compile (variant 0) or lower + link time, per mode
+	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
+	uint64_t win_words = 0;                  // winner words the apply step needs
+	uint32_t upd_stride = 0;                 // log record bytes
 	int last_exec = -1;                      // ebpf_dexec_info.exec of the last launch
 	int last_layout = -1;                    // its mode
 };
@@ -156,6 +163,8 @@ struct dprog_host {
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
+	uint32_t max_updates = 0;            // most map_update_elem calls on one path (0: none)
+	std::vector<uint16_t> upd_maps;      // table indices of the array maps those calls write
 	int error = 0;
 	std::string error_msg;
 };
@@ -184,5 +193,9 @@ int translate_program(struct ebpf_prog *ep, dprog_host &out);
 
 // gpu_runtime.cpp
 void set_last_error(const std::string &msg);
+// Copy a device batch's map writes back into the host copy (no-op unless em->dev_dirty).
+void map_pull_device_writes(struct ebpf_map *em);
+// A batch on `device` wrote the map (its writes land on `stream`, a hipStream_t).
+void map_mark_device_write(struct ebpf_map *em, int device, void *stream);
 void prog_release_device_state(struct ebpf_prog *ep);
 void map_release_device_state(struct ebpf_map *em);

@@ -1,0 +1,17 @@
+// map_writes.h — shared by the host runtime and map_writes.hip (the apply step of map writes).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// One array map a program writes, as the apply kernels see it.
+struct upd_map {
+	uint64_t dev_base;    // the device mirror
+	uint32_t value_size;
+	uint32_t max_entries;
+	uint64_t win_off;     // first winner word of this map (one u64 per key)
+};
+
+// Apply the log's records to the mirrors (last write per key, packet order) and re-arm the
+// log's counter; `win` holds sum(max_entries) zeroed u64 and is left zero.
+hipError_t launch_map_writes(const uint8_t *log, uint32_t cap, uint32_t stride, const upd_map *maps,
+			     unsigned long long *win, hipStream_t stream);

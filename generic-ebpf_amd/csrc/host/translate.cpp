@@ -14,6 +14,8 @@
 // is the only way the reference spins forever, and becomes an EBPF_FAULT_LOOP entry.
 #include "internal.h"
 
+#include <algorithm>
+
 #include <unordered_map>
 
 namespace {
@@ -314,11 +316,16 @@ struct Translator {
 					make_fault(EBPF_FAULT_HELPER);
 					return;
 				}
-				if (h != &eht_map_lookup_elem) {
+				if (h == &eht_map_lookup_elem) {
+					e.kind = DK_CALL_LOOKUP;
+				} else if (h == &eht_map_update_elem || h == &eht_map_delete_elem) {
+					// resolved against the map table after the dataflow pass
+					e.kind = DK_CALL_UPDATE;
+					e.aux = h == &eht_map_delete_elem ? 1 : 0;
+				} else {
 					make_fault(EBPF_FAULT_HELPER_UNSUPPORTED);
 					return;
 				}
-				e.kind = DK_CALL_LOOKUP;
 				break;
 			}
 			e.imm = jmp32 ? zx : sx;
@@ -431,6 +438,10 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 				if ((uint64_t)r[1].off == (uint64_t)(uintptr_t)out.maps[m])
 					res = mk(AV_MAPVAL_NULL, 0, (int16_t)m);
 		r[0] = res; // r1..r5 keep their values (a plain C call in the reference)
+		return;
+	}
+	if (k == DK_CALL_UPDATE) { // (update or, aux 1 before resolution, delete): an errno
+		r[0] = av();
 		return;
 	}
 	const uint8_t cls = k & 7;
@@ -647,6 +658,85 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 				out.maps.clear();
 				return EOPNOTSUPP;
 			}
+	// Map-writing helpers: the map must be a translation-time constant of the table.  delete
+	// on an array map is EINVAL whatever its arguments (ebpf_map.c delete -> ebpf_map_array.c:
+	// 246-250): a constant; on a hashtable it has no device form.  update keeps its entry,
+	// aux = the map's table index (its routine checks the arguments at run time).
+	for (size_t i = 0; i < out.entries.size(); i++) {
+		dp_entry &e = out.entries[i];
+		if (e.kind != DK_CALL_UPDATE || !out.annot[i].reached)
+			continue;
+		const av &m1 = out.annot[i].in[1];
+		int mi = -1;
+		if (m1.kind == AV_CONST)
+			for (size_t m = 0; m < out.maps.size(); m++)
+				if ((uint64_t)m1.off == (uint64_t)(uintptr_t)out.maps[m])
+					mi = (int)m;
+		if (mi < 0) {
+			out.error = EOPNOTSUPP;
+			out.error_msg = "device batches need the map of every map_update_elem / "
+					"map_delete_elem known at translation time (r1 loaded by LDDW)";
+			out.maps.clear();
+			return EOPNOTSUPP;
+		}
+		if (e.aux == 1) { // delete
+			if (out.maps[mi]->is_hashtable()) {
+				e.kind = DK_FAULT;
+				e.aux = EBPF_FAULT_HELPER_UNSUPPORTED;
+			} else {
+				e.kind = EBPF_OP_LDDW;
+				e.dst = 0;
+				e.imm = EINVAL;
+			}
+			continue;
+		}
+		e.aux = (uint16_t)mi;
+		if (!out.maps[mi]->is_hashtable() &&
+		    std::find(out.upd_maps.begin(), out.upd_maps.end(), (uint16_t)mi) == out.upd_maps.end())
+			out.upd_maps.push_back((uint16_t)mi); // (a hashtable's update faults instead)
+	}
+	// most update calls on one path from the start (the graph is a tree under the reference's
+	// stepping, a DAG under standard semantics): the per-packet bound of the write log
+	{
+		const size_t n = out.entries.size();
+		std::vector<uint32_t> best(n, 0);
+		std::vector<uint8_t> state(n, 0); // 0 new, 1 open, 2 done
+		std::vector<uint32_t> st{out.start};
+		auto succ_of = [&](uint32_t id, int k) -> uint32_t {
+			const dp_entry &e = out.entries[id];
+			if (e.kind == DK_FAULT || e.kind == EBPF_OP_EXIT)
+				return UINT32_MAX;
+			if (k == 0)
+				return e.next;
+			if (e.kind < 0x100 && ((e.kind & 7) == EBPF_CLS_JMP || (e.kind & 7) == DP_CLS_JMP32))
+				return e.target;
+			return UINT32_MAX;
+		};
+		while (!st.empty()) {
+			const uint32_t id = st.back();
+			if (state[id] == 0) {
+				state[id] = 1;
+				for (int k = 0; k < 2; k++) {
+					const uint32_t sx = succ_of(id, k);
+					if (sx < n && state[sx] == 0)
+						st.push_back(sx);
+				}
+				continue;
+			}
+			st.pop_back();
+			if (state[id] == 2)
+				continue;
+			uint32_t m = 0;
+			for (int k = 0; k < 2; k++) {
+				const uint32_t sx = succ_of(id, k);
+				if (sx < n)
+					m = std::max(m, best[sx]);
+			}
+			best[id] = m + (out.entries[id].kind == DK_CALL_UPDATE ? 1u : 0u);
+			state[id] = 2;
+		}
+		out.max_updates = best[out.start];
+	}
 	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
 	// its map while a later batch may still read it.
 	for (struct ebpf_map *m : out.maps)

@@ -23,7 +23,7 @@ EBPF_HIST_BINS = 257
 
 MAP_TYPE_ARRAY, MAP_TYPE_PERCPU_ARRAY, MAP_TYPE_HASHTABLE, MAP_TYPE_PERCPU_HASHTABLE = range(4)
 SEM_REFERENCE, SEM_STANDARD = 0, 1
-HELPER_LOOKUP, HELPER_UPDATE, HELPER_DELETE = range(3)
+HELPER_LOOKUP, HELPER_UPDATE, HELPER_DELETE, HELPER_OTHER = range(4)
 EBPF_ANY, EBPF_NOEXIST, EBPF_EXIST = 0, 1, 2
 
 FAULT_NAMES = ["NONE", "BAD_OPCODE", "DIV_ZERO", "MEM", "SLOT", "HELPER", "HELPER_UNSUPPORTED",
@@ -47,6 +47,10 @@ _PREDFN = ctypes.CFUNCTYPE(ctypes.c_bool, ctypes.c_void_p)
 class ProgType(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * EBPF_NAME_MAX), ("is_map_usable", _PREDFN),
                 ("is_helper_usable", _PREDFN)]
+
+
+class HelperType(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * EBPF_NAME_MAX), ("fn", ctypes.c_void_p)]
 
 
 class Config(ctypes.Structure):
@@ -165,11 +169,14 @@ _always = _PREDFN(lambda _p: True)
 
 
 class Env:
-    """ebpf_env with the reference test suite's configuration (tests/test_common.hpp:59-75)."""
+    """ebpf_env with the reference test suite's configuration (tests/test_common.hpp:59-75),
+    plus helper 3: a helper with no device implementation (CALL 3 faults HELPER_UNSUPPORTED
+    on the device)."""
 
     def __init__(self, helpers=None):
         L = lib()
         self._ptype = ProgType(b"test", _always, _always)
+        self._other = HelperType(b"other", None)
         self.config = Config()
         self.config.prog_types[0] = ctypes.addressof(self._ptype)
         for i, s in enumerate(["emt_array", "emt_percpu_array", "emt_hashtable",
@@ -178,7 +185,8 @@ class Env:
         hl = helpers if helpers is not None else {
             HELPER_LOOKUP: addr_of("eht_map_lookup_elem"),
             HELPER_UPDATE: addr_of("eht_map_update_elem"),
-            HELPER_DELETE: addr_of("eht_map_delete_elem")}
+            HELPER_DELETE: addr_of("eht_map_delete_elem"),
+            HELPER_OTHER: ctypes.addressof(self._other)}
         for i, a in hl.items():
             self.config.helper_types[i] = a
         self.ptr = ctypes.c_void_p()

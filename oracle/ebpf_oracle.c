@@ -10,6 +10,7 @@
  */
 #include "ebpf_oracle.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #ifdef _OPENMP
@@ -241,6 +242,123 @@ helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_
 	return (uint64_t)(uintptr_t)(m->data + (uint64_t)m->value_size * k);
 }
 
+/* ---- map-writing helpers, device-batch semantics (ebpf_oracle.h) ---- */
+struct wrec {
+	uint64_t pkt;
+	uint32_t seq;
+	uint32_t map;
+	uint32_t key;
+	uint64_t voff; /* value bytes in the log's arena */
+};
+struct wlog {
+	struct wrec *rec;
+	size_t n, cap;
+	uint8_t *arena;
+	size_t used, arena_cap;
+};
+static __thread struct wlog *t_wlog; /* set by oracle_run_batch per thread */
+static __thread uint64_t t_pkt;
+static __thread uint32_t t_seq;
+
+static void
+wlog_push(uint32_t map, uint32_t key, const uint8_t *value, uint32_t vs)
+{
+	struct wlog *w = t_wlog;
+	if (w == NULL)
+		return; /* single-packet oracle_run: the write is not kept */
+	if (w->n == w->cap) {
+		w->cap = w->cap ? 2 * w->cap : 1024;
+		w->rec = realloc(w->rec, w->cap * sizeof(*w->rec));
+	}
+	if (w->used + vs > w->arena_cap) {
+		w->arena_cap = (w->arena_cap ? 2 * w->arena_cap : 65536) + vs;
+		w->arena = realloc(w->arena, w->arena_cap);
+	}
+	memcpy(w->arena + w->used, value, vs);
+	w->rec[w->n++] = (struct wrec){t_pkt, t_seq++, map, key, w->used};
+	w->used += vs;
+}
+
+static const struct oracle_map *
+find_map(const struct oracle_prog *p, uint64_t handle, uint32_t *idx)
+{
+	for (uint32_t i = 0; i < p->nmaps; i++)
+		if (p->maps[i].handle == handle) {
+			*idx = i;
+			return &p->maps[i];
+		}
+	return NULL;
+}
+
+/* ebpf_map_update_elem (ebpf_map.c:101-108) -> array_map_update_elem (ebpf_map_array.c:185-211) */
+static inline uint64_t
+helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, uint64_t r3,
+		  uint64_t r4, int *fault)
+{
+	if (r1 == 0 || r2 == 0 || r3 == 0 || r4 > 2) /* EBPF_EXIST = 2 */
+		return 22;                             /* EINVAL */
+	uint32_t mi;
+	const struct oracle_map *m = find_map(re->p, r1, &mi);
+	if (m == NULL) {
+		*fault = F_BAD_MAP;
+		return 0;
+	}
+	if (m->kind == ORACLE_MAP_HASH) {
+		*fault = F_HELPER_UNSUPPORTED;
+		return 0;
+	}
+	if (r4 & 1)  /* EBPF_NOEXIST: every key of an array exists */
+		return 17; /* EEXIST */
+	if (checked && (*fault = check_access(re, r2, 4, 0)))
+		return 0;
+	const uint32_t k = (uint32_t)load_n(r2, 4);
+	if (k >= m->max_entries)
+		return 22;
+	if (checked && (*fault = check_access(re, r3, m->value_size, 0)))
+		return 0;
+	wlog_push(mi, k, (const uint8_t *)(uintptr_t)r3, m->value_size);
+	return 0;
+}
+
+/* ebpf_map_delete_elem (ebpf_map.c) -> array_map_delete_elem (ebpf_map_array.c:246-250) */
+static inline uint64_t
+helper_map_delete(const struct region_env *re, uint64_t r1, int *fault)
+{
+	uint32_t mi;
+	const struct oracle_map *m = r1 ? find_map(re->p, r1, &mi) : NULL;
+	if (r1 && m == NULL) {
+		*fault = F_BAD_MAP;
+		return 0;
+	}
+	if (m && m->kind == ORACLE_MAP_HASH) {
+		*fault = F_HELPER_UNSUPPORTED;
+		return 0;
+	}
+	return 22; /* EINVAL: NULL map / key, or an array map (no delete) */
+}
+
+/* CALL :282-284 — helper id imm of the configured table */
+static inline uint64_t
+helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_t *reg, int *fault)
+{
+	const struct oracle_prog *p = re->p;
+	if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
+		*fault = F_HELPER;
+		return 0;
+	}
+	switch (p->helper_kind[imm]) {
+	case ORACLE_HELPER_MAP_LOOKUP:
+		return helper_map_lookup(re, checked, reg[1], reg[2], fault);
+	case ORACLE_HELPER_MAP_UPDATE:
+		return helper_map_update(re, checked, reg[1], reg[2], reg[3], reg[4], fault);
+	case ORACLE_HELPER_MAP_DELETE:
+		return helper_map_delete(re, reg[1], fault);
+	default:
+		*fault = F_HELPER_UNSUPPORTED;
+		return 0;
+	}
+}
+
 static inline uint64_t
 run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
 	uint64_t *steps_out)
@@ -385,15 +503,9 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		case 0xdd: taken = (int64_t)D <= (int64_t)S; break;
 		case 0xd5: taken = (int64_t)D <= (int64_t)IS; break;
 		case 0x85: {                                                /* :282-284 CALL */
-			if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
-				fault = F_HELPER;
-				break;
-			}
-			if (p->helper_kind[imm] != ORACLE_HELPER_MAP_LOOKUP) {
-				fault = F_HELPER_UNSUPPORTED;
-				break;
-			}
-			reg[0] = helper_map_lookup(&re, checked, reg[1], reg[2], &fault);
+			uint64_t r = helper_call(&re, checked, imm, reg, &fault);
+			if (!fault)
+				reg[0] = r;
 			break;
 		}
 		case 0x95: r0 = reg[0]; goto done;                          /* :285-286 EXIT */
@@ -633,17 +745,12 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		case 0xc5: taken = (int64_t)D < (int64_t)IS; break;
 		case 0xdd: taken = (int64_t)D <= (int64_t)S; break;
 		case 0xd5: taken = (int64_t)D <= (int64_t)IS; break;
-		case 0x85:
-			if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
-				fault = F_HELPER;
-				break;
-			}
-			if (p->helper_kind[imm] != ORACLE_HELPER_MAP_LOOKUP) {
-				fault = F_HELPER_UNSUPPORTED;
-				break;
-			}
-			reg[0] = helper_map_lookup(&re, checked, reg[1], reg[2], &fault);
+		case 0x85: {
+			uint64_t r = helper_call(&re, checked, imm, reg, &fault);
+			if (!fault)
+				reg[0] = r;
 			break;
+		}
 		case 0x95: r0 = reg[0]; goto done;
 		case 0x71: msize = 1; goto ldx;
 		case 0x69: msize = 2; goto ldx;
@@ -835,7 +942,7 @@ run_raw(const struct oracle_prog *p, uint8_t *pkt, uint64_t *steps_out)
 		case 0xdd: JMPIF((int64_t)RD <= (int64_t)RS);
 		case 0x85: {
 			int f = 0;
-			reg[0] = helper_map_lookup(&re, 0, reg[1], reg[2], &f);
+			reg[0] = helper_call(&re, 0, ip->imm, reg, &f);
 			break;
 		}
 		case 0x95:
@@ -881,6 +988,15 @@ oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fau
 	return r;
 }
 
+static int
+wrec_cmp(const void *a, const void *b)
+{
+	const struct wrec *x = a, *y = b;
+	if (x->pkt != y->pkt)
+		return x->pkt < y->pkt ? -1 : 1;
+	return x->seq < y->seq ? -1 : (x->seq > y->seq);
+}
+
 uint64_t
 oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *offsets,
 		 uint64_t count, uint32_t stride, uint64_t *ret, uint8_t *faults, int nthreads)
@@ -888,25 +1004,72 @@ oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *off
 	uint64_t total = 0;
 	if (nthreads <= 0)
 		nthreads = 1;
+	int writes = 0;
+	for (int i = 0; i < 64; i++)
+		writes |= p->helper_kind[i] == ORACLE_HELPER_MAP_UPDATE;
+	struct wlog *logs = writes ? calloc((size_t)nthreads, sizeof(struct wlog)) : NULL;
 #ifdef _OPENMP
-#pragma omp parallel for num_threads(nthreads) schedule(static) reduction(+ : total)
+#pragma omp parallel num_threads(nthreads) reduction(+ : total)
 #endif
-	for (int64_t i = 0; i < (int64_t)count; i++) {
-		uint8_t *pkt;
-		uint64_t len;
-		if (offsets) {
-			pkt = data + offsets[i];
-			len = offsets[i + 1] - offsets[i];
-		} else {
-			pkt = data + (uint64_t)i * stride;
-			len = stride;
+	{
+#ifdef _OPENMP
+		const int tid = omp_get_thread_num();
+#else
+		const int tid = 0;
+#endif
+		t_wlog = logs ? &logs[tid] : NULL;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+		for (int64_t i = 0; i < (int64_t)count; i++) {
+			uint8_t *pkt;
+			uint64_t len;
+			if (offsets) {
+				pkt = data + offsets[i];
+				len = offsets[i + 1] - offsets[i];
+			} else {
+				pkt = data + (uint64_t)i * stride;
+				len = stride;
+			}
+			uint8_t f = 0;
+			uint64_t st = 0;
+			t_pkt = (uint64_t)i;
+			t_seq = 0;
+			size_t n0 = t_wlog ? t_wlog->n : 0;
+			ret[i] = oracle_run(p, pkt, len, &f, &st);
+			if (f && t_wlog) /* a packet that faults leaves no write behind */
+				t_wlog->n = n0;
+			if (faults)
+				faults[i] = f;
+			total += st;
 		}
-		uint8_t f = 0;
-		uint64_t st = 0;
-		ret[i] = oracle_run(p, pkt, len, &f, &st);
-		if (faults)
-			faults[i] = f;
-		total += st;
+		t_wlog = NULL;
+	}
+	if (logs) {
+		/* after the batch: every write in packet order (last writer of a key wins) */
+		size_t n = 0;
+		for (int t = 0; t < nthreads; t++)
+			n += logs[t].n;
+		struct wrec *all = malloc((n ? n : 1) * sizeof(*all));
+		size_t k = 0;
+		for (int t = 0; t < nthreads; t++)
+			for (size_t j = 0; j < logs[t].n; j++) {
+				all[k] = logs[t].rec[j];
+				all[k].voff = (uint64_t)(uintptr_t)(logs[t].arena + logs[t].rec[j].voff);
+				k++;
+			}
+		qsort(all, n, sizeof(*all), wrec_cmp);
+		for (size_t j = 0; j < n; j++) {
+			const struct oracle_map *m = &p->maps[all[j].map];
+			memcpy(m->data + (uint64_t)m->value_size * all[j].key,
+			       (const void *)(uintptr_t)all[j].voff, m->value_size);
+		}
+		free(all);
+		for (int t = 0; t < nthreads; t++) {
+			free(logs[t].rec);
+			free(logs[t].arena);
+		}
+		free(logs);
 	}
 	return total;
 }

@@ -12,7 +12,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-HELPER_UNSET, HELPER_MAP_LOOKUP, HELPER_OTHER = 0, 1, 2
+HELPER_UNSET, HELPER_MAP_LOOKUP, HELPER_OTHER, HELPER_MAP_UPDATE, HELPER_MAP_DELETE = 0, 1, 2, 3, 4
+# the engine's Env (generic_ebpf_amd.native): helpers 0..2 = lookup / update / delete as in the
+# reference tests' config (tests/test_common.hpp:69-73), 3 = a helper with no device form
+DEFAULT_HELPER_KINDS = {0: HELPER_MAP_LOOKUP, 1: HELPER_MAP_UPDATE, 2: HELPER_MAP_DELETE,
+                        3: HELPER_OTHER}
 
 
 class _Map(ctypes.Structure):
@@ -128,7 +132,7 @@ class OracleProgram:
         self.p = _Prog()
         self.p.insns = self.code.ctypes.data
         self.p.nslots = len(self.code) // 8
-        kinds = helper_kinds or {0: HELPER_MAP_LOOKUP, 1: HELPER_OTHER, 2: HELPER_OTHER}
+        kinds = helper_kinds or DEFAULT_HELPER_KINDS
         for i, v in kinds.items():
             self.p.helper_kind[i] = v
         self.p.maps = ctypes.addressof(self.maps_arr)
@@ -140,7 +144,9 @@ class OracleProgram:
 
     def run(self, data, count, stride=0, offsets=None, nthreads=1):
         """Runs in place on a COPY of ``data``; returns (ret u64[count], faults u8[count],
-        data_after u8[...], executed_instructions)."""
+        data_after u8[...], executed_instructions).  Map writes (map_update_elem) are applied
+        to this object's array-map data after the batch, in packet order (ebpf_oracle.h);
+        ``map_bytes(k)`` reads them back."""
         work = np.ascontiguousarray(np.array(data, dtype=np.uint8, copy=True).reshape(-1))
         ret = np.zeros(count, dtype=np.uint64)
         faults = np.zeros(count, dtype=np.uint8)
@@ -150,6 +156,10 @@ class OracleProgram:
                                        count, stride, ret.ctypes.data, faults.ctypes.data,
                                        nthreads)
         return ret, faults, work, int(steps)
+
+    def map_bytes(self, k):
+        """Current bytes of map k (array maps: max_entries * value_size)."""
+        return self.map_data[k].tobytes()
 
     def run_inplace(self, data, count, stride, offsets, ret, faults=None, nthreads=1):
         """Timed form for bench.py's cpu_baseline: runs on ``data`` itself (packet stores land

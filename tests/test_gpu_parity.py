@@ -66,7 +66,7 @@ def _fault_programs():
                                      I("ldxw", 0, 3, 0), I("exit")]).code,
         "slot": e(O["mov_imm"], 0, imm=1) + e(O["mov_imm"], 0, imm=2),
         "helper_unset": e(O["call"], imm=9) + e(O["exit"]),
-        "helper_unsupported": e(O["call"], imm=1) + e(O["exit"]),
+        "helper_unsupported": e(O["call"], imm=3) + e(O["exit"]),
         "bad_reg": e(O["mov_imm"], 11, imm=1) + e(O["exit"]),
         "loop": e(O["ja"], off=-1) + e(O["exit"]),
         "bad_map": layout.assemble([layout.LdDw(1, 0x1234), I("mov_imm", 2, imm=8),

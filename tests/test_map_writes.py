@@ -1,0 +1,283 @@
+"""Map writes in a device batch (§8(f) rank 4, write side; include/ebpf_gpu.h "Map writes in a
+device batch"): map_update_elem / map_delete_elem called by the program.
+
+Semantics (the oracle's ORACLE_HELPER_MAP_UPDATE mode, oracle/ebpf_oracle.h): every packet reads
+the maps as they were when the batch started; an update returns the reference's code
+(ebpf_map.c:101-108 -> ebpf_map_array.c:185-211: EINVAL for a NULL key / value or flags >
+EBPF_EXIST, EEXIST for EBPF_NOEXIST, EINVAL for a key >= max_entries, else 0) and its write
+lands after the batch in packet order (within a packet in call order); delete on an array map
+is EINVAL (ebpf_map_array.c:246-250).  Hashtable maps: both helpers fault HELPER_UNSUPPORTED.
+
+CPU tests pin the oracle mode with hand-computed answers and check the translator; GPU tests
+compare every device variant (results, faults and the map's contents after the batch, read back
+through the host API) with the oracle."""
+import errno
+
+import numpy as np
+import pytest
+
+import goldens
+import pyoracle
+from helpers import make_maps
+
+R0, R1, R2, R3, R4, R5, R6, R7, R8, R9, R10 = range(11)
+NKEYS = 16
+
+
+def _nodes():
+    from generic_ebpf_amd import isa, layout
+    return isa.Insn, layout.LdDw, layout.MapRef, layout.Branch
+
+
+def prog_static(second_update=False):
+    """key = pkt[0] & 31 (half the keys out of range), flags = pkt[1] & 3 (3: EINVAL),
+    value = pkt[8..16) — key and value on the stack at known offsets; then a lookup of the same
+    key (the batch's snapshot) and r0 = value ^ rc (or 1000 + rc when the key is out of range).
+    ``second_update``: a second update of the same key in the packet (value + 1, flags 0)."""
+    from generic_ebpf_amd import layout
+    I, LdDw, MapRef, Branch = _nodes()
+    n = [I("ldxb", R6, R1, 0), I("ldxb", R7, R1, 1), I("ldxdw", R8, R1, 8),
+         I("and_imm", R6, imm=31), I("and_imm", R7, imm=3),
+         I("stxw", R10, R6, -4), I("stxdw", R10, R8, -16),
+         LdDw(R1, MapRef(0)),
+         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+         I("mov_imm", R3, imm=0), I("mov64_reg", R3, R10), I("add64_imm", R3, imm=-16),
+         I("mov_imm", R4, imm=0), I("mov64_reg", R4, R7),
+         I("call", imm=1),
+         I("mov_imm", R9, imm=0), I("mov64_reg", R9, R0)]
+    if second_update:
+        n += [I("add64_imm", R8, imm=1), I("stxdw", R10, R8, -16), I("mov_imm", R4, imm=0),
+              I("call", imm=1), I("lsh64_imm", R0, imm=8), I("or64_reg", R9, R0)]
+    n += [LdDw(R1, MapRef(0)),
+          I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+          I("call", imm=0),
+          Branch(I("jeq_imm", R0, imm=0), [I("mov_imm", R0, imm=1000), I("add64_reg", R0, R9),
+                                           I("exit")]),
+          I("ldxdw", R0, R0, 0), I("xor64_reg", R0, R9), I("exit")]
+    return layout.assemble(n)
+
+
+def prog_generic():
+    """The key pointer is r10 - 4 times (pkt[2] & 1) — NULL for even bytes (EINVAL, nothing
+    read), a stack pointer of unknown provenance otherwise — and the value is read straight from
+    the packet (r3 = r1 + 16); then delete (EINVAL on an array) and r0 = rc | delete << 8."""
+    from generic_ebpf_amd import layout
+    I, LdDw, MapRef, Branch = _nodes()
+    n = [I("ldxb", R6, R1, 0), I("and_imm", R6, imm=15), I("stxw", R10, R6, -4),
+         I("ldxb", R5, R1, 2), I("and_imm", R5, imm=1),
+         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+         I("mul64_reg", R2, R5),
+         I("mov_imm", R3, imm=0), I("mov64_reg", R3, R1), I("add64_imm", R3, imm=16),
+         LdDw(R1, MapRef(0)), I("mov_imm", R4, imm=0),
+         I("call", imm=1), I("mov_imm", R9, imm=0), I("mov64_reg", R9, R0),
+         LdDw(R1, MapRef(0)),
+         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+         I("call", imm=2), I("lsh64_imm", R0, imm=8), I("or64_reg", R0, R9), I("exit")]
+    return layout.assemble(n)
+
+
+def prog_hash_update():
+    """An update on a hashtable map: HELPER_UNSUPPORTED on the device (and in the oracle)."""
+    from generic_ebpf_amd import layout
+    I, LdDw, MapRef, Branch = _nodes()
+    n = [I("ldxw", R6, R1, 0), I("stxw", R10, R6, -4), I("stxdw", R10, R6, -16),
+         LdDw(R1, MapRef(0)),
+         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+         I("mov_imm", R3, imm=0), I("mov64_reg", R3, R10), I("add64_imm", R3, imm=-16),
+         I("mov_imm", R4, imm=0), I("call", imm=1), I("exit")]
+    return layout.assemble(n)
+
+
+def _map_init(seed=5):
+    return np.random.default_rng(seed).integers(0, 2**63, NKEYS, dtype=np.uint64).tobytes()
+
+
+def _packets(n, seed):
+    from generic_ebpf_amd import workloads
+    return workloads.packets_random(n, 64, seed=seed)
+
+
+def _expect_static(pk, init, second=False):
+    """Hand computation of prog_static over packets pk (n x 64) on a map holding ``init``."""
+    vals = np.frombuffer(init, dtype=np.uint64).copy()
+    snap = vals.copy()
+    ret = []
+    for p in pk:
+        key, flags = int(p[0]) & 31, int(p[1]) & 3
+        value = int(np.frombuffer(p[8:16].tobytes(), dtype=np.uint64)[0])
+        rc = 22 if flags == 3 else 17 if flags & 1 else (22 if key >= NKEYS else 0)
+        if rc == 0:
+            vals[key] = value
+        if second:
+            rc2 = 22 if key >= NKEYS else 0
+            if rc2 == 0:
+                vals[key] = (value + 1) & 0xffffffffffffffff
+            rc |= rc2 << 8
+        ret.append(1000 + rc if key >= NKEYS else int(snap[key]) ^ rc)
+    return np.array(ret, dtype=np.uint64), vals.tobytes()
+
+
+@pytest.mark.parametrize("second", [False, True])
+def test_oracle_deferred_update_known_answers(second):
+    """The oracle's batch mode against the hand computation: return codes, the snapshot seen by
+    the lookup, and the map after the batch (last writer in packet order wins)."""
+    n = 3000
+    pk = _packets(n, 11)
+    init = _map_init()
+    lay = prog_static(second)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    ret, faults, _, _ = op.run(pk, n, 64, nthreads=4)
+    want, after = _expect_static(pk, init, second)
+    assert not faults.any()
+    np.testing.assert_array_equal(ret, want)
+    assert op.map_bytes(0) == after
+
+
+def test_oracle_generic_pointers_and_delete():
+    n = 2000
+    pk = _packets(n, 12)
+    init = _map_init(6)
+    lay = prog_generic()
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    ret, faults, _, _ = op.run(pk, n, 64, nthreads=4)
+    assert not faults.any()
+    vals = np.frombuffer(init, dtype=np.uint64).copy()
+    for i, p in enumerate(pk):
+        rc = 0 if p[2] & 1 else 22
+        assert int(ret[i]) == (22 << 8) | rc
+        if rc == 0:
+            vals[int(p[0]) & 15] = np.frombuffer(p[16:24].tobytes(), dtype=np.uint64)[0]
+    assert op.map_bytes(0) == vals.tobytes()
+
+
+def test_oracle_hash_update_faults():
+    lay = prog_hash_update()
+    spec = pyoracle.HashSpec(4, 8, items=[(b"\0\0\0\0", b"\1" * 8)])
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [spec])
+    ret, faults, _, _ = op.run(_packets(64, 3), 64, 64)
+    assert (faults == 6).all() and not ret.any()
+
+
+def test_translation_of_map_writes(native, env):
+    """The translator accepts update / delete with an LDDW-known map (device info works, the
+    compiled code builds) and refuses one whose map is known only at run time."""
+    from generic_ebpf_amd import isa
+    for lay in (prog_static(), prog_static(True), prog_generic()):
+        m = native.Map(env, NKEYS, 8)
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle]))
+        try:
+            p.info()
+            assert len(p.device_code(1)) > 0 and len(p.device_code(0)) > 0
+        finally:
+            p.destroy()
+            m.destroy()
+    e, O = isa.encode, isa.OPS
+    p = native.Prog(env, e(O["call"], imm=1) + e(O["exit"]))   # r1 = the packet, not a map
+    try:
+        with pytest.raises(native.EbpfError) as ei:
+            p.info()
+        assert ei.value.code == errno.EOPNOTSUPP
+    finally:
+        p.destroy()
+
+
+def _run_device(gpu, env, lay, maps_spec, pk, variant, resident):
+    import torch
+    n = len(pk)
+    case = goldens.Case("w", lay.code, lay.relocs, maps_spec, pk.reshape(-1), n, 64, None)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        gpu.set_variant(variant)
+        if resident:
+            dev = torch.device("cuda:0")
+            d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+            d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+            d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, d_flt.data_ptr(),
+                            None, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            ret, faults = d_ret.cpu().numpy().view(np.uint64), d_flt.cpu().numpy()
+        else:
+            ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        after = b"".join(maps[0].lookup(k)[1] for k in range(maps[0].max_entries))
+        return ret, faults, after
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("resident", [False, True])
+@pytest.mark.parametrize("which", ["static", "static2", "generic"])
+def test_device_map_writes_vs_oracle(gpu, env, variant, resident, which):
+    n = (1 << 18) + 77
+    pk = _packets(n, 21)
+    init = _map_init(7)
+    lay = {"static": prog_static, "static2": lambda: prog_static(True),
+           "generic": prog_generic}[which]()
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    want, wf, _, _ = op.run(pk, n, 64, nthreads=16)
+    ret, faults, after = _run_device(gpu, env, lay, [(8, NKEYS, init)], pk, variant, resident)
+    np.testing.assert_array_equal(faults, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == op.map_bytes(0)
+
+
+@pytest.mark.gpu
+def test_device_map_writes_across_batches(gpu, env):
+    """Batch 2 reads what batch 1 wrote (on the device, without a host round trip); a host
+    update between batches wins over the device's earlier write."""
+    import torch
+    n = 1 << 16
+    lay = prog_static()
+    init = _map_init(8)
+    pk1, pk2 = _packets(n, 31), _packets(n, 32)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    w1, _, _, _ = op.run(pk1, n, 64, nthreads=16)
+    op.maps_arr[0].data  # (the oracle's map now holds batch 1's writes)
+    mid = bytearray(op.map_bytes(0))
+    mid[3 * 8:4 * 8] = (12345).to_bytes(8, "little")          # host write between the batches
+    op2 = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, bytes(mid))])
+    w2, _, _, _ = op2.run(pk2, n, 64, nthreads=16)
+    case = goldens.Case("w", lay.code, lay.relocs, [(8, NKEYS, init)], pk1.reshape(-1), n, 64, None)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        st = torch.cuda.current_stream().cuda_stream
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        for pk, want, host_write in ((pk1, w1, True), (pk2, w2, False)):
+            d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+            if host_write:
+                assert maps[0].update(3, (12345).to_bytes(8, "little")) == 0
+        after = b"".join(maps[0].lookup(k)[1] for k in range(NKEYS))
+        assert after == op2.map_bytes(0)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 2])
+def test_device_hash_update_faults(gpu, env, variant):
+    lay = prog_hash_update()
+    hm = gpu.HashMap(env, 4, 8, 16)
+    hm.fill(np.zeros((1, 4), np.uint8), np.ones((1, 8), np.uint8))
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [hm.handle]))
+    try:
+        gpu.set_variant(variant)
+        pk = _packets(256, 4)
+        ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), 256, 64)
+        assert (faults == 6).all() and not ret.any()
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        hm.destroy()

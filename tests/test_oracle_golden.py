@@ -56,7 +56,7 @@ def test_oracle_fault_codes():
     assert run(e(O["ldxw"], 0, 1, 62) + e(O["exit"])) == 3                   # past 64 B
     assert run(e(O["mov_imm"], 0, imm=1) + e(O["mov_imm"], 0, imm=2)) == 4   # falls off
     assert run(e(O["call"], imm=5) + e(O["exit"])) == 5                      # unset helper
-    assert run(e(O["call"], imm=1) + e(O["exit"])) == 6                      # update helper
+    assert run(e(O["call"], imm=3) + e(O["exit"])) == 6                      # no device form
     assert run(e(O["mov_imm"], 12, imm=1) + e(O["exit"])) == 7               # r12
     assert run(e(O["ja"], off=-1) + e(O["exit"])) == 8                       # (0,1) self-loop
     from generic_ebpf_amd import layout
