@@ -31,6 +31,25 @@ extern "C" {
 struct ebpf_prog;
 struct ebpf_map;
 
+/* Map writes in a device batch.  The reference runs packets one at a time, so a program's
+ * map_update_elem (ebpf_map.c:101-108 -> ebpf_map_array.c:185-211) is seen by the next packet.
+ * A device batch runs its packets at once; its defined semantics are those of the caller's
+ * loop with the writes held back until the loop ends:
+ *   - every packet reads the maps as they were when the batch started (its own writes too);
+ *   - map_update_elem returns the reference's code: EINVAL for a NULL key or value or flags >
+ *     EBPF_EXIST, EEXIST for EBPF_NOEXIST (an array's keys all exist), EINVAL for a key >=
+ *     max_entries, else 0;
+ *   - after the batch the writes land in packet order, a packet's own in call order: the last
+ *     write of a key wins;
+ *   - map_delete_elem on an array map returns EINVAL (ebpf_map_array.c:246-250);
+ *   - on a hashtable map both helpers fault EBPF_FAULT_HELPER_UNSUPPORTED;
+ *   - the map of every write must be known at translation time (r1 loaded by LDDW), else the
+ *     batch functions return EOPNOTSUPP; a writing program runs its batch on one device
+ *     (the multi-device calls return EOPNOTSUPP).
+ * The written values live in the device's mirror of the map until the host API touches the map
+ * (lookup / update / delete / get_next_key, or a helper call from ebpf_prog_run), which copies
+ * them back first.  ebpf_prog_run itself keeps the reference's immediate writes. */
+
 /* Per-packet fault codes (0 = the program reached EXIT). */
 enum ebpf_fault {
 	EBPF_FAULT_NONE = 0,
@@ -39,10 +58,12 @@ enum ebpf_fault {
 	EBPF_FAULT_MEM = 3,          /* load/store outside this packet, its stack or a map value */
 	EBPF_FAULT_SLOT = 4,         /* stepping left the program (reference reads past the buffer) */
 	EBPF_FAULT_HELPER = 5,       /* CALL id outside [0,64) or an unset helper slot (:283) */
-	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation */
+	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation (incl. map writes
+	                                      to a hashtable: see "Map writes in a device batch") */
 	EBPF_FAULT_BAD_REG = 7,      /* dst/src register nibble >= 11 (reference overflows reg[]) */
 	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns */
-	EBPF_FAULT_MAP_WRITE = 9,    /* store into array-map value memory (read-only during a batch) */
+	EBPF_FAULT_MAP_WRITE = 9,    /* store into map value memory through a lookup result (values
+	                                change only through map_update_elem during a batch) */
 	EBPF_FAULT_BAD_MAP = 10,     /* map helper called with r1 not a map of this program's env */
 	EBPF_FAULT_MAX
 };
