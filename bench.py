@@ -75,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--pmc-dir", default="", help="where the PMC passes write (default: a temp dir)")
     ap.add_argument("--time-every", type=int, default=10,
                     help="event-time the kernel of every k-th timed step (default 10: each event pair is a GPU-side marker, C2 steps with a pair every 5th step took 14.2 us against 12.9 us with none; profiles/r02/ab_event)")
+    ap.add_argument("--sync-each", action="store_true",
+                    help="diagnostics: synchronise after every step (launches never queue)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)
@@ -391,6 +393,8 @@ def main():
                 native.time_next_launch(ev[0].cuda_event, ev[1].cuda_event)
             launch(hptr[b])
         red.issue(b)
+        if a.sync_each:
+            torch.cuda.synchronize()
 
     for i in range(a.warmup):
         step(i)

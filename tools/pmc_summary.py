@@ -2,8 +2,8 @@
 """Summarise tools/pmc.sh output: per-dispatch averages of each counter for the interpreter
 kernel, HBM traffic per launch with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md,
 HBM section: FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read; FETCH_SIZE /
-WRITE_SIZE are in KiB).  Writes profiles/<round>/pmc_<cfg>.json and, with --install,
-profiles/pmc_<cfg>.json (read by bench.py for roofline.traffic)."""
+WRITE_SIZE are in KiB).  Writes profiles/<round>/pmc_<cfg>.json.  (bench.py measures its own
+roofline.traffic with two rocprofv3 --pmc child passes; this summarises wider counter sets.)"""
 import csv
 import glob
 import json
@@ -32,7 +32,6 @@ def load(d):
 def main():
     T, rnd = sys.argv[1], sys.argv[2]
     cfgs = sys.argv[3:]
-    install = "--install" in cfgs
     cfgs = [c for c in cfgs if not c.startswith("--")]
     for cfg in cfgs:
         c = {}
@@ -71,10 +70,8 @@ def main():
                     out[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
         out["note"] = note
         os.makedirs(os.path.join(ROOT, "profiles", rnd), exist_ok=True)
-        for path in [os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % cfg)] + (
-                [os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg)] if install else []):
-            with open(path, "w") as f:
-                json.dump(out, f, indent=1)
+        with open(os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % cfg), "w") as f:
+            json.dump(out, f, indent=1)
         print(cfg, json.dumps({k: v for k, v in out.items() if k != "counters_per_dispatch"}))
         print("  ", {k: round(v) for k, v in c.items()})
 
