@@ -70,7 +70,7 @@ struct dp_map {
 	uint32_t flags;       // DP_MAP_HASH | log2(stride) << 16 | key_size (hashtable), else 0
 };
 #define DP_MAP_HASH 0x80000000u
-#define DP_HASH_MAX_KEY 256u
+#define DP_HASH_MAX_KEY 65535u // (the key size field of dp_map.flags)
 #if defined(__HIPCC__)
 #define DP_FN __host__ __device__ static inline
 #else

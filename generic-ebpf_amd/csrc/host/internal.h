@@ -55,7 +55,7 @@ struct map_mirror {
 // read-only open-addressing table (dprog.h dp_map).  Percpu maps mirror the copy of the CPU the
 // batch is submitted from: a device batch behaves like the caller's own loop over
 // ebpf_prog_run on its current CPU.  `bytes == 0` means no device form (hashtable keys over
-// DP_HASH_MAX_KEY).
+// DP_HASH_MAX_KEY, tables over 64 GiB).
 struct map_device_layout {
 	size_t bytes = 0;
 	uint32_t slots = 0; // dp_map.max_entries

@@ -514,19 +514,27 @@ dataflow(dprog_host &out)
 		uint32_t succ[2] = {e.next, UINT32_MAX};
 		if (e.kind < 0x100 && ((e.kind & 7) == EBPF_CLS_JMP || (e.kind & 7) == DP_CLS_JMP32))
 			succ[1] = e.target;
-		for (uint32_t sx : succ) {
+		// the taken edge of "JEQ dst, imm" knows dst == imm (the 64-bit compare)
+		av rt[EBPF_REG_MAX];
+		for (int i = 0; i < EBPF_REG_MAX; i++)
+			rt[i] = r[i];
+		if (e.kind == EBPF_OP_JEQ_IMM && e.dst < EBPF_REG_MAX)
+			rt[e.dst] = mk(AV_CONST, (int64_t)e.imm);
+		for (int k = 0; k < 2; k++) {
+			const uint32_t sx = succ[k];
+			const av *re = k ? rt : r;
 			if (sx == UINT32_MAX || sx >= n)
 				continue;
 			dp_annot &a = out.annot[sx];
 			bool changed = false;
 			if (!a.reached) {
 				for (int i = 0; i < EBPF_REG_MAX; i++)
-					a.in[i] = r[i];
+					a.in[i] = re[i];
 				a.reached = true;
 				changed = true;
 			} else {
 				for (int i = 0; i < EBPF_REG_MAX; i++)
-					if (a.in[i] != r[i] && a.in[i].kind != AV_UNKNOWN) {
+					if (a.in[i] != re[i] && a.in[i].kind != AV_UNKNOWN) {
 						a.in[i] = av();
 						changed = true;
 					}
@@ -643,21 +651,53 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		return EOPNOTSUPP;
 	}
 	dataflow(out);
-	// A hashtable lookup runs a probe specialised for its map, so every lookup of a program
-	// that uses a hashtable must name its map statically (r1 a known constant).
+	// A hashtable lookup runs a probe specialised for its map.  A lookup whose map is known only
+	// at run time, in a program with hashtables, becomes a compare chain on r1: one 64-bit JEQ
+	// per hashtable of the table, taken into the lookup with that map known, ending in the
+	// generic lookup (array maps, NULL, not a map).  Its successor then has several
+	// predecessors: the dataflow runs again over the graph.
 	bool any_hash = false;
 	for (struct ebpf_map *m : out.maps)
 		any_hash |= m->is_hashtable();
-	if (any_hash)
-		for (size_t i = 0; i < out.entries.size(); i++)
-			if (out.entries[i].kind == DK_CALL_LOOKUP && out.annot[i].reached &&
-			    out.annot[i].in[1].kind != AV_CONST) {
-				out.error = EOPNOTSUPP;
-				out.error_msg = "device batches with hashtable maps need every lookup's map "
-						"known at translation time (r1 loaded by LDDW on all paths)";
-				out.maps.clear();
-				return EOPNOTSUPP;
+	if (any_hash) {
+		const size_t n0 = out.entries.size();
+		bool grew = false;
+		for (size_t i = 0; i < n0; i++) {
+			if (out.entries[i].kind != DK_CALL_LOOKUP || !out.annot[i].reached ||
+			    out.annot[i].in[1].kind == AV_CONST)
+				continue;
+			const dp_entry call = out.entries[i];
+			auto add = [&](const dp_entry &x) {
+				out.entries.push_back(x);
+				return (uint32_t)(out.entries.size() - 1);
+			};
+			uint32_t chain = add(call); // the generic lookup at the end of the chain
+			for (size_t m = out.maps.size(); m-- > 0;) {
+				if (!out.maps[m]->is_hashtable())
+					continue;
+				dp_entry j;
+				memset(&j, 0, sizeof(j));
+				j.kind = EBPF_OP_JEQ_IMM;
+				j.dst = EBPF_R1;
+				j.imm = (uint64_t)(uintptr_t)out.maps[m];
+				j.next = chain;
+				j.target = add(call);
+				chain = add(j);
 			}
+			out.entries[i] = out.entries[chain]; // the first compare takes the call's place
+			out.entries[chain].kind = DK_FAULT;   // (its copy is unreachable)
+			out.entries[chain].aux = EBPF_FAULT_SLOT;
+			grew = true;
+		}
+		if (out.entries.size() >= kMaxEntries) {
+			out.error = E2BIG;
+			out.error_msg = "program state graph exceeds the device translation limit";
+			out.maps.clear();
+			return E2BIG;
+		}
+		if (grew)
+			dataflow(out);
+	}
 	// Map-writing helpers: the map must be a translation-time constant of the table.  delete
 	// on an array map is EINVAL whatever its arguments (ebpf_map.c delete -> ebpf_map_array.c:
 	// 246-250): a constant; on a hashtable it has no device form.  update keeps its entry,

@@ -196,3 +196,78 @@ def test_hash_cases_specialised_lookup(gpu, env, monkeypatch, knob):
     finally:
         p.destroy()
         m.destroy()
+
+
+def _runtime_map_program(sel_mask=1, scale=None):
+    """r1 = map 0 + sel * (map 1 - map 0), sel = pkt[5] & sel_mask: the lookup's map is known only
+    at run time (sel_mask 3 also makes r1 = map 0 + 2 * (map 1 - map 0) and + 3 *: not maps,
+    BAD_MAP); key = the packet's first 4 bytes on the stack; r0 = the value's first 8 bytes or
+    0xdead."""
+    from generic_ebpf_amd import isa
+    from generic_ebpf_amd.layout import Branch, LdDw, MapRef, assemble
+    I = isa.Insn
+    nodes = [I("mov_imm", 6, imm=0), I("mov64_reg", 6, 1), I("ldxw", 9, 6, 0), I("stxw", 10, 9, -8),
+             I("ldxb", 7, 6, 5), I("and_imm", 7, imm=sel_mask),
+             LdDw(1, MapRef(0)), LdDw(8, MapRef(1)), I("sub64_reg", 8, 1), I("mul64_reg", 8, 7),
+             I("add64_reg", 1, 8),
+             I("mov_imm", 2, imm=0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-8),
+             I("call", imm=0),
+             Branch(I("jeq_imm", 0, imm=0), [I("mov_imm", 0, imm=0xdead), I("exit")]),
+             I("ldxdw", 0, 0, 0), I("exit")]
+    return assemble(nodes)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("second", ["hash", "array"])
+@pytest.mark.parametrize("sel_mask", [1, 3])
+def test_hash_lookup_map_known_at_run_time(gpu, env, variant, second, sel_mask):
+    """The lookup's map is a run-time value: hashtable A, or hashtable / array B, or (sel_mask 3)
+    not a map at all (BAD_MAP), per packet — the translator's compare chain on r1 against the
+    oracle, whose helper resolves r1 at run time like the reference."""
+    rng = np.random.default_rng(91)
+    items_a, keys_a = hashprogs.make_table(rng, 4, 8, 40)
+    items_b, keys_b = hashprogs.make_table(rng, 4, 8, 40)
+    n = 4096
+    keys = keys_a + keys_b + [bytes([k, 0, 0, 0]) for k in range(16)]
+    pk = hashprogs.packets_with_keys(rng, n, 64, keys, 0, 4)
+    lay = _runtime_map_program(sel_mask)
+    spec_a = pyoracle.HashSpec(4, 8, items=items_a)
+    arr = rng.integers(0, 256, 16 * 8, dtype=np.uint8).tobytes()
+    spec_b = pyoracle.HashSpec(4, 8, items=items_b) if second == "hash" else (8, 16, arr)
+    want, wf, _ = hashprogs.oracle(lay, [spec_a, spec_b], pk.reshape(-1), n, 64)
+    ma = hashprogs.NativeHash(gpu, env, 4, 8, 64, items_a)
+    if second == "hash":
+        mb = hashprogs.NativeHash(gpu, env, 4, 8, 64, items_b)
+    else:
+        mb = gpu.Map(env, 16, 8)
+        mb.fill(arr)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [ma.handle, mb.handle]))
+    try:
+        gpu.set_variant(variant)
+        got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        np.testing.assert_array_equal(gf, wf)
+        np.testing.assert_array_equal(got, want)
+        assert (wf == 10).any() == (sel_mask == 3)
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        ma.destroy()
+        mb.destroy()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("ks,src,stride", [(300, "stack", 512), (600, "packet", 1024),
+                                           (257, "packet", 320)])
+def test_hash_long_keys(gpu, env, variant, ks, src, stride):
+    """Keys of hundreds of bytes (device slots of 512 B to 1 KB): on the stack and in the packet."""
+    rng = np.random.default_rng(ks)
+    items, keys = hashprogs.make_table(rng, ks, 8, 24)
+    n = 1024
+    pk = hashprogs.packets_with_keys(rng, n, stride, keys, 8, ks)
+    lay = hashprogs.lookup_program(ks, src, key_off=8)
+    spec = pyoracle.HashSpec(ks, 8, items=items)
+    want, wf, _ = hashprogs.oracle(lay, [spec], pk.reshape(-1), n, stride)
+    got, gf = run_device(gpu, env, lay, [spec], pk.reshape(-1), n, stride, variant=variant)
+    np.testing.assert_array_equal(gf, wf)
+    np.testing.assert_array_equal(got, want)
+    assert (want != 0xdead).any() and (want == 0xdead).any()

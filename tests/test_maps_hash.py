@@ -272,10 +272,10 @@ def test_prog_run_with_hashtable_lookup(native, env, typ):
 
 
 def test_device_translation_of_hashtable_programs(native, env):
-    """Hashtable lookups with a statically known map translate for the device (both code
-    layouts compile), percpu hashtables included; keys longer than 256 bytes and lookups whose
-    map is only known at run time do not (EOPNOTSUPP, the program still runs through
-    ebpf_prog_run)."""
+    """Hashtable lookups translate for the device (both code layouts compile): a statically
+    known map, percpu hashtables, keys of hundreds of bytes, and lookups whose map is known only
+    at run time (a compare chain on r1 over the program's hashtables).  Keys over 65535 bytes
+    have no device form (EOPNOTSUPP; the program still runs through ebpf_prog_run)."""
     from generic_ebpf_amd import isa
     from generic_ebpf_amd.layout import Branch, LdDw, MapRef, assemble
     I = isa.Insn
@@ -294,21 +294,27 @@ def test_device_translation_of_hashtable_programs(native, env):
         p2 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [pht.ptr.value]))
         progs.append(p2)
         assert native.lib().ebpf_prog_device_info(p2.ptr, ctypes.byref(i)) == 0   # percpu: the caller's CPU copy
-        big = HMap(native, env, HT, 300, 8, 4)      # keys too long for the device table
+        big = HMap(native, env, HT, 300, 8, 4)      # long keys: slots of 512 bytes
         extra.append(big)
         p4 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [big.ptr.value]))
         progs.append(p4)
-        assert native.lib().ebpf_prog_device_info(p4.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
+        assert native.lib().ebpf_prog_device_info(p4.ptr, ctypes.byref(i)) == 0
+        huge = HMap(native, env, HT, 65536, 8, 2)   # past the device table's key-size field
+        extra.append(huge)
+        p5 = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [huge.ptr.value]))
+        progs.append(p5)
+        assert native.lib().ebpf_prog_device_info(p5.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
         assert "no device form" in native.last_error()
-        # r1 = the hashtable's handle plus a packet byte: not resolvable at translation time
+        # r1 = the hashtable's handle plus a packet byte: resolved at run time
         nodes = [I("ldxw", 6, 1, 0), I("stxw", 10, 6, -4), I("ldxb", 7, 1, 4), LdDw(1, MapRef(0)),
                  I("add64_reg", 1, 7), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
                  I("call", imm=0), I("exit")]
         lay3 = assemble(nodes)
         p3 = native.Prog(env, native.patch_relocs(lay3.code, lay3.relocs, [ht.ptr.value]))
         progs.append(p3)
-        assert native.lib().ebpf_prog_device_info(p3.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
-        assert "known at translation time" in native.last_error()
+        assert native.lib().ebpf_prog_device_info(p3.ptr, ctypes.byref(i)) == 0
+        for layout in (0, 1):
+            assert len(p3.device_code(layout)) > 0
     finally:
         for p in progs:
             p.destroy()
