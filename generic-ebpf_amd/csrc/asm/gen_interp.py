@@ -39,7 +39,9 @@ V_PKT = 38           # v[38:39] packet base address
 V_LEN = 40           # packet length (bytes)
 V_T = 41             # parked entry byte offset
 V_STK = 42           # lane stack bottom (LDS byte address)
-V_L16 = 43           # lane * 16 (LDS-DMA staging offset)
+V_L16 = 43           # staged image: lane * 16 (LDS-DMA staging offset)
+V_IDX = 43           # general image: the lane's packet index in the launch (its group's, or in
+                     # a regrouped batch the queued packet's; see "Regrouping" below)
 # v[44:45] (RETK == 1) or v[64:64+2*RETK]: r0 of the lanes that retired, per group of the
 # current superblock (stored together at the start of the next superblock)
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
@@ -101,6 +103,21 @@ S_KMASK = 73         # superblock size - 1 of this launch (K' <= RETK, a power o
 S_WAVE = 3
 NSGPR = 76           # + VCC, XNACK, FLAT_SCRATCH; s[74:75]: compiled programs' short-lane mask
                      # in the general image (asm_cc.cpp ldxpkc_general)
+# Regrouping (general image, compiled programs; asm_jit.cpp regroup plan).  Lanes that reach the
+# head of a heavy subtree the compiler chose (a "regroup point", at most RQ_MAX) do not run it
+# with the group: they push (packet index, live registers) onto that point's queue, a ring of 128
+# entries in the wave's slice of dp_launch.rq_buf, and leave the group.  After each group the
+# compiled program's drain code runs every queue holding >= 64 entries as a batch of 64 lanes
+# that all take the same subtree (at the end of the wave's groups: every non-empty queue), so a
+# divergent program runs each heavy path with full waves instead of once per group with a few
+# lanes.  Queue q: u32 packet index [128] at +0, then live register k: u64 [128] at +512 + 1024k.
+S_DEFER = 76         # s[76:77] lanes of the running group that were queued (no result stored)
+S_QBASE = 78         # s[78:79] this wave's queue slice
+S_BMASK = 80         # s[80:81] lanes of the running batch
+S_QS = 82            # s82..s87: queue states, two per SGPR (bits 0-6 tail, 8-15 count; +16 odd q)
+RQ_MAX = 12
+NSGPR_GEN = S_QS + RQ_MAX // 2
+# s7 flags of regrouping: bit 6 queues active, bit 7 a batch is running, bit 8 final drain
 # staged image: s[74:75] .. s[96:97] hold the taken-lane masks of a structured compiled program's
 # pending branches (asm_jit.cpp; 12 levels); 98 SGPRs still allow the image's 6 waves per SIMD
 S_JOIN = 74
@@ -109,6 +126,9 @@ NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
 # general image with the join SGPRs too (structured compiled programs in the general kernels;
 # 98 SGPRs allow 7 instead of 8 waves per SIMD there)
 GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
+# (the join SGPRs s74..s97 would overlap the regroup SGPRs, and structured exits address the LDS
+# histogram through lane 0 of v43, which the general image uses for V_IDX)
+assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with regrouping (S_DEFER..) and V_IDX"
 # general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
 # hoist plan); 16 cost the general kernels 8 -> 6 waves per SIMD
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
@@ -990,8 +1010,7 @@ def update_routine():
           "v_mov_b32 %s, s67" % v(R[1]),
           "v_mad_u64_u32 %s, %s, %s, %s, s[64:65]" % (vp(R[4]), sp(S_JUNK), v(R[0]), v(R[1])),
           # packet index (pkt_base = this launch's first packet in its batch)
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[2]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[2]), s(S_GROUP), v(R[2])),
+          ] + lane_pkt_index(R[2]) + [
           "v_mov_b32 %s, s69" % v(R[3]),
           "v_add_co_u32 %s, vcc, s68, %s" % (v(R[2]), v(R[2])),
           "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[3]), v(R[3])),
@@ -1160,8 +1179,7 @@ def routines():
           ] + ret_slot_write("0", "0") + [
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lfl_nofault",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
+          ] + lane_pkt_index(R[9]) + [
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
           "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
           ".Lfl_nofault:",
@@ -1369,6 +1387,34 @@ def routines():
           ".Llk_sched:"] + goto(".Lr_schedule")
     L += hlookup_routine()
     L += update_routine()
+    if not STAGED_IMAGE:
+        # BATCH (regrouping; called by the compiled drain code): make the first n = S_T1 lanes the
+        # running batch of the queue at s[64:65] from ring slot head = S_T2 on: their packet
+        # indices (V_IDX), packet address / length and staged header; s7 bit 7 set.  Returns with
+        # exec = S_ALIVE = S_BMASK = the batch and H[2] = each lane's slot * 8 (the compiled code
+        # then loads the live registers: +512 + 1024k).  The wait first: the pushes (and this
+        # wave's earlier result and fault stores) have landed before a batch reads or rewrites.
+        L += [".Lr_batch:",
+              "s_waitcnt vmcnt(0)",
+              "s_bfm_b64 %s, %s, 0" % (sp(S_BMASK), s(S_T1)),
+              "s_cmp_eq_u32 %s, 64" % s(S_T1),
+              "s_cselect_b64 %s, -1, %s" % (sp(S_BMASK), sp(S_BMASK)),
+              "s_mov_b64 exec, %s" % sp(S_BMASK),
+              "s_mov_b64 %s, %s" % (sp(S_ALIVE), sp(S_BMASK)),
+              "s_or_b32 s7, s7, 128"] + lane_index(H[0]) + [
+              "v_add_u32 %s, %s, %s" % (v(H[0]), s(S_T2), v(H[0])),
+              "v_and_b32 %s, 0x7f, %s" % (v(H[0]), v(H[0])),
+              "v_lshlrev_b32 %s, 2, %s" % (v(H[1]), v(H[0])),
+              "v_lshlrev_b32 %s, 3, %s" % (v(H[2]), v(H[0])),
+              "global_load_dword v%d, %s, s[64:65]" % (V_IDX, v(H[1])),
+              "s_waitcnt vmcnt(0)",
+              # (defensive: a lane whose index is not a packet of this launch drops out rather
+              # than reading outside the batch)
+              "v_cmp_gt_u32_e64 vcc, %s, v%d" % (s(S_COUNT), V_IDX),
+              "s_and_b64 %s, %s, vcc" % (sp(S_BMASK), sp(S_BMASK)),
+              "s_mov_b64 exec, %s" % sp(S_BMASK),
+              "s_mov_b64 %s, %s" % (sp(S_ALIVE), sp(S_BMASK))] + pkt_setup(V_IDX, "b") + [
+              "s_setpc_b64 %s" % sp(S_LINK)]
     # DMA_NEXT (staged kernel, deferred mode s7 bit 4): issue the LDS DMA of this wave's next
     # group now, once per group (sets bit 5).  The group set-up defers only a full next group,
     # so this is always the 4-instruction full-group DMA.  Preserves exec, S_T*, s[66:71];
@@ -1435,11 +1481,82 @@ def kernel(name, staged, jit=False):
               "s_cbranch_scc0 .L%s_nogs" % k,
               "s_or_b32 s7, s7, 8",
               ".L%s_nogs:" % k]
+    if not staged and jit and not STAGED_IMAGE:
+        # regroup queues (dp_launch.rq_buf != 0): this wave's slice, empty queues
+        L += ["s_load_dwordx2 %s, s[0:1], 0x98" % sp(S_QBASE),
+              "s_load_dword %s, s[0:1], 0xa0" % s(S_BMASK),
+              "s_mov_b64 %s, 0" % sp(S_DEFER)] + [
+              "s_mov_b64 %s, 0" % sp(S_QS + 2 * i) for i in range(RQ_MAX // 4)] + [
+              "s_waitcnt lgkmcnt(0)",
+              "s_cmp_eq_u64 %s, 0" % sp(S_QBASE),
+              "s_cbranch_scc1 .L%s_norq" % k,
+              "s_lshl_b32 %s, s2, 2" % s(S_T0),
+              "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_WAVE)),
+              "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_BMASK)),
+              "s_add_u32 %s, %s, %s" % (s(S_QBASE), s(S_QBASE), s(S_T0)),
+              "s_addc_u32 %s, %s, 0" % (s(S_QBASE + 1), s(S_QBASE + 1)),
+              "s_or_b32 s7, s7, 64",
+              ".L%s_norq:" % k]
     L += ["s_branch .Lprologue"]
     return L
 
 
 V_RES = 44   # v[44:45]: r0 of the lanes that retired in the running group
+
+
+def lane_index(dst):
+    """dst = this lane's index in the wave (0..63)."""
+    if STAGED_IMAGE:
+        return ["v_lshrrev_b32 %s, 4, v%d" % (v(dst), V_L16)]
+    return ["v_mbcnt_lo_u32_b32 %s, -1, 0" % v(dst), "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(dst), v(dst))]
+
+
+def lane_pkt_index(dst):
+    """dst = the packet index of this lane in the launch (general image: V_IDX, which a
+    regrouped batch sets to the queued packet's)."""
+    if STAGED_IMAGE:
+        return ["v_lshrrev_b32 %s, 4, v%d" % (v(dst), V_L16),
+                "v_lshl_add_u32 %s, %s, 6, %s" % (v(dst), s(S_GROUP), v(dst))]
+    return ["v_mov_b32 %s, v%d" % (v(dst), V_IDX)]
+
+
+def pkt_setup(idx, tag):
+    """General kernels: V_PKT / V_LEN of the running lanes' packets (index in VGPR idx), and with
+    header staging (s7 bit 3) their first 64 bytes into v22..v37.  Clobbers H[1], H[4:5], R[0],
+    R[2], S_JUNK; leaves exec = the running lanes (s[S_MASK] holds them meanwhile)."""
+    return ["s_mov_b64 %s, exec" % sp(S_MASK),
+            "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
+            "s_cbranch_scc0 .Lps_offsets_%s" % tag,
+            "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
+            "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), idx,
+                                                         v(H[1]), sp(S_DATA)),
+            "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
+            "s_branch .Lps_stage_%s" % tag,
+            ".Lps_offsets_%s:" % tag,
+            "v_mov_b32 %s, 8" % v(H[1]),
+            "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[4]), sp(S_JUNK), idx, v(H[1]), sp(S_OFFS)),
+            "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[4])),
+            "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[4])),
+            "s_waitcnt vmcnt(0)",
+            "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
+            "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
+            "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
+            "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
+            "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
+            # header staging: the first 64 bytes of every packet at least that long into
+            # v22..v37 (what the staged kernels' LDS DMA provides)
+            ".Lps_stage_%s:" % tag,
+            "s_bitcmp1_b32 s7, 3",
+            "s_cbranch_scc0 .Lps_done_%s" % tag,
+            "v_cmp_lt_u32_e64 vcc, 63, v%d" % V_LEN,
+            "s_and_b64 exec, %s, vcc" % sp(S_MASK),
+            "s_cbranch_execz .Lps_done_%s" % tag] + [
+            "global_load_dwordx4 v[%d:%d], v[%d:%d], off offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
+                                                                       V_PKT, V_PKT + 1, 16 * q)
+            for q in range(4)] + [
+            "s_waitcnt vmcnt(0)",
+            ".Lps_done_%s:" % tag,
+            "s_mov_b64 exec, %s" % sp(S_MASK)]
 
 
 def ret_slot_write(x0, x1):
@@ -1476,8 +1593,9 @@ def store_prev_results(tag, final):
     # (all lanes: the current group's live mask says nothing about the stored groups)
     L += ["s_mov_b64 exec, -1",
           "s_andn2_b32 %s, %s, %s" % (s(S_T0), s(S_PREVG), s(S_KMASK)),
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[1]), s(S_T0), v(R[1])),
+          ] + (["v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),
+                "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[1]), s(S_T0), v(R[1]))] if STAGED_IMAGE else
+               ["v_mov_b32 %s, v%d" % (v(R[1]), V_IDX)]) + [
           "v_lshlrev_b32 %s, 3, %s" % (v(R[0]), v(R[1]))]
     for k in range(RETK):
         if k:
@@ -1566,17 +1684,24 @@ def common_group_code():
           "s_cbranch_scc0 .Lgroup_check",
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
-    L += [".Lgroup_done:",
-          "s_and_b32 %s, s7, 48" % s(S_BYTES),
+    L += [".Lgroup_done:"]
+    if not STAGED_IMAGE:
+        L += ["s_bitcmp1_b32 s7, 6",
+              "s_cbranch_scc1 .Lrg_done"]
+    L += ["s_and_b32 %s, s7, 48" % s(S_BYTES),
           "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
           "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
-          ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
+          ".Lgd_dma_ok:"] + slot_commit() + [
+          ".Ldrain_ret:"] + ([] if STAGED_IMAGE else [
+          # (the compiled drain code returns here when no queue holds a batch to run)
+          "s_bitcmp1_b32 s7, 8",
+          "s_cbranch_scc1 .Lfinish_body"]) + next_group(S_T0) + [
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
           "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
           "s_cbranch_scc0 .Lfinish",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
+          ] + lane_index(H[0]) + [
           "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
           "s_bitcmp1_b32 s7, 0",
@@ -1625,55 +1750,27 @@ def common_group_code():
           "v_mov_b32 v%d, 64" % V_LEN,
           "s_branch .Lgs_init",
           ".Lgs_general:",
-          "s_mov_b64 exec, %s" % sp(S_ALIVE),
-          # packet address / length
-          "s_cmp_eq_u64 %s, 0" % sp(S_OFFS),
-          "s_cbranch_scc0 .Lgs_offsets",
-          "v_mov_b32 %s, %s" % (v(H[1]), s(S_STRIDE)),
-          "v_mad_u64_u32 v[%d:%d], %s, v%d, %s, %s" % (V_PKT, V_PKT + 1, sp(S_JUNK), H[3],
-                                                       v(H[1]), sp(S_DATA)),
-          "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
-          "s_branch .Lgs_gstage",
-          ".Lgs_offsets:",
-          "v_mov_b32 %s, 8" % v(H[1]),
-          "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[4]), sp(S_JUNK), H[3], v(H[1]), sp(S_OFFS)),
-          "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[4])),
-          "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[4])),
-          "s_waitcnt vmcnt(0)",
-          "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
-          "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
-          "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
-          "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
-          "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
-          # general kernels with header staging: the first 64 bytes of every packet at least
-          # that long into v22..v37 (what the staged kernels' LDS DMA provides)
-          ".Lgs_gstage:",
-          "s_bitcmp1_b32 s7, 3",
-          "s_cbranch_scc0 .Lgs_init",
-          "v_cmp_lt_u32_e64 vcc, 63, v%d" % V_LEN,
-          "s_and_b64 exec, %s, vcc" % sp(S_ALIVE),
-          "s_cbranch_execz .Lgs_gs_done"] + [
-          "global_load_dwordx4 v[%d:%d], v[%d:%d], off offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
-                                                                     V_PKT, V_PKT + 1, 16 * q)
-          for q in range(4)] + [
-          "s_waitcnt vmcnt(0)",
-          ".Lgs_gs_done:",
-          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          "s_mov_b64 exec, %s" % sp(S_ALIVE)] + pkt_setup(H[3], "g") + [
           ".Lgs_init:"] + store_prev_results("g", False) + [
-          "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP)),
+          "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP))] + ([] if STAGED_IMAGE else [
+          # V_IDX: this group's packet indices (after the previous group's store read them);
+          # with queues the group's results are stored when it is done, not here
+          "s_mov_b64 exec, -1",
+          "v_mov_b32 v%d, v%d" % (V_IDX, H[3]),
+          "s_bitcmp1_b32 s7, 6",
+          "s_cselect_b32 %s, -1, %s" % (s(S_PREVG), s(S_PREVG))]) + [
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
           # fault code 0 for the whole group up front (a faulting lane overwrites its byte)
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
           "s_cbranch_scc1 .Lgs_nofz",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[9]), V_L16),
-          "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[9]), s(S_GROUP), v(R[9])),
+          ] + lane_pkt_index(R[9]) + [
           "v_mov_b32 %s, 0" % v(R[8]),
           "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
           ".Lgs_nofz:",
           # a compiled program (s7 bit 1) starts at the head of its code area and sets up the
           # registers it reads itself (packet address, r1, r10, zeroes: asm_cc.cpp prologue)
           "s_bitcmp1_b32 s7, 1",
-          "s_cbranch_scc0 .Lgs_interp"] + goto("ebpf_jit_area") + [
+          "s_cbranch_scc0 .Lgs_interp"] + goto("ebpf_jit_area+16") + [
           ".Lgs_interp:"]
     # r0, r2..r9 start at zero
     for r in range(0, 20, 2):
@@ -1691,14 +1788,40 @@ def common_group_code():
     # histogram (stored, or added), then re-arms the ticket.  One kernel per launch: no
     # second-stage reduce (hand-off form: 8-B agent atomics on both sides, MI355X_MICROARCH.md
     # "Valid forms")
+    if not STAGED_IMAGE:
+        # Regrouping.  A group is done: store its results but the queued lanes', then let the
+        # compiled drain code (ebpf_jit_area + 0) run the full queues.  A batch is done: store its
+        # lanes' results at their packets, back to the drain code.
+        L += [".Lrg_done:",
+              "s_bitcmp1_b32 s7, 7",
+              "s_cbranch_scc1 .Lrg_batch_done",
+              "s_mov_b64 exec, -1",
+              "v_cmp_gt_u32_e64 vcc, %s, v%d" % (s(S_COUNT), V_IDX),
+              "s_andn2_b64 exec, vcc, %s" % sp(S_DEFER),
+              "v_lshlrev_b32 %s, 3, v%d" % (v(R[0]), V_IDX),
+              "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RES, V_RES + 1, sp(S_RET),
+                                                          ST_POLICY),
+              "s_mov_b64 %s, 0" % sp(S_DEFER)] + goto("ebpf_jit_area") + [
+              ".Lrg_batch_done:",
+              "s_mov_b64 exec, %s" % sp(S_BMASK),
+              "v_lshlrev_b32 %s, 3, v%d" % (v(R[0]), V_IDX),
+              "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RES, V_RES + 1, sp(S_RET),
+                                                          ST_POLICY),
+              "s_and_b32 s7, s7, ~128"] + goto("ebpf_jit_area")
     HR = HIST_REPLICA_BYTES
-    L += [".Lfinish:"] + store_prev_results("f", True) + [
+    L += [".Lfinish:"] + store_prev_results("f", True)
+    if not STAGED_IMAGE:
+        # every group done: the drain code runs what the queues still hold (bit 8: any count)
+        L += ["s_bitcmp1_b32 s7, 6",
+              "s_cbranch_scc0 .Lfinish_body",
+              "s_or_b32 s7, s7, 256"] + goto("ebpf_jit_area")
+    L += [".Lfinish_body:",
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_barrier",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfin_end",
-          "v_lshrrev_b32 %s, 4, v%d" % (v(H[0]), V_L16),
+          ] + lane_index(H[0]) + [
           "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # bin
           "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[1])),
@@ -1961,7 +2084,8 @@ def jit_templates():
         ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
         ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", ".Lr_exit", ".Lr_fault",
-        ".Lr_hlookup", ".Lgroup_done", "ebpf_jit_area"]
+        ".Lr_hlookup", ".Lgroup_done", ".Lr_batch" if not STAGED_IMAGE else ".Lgroup_done",
+        ".Lr_schedule", ".Ldrain_ret", "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
     return L
@@ -2059,6 +2183,11 @@ def generate(out_s, staged_image):
     header.append("#define AH_GEN_JOIN %d  // the general image holds the join SGPRs too" % GEN_JOIN)
     header.append("#define AH_GEN_HOIST_BASE 64  // general image: spare VGPRs for hoisted loads")
     header.append("#define AH_GEN_HOIST_REGS %d" % GEN_HOIST_REGS)
+    header.append("#define AH_S_DEFER %d  // regrouping (general image): queued lanes of the group" % S_DEFER)
+    header.append("#define AH_S_QBASE %d  // the wave's queue slice" % S_QBASE)
+    header.append("#define AH_S_QS %d  // queue states, two per SGPR" % S_QS)
+    header.append("#define AH_RQ_MAX %d" % RQ_MAX)
+    header.append("#define AH_V_IDX %d  // general image: the lane's packet index" % V_IDX)
     header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
@@ -2068,8 +2197,8 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 152
-    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR
+    kernarg = 168
+    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_jit_s64", kernarg, 0, NVGPR, nsg, 256),

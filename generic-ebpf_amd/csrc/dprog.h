@@ -117,8 +117,14 @@ struct dp_launch {
 	uint32_t upd_cap;         // records the log holds
 	uint32_t upd_stride;
 	uint64_t pkt_base;        // index of this launch's first packet in its batch
+	// regrouping (compiled programs, general kernels; gen_interp.py "Regrouping"): the queue
+	// buffer, rq_wave_bytes per wave of the launch (wave w = workgroup * 4 + wave in it); NULL:
+	// no queues
+	uint8_t *rq_buf;
+	uint32_t rq_wave_bytes;
+	uint32_t rq_pad;
 };
-static_assert(sizeof(dp_launch) == 152, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 168, "dp_launch layout is shared with the assembly kernels");
 
 // Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
 // EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B

@@ -41,6 +41,8 @@
 // Encodings: VOP1/VOP2/VOPC (e32, literal allowed in src0), VOP3 (no literal on gfx9), SOP1,
 // SOP2, DS.  Field layouts and opcodes are from llvm-mc -show-encoding for gfx950;
 // tests/test_compile.py checks decoded forms.
+#include <algorithm>
+
 #include "asm_handlers.h"
 #include "internal.h"
 
@@ -1439,6 +1441,8 @@ copied_uses(int fam, int d, int s)
 	case AHF_LDXSTK1: case AHF_LDXSTK2: case AHF_LDXSTK4: case AHF_LDXSTK8: return 0;
 	case AHF_LDXPKC1: case AHF_LDXPKC2: case AHF_LDXPKC4: case AHF_LDXPKC8: return 0;
 	case AHF_A64I_MOV: return 0;
+	case AHF_A32I_MOV: return 0;
+	case AHF_A32R_MOV: case AHF_MOV64R: return m(s);
 	default: return m(d) | m(s); // (LDX*: s = the address; ST*: d = base, s = value; ALU: both)
 	}
 }
@@ -1559,10 +1563,259 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vecto
 			P.vop1(V1_MOV_B64, 2 * r, opnd{128});
 }
 
+namespace {
+
+// families a regroup point's subtree may hold: they read and write registers and the packet
+// (through V_PKT / the staged header, never r1), nothing lane-position dependent
+bool
+regroup_safe(int fam)
+{
+	if ((fam >= AHF_A64R_ADD && fam <= AHF_A64R_MOD) || (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD) ||
+	    (fam >= AHF_A64I_ADD && fam <= AHF_A64I_MOV) || (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD) ||
+	    (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) || (fam >= AHF_LDXPKC1 && fam <= AHF_LDXPKC8) ||
+	    (fam >= AHF_MOV64R && fam <= AHF_MOD32Z) || is_cond_fam(fam))
+		return true;
+	switch (fam) {
+	case AHF_BSWAP16: case AHF_BSWAP32: case AHF_BSWAP64:
+	case AHF_EXIT: case AHF_FAULT: case AHF_NOP:
+		return true;
+	default:
+		return false;
+	}
+}
+
+// SOP2 / SOP1 / SOPC / SOPP opcodes used by the regroup code (llvm-mc, gfx950)
+enum : uint32_t {
+	S2_ADD_U32 = 0x00, S2_SUB_U32 = 0x01, S2_ADDC_U32 = 0x04, S2_MIN_U32 = 0x07, S2_CSELECT_B32 = 0x0a,
+	S2_AND_B32 = 0x0c, S2_OR_B32 = 0x0e, S2_OR_B64 = 0x0f, S2_ANDN2_B64 = 0x13, S2_LSHL_B32 = 0x1c,
+	S2_BFE_U32 = 0x25,
+	S1_BCNT1_I32_B64 = 0x0d, S1_SETPC_B64 = 0x1d, S1_SWAPPC_B64 = 0x1e,
+	SC_CMP_GE_U32 = 0x09, SC_BITCMP1_B32 = 0x0d,
+	V3_MBCNT_LO = 0x28c, V3_MBCNT_HI = 0x28d,
+	G_LOAD_DWORDX2 = 0x15, G_STORE_DWORD = 0x1c, G_STORE_DWORDX2 = 0x1d,
+};
+const int RG_T0 = 53, RG_T1 = 54, RG_T2 = 55, RG_T3 = 56; // gen_interp.py S_T0..S_T3
+const int RG_REC = 64;                                    // s[64:65]: the queue's base
+
+void
+sopc(enc &E, uint32_t op, opnd a, opnd b)
+{
+	E.w(0xbf000000u | (op << 16) | (b.code << 8) | a.code);
+	E.lit(a);
+	E.lit(b);
+}
+
+// global load/store, SGPR base s[sbase:+1] + VGPR byte offset voff + imm
+void
+gmem(enc &E, uint32_t op, int voff, int data_or_vdst, int sbase, uint32_t imm, bool store)
+{
+	E.w(0xdc000000u | (op << 18) | 0x8000u | (imm & 0x1fffu));
+	E.w((uint32_t)voff | (store ? ((uint32_t)data_or_vdst << 8) : ((uint32_t)data_or_vdst << 24)) |
+	    ((uint32_t)sbase << 16));
+}
+
+// jump (or call, link s[50:51]) to .Lcb + off
+void
+jump_cb(enc &E, uint32_t off, bool call)
+{
+	const int P = call ? 50 : S_JUNK;
+	E.sop2(S2_ADD_U32, P, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, off});
+	E.sop2(S2_ADDC_U32, P + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});
+	E.sop1(call ? S1_SWAPPC_B64 : S1_SETPC_B64, call ? P : 0, opnd{(uint32_t)P});
+}
+
+} // namespace
+
+void
+cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
+		std::vector<cc_regroup_point> &points)
+{
+	points.clear();
+	// opt-in (EBPF_CC_REGROUP=1): measured slower than per-group divergence on C5
+	const char *on = getenv("EBPF_CC_REGROUP");
+	if (on == nullptr || atoi(on) == 0)
+		return;
+	// entries each side of the divergent conditional at least holds: a queued lane costs its
+	// push, a batch slot and the batch set-up (packet address, header), worth it for long paths
+	uint32_t rg_min = 96;
+	if (const char *m = getenv("EBPF_CC_RG_MIN"))
+		rg_min = (uint32_t)atoi(m);
+	const size_t n = low.size();
+	auto fam_of = [&](uint32_t e) { return (int)ah_fam[(uint32_t)low[e].handler]; };
+	auto is_term = [&](uint32_t e) { return fam_of(e) == AHF_EXIT || fam_of(e) == AHF_FAULT; };
+	auto is_cond = [&](uint32_t e) { return (ah_flags[(uint32_t)low[e].handler] & 1) != 0; };
+	std::vector<uint32_t> parent(n, UINT32_MAX), npred(n, 0);
+	for (uint32_t e : order) {
+		if (is_term(e))
+			continue;
+		const uint32_t nx = xl.entries[e].next;
+		if (nx < n) {
+			npred[nx]++;
+			parent[nx] = e;
+		}
+		if (is_cond(e) && xl.entries[e].target < n) {
+			npred[xl.entries[e].target]++;
+			parent[xl.entries[e].target] = e;
+		}
+	}
+	// backward over the tree (children follow their parent in `order`): subtree size, safety,
+	// conservative liveness (every register a copied handler body would read)
+	std::vector<uint32_t> sz(n, 0);
+	std::vector<char> safe(n, 0), cand(n, 0), below(n, 0);
+	std::vector<uint16_t> live(n, 0);
+	for (size_t k = order.size(); k-- > 0;) {
+		const uint32_t e = order[k];
+		const int fam = fam_of(e);
+		const int d = ah_dst[(uint32_t)low[e].handler], sr = ah_src[(uint32_t)low[e].handler];
+		uint32_t size = 1;
+		bool ok = regroup_safe(fam);
+		uint16_t lo = 0;
+		if (!is_term(e)) {
+			uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
+			for (uint32_t c : ch) {
+				if (c >= n)
+					continue;
+				size += sz[c];
+				ok = ok && safe[c];
+				lo |= live[c];
+			}
+		}
+		const int wr = written_reg(fam, d);
+		uint16_t li = lo;
+		if (wr >= 0)
+			li &= (uint16_t)~(1u << wr);
+		li |= copied_uses(fam, d, sr);
+		sz[e] = size;
+		safe[e] = ok;
+		live[e] = li;
+	}
+	// candidates: the entry heads one side of a conditional whose both sides are heavy (sizes
+	// complete now: a taken subtree is laid out after its fall-through sibling)
+	for (uint32_t e : order) {
+		const uint32_t p = parent[e];
+		if (safe[e] && e != xl.start && npred[e] == 1 && p < n && is_cond(p) && sz[e] >= rg_min &&
+		    __builtin_popcount(live[e]) <= 3) {
+			const uint32_t o = xl.entries[p].next == e ? xl.entries[p].target : xl.entries[p].next;
+			cand[e] = o < n && sz[o] >= rg_min;
+		}
+	}
+	for (size_t k = order.size(); k-- > 0;) {
+		const uint32_t e = order[k];
+		if (is_term(e))
+			continue;
+		uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
+		for (uint32_t c : ch)
+			if (c < n)
+				below[e] = below[e] || cand[c] || below[c];
+	}
+	std::vector<uint32_t> pick;
+	for (uint32_t e : order)
+		if (cand[e] && !below[e])
+			pick.push_back(e);
+	if (pick.size() > (size_t)AH_RQ_MAX) {
+		std::stable_sort(pick.begin(), pick.end(), [&](uint32_t a, uint32_t b) { return sz[a] > sz[b]; });
+		pick.resize(AH_RQ_MAX);
+	}
+	if (getenv("EBPF_CC_RG_DEBUG")) {
+		for (uint32_t e : order)
+			if (cand[e])
+				fprintf(stderr, "regroup candidate %u size %u live %#x below %d\n", e, sz[e], live[e],
+					(int)below[e]);
+		fprintf(stderr, "regroup points: %zu\n", pick.size());
+		int shown = 0;
+		for (uint32_t e : order)
+			if (!regroup_safe(fam_of(e)) && shown++ < 10)
+				fprintf(stderr, "unsafe entry %u family %d\n", e, fam_of(e));
+	}
+	if (pick.size() < 2)
+		return;
+	for (uint32_t e : pick) {
+		cc_regroup_point pt;
+		pt.entry = e;
+		for (int r = 0; r < AH_NREGS; r++)
+			if (live[e] & (1u << r))
+				pt.live.push_back((uint8_t)r);
+		points.push_back(pt);
+	}
+}
+
+void
+cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t sched_off,
+	     std::vector<uint8_t> &out)
+{
+	enc E{out};
+	const int QS = AH_S_QS + q / 2, sh = 16 * (q & 1);
+	E.sop1(S1_BCNT1_I32_B64, RG_T0, opnd{SRC_EXEC});                          // n
+	E.vop3(V3_MBCNT_LO, T0, SRC_EXEC, 128, 0);                                 // rank in exec
+	E.vop3(V3_MBCNT_HI, T0, SRC_EXEC + 1, VGPR0 + T0, 0);
+	E.sop2(S2_BFE_U32, RG_T1, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)sh | (7u << 16)}); // tail
+	E.vop2(V2_ADD_U32, T0, opnd{(uint32_t)RG_T1}, T0);
+	E.vop2(V2_AND, T0, opnd{SRC_LIT, 0x7f}, T0);                               // slot
+	E.vop2(V2_LSHLREV_B32, T1, opnd{128 + 2}, T0);
+	E.vop2(V2_LSHLREV_B32, T0, opnd{128 + 3}, T0);
+	E.sop2(S2_ADD_U32, RG_REC, opnd{(uint32_t)AH_S_QBASE}, opnd{SRC_LIT, (uint32_t)q * qbytes});
+	E.sop2(S2_ADDC_U32, RG_REC + 1, opnd{(uint32_t)AH_S_QBASE + 1}, opnd{128});
+	gmem(E, G_STORE_DWORD, T1, AH_V_IDX, RG_REC, 0, true);
+	for (size_t k = 0; k < live.size(); k++)
+		gmem(E, G_STORE_DWORDX2, T0, 2 * live[k], RG_REC, 512u + 1024u * (uint32_t)k, true);
+	// tail += n (mod 128), count += n
+	E.sop2(S2_LSHL_B32, RG_T2, opnd{(uint32_t)RG_T0}, opnd{128 + 8});
+	E.sop2(S2_OR_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{(uint32_t)RG_T0});
+	if (sh)
+		E.sop2(S2_LSHL_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{128 + 16});
+	E.sop2(S2_ADD_U32, QS, opnd{(uint32_t)QS}, opnd{(uint32_t)RG_T2});
+	E.sop2(S2_AND_B32, QS, opnd{(uint32_t)QS}, opnd{SRC_LIT, ~(0x80u << sh)});
+	E.sop2(S2_OR_B64, AH_S_DEFER, opnd{(uint32_t)AH_S_DEFER}, opnd{SRC_EXEC});  // queued, not stored
+	E.sop2(S2_ANDN2_B64, 16, opnd{16}, opnd{SRC_EXEC});                        // S_ALIVE
+	jump_cb(E, sched_off, false);
+}
+
+void
+cc_drain_code(const std::vector<cc_regroup_point> &points, uint32_t qbytes,
+	      const std::vector<uint32_t> &resume, uint32_t batch_off, uint32_t drain_ret_off,
+	      std::vector<uint8_t> &out)
+{
+	enc E{out};
+	const size_t nq = points.size();
+	sopc(E, SC_BITCMP1_B32, opnd{7}, opnd{128 + 8});                             // final drain?
+	E.sop2(S2_CSELECT_B32, RG_T3, opnd{128 + 1}, opnd{128 + 64});             // threshold
+	std::vector<size_t> br(nq);
+	for (size_t q = 0; q < nq; q++) {
+		const int QS = AH_S_QS + (int)q / 2, sh = 16 * (int)(q & 1);
+		E.sop2(S2_BFE_U32, RG_T0, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)(8 + sh) | (8u << 16)});
+		sopc(E, SC_CMP_GE_U32, opnd{(uint32_t)RG_T0}, opnd{(uint32_t)RG_T3});
+		br[q] = out.size();
+		E.w(0xbf850000u);                                                  // s_cbranch_scc1 run_q
+	}
+	jump_cb(E, drain_ret_off, false);
+	for (size_t q = 0; q < nq; q++) {
+		const int QS = AH_S_QS + (int)q / 2, sh = 16 * (int)(q & 1);
+		const uint32_t rel = (uint32_t)((out.size() - br[q] - 4) / 4);
+		out[br[q]] = (uint8_t)(rel & 0xff);
+		out[br[q] + 1] = (uint8_t)(rel >> 8);
+		E.sop2(S2_MIN_U32, RG_T1, opnd{(uint32_t)RG_T0}, opnd{128 + 64});      // n
+		E.sop2(S2_BFE_U32, RG_T2, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)sh | (7u << 16)});
+		E.sop2(S2_SUB_U32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{(uint32_t)RG_T0});
+		E.sop2(S2_AND_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{SRC_LIT, 0x7f});   // head
+		E.sop2(S2_LSHL_B32, RG_T0, opnd{(uint32_t)RG_T1}, opnd{128 + 8 + (uint32_t)sh});
+		E.sop2(S2_SUB_U32, QS, opnd{(uint32_t)QS}, opnd{(uint32_t)RG_T0});        // count -= n
+		E.sop2(S2_ADD_U32, RG_REC, opnd{(uint32_t)AH_S_QBASE}, opnd{SRC_LIT, (uint32_t)q * qbytes});
+		E.sop2(S2_ADDC_U32, RG_REC + 1, opnd{(uint32_t)AH_S_QBASE + 1}, opnd{128});
+		jump_cb(E, batch_off, true);                                     // .Lr_batch
+		for (size_t k = 0; k < points[q].live.size(); k++)
+			gmem(E, G_LOAD_DWORDX2, T2, 2 * points[q].live[k], RG_REC, 512u + 1024u * (uint32_t)k,
+			     false);
+		// (the lanes whose packet is shorter than 64 bytes, as the prologue sets them)
+		E.vop3(VC_U32 + P_GT, 74, 128 + 64, VGPR0 + 40, 0);
+		E.w(0xbf8c0f70u);                                                  // s_waitcnt vmcnt(0)
+		jump_cb(E, resume[q], false);
+	}
+}
+
 void
 cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 	   const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
-	   const std::vector<dp_map> &table, std::vector<cc_block> &out)
+	   const std::vector<dp_map> &table, const std::vector<char> &regroup, std::vector<cc_block> &out)
 {
 	const size_t n = low.size();
 	std::vector<mapinfo> maps(table.size());
@@ -1663,7 +1916,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 		std::vector<int16_t> movfuse_fam(n, -1); // ... as this 32-bit operation
 		for (size_t k = 0; k < order.size(); k++) {
 			const uint32_t e = order[k];
-			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u);
+			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u) && !regroup[e];
 			facts f = valid ? in[e] : facts();
 			if (!valid)
 				for (bool &p : f.pv)

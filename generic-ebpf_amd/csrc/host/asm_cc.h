@@ -36,9 +36,44 @@ struct cc_routines {
 // mode 1 = staged 64-B packets (packet loads read v22..v37).  structured: the program runs with
 // structured control flow (asm_jit.cpp): exits and faults are calls that return, compares
 // always leave VCC.  table: the program's maps.
+// regroup[e]: e is a regroup point (its code assumes nothing it did not compute itself).
 void cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 		const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
-		const std::vector<dp_map> &table, std::vector<cc_block> &out);
+		const std::vector<dp_map> &table, const std::vector<char> &regroup,
+		std::vector<cc_block> &out);
+
+// Regrouping (gen_interp.py "Regrouping"; general kernels, unstructured compiled programs).
+// A regroup point is the head of a subtree that both sides of a divergent conditional make
+// heavy and that only computes (ALU, compares, packet loads at constant offsets, exits, faults:
+// no stack, map or helper), so its lanes can run it later in another lane with their packet index
+// and live registers restored.  cc_regroup_plan picks at most AH_RQ_MAX of them (the deepest,
+// none inside another) and returns their live registers (<= 3, ascending), or no point at all
+// when fewer than two qualify.
+struct cc_regroup_point {
+	uint32_t entry;
+	std::vector<uint8_t> live;
+};
+void cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low,
+		     const std::vector<uint32_t> &order, std::vector<cc_regroup_point> &points);
+
+// Bytes of one queue: u32 packet indices [128], then u64 [128] per live-register slot.
+inline uint32_t
+cc_queue_bytes(uint32_t live_slots)
+{
+	return 512u + 1024u * live_slots;
+}
+
+// Code at the head of regroup point q: queue the running lanes (packet index, `live`) and leave
+// the group (jump to the scheduler at sched_off from .Lcb).
+void cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t sched_off,
+		  std::vector<uint8_t> &out);
+
+// The drain code (entered at ebpf_jit_area + 0): run the first queue holding a batch (>= 64
+// entries, or any with s7 bit 8) through .Lr_batch (batch_off) and its point's code (resume[q]),
+// or return to the kernel (drain_ret_off) when none does.
+void cc_drain_code(const std::vector<cc_regroup_point> &points, uint32_t qbytes,
+		   const std::vector<uint32_t> &resume, uint32_t batch_off, uint32_t drain_ret_off,
+		   std::vector<uint8_t> &out);
 
 // The group set-up a compiled program does itself (the kernel jumps straight to it): the packet
 // address (staged mode), r1 = packet, r10 = stack top, zeroes for r0, r2..r9 — the registers in

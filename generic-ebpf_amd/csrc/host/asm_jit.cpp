@@ -33,8 +33,8 @@ enum jt_index {
 	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
-	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE, JT_AREA,
-	JT_AREA_BYTES,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE, JT_RBATCH,
+	JT_SCHED, JT_DRAINRET, JT_AREA, JT_AREA_BYTES,
 	JT_COUNT
 };
 
@@ -144,11 +144,18 @@ fits_simm16(int64_t bytes)
 
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
+// *rq_wave_bytes: the regroup queue bytes each wave of a launch needs (0: the program has no
+// regroup point; gen_interp.py "Regrouping").
+// Area layout: +0 the drain entry (16 bytes: a jump to the drain code, or s_endpgm), +16 the
+// program's start block (where the kernel enters each group), the blocks, the drain code.
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-	     uint32_t *stack_stride, std::string *err)
+	     uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes)
 {
+	if (rq_wave_bytes)
+		*rq_wave_bytes = 0;
+	const uint32_t HDR = 16;
 	const jit_image &I = image_info(mode);
 	if (!I.ok) {
 		*err = I.why;
@@ -267,11 +274,35 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			}
 		}
 	}
+	// regroup points (general kernels, unstructured compiled programs): each block starts with
+	// its push code; the drain code resumes a batch right after it (an entry point)
+	std::vector<cc_regroup_point> rg;
+	std::vector<char> regroup(n, 0);
+	std::vector<int> rq_of(n, -1);
+	std::vector<std::vector<uint8_t>> push(n);
+	uint32_t qbytes = 0;
+	if (mode == 0 && !structured && getenv("EBPF_JIT_NOCC") == nullptr)
+		cc_regroup_plan(xl, low, order, rg);
+	if (!rg.empty()) {
+		size_t slots = 0;
+		for (const cc_regroup_point &p : rg)
+			slots = std::max(slots, p.live.size());
+		qbytes = cc_queue_bytes((uint32_t)slots);
+		for (size_t q = 0; q < rg.size(); q++) {
+			const uint32_t e = rg[q].entry;
+			regroup[e] = 1;
+			entry_point[e] = 1;
+			rq_of[e] = (int)q;
+			cc_push_code((int)q, rg[q].live, qbytes, T[JT_SCHED], push[e]);
+		}
+		if (rq_wave_bytes)
+			*rq_wave_bytes = (uint32_t)rg.size() * qbytes;
+	}
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
 	if (getenv("EBPF_JIT_NOCC") == nullptr)
 		cc_compile(xl, low, order, entry_point, mode, structured,
-			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, cb);
+			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, regroup, cb);
 	else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
 		cc_prologue(mode, 0x7ff, true, false, cb[xl.start].prologue);
@@ -357,8 +388,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() + (uint32_t)cb[e].hoist.size() +
-			      pre_len(e);
+		uint32_t sz = (uint32_t)push[e].size() + join_len(e) + (uint32_t)cb[e].prologue.size() +
+			      (uint32_t)cb[e].hoist.size() + pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
 			sz += (uint32_t)cb[e].body.size();
@@ -387,7 +418,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	auto cont_pos = [&](uint32_t c) { return c == GROUP_END ? end_pos : pos[c]; };
 	uint32_t total = 0;
 	for (int iter = 0; iter < 8; iter++) {
-		total = 0;
+		total = HDR;
 		for (uint32_t e : order) {
 			uint32_t pre, be;
 			pos[e] = total;
@@ -439,6 +470,13 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		if (!changed)
 			break;
 	}
+	// the drain code (its size does not depend on the offsets it jumps to)
+	const uint32_t drain_pos = total;
+	if (!rg.empty()) {
+		std::vector<uint8_t> probe;
+		cc_drain_code(rg, qbytes, std::vector<uint32_t>(rg.size(), 0), 0, 0, probe);
+		total += (uint32_t)probe.size();
+	}
 	if (total > (uint32_t)AH_JIT_AREA_BYTES) {
 		*err = "compiled program exceeds the code area";
 		return E2BIG;
@@ -482,6 +520,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			put32(a, 0xbf800000u | (op << 16) | ((uint32_t)d & 0xffffu));
 		};
 		const uint32_t OP_BRANCH = 0x02, OP_EXECZ = 0x08, OP_EXECNZ = 0x09;
+		if (!push[e].empty()) {
+			memcpy(&img[area + at], push[e].data(), push[e].size());
+			at += push[e].size();
+		}
 		if (structured && join_of[e] >= 0) {
 			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[join_of[e]];
 			put32(at, 0xbe800000u | (126u << 16) | (0x01u << 8) | sk); // s_mov_b64 exec, s[Tk]
@@ -607,6 +649,22 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
 		put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
 	}
+	if (!rg.empty()) { // the drain entry at +0 and the drain code
+		std::vector<uint32_t> resume(rg.size());
+		for (size_t q = 0; q < rg.size(); q++)
+			resume[q] = code_off(rg[q].entry) + (uint32_t)push[rg[q].entry].size();
+		std::vector<uint8_t> dr;
+		cc_drain_code(rg, qbytes, resume, T[JT_RBATCH], T[JT_DRAINRET], dr);
+		if (drain_pos + dr.size() != total) {
+			*err = "internal error: drain code size mismatch";
+			return EINVAL;
+		}
+		memcpy(&img[area + drain_pos], dr.data(), dr.size());
+		put32(0, 0x80000000u | (60u << 16) | (255u << 8) | 4u);           // s_add_u32 s60, s4, lit
+		put32(4, T[JT_AREA] + drain_pos);
+		put32(8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
+		put32(12, 0xbe800000u | (0x1du << 8) | 60u);                        // s_setpc_b64 s[60:61]
+	}
 	if (code)
 		code->assign(img.begin() + area, img.begin() + area + total);
 	return 0;
@@ -616,10 +674,11 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 // module and its kernel.
 int
 asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err)
+	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
+	      uint32_t *rq_wave_bytes)
 {
 	std::vector<unsigned char> img;
-	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err);
+	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, rq_wave_bytes);
 	if (e)
 		return e;
 	if (hipSetDevice(device) != hipSuccess)

@@ -32,11 +32,12 @@ int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vec
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 // asm_jit.cpp
 int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err);
+		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
+		  uint32_t *rq_wave_bytes);
 void asm_jit_release(void *mod);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-		 uint32_t *stack_stride, std::string *err);
+		 uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes = nullptr);
 
 
 namespace {
@@ -90,6 +91,9 @@ struct rows_slot {
 	size_t log_bytes = 0;
 	void *win = nullptr;
 	size_t win_bytes = 0;
+	// compiled programs with regroup points: the stream's queue buffer (any contents)
+	void *rq = nullptr;
+	size_t rq_bytes = 0;
 };
 std::mutex g_rows_lock;
 std::vector<std::vector<rows_slot>> g_rows; // per device (capacity kRowsMax: slots never move)
@@ -201,6 +205,20 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 	*log = static_cast<uint8_t *>(r->log);
 	*win = static_cast<unsigned long long *>(r->win);
 	return 0;
+}
+
+// The stream's regroup queue buffer (>= bytes).
+int
+rq_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		err = grow_zeroed(&r->rq, &r->rq_bytes, bytes);
+	if (!err)
+		*out = static_cast<uint8_t *>(r->rq);
+	return err;
 }
 
 thread_local std::string t_err;
@@ -410,7 +428,7 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	std::string msg;
 	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
-				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg);
+				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_rq_bytes[mode]);
 	dp->build_ms[mode] =
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
@@ -519,6 +537,12 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];
 			fn = dp->jit_fn[mode];
+			if (dp->jit_rq_bytes[mode]) { // regroup queues: a slice per wave the launch can have
+				const size_t bytes = (size_t)asm_max_workgroups(dp->device) * 4 * dp->jit_rq_bytes[mode];
+				if ((err = rq_acquire(dp->device, stream, bytes, &L.rq_buf)))
+					return fail(err, "regroup queues");
+				L.rq_wave_bytes = dp->jit_rq_bytes[mode];
+			}
 		} else {
 			if (variant == 0 && err != E2BIG)
 				return err;

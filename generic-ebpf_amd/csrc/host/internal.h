@@ -121,6 +121,7 @@ struct dprog_device {
 	void *jit_mod[2] = {nullptr, nullptr};   // variant 0: compiled program module, per mode
 	void *jit_fn[2] = {nullptr, nullptr};    // its kernel
 	uint32_t jit_stride[2] = {0, 0};
+	uint32_t jit_rq_bytes[2] = {0, 0};      // regroup queue bytes per wave (0: none)
 	int jit_err[2] = {0, 0};                 // E2BIG etc.: run the interpreter instead
 	double build_ms[2] = {0, 0};             // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
