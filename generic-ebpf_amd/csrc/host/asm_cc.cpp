@@ -1218,7 +1218,7 @@ struct emitter {
 			f.def(d, rf());
 		} else {
 			E.vop1(V1_MOV_B32, L(d), vreg(tmp));
-			mov32(Hi(d), 0);
+			hi0(d);
 			f.def(d, kbits(8 * z));
 		}
 	}
