@@ -2,7 +2,8 @@
 programs (generic-ebpf_amd/randprog.py: every opcode and reference quirk) on the device against the
 oracle, for every device variant, on both kernels: 64-B packets (staged) and packets of random
 length 16..79 at CSR offsets (general kernels, short packets fault), and with regrouping forced
-(EBPF_CC_REGROUP=1, a low size threshold) so that random subtrees are queued and batched.
+(EBPF_CC_REGROUP=1, size thresholds 2 and 1: most random programs get regroup points, so random
+subtrees are queued and batched).
 Compares results, fault codes and post-run packet bytes.
 
   python tools/fuzz_gpu.py [--programs N] [--seed S] [--out DIR]
@@ -56,12 +57,12 @@ def main():
     a = ap.parse_args()
     env = native.Env()
     failed = False
-    configs = [(v, lay, False) for v in (0, 1, 2) for lay in ("staged", "general")]
-    configs += [(0, "general", True)]
+    configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
+    configs += [(0, "general", 2), (0, "general", 1)]   # regrouping, size threshold 2 / 1
     for variant, layout, rg in configs:
         if rg:
             os.environ["EBPF_CC_REGROUP"] = "1"
-            os.environ["EBPF_CC_RG_MIN"] = "4"
+            os.environ["EBPF_CC_RG_MIN"] = str(rg)
         t0 = time.time()
         bad, faults = [], 0
         for k in range(a.programs):
@@ -75,7 +76,7 @@ def main():
         os.environ.pop("EBPF_CC_REGROUP", None)
         os.environ.pop("EBPF_CC_RG_MIN", None)
         print("variant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            variant, layout, " regroup" if rg else "", a.programs, faults, len(bad), bad[:20],
+            variant, layout, " regroup>=%d" % rg if rg else "", a.programs, faults, len(bad), bad[:20],
             time.time() - t0), flush=True)
         failed = failed or bool(bad)
     env.destroy()
