@@ -762,6 +762,22 @@ ebpf_gpu_device_count(void)
 }
 
 EBPF_EXPORT int
+ebpf_dev_init(int ndev)
+{
+	const int n = device_count();
+	if (n <= 0)
+		return fail(ENODEV, "no GPU visible");
+	if (ndev <= 0)
+		ndev = n;
+	if (ndev > n)
+		return fail(ENODEV, "ebpf_dev_init: more devices asked for than visible");
+	for (int d = 0; d < ndev; d++)
+		if (!asm_available(d))
+			return fail(EIO, "device " + std::to_string(d) + ": the kernels' code object did not load");
+	return 0;
+}
+
+EBPF_EXPORT int
 ebpf_gpu_set_device(int device)
 {
 	if (device < 0 || device >= device_count())

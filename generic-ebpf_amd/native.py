@@ -102,7 +102,7 @@ FUNCS = {
     "ebpf_map_get_next_key_from_user": (_I, [_VP, _VP, _VP]),
     "ebpf_map_destroy": (None, [_VP]),
     # ebpf_gpu.h
-    "ebpf_gpu_device_count": (_I, []), "ebpf_gpu_set_device": (_I, [_I]),
+    "ebpf_gpu_device_count": (_I, []), "ebpf_gpu_set_device": (_I, [_I]), "ebpf_dev_init": (_I, [_I]),
     "ebpf_gpu_set_variant": (_I, [_I]), "ebpf_gpu_time_next_launch": (_I, [_VP, _VP]), "ebpf_gpu_last_error": (ctypes.c_char_p, []),
     "ebpf_prog_prepare_device": (_I, [_VP, _I]),
     "ebpf_prog_run_batch": (_I, [_VP, _VP, _VP, _VP, _VP]),
@@ -410,6 +410,11 @@ class Prog:
 
 def gpu_count():
     return lib().ebpf_gpu_device_count()
+
+
+def dev_init(ndev=0):
+    """ebpf_dev_init: load the kernels on devices 0..ndev-1 (0: all); raises EbpfError."""
+    _check(lib().ebpf_dev_init(ndev), "ebpf_dev_init")
 
 
 def time_next_launch(start_event, stop_event):

@@ -98,6 +98,12 @@ struct ebpf_batch_stats {
 /* Number of visible GPUs (0 on a host without one). Never fails. */
 int ebpf_gpu_device_count(void);
 
+/* Initialise the device backend on GPUs 0..ndev-1 (ndev <= 0: every visible GPU): load the
+ * kernels' code object on each, which the first batch on a device would otherwise do.  Optional.
+ * Returns 0, ENODEV (no GPU, or ndev above the visible count), EIO (a code object did not
+ * load on a device; ebpf_gpu_last_error says which).  (ebpf_dev_init) */
+int ebpf_dev_init(int ndev);
+
 /* Translate + upload the program (and its maps) to `device`.  Called implicitly by the run
  * functions; explicit calls move the one-time cost out of a timed region.
  * Returns 0, ENODEV (no GPU / no device code object), E2BIG (program state graph too large),

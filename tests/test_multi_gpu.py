@@ -48,6 +48,23 @@ def test_multi_rejects_bad_devices(env):
             m.destroy()
 
 
+def test_dev_init(native):
+    """ebpf_dev_init: ENODEV with no GPU or more devices than visible; on a GPU
+    host every visible device loads its kernels."""
+    import errno
+    n = native.gpu_count()
+    with pytest.raises(native.EbpfError) as ei:
+        native.dev_init(n + 1)
+    assert ei.value.code == errno.ENODEV
+    if n == 0:
+        with pytest.raises(native.EbpfError) as ei:
+            native.dev_init(0)
+        assert ei.value.code == errno.ENODEV
+    else:
+        native.dev_init(0)
+        native.dev_init(1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ndev", [1, 2, 3])
 def test_run_batch_multi_host_buffers(gpu, env, ndev):
