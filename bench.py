@@ -83,7 +83,7 @@ def parse(argv=None):
 
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
-                   "c4": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26}
+                   "c4": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24, "c5lit": 1 << 22}
 C4H_SLOT_BYTES = 32  # device table slot: u32 used | u32 hash | 4-B key (8-B padded) | 8-B value
 DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
 
@@ -99,7 +99,7 @@ class Workload:
         self.lay = workloads.CONFIGS[cfg]["prog"]()
         self.maps = []
         self.offs = None
-        if cfg == "c5":
+        if workloads.CONFIGS[cfg]["pkt"] == "imix":
             self.pk, self.offs, _ = workloads.packets_imix_range(lo, hi, seed=5)
             self.D = self.n
             return
@@ -129,8 +129,14 @@ class Workload:
         return d_pk.reshape(-1), None
 
     def algorithmic_bytes(self):
-        if self.offs is not None:  # every packet byte + the offsets array
-            return int(np.diff(self.offs).sum()) + 8 * (self.n + 1)
+        if self.offs is not None:
+            # sum of min(len, W) rounded up to 64 B (W = the program's largest
+            # load extent; C5 reads anywhere in its packets) + the offsets array
+            lens = np.diff(self.offs)
+            w = workloads.CONFIGS[self.cfg].get("extent")
+            if w is not None:
+                lens = np.minimum(lens, (w + 63) // 64 * 64)
+            return int(lens.sum()) + 8 * (self.n + 1)
         b = self.n * 64
         if self.cfg == "c4h":  # + one table slot per packet that reaches the lookup (IPv4, not ICMP)
             pk = self.pk

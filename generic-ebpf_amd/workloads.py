@@ -308,6 +308,38 @@ def prog_c5(seed=7, target=256):
     raise ValueError("cannot fit C5")
 
 
+_LIT_BODY = [I("ldxh", R2, R1, 12), I("be", R2, imm=16), I("ldxw", R3, R1, 26),
+             I("be", R3, imm=32), I("xor64_reg", R2, R3), I("mul64_imm", R2, imm=0x1E3779B1),
+             I("ldxw", R4, R1, 30), I("xor64_reg", R2, R4)]
+_LIT_MORE = [I("ldxh", R5, R1, 34), I("xor64_reg", R2, R5), I("ldxh", R5, R1, 36),
+             I("add64_reg", R2, R5), I("mul64_imm", R2, imm=0x27D4EB2D), I("ldxb", R5, R1, 23),
+             I("xor64_reg", R2, R5), I("ldxw", R5, R1, 40), I("xor64_reg", R2, R5),
+             I("rsh64_imm", R2, imm=7), I("ldxdw", R5, R1, 48), I("add64_reg", R2, R5)]
+_LIT_TAIL = [I("and64_imm", R2, imm=0xff), I("mov_reg", R0, R2)]
+
+
+def prog_literal(nslots):
+    """The literal N-slot variant of a classifier: the program written as N
+    consecutive slots, of which the reference's cumulative stepping (slot i at step p goes to
+    i + p) executes only slots 0, 1, 3, 6, 10, ... — 11 of 64, 23 of 256.  The executed slots
+    hold header loads (offsets < 64) and mixing ending in EXIT; the others a never-executed
+    filler."""
+    execd = []
+    i, p = 0, 1
+    while i < nslots:
+        execd.append(i)
+        i, p = i + p, p + 1
+    body = _LIT_BODY + (_LIT_MORE if len(execd) > 11 else [])
+    n = len(execd) - 1 - len(_LIT_TAIL)
+    body = (body * ((n + len(body) - 1) // len(body)))[:n] + _LIT_TAIL + [I("exit")]
+    filler = I("mov_imm", R9, imm=0x5eed).encode()
+    code = [filler] * nslots
+    for s_, ins in zip(execd, body):
+        code[s_] = ins.encode()
+    from .layout import Layout
+    return Layout(b"".join(code), [], len(execd), nslots)
+
+
 def prog_c0():
     """Floor: MOV r0, 2; EXIT (2 executed instructions) — measures staging + retirement."""
     return assemble([I("mov_imm", R0, imm=2), I("exit")])
@@ -336,4 +368,8 @@ CONFIGS = {
                pkt="imix"),
     "c4h": dict(desc="64-insn classify + hashtable lookup (1M-entry table keyed by IPv4 dst), "
                      "64 B packets", prog=prog_c4h, pkt="c4h"),
+    "c3lit": dict(desc="literal 64-slot classify (11 executed), 64 B packets",
+                  prog=lambda: prog_literal(64), pkt="l2l3"),
+    "c5lit": dict(desc="literal 256-slot filter (23 executed), IMIX 64-1500 B packets",
+                  prog=lambda: prog_literal(256), pkt="imix", extent=64),
 }

@@ -407,3 +407,19 @@ def test_many_streams_separate_histograms(gpu, env):
         p.destroy()
         for m in maps:
             m.destroy()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_literal_slot_programs(gpu, env, variant):
+    """The literal 64- and 256-slot variants (bench c3lit / c5lit) on 64-B and IMIX packets."""
+    from generic_ebpf_amd import workloads
+    for n_slots in (64, 256):
+        lay = workloads.prog_literal(n_slots)
+        n = 50000
+        data, offs, _ = workloads.packets_imix(n)
+        for c in (goldens.Case("lit", lay.code, [], [], workloads.packets_l2l3(n, 64), n, 64, None),
+                  goldens.Case("lit", lay.code, [], [], data, n, 0, offs)):
+            want, wf, _, _ = oracle_run(c, nthreads=8)
+            got, gf, _ = device_run(gpu, env, c, variant)
+            np.testing.assert_array_equal(want, got)
+            np.testing.assert_array_equal(wf, gf)

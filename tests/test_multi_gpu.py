@@ -66,6 +66,12 @@ def test_dev_init(native):
 
 
 @pytest.mark.gpu
+def test_dev_init_gpu(gpu):
+    gpu.dev_init(0)
+    gpu.dev_init(gpu.gpu_count())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ndev", [1, 2, 3])
 def test_run_batch_multi_host_buffers(gpu, env, ndev):
     """Shards on one GPU (repeated device index): results, faults and the summed histogram equal

@@ -62,3 +62,14 @@ def test_all_goldens_translate(native, env):
     for f in goldens.all_golden_files():
         for c in goldens.load(f):
             assert _info(native, env, c.code).nentries >= 1
+
+
+def test_literal_slot_programs_execute_the_stepped_slots():
+    """SURVEY.md §8(d) literal N-slot variants: 64 slots execute 11, 256 execute 23 (slots
+    0, 1, 3, 6, ... under cumulative stepping), ending in EXIT."""
+    from generic_ebpf_amd import layout, workloads
+    for n, k in ((64, 11), (256, 23)):
+        lay = workloads.prog_literal(n)
+        seq, how = layout.simulate_slots(lay.code)
+        assert len(lay.code) == 8 * n and how == "exit" and len(seq) == k == lay.main_path_steps
+        assert seq == [i * (i + 1) // 2 for i in range(k)]
