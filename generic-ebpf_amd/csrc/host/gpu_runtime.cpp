@@ -564,13 +564,15 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.hist_rows = static_cast<uint32_t *>(part);
 			L.hist = static_cast<unsigned long long *>(part);
 		}
-		// a program that probes hashtables is bound by their latency and wants every wave;
-		// the others stream packets (asm_runtime.cpp, occupancy)
+		// a compiled program that probes hashtables is bound by their latency and wants every
+		// wave; the others stream packets at 4 workgroups per CU (asm_runtime.cpp, occupancy).
+		// The interpreter (fn == NULL) is bound by its scalar dispatch and wants every wave too:
+		// C4 1.86 -> 1.42 ms at 6 instead of 4 workgroups per CU (profiles/r02/v2occ)
 		bool probes = false;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-				      (mode == 1 && !probes) ? 4u : 0u, ev_start, ev_stop, user_hist,
+				      (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
 				      hist_overwrite);
 	} else {
 		L.prog = dp->d_entries;

@@ -555,8 +555,10 @@ map_device_layout_of(const struct ebpf_map *em)
 	}
 	// at most a quarter full: linear probing then ends within a slot or two almost always
 	// (an unsuccessful search probes (1 + 1/(1-a)^2)/2 = 1.4 slots on average at a = 1/4)
-	uint64_t slots = 16;
-	while (slots < 4ull * em->max_entries)
+	uint64_t slots = 16, per = 4;
+	if (const char *f = getenv("EBPF_HASH_SLOTS_PER_ENTRY")) // (A/B: table size vs probe length)
+		per = std::max<uint64_t>(2, strtoull(f, nullptr, 0));
+	while (slots < per * em->max_entries)
 		slots <<= 1;
 	if (lg > 31 || slots > (1ull << 31) || slots * stride > (1ull << 36))
 		return l;
