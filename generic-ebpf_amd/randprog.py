@@ -22,10 +22,11 @@ _SPECIAL_IMM = [0, 1, -1, 2, 7, 8, 15, 16, 31, 32, 33, 48, 63, 64, 65, 127, 255,
 
 
 class _Gen:
-    def __init__(self, seed, nmaps, map_value_size):
+    def __init__(self, seed, nmaps, map_value_size, writes=False):
         self.g = np.random.default_rng(seed)
         self.nmaps = nmaps
         self.vs = map_value_size
+        self.writes = writes
         self.scalars = [0, 2, 3, 4, 5, 6, 7, 8, 9]
         self.ctx = 1
         self.stack_ok = set()   # initialised stack byte offsets (negative, relative to r10)
@@ -151,6 +152,40 @@ class _Gen:
                 I("mov_imm", 2, imm=self.imm())]
         return out
 
+    def update(self):
+        """map_update_elem (helper 1) or map_delete_elem (helper 2, EINVAL on an array): key and
+        value from the stack, flags 0..3 (3: EINVAL); the return code mixed into a scalar; the
+        pointer-holding argument registers reset to scalars afterwards (the test environment's
+        helper slots, oracle/pyoracle.py DEFAULT_HELPER_KINDS)."""
+        if self.nmaps == 0:
+            return self.alu()
+        out = []
+        if self.ctx != 6:
+            out += [I("mov_imm", 6, imm=0), I("mov64_reg", 6, self.ctx)]
+            self.ctx = 6
+            self.scalars = [0, 2, 3, 4, 5, 7, 8, 9]
+        k = self.scalar()
+        key_mask = self.pick([0x7, 0xff, 0xffffffff])
+        out += [I("mov_reg", 7, k), I("and64_imm", 7, imm=isa.s32(key_mask)),
+                I("stxw", 10, 7, -4)]
+        for off in range(0, self.vs, 8):
+            out.append(I("stxdw", 10, self.scalar(), -32 + off))
+        for b in list(range(-4, 0)) + list(range(-32, -32 + self.vs)):
+            self.stack_ok.add(b)
+        out += [LdDw(1, MapRef(self.r(self.nmaps))),
+                I("mov_imm", 2, imm=0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4)]
+        if self.r(4) == 0:
+            out += [I("call", imm=2)]
+        else:
+            out += [I("mov_imm", 3, imm=0), I("mov64_reg", 3, 10), I("add64_imm", 3, imm=-32),
+                    I("mov_imm", 4, imm=self.r(4)), I("call", imm=1)]
+        dst = self.pick([3, 4, 5, 8, 9])
+        out += [I("mov_imm", dst, imm=self.imm()), I("xor64_reg", dst, 0)]
+        for r in (1, 2, 3, 4):
+            if r != dst:
+                out.append(I("mov_imm", r, imm=self.imm()))
+        return out
+
     def branch(self, depth):
         name = self.pick(_JMP)
         d = self.scalar()
@@ -182,7 +217,7 @@ class _Gen:
             elif k < 16:
                 out += self.pkt_store()
             elif k < 17:
-                out += self.lookup()
+                out += self.update() if (self.writes and self.r(2) == 0) else self.lookup()
             elif depth < 3:
                 out += self.branch(depth)
             else:
@@ -208,8 +243,10 @@ class _Gen:
         return out + [I("exit")]
 
 
-def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None):
-    gen = _Gen(seed, nmaps, map_value_size)
+def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None, writes=False):
+    """writes: half the map helper calls are map_update_elem / map_delete_elem (the device
+    batch semantics: ebpf_gpu.h "Map writes in a device batch")."""
+    gen = _Gen(seed, nmaps, map_value_size, writes)
     nodes = gen.prologue() + gen.block(length) + gen.epilogue()
     rs = reset_stride if reset_stride is not None else int(gen.g.integers(3, 12))
     return assemble(nodes, reset_stride=rs)

@@ -4,7 +4,8 @@ oracle, for every device variant, on both kernels: 64-B packets (staged) and pac
 length 16..79 at CSR offsets (general kernels, short packets fault), and with regrouping forced
 (EBPF_CC_REGROUP=1, size thresholds 2 and 1: most random programs get regroup points, so random
 subtrees are queued and batched).
-Compares results, fault codes and post-run packet bytes.
+Odd-numbered programs also call map_update_elem / map_delete_elem (the device batch semantics).
+Compares results, fault codes, post-run packet bytes and the maps after the batch.
 
   python tools/fuzz_gpu.py [--programs N] [--seed S] [--out DIR]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
@@ -22,7 +23,8 @@ import pkgload  # noqa: E402
 
 pkgload.load()
 import goldens  # noqa: E402
-from helpers import device_run, oracle_run  # noqa: E402
+import pyoracle  # noqa: E402
+from helpers import make_maps  # noqa: E402
 from generic_ebpf_amd import native, randprog, workloads  # noqa: E402
 
 
@@ -40,7 +42,7 @@ def case(k, seed, layout):
     vs = int(g.choice([8, 16]))
     me = int(g.choice([16, 256]))
     lay = randprog.random_program(seed * 100000 + k, length=int(g.integers(10, 120)), nmaps=2,
-                                  map_value_size=vs)
+                                  map_value_size=vs, writes=bool(k & 1))
     maps = [(vs, me, g.integers(0, 256, vs * me, dtype=np.uint8).tobytes()) for _ in range(2)]
     n = int(g.choice([1, 63, 64, 65, 777, 2048]))
     if layout == "staged":
@@ -48,6 +50,29 @@ def case(k, seed, layout):
                             workloads.packets_random(n, 64, seed=k), n, 64, None)
     data, offs = ragged_packets(n, seed * 31 + k)
     return goldens.Case("r%d" % k, lay.code, lay.relocs, maps, data, n, 0, offs)
+
+
+def oracle(c):
+    """(ret, faults, packet bytes after, map bytes after the batch)"""
+    op = pyoracle.OracleProgram(c.code, c.relocs, c.maps)
+    ret, faults, data, _ = op.run(c.data, c.count, c.stride, c.offsets, nthreads=8)
+    return ret, faults, data, [op.map_bytes(i) for i in range(len(c.maps))]
+
+
+def device(env, c, variant):
+    maps = make_maps(native, env, c)
+    p = native.Prog(env, native.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        native.set_variant(variant)
+        data = np.ascontiguousarray(c.data.copy())
+        ret, faults, _ = p.run_batch(data, c.count, c.stride, c.offsets)
+        after = [b"".join(m.lookup(i)[1] for i in range(m.max_entries)) for m in maps]
+        return ret, faults, data, after
+    finally:
+        native.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
 
 
 def main():
@@ -67,11 +92,11 @@ def main():
         bad, faults = [], 0
         for k in range(a.programs):
             c = case(k, a.seed, layout)
-            want, wf, wdata, _ = oracle_run(c, nthreads=8)
-            got, gf, gdata = device_run(native, env, c, variant)
+            want, wf, wdata, wmaps = oracle(c)
+            got, gf, gdata, gmaps = device(env, c, variant)
             faults += int(np.count_nonzero(wf))
             if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
-                    np.array_equal(wdata, gdata)):
+                    np.array_equal(wdata, gdata) and wmaps == gmaps):
                 bad.append(k)
         os.environ.pop("EBPF_CC_REGROUP", None)
         os.environ.pop("EBPF_CC_RG_MIN", None)
