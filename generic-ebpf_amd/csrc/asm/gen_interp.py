@@ -1183,6 +1183,20 @@ def routines():
           "v_mov_b32 %s, %s" % (v(R[8]), s(S_CODE)),
           "global_store_byte %s, %s, %s" % (v(R[9]), v(R[8]), sp(S_FAULTS)),
           ".Lfl_nofault:",
+          # a program with map writes: the packet's bit in dp_launch.upd_faulted (its logged
+          # writes do not land; map_writes.hip)
+          "s_load_dwordx2 %s, s[0:1], 0xa8" % sp(S_JUNK),
+          "s_load_dword %s, s[0:1], 0x90" % s(S_BYTES),            # pkt_base (low word)
+          "s_waitcnt lgkmcnt(0)",
+          "s_cmp_eq_u64 %s, 0" % sp(S_JUNK),
+          "s_cbranch_scc1 .Lfl_nomark"] + lane_pkt_index(R[9]) + [
+          "v_add_u32 %s, %s, %s" % (v(R[9]), s(S_BYTES), v(R[9])),
+          "v_lshrrev_b32 %s, 5, %s" % (v(R[8]), v(R[9])),
+          "v_lshlrev_b32 %s, 2, %s" % (v(R[8]), v(R[8])),
+          "v_and_b32 %s, 31, %s" % (v(R[10]), v(R[9])),
+          "v_lshlrev_b32_e64 %s, %s, 1" % (v(R[10]), v(R[10])),
+          "global_atomic_or %s, %s, %s" % (v(R[8]), v(R[10]), sp(S_JUNK)),
+          ".Lfl_nomark:",
           # bin 256 (faulted) goes straight to the global histogram: faults are rare, and the
           # LDS histogram then holds exactly 256 bins (1 KB)
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
@@ -2197,7 +2211,7 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 168
+    kernarg = 176
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),

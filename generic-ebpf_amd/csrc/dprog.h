@@ -123,8 +123,12 @@ struct dp_launch {
 	uint8_t *rq_buf;
 	uint32_t rq_wave_bytes;
 	uint32_t rq_pad;
+	// map writes: one bit per packet of the batch (index pkt_base + i, cleared by the host before
+	// the batch), set when the packet faults; the apply step skips a faulted packet's logged
+	// writes (a packet that faults leaves no write behind).  NULL for programs without map writes
+	uint32_t *upd_faulted;
 };
-static_assert(sizeof(dp_launch) == 168, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 176, "dp_launch layout is shared with the assembly kernels");
 
 // Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
 // EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B

@@ -398,6 +398,10 @@ ebpf_interp_v0(dp_launch L)
 		L.ret[gid] = fault ? 0 : result;
 		if (L.faults)
 			L.faults[gid] = (uint8_t)fault;
+		if (fault && L.upd_faulted) { // its logged map writes do not land
+			const uint32_t b = (uint32_t)(L.pkt_base + gid);
+			atomicOr(&L.upd_faulted[b >> 5], 1u << (b & 31));
+		}
 		if (L.hist)
 			atomicAdd(&hist[fault ? 256 : (result < 255 ? (unsigned)result : 255u)], 1u);
 	}

@@ -25,11 +25,15 @@ rec_order(const uint8_t *r)
 
 __global__ void __launch_bounds__(256)
 upd_offer(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
-	  const upd_map *__restrict__ maps, unsigned long long *__restrict__ win)
+	  const upd_map *__restrict__ maps, unsigned long long *__restrict__ win,
+	  const uint32_t *__restrict__ faulted)
 {
 	const uint32_t n = min(*reinterpret_cast<const uint32_t *>(log), cap);
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
 		const uint8_t *r = log + 64 + (uint64_t)i * stride;
+		const uint32_t pkt = *reinterpret_cast<const uint32_t *>(r);
+		if (faulted && ((faulted[pkt >> 5] >> (pkt & 31)) & 1u))
+			continue; // the packet faulted after this write: no write of it lands
 		const uint32_t mi = *reinterpret_cast<const uint32_t *>(r + 8) >> 20;
 		const uint32_t key = *reinterpret_cast<const uint32_t *>(r + 12);
 		atomicMax(&win[maps[mi].win_off + key], (unsigned long long)rec_order(r));
@@ -60,12 +64,13 @@ upd_apply(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 
 hipError_t
 launch_map_writes(const uint8_t *log, uint32_t cap, uint32_t stride, const upd_map *maps,
-		  unsigned long long *win, hipStream_t stream)
+		  unsigned long long *win, const uint32_t *faulted, hipStream_t stream)
 {
 	if (cap == 0)
 		return hipSuccess;
 	const uint32_t blocks = std::min<uint32_t>((cap + 255) / 256, 2048);
-	hipLaunchKernelGGL(upd_offer, dim3(blocks), dim3(256), 0, stream, log, cap, stride, maps, win);
+	hipLaunchKernelGGL(upd_offer, dim3(blocks), dim3(256), 0, stream, log, cap, stride, maps, win,
+			   faulted);
 	hipLaunchKernelGGL(upd_apply, dim3(blocks), dim3(256), 0, stream, log, cap, stride, maps, win);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)

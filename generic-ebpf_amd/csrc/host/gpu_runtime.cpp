@@ -468,19 +468,41 @@ struct upd_plan {
 	unsigned long long *win = nullptr;
 	uint32_t cap = 0;
 	uint64_t pkt_base = 0;
+	uint32_t *faulted = nullptr; // one bit per packet of the batch (after the records)
+	size_t faulted_bytes = 0;
 };
 
-// Log capacity for `count` packets of a map-writing program (records, and bytes).
+// Log capacity for `count` packets of a map-writing program (records, and bytes: the records,
+// then the faulted-packet bitmap at *bitmap_off, *bitmap_bytes long).
 int
 upd_size(const struct ebpf_prog *ep, const dprog_device *dp, uint64_t count, uint32_t *cap,
-	 size_t *bytes)
+	 size_t *bytes, size_t *bitmap_off, size_t *bitmap_bytes)
 {
 	const uint64_t rec = count * ep->xlated->max_updates;
 	if (rec > UINT32_MAX)
 		return fail(E2BIG, "map-writing program: more than 2^32 writes in one batch");
 	*cap = (uint32_t)rec;
-	*bytes = 64 + rec * dp->upd_stride;
+	*bitmap_off = (64 + rec * dp->upd_stride + 255) & ~(size_t)255;
+	*bitmap_bytes = ((count + 31) / 32) * 4;
+	*bytes = *bitmap_off + *bitmap_bytes;
 	return 0;
+}
+
+// The log (and its bitmap) for `count` packets on `stream`.
+int
+upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t stream, upd_plan *P)
+{
+	size_t bytes, boff, bbytes;
+	int err = upd_size(ep, dp, count, &P->cap, &bytes, &boff, &bbytes);
+	if (!err)
+		err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &P->log, &P->win);
+	if (err)
+		return fail(err, "map-write log");
+	P->faulted = reinterpret_cast<uint32_t *>(P->log + boff);
+	P->faulted_bytes = bbytes;
+	// (the buffer is reused at other sizes: whatever lies where the bitmap now starts is stale)
+	hipError_t e = hipMemsetAsync(P->faulted, 0, bbytes, stream);
+	return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync(faulted-packet bitmap)");
 }
 
 // After the batch: the logged writes land in the mirrors (packet order), and the written maps
@@ -489,7 +511,7 @@ int
 upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
 {
 	hipError_t e = launch_map_writes(P.log, P.cap, dp->upd_stride,
-					 static_cast<const upd_map *>(dp->d_upd), P.win, stream);
+					 static_cast<const upd_map *>(dp->d_upd), P.win, P.faulted, stream);
 	if (e != hipSuccess)
 		return hip_fail(e, "map writes");
 	for (uint16_t t : ep->xlated->upd_maps)
@@ -513,18 +535,14 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	hipError_t e;
 	upd_plan own;
 	if (ep->xlated->max_updates) {
-		if (plan == nullptr) { // this launch is the whole batch: its own log, applied below
-			size_t bytes;
-			if ((err = upd_size(ep, dp, L0.count, &own.cap, &bytes)) ||
-			    (err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &own.log,
-					       &own.win)))
-				return fail(err, "map-write log");
-		}
+		if (plan == nullptr && (err = upd_plan_for(ep, dp, L0.count, stream, &own)))
+			return err; // (this launch is the whole batch: its own log, applied below)
 		const upd_plan &P = plan ? *plan : own;
 		L.upd_log = P.log;
 		L.upd_cap = P.cap;
 		L.upd_stride = dp->upd_stride;
 		L.pkt_base = P.pkt_base;
+		L.upd_faulted = P.faulted;
 	}
 	const int variant = effective_variant(dp->device);
 	if (variant == 0 || variant == 2) {
@@ -971,13 +989,8 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	// a map-writing program: one log for the whole shard, applied after its last chunk (every
 	// chunk reads the maps as they were when the batch started)
 	upd_plan plan;
-	if (ep->xlated->max_updates) {
-		size_t bytes;
-		if ((err = upd_size(ep, dp, hi - lo, &plan.cap, &bytes)) ||
-		    (err = upd_acquire(S.device, S.stream[0], bytes, dp->win_words * 8, &plan.log,
-				       &plan.win)))
-			return fail(err, "map-write log");
-	}
+	if (ep->xlated->max_updates && (err = upd_plan_for(ep, dp, hi - lo, S.stream[0], &plan)))
+		return err;
 	bool timed[2] = {false, false};
 	// on any error: drain both streams (buffers stay valid for the copies in flight)
 	auto drain = [&](int rc) {

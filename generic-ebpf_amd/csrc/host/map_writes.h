@@ -11,7 +11,8 @@ struct upd_map {
 	uint64_t win_off;     // first winner word of this map (one u64 per key)
 };
 
-// Apply the log's records to the mirrors (last write per key, packet order) and re-arm the
+// Apply the log's records to the mirrors (last write per key, packet order) but those of the
+// packets whose bit is set in `faulted` (the host clears it before the batch), and re-arm the
 // log's counter; `win` holds sum(max_entries) zeroed u64 and is left zero.
 hipError_t launch_map_writes(const uint8_t *log, uint32_t cap, uint32_t stride, const upd_map *maps,
-			     unsigned long long *win, hipStream_t stream);
+			     unsigned long long *win, const uint32_t *faulted, hipStream_t stream);

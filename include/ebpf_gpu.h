@@ -40,7 +40,8 @@ struct ebpf_map;
  *     EBPF_EXIST, EEXIST for EBPF_NOEXIST (an array's keys all exist), EINVAL for a key >=
  *     max_entries, else 0;
  *   - after the batch the writes land in packet order, a packet's own in call order: the last
- *     write of a key wins;
+ *     write of a key wins; a packet that faults (any code, even after its writes) leaves no
+ *     write behind;
  *   - map_delete_elem on an array map returns EINVAL (ebpf_map_array.c:246-250);
  *   - on a hashtable map both helpers fault EBPF_FAULT_HELPER_UNSUPPORTED;
  *   - the map of every write must be known at translation time (r1 loaded by LDDW), else the

@@ -88,6 +88,51 @@ def prog_hash_update():
     return layout.assemble(n)
 
 
+def prog_fault_after_write():
+    """key = pkt[0] & 15, value = pkt[8..16): an update (always in range, flags 0), then
+    r0 = 7 / (pkt[1] & 1): a packet with an even pkt[1] faults DIV_ZERO after its write."""
+    from generic_ebpf_amd import layout
+    I, LdDw, MapRef, Branch = _nodes()
+    n = [I("ldxb", R6, R1, 0), I("ldxb", R7, R1, 1), I("ldxdw", R8, R1, 8),
+         I("and_imm", R6, imm=15), I("and_imm", R7, imm=1),
+         I("stxw", R10, R6, -4), I("stxdw", R10, R8, -16),
+         LdDw(R1, MapRef(0)),
+         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+         I("mov_imm", R3, imm=0), I("mov64_reg", R3, R10), I("add64_imm", R3, imm=-16),
+         I("mov_imm", R4, imm=0), I("call", imm=1),
+         I("mov_imm", R0, imm=7), I("div64_reg", R0, R7), I("exit")]
+    return layout.assemble(n)
+
+
+def _expect_fault_after_write(pk, init):
+    vals = np.frombuffer(init, dtype=np.uint64).copy()
+    ret, faults = [], []
+    for p in pk:
+        if int(p[1]) & 1:
+            vals[int(p[0]) & 15] = np.frombuffer(p[8:16].tobytes(), dtype=np.uint64)[0]
+            ret.append(7)
+            faults.append(0)
+        else:
+            ret.append(0)
+            faults.append(2)
+    return np.array(ret, dtype=np.uint64), np.array(faults, dtype=np.uint8), vals.tobytes()
+
+
+def test_oracle_faulting_packet_leaves_no_write():
+    """A packet that faults after its map_update_elem leaves no write behind (include/ebpf_gpu.h,
+    "Map writes in a device batch")."""
+    n = 3000
+    pk = _packets(n, 13)
+    init = _map_init(8)
+    lay = prog_fault_after_write()
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    ret, faults, _, _ = op.run(pk, n, 64, nthreads=4)
+    want, wf, after = _expect_fault_after_write(pk, init)
+    np.testing.assert_array_equal(ret, want)
+    np.testing.assert_array_equal(faults, wf)
+    assert op.map_bytes(0) == after
+
+
 def _map_init(seed=5):
     return np.random.default_rng(seed).integers(0, 2**63, NKEYS, dtype=np.uint64).tobytes()
 
@@ -281,3 +326,18 @@ def test_device_hash_update_faults(gpu, env, variant):
         gpu.set_variant(0)
         p.destroy()
         hm.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_faulting_packet_leaves_no_write(gpu, env, variant, resident):
+    n = (1 << 17) + 5
+    pk = _packets(n, 14)
+    init = _map_init(9)
+    ret, faults, after = _run_device(gpu, env, prog_fault_after_write(), [(8, NKEYS, init)], pk,
+                                     variant, resident)
+    want, wf, want_after = _expect_fault_after_write(pk, init)
+    np.testing.assert_array_equal(faults, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == want_after
