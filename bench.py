@@ -23,7 +23,9 @@ launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so 
 with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 10th timed step
 carries the events (--time-every).  roofline.traffic is measured by THIS run: two child passes
 of this script under rocprofv3 --pmc (FETCH_SIZE, then WRITE_SIZE) on the same workload, after
-the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).
+the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).  Programs on
+the general kernel (divergent, any packet size: C5) get a third pass (SQ_INSTS_VALU / _SALU /
+_VMEM_RD) for roofline.issue, the VALU-issue floor that divergence puts under such a launch.
 
 Prints ONE JSON line on rank 0.
 """
@@ -49,6 +51,8 @@ pkg = pkgload.load()
 from generic_ebpf_amd import native, shard, workloads  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+SIMDS, CLOCK_GHZ, VALU_ISSUE_CYCLES = 256 * 4, 2.4, 4  # MI355X: 256 CUs x 4 SIMD16, wave64 VALU
+ISSUE_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD")
 METRIC = "Mpkt/s device-resident (64-insn filter, 64B pkts); achieved HBM GB/s vs peak"
 # Round-1 calibration in the build container, C4, 1 thread: the genuine reference libebpf.so
 # 9.1 Mpkt/s, this oracle (port) 7.6 Mpkt/s
@@ -289,10 +293,15 @@ def pmc_traffic(a, w, total, layout):
              str(total), "--steps", "2", "--warmup", "1", "--variant", str(a.variant),
              "--no-cpu-baseline", "--no-pmc", "--no-verify"]
     vals = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    # general kernels (divergent programs): also the instruction counts of the issue roofline
+    passes = [("FETCH_SIZE",), ("WRITE_SIZE",)]
+    if layout == 0:
+        passes.append(ISSUE_COUNTERS)
+    for group in passes:
+        counter = group[0]
         d = os.path.join(out, "pmc_%s_%s" % (a.config, counter))
         os.makedirs(d, exist_ok=True)
-        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "--kernel-trace",
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc"] + list(group) + ["--kernel-trace",
                "--kernel-include-regex", "ebpf_(interp|jit)", "--output-format", "csv",
                "-d", d, "-o", "pmc", "--"] + child
         env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
@@ -300,25 +309,47 @@ def pmc_traffic(a, w, total, layout):
         if r.returncode != 0:
             return None, "%s pass exited %d: %s" % (counter, r.returncode,
                                                      r.stderr.decode(errors="replace")[-300:])
-        per = {}
-        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    kn = row.get("Kernel_Name", "")
-                    if row.get("Counter_Name") != counter or not (
-                            "ebpf_interp" in kn or "ebpf_jit" in kn):
-                        continue
-                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-        if not per:
-            return None, "%s pass recorded no engine dispatch" % counter
-        vals[counter] = sum(per.values()) / len(per) * 1024.0
+        for c in group:
+            per = {}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        kn = row.get("Kernel_Name", "")
+                        if row.get("Counter_Name") != c or not (
+                                "ebpf_interp" in kn or "ebpf_jit" in kn):
+                            continue
+                        per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+            if not per:
+                return None, "%s pass recorded no engine dispatch" % c
+            vals[c] = sum(per.values()) / len(per) * (1024.0 if c.endswith("_SIZE") else 1.0)
     fetch = vals["FETCH_SIZE"]
     note = "FETCH_SIZE + WRITE_SIZE per launch, this run"
     if layout == 1:
         fetch += w.n * 64 / 2.0
         note += "; staged 64-B packet DMA: half its bytes added (gfx950 16-B/lane undercount)"
     return {"bytes": fetch + vals["WRITE_SIZE"], "fetch_reported": vals["FETCH_SIZE"],
-            "write": vals["WRITE_SIZE"], "note": note}, None
+            "write": vals["WRITE_SIZE"], "note": note,
+            "insts": {c: vals[c] for c in ISSUE_COUNTERS if c in vals}}, None
+
+
+def issue_roofline(insts, kern_ms, groups):
+    """The second roofline of a divergent program (general kernels): VALU issue.  A wave64
+    VALU instruction occupies its SIMD (16 lanes wide) for 4 cycles, so the launch cannot
+    finish before SQ_INSTS_VALU x 4 / (SIMDs x clock) (MI355X: 256 CUs x 4 SIMDs, 2.4 GHz
+    peak engine clock; MI355X_MICROARCH.md).  Divergence multiplies the VALU count: every path
+    a 64-packet group takes is issued once for the whole wave."""
+    valu = insts.get("SQ_INSTS_VALU")
+    if not valu:
+        return None
+    floor_ms = valu * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_GHZ * 1e9) * 1e3
+    return {"bound": "valu-issue", "valu_insts": int(valu),
+            "valu_per_group": round(valu / max(1, groups), 1),
+            "salu_per_group": round(insts.get("SQ_INSTS_SALU", 0) / max(1, groups), 1),
+            "vmem_rd_per_group": round(insts.get("SQ_INSTS_VMEM_RD", 0) / max(1, groups), 1),
+            "floor_ms": round(floor_ms, 4), "kernel_ms": round(kern_ms, 4),
+            "frac": round(floor_ms / kern_ms, 4) if kern_ms > 0 else None,
+            "model": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz), this run's PMC pass" % (
+                VALU_ISSUE_CYCLES, SIMDS, CLOCK_GHZ)}
 
 
 def main():
@@ -453,9 +484,12 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(w, a.cpu_seconds)
         traffic, pmc_note = None, "not collected (N > 1)" if world > 1 else "disabled (--no-pmc)"
+        issue = None
         if not a.no_pmc and world == 1:
             t, err = pmc_traffic(a, w, total, layout)
             traffic, pmc_note = (t["bytes"], t["note"]) if t else (None, err)
+            if t and t["insts"]:
+                issue = issue_roofline(t["insts"], kern_ms, (n + 63) // 64)
         out = {
             "metric": METRIC,
             "value": round(value, 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
@@ -477,7 +511,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": traffic, "traffic_note": pmc_note,
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": len(evs),
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "issue": issue},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

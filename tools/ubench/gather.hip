@@ -10,6 +10,9 @@
 //   MODE 4: NL distinct 16-B aligned windows per lane as dwordx4 loads (the same bytes fetched
 //           with fewer, wider lane loads)
 //   MODE 5: NL distinct 8-B aligned windows per lane as dwordx2 loads
+//   MODE 6: as 2, but the loads are FLAT loads whose addresses fall in the LDS aperture (does
+//           a flat load routed to LDS cost what ds_read does, or what the TA gather path does?)
+//   MODE 7: as 6 with half the lanes' packets left in global memory (per-lane routing mix)
 // Grid: waves per CU x 256 CUs workgroups of one wave.  Prints ms and lane-loads per ns.
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -80,7 +83,19 @@ __global__ void __launch_bounds__(64) k_gather(const uint8_t *__restrict__ in, u
 	for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
 		const uint64_t pkt = (uint64_t)g * 64 + lane;
 		uint64_t acc = 0;
-		if constexpr (MODE == 2) {
+		if constexpr (MODE == 6 || MODE == 7) {
+			const uint8_t *src = in + (uint64_t)g * 64 * P;
+			constexpr uint32_t span = 64u * P;
+			for (uint32_t q = 0; q < span; q += 1024)
+				__builtin_amdgcn_global_load_lds((const void *)(src + q + lane * 16), LDS_PTR(lds + q), 16, 0, 2);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			const uint8_t *gp = (const uint8_t *)lds + lane * P;
+			if (MODE == 7 && (lane & 1))
+				gp = in + pkt * P;
+			asm volatile("" : "+v"(gp));   // generic pointer: flat loads
+			fold<P, NL>(gp, acc);
+			asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n s_barrier" ::: "memory");
+		} else if constexpr (MODE == 2) {
 			const uint8_t *src = in + (uint64_t)g * 64 * P;
 			constexpr uint32_t span = 64u * P;
 			for (uint32_t q = 0; q < span; q += 1024)
@@ -112,7 +127,7 @@ static void run(int wpc, uint32_t npkt) {
 	hipMalloc(&in, (size_t)npkt * P);
 	hipMalloc(&out, (size_t)npkt * 8);
 	hipMemset(in, 0x5b, (size_t)npkt * P);
-	const size_t lds = MODE == 2 ? 64u * P : 0;
+	const size_t lds = (MODE == 2 || MODE >= 6) ? 64u * P : 0;
 	if (lds > 65536)
 		hipFuncSetAttribute((const void *)k_gather<P, NL, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				    (int)lds);
@@ -141,6 +156,15 @@ static void run(int wpc, uint32_t npkt) {
 
 int main(int argc, char **argv) {
 	const uint32_t n = 1u << 22;
+	if (argc > 1 && argv[1][0] == 'f') {   // flat-to-LDS study
+		for (int w : {1, 2, 4}) {
+			run<576, 56, 2>(w, n);
+			run<576, 56, 6>(w, n);
+			run<576, 56, 7>(w, n);
+		}
+		run<576, 56, 0>(8, n);
+		return 0;
+	}
 	for (int w : {8, 24}) {
 		run<576, 56, 0>(w, n);
 		run<576, 29, 4>(w, n);
