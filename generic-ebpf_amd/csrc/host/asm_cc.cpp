@@ -1204,14 +1204,41 @@ struct emitter {
 	// hoist plan in cc_compile): the bounds check at its own place (MEM fault for lanes whose
 	// packet is shorter than off + z, like the handler), then wait for it (vmcnt <= the loads
 	// issued after it) and copy.
-	void ldx_hoisted(int d, int z, uint32_t off, int tmp, uint32_t later, uint32_t fault_off)
+	//
+	// With the run mask (s[76:77], see cc_compile) the lanes in the mask hold the load already
+	// and cannot fault on it; only when a running lane is outside the mask does the use compare:
+	// fault the lanes past their packet's end, load for the others directly (and wait for it).
+	void ldx_hoisted(int d, int z, uint32_t off, int tmp, uint32_t later, uint32_t fault_off,
+			 bool runmask)
 	{
-		const int S_MASK = 48, S_CODE = 52, V_LEN = 40;
+		const int S_MASK = 48, S_CODE = 52, V_LEN = 40, S_JUNK_ = 60, V_PKT = 38;
+		size_t br = 0, from = 0;
+		if (runmask) {
+			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_DEFER}); // s_andn2_b64
+			br = E.b.size();
+			E.w(0xbf840000u); // s_cbranch_scc0 over the block below (its length set at its end)
+			from = E.b.size();
+		}
 		E.vopc(VC_U32 + P_GT, k32(off + (uint32_t)z), V_LEN);          // vcc = off + z > len
 		E.sop2(0x0d, S_MASK, opnd{SRC_VCC}, opnd{SRC_EXEC});             // s_and_b64
 		E.w(0xbf840000u | 5u);                                           // s_cbranch_scc0 +5
 		E.sop1(0x00, S_CODE, opnd{128 + 3});                             // s_mov_b32 s52, 3
 		call_routine(fault_off, 0);                                      // (4 dwords)
+		if (runmask) {
+			static const uint32_t gop[4] = {0x10, 0x12, 0x14, 0x15};
+			const int zi = z == 1 ? 0 : z == 2 ? 1 : z == 4 ? 2 : 3;
+			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_DEFER}); // in bounds, unmasked
+			E.w(0xbf840000u | 6u);                                           // s_cbranch_scc0 +6
+			E.sop1(0x01, S_JUNK_, opnd{SRC_EXEC});                           // s_mov_b64 s60, exec
+			E.sop1(0x01, 126, opnd{(uint32_t)S_MASK});                       // s_mov_b64 exec, s48
+			E.w(0xdc008000u | (gop[zi] << 18) | off);                        // global_load_* tmp
+			E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)tmp << 24));
+			E.w(0xbf8c0f70u);                                                // s_waitcnt vmcnt(0)
+			E.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});                      // s_mov_b64 exec, s60
+			const uint32_t skip = (uint32_t)((E.b.size() - from) / 4);
+			E.b[br] = (uint8_t)skip;
+			E.b[br + 1] = (uint8_t)(skip >> 8);
+		}
 		E.w(0xbf8c0000u | (later & 15u) | (7u << 4) | (15u << 8) | ((later >> 4) & 3u) << 14);
 		if (z == 8) {
 			E.vop1(V1_MOV_B64, L(d), vreg(tmp));
@@ -1841,6 +1868,16 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	std::vector<uint16_t> hoist_later(n, 0);
 	std::vector<std::vector<uint32_t>> hoist_at(n);
 	std::vector<uint32_t> hoist_next(n, UINT32_MAX); // the load to issue after this one is used
+	// Run mask (general kernels, programs without regroup points, whose s[76:77] is then free):
+	// the run head tests every running lane against the run's largest load extent once (one
+	// VALU compare into s[76:77]); the run's loads are issued for those lanes with no per-load
+	// compare, and a use only compares (bounds check, fault, direct load) when some running
+	// lane missed the mask.  Two VALU per hoisted load fewer; EBPF_CC_NORUNMASK=1 keeps the
+	// per-load compares (A/B).
+	const bool runmask = mode == 0 &&
+			     std::none_of(regroup.begin(), regroup.end(), [](char c) { return c != 0; }) &&
+			     getenv("EBPF_CC_NORUNMASK") == nullptr;
+	std::vector<uint32_t> run_ext(n, 0); // run head: the largest off + size of its hoisted loads
 	if (mode == 0 && AH_GEN_HOIST_REGS > 0 && getenv("EBPF_CC_NOHOIST") == nullptr) {
 		size_t k = 0;
 		while (k < order.size()) {
@@ -1894,6 +1931,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				const size_t slots = AH_GEN_HOIST_REGS / 2;
 				size_t issued = std::min(slots, ld.size());
 				hoist_at[order[k]].assign(ld.begin(), ld.begin() + issued);
+				for (uint32_t x : ld)
+					run_ext[order[k]] = std::max<uint32_t>(
+					    run_ext[order[k]],
+					    (uint32_t)low[x].imm + (1u << (ah_fam[(uint32_t)low[x].handler] - AHF_LDXPKTG1)));
 				for (size_t i = 0; i < ld.size(); i++) {
 					hoist_tmp[ld[i]] = (int16_t)(AH_GEN_HOIST_BASE + 2 * (i % slots));
 					hoist_later[ld[i]] = (uint16_t)(issued - 1 - i);
@@ -1954,22 +1995,38 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			em.off = off;
 			bool break_mov = false;
 			// issue packet load x into its ring slot, for the lanes whose packet holds it
-			auto issue = [&](enc &Hq, uint32_t x) {
+			// (masked: exec is already the lanes to load for, the run head's batch)
+			auto issue = [&](enc &Hq, uint32_t x, bool masked = false) {
 				const int S_JUNK_ = 60, V_LEN = 40, V_PKT = 38;
 				const int fx = ah_fam[(uint32_t)low[x].handler];
 				const int z = 1 << (fx - AHF_LDXPKTG1);
 				const uint32_t K32 = (uint32_t)low[x].imm;
 				static const uint32_t gop[4] = {0x10, 0x12, 0x14, 0x15};
-				Hq.vopc(VC_U32 + P_LE, k32(K32 + (uint32_t)z), V_LEN); // vcc = off+z <= len
-				Hq.sop1(0x20, S_JUNK_, opnd{SRC_VCC});                  // s_and_saveexec_b64
+				if (masked) {
+				} else if (runmask) {
+					Hq.sop1(0x20, S_JUNK_, opnd{(uint32_t)AH_S_DEFER}); // s_and_saveexec_b64
+				} else {
+					Hq.vopc(VC_U32 + P_LE, k32(K32 + (uint32_t)z), V_LEN); // vcc = off+z <= len
+					Hq.sop1(0x20, S_JUNK_, opnd{SRC_VCC});                  // s_and_saveexec_b64
+				}
 				Hq.w(0xdc008000u | (gop[fx - AHF_LDXPKTG1] << 18) | K32);  // global_load_*
 				Hq.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)hoist_tmp[x] << 24));
-				Hq.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});           // s_mov_b64 exec
+				if (!masked)
+					Hq.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});       // s_mov_b64 exec
 			};
 			if (!hoist_at[e].empty()) {
 				enc Hq{blk.hoist};
-				for (uint32_t x : hoist_at[e])
-					issue(Hq, x);
+				if (runmask) { // s[76:77] = the running lanes whose packet holds every load of the run
+					Hq.vopc(VC_U32 + P_LE, k32(run_ext[e]), 40); // vcc = ext <= len (v40)
+					Hq.sop1(0x01, AH_S_DEFER, opnd{SRC_VCC});    // s_mov_b64
+					Hq.sop1(0x20, 60, opnd{SRC_VCC});            // s_and_saveexec_b64 s[60:61]
+					for (uint32_t x : hoist_at[e])
+						issue(Hq, x, true);
+					Hq.sop1(0x01, 126, opnd{60u});               // s_mov_b64 exec, s[60:61]
+				} else {
+					for (uint32_t x : hoist_at[e])
+						issue(Hq, x);
+				}
 			}
 			bool ok = true, spec_map = false;
 			// a 32-bit MOV d = s whose only successor operates on d with an immediate: the
@@ -2003,7 +2060,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = em.alu32i(movfuse_fam[e], d, (uint32_t)K, movfuse_src[e]);
 			} else if (hoist_tmp[e] >= 0) {
 				em.ldx_hoisted(d, 1 << (fam - AHF_LDXPKTG1), (uint32_t)K, hoist_tmp[e], hoist_later[e],
-					       rt.fault);
+					       rt.fault, runmask);
 				if (hoist_next[e] != UINT32_MAX)
 					issue(em.E, hoist_next[e]);
 			}
