@@ -360,13 +360,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # nccl (= RCCL) on the node; EBPF_BENCH_BACKEND=gloo rehearses N > 1 on one GPU
-        dist.init_process_group(os.environ.get("EBPF_BENCH_BACKEND", "nccl"))
-    if world > 1 and os.environ.get("EBPF_BENCH_BACKEND") == "gloo":
+    backend = os.environ.get("EBPF_BENCH_BACKEND", "nccl")
+    if world > 1 and backend == "gloo":   # rehearsal of N > 1 with every rank on one GPU
         local = local % max(1, torch.cuda.device_count())
+    # the rank's GPU is bound before the process group exists, so that RCCL's communicator and
+    # its barrier use this device (not a guess from the rank number)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # nccl (= RCCL) on the node; EBPF_BENCH_BACKEND=gloo rehearses N > 1 on one GPU
+        dist.init_process_group(backend)
     cfg = a.config
     size = a.packets or DEFAULT_PACKETS[cfg]
     if a.scaling == "strong":

@@ -1,6 +1,7 @@
 """Re-expression of the reference's own API tests (tests/ebpf_prog_tests/prog_load_test.cpp,
 tests/ebpf_map_tests/{map_*,array_map_*}_test.cpp) against the engine's libebpf.so, plus the
 drop-in ABI: struct layouts and every exported symbol the headers declare."""
+import os
 import ctypes
 import errno
 import struct
@@ -224,3 +225,18 @@ def test_batch_flags_validation(native, env):
         assert L.ebpf_prog_run_batch(p.ptr, ctypes.byref(host), ret, None, None) == errno.EINVAL
     finally:
         p.destroy()
+
+
+def test_bench_issue_roofline():
+    """bench.py's VALU-issue roofline (general kernels): SQ_INSTS_VALU x 4 cycles over 1,024
+    SIMDs at 2.4 GHz, per group and as a fraction of the kernel time."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    r = b.issue_roofline({"SQ_INSTS_VALU": 1024 * 2.4e6 / 4, "SQ_INSTS_SALU": 100.0,
+                          "SQ_INSTS_VMEM_RD": 10.0}, kern_ms=2.0, groups=10)
+    assert r["bound"] == "valu-issue" and abs(r["floor_ms"] - 1.0) < 1e-9
+    assert r["frac"] == 0.5 and r["salu_per_group"] == 10.0 and r["vmem_rd_per_group"] == 1.0
+    assert b.issue_roofline({}, 1.0, 1) is None

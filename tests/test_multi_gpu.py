@@ -156,3 +156,25 @@ def test_two_ranks_gloo_equal_one_launch(gpu, cfg, total):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240, env=env)
     assert r.returncode == 0, (r.stdout.decode()[-2000:], r.stderr.decode()[-3000:])
     assert '"hist_equal": true' in r.stdout.decode()
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo():
+    """bench.py's own N > 1 path (the driver's scaling run uses it with RCCL on 8 GPUs): two
+    ranks on cuda:0 over gloo, strong sharding of one C4 batch; rank 0 prints one verified line
+    counting both shards."""
+    import json
+    total = (1 << 21) + 77
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29631",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--packets", str(total), "--no-cpu-baseline", "--no-pmc"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", EBPF_BENCH_BACKEND="gloo")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout.decode()[-2000:], r.stderr.decode()[-3000:])
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout.decode()[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["verified"] is True and d["scaling"] == "strong"
+    assert d["config"]["packets_total"] == total
+    assert d["config"]["packets_per_gpu"] == (total + 1) // 2
