@@ -133,13 +133,14 @@ def test_c5_imix_vs_oracle(gpu, env, variant):
     np.testing.assert_array_equal(want, got)
 
 
-@pytest.mark.parametrize("runmask", [True, False])
-def test_c5_truncated_packets_vs_oracle(gpu, env, runmask, monkeypatch):
-    """C5 on IMIX packets whose lengths are cut at random (kept 64-B aligned in memory): lanes of
-    one group now end inside a leaf's straight run, so the compiled code's run mask (asm_cc.cpp:
-    one extent compare per run) misses them and the per-load path must fault those past their
-    end at the right load and load directly for the others.  EBPF_CC_NORUNMASK=1 compiles the
-    per-load compares instead; both must equal the oracle."""
+@pytest.mark.parametrize("variant,runmask", [(0, True), (0, False), (2, True)])
+def test_c5_truncated_packets_vs_oracle(gpu, env, variant, runmask, monkeypatch):
+    """C5 on IMIX packets whose lengths are cut at random and stored unpadded (CSR packets at
+    any byte offset): lanes of one group now end inside a leaf's straight run, so the compiled
+    code's run mask (asm_cc.cpp: one extent compare per run) misses them and the per-load path
+    must fault those past their end at the right load and load directly for the others.
+    EBPF_CC_NORUNMASK=1 compiles the per-load compares instead; the assembly interpreter
+    (variant 2) runs the same packets through its general handlers.  All must equal the oracle."""
     from generic_ebpf_amd import native, workloads
     if not runmask:
         monkeypatch.setenv("EBPF_CC_NORUNMASK", "1")
@@ -150,9 +151,7 @@ def test_c5_truncated_packets_vs_oracle(gpu, env, runmask, monkeypatch):
     cut = g.random(n) < 0.3
     lens = sizes.astype(np.int64)
     lens[cut] = g.integers(18, lens[cut] + 1)
-    # packet i keeps its 64-B aligned start; its length is given by an offsets array over a
-    # copy in which every packet is followed by the bytes up to the next aligned start, so the
-    # CSR form needs one packet per slot: rebuild data as [pkt0 bytes][pkt1 bytes]... unpadded
+    # the kept bytes of every packet, back to back (CSR offsets, no padding)
     starts = offs[:-1].astype(np.int64)
     parts = [data[s:s + L] for s, L in zip(starts, lens)]
     new_offs = np.zeros(n + 1, dtype=np.uint64)
@@ -161,7 +160,7 @@ def test_c5_truncated_packets_vs_oracle(gpu, env, runmask, monkeypatch):
     c = goldens.Case("c5cut", lay.code, [], [], new_data, n, 0, new_offs)
     want, wf, _, _ = oracle_run(c, nthreads=8)
     assert wf.any() and (~wf.astype(bool)).any()
-    got, gf, _ = device_run(gpu, env, c, 0)
+    got, gf, _ = device_run(gpu, env, c, variant)
     np.testing.assert_array_equal(wf, gf)
     np.testing.assert_array_equal(want, got)
 
