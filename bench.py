@@ -27,6 +27,10 @@ the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them
 the general kernel (divergent, any packet size: C5) get a third pass (SQ_INSTS_VALU / _SALU /
 _VMEM_RD) for roofline.issue, the VALU-issue floor that divergence puts under such a launch.
 
+The same run also measures BASELINE config 5 (C5: the 256-insn filter over IMIX packets; --also),
+sharded the same way and verified the same way, reported under "also" — so the driver's 1/2/4/8-GPU
+runs carry the C5 line at every N too.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -81,6 +85,9 @@ def parse(argv=None):
                     help="event-time the kernel of every k-th timed step (default 10: each event pair is a GPU-side marker, C2 steps with a pair every 5th step took 14.2 us against 12.9 us with none; profiles/r02/ab_event)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every step (launches never queue)")
+    ap.add_argument("--also", default="c5",
+                    help="comma-separated further configs measured in the same run (sharded the same way) "
+                         "and reported under 'also' (default c5: BASELINE config 5, the IMIX filter); '' for none")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)
@@ -291,7 +298,7 @@ def pmc_traffic(a, w, total, layout):
     out = a.pmc_dir or tempfile.mkdtemp(prefix="ebpf_pmc_")
     child = [sys.executable, os.path.abspath(__file__), "--config", a.config, "--packets",
              str(total), "--steps", "2", "--warmup", "1", "--variant", str(a.variant),
-             "--no-cpu-baseline", "--no-pmc", "--no-verify"]
+             "--no-cpu-baseline", "--no-pmc", "--no-verify", "--also="]
     vals = {}
     # general kernels (divergent programs): also the instruction counts of the issue roofline
     passes = [("FETCH_SIZE",), ("WRITE_SIZE",)]
@@ -352,26 +359,10 @@ def issue_roofline(insts, kern_ms, groups):
                 VALU_ISSUE_CYCLES, SIMDS, CLOCK_GHZ)}
 
 
-def main():
-    a = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("EBPF_BENCH_BACKEND", "nccl")
-    if world > 1 and backend == "gloo":   # rehearsal of N > 1 with every rank on one GPU
-        local = local % max(1, torch.cuda.device_count())
-    # the rank's GPU is bound before the process group exists, so that RCCL's communicator and
-    # its barrier use this device (not a guess from the rank number)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        # nccl (= RCCL) on the node; EBPF_BENCH_BACKEND=gloo rehearses N > 1 on one GPU
-        dist.init_process_group(backend)
-    cfg = a.config
-    size = a.packets or DEFAULT_PACKETS[cfg]
+def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
+    """One configuration on this rank: build its shard, warm up, time a.steps launches (barrier
+    and max over ranks), verify the last launch.  Returns the numbers of the JSON line."""
+    size = packets or DEFAULT_PACKETS[cfg]
     if a.scaling == "strong":
         total = size
         lo, hi = shard.shard_bounds(total, rank, world)
@@ -481,6 +472,58 @@ def main():
     elif int(hist.sum()) != total:
         ok = False
         vinfo = {"verified": False, "hist_total": int(hist.sum())}
+    info = prog.info()
+    prog.destroy()
+    for m in maps:
+        m.destroy()
+    env.destroy()
+    return dict(w=w, n=n, total=total, value=value, ms_per_step=ms_per_step, kern_ms=kern_ms,
+                achieved=achieved, bytes_per_launch=bytes_per_launch, exec_name=exec_name,
+                layout=layout, translate_ms=translate_ms, build_ms=build_ms, faulted=faulted,
+                vinfo=vinfo, ok=ok, nentries=info.nentries, graph=graphs is not None,
+                samples=len(evs))
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("EBPF_BENCH_BACKEND", "nccl")
+    if world > 1 and backend == "gloo":   # rehearsal of N > 1 with every rank on one GPU
+        local = local % max(1, torch.cuda.device_count())
+    # the rank's GPU is bound before the process group exists, so that RCCL's communicator and
+    # its barrier use this device (not a guess from the rank number)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        # nccl (= RCCL) on the node; EBPF_BENCH_BACKEND=gloo rehearses N > 1 on one GPU
+        dist.init_process_group(backend)
+    R = measure(a, a.config, a.packets, torch, dist, world, rank, local, dev)
+    ok = R["ok"]
+    w, n, total, layout, kern_ms = R["w"], R["n"], R["total"], R["layout"], R["kern_ms"]
+    cfg = a.config
+    # further BASELINE configurations measured in the same run, sharded the same way (a line of
+    # their own under "also"; a failed check there is reported, it does not void the line)
+    also = {}
+    for c in [x for x in a.also.split(",") if x and x != cfg]:
+        try:
+            S = measure(a, c, 0, torch, dist, world, rank, local, dev)
+        except Exception as e:  # reported in the line; the primary measurement stands
+            also[c] = {"error": "%s: %s" % (type(e).__name__, e)}
+            continue
+        also[c] = {"value": round(S["value"], 1), "unit": "Mpkt/s", "ms_per_step": round(S["ms_per_step"], 4),
+                   "packets_total": S["total"], "packets_per_gpu": S["n"], "verified": S["vinfo"].get("verified"),
+                   "check": S["vinfo"], "exec": S["exec_name"],
+                   "kernel_layout": "staged64" if S["layout"] == 1 else "general",
+                   "roofline": {"bound": "hbm", "achieved": round(S["achieved"], 1), "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": round(S["achieved"] / PEAK_HBM_GBS, 4),
+                                "kernel_ms": round(S["kern_ms"], 4),
+                                "algorithmic_bytes_per_launch": S["bytes_per_launch"]},
+                   "desc": workloads.CONFIGS[c]["desc"]}
 
     if rank == 0:
         cpu = None
@@ -495,34 +538,31 @@ def main():
                 issue = issue_roofline(t["insts"], kern_ms, (n + 63) // 64)
         out = {
             "metric": METRIC,
-            "value": round(value, 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "value": round(R["value"], 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(R["ms_per_step"], 4), "higher_is_better": True,
             "scaling": a.scaling, "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "verified": vinfo.get("verified"),
+            "verified": R["vinfo"].get("verified"),
             "config": {"workload": cfg, "desc": workloads.CONFIGS[cfg]["desc"],
                        "packets_total": total, "packets_per_gpu": n,
                        "packet_bytes": 64 if w.offs is None else "IMIX",
                        "main_path_insns": w.lay.main_path_steps, "prog_slots": w.lay.nslots,
-                       "dprog_entries": prog.info().nentries, "variant": a.variant,
-                       "exec": exec_name, "kernel_layout": "staged64" if layout == 1 else "general",
-                       "translate_ms": round(translate_ms, 3), "build_ms": round(build_ms, 3),
+                       "dprog_entries": R["nentries"], "variant": a.variant,
+                       "exec": R["exec_name"], "kernel_layout": "staged64" if layout == 1 else "general",
+                       "translate_ms": round(R["translate_ms"], 3), "build_ms": round(R["build_ms"], 3),
                        "parallelism": "dp%d" % world,
-                       "launch": "graph" if graphs is not None else "eager",
-                       "faulted_packets": faulted},
-            "check": vinfo,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                       "launch": "graph" if R["graph"] else "eager",
+                       "faulted_packets": R["faulted"]},
+            "check": R["vinfo"],
+            "roofline": {"bound": "hbm", "achieved": round(R["achieved"], 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(R["achieved"] / PEAK_HBM_GBS, 4),
                          "traffic": traffic, "traffic_note": pmc_note,
-                         "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": len(evs),
-                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": R["samples"],
+                         "algorithmic_bytes_per_launch": R["bytes_per_launch"],
                          "issue": issue},
             "cpu_baseline": cpu,
+            "also": also,
         }
         print(json.dumps(out), flush=True)
-    prog.destroy()
-    for m in maps:
-        m.destroy()
-    env.destroy()
     if world > 1:
         dist.destroy_process_group()
     if not ok:

@@ -162,7 +162,7 @@ def test_two_ranks_gloo_equal_one_launch(gpu, cfg, total):
 def test_bench_two_ranks_gloo():
     """bench.py's own N > 1 path (the driver's scaling run uses it with RCCL on 8 GPUs): two
     ranks on cuda:0 over gloo, strong sharding of one C4 batch; rank 0 prints one verified line
-    counting both shards."""
+    counting both shards, with C5 (BASELINE config 5) measured the same way under "also"."""
     import json
     total = (1 << 21) + 77
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -178,3 +178,6 @@ def test_bench_two_ranks_gloo():
     assert d["n_gpus"] == 2 and d["verified"] is True and d["scaling"] == "strong"
     assert d["config"]["packets_total"] == total
     assert d["config"]["packets_per_gpu"] == (total + 1) // 2
+    # BASELINE config 5 in the same run, sharded the same way
+    c5 = d["also"]["c5"]
+    assert c5["verified"] is True and c5["packets_total"] == 1 << 22, c5

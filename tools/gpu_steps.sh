@@ -31,14 +31,14 @@ for st in "$@"; do
     prof:*)
       rest="${st#prof:}"; name="${rest%%:*}"; args="${rest#*:}"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o prof -- \
-        python3 bench.py --no-cpu-baseline --no-pmc --no-verify $args > "$O/prof_$name.json" 2> "$O/prof_$name.err" \
+        python3 bench.py --no-cpu-baseline --no-pmc --no-verify --also= $args > "$O/prof_$name.json" 2> "$O/prof_$name.err" \
         || { tail -5 "$O/prof_$name.err"; exit 1; }
       f=$(ls "$O"/prof_$name/*/prof_kernel_stats.csv "$O"/prof_$name/prof_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && head -4 "$f" ;;
     pmc:*)
       rest="${st#pmc:}"; name="${rest%%:*}"; rest="${rest#*:}"; ctr="${rest%%:*}"; args="${rest#*:}"
       timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --kernel-include-regex 'ebpf_(interp|jit)' \
-        --output-format csv -d "$O/pmc_$name" -o pmc -- python3 bench.py --no-cpu-baseline --no-pmc --no-verify \
+        --output-format csv -d "$O/pmc_$name" -o pmc -- python3 bench.py --no-cpu-baseline --no-pmc --no-verify --also= \
         $args > "$O/pmc_$name.json" 2> "$O/pmc_$name.err" || { tail -5 "$O/pmc_$name.err"; exit 1; } ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
