@@ -29,7 +29,10 @@ ST_POLICY = " nt" if _NT & 1 else ""
 LD_POLICY = " nt" if _NT & 2 else ""
 # explicit cache-policy strings (A/B probes of the gfx950 sc0/sc1/nt bits), "+"-separated,
 # e.g. EBPF_ASM_LDPOL=sc1+nt ("none" = no bits)
-for _v, _n in (("EBPF_ASM_STPOL", "ST_POLICY"), ("EBPF_ASM_LDPOL", "LD_POLICY")):
+# hashtable probe loads (A/B: EBPF_ASM_PROBEPOL, same form; default policy)
+PROBE_POLICY = ""
+for _v, _n in (("EBPF_ASM_STPOL", "ST_POLICY"), ("EBPF_ASM_LDPOL", "LD_POLICY"),
+               ("EBPF_ASM_PROBEPOL", "PROBE_POLICY")):
     if os.environ.get(_v):
         _p = os.environ[_v].replace("+", " ")
         globals()[_n] = "" if _p == "none" else " " + _p
@@ -851,11 +854,11 @@ def hlookup_routine():
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
           "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
-          "global_load_dwordx4 v[%d:%d], %s, off" % (R[6], R[9], sa),
+          "global_load_dwordx4 v[%d:%d], %s, off%s" % (R[6], R[9], sa, PROBE_POLICY),
           # the slot's first 8 value bytes (value offset 16 for keys of <= 8 bytes), same line:
           # lanes that meet their key here keep them in v[50:51] for the code generator's
           # forwarded value loads (asm_cc.cpp AHF_LDXHV)
-          "global_load_dwordx2 %s, %s, off offset:16" % (vp(H[4]), sa)] + probe_wait("hq") + [
+          "global_load_dwordx2 %s, %s, off offset:16%s" % (vp(H[4]), sa, PROBE_POLICY)] + probe_wait("hq") + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),           # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[7]), c),
