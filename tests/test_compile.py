@@ -204,3 +204,42 @@ def test_hash_value_loads_forwarded(native, env):
             assert loads(out) == loads(out_off) - 1
     finally:
         m.destroy()
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+def test_run_mask_code_shape(native, env):
+    """General layout (C5): every straight run of hoisted packet loads starts with ONE extent
+    compare into s[76:77] and issues its loads under it with no per-load compare; each use tests
+    s[76:77] with a scalar AND-NOT before any vector compare.  EBPF_CC_NORUNMASK=1 restores the
+    per-load compares (two per hoisted load), so that build has more VALU compares."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c5()
+
+    def decode(off):
+        if off:
+            os.environ["EBPF_CC_NORUNMASK"] = "1"
+        try:
+            p = native.Prog(env, lay.code)
+            try:
+                dc = p.device_code(0)
+            finally:
+                p.destroy()
+        finally:
+            os.environ.pop("EBPF_CC_NORUNMASK", None)
+        out, err = _decode(dc)
+        assert "invalid" not in err.lower(), err[:500]
+        return [ln.strip() for ln in out.splitlines() if ln.strip()]
+
+    on, off = decode(False), decode(True)
+    assert "s_mov_b64 s[76:77], vcc" in on and "s_mov_b64 s[76:77], vcc" not in off
+    assert "s_andn2_b64 s[48:49], exec, s[76:77]" in on
+    # the run head: compare, mask, one saveexec, the hoisted loads back to back, restore
+    k = on.index("s_mov_b64 s[76:77], vcc")
+    assert on[k - 1].startswith("v_cmp_le_u32_e32 vcc,") and on[k + 1] == "s_and_saveexec_b64 s[60:61], vcc"
+    j = k + 2
+    while on[j].startswith("global_load_"):
+        j += 1
+    assert j - (k + 2) >= 2 and on[j] == "s_mov_b64 exec, s[60:61]", on[k:j + 1]
+    cmps_on = sum(ln.startswith("v_cmp_") for ln in on)
+    cmps_off = sum(ln.startswith("v_cmp_") for ln in off)
+    assert cmps_on < cmps_off, (cmps_on, cmps_off)
