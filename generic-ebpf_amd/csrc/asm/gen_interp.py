@@ -244,8 +244,10 @@ def sp(i):
 
 
 def dispatch(next_reg=12):
-    return ["s_mov_b32 s6, s%d" % next_reg,
-            "s_load_dwordx8 s[8:15], s[%d:%d], s6" % (S_PROG, S_PROG + 1),
+    """Fetch the entry at byte offset s[next_reg] (inside the entry being replaced: the offset
+    is read when the load issues, and the code object is xnack-, so no replay can re-read it)
+    and jump to its handler."""
+    return ["s_load_dwordx8 s[8:15], s[%d:%d], s%d" % (S_PROG, S_PROG + 1, next_reg),
             "s_waitcnt lgkmcnt(0)",
             "s_setpc_b64 s[8:9]"]
 
