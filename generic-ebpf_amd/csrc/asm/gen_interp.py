@@ -414,12 +414,13 @@ def h_cond(c, d, sr, imm):
         out.append("v_cmp_ne_u64_e64 vcc, %s, 0" % vp(H[0]))
     else:
         out.append("v_cmp_%s_e64 vcc, %s, %s" % (CMP[c], pair(d), srcop))
+    # (no lane taken, the usual uniform case, costs two scalar instructions: the AND's SCC says
+    # whether any lane takes the branch)
     out += ["@CMPEND",
             "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+            "s_cbranch_scc0 .Lnt_{uid}",
             "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
             "s_cbranch_scc1 .Ltk_{uid}",
-            "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
-            "s_cbranch_scc1 .Lnt_{uid}",
             ] + goto(".Lr_diverge") + [
             ".Ltk_{uid}:"] + dispatch(13) + [".Lnt_{uid}:"] + dispatch(12)
     return out, True   # (body, has own dispatch)
