@@ -1,0 +1,171 @@
+// pcap.cpp — a packet capture as a batch (the path starts in host memory,
+// "a NIC ring or pcap buffer").  The classic libpcap file format: a 24-byte global header
+// (magic, version, thiszone, sigfigs, snaplen, linktype) and per packet a 16-byte record header
+// (ts_sec, ts_usec or ts_nsec, incl_len, orig_len) followed by incl_len captured bytes.  The
+// magic tells the byte order and the timestamp unit: 0xa1b2c3d4 (microseconds) or 0xa1b23c4d
+// (nanoseconds), as written or byte-swapped.
+//
+// The records' captured bytes are gathered into one buffer in offsets form (ebpf_pkt_batch:
+// packet i = data[offsets[i], offsets[i+1])), which ebpf_prog_run_batch consumes directly; the
+// program sees each packet's captured bytes, as a caller that hands a record's buffer to the
+// reference's ebpf_prog_run would.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+#include "internal.h"
+
+namespace {
+
+// buffers this file handed out: pinned (hipHostMalloc) or not (malloc)
+std::mutex g_lock;
+std::unordered_map<const void *, bool> g_bufs;
+
+uint32_t
+rd32(const uint8_t *p, bool swap)
+{
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return swap ? __builtin_bswap32(v) : v;
+}
+
+void *
+alloc(size_t bytes, bool pinned)
+{
+	if (bytes == 0)
+		bytes = 1;
+	if (pinned) {
+		int n = 0;
+		void *p = nullptr;
+		if (hipGetDeviceCount(&n) == hipSuccess && n > 0 &&
+		    hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
+			std::lock_guard<std::mutex> g(g_lock);
+			g_bufs[p] = true;
+			return p;
+		}
+		(void)hipGetLastError(); // no GPU: pageable memory instead
+	}
+	void *p = malloc(bytes);
+	if (p) {
+		std::lock_guard<std::mutex> g(g_lock);
+		g_bufs[p] = false;
+	}
+	return p;
+}
+
+void
+release(const void *p)
+{
+	if (!p)
+		return;
+	bool pinned;
+	{
+		std::lock_guard<std::mutex> g(g_lock);
+		auto it = g_bufs.find(p);
+		if (it == g_bufs.end())
+			return; // not ours
+		pinned = it->second;
+		g_bufs.erase(it);
+	}
+	if (pinned)
+		(void)hipHostFree(const_cast<void *>(p));
+	else
+		free(const_cast<void *>(p));
+}
+
+} // namespace
+
+EBPF_EXPORT int
+ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
+		struct ebpf_pcap_info *info)
+{
+	if (!capture || !batch || len < 24) {
+		set_last_error("pcap: NULL argument or shorter than the 24-byte global header");
+		return EINVAL;
+	}
+	const uint8_t *b = static_cast<const uint8_t *>(capture);
+	uint32_t magic;
+	memcpy(&magic, b, 4);
+	bool swap, nsec;
+	switch (magic) {
+	case 0xa1b2c3d4u: swap = false; nsec = false; break;
+	case 0xa1b23c4du: swap = false; nsec = true; break;
+	case 0xd4c3b2a1u: swap = true; nsec = false; break;
+	case 0x4d3cb2a1u: swap = true; nsec = true; break;
+	default:
+		set_last_error("pcap: unknown magic (not a classic libpcap capture)");
+		return EINVAL;
+	}
+	const uint32_t snaplen = rd32(b + 16, swap), linktype = rd32(b + 20, swap);
+	// pass 1: count the records and their bytes, validating every header
+	uint64_t count = 0, bytes = 0, truncated = 0;
+	size_t at = 24;
+	while (at < len) {
+		if (len - at < 16) {
+			set_last_error("pcap: truncated record header at byte " + std::to_string(at));
+			return EINVAL;
+		}
+		const uint32_t incl = rd32(b + at + 8, swap), orig = rd32(b + at + 12, swap);
+		if (incl > len - at - 16) {
+			set_last_error("pcap: record at byte " + std::to_string(at) + " runs past the end");
+			return EINVAL;
+		}
+		if (snaplen && incl > snaplen) {
+			set_last_error("pcap: record at byte " + std::to_string(at) + " longer than snaplen");
+			return EINVAL;
+		}
+		truncated += incl < orig;
+		count++;
+		bytes += incl;
+		at += 16 + (size_t)incl;
+	}
+	// pass 2: gather the captured bytes
+	uint8_t *data = static_cast<uint8_t *>(alloc((size_t)bytes, pinned != 0));
+	uint64_t *offs = static_cast<uint64_t *>(alloc((size_t)(count + 1) * sizeof(uint64_t), false));
+	if (!data || !offs) {
+		release(data);
+		release(offs);
+		return ENOMEM;
+	}
+	uint64_t o = 0, i = 0;
+	at = 24;
+	while (at < len) {
+		const uint32_t incl = rd32(b + at + 8, swap);
+		offs[i++] = o;
+		memcpy(data + o, b + at + 16, incl);
+		o += incl;
+		at += 16 + (size_t)incl;
+	}
+	offs[count] = o;
+	memset(batch, 0, sizeof(*batch));
+	batch->data = data;
+	batch->offsets = offs;
+	batch->count = count;
+	if (info) {
+		info->linktype = linktype;
+		info->snaplen = snaplen;
+		info->nanosecond = nsec ? 1u : 0u;
+		info->byte_swapped = swap ? 1u : 0u;
+		info->truncated = truncated;
+		info->bytes = bytes;
+	}
+	return 0;
+}
+
+EBPF_EXPORT void
+ebpf_pcap_batch_free(struct ebpf_pkt_batch *batch)
+{
+	if (!batch)
+		return;
+	release(batch->data);
+	release(batch->offsets);
+	batch->data = nullptr;
+	batch->offsets = nullptr;
+	batch->count = 0;
+}

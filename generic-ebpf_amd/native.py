@@ -80,6 +80,12 @@ class DexecInfo(ctypes.Structure):
 EXEC_NAMES = {0: "compiled", 1: "hip", 2: "interpreter"}
 
 
+class PcapInfo(ctypes.Structure):
+    _fields_ = [("linktype", ctypes.c_uint32), ("snaplen", ctypes.c_uint32),
+                ("nanosecond", ctypes.c_uint32), ("byte_swapped", ctypes.c_uint32),
+                ("truncated", ctypes.c_uint64), ("bytes", ctypes.c_uint64)]
+
+
 class DprogInfo(ctypes.Structure):
     _fields_ = [("nslots", ctypes.c_uint32), ("nentries", ctypes.c_uint32),
                 ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
@@ -113,6 +119,8 @@ FUNCS = {
     "ebpf_prog_device_exec": (_I, [_VP, _I, _VP]),
     "ebpf_prog_device_code": (_I, [_VP, _I, _VP, ctypes.POINTER(ctypes.c_size_t)]),
     "ebpf_prog_set_semantics": (_I, [_VP, _I]),
+    "ebpf_pcap_batch": (_I, [_VP, ctypes.c_size_t, _I, _VP, _VP]),
+    "ebpf_pcap_batch_free": (None, [_VP]),
 }
 DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_hashtable",
                 "eht_map_lookup_elem", "eht_map_update_elem", "eht_map_delete_elem"]
@@ -121,6 +129,44 @@ _lib = None
 
 
 BATCH_HIST_OVERWRITE = 0x1  # include/ebpf_gpu.h EBPF_BATCH_HIST_OVERWRITE
+
+
+class PcapBatch:
+    """ebpf_pcap_batch: a classic pcap capture (bytes) as a library-allocated batch in offsets
+    form.  ``batch`` is the ebpf_pkt_batch to hand to the run functions; ``data()`` /
+    ``offsets()`` copy it out; ``free()`` (or the context manager) releases it."""
+
+    def __init__(self, capture, pinned=False):
+        buf = np.frombuffer(bytes(capture), dtype=np.uint8)
+        self.batch = PktBatch()
+        self.info = PcapInfo()
+        _check(lib().ebpf_pcap_batch(buf.ctypes.data if len(buf) else None, len(buf),
+                                     1 if pinned else 0, ctypes.byref(self.batch),
+                                     ctypes.byref(self.info)), "ebpf_pcap_batch")
+
+    @property
+    def count(self):
+        return int(self.batch.count)
+
+    def offsets(self):
+        return np.ctypeslib.as_array((ctypes.c_uint64 * (self.count + 1)).from_address(
+            self.batch.offsets)).copy()
+
+    def data(self):
+        n = int(self.info.bytes)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint8)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(self.batch.data)).copy()
+
+    def free(self):
+        if self.batch.data is not None or self.batch.offsets is not None:
+            lib().ebpf_pcap_batch_free(ctypes.byref(self.batch))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
 
 
 def lib():
@@ -333,6 +379,17 @@ class Prog:
                      stride, 0)
         st = BatchStats()
         _check(lib().ebpf_prog_run_batch(self.ptr, ctypes.byref(b), ret.ctypes.data,
+                                         None if faults is None else faults.ctypes.data,
+                                         ctypes.byref(st)), "ebpf_prog_run_batch")
+        return ret, faults, st
+
+    def run_pcap(self, pcap, want_faults=True):
+        """ebpf_prog_run_batch over a PcapBatch as the library built it (its own buffers, pinned
+        or not).  Returns (ret, faults, stats) like run_batch."""
+        ret = np.zeros(pcap.count, dtype=np.uint64)
+        faults = np.zeros(pcap.count, dtype=np.uint8) if want_faults else None
+        st = BatchStats()
+        _check(lib().ebpf_prog_run_batch(self.ptr, ctypes.byref(pcap.batch), ret.ctypes.data,
                                          None if faults is None else faults.ctypes.data,
                                          ctypes.byref(st)), "ebpf_prog_run_batch")
         return ret, faults, st

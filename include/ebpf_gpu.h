@@ -96,6 +96,26 @@ struct ebpf_batch_stats {
 	double total_ms;      /* wall time including H2D/D2H */
 };
 
+/* A packet capture as a batch (the path starts in host memory: a NIC ring or a pcap buffer).
+ * `capture` holds a classic libpcap file (magic 0xa1b2c3d4 / 0xa1b23c4d, either byte order):
+ * packet i of the batch is record i's captured bytes, in offsets form, ready for
+ * ebpf_prog_run_batch.  The library allocates batch->data (pinned host memory when `pinned` and
+ * a GPU is present, else pageable) and batch->offsets; release both with ebpf_pcap_batch_free.
+ * The capture buffer stays the caller's and is not referenced afterwards.
+ * Returns 0, EINVAL (not a classic pcap capture, a truncated record, or a record longer than
+ * the snaplen; ebpf_gpu_last_error says which), ENOMEM.  Host only: no GPU needed. */
+struct ebpf_pcap_info {
+	uint32_t linktype;     /* the capture's link-layer type (1 = Ethernet) */
+	uint32_t snaplen;
+	uint32_t nanosecond;   /* 1: nanosecond timestamps (magic 0xa1b23c4d) */
+	uint32_t byte_swapped; /* 1: written in the other byte order */
+	uint64_t truncated;    /* records whose captured length is below the original length */
+	uint64_t bytes;        /* captured bytes of all records (batch->offsets[count]) */
+};
+int ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
+		    struct ebpf_pcap_info *info);
+void ebpf_pcap_batch_free(struct ebpf_pkt_batch *batch);
+
 /* Number of visible GPUs (0 on a host without one). Never fails. */
 int ebpf_gpu_device_count(void);
 
