@@ -15,9 +15,12 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "internal.h"
 
@@ -138,11 +141,34 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 	while (at < len) {
 		const uint32_t incl = rd32(b + at + 8, swap);
 		offs[i++] = o;
-		memcpy(data + o, b + at + 16, incl);
 		o += incl;
 		at += 16 + (size_t)incl;
 	}
 	offs[count] = o;
+	// record i's bytes start at 24 + 16 (i + 1) + offs[i] in the capture: the copies are
+	// independent, so large captures are gathered by several threads (contiguous packet ranges)
+	auto gather = [&](uint64_t lo, uint64_t hi) {
+		for (uint64_t k = lo; k < hi; k++)
+			memcpy(data + offs[k], b + 24 + 16 * (k + 1) + offs[k], (size_t)(offs[k + 1] - offs[k]));
+	};
+	unsigned nt = std::thread::hardware_concurrency();
+	nt = std::max(1u, std::min(nt, 16u));
+	if (bytes < (16u << 20) || count < 4096)
+		nt = 1;
+	if (nt == 1) {
+		gather(0, count);
+	} else {
+		std::vector<std::thread> th;
+		unsigned t = 0;
+		try {
+			for (; t < nt; t++)
+				th.emplace_back(gather, count * t / nt, count * (t + 1) / nt);
+		} catch (...) { // no thread to be had: this one copies the ranges not started
+			gather(count * t / nt, count);
+		}
+		for (std::thread &x : th)
+			x.join();
+	}
 	memset(batch, 0, sizeof(*batch));
 	batch->data = data;
 	batch->offsets = offs;

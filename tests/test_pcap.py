@@ -53,6 +53,23 @@ def test_pcap_batch_truncated_records_and_empty(native):
         assert b.count == 0 and b.offsets().tolist() == [0]
 
 
+def test_pcap_batch_large_capture_threaded(native):
+    """A capture above 16 MB is gathered by several threads (contiguous packet ranges): the
+    batch must be byte-identical to the records' concatenation."""
+    g = np.random.default_rng(4)
+    n = 150000
+    lens = g.integers(0, 240, n)
+    blob = g.integers(0, 256, int(lens.sum()), dtype=np.uint8).tobytes()
+    ends = np.cumsum(lens)
+    pk = [blob[e - l:e] for e, l in zip(ends, lens)]
+    cap = make_pcap(pk)
+    assert len(cap) > (16 << 20)
+    with native.PcapBatch(cap) as b:
+        assert b.count == n
+        assert np.array_equal(b.offsets(), np.concatenate([[0], ends]).astype(np.uint64))
+        assert b.data().tobytes() == blob
+
+
 @pytest.mark.parametrize("bad", ["magic", "short_header", "record_header", "record_data",
                                  "snaplen", "empty"])
 def test_pcap_batch_rejects(native, bad):
