@@ -130,7 +130,7 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 	}
 	// pass 2: gather the captured bytes
 	uint8_t *data = static_cast<uint8_t *>(alloc((size_t)bytes, pinned != 0));
-	uint64_t *offs = static_cast<uint64_t *>(alloc((size_t)(count + 1) * sizeof(uint64_t), false));
+	uint64_t *offs = static_cast<uint64_t *>(alloc((size_t)(count + 1) * sizeof(uint64_t), pinned != 0));
 	if (!data || !offs) {
 		release(data);
 		release(offs);

@@ -99,8 +99,8 @@ struct ebpf_batch_stats {
 /* A packet capture as a batch (the path starts in host memory: a NIC ring or a pcap buffer).
  * `capture` holds a classic libpcap file (magic 0xa1b2c3d4 / 0xa1b23c4d, either byte order):
  * packet i of the batch is record i's captured bytes, in offsets form, ready for
- * ebpf_prog_run_batch.  The library allocates batch->data (pinned host memory when `pinned` and
- * a GPU is present, else pageable) and batch->offsets; release both with ebpf_pcap_batch_free.
+ * ebpf_prog_run_batch.  The library allocates batch->data and batch->offsets (pinned host memory
+ * when `pinned` and a GPU is present, else pageable); release both with ebpf_pcap_batch_free.
  * The capture buffer stays the caller's and is not referenced afterwards.
  * Returns 0, EINVAL (not a classic pcap capture, a truncated record, or a record longer than
  * the snaplen; ebpf_gpu_last_error says which), ENOMEM.  Host only: no GPU needed. */
