@@ -806,6 +806,12 @@ ebpf_gpu_set_device(int device)
 	return 0;
 }
 
+int
+current_device()
+{
+	return t_dev;
+}
+
 EBPF_EXPORT int
 ebpf_gpu_time_next_launch(void *start_event, void *stop_event)
 {

@@ -194,6 +194,8 @@ int translate_program(struct ebpf_prog *ep, dprog_host &out);
 
 // gpu_runtime.cpp
 void set_last_error(const std::string &msg);
+// the calling thread's device for the host-buffer entry points (ebpf_gpu_set_device)
+int current_device();
 // Copy a device batch's map writes back into the host copy (no-op unless em->dev_dirty).
 void map_pull_device_writes(struct ebpf_map *em);
 // A batch on `device` wrote the map (its writes land on `stream`, a hipStream_t).

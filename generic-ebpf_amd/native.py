@@ -121,6 +121,8 @@ FUNCS = {
     "ebpf_prog_set_semantics": (_I, [_VP, _I]),
     "ebpf_pcap_batch": (_I, [_VP, ctypes.c_size_t, _I, _VP, _VP]),
     "ebpf_pcap_batch_free": (None, [_VP]),
+    "ebpf_prog_run_batch_async": (_I, [_VP, _VP, _VP, _VP, ctypes.POINTER(_VP)]),
+    "ebpf_batch_wait": (_I, [_VP, _VP]),
 }
 DATA_SYMBOLS = ["emt_array", "emt_percpu_array", "emt_hashtable", "emt_percpu_hashtable",
                 "eht_map_lookup_elem", "eht_map_update_elem", "eht_map_delete_elem"]
@@ -129,6 +131,23 @@ _lib = None
 
 
 BATCH_HIST_OVERWRITE = 0x1  # include/ebpf_gpu.h EBPF_BATCH_HIST_OVERWRITE
+
+
+class _AsyncJob:
+    """An ebpf_prog_run_batch_async job and the buffers it writes (see Prog.run_batch_async)."""
+
+    def __init__(self, data, count, offsets, want_faults):
+        self.data = data
+        self.offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.ret = np.zeros(count, dtype=np.uint64)
+        self.faults = np.zeros(count, dtype=np.uint8) if want_faults else None
+        self.handle = None
+
+    def wait(self):
+        st = BatchStats()
+        h, self.handle = self.handle, None
+        _check(lib().ebpf_batch_wait(h, ctypes.byref(st)), "ebpf_batch_wait")
+        return self.ret, self.faults, st
 
 
 class PcapBatch:
@@ -382,6 +401,21 @@ class Prog:
                                          None if faults is None else faults.ctypes.data,
                                          ctypes.byref(st)), "ebpf_prog_run_batch")
         return ret, faults, st
+
+    def run_batch_async(self, data, count, stride=0, offsets=None, want_faults=True):
+        """ebpf_prog_run_batch_async: returns a job; job.wait() -> (ret, faults, stats) as
+        run_batch.  ``data`` (and ``offsets``) must stay alive until the wait (the job keeps
+        references)."""
+        assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
+        job = _AsyncJob(data, count, offsets, want_faults)
+        b = PktBatch(data.ctypes.data, None if job.offs is None else job.offs.ctypes.data, count,
+                     stride, 0)
+        h = ctypes.c_void_p()
+        _check(lib().ebpf_prog_run_batch_async(self.ptr, ctypes.byref(b), job.ret.ctypes.data,
+                                               None if job.faults is None else job.faults.ctypes.data,
+                                               ctypes.byref(h)), "ebpf_prog_run_batch_async")
+        job.handle = h
+        return job
 
     def run_pcap(self, pcap, want_faults=True):
         """ebpf_prog_run_batch over a PcapBatch as the library built it (its own buffers, pinned

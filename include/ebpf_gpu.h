@@ -137,6 +137,17 @@ int ebpf_prog_prepare_device(struct ebpf_prog *ep, int device);
 int ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
 			uint64_t *ret, uint8_t *faults, struct ebpf_batch_stats *stats);
 
+/* ebpf_prog_run_batch without blocking the caller: the job is queued on a worker bound to the
+ * calling thread's current device and returns at once, so a NIC-ring or capture consumer can
+ * fill its next segment meanwhile; ebpf_batch_wait blocks until ret/faults hold the results,
+ * returns the batch's error code (ebpf_prog_run_batch's) and releases the job.  The batch's
+ * buffers, ret and faults must stay valid until the wait; several jobs may be in flight.
+ * Returns 0, EINVAL (NULL argument), ENODEV (no GPU), ENOMEM, EAGAIN (no thread). */
+struct ebpf_batch_job;
+int ebpf_prog_run_batch_async(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
+			      uint64_t *ret, uint8_t *faults, struct ebpf_batch_job **job);
+int ebpf_batch_wait(struct ebpf_batch_job *job, struct ebpf_batch_stats *stats);
+
 /* Device-resident batch: every pointer (batch->data, batch->offsets, ret_dev, faults_dev,
  * hist_dev) is device memory on `device`.  Enqueued on `stream` (hipStream_t, NULL = default
  * stream) and returns without synchronising.  faults_dev / hist_dev may be NULL; hist_dev is
