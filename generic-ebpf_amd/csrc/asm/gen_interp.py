@@ -135,6 +135,8 @@ assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with regrouping (S_DEFER..) and
 # general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
 # hoist plan); 16 cost the general kernels 8 -> 6 waves per SIMD
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
+# A/B: XCD-major logical workgroup order (common_group_code)
+XCD_MAJOR = os.environ.get("EBPF_ASM_XCD") == "1"
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -1686,7 +1688,24 @@ def common_group_code():
     # groups of 64 packets: group = workgroup*4 + wave, stride = total waves
     L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
           "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
-          "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
+          ] + ([
+          # (A/B, EBPF_ASM_XCD=1) XCD-major workgroup order: workgroups go to the 8 XCDs round
+          # robin, so logical workgroup (wg % 8) * (nwg / 8) + wg / 8 gives each XCD one
+          # contiguous share of the batch (when nwg is a multiple of 8)
+          "s_load_dword %s, s[0:1], 0x7c" % s(S_T1),
+          "s_waitcnt lgkmcnt(0)",
+          "s_mov_b32 %s, s2" % s(S_GROUP),
+          "s_and_b32 %s, %s, 7" % (s(S_T2), s(S_T1)),
+          "s_cmp_eq_u32 %s, 0" % s(S_T2),
+          "s_cbranch_scc0 .Lxcd_done",
+          "s_lshr_b32 %s, %s, 3" % (s(S_T1), s(S_T1)),
+          "s_and_b32 %s, s2, 7" % s(S_T2),
+          "s_mul_i32 %s, %s, %s" % (s(S_T2), s(S_T2), s(S_T1)),
+          "s_lshr_b32 %s, s2, 3" % s(S_GROUP),
+          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_T2)),
+          ".Lxcd_done:",
+          "s_lshl_b32 %s, %s, 2" % (s(S_GROUP), s(S_GROUP))] if XCD_MAJOR else [
+          "s_lshl_b32 %s, s2, 2" % s(S_GROUP)]) + [
           "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
           # K' = superblock size of this launch (total_waves bits 28..29 = log2 K')
           "s_lshr_b32 %s, %s, 28" % (s(S_T1), s(S_GSTRIDE)),
