@@ -140,8 +140,9 @@ int ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch
 /* ebpf_prog_run_batch without blocking the caller: the job is queued on a worker bound to the
  * calling thread's current device and returns at once, so a NIC-ring or capture consumer can
  * fill its next segment meanwhile; ebpf_batch_wait blocks until ret/faults hold the results,
- * returns the batch's error code (ebpf_prog_run_batch's) and releases the job.  The batch's
- * buffers, ret and faults must stay valid until the wait; several jobs may be in flight.
+ * returns the batch's error code (ebpf_prog_run_batch's) and releases the job (wait once per
+ * job).  The program, the batch's buffers, ret and faults must stay valid until the wait;
+ * several jobs may be in flight.
  * Returns 0, EINVAL (NULL argument), ENODEV (no GPU), ENOMEM, EAGAIN (no thread). */
 struct ebpf_batch_job;
 int ebpf_prog_run_batch_async(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
