@@ -108,3 +108,27 @@ def test_consumer_program_batch_gpu(tmp_path):
     n = (1 << 20) + 13
     code, got = run_consumer(exe, "batch", n, tmp_path)
     check(code, got, n)
+
+
+def _build_pcap_consumer(tmp_path):
+    r, exe = _cc(["-I", INC, os.path.join(ROOT, "tests", "c", "pcap_async_consumer.c"),
+                  "-L", LIBDIR, "-Wl,-rpath," + LIBDIR, "-lebpf"], tmp_path, "pcap_async")
+    assert r.returncode == 0, r.stderr.decode()
+    return exe
+
+
+def test_pcap_consumer_c_cpu(tmp_path):
+    """include/ebpf_gpu.h's pcap entry point from C: a capture built in memory becomes a batch
+    whose offsets and bytes are the records'."""
+    exe = _build_pcap_consumer(tmp_path)
+    r = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode == 0 and r.stdout.decode().strip() == "ok", (r.stdout, r.stderr)
+
+
+@pytest.mark.gpu
+def test_pcap_async_consumer_c_gpu(tmp_path):
+    """The same C consumer runs a program over the capture with ebpf_prog_run_batch_async /
+    ebpf_batch_wait and checks every verdict and MEM fault."""
+    exe = _build_pcap_consumer(tmp_path)
+    r = subprocess.run([exe, "gpu"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode == 0 and r.stdout.decode().strip() == "ok", (r.stdout, r.stderr)
