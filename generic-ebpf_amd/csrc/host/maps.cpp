@@ -554,8 +554,10 @@ map_device_layout_of(const struct ebpf_map *em)
 		lg++;
 	}
 	// at most a quarter full: linear probing then ends within a slot or two almost always
-	// (an unsuccessful search probes (1 + 1/(1-a)^2)/2 = 1.4 slots on average at a = 1/4)
-	uint64_t slots = 16, per = 4;
+	// (an unsuccessful search probes (1 + 1/(1-a)^2)/2 = 1.4 slots on average at a = 1/4);
+	// an eighth full where the table stays within 1 GiB of HBM (C4H, 1M entries: 2% faster,
+	// profiles/r02/v2occ/hash_slots_c4h.txt)
+	uint64_t slots = 16, per = (uint64_t)em->max_entries * 8 * stride <= (1ull << 30) ? 8 : 4;
 	if (const char *f = getenv("EBPF_HASH_SLOTS_PER_ENTRY")) // (A/B: table size vs probe length)
 		per = std::max<uint64_t>(2, strtoull(f, nullptr, 0));
 	while (slots < per * em->max_entries)
