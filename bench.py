@@ -20,8 +20,9 @@ tiles; any mismatch prints the line with "verified": false and exits 1.
 
 roofline.kernel_ms is the engine's kernel alone: HIP events that the library records on the
 launch stream just before and after that kernel (ebpf_gpu_time_next_launch), so it compares
-with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 10th timed step
-carries the events (--time-every).  roofline.traffic is measured by THIS run: two child passes
+with the kernel's average in a rocprofv3 --kernel-trace --stats summary.  Every 2nd timed step
+carries the events (--time-every; 10 samples in the driver's 20-step run) and kernel_ms is their
+MEDIAN (the mean, min and max are in the line too; a median above ms_per_step is flagged).  roofline.traffic is measured by THIS run: two child passes
 of this script under rocprofv3 --pmc (FETCH_SIZE, then WRITE_SIZE) on the same workload, after
 the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).  Programs on
 the general kernel (divergent, any packet size: C5) get a third pass (SQ_INSTS_VALU / _SALU /
@@ -81,8 +82,8 @@ def parse(argv=None):
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle check (PMC child passes)")
     ap.add_argument("--no-pmc", action="store_true", help="no rocprofv3 --pmc passes for roofline.traffic")
     ap.add_argument("--pmc-dir", default="", help="where the PMC passes write (default: a temp dir)")
-    ap.add_argument("--time-every", type=int, default=10,
-                    help="event-time the kernel of every k-th timed step (default 10: each event pair is a GPU-side marker, C2 steps with a pair every 5th step took 14.2 us against 12.9 us with none; profiles/r02/ab_event)")
+    ap.add_argument("--time-every", type=int, default=2,
+                    help="event-time the kernel of every k-th timed step (default 2: the events come from the kernel's own dispatch packet, ebpf_gpu_time_next_launch, so a timed step costs no extra GPU-side marker)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every step (launches never queue)")
     ap.add_argument("--also", default="c5",
@@ -286,7 +287,7 @@ def cpu_baseline(w, budget_s):
                           mp, thr, mel, sp, core, sel)}
 
 
-def pmc_traffic(a, w, total, layout):
+def pmc_traffic(a, w, total, layout, cfg=None):
     """HBM bytes per launch of the engine's kernel, from two rocprofv3 --pmc child passes of
     this script on the same workload (each counter group in a run of its own, kernel trace
     only besides --pmc: MI355X_MICROARCH.md, HBM/rocprofv3).  FETCH_SIZE/WRITE_SIZE are KiB;
@@ -295,8 +296,9 @@ def pmc_traffic(a, w, total, layout):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not found"
+    cfg = cfg or a.config
     out = a.pmc_dir or tempfile.mkdtemp(prefix="ebpf_pmc_")
-    child = [sys.executable, os.path.abspath(__file__), "--config", a.config, "--packets",
+    child = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--packets",
              str(total), "--steps", "2", "--warmup", "1", "--variant", str(a.variant),
              "--no-cpu-baseline", "--no-pmc", "--no-verify", "--also="]
     vals = {}
@@ -306,7 +308,7 @@ def pmc_traffic(a, w, total, layout):
         passes.append(ISSUE_COUNTERS)
     for group in passes:
         counter = group[0]
-        d = os.path.join(out, "pmc_%s_%s" % (a.config, counter))
+        d = os.path.join(out, "pmc_%s_%s" % (cfg, counter))
         os.makedirs(d, exist_ok=True)
         cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc"] + list(group) + ["--kernel-trace",
                "--kernel-include-regex", "ebpf_(interp|jit)", "--output-format", "csv",
@@ -453,7 +455,8 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    kern_samples = [s.elapsed_time(e) for s, e in evs]
+    kern_ms = float(np.median(kern_samples))
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -481,7 +484,17 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
                 achieved=achieved, bytes_per_launch=bytes_per_launch, exec_name=exec_name,
                 layout=layout, translate_ms=translate_ms, build_ms=build_ms, faulted=faulted,
                 vinfo=vinfo, ok=ok, nentries=info.nentries, graph=graphs is not None,
-                samples=len(evs))
+                samples=len(evs), kern_stats=kernel_stats(kern_samples, ms_per_step))
+
+
+def kernel_stats(samples, ms_per_step):
+    """The event-timed kernel durations of this rank: how many, their mean / min / max, and
+    whether the median exceeds the step (it cannot, for back-to-back launches on one stream,
+    unless the sample is unrepresentative)."""
+    med = float(np.median(samples))
+    return {"n": len(samples), "median": round(med, 4), "mean": round(float(np.mean(samples)), 4),
+            "min": round(float(np.min(samples)), 4), "max": round(float(np.max(samples)), 4),
+            "median_exceeds_step": bool(med > ms_per_step)}
 
 
 def main():
@@ -515,14 +528,22 @@ def main():
         except Exception as e:  # reported in the line; the primary measurement stands
             also[c] = {"error": "%s: %s" % (type(e).__name__, e)}
             continue
+        if rank == 0 and not a.no_pmc and world == 1:  # the same PMC passes as the primary line
+            t, err = pmc_traffic(a, S["w"], S["total"], S["layout"], c)
+            S["traffic"], S["traffic_note"] = (t["bytes"], t["note"]) if t else (None, err)
+            S["issue"] = (issue_roofline(t["insts"], S["kern_ms"], (S["n"] + 63) // 64)
+                          if t and t["insts"] else None)
         also[c] = {"value": round(S["value"], 1), "unit": "Mpkt/s", "ms_per_step": round(S["ms_per_step"], 4),
                    "packets_total": S["total"], "packets_per_gpu": S["n"], "verified": S["vinfo"].get("verified"),
                    "check": S["vinfo"], "exec": S["exec_name"],
                    "kernel_layout": "staged64" if S["layout"] == 1 else "general",
                    "roofline": {"bound": "hbm", "achieved": round(S["achieved"], 1), "peak": PEAK_HBM_GBS,
                                 "unit": "GB/s", "frac": round(S["achieved"] / PEAK_HBM_GBS, 4),
-                                "kernel_ms": round(S["kern_ms"], 4),
-                                "algorithmic_bytes_per_launch": S["bytes_per_launch"]},
+                                "kernel_ms": round(S["kern_ms"], 4), "kernel_ms_stats": S["kern_stats"],
+                                "traffic": S.get("traffic"),
+                                "traffic_note": S.get("traffic_note", "not collected (N > 1 or --no-pmc)"),
+                                "algorithmic_bytes_per_launch": S["bytes_per_launch"],
+                                "issue": S.get("issue")},
                    "desc": workloads.CONFIGS[c]["desc"]}
 
     if rank == 0:
@@ -557,6 +578,7 @@ def main():
                          "unit": "GB/s", "frac": round(R["achieved"] / PEAK_HBM_GBS, 4),
                          "traffic": traffic, "traffic_note": pmc_note,
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": R["samples"],
+                         "kernel_ms_stats": R["kern_stats"],
                          "algorithmic_bytes_per_launch": R["bytes_per_launch"],
                          "issue": issue},
             "cpu_baseline": cpu,

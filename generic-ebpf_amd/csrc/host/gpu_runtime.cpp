@@ -13,8 +13,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <functional>
 #include <thread>
 
+#include "hist_ops.h"
 #include "internal.h"
 #include "map_writes.h"
 
@@ -94,6 +96,12 @@ struct rows_slot {
 	// compiled programs with regroup points: the stream's queue buffer (any contents)
 	void *rq = nullptr;
 	size_t rq_bytes = 0;
+	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
+	// shard on the device (any contents: every launch overwrites its row), and fork/join events
+	void *mh = nullptr;
+	size_t mh_bytes = 0;
+	std::vector<hipEvent_t> ev;
+	bool per_thread = false; // hipStreamPerThread: `stream` names a different stream per thread
 };
 std::mutex g_rows_lock;
 std::vector<std::vector<rows_slot>> g_rows; // per device (capacity kRowsMax: slots never move)
@@ -109,7 +117,12 @@ slot_for(int device, hipStream_t stream, rows_slot **out)
 	static const get_id_fn get_id =
 	    reinterpret_cast<get_id_fn>(dlsym(RTLD_DEFAULT, "hipStreamGetId"));
 	unsigned long long sid = (unsigned long long)(uintptr_t)stream;
-	if (get_id && get_id(stream, &sid) != hipSuccess)
+	// hipStreamPerThread is one handle for one stream PER THREAD: two threads launching on it
+	// run unordered, so each thread's stream gets its own slot (keyed by the thread)
+	const bool per_thread = stream == hipStreamPerThread;
+	if (per_thread)
+		sid = (1ull << 63) | (unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id());
+	else if (get_id && get_id(stream, &sid) != hipSuccess)
 		return EIO;
 	if ((int)g_rows.size() <= device)
 		g_rows.resize(device + 1);
@@ -136,21 +149,29 @@ slot_for(int device, hipStream_t stream, rows_slot **out)
 		}
 		r.sid = sid;
 		r.stream = stream;
+		r.per_thread = per_thread;
 		r.last = ++g_rows_tick;
 		pool.push_back(r);
 		*out = &pool.back();
 		return 0;
 	}
-	hipEvent_t ev;
-	if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-		return ENOMEM;
-	hipError_t e = hipEventRecord(ev, lru->stream);
-	e = (e == hipSuccess) ? hipStreamWaitEvent(stream, ev, 0) : hipDeviceSynchronize();
-	hipEventDestroy(ev);
+	hipError_t e;
+	if (lru->per_thread) {
+		// (the handle names the calling thread's stream, not the owner's: drain the device)
+		e = hipDeviceSynchronize();
+	} else {
+		hipEvent_t ev;
+		if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+			return ENOMEM;
+		e = hipEventRecord(ev, lru->stream);
+		e = (e == hipSuccess) ? hipStreamWaitEvent(stream, ev, 0) : hipDeviceSynchronize();
+		hipEventDestroy(ev);
+	}
 	if (e != hipSuccess)
 		return EIO;
 	lru->sid = sid;
 	lru->stream = stream;
+	lru->per_thread = per_thread;
 	lru->last = ++g_rows_tick;
 	*out = lru;
 	return 0;
@@ -219,6 +240,29 @@ rq_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
 	if (!err)
 		*out = static_cast<uint8_t *>(r->rq);
 	return err;
+}
+
+// The leading stream's multi-device scratch: `rows` histogram rows and `nev` events.
+int
+multi_acquire(int device, hipStream_t stream, uint32_t rows, size_t nev, unsigned long long **mh,
+	      hipEvent_t **ev)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		err = grow_zeroed(&r->mh, &r->mh_bytes, (size_t)rows * EBPF_HIST_BINS * 8);
+	while (!err && r->ev.size() < nev) {
+		hipEvent_t e;
+		if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+			return ENOMEM;
+		r->ev.push_back(e);
+	}
+	if (err)
+		return err;
+	*mh = static_cast<unsigned long long *>(r->mh);
+	*ev = r->ev.data();
+	return 0;
 }
 
 thread_local std::string t_err;
@@ -308,14 +352,23 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 {
 	const uint16_t cpu = map_current_cpu();
 	for (struct ebpf_map *em : ep->xlated->maps) {
-		// a batch on another device wrote the map: its writes reach the host copy first
+		const uint16_t c = em->percpu ? cpu : 0;
+		// a batch wrote the map on another device, or on this one for another CPU's copy of a
+		// percpu map (which is about to be replaced by this CPU's): its writes reach the host
+		// copy first
 		const int dd = em->dev_dirty.load(std::memory_order_acquire);
-		if (dd >= 0 && dd != device)
-			map_pull_device_writes(em);
+		if (dd >= 0) {
+			bool pull = dd != device;
+			if (!pull) {
+				std::lock_guard<std::mutex> g(em->mirror_lock);
+				pull = em->mirrors[device].cpu != c;
+			}
+			if (pull && map_pull_device_writes(em) != 0)
+				return fail(EIO, "copying a device batch's map writes back failed");
+		}
 		std::lock_guard<std::mutex> g(em->mirror_lock);
 		map_mirror &m = em->mirrors[device];
 		uint64_t v = em->version.load();
-		const uint16_t c = em->percpu ? cpu : 0;
 		if (m.version != v || m.cpu != c) {
 			hipError_t e;
 			if (em->is_hashtable()) {
@@ -700,9 +753,23 @@ set_last_error(const std::string &msg)
 	t_err = msg;
 }
 
+device_guard::device_guard()
+{
+	if (hipGetDevice(&prev) != hipSuccess)
+		prev = -1;
+}
+
+device_guard::~device_guard()
+{
+	int now = -1;
+	if (prev >= 0 && (hipGetDevice(&now) != hipSuccess || now != prev))
+		hipSetDevice(prev);
+}
+
 void
 prog_release_device_state(struct ebpf_prog *ep)
 {
+	device_guard dg;
 	for (auto &dp : ep->dev) {
 		if (!dp)
 			continue;
@@ -726,6 +793,7 @@ prog_release_device_state(struct ebpf_prog *ep)
 void
 map_release_device_state(struct ebpf_map *em)
 {
+	device_guard dg;
 	if (em->wb_event) {
 		hipEventSynchronize(static_cast<hipEvent_t>(em->wb_event));
 		hipEventDestroy(static_cast<hipEvent_t>(em->wb_event));
@@ -749,6 +817,10 @@ map_mark_device_write(struct ebpf_map *em, int device, void *stream)
 		if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
 			return;
 		em->wb_event = ev;
+	} else if (em->dev_dirty.load() == device) {
+		// another stream may have written the mirror and not finished: the event recorded below
+		// must cover that apply too (the pull waits for every writer, not only the last)
+		hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(em->wb_event), 0);
 	}
 	hipEventRecord(static_cast<hipEvent_t>(em->wb_event), static_cast<hipStream_t>(stream));
 	const uint64_t v = em->version.fetch_add(1) + 1;
@@ -757,22 +829,27 @@ map_mark_device_write(struct ebpf_map *em, int device, void *stream)
 	em->dev_dirty.store(device, std::memory_order_release);
 }
 
-void
+int
 map_pull_device_writes(struct ebpf_map *em)
 {
 	if (em->dev_dirty.load(std::memory_order_acquire) < 0)
-		return;
+		return 0;
 	std::lock_guard<std::mutex> g(em->mirror_lock);
 	const int d = em->dev_dirty.load(std::memory_order_acquire);
 	if (d < 0 || d >= (int)em->mirrors.size())
-		return;
+		return 0;
 	const map_mirror &m = em->mirrors[d];
-	hipEventSynchronize(static_cast<hipEvent_t>(em->wb_event));
+	hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(em->wb_event));
 	// array / percpu array: the mirror is the (submitting CPU's) value array
 	uint8_t *dst = const_cast<uint8_t *>(map_array_image(em, em->percpu ? m.cpu : 0));
-	if (dst && m.dev)
-		hipMemcpy(dst, m.dev, (size_t)em->value_size * em->max_entries, hipMemcpyDeviceToHost);
+	if (e == hipSuccess && dst && m.dev)
+		e = hipMemcpy(dst, m.dev, (size_t)em->value_size * em->max_entries, hipMemcpyDeviceToHost);
+	if (e != hipSuccess) {
+		set_last_error(std::string("map write-back: ") + hipGetErrorString(e));
+		return EIO; // (still dirty: a later call tries again)
+	}
 	em->dev_dirty.store(-1, std::memory_order_release);
+	return 0;
 }
 
 EBPF_EXPORT int
@@ -791,6 +868,7 @@ ebpf_dev_init(int ndev)
 		ndev = n;
 	if (ndev > n)
 		return fail(ENODEV, "ebpf_dev_init: more devices asked for than visible");
+	device_guard dg;
 	for (int d = 0; d < ndev; d++)
 		if (!asm_available(d))
 			return fail(EIO, "device " + std::to_string(d) + ": the kernels' code object did not load");
@@ -842,6 +920,7 @@ ebpf_prog_prepare_device(struct ebpf_prog *ep, int device)
 {
 	if (ep == nullptr)
 		return fail(EINVAL, "prog is NULL");
+	device_guard dg;
 	dprog_device *dp;
 	return prepare(ep, device, &dp);
 }
@@ -937,6 +1016,7 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	if (err)
 		return err;
 	const bool overwrite = (batch->flags & EBPF_BATCH_HIST_OVERWRITE) != 0;
+	device_guard dg;
 	dprog_device *dp;
 	err = prepare(ep, device, &dp);
 	if (err)
@@ -1120,6 +1200,10 @@ check_devices(int ndev, const int *devices, bool distinct)
 int rccl_hist_allreduce(int ndev, const int *devices, uint64_t *const *hist, hipStream_t *streams,
 			std::string *msg);
 
+namespace {
+std::mutex g_multi_lock; // ebpf_prog_run_batch_multi_dev's enqueue (its scratch is per stream)
+}
+
 EBPF_EXPORT int
 ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, uint64_t *ret,
 		    uint8_t *faults, struct ebpf_batch_stats *stats)
@@ -1131,6 +1215,7 @@ ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch, ui
 		return err;
 	auto t0 = std::chrono::steady_clock::now();
 	const int device = t_dev;
+	device_guard dg;
 	dprog_device *dp;
 	if ((err = prepare(ep, device, &dp)))
 		return err;
@@ -1161,6 +1246,7 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 	if (err || (err = check_devices(ndev, devices, false)))
 		return err;
 	auto t0 = std::chrono::steady_clock::now();
+	device_guard dg;
 	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
 		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
 					"land in packet order in one mirror)");
@@ -1220,25 +1306,111 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 {
 	if (ep == nullptr || shards == nullptr || ret_dev == nullptr)
 		return fail(EINVAL, "prog, shards or ret_dev is NULL");
-	int err = check_devices(ndev, devices, true);
+	int err = check_devices(ndev, devices, false);
 	if (err)
 		return err;
+	for (int d = 0; d < ndev; d++)
+		if ((err = validate_batch(&shards[d], EBPF_BATCH_HIST_OVERWRITE)))
+			return err;
 	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
 		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
 					"land in packet order in one mirror)");
+	device_guard dg;
 	std::vector<hipStream_t> st(ndev);
-	for (int d = 0; d < ndev; d++) {
+	for (int d = 0; d < ndev; d++)
 		st[d] = streams ? static_cast<hipStream_t>(streams[d]) : nullptr;
-		if ((err = ebpf_prog_run_batch_dev(ep, devices[d], &shards[d], ret_dev[d],
-						   faults_dev ? faults_dev[d] : nullptr,
-						   hist_dev ? hist_dev[d] : nullptr, st[d])))
-			return err;
+	if (hist_dev == nullptr) { // no collective: independent launches
+		for (int d = 0; d < ndev; d++)
+			if ((err = ebpf_prog_run_batch_dev(ep, devices[d], &shards[d], ret_dev[d],
+							   faults_dev ? faults_dev[d] : nullptr, nullptr, st[d])))
+				return err;
+		return 0;
+	}
+	// The histogram: every shard's launch SETS its row of the scratch of its device's leading
+	// stream (the first shard on that device); the rows of one device are summed into row 0,
+	// row 0 is summed across devices (RCCL), and only then stored into (EBPF_BATCH_HIST_OVERWRITE)
+	// or added to each caller histogram.  The caller's buffers never take part in the collective.
+	std::lock_guard<std::mutex> serial(g_multi_lock); // (one call's enqueue at a time: the scratch)
+	struct group {
+		int device;
+		std::vector<int> shard; // shard[0] leads
+		unsigned long long *mh = nullptr;
+		hipEvent_t *ev = nullptr;
+	};
+	std::vector<group> G;
+	for (int d = 0; d < ndev; d++) {
+		auto it = std::find_if(G.begin(), G.end(), [&](const group &g) { return g.device == devices[d]; });
+		if (it == G.end()) {
+			G.push_back(group{devices[d], {}});
+			it = G.end() - 1;
+		}
+		it->shard.push_back(d);
+	}
+	hipError_t e;
+	for (group &g : G) {
+		const hipStream_t lead = st[g.shard[0]];
+		if ((e = hipSetDevice(g.device)) != hipSuccess)
+			return hip_fail(e, "hipSetDevice");
+		// events: [0] fork (lead -> the others), [1 + j] join of shard j, [1 + k] the result
+		const size_t k = g.shard.size();
+		if ((err = multi_acquire(g.device, lead, (uint32_t)k, k + 2, &g.mh, &g.ev)))
+			return fail(err, "multi-device histogram scratch");
+		if (k > 1 && (e = hipEventRecord(g.ev[0], lead)) != hipSuccess)
+			return hip_fail(e, "hipEventRecord");
+		for (size_t j = 0; j < k; j++) {
+			const int d = g.shard[j];
+			if (j > 0 && st[d] != lead && (e = hipStreamWaitEvent(st[d], g.ev[0], 0)) != hipSuccess)
+				return hip_fail(e, "hipStreamWaitEvent");
+			struct ebpf_pkt_batch b = shards[d];
+			b.flags |= EBPF_BATCH_HIST_OVERWRITE;
+			if ((err = ebpf_prog_run_batch_dev(ep, g.device, &b, ret_dev[d],
+							   faults_dev ? faults_dev[d] : nullptr,
+							   reinterpret_cast<uint64_t *>(g.mh + j * EBPF_HIST_BINS),
+							   st[d])))
+				return err;
+			if (j > 0 && st[d] != lead &&
+			    ((e = hipEventRecord(g.ev[1 + j], st[d])) != hipSuccess ||
+			     (e = hipStreamWaitEvent(lead, g.ev[1 + j], 0)) != hipSuccess))
+				return hip_fail(e, "shard join");
+		}
+		if ((e = hipSetDevice(g.device)) != hipSuccess ||
+		    (e = launch_hist_sum_rows(g.mh, (uint32_t)k, lead)) != hipSuccess)
+			return hip_fail(e, "histogram rows");
 	}
 	const char *force = getenv("EBPF_FORCE_RCCL"); // (tests: the collective on one GPU)
-	if (hist_dev == nullptr || (ndev == 1 && !(force && *force == '1')))
-		return 0;
-	std::string msg;
-	if ((err = rccl_hist_allreduce(ndev, devices, hist_dev, st.data(), &msg)))
-		return fail(err, msg);
+	if (G.size() > 1 || (force && *force == '1')) {
+		std::vector<int> dv;
+		std::vector<uint64_t *> hv;
+		std::vector<hipStream_t> sv;
+		for (const group &g : G) {
+			dv.push_back(g.device);
+			hv.push_back(reinterpret_cast<uint64_t *>(g.mh));
+			sv.push_back(st[g.shard[0]]);
+		}
+		std::string msg;
+		if ((err = rccl_hist_allreduce((int)G.size(), dv.data(), hv.data(), sv.data(), &msg)))
+			return fail(err, msg);
+	}
+	for (group &g : G) {
+		const hipStream_t lead = st[g.shard[0]];
+		const size_t k = g.shard.size();
+		if ((e = hipSetDevice(g.device)) != hipSuccess)
+			return hip_fail(e, "hipSetDevice");
+		for (size_t j = 0; j < k; j++) {
+			const int d = g.shard[j];
+			const bool ow = (shards[d].flags & EBPF_BATCH_HIST_OVERWRITE) != 0;
+			if ((e = launch_hist_store(reinterpret_cast<unsigned long long *>(hist_dev[d]), g.mh, ow,
+						   lead)) != hipSuccess)
+				return hip_fail(e, "histogram store");
+		}
+		// the other shards' streams see their histogram (and the scratch is free) after this
+		if (k > 1 && (e = hipEventRecord(g.ev[1 + k], lead)) != hipSuccess)
+			return hip_fail(e, "hipEventRecord");
+		for (size_t j = 1; j < k; j++) {
+			const int d = g.shard[j];
+			if (st[d] != lead && (e = hipStreamWaitEvent(st[d], g.ev[1 + k], 0)) != hipSuccess)
+				return hip_fail(e, "hipStreamWaitEvent");
+		}
+	}
 	return 0;
 }

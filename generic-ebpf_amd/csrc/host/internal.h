@@ -197,8 +197,19 @@ void set_last_error(const std::string &msg);
 // the calling thread's device for the host-buffer entry points (ebpf_gpu_set_device)
 int current_device();
 // Copy a device batch's map writes back into the host copy (no-op unless em->dev_dirty).
-void map_pull_device_writes(struct ebpf_map *em);
+// Returns 0, or EIO when the copy failed (the map then stays marked dirty).
+int map_pull_device_writes(struct ebpf_map *em);
 // A batch on `device` wrote the map (its writes land on `stream`, a hipStream_t).
 void map_mark_device_write(struct ebpf_map *em, int device, void *stream);
 void prog_release_device_state(struct ebpf_prog *ep);
 void map_release_device_state(struct ebpf_map *em);
+
+// The calling thread's current HIP device, restored when the scope ends: a C library must not
+// change it (every exported entry point that selects a device holds one).
+struct device_guard {
+	int prev = -1;
+	device_guard();
+	~device_guard();
+	device_guard(const device_guard &) = delete;
+	device_guard &operator=(const device_guard &) = delete;
+};

@@ -657,7 +657,8 @@ ebpf_map_lookup_elem(struct ebpf_map *em, void *key)
 {
 	if (em == nullptr || key == nullptr)
 		return nullptr;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return nullptr; // (the device's writes could not be copied back: no stale value)
 	return em->emt->ops.lookup_elem(em, key);
 }
 
@@ -666,7 +667,8 @@ ebpf_map_lookup_elem_from_user(struct ebpf_map *em, void *key, void *value)
 {
 	if (em == nullptr || key == nullptr || value == nullptr)
 		return EINVAL;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.lookup_elem_from_user(em, key, value);
 }
 
@@ -675,7 +677,8 @@ ebpf_map_update_elem(struct ebpf_map *em, void *key, void *value, uint64_t flags
 {
 	if (em == nullptr || key == nullptr || value == nullptr || flags > EBPF_EXIST)
 		return EINVAL;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.update_elem(em, key, value, flags);
 }
 
@@ -684,7 +687,8 @@ ebpf_map_update_elem_from_user(struct ebpf_map *em, void *key, void *value, uint
 {
 	if (em == nullptr)
 		return EINVAL; // the reference performs no argument checks here (ebpf_map.c:112-123)
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.update_elem_from_user(em, key, value, flags);
 }
 
@@ -693,7 +697,8 @@ ebpf_map_delete_elem(struct ebpf_map *em, void *key)
 {
 	if (em == nullptr || key == nullptr)
 		return EINVAL;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.delete_elem(em, key);
 }
 
@@ -702,7 +707,8 @@ ebpf_map_delete_elem_from_user(struct ebpf_map *em, void *key)
 {
 	if (em == nullptr || key == nullptr)
 		return EINVAL;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.delete_elem_from_user(em, key);
 }
 
@@ -712,7 +718,8 @@ ebpf_map_get_next_key_from_user(struct ebpf_map *em, void *key, void *next_key)
 	// key == NULL is valid: "give me the first key" (ebpf_map.c:148-151)
 	if (em == nullptr || next_key == nullptr)
 		return EINVAL;
-	map_pull_device_writes(em);
+	if (map_pull_device_writes(em) != 0)
+		return EIO;
 	return em->emt->ops.get_next_key_from_user(em, key, next_key);
 }
 

@@ -68,13 +68,15 @@ load()
 
 } // namespace
 
-// Sum hist[d] (EBPF_HIST_BINS u64 on devices[d]) over d in place, each on streams[d], as one
-// RCCL group.  Asynchronous.  Returns 0, ENOSYS (no RCCL) or EIO (RCCL error; *msg says which).
+// Sum hist[d] (EBPF_HIST_BINS u64 on devices[d], distinct devices) over d in place, each on
+// streams[d], as one RCCL group.  Asynchronous.  hist[d] is the library's scratch, never a caller's
+// histogram (ebpf_prog_run_batch_multi_dev adds the sum into those afterwards).  Returns 0, ENOSYS (no RCCL) or EIO (RCCL error; *msg says which).
 int
 rccl_hist_allreduce(int ndev, const int *devices, uint64_t *const *hist, hipStream_t *streams,
 		    std::string *msg)
 {
 	std::lock_guard<std::mutex> g(g_lock);
+	device_guard dg;
 	if (!load()) {
 		*msg = g_api.err;
 		return ENOSYS;

@@ -645,7 +645,8 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	if (unsupported != nullptr) {
 		out.error = EOPNOTSUPP;
 		out.error_msg = std::string("the program uses a ") + unsupported->emt->name +
-				" map with no device form (hashtable keys over 256 bytes; run it with "
+				" map with no device form (hashtable keys over 65535 bytes or a table over 64 GiB; "
+				"run it with "
 				"ebpf_prog_run)";
 		out.maps.clear(); // (not pinned: nothing to release)
 		return EOPNOTSUPP;

@@ -15,7 +15,7 @@
  *   the 18 API functions         ↔ :107-128
  *   the 7 exported descriptors   ↔ :130-136
  * Layouts are byte-identical on x86-64 (checked by static asserts in the library and by
- * tests/test_abi.py); behaviour (validation order, errno values, refcounting) follows the
+ * tests/test_api.py); behaviour (validation order, errno values, refcounting) follows the
  * reference implementation files cited at each definition in generic-ebpf_amd/csrc/host/.
  *
  * The GPU batch extension lives in ebpf_gpu.h.

@@ -137,13 +137,15 @@ int ebpf_prog_prepare_device(struct ebpf_prog *ep, int device);
 int ebpf_prog_run_batch(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
 			uint64_t *ret, uint8_t *faults, struct ebpf_batch_stats *stats);
 
-/* ebpf_prog_run_batch without blocking the caller: the job is queued on a worker bound to the
- * calling thread's current device and returns at once, so a NIC-ring or capture consumer can
- * fill its next segment meanwhile; ebpf_batch_wait blocks until ret/faults hold the results,
- * returns the batch's error code (ebpf_prog_run_batch's) and releases the job (wait once per
- * job).  The program, the batch's buffers, ret and faults must stay valid until the wait;
- * several jobs may be in flight.
- * Returns 0, EINVAL (NULL argument), ENODEV (no GPU), ENOMEM, EAGAIN (no thread). */
+/* ebpf_prog_run_batch without blocking the caller: the job is queued for the worker pool of the
+ * calling thread's current device (two persistent threads per device, a FIFO of at most 64
+ * queued jobs) and the call returns at once, so a NIC-ring or capture consumer can fill its next
+ * segment meanwhile; ebpf_batch_wait blocks until ret/faults hold the results, returns the
+ * batch's error code (ebpf_prog_run_batch's) and releases the job (wait once per job).  The
+ * program, the batch's buffers, ret and faults must stay valid until the wait; several jobs may
+ * be in flight.
+ * Returns 0, EINVAL (NULL argument), ENODEV (no GPU), ENOMEM, EAGAIN (the device's queue is
+ * full — wait for an earlier job — or no worker thread could be started). */
 struct ebpf_batch_job;
 int ebpf_prog_run_batch_async(struct ebpf_prog *ep, const struct ebpf_pkt_batch *batch,
 			      uint64_t *ret, uint8_t *faults, struct ebpf_batch_job **job);
@@ -167,11 +169,16 @@ int ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_
  *   shards then share it).  stats->hist is the sum of the shards' histograms, stats->kernel_ms
  *   the slowest shard's device time.
  * ebpf_prog_run_batch_multi_dev: device-resident, asynchronous: shards[d], ret_dev[d],
- *   faults_dev[d] (optional), hist_dev[d] (optional) live on devices[d] (distinct devices) and
- *   each launch is enqueued on streams[d] (NULL array = default streams).  With hist_dev, each
- *   hist_dev[d] then holds the SUM over all devices: one RCCL all-reduce (uint64, sum) over the
- *   devices' streams, the path's only collective.  Returns ENOSYS if ndev > 1 and RCCL
- *   (librccl.so.1) cannot be loaded.
+ *   faults_dev[d] (optional), hist_dev[d] (optional) live on devices[d] and each launch is
+ *   enqueued on streams[d] (NULL array = default streams).  `devices` may repeat a device.  With
+ *   hist_dev, the batch's histogram — the SUM over all shards — is added to each hist_dev[d], or
+ *   stored into it when shards[d].flags has EBPF_BATCH_HIST_OVERWRITE, as ebpf_prog_run_batch_dev
+ *   does for one shard.  The sum is formed in library-owned scratch (the shards of one device
+ *   summed on the first one's stream, then one RCCL all-reduce (uint64, sum) over the distinct
+ *   devices: the path's only collective); streams[d] sees hist_dev[d] complete in stream order.
+ *   Returns ENOSYS if several distinct devices are given and RCCL (librccl.so.1) cannot be
+ *   loaded.
+ * Neither changes the calling thread's current HIP device (no entry point of this header does).
  * Both return 0 or an errno (ENODEV: a device index out of range; EINVAL: bad arguments). */
 int ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 			      const struct ebpf_pkt_batch *batch, uint64_t *ret, uint8_t *faults,
@@ -193,10 +200,10 @@ int ebpf_gpu_set_device(int device);
 int ebpf_gpu_set_variant(int variant);
 
 /* Measurement hook (extension): the calling thread's next ebpf_prog_run_batch_dev records
- * `start_event` just before the interpreter kernel and `stop_event` just after it, on the launch
- * stream, so that hipEventElapsedTime gives the interpreter kernel's own duration (the verdict
- * histogram's second-stage reduce comes after `stop_event`).  Both are hipEvent_t of the HIP
- * runtime the library runs on; NULL, NULL cancels.  Returns 0, or EINVAL if only one is NULL. */
+ * `start_event` at the start of the launch's kernel and `stop_event` at its end, on the launch
+ * stream, so that hipEventElapsedTime gives the kernel's own duration (a launch is one kernel:
+ * the verdict histogram is reduced inside it).  Both are hipEvent_t of the HIP runtime the
+ * library runs on; NULL, NULL cancels.  Returns 0, or EINVAL if only one is NULL. */
 int ebpf_gpu_time_next_launch(void *start_event, void *stop_event);
 
 /* Instruction semantics of a program (extension: the reference has only the first).

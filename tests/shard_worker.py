@@ -1,4 +1,4 @@
-"""Worker for tests/test_shard_gpu.py (run under torch.distributed.run, gloo, every rank on
+"""Worker for tests/test_multi_gpu.py::test_two_ranks_gloo_equal_one_launch (run under torch.distributed.run, gloo, every rank on
 cuda:0): each rank runs its contiguous shard of one C4 / C5 batch on the device
 (ebpf_prog_run_batch_dev, the bench's path), the shards' results are gathered to rank 0 and the
 histograms summed (the only collective); rank 0 compares them with ONE launch over the whole

@@ -114,14 +114,15 @@ def test_run_batch_multi_imix(gpu, env):
 @pytest.mark.gpu
 def test_run_batch_multi_dev_rccl(gpu, env, monkeypatch):
     """Device-resident multi launch through the RCCL all-reduce (forced at one device: the
-    communicator, the grouped all-reduce and the dlopen of RCCL all run), histogram exact;
-    a repeated device is refused."""
-    import errno
+    communicator, the grouped all-reduce and the dlopen of RCCL all run), histogram exact in
+    overwrite mode and in add mode over three consecutive calls (the caller's earlier counts are
+    added to, never multiplied by the collective)."""
     import torch
     monkeypatch.setenv("EBPF_FORCE_RCCL", "1")
     n = 1 << 20
     c = _c4_case(n, seed=21)
     want, _, _, _ = oracle_run(c, nthreads=16)
+    h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
     maps = make_maps(gpu, env, c)
     p = gpu.Prog(env, gpu.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
     try:
@@ -134,16 +135,101 @@ def test_run_batch_multi_dev_rccl(gpu, env, monkeypatch):
                               hists=[d_hist.data_ptr()], streams=[st], hist_overwrite=True)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
-        h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
         np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
-        with pytest.raises(gpu.EbpfError) as ei:
-            p.run_batch_multi_dev([0, 0], [(d_pk.data_ptr(), n, 64, None)] * 2,
-                                  [d_ret.data_ptr()] * 2)
-        assert ei.value.code == errno.EINVAL
+        d_hist.fill_(5)
+        for _ in range(3):
+            p.run_batch_multi_dev([0], [(d_pk.data_ptr(), n, 64, None)], [d_ret.data_ptr()],
+                                  hists=[d_hist.data_ptr()], streams=[st])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), 5 + 3 * h)
     finally:
         p.destroy()
         for m in maps:
             m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("same_stream", [False, True])
+def test_run_batch_multi_dev_shards_one_device(gpu, env, same_stream):
+    """Two shards on one device (a repeated device index): each caller histogram receives the
+    SUM over both shards, added to what it held (three calls in add mode: 3x the oracle's plus
+    the initial counts) or set (overwrite); shards on two streams join and fork correctly."""
+    import torch
+    n = (1 << 20) + 333
+    c = _c4_case(n, seed=22)
+    want, _, _, _ = oracle_run(c, nthreads=16)
+    h = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
+    maps = make_maps(gpu, env, c)
+    p = gpu.Prog(env, gpu.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(c.data).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        h0 = torch.full((257,), 7, dtype=torch.int64, device=dev)
+        h1 = torch.full((257,), 11, dtype=torch.int64, device=dev)
+        s0 = torch.cuda.Stream()
+        s1 = s0 if same_stream else torch.cuda.Stream()
+        torch.cuda.synchronize()
+        half = n // 2
+        shards = [(d_pk.data_ptr(), half, 64, None),
+                  (d_pk.data_ptr() + half * 64, n - half, 64, None)]
+        rets = [d_ret.data_ptr(), d_ret.data_ptr() + half * 8]
+        for _ in range(3):
+            p.run_batch_multi_dev([0, 0], shards, rets, hists=[h0.data_ptr(), h1.data_ptr()],
+                                  streams=[s0.cuda_stream, s1.cuda_stream])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+        np.testing.assert_array_equal(h0.cpu().numpy(), 7 + 3 * h)
+        np.testing.assert_array_equal(h1.cpu().numpy(), 11 + 3 * h)
+        p.run_batch_multi_dev([0, 0], shards, rets, hists=[h0.data_ptr(), h1.data_ptr()],
+                              streams=[s0.cuda_stream, s1.cuda_stream], hist_overwrite=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(h0.cpu().numpy(), h)
+        np.testing.assert_array_equal(h1.cpu().numpy(), h)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+def test_entry_points_keep_current_device(gpu, env):
+    """A C library must not change its caller's current device: after every entry point the
+    thread's device is the one it set (on a box with several GPUs the caller sits on the last
+    one and the library works on device 0)."""
+    import torch
+    nd = torch.cuda.device_count()
+    mine = nd - 1
+    torch.cuda.set_device(mine)
+    n = 4096
+    c = _c4_case(n, seed=23)
+    maps = make_maps(gpu, env, c)
+    p = gpu.Prog(env, gpu.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
+    try:
+        gpu.dev_init(0)
+        assert torch.cuda.current_device() == mine
+        p.prepare(0)
+        assert torch.cuda.current_device() == mine
+        ret, faults, st = p.run_batch(np.ascontiguousarray(c.data), n, 64)
+        assert torch.cuda.current_device() == mine
+        p.run_batch_multi([0, 0], np.ascontiguousarray(c.data), n, 64)
+        assert torch.cuda.current_device() == mine
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(c.data).to(dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+        torch.cuda.set_device(mine)
+        p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), hist_ptr=d_hist.data_ptr())
+        assert torch.cuda.current_device() == mine
+        p.run_batch_multi_dev([0], [(d_pk.data_ptr(), n, 64, None)], [d_ret.data_ptr()],
+                              hists=[d_hist.data_ptr()])
+        assert torch.cuda.current_device() == mine
+        torch.cuda.synchronize(dev)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+        torch.cuda.set_device(0)
 
 
 @pytest.mark.gpu
