@@ -553,9 +553,15 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 		return fail(err, "map-write log");
 	P->faulted = reinterpret_cast<uint32_t *>(P->log + boff);
 	P->faulted_bytes = bbytes;
-	// (the buffer is reused at other sizes: whatever lies where the bitmap now starts is stale)
+	// (the buffer is reused at other sizes: whatever lies where the bitmap now starts is stale).
+	// The log's counter and the winner words are zero after every apply step; they are zeroed
+	// here too, so that a batch whose launch failed before its apply leaves nothing behind
 	hipError_t e = hipMemsetAsync(P->faulted, 0, bbytes, stream);
-	return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync(faulted-packet bitmap)");
+	if (e == hipSuccess)
+		e = hipMemsetAsync(P->log, 0, 4, stream);
+	if (e == hipSuccess && dp->win_words)
+		e = hipMemsetAsync(P->win, 0, dp->win_words * 8, stream);
+	return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync(map-write log)");
 }
 
 // After the batch: the logged writes land in the mirrors (packet order), and the written maps
@@ -685,6 +691,7 @@ struct staging {
 	int device = -1;
 	hipStream_t stream[2] = {nullptr, nullptr};
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	hipEvent_t ev_plan = nullptr; // map-writing programs: the log's set-up on stream 0 (stream 1 waits)
 	void *d_data[2] = {nullptr, nullptr};
 	size_t data_cap[2] = {0, 0};
 	void *d_small[2] = {nullptr, nullptr}; // ret | faults | offsets, per chunk
@@ -714,6 +721,8 @@ staging_acquire(int device, staging **out)
 		e = hipStreamCreateWithFlags(&S->stream[i], hipStreamNonBlocking);
 	for (int i = 0; i < 4 && e == hipSuccess; i++)
 		e = hipEventCreate(&S->ev[i]);
+	if (e == hipSuccess)
+		e = hipEventCreateWithFlags(&S->ev_plan, hipEventDisableTiming);
 	if (e == hipSuccess)
 		e = hipMalloc(&S->d_hist, EBPF_HIST_BINS * sizeof(unsigned long long));
 	if (e != hipSuccess)
@@ -1075,8 +1084,14 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	// a map-writing program: one log for the whole shard, applied after its last chunk (every
 	// chunk reads the maps as they were when the batch started)
 	upd_plan plan;
-	if (ep->xlated->max_updates && (err = upd_plan_for(ep, dp, hi - lo, S.stream[0], &plan)))
-		return err;
+	if (ep->xlated->max_updates) {
+		// the log is set up on stream 0; the odd chunks run on stream 1 and log into it too
+		if ((err = upd_plan_for(ep, dp, hi - lo, S.stream[0], &plan)))
+			return err;
+		if ((e = hipEventRecord(S.ev_plan, S.stream[0])) != hipSuccess ||
+		    (e = hipStreamWaitEvent(S.stream[1], S.ev_plan, 0)) != hipSuccess)
+			return hip_fail(e, "map-write log set-up");
+	}
 	bool timed[2] = {false, false};
 	// on any error: drain both streams (buffers stay valid for the copies in flight)
 	auto drain = [&](int rc) {

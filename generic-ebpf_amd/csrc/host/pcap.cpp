@@ -107,7 +107,7 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 	}
 	const uint32_t snaplen = rd32(b + 16, swap), linktype = rd32(b + 20, swap);
 	// pass 1: count the records and their bytes, validating every header
-	uint64_t count = 0, bytes = 0, truncated = 0;
+	uint64_t count = 0, bytes = 0, truncated = 0, cut = 0;
 	size_t at = 24;
 	while (at < len) {
 		if (len - at < 16) {
@@ -119,13 +119,13 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 			set_last_error("pcap: record at byte " + std::to_string(at) + " runs past the end");
 			return EINVAL;
 		}
-		if (snaplen && incl > snaplen) {
-			set_last_error("pcap: record at byte " + std::to_string(at) + " longer than snaplen");
-			return EINVAL;
-		}
-		truncated += incl < orig;
+		// a record longer than the header's snaplen (some writers get the snaplen wrong): as
+		// libpcap's reader does, the packet is its first snaplen bytes (counted as truncated)
+		const uint32_t keep = (snaplen && incl > snaplen) ? snaplen : incl;
+		cut += keep < incl;
+		truncated += keep < orig;
 		count++;
-		bytes += incl;
+		bytes += keep;
 		at += 16 + (size_t)incl;
 	}
 	// pass 2: gather the captured bytes
@@ -136,20 +136,35 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 		release(offs);
 		return ENOMEM;
 	}
+	// where record i's bytes start in the capture: 24 + 16 (i + 1) + offs[i] unless a record
+	// was cut to the snaplen (then from a table)
+	std::vector<size_t> src;
+	if (cut) {
+		try {
+			src.resize(count);
+		} catch (...) {
+			release(data);
+			release(offs);
+			return ENOMEM;
+		}
+	}
 	uint64_t o = 0, i = 0;
 	at = 24;
 	while (at < len) {
 		const uint32_t incl = rd32(b + at + 8, swap);
+		if (cut)
+			src[i] = at + 16;
 		offs[i++] = o;
-		o += incl;
+		o += (snaplen && incl > snaplen) ? snaplen : incl;
 		at += 16 + (size_t)incl;
 	}
 	offs[count] = o;
-	// record i's bytes start at 24 + 16 (i + 1) + offs[i] in the capture: the copies are
-	// independent, so large captures are gathered by several threads (contiguous packet ranges)
+	// the copies are independent, so large captures are gathered by several threads (contiguous
+	// packet ranges)
 	auto gather = [&](uint64_t lo, uint64_t hi) {
 		for (uint64_t k = lo; k < hi; k++)
-			memcpy(data + offs[k], b + 24 + 16 * (k + 1) + offs[k], (size_t)(offs[k + 1] - offs[k]));
+			memcpy(data + offs[k], b + (cut ? src[k] : 24 + 16 * (k + 1) + offs[k]),
+			       (size_t)(offs[k + 1] - offs[k]));
 	};
 	unsigned nt = std::thread::hardware_concurrency();
 	nt = std::max(1u, std::min(nt, 16u));

@@ -102,8 +102,10 @@ struct ebpf_batch_stats {
  * ebpf_prog_run_batch.  The library allocates batch->data and batch->offsets (pinned host memory
  * when `pinned` and a GPU is present, else pageable); release both with ebpf_pcap_batch_free.
  * The capture buffer stays the caller's and is not referenced afterwards.
- * Returns 0, EINVAL (not a classic pcap capture, a truncated record, or a record longer than
- * the snaplen; ebpf_gpu_last_error says which), ENOMEM.  Host only: no GPU needed. */
+ * A record whose captured length exceeds the header's snaplen becomes its first snaplen bytes
+ * (libpcap's reader does the same), counted in info->truncated.
+ * Returns 0, EINVAL (not a classic pcap capture, or a record header or record that runs past
+ * the end of `capture`; ebpf_gpu_last_error says which), ENOMEM.  Host only: no GPU needed. */
 struct ebpf_pcap_info {
 	uint32_t linktype;     /* the capture's link-layer type (1 = Ethernet) */
 	uint32_t snaplen;

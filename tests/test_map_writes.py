@@ -341,3 +341,83 @@ def test_device_faulting_packet_leaves_no_write(gpu, env, variant, resident):
     np.testing.assert_array_equal(faults, wf)
     np.testing.assert_array_equal(ret, want)
     assert after == want_after
+
+
+def _percpu_copies(gpu, m, ncpu):
+    """lookup_from_user on a percpu array: every CPU's value of every key
+    (ebpf_map_array.c:153-170) -> {cpu: bytes of the whole array as that CPU sees it}."""
+    import ctypes
+    L = gpu.lib()
+    per = {c: bytearray() for c in range(ncpu)}
+    for k in range(NKEYS):
+        kk = ctypes.c_uint32(k)
+        buf = ctypes.create_string_buffer(8 * ncpu)
+        assert L.ebpf_map_lookup_elem_from_user(m.ptr, ctypes.byref(kk), buf) == 0
+        for c in range(ncpu):
+            per[c] += buf.raw[8 * c: 8 * c + 8]
+    return {c: bytes(v) for c, v in per.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_percpu_array_writes(gpu, env, variant, resident):
+    """Program-side map_update_elem on a percpu array lands in the copy of the CPU the batch is
+    submitted from (ebpf_map_array.c:213-226: ma + ebpf_curcpu()).  Batches from two pinned CPUs:
+    each CPU's copy holds exactly its own batch's writes (the others keep the initial values), the
+    host's lookup_from_user sees them, and a third batch from the first CPU reads the first
+    batch's writes — which a batch from the second CPU on the same device must not discard."""
+    import os
+    import torch
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 2:
+        pytest.skip("needs two CPUs")
+    c1, c2 = cpus[0], cpus[-1]
+    ncpu = os.sysconf("SC_NPROCESSORS_ONLN")
+    saved = os.sched_getaffinity(0)
+    n = (1 << 16) + 9
+    lay = prog_static()
+    init = _map_init(10)
+    pks = [_packets(n, 41), _packets(n, 42), _packets(n, 43)]
+    # the oracle: per CPU, a plain array map that only that CPU's batches touch
+    state = {c1: init, c2: init}
+    expect = []
+    for pk, c in zip(pks, (c1, c2, c1)):
+        op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, state[c])])
+        want, wf, _, _ = op.run(pk, n, 64, nthreads=16)
+        state[c] = op.map_bytes(0)
+        expect.append((want, wf, dict(state)))
+    m = gpu.Map(env, NKEYS, 8, type=gpu.MAP_TYPE_PERCPU_ARRAY)
+    for k in range(NKEYS):   # from user: every CPU's copy
+        assert m.update(k, init[8 * k: 8 * k + 8]) == 0
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle]))
+    dev = torch.device("cuda:0")
+    try:
+        gpu.set_variant(variant)
+        for (pk, c), (want, wf, st) in zip(zip(pks, (c1, c2, c1)), expect):
+            os.sched_setaffinity(0, {c})
+            if resident:
+                d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+                d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+                d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+                p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None,
+                                d_flt.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                ret, faults = d_ret.cpu().numpy().view(np.uint64), d_flt.cpu().numpy()
+            else:
+                ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+            np.testing.assert_array_equal(faults, wf)
+            np.testing.assert_array_equal(ret, want)
+        os.sched_setaffinity(0, saved)
+        copies = _percpu_copies(gpu, m, ncpu)
+        final = expect[-1][2]
+        assert copies[c1] == final[c1]
+        assert copies[c2] == final[c2]
+        for c in range(ncpu):
+            if c not in (c1, c2):
+                assert copies[c] == init, c
+    finally:
+        os.sched_setaffinity(0, saved)
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()

@@ -71,17 +71,30 @@ def test_pcap_batch_large_capture_threaded(native):
 
 
 @pytest.mark.parametrize("bad", ["magic", "short_header", "record_header", "record_data",
-                                 "snaplen", "empty"])
+                                 "empty"])
 def test_pcap_batch_rejects(native, bad):
     good = make_pcap(_packets(4, seed=3), snaplen=256)
     cap = {"magic": b"\0\0\0\0" + good[4:], "short_header": good[:20],
            "record_header": good + b"\1\2\3", "record_data": good[:-1],
-           "snaplen": make_pcap([b"x" * 300], snaplen=256), "empty": b""}[bad]
+           "empty": b""}[bad]
     with pytest.raises(native.EbpfError) as ei:
         native.PcapBatch(cap)
     assert ei.value.code == errno.EINVAL
     if bad != "empty":
         assert "pcap" in native.last_error()
+
+
+def test_pcap_records_longer_than_snaplen(native):
+    """A record whose captured length exceeds the header's snaplen is cut to the snaplen (as
+    libpcap's reader does) and counted as truncated; the records after it stay aligned."""
+    pk = [b"a" * 300, b"b" * 100, bytes(range(256)) + b"c" * 44, b"", b"d" * 256]
+    with native.PcapBatch(make_pcap(pk, snaplen=256)) as b:
+        assert b.count == 5
+        want = [p[:256] for p in pk]
+        lens = [len(p) for p in want]
+        assert np.array_equal(b.offsets(), np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64))
+        assert b.data().tobytes() == b"".join(want)
+        assert b.info.truncated == 2
 
 
 @pytest.mark.gpu
