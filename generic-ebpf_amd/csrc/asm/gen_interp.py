@@ -137,6 +137,24 @@ assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with regrouping (S_DEFER..) and
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
 # A/B: XCD-major logical workgroup order (common_group_code)
 XCD_MAJOR = os.environ.get("EBPF_ASM_XCD") == "1"
+# Length-bucketed launches (general image; dp_launch.perm, gpu_runtime.cpp bucketing).  A launch
+# runs one length class of a batch: its slots are perm[start .. start + n) (packet indices,
+# bucket.hip), G per group (G <= 64 lanes; the rest idle).  These SGPRs share s78..s83 with the
+# regroup queues: the host never combines the two (a regrouping program is not bucketed).
+S_PERM = 78          # s[78:79] this launch's slots (perm + start); 0 = slot i is packet i
+S_SPAN = 80          # span image: bytes of LDS per lane slot (dp_launch.span_slot, a multiple of
+                     # 16 with an odd number of 16-B blocks: ds_read_b128 at one offset is
+                     # conflict-free), 0 = no span staging
+S_G = 81             # packets per group (64 unless the slots are large)
+S_NSLOT = 82         # slots in this launch (the class's packet count)
+S_MAGN = 83          # (spare)
+# Span image (the third code object, interp_m2): every packet of a group is DMA'd whole into the
+# wave's slice of LDS before the program runs (one LDS-DMA per packet, 16 B per lane), and its
+# packet pointer is the slot's LDS-aperture address: constant-offset packet loads become LDS
+# reads (the compiler's b128 hoisted loads, asm_cc.cpp mode 2) instead of per-lane gathers of
+# 64 distinct lines each.  Bigger hoist ring: the launch is LDS-bound to one workgroup per CU.
+SPAN_IMAGE = False
+SPAN_HOIST_REGS = int(os.environ.get("EBPF_ASM_SPANHOIST", "48"))
 
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
@@ -565,12 +583,25 @@ def h_ldx_pkt_general(z, d):
            "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
            "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
            "s_cbranch_scc1 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:"]
+    if SPAN_IMAGE:
+        # (the packet's slot in LDS when span-staged; else its global address: s7 bit 10)
+        out += ["s_bitcmp1_b32 s7, 10",
+                "s_cbranch_scc0 .Lpg_{uid}",
+                "v_add_u32 %s, s10, v%d" % (v(t[0]), V_PKT),
+                "%s %s, %s" % ({1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[z],
+                               pair(d) if z == 8 else lo(d), v(t[0])),
+                "s_waitcnt lgkmcnt(0)"]
+        if z < 8:
+            out.append("v_mov_b32 %s, 0" % hi(d))
+        out += ["s_branch .Lpd_{uid}", ".Lpg_{uid}:"]
     out.append("v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(t[0]), vp(V_PKT)))
     if z == 8:
         out.append("%s %s, %s, off" % (LOADS[8], pair(d), vp(t[0])))
     else:
         out += ["%s %s, %s, off" % (LOADS[z], lo(d), vp(t[0])), "v_mov_b32 %s, 0" % hi(d)]
     out.append("s_waitcnt vmcnt(0)")
+    if SPAN_IMAGE:
+        out.append(".Lpd_{uid}:")
     return out
 
 
@@ -1519,6 +1550,33 @@ def kernel(name, staged, jit=False):
               "s_addc_u32 %s, %s, 0" % (s(S_QBASE + 1), s(S_QBASE + 1)),
               "s_or_b32 s7, s7, 64",
               ".L%s_norq:" % k]
+    if not staged and not STAGED_IMAGE:
+        # length-bucketed launch (dp_launch.perm != 0): s7 bit 9 = slot mode (this launch's slots
+        # are perm[start .. start + n), G per group), bit 10 = span staging (span image)
+        L += ["s_bitcmp1_b32 s7, 6",                 # (regrouping: s78.. hold the queues)
+              "s_cbranch_scc1 .L%s_noperm" % k,
+              "s_load_dwordx2 %s, s[0:1], 0xb0" % sp(S_PERM),
+              "s_load_dwordx2 s[54:55], s[0:1], 0xb8",
+              "s_load_dwordx4 s[80:83], s[0:1], 0xc0",   # span_slot, G, magic(G), pad
+              "s_waitcnt lgkmcnt(0)",
+              "s_cmp_eq_u64 %s, 0" % sp(S_PERM),
+              "s_cbranch_scc1 .L%s_noperm" % k,
+              "s_load_dwordx2 s[54:55], s[54:55], 0x0",  # {start, n} of the class
+              "s_waitcnt lgkmcnt(0)",
+              "s_lshl_b32 s54, s54, 2",
+              "s_add_u32 %s, %s, s54" % (s(S_PERM), s(S_PERM)),
+              "s_addc_u32 %s, %s, 0" % (s(S_PERM + 1), s(S_PERM + 1)),
+              # groups = ceil(n / G) = mul_hi(n + G - 1, ceil(2^32 / G)), into s83 until
+              # common_group_code takes it
+              "s_add_u32 s83, s55, %s" % s(S_G),
+              "s_sub_u32 s83, s83, 1",
+              "s_mul_hi_u32 s83, s83, s82",
+              "s_mov_b32 %s, s55" % s(S_NSLOT),
+              "s_or_b32 s7, s7, 512",
+              "s_cmp_eq_u32 %s, 0" % s(S_SPAN),
+              "s_cbranch_scc1 .L%s_noperm" % k,
+              "s_or_b32 s7, s7, 1024",
+              ".L%s_noperm:" % k]
     L += ["s_branch .Lprologue"]
     return L
 
@@ -1565,6 +1623,7 @@ def pkt_setup(idx, tag):
             "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
             "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
             "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
+            ] + (span_stage(tag) if SPAN_IMAGE else []) + [
             # header staging: the first 64 bytes of every packet at least that long into
             # v22..v37 (what the staged kernels' LDS DMA provides)
             ".Lps_stage_%s:" % tag,
@@ -1579,6 +1638,57 @@ def pkt_setup(idx, tag):
             "s_waitcnt vmcnt(0)",
             ".Lps_done_%s:" % tag,
             "s_mov_b64 exec, %s" % sp(S_MASK)]
+
+
+def span_stage(tag):
+    """Span image, s7 bit 10: the group's packets (16-B aligned, at most S_SPAN bytes: the host's
+    length class) are DMA'd whole into the wave's LDS slots, packet p at S_PKTLDS + p * S_SPAN,
+    one LDS-DMA of 16 B per lane per 1 KB of packet (coalesced: consecutive lanes, consecutive
+    bytes of one packet); then V_PKT = the slot's LDS-aperture address.  The last 16-B block of a
+    packet is read whole: an aligned block holding a packet byte never leaves its page.
+    Entered with exec = s[S_MASK] (the running lanes, V_PKT / V_LEN set); clobbers R[3:5],
+    s[64:65], S_T1, S_T2, m0."""
+    return ["s_bitcmp1_b32 s7, 10",
+            "s_cbranch_scc0 .Lps_stage_%s" % tag,
+            "v_add_u32 %s, 15, v%d" % (v(R[3]), V_LEN),
+            "v_lshrrev_b32 %s, 4, %s" % (v(R[3]), v(R[3])),       # 16-B blocks of the lane's packet
+            "s_not_b64 exec, %s" % sp(S_MASK),
+            "v_mov_b32 %s, 0" % v(R[3]),
+            "s_mov_b64 exec, -1",
+            "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(R[5]),
+            "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(R[5]), v(R[5])),
+            "v_lshlrev_b32 %s, 4, %s" % (v(R[4]), v(R[5])),
+            "s_mov_b32 %s, 0" % s(S_T1),
+            "s_mov_b32 m0, %s" % s(S_PKTLDS),
+            ".Lsp_loop_%s:" % tag,
+            "v_readlane_b32 s64, v%d, %s" % (V_PKT, s(S_T1)),
+            "v_readlane_b32 s65, v%d, %s" % (V_PKT + 1, s(S_T1)),
+            "v_readlane_b32 %s, %s, %s" % (s(S_T2), v(R[3]), s(S_T1)),
+            "s_nop 4",                        # (VALU-written SGPRs read by a memory instruction)
+            "s_cmp_eq_u32 %s, 0" % s(S_T2),
+            "s_cbranch_scc1 .Lsp_next_%s" % tag,
+            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T2), v(R[5])),
+            "s_mov_b64 exec, vcc",
+            "global_load_lds_dwordx4 %s, s[64:65] offset:0%s" % (v(R[4]), LD_POLICY),
+            "s_sub_u32 %s, %s, 64" % (s(S_T2), s(S_T2)),
+            "s_cmp_le_i32 %s, 0" % s(S_T2),
+            "s_cbranch_scc1 .Lsp_one_%s" % tag,
+            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T2), v(R[5])),
+            "s_mov_b64 exec, vcc",
+            "global_load_lds_dwordx4 %s, s[64:65] offset:1024%s" % (v(R[4]), LD_POLICY),
+            ".Lsp_one_%s:" % tag,
+            "s_mov_b64 exec, -1",
+            ".Lsp_next_%s:" % tag,
+            "s_add_u32 m0, m0, %s" % s(S_SPAN),
+            "s_add_u32 %s, %s, 1" % (s(S_T1), s(S_T1)),
+            "s_cmp_lt_u32 %s, %s" % (s(S_T1), s(S_G)),
+            "s_cbranch_scc1 .Lsp_loop_%s" % tag,
+            "s_waitcnt vmcnt(0)",
+            "s_mov_b64 exec, %s" % sp(S_MASK),
+            "v_mul_u32_u24 %s, %s, %s" % (v(R[4]), s(S_SPAN), v(R[5])),
+            "v_add_u32 v%d, %s, %s" % (V_PKT, s(S_PKTLDS), v(R[4])),
+            "v_mov_b32 v%d, %s" % (V_PKT + 1, s(S_SHARED + 1)),
+            "s_branch .Lps_done_%s" % tag]
 
 
 def ret_slot_write(x0, x1):
@@ -1713,11 +1823,22 @@ def common_group_code():
           "s_lshl_b32 %s, 1, %s" % (s(S_KMASK), s(S_T1)),
           "s_sub_u32 %s, %s, 1" % (s(S_KMASK), s(S_KMASK)),
           "s_lshl_b32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_T1)),
+          ] + ([] if STAGED_IMAGE else [
+          # slot mode: ceil(n / G) groups (prologue)
+          "s_bitcmp1_b32 s7, 9",
+          "s_cselect_b32 %s, s83, %s" % (s(S_NGROUPS), s(S_NGROUPS))]) + [
           # superblock jump: (total waves - 1) * K' + 1
           "s_lshl_b32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_T1)),
           "s_sub_u32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_KMASK)),
           # this wave's packet buffer (staged kernel); first group's prefetch
           "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
+          ] + ([] if STAGED_IMAGE else [
+          # (span staging: G slots of S_SPAN bytes per wave)
+          "s_bitcmp1_b32 s7, 10",
+          "s_cbranch_scc0 .Lpk_std",
+          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_G), s(S_SPAN)),
+          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_WAVE)),
+          ".Lpk_std:"]) + [
           "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),
           "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgroup_check",
@@ -1743,6 +1864,24 @@ def common_group_code():
           ] + lane_index(H[0]) + [
           "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
+          ] + ([] if STAGED_IMAGE else [
+          # slot mode: slot group * G + lane (lanes < G), its packet perm[slot]; the other lanes
+          # get index ~0 (no result, no fault byte)
+          "s_bitcmp1_b32 s7, 9",
+          "s_cbranch_scc0 .Lgc_slots_done",
+          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_G)),
+          "v_add_u32 v%d, %s, %s" % (H[3], s(S_T0), v(H[0])),
+          "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_NSLOT), H[3]),
+          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_G), v(H[0])),
+          "s_and_b64 %s, %s, vcc" % (sp(S_ALIVE), sp(S_ALIVE)),
+          "v_lshlrev_b32 %s, 2, v%d" % (v(H[4]), H[3]),
+          "s_mov_b64 exec, %s" % sp(S_ALIVE),
+          "global_load_dword v%d, %s, %s" % (H[3], v(H[4]), sp(S_PERM)),
+          "s_waitcnt vmcnt(0)",
+          "s_not_b64 exec, %s" % sp(S_ALIVE),
+          "v_mov_b32 v%d, -1" % H[3],
+          "s_mov_b64 exec, -1",
+          ".Lgc_slots_done:"]) + [
           "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgs_general",
           # staged: this group's packets are (or are being) DMA'd into the packet buffer
@@ -2131,14 +2270,16 @@ def jit_templates():
 
 
 def main():
-    """gen_interp.py <staged.s> <general.s> <handlers.h>"""
-    out_s1, out_s0, out_h = sys.argv[1], sys.argv[2], sys.argv[3]
+    """gen_interp.py <staged.s> <general.s> <span.s> <handlers.h>"""
+    out_s1, out_s0, out_s2, out_h = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
     header = None
-    for out_s, k, staged in ((out_s1, RETK_STAGED, True), (out_s0, 1, False)):
+    global SPAN_IMAGE, NVGPR
+    for out_s, k, staged, span in ((out_s1, RETK_STAGED, True, False), (out_s0, 1, False, False),
+                                   (out_s2, 1, False, True)):
         set_retk(k)
+        SPAN_IMAGE = span
         if not staged:
-            global NVGPR
-            NVGPR += GEN_HOIST_REGS
+            NVGPR += SPAN_HOIST_REGS if span else GEN_HOIST_REGS
         h = generate(out_s, staged)
         header = header or h
         assert h[:-2] == header[:-2]   # identical but for the RETK-dependent lines
@@ -2146,7 +2287,9 @@ def main():
                             % RETK_STAGED,
                             "#define AH_NVGPR_STAGED %d" % (64 if RETK_STAGED == 1 else 64 + 2 * RETK_STAGED),
                             "#define AH_RET_GROUPS_GENERAL 1",
-                            "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS)]
+                            "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS),
+                            "#define AH_SPAN_HOIST_REGS %d  // span image: hoisted-load VGPRs from v64" % SPAN_HOIST_REGS,
+                            "#define AH_NVGPR_SPAN %d" % (64 + SPAN_HOIST_REGS)]
     with open(out_h, "w") as f:
         f.write("\n".join(header) + "\n")
 
@@ -2236,7 +2379,7 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
-    kernarg = 176
+    kernarg = 208
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
     ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),

@@ -12,6 +12,7 @@
 // Shared by host C++ and HIP device code: plain C layout, 32 bytes per entry.
 #pragma once
 #include <stdint.h>
+#include <stddef.h>
 
 enum dp_kind : uint16_t {
 	// 0x00..0xff: the eBPF opcode itself (ALU, ALU64, LDX, ST, STX, LDDW, cond jumps, EXIT)
@@ -127,8 +128,21 @@ struct dp_launch {
 	// the batch), set when the packet faults; the apply step skips a faulted packet's logged
 	// writes (a packet that faults leaves no write behind).  NULL for programs without map writes
 	uint32_t *upd_faulted;
+	// length-bucketed launches (general kernels; gen_interp.py "Length-bucketed launches"):
+	// this launch runs slots perm[perm_cls[0] .. perm_cls[0] + perm_cls[1]) (packet indices, both
+	// on the device: written by the bucketing kernels, bucket.hip), span_g per group; NULL = every
+	// packet, 64 per group.  span_slot != 0 (span image only): each packet is staged whole in
+	// LDS, span_slot bytes per lane (a multiple of 16 with an odd number of 16-B blocks)
+	const uint32_t *perm;
+	const uint32_t *perm_cls;
+	uint32_t span_slot;
+	uint32_t span_g;
+	uint32_t span_magic_g;    // ceil(2^32 / span_g)
+	uint32_t span_pad;
 };
-static_assert(sizeof(dp_launch) == 176, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 208, "dp_launch layout is shared with the assembly kernels");
+static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_slot) == 192,
+	      "gen_interp.py loads these fields at fixed offsets");
 
 // Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
 // EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B

@@ -70,7 +70,7 @@ enum : uint32_t {
 // DS opcodes (bits 24:17)
 enum : uint32_t {
 	DS_WRITE_B32 = 0x0d, DS_WRITE2_B32 = 0x0e, DS_WRITE_B8 = 0x1e, DS_WRITE_B16 = 0x1f,
-	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c,
+	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c, DS_READ_B128 = 0xff,
 };
 // VOPC compare codes: base + {lt 1, eq 2, le 3, gt 4, ne 5, ge 6}
 enum : uint32_t { VC_I32 = 0xc0, VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
@@ -816,6 +816,41 @@ struct emitter {
 		patch(to_end1);
 		patch(to_end2);
 	}
+	// z bytes at byte b of the 16-B block held in VGPRs base..base+3 (b + z <= 16) into d
+	void slot_extract(int d, int z, uint32_t b, int base)
+	{
+		const int k = (int)(b >> 2), sh = (int)(b & 3);
+		const int lo = base + k, nx = base + (k + 1 < 4 ? k + 1 : k);
+		if (z == 1) {
+			E.vop3(V3_BFE_U32, L(d), VGPR0 + lo, 128 + 8 * sh, 128 + 8);
+		} else if (z == 2) {
+			if (sh <= 2)
+				E.vop3(V3_BFE_U32, L(d), VGPR0 + lo, 128 + 8 * sh, 128 + 16);
+			else
+				E.vop3(V3_PERM_B32, L(d), VGPR0 + nx, VGPR0 + lo, sconst(0x0c0c0403u));
+		} else if (z == 4) {
+			if (sh == 0)
+				E.vop1(V1_MOV_B32, L(d), vreg(lo));
+			else
+				E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + nx, VGPR0 + lo, 128 + sh);
+		} else {
+			if (sh == 0) {
+				if ((lo & 1) == 0) {
+					E.vop1(V1_MOV_B64, L(d), vreg(lo));
+				} else {
+					E.vop1(V1_MOV_B32, L(d), vreg(lo));
+					E.vop1(V1_MOV_B32, Hi(d), vreg(lo + 1));
+				}
+			} else {
+				E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + lo + 1, VGPR0 + lo, 128 + sh);
+				E.vop3(V3_ALIGNBYTE, Hi(d), VGPR0 + lo + 2, VGPR0 + lo + 1, 128 + sh);
+			}
+			f.def(d, rf());
+			return;
+		}
+		hi0(d);
+		f.def(d, kbits(8 * z));
+	}
 	void ldxpkc(int d, int z, int off, int swap_bytes)
 	{
 		const int k = off >> 2, sh = off & 3;
@@ -1208,8 +1243,12 @@ struct emitter {
 	// With the run mask (s[76:77], see cc_compile) the lanes in the mask hold the load already
 	// and cannot fault on it; only when a running lane is outside the mask does the use compare:
 	// fault the lanes past their packet's end, load for the others directly (and wait for it).
+	//
+	// Span-staged launches (span: the packet is in LDS, asm_cc mode 2): the slot `tmp` holds the
+	// 16-B block of the packet that contains the load (ds_read_b128, one per hoisted load, waited
+	// for with lgkmcnt: LDS reads complete in order), and the value is extracted from it.
 	void ldx_hoisted(int d, int z, uint32_t off, int tmp, uint32_t later, uint32_t fault_off,
-			 bool runmask)
+			 bool runmask, bool span = false)
 	{
 		const int S_MASK = 48, S_CODE = 52, V_LEN = 40, S_JUNK_ = 60, V_PKT = 38;
 		size_t br = 0, from = 0;
@@ -1231,13 +1270,23 @@ struct emitter {
 			E.w(0xbf840000u | 6u);                                           // s_cbranch_scc0 +6
 			E.sop1(0x01, S_JUNK_, opnd{SRC_EXEC});                           // s_mov_b64 s60, exec
 			E.sop1(0x01, 126, opnd{(uint32_t)S_MASK});                       // s_mov_b64 exec, s48
-			E.w(0xdc008000u | (gop[zi] << 18) | off);                        // global_load_* tmp
-			E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)tmp << 24));
-			E.w(0xbf8c0f70u);                                                // s_waitcnt vmcnt(0)
+			if (span) {
+				E.ds(DS_READ_B128, V_PKT, 0, 0, tmp, off & ~15u);              // ds_read_b128 tmp
+				E.w(0xbf8cc07fu);                                            // s_waitcnt lgkmcnt(0)
+			} else {
+				E.w(0xdc008000u | (gop[zi] << 18) | off);                    // global_load_* tmp
+				E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)tmp << 24));
+				E.w(0xbf8c0f70u);                                            // s_waitcnt vmcnt(0)
+			}
 			E.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});                      // s_mov_b64 exec, s60
 			const uint32_t skip = (uint32_t)((E.b.size() - from) / 4);
 			E.b[br] = (uint8_t)skip;
 			E.b[br + 1] = (uint8_t)(skip >> 8);
+		}
+		if (span) {
+			E.w(0xbf8c0000u | 15u | (7u << 4) | ((later & 15u) << 8) | (3u << 14)); // lgkmcnt(later)
+			slot_extract(d, z, off & 15u, tmp);
+			return;
 		}
 		E.w(0xbf8c0000u | (later & 15u) | (7u << 4) | (15u << 8) | ((later >> 4) & 3u) << 14);
 		if (z == 8) {
@@ -1844,6 +1893,12 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	   const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 	   const std::vector<dp_map> &table, const std::vector<char> &regroup, std::vector<cc_block> &out)
 {
+	// mode 2: the general kernels of a span-staged launch (the packet is in LDS: its constant-
+	// offset loads are LDS reads, hoisted as one ds_read_b128 of the 16-B block each); otherwise
+	// compiled as mode 0
+	const bool span = mode == 2;
+	if (span)
+		mode = 0;
 	const size_t n = low.size();
 	std::vector<mapinfo> maps(table.size());
 	for (size_t i = 0; i < table.size(); i++)
@@ -1878,7 +1933,9 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 			     std::none_of(regroup.begin(), regroup.end(), [](char c) { return c != 0; }) &&
 			     getenv("EBPF_CC_NORUNMASK") == nullptr;
 	std::vector<uint32_t> run_ext(n, 0); // run head: the largest off + size of its hoisted loads
-	if (mode == 0 && AH_GEN_HOIST_REGS > 0 && getenv("EBPF_CC_NOHOIST") == nullptr) {
+	const int hoist_regs = span ? AH_SPAN_HOIST_REGS : AH_GEN_HOIST_REGS;
+	const int slot_regs = span ? 4 : 2;
+	if (mode == 0 && hoist_regs > 0 && getenv("EBPF_CC_NOHOIST") == nullptr) {
 		size_t k = 0;
 		while (k < order.size()) {
 			size_t j = k; // run [k, j]
@@ -1923,12 +1980,14 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				if (fam < AHF_LDXPKTG1 || fam > AHF_LDXPKTG8)
 					continue;
 				const int z = 1 << (fam - AHF_LDXPKTG1);
-				if (low[e].imm + (uint64_t)z > 4095)
+				if (low[e].imm + (uint64_t)z > (span ? 65535u : 4095u))
 					continue;
+				if (span && (low[e].imm & 15) + (uint64_t)z > 16)
+					continue; // (straddles two blocks: the handler's own LDS read)
 				ld.push_back(e);
 			}
 			if (ld.size() >= 2) {
-				const size_t slots = AH_GEN_HOIST_REGS / 2;
+				const size_t slots = (size_t)(hoist_regs / slot_regs);
 				size_t issued = std::min(slots, ld.size());
 				hoist_at[order[k]].assign(ld.begin(), ld.begin() + issued);
 				for (uint32_t x : ld)
@@ -1936,7 +1995,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					    run_ext[order[k]],
 					    (uint32_t)low[x].imm + (1u << (ah_fam[(uint32_t)low[x].handler] - AHF_LDXPKTG1)));
 				for (size_t i = 0; i < ld.size(); i++) {
-					hoist_tmp[ld[i]] = (int16_t)(AH_GEN_HOIST_BASE + 2 * (i % slots));
+					hoist_tmp[ld[i]] = (int16_t)(AH_GEN_HOIST_BASE + slot_regs * (i % slots));
 					hoist_later[ld[i]] = (uint16_t)(issued - 1 - i);
 					if (i + slots < ld.size()) {
 						hoist_next[ld[i]] = ld[i + slots];
@@ -2009,8 +2068,12 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					Hq.vopc(VC_U32 + P_LE, k32(K32 + (uint32_t)z), V_LEN); // vcc = off+z <= len
 					Hq.sop1(0x20, S_JUNK_, opnd{SRC_VCC});                  // s_and_saveexec_b64
 				}
-				Hq.w(0xdc008000u | (gop[fx - AHF_LDXPKTG1] << 18) | K32);  // global_load_*
-				Hq.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)hoist_tmp[x] << 24));
+				if (span) {
+					Hq.ds(DS_READ_B128, V_PKT, 0, 0, hoist_tmp[x], K32 & ~15u); // ds_read_b128
+				} else {
+					Hq.w(0xdc008000u | (gop[fx - AHF_LDXPKTG1] << 18) | K32);  // global_load_*
+					Hq.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)hoist_tmp[x] << 24));
+				}
 				if (!masked)
 					Hq.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});       // s_mov_b64 exec
 			};
@@ -2060,7 +2123,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = em.alu32i(movfuse_fam[e], d, (uint32_t)K, movfuse_src[e]);
 			} else if (hoist_tmp[e] >= 0) {
 				em.ldx_hoisted(d, 1 << (fam - AHF_LDXPKTG1), (uint32_t)K, hoist_tmp[e], hoist_later[e],
-					       rt.fault, runmask);
+					       rt.fault, runmask, span);
 				if (hoist_next[e] != UINT32_MAX)
 					issue(em.E, hoist_next[e]);
 			}

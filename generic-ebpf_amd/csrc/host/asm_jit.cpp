@@ -88,8 +88,8 @@ find_symbols(const unsigned char *img, size_t len, const char *const *names, siz
 const jit_image &
 image_info(int mode)
 {
-	static jit_image info[2];
-	static std::once_flag once[2];
+	static jit_image info[kModes];
+	static std::once_flag once[kModes];
 	std::call_once(once[mode], [mode] {
 		jit_image &I = info[mode];
 		const unsigned char *img = asm_image(mode);
@@ -156,6 +156,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	if (rq_wave_bytes)
 		*rq_wave_bytes = 0;
 	const uint32_t HDR = 16;
+	// mode 2 (span-staged general launches) compiles as mode 0 but for its packet loads (asm_cc)
+	const int gm = mode == 2 ? 0 : mode;
 	const jit_image &I = image_info(mode);
 	if (!I.ok) {
 		*err = I.why;
@@ -232,7 +234,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<uint32_t> cont(n, GROUP_END); // where a path through the entry continues
 	std::vector<int> jdepth(n, 0);            // pending branches (join masks in use)
 	std::vector<int> join_of(n, -1);          // entry e is the taken block of conditional k
-	bool structured = (mode == 1 || AH_GEN_JOIN) && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
+	bool structured = (gm == 1 || AH_GEN_JOIN) && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
 			  getenv("EBPF_JIT_NOCC") == nullptr;
 	for (uint32_t e : order) {
 		const uint32_t h = (uint32_t)low[e].handler;
@@ -282,7 +284,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<std::vector<uint8_t>> push(n);
 	uint32_t qbytes = 0;
 	if (mode == 0 && !structured && getenv("EBPF_JIT_NOCC") == nullptr)
-		cc_regroup_plan(xl, low, order, rg);
+		cc_regroup_plan(xl, low, order, rg); // (never in span launches: s78.. are theirs)
 	if (!rg.empty()) {
 		size_t slots = 0;
 		for (const cc_regroup_point &p : rg)
@@ -305,7 +307,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, regroup, cb);
 	else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
-		cc_prologue(mode, 0x7ff, true, false, cb[xl.start].prologue);
+		cc_prologue(gm, 0x7ff, true, false, cb[xl.start].prologue);
 	}
 	auto reads_of = [&](uint32_t e) -> uint8_t {
 		return cb[e].fast ? cb[e].reads : ah_reads[(uint32_t)low[e].handler];

@@ -16,6 +16,7 @@
 #include <functional>
 #include <thread>
 
+#include "bucket.h"
 #include "hist_ops.h"
 #include "internal.h"
 #include "map_writes.h"
@@ -30,6 +31,7 @@ int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_program_needs_general(const dprog_host &xl);
 bool asm_program_gstage(const dprog_host &xl);
+bool asm_program_span(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 // asm_jit.cpp
@@ -96,6 +98,9 @@ struct rows_slot {
 	// compiled programs with regroup points: the stream's queue buffer (any contents)
 	void *rq = nullptr;
 	size_t rq_bytes = 0;
+	// length-bucketed launches: perm, per-tile counts and the class table (bucket.h)
+	void *bk = nullptr;
+	size_t bk_bytes = 0;
 	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
 	// shard on the device (any contents: every launch overwrites its row), and fork/join events
 	void *mh = nullptr;
@@ -228,6 +233,20 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 	return 0;
 }
 
+// The stream's bucketing buffer (>= bytes, any contents).
+int
+bk_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		err = grow_zeroed(&r->bk, &r->bk_bytes, bytes);
+	if (!err)
+		*out = static_cast<uint8_t *>(r->bk);
+	return err;
+}
+
 // The stream's regroup queue buffer (>= bytes).
 int
 rq_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
@@ -316,6 +335,7 @@ ensure_translated(struct ebpf_prog *ep)
 	if (!x->error) {
 		x->asm_needs_general = asm_program_needs_general(*x);
 		x->asm_gstage = asm_program_gstage(*x);
+		x->asm_span = asm_program_span(*x);
 	}
 	ep->xlated = std::move(x);
 	if (ep->xlated->error)
@@ -578,6 +598,116 @@ upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t
 	return 0;
 }
 
+// Length-bucketed launch of a mixed-size batch (offsets form) of a compiled program that reads
+// past the packets' first 64 bytes (asm_program_span): bucket.hip sorts the packet indices into
+// length classes, then one launch per class runs the class's packets G per wave — class 0 (up to
+// 64 bytes, longer than the last class, or not 16-B aligned) on the general kernels, classes 1..
+// on the span-staged kernels (mode 2: each packet DMA'd whole into an LDS slot of `slot` bytes,
+// its loads LDS reads).  Every packet keeps its own result and fault slot (ret[i], faults[i]).
+// Returns 0 with *done set when it ran the batch; 0 with *done clear when the batch should run
+// as one plain launch instead (no span code, LDS too small); else an error.
+struct span_class {
+	uint32_t lim;  // longest packet of the class
+	uint32_t slot; // LDS bytes per packet (a multiple of 16, an odd count of 16-B blocks)
+};
+const span_class kSpanClasses[3] = {{64, 0}, {576, 592}, {1536, 1552}};
+constexpr uint64_t kBucketMin = 1u << 16;  // smaller batches: one plain launch
+constexpr uint64_t kBucketMax = 1u << 26;  // (the kernels' group-count division is exact below)
+
+bool
+bucket_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
+{
+	// opt-in (EBPF_BUCKET=1) until it beats the plain launch on C5
+	const char *on = getenv("EBPF_BUCKET");
+	return on && *on == '1' && L.offsets != nullptr && L.count >= kBucketMin && L.count < kBucketMax &&
+	       ep->xlated->asm_span && ep->xlated->max_updates == 0 && dp->jit_rq_bytes[0] == 0;
+}
+
+int
+launch_bucketed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
+		hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
+		bool *done)
+{
+	*done = false;
+	if (jit_entries(ep, dp, 2) != 0)
+		return 0; // (no span code for this program: the plain launch)
+	const uint32_t pkt_base = kMapLdsBase + dp->map_lds_bytes;
+	const uint32_t stack = 256 * std::max(dp->jit_stride[0], dp->jit_stride[2]);
+	if (pkt_base + stack >= 160 * 1024)
+		return 0;
+	// packets per group of each span class: as many slots as the LDS left by the stacks and
+	// maps holds (a program with generic memory accesses has the reference's 512-B stack per
+	// lane); a class that would get fewer than 8 is left out (its packets go to class 0, as
+	// "longer than the last class")
+	uint32_t nclass = 1;
+	uint32_t G[3] = {64, 0, 0};
+	// (EBPF_SPAN_WAVES=w: size G for w workgroups per CU; EBPF_SPAN_G<k>: force G of class k)
+	static const char *sw = getenv("EBPF_SPAN_WAVES");
+	const uint32_t wgs = sw && atoi(sw) > 0 ? (uint32_t)atoi(sw) : 1;
+	for (uint32_t k = 1; k < 3; k++) {
+		const uint32_t per_wg = 160 * 1024 / wgs;
+		if (per_wg <= pkt_base + stack)
+			break;
+		G[k] = std::min<uint32_t>(64, (per_wg - pkt_base - stack) / (4 * kSpanClasses[k].slot));
+		char nm[16];
+		snprintf(nm, sizeof(nm), "EBPF_SPAN_G%u", k);
+		if (const char *g = getenv(nm))
+			G[k] = std::min<uint32_t>((uint32_t)atoi(g), G[k]);
+		if (G[k] < 4)
+			break;
+		nclass = k + 1;
+	}
+	if (nclass == 1)
+		return 0;
+	uint32_t tile;
+	const uint32_t tiles = bucket_tiles(L.count, &tile);
+	const size_t perm_bytes = (L.count * 4 + 255) & ~(size_t)255;
+	const size_t blk_bytes = (size_t)kBucketMaxTiles * kBucketMaxClass * 4;
+	uint8_t *bk;
+	int err = bk_acquire(dp->device, stream, perm_bytes + blk_bytes + 256, &bk);
+	if (err)
+		return fail(err, "bucketing buffer");
+	bucket_args a;
+	memset(&a, 0, sizeof(a));
+	a.offsets = L.offsets;
+	a.off_base = L.off_base;
+	a.data = L.data;
+	a.count = L.count;
+	for (uint32_t k = 0; k < nclass; k++)
+		a.lim[k] = kSpanClasses[k].lim;
+	a.nclass = nclass;
+	a.tile = tile;
+	a.perm = reinterpret_cast<uint32_t *>(bk);
+	a.blk_cnt = reinterpret_cast<uint32_t *>(bk + perm_bytes);
+	a.cls = reinterpret_cast<uint32_t *>(bk + perm_bytes + blk_bytes);
+	hipError_t e;
+	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	if ((e = launch_bucket(a, tiles, stream)) != hipSuccess)
+		return hip_fail(e, "bucketing kernels");
+	for (uint32_t k = 0; k < nclass; k++) {
+		const int mode = k ? 2 : 0;
+		dp_launch Lk = L;
+		Lk.perm = a.perm;
+		Lk.perm_cls = a.cls + 2 * k;
+		Lk.span_slot = kSpanClasses[k].slot;
+		Lk.span_g = G[k];
+		Lk.span_magic_g = (uint32_t)((0x100000000ull + G[k] - 1) / G[k]);
+		Lk.stack_stride = dp->jit_stride[mode];
+		if (mode == 2)
+			Lk.lds_pkt_base = 0; // (no header staging: every load reads the LDS slot)
+		e = launch_interp_asm(Lk, stream, dp->device, mode, dp->map_lds_bytes, dp->jit_fn[mode], 0,
+				      nullptr, nullptr, user_hist, overwrite && k == 0);
+		if (e != hipSuccess)
+			return hip_fail(e, "length-class launch");
+	}
+	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	dp->last_layout = 2;
+	*done = true;
+	return 0;
+}
+
 int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false,
@@ -648,9 +778,15 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		bool probes = false;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
-		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-				      (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
-				      hist_overwrite);
+		bool done = false;
+		if (fn && mode == 0 && bucket_wanted(ep, dp, L) &&
+		    (err = launch_bucketed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
+					   &done)))
+			return err;
+		e = done ? hipSuccess
+			 : launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
+					     (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
+					     hist_overwrite);
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;
@@ -986,7 +1122,7 @@ ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *
 EBPF_EXPORT int
 ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 {
-	if (ep == nullptr || len == nullptr || (layout != 0 && layout != 1))
+	if (ep == nullptr || len == nullptr || layout < 0 || layout > 2)
 		return fail(EINVAL, "bad argument");
 	std::lock_guard<std::mutex> g(ep->dlock);
 	int err = ensure_translated(ep);

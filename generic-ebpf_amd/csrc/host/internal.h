@@ -99,12 +99,20 @@ constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 
-// The assembly interpreter's two code objects (build/asm_image.cpp): mode 1 = staged 64-B
-// kernels, mode 0 = general kernels.
-extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[];
-extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len;
-inline const unsigned char *asm_image(int mode) { return mode == 1 ? ebpf_asm_hsaco_m1 : ebpf_asm_hsaco_m0; }
-inline size_t asm_image_len(int mode) { return mode == 1 ? ebpf_asm_hsaco_m1_len : ebpf_asm_hsaco_m0_len; }
+// The assembly interpreter's three code objects (build/asm_image.cpp): mode 1 = staged 64-B
+// kernels, mode 0 = general kernels, mode 2 = general kernels of span-staged (length-bucketed)
+// launches, whose packets sit in LDS (compiled programs only).
+constexpr int kModes = 3;
+extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[];
+extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len;
+inline const unsigned char *asm_image(int mode)
+{
+	return mode == 1 ? ebpf_asm_hsaco_m1 : mode == 2 ? ebpf_asm_hsaco_m2 : ebpf_asm_hsaco_m0;
+}
+inline size_t asm_image_len(int mode)
+{
+	return mode == 1 ? ebpf_asm_hsaco_m1_len : mode == 2 ? ebpf_asm_hsaco_m2_len : ebpf_asm_hsaco_m0_len;
+}
 
 // Per (program, device): entries for each interpreter variant and the map table.
 struct dprog_device {
@@ -115,15 +123,15 @@ struct dprog_device {
 	uint32_t nentries = 0;
 	uint32_t nmaps = 0;
 	uint32_t map_lds_bytes = 0;      // LDS bytes taken by LDS-resident map copies (asm kernels)
-	dp_entry *d_asm[2] = {nullptr, nullptr}; // variant 0: lowered + linked, per mode
-	uint32_t asm_stride[2] = {0, 0};         // LDS stack bytes per lane, per mode
-	int asm_err[2] = {0, 0};
-	void *jit_mod[2] = {nullptr, nullptr};   // variant 0: compiled program module, per mode
-	void *jit_fn[2] = {nullptr, nullptr};    // its kernel
-	uint32_t jit_stride[2] = {0, 0};
-	uint32_t jit_rq_bytes[2] = {0, 0};      // regroup queue bytes per wave (0: none)
-	int jit_err[2] = {0, 0};                 // E2BIG etc.: run the interpreter instead
-	double build_ms[2] = {0, 0};             // compile (variant 0) or lower + link time, per mode
+	dp_entry *d_asm[kModes] = {};            // variant 2: lowered + linked, per mode
+	uint32_t asm_stride[kModes] = {};        // LDS stack bytes per lane, per mode
+	int asm_err[kModes] = {};
+	void *jit_mod[kModes] = {};              // variant 0: compiled program module, per mode
+	void *jit_fn[kModes] = {};               // its kernel
+	uint32_t jit_stride[kModes] = {};
+	uint32_t jit_rq_bytes[kModes] = {};      // regroup queue bytes per wave (0: none)
+	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
+	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
 	uint64_t win_words = 0;                  // winner words the apply step needs
 	uint32_t upd_stride = 0;                 // log record bytes
@@ -162,6 +170,7 @@ struct dprog_host {
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
+	bool asm_span = false;               // length-bucketed launches pay (asm_program_span)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
 	uint32_t max_updates = 0;            // most map_update_elem calls on one path (0: none)
