@@ -1,4 +1,4 @@
-export TMPDIR=/tmp
+export TMPDIR=/tmp EBPF_BUCKET=1
 mkdir -p gpurun_out/r03e
 for w in 1 2 4; do
   for e in "" ; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the bucketed C5 launch (one rocprofv3 --pmc run per counter group, kernel trace
 # only besides): per-dispatch counters of the ebpf kernels, for tools/pmc_classes.py.
-export TMPDIR=/tmp
+export TMPDIR=/tmp EBPF_BUCKET=1
 O=gpurun_out/${TAG:-pmcspan}
 mkdir -p $O
 i=0
