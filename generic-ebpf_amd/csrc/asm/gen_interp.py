@@ -223,6 +223,11 @@ for c in CONDS:
     fam("J32" + c[1:] + "_R", 2)
 for c in CONDS:
     fam("J32" + c[1:] + "_I", 1)
+# loops under standard semantics (dprog.h DK_LOOPINIT / DK_LOOPCNT): the lane's count of taken
+# backward jumps in the first 4 bytes of its stack slice (below the frame the program addresses)
+fam("LOOPINIT", 0)
+fam("LOOPCNT", 0)
+LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 
 
 def variants(arity):
@@ -1142,6 +1147,18 @@ def handler_body(name, d, sr):
         return call(".Lr_hlookup"), False
     if name == "UPDATE":
         return call(".Lr_update"), False
+    if name == "LOOPINIT":
+        return ["v_mov_b32 %s, 0" % v(H[0]), "ds_write_b32 v%d, %s" % (V_STK, v(H[0]))], False
+    if name == "LOOPCNT":
+        # count the taken backward jump; lanes past the budget fault LOOP (EBPF_FAULT_LOOP = 8)
+        return ["ds_read_b32 %s, v%d" % (v(H[0]), V_STK),
+                "s_waitcnt lgkmcnt(0)",
+                "v_add_u32 %s, 1, %s" % (v(H[0]), v(H[0])),
+                "ds_write_b32 v%d, %s" % (V_STK, v(H[0])),
+                "v_cmp_lt_u32_e32 vcc, %d, %s" % (LOOP_BUDGET, v(H[0])),
+                "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+                "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+                "s_cbranch_scc1 .Lok_{uid}"] + fault_mask(S_MASK, 8) + [".Lok_{uid}:"], False
     raise ValueError(name)
 
 

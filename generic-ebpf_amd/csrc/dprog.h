@@ -35,7 +35,15 @@ enum dp_kind : uint16_t {
 	// map-writing helpers (device-batch semantics, ebpf_gpu.h "Map writes in a device batch");
 	// the map is a translation-time constant: aux = its index in the dp_map table
 	DK_CALL_UPDATE = 0x10d, // r0 = map_update_elem(map, r2, r3, r4) (ebpf_map.c:101-108)
+	// Loops (standard semantics only; the reference's state graph is a tree): every taken
+	// backward jump (a jump whose target is at or before its own slot) passes a LOOPCNT entry
+	// that counts it for the lane; the (DP_LOOP_BUDGET + 1)-th faults EBPF_FAULT_LOOP.  The
+	// program starts at a LOOPINIT entry (the lane's count = 0).  The count lives in the first
+	// 4 bytes of the lane's stack slice, below the frame the program can address.
+	DK_LOOPINIT = 0x10e,
+	DK_LOOPCNT = 0x10f,
 };
+#define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
 
 struct dp_entry {

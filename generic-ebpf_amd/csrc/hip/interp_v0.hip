@@ -136,6 +136,7 @@ ebpf_interp_v0(dp_launch L)
 	bool active = live;
 	int fault = F_NONE;
 	uint64_t result = 0;
+	uint32_t back = 0; // taken backward jumps (DK_LOOPCNT, standard semantics)
 
 	for (;;) {
 		const uint64_t am = __ballot(active);
@@ -161,6 +162,17 @@ ebpf_interp_v0(dp_launch L)
 		if (k == 0x95) { // EXIT
 			result = R[0][tid];
 			active = false;
+			continue;
+		}
+		if (k == DK_LOOPINIT) {
+			back = 0;
+			continue;
+		}
+		if (k == DK_LOOPCNT) {
+			if (++back > DP_LOOP_BUDGET) {
+				fault = F_LOOP;
+				active = false;
+			}
 			continue;
 		}
 		if (k == DK_CALL_LOOKUP) {

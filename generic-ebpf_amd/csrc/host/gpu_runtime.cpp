@@ -739,8 +739,11 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
 		// variant 0: the compiled program; a program too large for the code area runs on the
 		// assembly interpreter instead (still the device path)
+		// (a program with loops runs on the interpreter: the code generator's liveness and
+		// facts assume an acyclic graph)
 		void *fn = nullptr;
-		if (variant == 0 && (err = jit_entries(ep, dp, mode)) == 0) {
+		const bool compile = variant == 0 && !ep->xlated->has_loops;
+		if (compile && (err = jit_entries(ep, dp, mode)) == 0) {
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];
 			fn = dp->jit_fn[mode];
@@ -751,7 +754,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 				L.rq_wave_bytes = dp->jit_rq_bytes[mode];
 			}
 		} else {
-			if (variant == 0 && err != E2BIG)
+			if (compile && err != E2BIG)
 				return err;
 			if ((err = asm_entries(ep, dp, mode)))
 				return err;

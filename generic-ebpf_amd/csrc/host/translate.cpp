@@ -68,6 +68,7 @@ struct Translator {
 	std::unordered_map<uint64_t, uint32_t> state_id;
 	uint32_t fault_id[EBPF_FAULT_MAX];
 	std::vector<std::pair<uint32_t, uint64_t>> pending; // (entry, state) to fill
+	std::vector<std::pair<uint32_t, uint64_t>> loop_next; // (LOOPCNT entry, state it leads to)
 	bool overflow = false;
 	bool std_mode = false; // EBPF_SEM_STANDARD: sequential pc, the state is the slot alone
 
@@ -104,6 +105,17 @@ struct Translator {
 		return fault_id[code];
 	}
 
+	// A taken backward jump to slot `idx` (standard semantics): a LOOPCNT entry on the edge,
+	// which counts the jump and continues at the target's entry (resolved in run()).
+	uint32_t loop_edge(uint64_t idx)
+	{
+		const uint32_t id = new_entry();
+		out.entries[id].kind = DK_LOOPCNT;
+		loop_next.push_back({id, key(idx, 0)});
+		out.has_loops = true;
+		return id;
+	}
+
 	// Entry for state (idx, pc), following JA chains.  New states are queued for filling.
 	uint32_t get(uint64_t idx, uint32_t pc, bool *created)
 	{
@@ -126,6 +138,10 @@ struct Translator {
 				const uint64_t nidx = idx + 1 + (uint64_t)(int64_t)in.offset;
 				if (nidx == idx) {
 					id = fault(EBPF_FAULT_LOOP);
+					break;
+				}
+				if (in.offset < 0) { // a backward JA: counted
+					id = loop_edge(nidx);
 					break;
 				}
 				idx = nidx;
@@ -336,6 +352,9 @@ struct Translator {
 				if (tidx == idx && tpc == pc) {
 					uint32_t f = fault(EBPF_FAULT_LOOP); // may grow entries: no `e` after this
 					out.entries[id].target = f;
+				} else if (std_mode && in.offset < 0) {
+					const uint32_t c = loop_edge(tidx); // (grows entries too)
+					out.entries[id].target = c;
 				} else {
 					deferred_taken.push_back(key(tidx, tpc));
 					deferred_taken_entry.push_back(id);
@@ -359,7 +378,7 @@ struct Translator {
 		out.start = get(0, 1, &created);
 		std::vector<uint64_t> dt;
 		std::vector<uint32_t> dte;
-		size_t pi = 0, di = 0;
+		size_t pi = 0, di = 0, li = 0;
 		while (!overflow) {
 			// pending entries are processed in creation order; a straight run is filled
 			// eagerly so fallthrough successors get consecutive indices.
@@ -371,12 +390,25 @@ struct Translator {
 				fill(id, k >> 32, (uint32_t)k, dt, dte, &nn);
 				continue;
 			}
+			if (li < loop_next.size()) {
+				const uint32_t from = loop_next[li].first;
+				const uint64_t k = loop_next[li].second;
+				li++;
+				out.entries[from].next = get(k >> 32, (uint32_t)k, &created);
+				continue;
+			}
 			if (di >= dt.size())
 				break;
 			uint64_t k = dt[di];
 			uint32_t from = dte[di];
 			di++;
 			out.entries[from].target = get(k >> 32, (uint32_t)k, &created);
+		}
+		if (!overflow && out.has_loops) { // every lane's loop count starts at 0
+			const uint32_t init = new_entry();
+			out.entries[init].kind = DK_LOOPINIT;
+			out.entries[init].next = out.start;
+			out.start = init;
 		}
 		if (overflow) {
 			out.error = E2BIG;
@@ -444,6 +476,8 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		r[0] = av();
 		return;
 	}
+	if (k == DK_LOOPINIT || k == DK_LOOPCNT)
+		return;
 	const uint8_t cls = k & 7;
 	if (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32 || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
 		return;
@@ -547,50 +581,6 @@ dataflow(dprog_host &out)
 	}
 }
 
-// Any cycle in the entry graph (standard semantics only: the reference's state graph is a tree).
-bool
-has_cycle(const dprog_host &x)
-{
-	const size_t n = x.entries.size();
-	std::vector<uint8_t> color(n, 0); // 0 new, 1 on the stack, 2 done
-	std::vector<std::pair<uint32_t, int>> st;
-	auto succ = [&](uint32_t e, int k) -> uint32_t {
-		const dp_entry &d = x.entries[e];
-		if (d.kind == DK_FAULT || d.kind == EBPF_OP_EXIT)
-			return UINT32_MAX;
-		if (k == 0)
-			return d.next;
-		const uint8_t cls = d.kind & 7;
-		if (d.kind < 0x100 && (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32))
-			return d.target;
-		return UINT32_MAX;
-	};
-	for (uint32_t r = 0; r < n; r++) {
-		if (color[r])
-			continue;
-		st.push_back({r, 0});
-		color[r] = 1;
-		while (!st.empty()) {
-			auto &top = st.back();
-			if (top.second >= 2) {
-				color[top.first] = 2;
-				st.pop_back();
-				continue;
-			}
-			const uint32_t s = succ(top.first, top.second++);
-			if (s >= n)
-				continue;
-			if (color[s] == 1)
-				return true;
-			if (color[s] == 0) {
-				color[s] = 1;
-				st.push_back({s, 0});
-			}
-		}
-	}
-	return false;
-}
-
 } // namespace
 
 int
@@ -603,12 +593,6 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	int err = t.run();
 	if (err)
 		return err;
-	if (std_sem && has_cycle(out)) {
-		out.error = EOPNOTSUPP;
-		out.error_msg = "device batches run loop-free standard-eBPF programs only (the program "
-				"has a backward jump cycle; run it with ebpf_prog_run)";
-		return EOPNOTSUPP;
-	}
 
 	// Resolve LDDW immediates that are live maps of this env: the device map table.
 	struct ebpf_env *ee = ep->eo.eo_ee;
@@ -736,8 +720,18 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		    std::find(out.upd_maps.begin(), out.upd_maps.end(), (uint16_t)mi) == out.upd_maps.end())
 			out.upd_maps.push_back((uint16_t)mi); // (a hashtable's update faults instead)
 	}
+	// a map write inside a loop has no per-packet bound for the batch's write log
+	if (out.has_loops)
+		for (size_t i = 0; i < out.entries.size(); i++)
+			if (out.entries[i].kind == DK_CALL_UPDATE && out.annot[i].reached) {
+				out.error = EOPNOTSUPP;
+				out.error_msg = "device batches run map_update_elem only in loop-free programs "
+						"(run this one with ebpf_prog_run)";
+				out.maps.clear();
+				return EOPNOTSUPP;
+			}
 	// most update calls on one path from the start (the graph is a tree under the reference's
-	// stepping, a DAG under standard semantics): the per-packet bound of the write log
+	// stepping, a DAG under loop-free standard semantics): the per-packet bound of the write log
 	{
 		const size_t n = out.entries.size();
 		std::vector<uint32_t> best(n, 0);

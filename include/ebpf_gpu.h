@@ -62,7 +62,8 @@ enum ebpf_fault {
 	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation (incl. map writes
 	                                      to a hashtable: see "Map writes in a device batch") */
 	EBPF_FAULT_BAD_REG = 7,      /* dst/src register nibble >= 11 (reference overflows reg[]) */
-	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns */
+	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns;
+	                                standard semantics: the loop budget is spent (see below) */
 	EBPF_FAULT_MAP_WRITE = 9,    /* store into map value memory through a lookup result (values
 	                                change only through map_update_elem during a batch) */
 	EBPF_FAULT_BAD_MAP = 10,     /* map helper called with r1 not a map of this program's env */
@@ -215,8 +216,12 @@ int ebpf_gpu_time_next_launch(void *start_event, void *stop_event);
  *   EBPF_SEM_STANDARD: standard eBPF as compilers emit it: sequential pc (a jump goes to
  *       pc + 1 + off), MOV64 moves (imm sign-extended), NEG/NEG64 negate dst, arithmetic ARSH,
  *       DIV by zero gives 0 and MOD by zero leaves dst (32-bit ops: truncated), and the JMP32
- *       class (opcode class 0x06, compares of the low 32 bits).  Device batches accept
- *       loop-free programs (EOPNOTSUPP otherwise); ebpf_prog_run runs any.
+ *       class (opcode class 0x06, compares of the low 32 bits).  Loops: in a device batch a
+ *       packet may take 2^20 backward jumps (taken jumps whose target is at or before their own
+ *       slot); the next one stops it with EBPF_FAULT_LOOP.  Programs with loops run on the
+ *       assembly interpreter (variant 0 compiles loop-free programs only); a map_update_elem in
+ *       a program with loops makes the batch functions return EOPNOTSUPP.  ebpf_prog_run runs
+ *       any program unbounded.
  * Applies to ebpf_prog_run and to device batches.  Returns 0, EINVAL (bad argument) or EBUSY
  * (the program was already translated for a device). */
 #define EBPF_SEM_REFERENCE 0

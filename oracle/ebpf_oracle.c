@@ -584,8 +584,10 @@ done:
  * dst (32-bit: truncated), the JMP32 class comparing the low 32 bits.  Everything else (memory
  * regions, helpers, LDDW, byte swaps, masked shift counts, fault codes) as in run_ref.
  * No reference implementation exists to pin this against: it is pinned
- * by hand-computed known-answer tests (tests/test_standard.py).  A program still running after
- * 1M instructions is stopped with F_LOOP. */
+ * by hand-computed known-answer tests (tests/test_standard.py).  Loops: a lane may take
+ * 2^20 backward jumps (taken, off < 0: the target is at or before the jump's own slot); the
+ * next one faults F_LOOP (the device's budget, dprog.h DP_LOOP_BUDGET: the packet's run has no
+ * other bound there). */
 static uint64_t
 run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
 	uint64_t *steps_out)
@@ -593,7 +595,7 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	uint64_t reg[11];
 	uint8_t stack[STACK_BYTES];
 	struct region_env re;
-	uint64_t pc = 0, steps = 0, r0 = 0;
+	uint64_t pc = 0, steps = 0, r0 = 0, back = 0;
 	int fault = F_NONE;
 
 	if (checked)
@@ -613,10 +615,7 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			fault = F_SLOT;
 			break;
 		}
-		if (++steps > 1000000) {
-			fault = F_LOOP;
-			break;
-		}
+		steps++;
 		const uint8_t *ip = p->insns + pc * 8;
 		uint8_t op = ip[0];
 		uint8_t d = ip[1] & 0x0f, s = ip[1] >> 4;
@@ -802,6 +801,10 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			break;
 		if (taken > 0) {
 			int64_t npc = (int64_t)pc + off;
+			if (off < 0 && ++back > (1u << 20)) {
+				fault = F_LOOP;
+				break;
+			}
 			if (npc < 0) {
 				fault = F_SLOT;
 				break;

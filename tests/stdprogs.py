@@ -189,3 +189,70 @@ def gen_program(seed, length=40, with_map=False):
         items.append(("label", lab))
     items.append(I("exit"))
     return asm(items)
+
+
+# Loops (standard semantics): every taken backward jump counts against the lane's budget of
+# 2^20 (dprog.h DP_LOOP_BUDGET, oracle run_std); the next one faults LOOP (8).
+LOOP_BUDGET = 1 << 20
+
+
+def countdown(n):
+    """r2 = n; do { r0 += r2; r2 -= 1 } while (r2 != 0): n - 1 taken backward jumps, r0 = the
+    sum 1..n."""
+    return asm([I("mov64_imm", 0, imm=0), ("lddw", 2, n), ("label", "L"),
+                I("add64_reg", 0, 2), I("sub64_imm", 2, imm=1),
+                I("jne_imm", 2, imm=0, off="L"), I("exit")])
+
+
+def gen_loop_program(seed, length=30, forever_every=0):
+    """A standard program with counted loops: a loop-free prefix (gen_program's ops), then 1-2
+    loops (one nested sometimes) whose trip counts come from packet bytes (1-16: lanes diverge),
+    with random ALU ops and a forward branch inside the bodies; one loop's exit is a JA back
+    edge variant.  forever_every = k > 0: packets whose byte 3 is a multiple of k loop forever
+    (a JA back edge that nothing breaks) and fault LOOP at the budget."""
+    g = np.random.default_rng(seed)
+    regs = [0, 3, 4, 7, 8, 9]
+    items = [I("mov64_reg", 6, 1)]
+    for r in regs:
+        items.append(I("mov64_imm", r, imm=int(g.integers(-2**31, 2**31))))
+    alu = ["add", "sub", "mul", "or", "and", "lsh", "rsh", "xor", "arsh"]
+
+    def body(k, tag):
+        out = []
+        for j in range(k):
+            d = int(g.choice(regs))
+            name = alu[int(g.integers(0, len(alu)))]
+            w = "64" if g.random() < 0.6 else ""
+            if g.random() < 0.5:
+                out.append(I(name + w + "_imm", d, imm=int(g.integers(-40, 40))))
+            else:
+                out.append(I(name + w + "_reg", d, int(g.choice(regs))))
+            if j == k // 2:    # a forward branch inside the body
+                out += [I("jgt_imm", d, imm=int(g.integers(0, 2**20)), off="S" + tag),
+                        I("xor64_imm", 0, imm=int(g.integers(1, 1000))), ("label", "S" + tag)]
+        return out
+
+    nloops = 1 + int(g.random() < 0.6)
+    for li in range(nloops):
+        tag = "%d" % li
+        off = int(g.integers(0, 60))
+        items += [I("ldxb", 5, 6, off), I("and64_imm", 5, imm=15), I("add64_imm", 5, imm=1),
+                  ("label", "L" + tag)]
+        items += body(int(g.integers(2, 8)), tag + "a")
+        if li == 0 and nloops == 2 and g.random() < 0.5:   # nested inner loop on r2
+            items += [I("ldxb", 2, 6, int(g.integers(0, 60))), I("and64_imm", 2, imm=3),
+                      I("add64_imm", 2, imm=1), ("label", "N"),
+                      I("add64_reg", 0, 2), I("sub64_imm", 2, imm=1),
+                      I("jne_imm", 2, imm=0, off="N")]
+        items += [I("add64_reg", 0, 5), I("sub64_imm", 5, imm=1)]
+        if g.random() < 0.5:
+            items.append(I("jne_imm", 5, imm=0, off="L" + tag))
+        else:   # exit test forward, JA back
+            items += [I("jeq_imm", 5, imm=0, off="E" + tag), I("ja", off="L" + tag),
+                      ("label", "E" + tag)]
+    if forever_every:
+        items += [I("ldxb", 2, 6, 3), I("mod64_imm", 2, imm=forever_every),
+                  I("jne_imm", 2, imm=0, off="F"), ("label", "H"), I("add64_imm", 0, imm=1),
+                  I("ja", off="H"), ("label", "F")]
+    items += [I("xor64_reg", 0, int(g.choice(regs))), I("exit")]
+    return asm(items)

@@ -80,3 +80,39 @@ def test_full_size_random_program(gpu, env, variant):
                          64, variant)
     assert not gf.any()
     np.testing.assert_array_equal(got.reshape(tiles, distinct), np.broadcast_to(want, (tiles, distinct)))
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("extra,fault", [(0, 0), (1, 8)])
+def test_loop_budget_on_device(gpu, env, variant, extra, fault):
+    """2^20 taken backward jumps run to EXIT, the next one faults LOOP (dprog.h DP_LOOP_BUDGET;
+    oracle run_std; the same hand count as tests/test_standard.py)."""
+    n = stdprogs.LOOP_BUDGET + 1 + extra
+    code, rel = stdprogs.countdown(n)
+    pk = np.zeros((64, 64), dtype=np.uint8)
+    got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), 64, 64, variant)
+    assert (gf == fault).all()
+    assert (got == (0 if fault else n * (n + 1) // 2)).all()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_loop_programs_vs_oracle(gpu, env, variant):
+    """Random programs with counted loops (data-dependent trip counts, nested loops, JA and
+    conditional back edges, forward branches inside the bodies); every 8th also has packets that
+    loop forever and fault LOOP at the budget.  Staged (64 B) and general (72 B) kernels."""
+    bad = []
+    for seed in range(24):
+        forever = 97 if seed % 8 == 0 else 0
+        code, rel = stdprogs.gen_loop_program(9000 + seed, forever_every=forever)
+        g = np.random.default_rng(seed)
+        stride = 64 if seed % 2 == 0 else 72
+        n = 2048
+        pk = g.integers(0, 256, (n, stride), dtype=np.uint8)
+        want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(
+            pk.reshape(-1), n, stride, nthreads=8)
+        if forever:
+            assert (wf == 8).any()
+        got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), n, stride, variant)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad.append((seed, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
+    assert not bad, bad

@@ -109,9 +109,9 @@ def test_device_translation_compiles(native, env, seed):
         p.destroy()
 
 
-def test_device_rejects_loops_cpu_runs_them(native, env):
+def test_device_accepts_loops_cpu_runs_them(native, env):
     """A bounded loop (r0 = 0; r2 = 5; do r0 += r2 while --r2 != 0): 15 on the CPU path; the
-    device refuses programs with cycles (EOPNOTSUPP)."""
+    device translation accepts it (its backward jump is counted: dprog.h DK_LOOPCNT)."""
     I = stdprogs.I
     code, _ = stdprogs.asm([I("mov64_imm", 0, imm=0), I("mov64_imm", 2, imm=5), ("label", "L"),
                             I("add64_reg", 0, 2), I("sub64_imm", 2, imm=1),
@@ -120,9 +120,36 @@ def test_device_rejects_loops_cpu_runs_them(native, env):
     try:
         p.set_semantics(native.SEM_STANDARD)
         assert p.run_cpu(stdprogs.PKT)[0] == 15
-        i = native.DprogInfo()
-        import ctypes
-        assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == errno.EOPNOTSUPP
-        assert "loop-free" in native.last_error()
+        p.info()
+    finally:
+        p.destroy()
+
+
+@pytest.mark.parametrize("extra,fault", [(0, 0), (1, 8)])
+def test_oracle_loop_budget(extra, fault):
+    """The budget: 2^20 taken backward jumps run, the next one faults LOOP (hand count: the
+    countdown from n takes n - 1 backward jumps and sums 1..n)."""
+    n = stdprogs.LOOP_BUDGET + 1 + extra
+    code, rel = stdprogs.countdown(n)
+    want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(
+        np.zeros(64, np.uint8), 1, 64)
+    assert int(wf[0]) == fault
+    assert int(want[0]) == (0 if fault else n * (n + 1) // 2)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_loop_programs_oracle_vs_cpu_path(native, env, seed):
+    """Random counted-loop programs (no packet loops forever): the oracle's run_std and the CPU
+    ebpf_prog_run agree."""
+    code, rel = stdprogs.gen_loop_program(7000 + seed)
+    pk = np.random.default_rng(seed).integers(0, 256, (32, 64), dtype=np.uint8)
+    want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(pk.reshape(-1), 32, 64)
+    assert not wf.any()
+    p = native.Prog(env, code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        for i in range(len(pk)):
+            assert p.run_cpu(pk[i].tobytes())[0] == int(want[i]), i
+        p.info()
     finally:
         p.destroy()
