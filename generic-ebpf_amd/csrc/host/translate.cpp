@@ -683,6 +683,73 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		if (grew)
 			dataflow(out);
 	}
+	// Map-writing helpers whose map is known only at run time (r1 not a translation-time
+	// constant of the map table): a compare chain on r1 as for lookups, one 64-bit JEQ per map of the table taken
+	// into a copy of the call with that map known; when none matches, the reference's argument
+	// checks come first (ebpf_map.c:101-108: em, key or value NULL, or flags > EBPF_EXIST ->
+	// EINVAL; delete :130-136: em or key NULL -> EINVAL), then the call dereferences a pointer
+	// that is not a map of this env: EBPF_FAULT_BAD_MAP.
+	{
+		const size_t n0 = out.entries.size();
+		bool grew = false;
+		for (size_t i = 0; i < n0; i++) {
+			if (out.entries[i].kind != DK_CALL_UPDATE || !out.annot[i].reached)
+				continue;
+			const av &r1 = out.annot[i].in[1];
+			if (r1.kind == AV_CONST &&
+			    std::any_of(out.maps.begin(), out.maps.end(), [&](const struct ebpf_map *m) {
+				    return (uint64_t)r1.off == (uint64_t)(uintptr_t)m;
+			    }))
+				continue; // (resolved below)
+			const dp_entry call = out.entries[i];
+			const bool del = call.aux == 1;
+			auto add = [&](const dp_entry &x) {
+				out.entries.push_back(x);
+				return (uint32_t)(out.entries.size() - 1);
+			};
+			dp_entry x;
+			memset(&x, 0, sizeof(x));
+			x.kind = EBPF_OP_LDDW; // r0 = EINVAL, then the call's successor
+			x.imm = EINVAL;
+			x.next = call.next;
+			const uint32_t einval = add(x);
+			memset(&x, 0, sizeof(x));
+			x.kind = DK_FAULT;
+			x.aux = EBPF_FAULT_BAD_MAP;
+			uint32_t chain = add(x);
+			auto cmp = [&](uint16_t kind, uint8_t reg, uint64_t imm, uint32_t taken, uint32_t next) {
+				dp_entry j;
+				memset(&j, 0, sizeof(j));
+				j.kind = kind;
+				j.dst = reg;
+				j.imm = imm;
+				j.target = taken;
+				j.next = next;
+				return add(j);
+			};
+			if (!del)
+				chain = cmp(EBPF_OP_JGT_IMM, EBPF_R4, EBPF_EXIST, einval, chain);
+			if (!del)
+				chain = cmp(EBPF_OP_JEQ_IMM, EBPF_R3, 0, einval, chain);
+			chain = cmp(EBPF_OP_JEQ_IMM, EBPF_R2, 0, einval, chain);
+			chain = cmp(EBPF_OP_JEQ_IMM, EBPF_R1, 0, einval, chain);
+			for (size_t m = out.maps.size(); m-- > 0;)
+				chain = cmp(EBPF_OP_JEQ_IMM, EBPF_R1, (uint64_t)(uintptr_t)out.maps[m], add(call),
+					    chain);
+			out.entries[i] = out.entries[chain]; // the first compare takes the call's place
+			out.entries[chain].kind = DK_FAULT;   // (its copy is unreachable)
+			out.entries[chain].aux = EBPF_FAULT_SLOT;
+			grew = true;
+		}
+		if (out.entries.size() >= kMaxEntries) {
+			out.error = E2BIG;
+			out.error_msg = "program state graph exceeds the device translation limit";
+			out.maps.clear();
+			return E2BIG;
+		}
+		if (grew)
+			dataflow(out);
+	}
 	// Map-writing helpers: the map must be a translation-time constant of the table.  delete
 	// on an array map is EINVAL whatever its arguments (ebpf_map.c delete -> ebpf_map_array.c:
 	// 246-250): a constant; on a hashtable it has no device form.  update keeps its entry,
@@ -697,17 +764,33 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 			for (size_t m = 0; m < out.maps.size(); m++)
 				if ((uint64_t)m1.off == (uint64_t)(uintptr_t)out.maps[m])
 					mi = (int)m;
-		if (mi < 0) {
-			out.error = EOPNOTSUPP;
-			out.error_msg = "device batches need the map of every map_update_elem / "
-					"map_delete_elem known at translation time (r1 loaded by LDDW)";
-			out.maps.clear();
-			return EOPNOTSUPP;
+		if (mi < 0) { // (a constant that is not a map of the table)
+			e.kind = DK_FAULT;
+			e.aux = EBPF_FAULT_BAD_MAP;
+			continue;
 		}
 		if (e.aux == 1) { // delete
 			if (out.maps[mi]->is_hashtable()) {
-				e.kind = DK_FAULT;
-				e.aux = EBPF_FAULT_HELPER_UNSUPPORTED;
+				// a NULL key is EINVAL before the map is touched (ebpf_map.c:130-136)
+				dp_entry j, a, f;
+				memset(&j, 0, sizeof(j));
+				memset(&a, 0, sizeof(a));
+				memset(&f, 0, sizeof(f));
+				a.kind = EBPF_OP_LDDW;
+				a.imm = EINVAL;
+				a.next = e.next;
+				f.kind = DK_FAULT;
+				f.aux = EBPF_FAULT_HELPER_UNSUPPORTED;
+				j.kind = EBPF_OP_JEQ_IMM;
+				j.dst = EBPF_R2;
+				j.imm = 0;
+				out.entries.push_back(a);
+				j.target = (uint32_t)(out.entries.size() - 1);
+				out.entries.push_back(f);
+				j.next = (uint32_t)(out.entries.size() - 1);
+				out.entries[i] = j; // (no reference into entries is held across the pushes)
+				out.annot.resize(out.entries.size());
+				out.annot[j.target] = out.annot[j.next] = out.annot[i];
 			} else {
 				e.kind = EBPF_OP_LDDW;
 				e.dst = 0;

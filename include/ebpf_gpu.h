@@ -43,10 +43,13 @@ struct ebpf_map;
  *     write of a key wins; a packet that faults (any code, even after its writes) leaves no
  *     write behind;
  *   - map_delete_elem on an array map returns EINVAL (ebpf_map_array.c:246-250);
- *   - on a hashtable map both helpers fault EBPF_FAULT_HELPER_UNSUPPORTED;
- *   - the map of every write must be known at translation time (r1 loaded by LDDW), else the
- *     batch functions return EOPNOTSUPP; a writing program runs its batch on one device
- *     (the multi-device calls return EOPNOTSUPP).
+ *   - on a hashtable map both helpers fault EBPF_FAULT_HELPER_UNSUPPORTED (after the
+ *     reference's NULL-argument checks, which return EINVAL);
+ *   - the map may be known only at run time (r1 computed or loaded): the helper then checks r1
+ *     against the maps of the program; r1 NULL (or a NULL key / value, or flags > EBPF_EXIST)
+ *     is EINVAL as in ebpf_map.c:101-108 / :130-136, a pointer that is no map of them faults
+ *     EBPF_FAULT_BAD_MAP (the reference dereferences it); a writing program runs its batch on
+ *     one device (the multi-device calls return EOPNOTSUPP).
  * The written values live in the device's mirror of the map until the host API touches the map
  * (lookup / update / delete / get_next_key, or a helper call from ebpf_prog_run), which copies
  * them back first.  ebpf_prog_run itself keeps the reference's immediate writes. */

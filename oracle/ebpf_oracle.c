@@ -322,11 +322,13 @@ helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_
 
 /* ebpf_map_delete_elem (ebpf_map.c) -> array_map_delete_elem (ebpf_map_array.c:246-250) */
 static inline uint64_t
-helper_map_delete(const struct region_env *re, uint64_t r1, int *fault)
+helper_map_delete(const struct region_env *re, uint64_t r1, uint64_t r2, int *fault)
 {
 	uint32_t mi;
-	const struct oracle_map *m = r1 ? find_map(re->p, r1, &mi) : NULL;
-	if (r1 && m == NULL) {
+	if (r1 == 0 || r2 == 0) /* ebpf_map.c:130-136: checked before the map is touched */
+		return 22;        /* EINVAL */
+	const struct oracle_map *m = find_map(re->p, r1, &mi);
+	if (m == NULL) {
 		*fault = F_BAD_MAP;
 		return 0;
 	}
@@ -352,7 +354,7 @@ helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_
 	case ORACLE_HELPER_MAP_UPDATE:
 		return helper_map_update(re, checked, reg[1], reg[2], reg[3], reg[4], fault);
 	case ORACLE_HELPER_MAP_DELETE:
-		return helper_map_delete(re, reg[1], fault);
+		return helper_map_delete(re, reg[1], reg[2], fault);
 	default:
 		*fault = F_HELPER_UNSUPPORTED;
 		return 0;

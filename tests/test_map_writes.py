@@ -203,9 +203,72 @@ def test_oracle_hash_update_faults():
     assert (faults == 6).all() and not ret.any()
 
 
+def prog_runtime_map():
+    """The map of the update and of the delete is chosen at run time (pkt[1] & 3: map 0, map 1,
+    NULL, or r10 — a pointer that is no map); key = pkt[0] & 15, value = pkt[8..16);
+    r0 = delete rc << 8 | update rc.  (The reference's stepping needs a tree: every branch
+    carries its own copy of the tail.)"""
+    from generic_ebpf_amd import layout
+    I, LdDw, MapRef, Branch = _nodes()
+
+    def tail():
+        # (the pointer goes through the stack: the translator no longer knows which map it is,
+        # so the helpers run through the run-time compare chain)
+        return [I("stxdw", R10, R1, -24), I("ldxdw", R1, R10, -24),
+                I("mov_imm", R9, imm=0), I("mov64_reg", R9, R1),          # r9 = the map pointer
+                I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+                I("mov_imm", R3, imm=0), I("mov64_reg", R3, R10), I("add64_imm", R3, imm=-16),
+                I("mov_imm", R4, imm=0), I("call", imm=1),
+                I("mov_imm", R1, imm=0), I("mov64_reg", R1, R9), I("mov_imm", R9, imm=0),
+                I("mov64_reg", R9, R0),
+                I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+                I("call", imm=2), I("lsh64_imm", R0, imm=8), I("or64_reg", R0, R9), I("exit")]
+
+    n = [I("ldxb", R6, R1, 0), I("ldxdw", R8, R1, 8), I("and_imm", R6, imm=15),
+         I("stxw", R10, R6, -4), I("stxdw", R10, R8, -16),
+         I("ldxb", R7, R1, 1), I("and_imm", R7, imm=3),
+         Branch(I("jeq_imm", R7, imm=0), [LdDw(R1, MapRef(0))] + tail()),
+         Branch(I("jeq_imm", R7, imm=1), [LdDw(R1, MapRef(1))] + tail()),
+         Branch(I("jeq_imm", R7, imm=2), [I("mov_imm", R1, imm=0)] + tail()),
+         I("mov_imm", R1, imm=0), I("mov64_reg", R1, R10)] + tail()
+    return layout.assemble(n)
+
+
+def _expect_runtime_map(pk, inits):
+    vals = [np.frombuffer(x, dtype=np.uint64).copy() for x in inits]
+    ret, faults = [], []
+    for p in pk:
+        key, sel = int(p[0]) & 15, int(p[1]) & 3
+        if sel == 3:
+            ret.append(0)
+            faults.append(10)       # BAD_MAP: the update dereferences r10 as a map
+            continue
+        if sel == 2:
+            ret.append((22 << 8) | 22)
+        else:
+            vals[sel][key] = np.frombuffer(p[8:16].tobytes(), dtype=np.uint64)[0]
+            ret.append(22 << 8)
+        faults.append(0)
+    return (np.array(ret, dtype=np.uint64), np.array(faults, dtype=np.uint8),
+            [v.tobytes() for v in vals])
+
+
+def test_oracle_runtime_map_known_answers():
+    n = 3000
+    pk = _packets(n, 15)
+    inits = [_map_init(30), _map_init(31)]
+    lay = prog_runtime_map()
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, inits[0]), (8, NKEYS, inits[1])])
+    ret, faults, _, _ = op.run(pk, n, 64, nthreads=4)
+    want, wf, after = _expect_runtime_map(pk, inits)
+    np.testing.assert_array_equal(faults, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert op.map_bytes(0) == after[0] and op.map_bytes(1) == after[1]
+
+
 def test_translation_of_map_writes(native, env):
     """The translator accepts update / delete with an LDDW-known map (device info works, the
-    compiled code builds) and refuses one whose map is known only at run time."""
+    compiled code builds), and with a map known only at run time (a compare chain on r1)."""
     from generic_ebpf_amd import isa
     for lay in (prog_static(), prog_static(True), prog_generic()):
         m = native.Map(env, NKEYS, 8)
@@ -219,11 +282,20 @@ def test_translation_of_map_writes(native, env):
     e, O = isa.encode, isa.OPS
     p = native.Prog(env, e(O["call"], imm=1) + e(O["exit"]))   # r1 = the packet, not a map
     try:
-        with pytest.raises(native.EbpfError) as ei:
-            p.info()
-        assert ei.value.code == errno.EOPNOTSUPP
+        p.info()
+        assert len(p.device_code(0)) > 0
     finally:
         p.destroy()
+    lay = prog_runtime_map()
+    maps = [native.Map(env, NKEYS, 8), native.Map(env, NKEYS, 8)]
+    p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        assert p.info().nmaps == 2
+        assert len(p.device_code(1)) > 0 and len(p.device_code(0)) > 0
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
 
 
 def _run_device(gpu, env, lay, maps_spec, pk, variant, resident):
@@ -421,3 +493,49 @@ def test_device_percpu_array_writes(gpu, env, variant, resident):
         gpu.set_variant(0)
         p.destroy()
         m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_runtime_map_writes(gpu, env, variant, resident):
+    """map_update_elem / map_delete_elem whose map is chosen at run time (ebpf_map.c:101-108,
+    :130-136): two array maps, NULL (EINVAL) and a pointer that is no map (BAD_MAP), against the
+    oracle and the hand computation; both maps' contents after the batch."""
+    import torch
+    n = (1 << 16) + 3
+    pk = _packets(n, 16)
+    inits = [_map_init(32), _map_init(33)]
+    lay = prog_runtime_map()
+    want, wf, after = _expect_runtime_map(pk, inits)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, inits[0]), (8, NKEYS, inits[1])])
+    ow, owf, _, _ = op.run(pk, n, 64, nthreads=16)
+    np.testing.assert_array_equal(ow, want)
+    np.testing.assert_array_equal(owf, wf)
+    case = goldens.Case("w", lay.code, lay.relocs, [(8, NKEYS, inits[0]), (8, NKEYS, inits[1])],
+                        pk.reshape(-1), n, 64, None)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        gpu.set_variant(variant)
+        if resident:
+            dev = torch.device("cuda:0")
+            d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+            d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+            d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, d_flt.data_ptr(),
+                            None, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            ret, faults = d_ret.cpu().numpy().view(np.uint64), d_flt.cpu().numpy()
+        else:
+            ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        np.testing.assert_array_equal(faults, wf)
+        np.testing.assert_array_equal(ret, want)
+        for k in range(2):
+            got = b"".join(maps[k].lookup(i)[1] for i in range(NKEYS))
+            assert got == after[k], k
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
