@@ -708,6 +708,83 @@ launch_bucketed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 	return 0;
 }
 
+// A shard's write log brought to the host (a batch whose shards ran on several devices: the
+// logs are merged there, in global packet order).  Records as on the device (map_writes.h);
+// `first` = the global index of the shard's packet 0.
+struct host_log {
+	std::vector<uint8_t> rec;
+	uint32_t count = 0;
+	uint32_t stride = 0;
+	std::vector<uint32_t> faulted;
+	uint64_t first = 0;
+};
+
+// Copy the plan's log (its records and faulted-packet bitmap) to the host.  Synchronous.
+int
+upd_fetch(const dprog_device *dp, const upd_plan &P, hipStream_t stream, uint64_t first, host_log *out)
+{
+	hipError_t e = hipStreamSynchronize(stream);
+	uint32_t n = 0;
+	if (e == hipSuccess)
+		e = hipMemcpy(&n, P.log, 4, hipMemcpyDeviceToHost);
+	out->count = std::min(n, P.cap);
+	out->stride = dp->upd_stride;
+	out->first = first;
+	out->rec.resize((size_t)out->count * out->stride);
+	out->faulted.resize(P.faulted_bytes / 4);
+	if (e == hipSuccess && out->count)
+		e = hipMemcpy(out->rec.data(), P.log + 64, out->rec.size(), hipMemcpyDeviceToHost);
+	if (e == hipSuccess && P.faulted_bytes)
+		e = hipMemcpy(out->faulted.data(), P.faulted, P.faulted_bytes, hipMemcpyDeviceToHost);
+	// the log's counter is re-armed for the stream's next batch (upd_plan_for zeroes it too)
+	if (e == hipSuccess)
+		e = hipMemset(P.log, 0, 4);
+	return e == hipSuccess ? 0 : hip_fail(e, "map-write log copy");
+}
+
+// The merged logs of a batch applied to the host copies of the written maps: every record of a
+// packet that did not fault, in (global packet, call) order, so the last write of a key wins —
+// the same rule as the device apply step (map_writes.hip).  Then every device mirror of those
+// maps is stale (the host copy is the newest).
+int
+upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs)
+{
+	struct ref {
+		uint64_t order;
+		const uint8_t *r;
+	};
+	std::vector<ref> all;
+	for (const host_log &h : logs)
+		for (uint32_t i = 0; i < h.count; i++) {
+			const uint8_t *r = h.rec.data() + (size_t)i * h.stride;
+			uint64_t pkt;
+			uint32_t em;
+			memcpy(&pkt, r, 8);
+			memcpy(&em, r + 8, 4);
+			if (pkt / 32 < h.faulted.size() && ((h.faulted[pkt / 32] >> (pkt % 32)) & 1))
+				continue; // the packet faulted: none of its writes land
+			all.push_back(ref{((h.first + pkt) << 20) | (em & 0xfffff), r});
+		}
+	std::stable_sort(all.begin(), all.end(), [](const ref &a, const ref &b) { return a.order < b.order; });
+	const uint16_t cpu = map_current_cpu();
+	for (uint16_t t : ep->xlated->upd_maps)
+		if (map_pull_device_writes(ep->xlated->maps[t]) != 0)
+			return fail(EIO, "copying a device batch's map writes back failed");
+	for (const ref &x : all) {
+		uint32_t em, key;
+		memcpy(&em, x.r + 8, 4);
+		memcpy(&key, x.r + 12, 4);
+		struct ebpf_map *m = ep->xlated->maps[em >> 20];
+		if (key >= m->max_entries)
+			continue; // (never: the routine checked it)
+		uint8_t *img = const_cast<uint8_t *>(map_array_image(m, m->percpu ? cpu : 0));
+		memcpy(img + (size_t)m->value_size * key, x.r + 16, m->value_size);
+	}
+	for (uint16_t t : ep->xlated->upd_maps)
+		ep->xlated->maps[t]->version.fetch_add(1);
+	return 0;
+}
+
 int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false,
@@ -1151,9 +1228,15 @@ ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 	return 0;
 }
 
-EBPF_EXPORT int
-ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
-			uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev, void *stream)
+namespace {
+
+// One device-resident batch (ebpf_prog_run_batch_dev); with `keep` (a shard of a multi-device
+// batch of a map-writing program) its writes stay in their log, described by *keep (keep->cap
+// stays 0 for a program without writes), for the host-side merge instead of being applied on
+// the device.
+int
+batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch, uint64_t *ret_dev,
+	  uint8_t *faults_dev, uint64_t *hist_dev, void *stream, upd_plan *keep)
 {
 	// the measurement hook is consumed by this call, whatever it returns
 	hipEvent_t ev_start = t_time_ev[0], ev_stop = t_time_ev[1];
@@ -1195,7 +1278,23 @@ ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_
 	L.hist = reinterpret_cast<unsigned long long *>(hist_dev);
 	L.count = batch->count;
 	L.stride = batch->stride;
-	return launch(ep, dp, L, static_cast<hipStream_t>(stream), ev_start, ev_stop, overwrite);
+	hipStream_t st = static_cast<hipStream_t>(stream);
+	if (keep && ep->xlated->max_updates) {
+		if ((err = sync_map_mirrors(ep, device, st)) ||
+		    (err = upd_plan_for(ep, dp, batch->count, st, keep)))
+			return err;
+		return launch(ep, dp, L, st, ev_start, ev_stop, overwrite, keep);
+	}
+	return launch(ep, dp, L, st, ev_start, ev_stop, overwrite);
+}
+
+} // namespace
+
+EBPF_EXPORT int
+ebpf_prog_run_batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch,
+			uint64_t *ret_dev, uint8_t *faults_dev, uint64_t *hist_dev, void *stream)
+{
+	return batch_dev(ep, device, batch, ret_dev, faults_dev, hist_dev, stream, nullptr);
 }
 
 namespace {
@@ -1207,7 +1306,7 @@ namespace {
 int
 run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	       const struct ebpf_pkt_batch *batch, uint64_t lo, uint64_t hi, uint64_t *ret,
-	       uint8_t *faults, double *kernel_ms)
+	       uint8_t *faults, double *kernel_ms, host_log *log_out = nullptr)
 {
 	hipError_t e = hipSetDevice(S.device);
 	if (e != hipSuccess)
@@ -1290,7 +1389,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 		L.stride = batch->stride;
 		if ((e = hipEventRecord(S.ev[2 * b], st)) != hipSuccess)
 			return drain(hip_fail(e, "hipEventRecord"));
-		plan.pkt_base = c0;
+		plan.pkt_base = c0 - lo; // (the shard's own packet index: its bitmap starts at lo)
 		if ((err = launch(ep, dp, L, st, nullptr, nullptr, false, &plan)))
 			return drain(err);
 		if ((e = hipEventRecord(S.ev[2 * b + 1], st)) != hipSuccess)
@@ -1311,6 +1410,8 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 			return drain(hip_fail(e, "batch"));
 	}
 	if (ep->xlated->max_updates && hi > lo) {
+		if (log_out) // (several shards: the caller merges the logs)
+			return upd_fetch(dp, plan, S.stream[0], lo, log_out);
 		if ((err = upd_apply(ep, dp, plan, S.stream[0])))
 			return drain(err);
 		if ((e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
@@ -1401,9 +1502,10 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 		return err;
 	auto t0 = std::chrono::steady_clock::now();
 	device_guard dg;
-	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
-		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
-					"land in packet order in one mirror)");
+	// a map-writing program: each shard's writes stay in its log, merged and applied on the host
+	// in global packet order after every shard is done
+	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates;
+	std::vector<host_log> logs(merge ? ndev : 0);
 	std::vector<dprog_device *> dps(ndev);
 	std::vector<staging *> S(ndev, nullptr);
 	for (int d = 0; d < ndev && !err; d++)
@@ -1421,7 +1523,8 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 			const uint64_t lo = d * base + std::min<uint64_t>(d, extra);
 			const uint64_t hi = lo + base + ((uint64_t)d < extra ? 1 : 0);
 			th.emplace_back([&, d, lo, hi] {
-				rc[d] = run_host_shard(ep, dps[d], *S[d], batch, lo, hi, ret, faults, &kms[d]);
+				rc[d] = run_host_shard(ep, dps[d], *S[d], batch, lo, hi, ret, faults, &kms[d],
+						       merge ? &logs[d] : nullptr);
 				hipError_t e;
 				if (!rc[d] && (e = hipMemcpy(&h[(size_t)d * EBPF_HIST_BINS], S[d]->d_hist,
 							     EBPF_HIST_BINS * 8, hipMemcpyDeviceToHost)) !=
@@ -1439,6 +1542,8 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 	for (staging *s : S)
 		if (s)
 			staging_release(s);
+	if (!err && merge)
+		err = upd_apply_host(ep, logs);
 	if (err || !stats)
 		return err;
 	// the results came back over PCIe anyway: the per-shard histograms are summed here
@@ -1466,19 +1571,37 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 	for (int d = 0; d < ndev; d++)
 		if ((err = validate_batch(&shards[d], EBPF_BATCH_HIST_OVERWRITE)))
 			return err;
-	if (ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates)
-		return fail(EOPNOTSUPP, "a map-writing program runs its batch on one device (its writes "
-					"land in packet order in one mirror)");
 	device_guard dg;
 	std::vector<hipStream_t> st(ndev);
 	for (int d = 0; d < ndev; d++)
 		st[d] = streams ? static_cast<hipStream_t>(streams[d]) : nullptr;
+	// A map-writing program on several shards: the batch is the shards in list order; each
+	// shard's writes stay in its log, copied to the host after its launch (synchronous), and
+	// the merged logs are applied there in global packet order when every shard is done.
+	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates;
+	std::vector<host_log> logs(merge ? ndev : 0);
+	auto run_shard = [&](int d, const struct ebpf_pkt_batch *b, uint64_t *hist) -> int {
+		if (!merge)
+			return batch_dev(ep, devices[d], b, ret_dev[d], faults_dev ? faults_dev[d] : nullptr,
+					 hist, st[d], nullptr);
+		uint64_t first = 0;
+		for (int q = 0; q < d; q++)
+			first += shards[q].count;
+		upd_plan plan;
+		int rc = batch_dev(ep, devices[d], b, ret_dev[d], faults_dev ? faults_dev[d] : nullptr, hist,
+				   st[d], &plan);
+		if (rc == 0 && plan.log) {
+			device_guard g2;
+			hipSetDevice(devices[d]);
+			rc = upd_fetch(ep->dev[devices[d]].get(), plan, st[d], first, &logs[d]);
+		}
+		return rc;
+	};
 	if (hist_dev == nullptr) { // no collective: independent launches
 		for (int d = 0; d < ndev; d++)
-			if ((err = ebpf_prog_run_batch_dev(ep, devices[d], &shards[d], ret_dev[d],
-							   faults_dev ? faults_dev[d] : nullptr, nullptr, st[d])))
+			if ((err = run_shard(d, &shards[d], nullptr)))
 				return err;
-		return 0;
+		return merge ? upd_apply_host(ep, logs) : 0;
 	}
 	// The histogram: every shard's launch SETS its row of the scratch of its device's leading
 	// stream (the first shard on that device); the rows of one device are summed into row 0,
@@ -1517,10 +1640,7 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 				return hip_fail(e, "hipStreamWaitEvent");
 			struct ebpf_pkt_batch b = shards[d];
 			b.flags |= EBPF_BATCH_HIST_OVERWRITE;
-			if ((err = ebpf_prog_run_batch_dev(ep, g.device, &b, ret_dev[d],
-							   faults_dev ? faults_dev[d] : nullptr,
-							   reinterpret_cast<uint64_t *>(g.mh + j * EBPF_HIST_BINS),
-							   st[d])))
+			if ((err = run_shard(d, &b, reinterpret_cast<uint64_t *>(g.mh + j * EBPF_HIST_BINS))))
 				return err;
 			if (j > 0 && st[d] != lead &&
 			    ((e = hipEventRecord(g.ev[1 + j], st[d])) != hipSuccess ||
@@ -1566,5 +1686,5 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 				return hip_fail(e, "hipStreamWaitEvent");
 		}
 	}
-	return 0;
+	return merge ? upd_apply_host(ep, logs) : 0;
 }

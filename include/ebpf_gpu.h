@@ -48,8 +48,11 @@ struct ebpf_map;
  *   - the map may be known only at run time (r1 computed or loaded): the helper then checks r1
  *     against the maps of the program; r1 NULL (or a NULL key / value, or flags > EBPF_EXIST)
  *     is EINVAL as in ebpf_map.c:101-108 / :130-136, a pointer that is no map of them faults
- *     EBPF_FAULT_BAD_MAP (the reference dereferences it); a writing program runs its batch on
- *     one device (the multi-device calls return EOPNOTSUPP).
+ *     EBPF_FAULT_BAD_MAP (the reference dereferences it);
+ *   - a writing program sharded over several devices (ebpf_prog_run_batch_multi*): the batch is
+ *     the shards in order, every shard reads the batch-start maps, and the shards' writes are
+ *     merged on the host in that global packet order after the last shard — the same result as
+ *     one batch on one device (ebpf_prog_run_batch_multi_dev then synchronises its streams).
  * The written values live in the device's mirror of the map until the host API touches the map
  * (lookup / update / delete / get_next_key, or a helper call from ebpf_prog_run), which copies
  * them back first.  ebpf_prog_run itself keeps the reference's immediate writes. */

@@ -539,3 +539,78 @@ def test_device_runtime_map_writes(gpu, env, variant, resident):
         p.destroy()
         for m in maps:
             m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [2, 3])
+@pytest.mark.parametrize("which", ["static2", "runtime"])
+def test_multi_device_writers_host_buffers(gpu, env, ndev, which):
+    """A map-writing program sharded over several devices (here one GPU listed `ndev` times, so
+    each shard has its own staging set and log): the shards' logs merge on the host in global
+    packet order, so the results and the maps equal ONE batch over the whole input (the
+    oracle)."""
+    n = (1 << 18) + 7
+    pk = _packets(n, 51)
+    if which == "static2":
+        lay, specs = prog_static(True), [(8, NKEYS, _map_init(52))]
+    else:
+        lay, specs = prog_runtime_map(), [(8, NKEYS, _map_init(53)), (8, NKEYS, _map_init(54))]
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, specs)
+    want, wf, _, _ = op.run(pk, n, 64, nthreads=16)
+    case = goldens.Case("w", lay.code, lay.relocs, specs, pk.reshape(-1), n, 64, None)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        ret, faults, st = p.run_batch_multi([0] * ndev, np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        np.testing.assert_array_equal(faults, wf)
+        np.testing.assert_array_equal(ret, want)
+        for k in range(len(maps)):
+            assert b"".join(maps[k].lookup(i)[1] for i in range(NKEYS)) == op.map_bytes(k), k
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("same_stream", [False, True])
+def test_multi_device_writers_device_resident(gpu, env, same_stream):
+    """ebpf_prog_run_batch_multi_dev with a map-writing program: two shards (one GPU listed
+    twice), histogram summed; the logs merge in shard order = one batch; a second call reads the
+    first one's writes."""
+    import torch
+    n = (1 << 17) + 11
+    half = n // 2
+    lay, init = prog_static(), _map_init(55)
+    pk1, pk2 = _packets(n, 56), _packets(n, 57)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, init)])
+    w1, _, _, _ = op.run(pk1, n, 64, nthreads=16)
+    op2 = pyoracle.OracleProgram(lay.code, lay.relocs, [(8, NKEYS, op.map_bytes(0))])
+    w2, _, _, _ = op2.run(pk2, n, 64, nthreads=16)
+    case = goldens.Case("w", lay.code, lay.relocs, [(8, NKEYS, init)], pk1.reshape(-1), n, 64, None)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    try:
+        dev = torch.device("cuda:0")
+        s0 = torch.cuda.Stream()
+        s1 = s0 if same_stream else torch.cuda.Stream()
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        hists = [torch.zeros(257, dtype=torch.int64, device=dev) for _ in range(2)]
+        for pk, want in ((pk1, w1), (pk2, w2)):
+            d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+            torch.cuda.synchronize()
+            p.run_batch_multi_dev([0, 0], [(d_pk.data_ptr(), half, 64, None),
+                                           (d_pk.data_ptr() + half * 64, n - half, 64, None)],
+                                  [d_ret.data_ptr(), d_ret.data_ptr() + half * 8],
+                                  hists=[h.data_ptr() for h in hists],
+                                  streams=[s0.cuda_stream, s1.cuda_stream], hist_overwrite=True)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+            hw = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257)
+            for h in hists:
+                np.testing.assert_array_equal(h.cpu().numpy(), hw)
+        assert b"".join(maps[0].lookup(i)[1] for i in range(NKEYS)) == op2.map_bytes(0)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
