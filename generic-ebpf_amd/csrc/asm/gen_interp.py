@@ -227,6 +227,7 @@ for c in CONDS:
 # backward jumps in the first 4 bytes of its stack slice (below the frame the program addresses)
 fam("LOOPINIT", 0)
 fam("LOOPCNT", 0)
+fam("HDELETE", 0)              # map_delete_elem on a hashtable known at translation time (s14, s15)
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 
 
@@ -764,12 +765,12 @@ def _hl_word(dst, off, n):
     for j in range(4):
         out += ["s_add_u32 %s, %s, %d" % (s(S_BYTES), s(off), j + 1),
                 "s_cmp_le_u32 %s, %s" % (s(S_BYTES), s(S_T0)),
-                "s_cbranch_scc0 .Lhw_z%d_%d" % (n, j),
+                "s_cbranch_scc0 .Lhw_z%s_%d" % (n, j),
                 "flat_load_ubyte %s, %s offset:%d" % (t[j], vp(R[8]), j),
-                "s_branch .Lhw_d%d_%d" % (n, j),
-                ".Lhw_z%d_%d:" % (n, j),
+                "s_branch .Lhw_d%s_%d" % (n, j),
+                ".Lhw_z%s_%d:" % (n, j),
                 "v_mov_b32 %s, 0" % t[j],
-                ".Lhw_d%d_%d:" % (n, j)]
+                ".Lhw_d%s_%d:" % (n, j)]
     out += ["s_waitcnt vmcnt(0) lgkmcnt(0)",
             "v_lshl_or_b32 %s, %s, 8, %s" % (dst, t[1], t[0]),
             "v_lshl_or_b32 %s, %s, 16, %s" % (dst, t[2], dst),
@@ -823,23 +824,36 @@ def hlookup_routine():
     (r0 = NULL).  r2 == 0 gives NULL with no access, as the reference's NULL-key check.
     Uses s[8:9] (return address), s[10:11] (entry exec), R[*], H[*]; compiled programs treat
     s10..s11 as clobbered after it."""
-    a, b, c = v(R[0]), v(R[1]), v(R[2])
-    t = v(R[3])
     L = [".Lr_hlookup:",
          "s_mov_b64 s[8:9], %s" % sp(S_LINK),
          "s_mov_b64 s[10:11], exec",
          "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
          "v_cmp_ne_u64_e64 vcc, 0, v[4:5]",
          "s_and_b64 exec, exec, vcc",              # NULL keys: r0 = NULL, nothing read
-         "s_cbranch_execz .Lhl_ret",
-         "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+         "s_cbranch_execz .Lhl_ret"] + hprobe_body("") + [
+         ".Lhl_ret:",
+         # every lane that entered and did not fault (S_ALIVE lost the faulted ones)
+         "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
+         "s_setpc_b64 s[8:9]"]
+    return L
+
+
+def hprobe_body(tag):
+    """The probe of HLOOKUP (shared with the hashtable path of UPDATE, whose labels carry `tag`):
+    for the lanes in exec, v[0:1] = the value address of the key at r2 in the map at s14, or
+    NULL; lanes whose key is not readable fault MEM.  Ends at .Lhl_ret<tag> (defined by the
+    caller) with exec arbitrary.  Uses R[*], H[*], S_T*, S_OK, S_JUNK, s[64:71]."""
+    a, b, c = v(R[0]), v(R[1]), v(R[2])
+    t = v(R[3])
+    T = tag
+    L = ["s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
          "s_waitcnt lgkmcnt(0)",
          "s_and_b32 %s, s71, 0xffff" % s(S_T0),    # key size
          "s_mov_b32 %s, 0" % s(S_T1),
          "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1])] + call(".Lr_check") + [
          # exec = the lanes whose key is readable (the others retired with a fault); a
          # structured compiled program may come back with none
-         "s_cbranch_execz .Lhl_ret",
+         "s_cbranch_execz .Lhl_ret%s" % T,
          "s_mov_b64 %s, exec" % sp(S_MASK),
          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
          "s_waitcnt lgkmcnt(0)",
@@ -854,15 +868,15 @@ def hlookup_routine():
          "v_mov_b32 %s, %s" % (c, s(S_JUNK)),
          "s_mov_b32 %s, 0" % s(S_T2),                       # byte offset
          "s_mov_b32 %s, %s" % (s(S_T3), s(S_T0)),           # bytes left
-         ".Lhh_loop:",
+         ".Lhh_loop%s:" % T,
          "s_cmp_le_u32 %s, 12" % s(S_T3),
-         "s_cbranch_scc1 .Lhh_tail"]
+         "s_cbranch_scc1 .Lhh_tail%s" % T]
     n = [0]
 
     def add_words(keep=False):
         out = []
         for i, x in enumerate((a, b, c)):
-            out += _hl_word(t, S_T2, n[0])
+            out += _hl_word(t, S_T2, "%s%d" % (T, n[0]))
             n[0] += 1
             out += ["v_add_u32 %s, %s, %s" % (x, x, t), "s_add_u32 %s, %s, 4" % (s(S_T2), s(S_T2))]
             if keep and i < 2:   # keys of <= 8 bytes: the tail's first two words are the key
@@ -875,8 +889,8 @@ def hlookup_routine():
         L += ["v_sub_u32 %s, %s, %s" % (x, x, y)] + _rot(t, y, k) + \
              ["v_xor_b32 %s, %s, %s" % (x, x, t), "v_add_u32 %s, %s, %s" % (y, y, z)]
     L += ["s_sub_u32 %s, %s, 12" % (s(S_T3), s(S_T3)),
-          "s_branch .Lhh_loop",
-          ".Lhh_tail:"]
+          "s_branch .Lhh_loop%s" % T,
+          ".Lhh_tail%s:" % T]
     L += add_words(keep=True)
     for (x, y, k) in ((c, b, 14), (a, c, 11), (b, a, 25), (c, b, 16), (a, c, 4), (b, a, 14), (c, b, 24)):
         # x ^= y; x -= rot(y, k)
@@ -886,11 +900,11 @@ def hlookup_routine():
     # keys of up to 8 bytes: one 16-byte load per slot (used, hash, key) compared in registers
     k0, k1 = v(H[2]), v(H[3])
     L += ["s_cmp_le_u32 %s, 8" % s(S_T0),
-          "s_cbranch_scc0 .Lhp_general",
+          "s_cbranch_scc0 .Lhp_general%s" % T,
           "v_mov_b32 %s, %s" % (k1, v(R[5])),
           "v_and_b32 %s, s69, %s" % (idx, c),
           "s_mov_b64 %s, exec" % sp(S_OK),
-          ".Lhq_loop:",
+          ".Lhq_loop%s:" % T,
           "v_mov_b32 %s, %s" % (v(R[4]), idx),
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
@@ -899,7 +913,7 @@ def hlookup_routine():
           # the slot's first 8 value bytes (value offset 16 for keys of <= 8 bytes), same line:
           # lanes that meet their key here keep them in v[50:51] for the code generator's
           # forwarded value loads (asm_cc.cpp AHF_LDXHV)
-          "global_load_dwordx2 %s, %s, off offset:16%s" % (vp(H[4]), sa, PROBE_POLICY)] + probe_wait("hq") + [
+          "global_load_dwordx2 %s, %s, off offset:16%s" % (vp(H[4]), sa, PROBE_POLICY)] + probe_wait("hq" + T) + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),           # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[7]), c),
@@ -912,53 +926,125 @@ def hlookup_routine():
           "v_addc_co_u32 v1, vcc, 0, %s, vcc" % v(R[5]),
           "s_andn2_b64 %s, %s, exec" % (sp(S_OK), sp(S_OK)),
           "s_mov_b64 exec, %s" % sp(S_OK),
-          "s_cbranch_execz .Lhl_ret",
+          "s_cbranch_execz .Lhl_ret%s" % T,
           "v_add_u32 %s, 1, %s" % (idx, idx),
           "v_and_b32 %s, s69, %s" % (idx, idx),
-          "s_branch .Lhq_loop",
-          ".Lhp_general:"]
+          "s_branch .Lhq_loop%s" % T,
+          ".Lhp_general%s:" % T]
     L += ["v_and_b32 %s, s69, %s" % (idx, c),
           "s_mov_b64 %s, exec" % sp(S_OK),                  # lanes still probing
-          ".Lhp_loop:",
+          ".Lhp_loop%s:" % T,
           "v_mov_b32 %s, %s" % (v(R[4]), idx),
           "v_mov_b32 %s, 0" % v(R[5]),
           "v_lshlrev_b64 %s, %s, %s" % (sa, s(S_T1), sa),
           "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (sa, sa),
-          "global_load_dwordx2 %s, %s, off" % (hd, sa)] + probe_wait("hp") + [
+          "global_load_dwordx2 %s, %s, off" % (hd, sa)] + probe_wait("hp" + T) + [
           "v_cmp_eq_u32_e64 vcc, 0, %s" % v(R[6]),          # empty slot: not found
           "s_andn2_b64 %s, %s, vcc" % (sp(S_OK), sp(S_OK)),
           "s_and_b64 exec, exec, %s" % sp(S_OK),
           "v_cmp_eq_u32_e64 vcc, %s, %s" % (v(R[7]), c),    # stored hash matches: compare keys
           "s_and_b64 exec, exec, vcc",
-          "s_cbranch_execz .Lhp_next",
+          "s_cbranch_execz .Lhp_next%s" % T,
           "s_mov_b32 %s, 0" % s(S_T2),
-          ".Lhc_loop:",
+          ".Lhc_loop%s:" % T,
           "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_T0)),
-          "s_cbranch_scc1 .Lhc_found"] + _hl_word(v(R[6]), S_T2, 99) + [
+          "s_cbranch_scc1 .Lhc_found%s" % T] + _hl_word(v(R[6]), S_T2, T + "99") + [
           "v_add_co_u32 %s, vcc, %s, %s" % (v(R[8]), s(S_T2), v(R[4])),
           "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[9]), v(R[5])),
           "global_load_dword %s, %s, off offset:8" % (v(R[7]), vp(R[8])),
           "s_waitcnt vmcnt(0)",
           "v_cmp_ne_u32_e64 vcc, %s, %s" % (v(R[6]), v(R[7])),
           "s_andn2_b64 exec, exec, vcc",
-          "s_cbranch_execz .Lhp_next",
+          "s_cbranch_execz .Lhp_next%s" % T,
           "s_add_u32 %s, %s, 4" % (s(S_T2), s(S_T2)),
-          "s_branch .Lhc_loop",
-          ".Lhc_found:",
+          "s_branch .Lhc_loop%s" % T,
+          ".Lhc_found%s:" % T,
           "v_add_co_u32 v0, vcc, s70, %s" % v(R[4]),
           "v_addc_co_u32 v1, vcc, 0, %s, vcc" % v(R[5]),
           "s_andn2_b64 %s, %s, exec" % (sp(S_OK), sp(S_OK)),
-          ".Lhp_next:",
+          ".Lhp_next%s:" % T,
           "s_mov_b64 exec, %s" % sp(S_OK),
-          "s_cbranch_execz .Lhl_ret",
+          "s_cbranch_execz .Lhl_ret%s" % T,
           "v_add_u32 %s, 1, %s" % (idx, idx),
           "v_and_b32 %s, s69, %s" % (idx, idx),
-          "s_branch .Lhp_loop",
-          ".Lhl_ret:",
-          # every lane that entered and did not fault (S_ALIVE lost the faulted ones)
-          "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
-          "s_setpc_b64 s[8:9]"]
+          "s_branch .Lhp_loop%s" % T]
     return L
+
+
+def log_record(T, word, ret):
+    """For the lanes in exec: a slot in the launch's write log (one atomic add on its counter per
+    wave), R[4:5] = the record's address (log + 64 + slot * stride), its first 16 bytes written:
+    {u64 packet index, u32 entry | map << 20, u32 `word`}.  A full log (the host sizes it for the
+    program's most writes per path: a library bug) faults MEM, loudly, rather than lose a write;
+    exec empty after that branches to `ret`.  Uses R[0:7], S_T0..2, S_MASK, S_JUNK, s[64:69]."""
+    return [
+        # a log slot per lane: one atomic add on the log's counter for the wave
+        "s_load_dwordx4 s[64:67], s[0:1], 0x80",         # upd_log, upd_cap, upd_stride
+        "s_load_dwordx2 s[68:69], s[0:1], 0x90",         # pkt_base
+        "s_waitcnt lgkmcnt(0)",
+        "s_bcnt1_i32_b64 %s, exec" % s(S_T0),
+        "v_mbcnt_lo_u32_b32 %s, exec_lo, 0" % v(R[0]),
+        "v_mbcnt_hi_u32_b32 %s, exec_hi, %s" % (v(R[0]), v(R[0])),
+        "s_mov_b64 %s, exec" % sp(S_MASK),
+        "s_ff1_i32_b64 %s, exec" % s(S_T1),
+        "s_lshl_b64 exec, 1, %s" % s(S_T1),
+        "v_mov_b32 %s, %s" % (v(R[1]), s(S_T0)),
+        "v_mov_b32 %s, 0" % v(R[2]),
+        "global_atomic_add %s, %s, %s, s[64:65] sc0" % (v(R[3]), v(R[2]), v(R[1])),
+        "s_waitcnt vmcnt(0)",
+        "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[3])),
+        "s_mov_b64 exec, %s" % sp(S_MASK),
+        "v_add_u32 %s, %s, %s" % (v(R[0]), s(S_T2), v(R[0])),      # this lane's slot
+        # (the host sizes the log for the program's most updates per path; a full log is a
+        # library bug: MEM fault, loudly, rather than a lost write)
+        "v_cmp_gt_u32_e64 vcc, s66, %s" % v(R[0]),
+        "s_andn2_b64 %s, exec, vcc" % sp(S_MASK),
+        "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+        "s_cbranch_scc1 .Lup_room%s" % T,
+        "s_mov_b32 %s, 3" % s(S_CODE)] + call(".Lr_fault") + [
+        "s_cbranch_execz %s" % ret,
+        "s_load_dwordx4 s[64:67], s[0:1], 0x80",
+        "s_load_dwordx2 s[68:69], s[0:1], 0x90",
+        "s_waitcnt lgkmcnt(0)",
+        ".Lup_room%s:" % T,
+        # the record: log + 64 + slot * stride
+        "s_add_u32 s64, s64, 64",
+        "s_addc_u32 s65, s65, 0",
+        "v_mov_b32 %s, s67" % v(R[1]),
+        "v_mad_u64_u32 %s, %s, %s, %s, s[64:65]" % (vp(R[4]), sp(S_JUNK), v(R[0]), v(R[1])),
+        # packet index (pkt_base = this launch's first packet in its batch)
+    ] + lane_pkt_index(R[2]) + [
+        "v_mov_b32 %s, s69" % v(R[3]),
+        "v_add_co_u32 %s, vcc, s68, %s" % (v(R[2]), v(R[2])),
+        "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[3]), v(R[3])),
+        "global_store_dwordx2 %s, %s, off" % (vp(R[4]), vp(R[2])),
+        "s_lshr_b32 %s, s14, 5" % s(S_T0),                  # map index
+        "s_lshl_b32 %s, %s, 20" % (s(S_T0), s(S_T0)),
+        "s_or_b32 %s, %s, s15" % (s(S_T0), s(S_T0)),        # | entry index
+        "v_mov_b32 %s, %s" % (v(R[6]), s(S_T0)),
+        "v_mov_b32 %s, %s" % (v(R[7]), word),
+        "global_store_dwordx2 %s, %s, off offset:8" % (vp(R[4]), vp(R[6]))]
+
+
+def copy_record(T, src, n, off):
+    """Bytes [0, s[n]) at the flat address v[src:src+1] into the record at R[4:5] + s[off]
+    (byte by byte: the source may be the stack, the packet or a map value).  Uses S_T0, S_T1,
+    H[0], H[1], H[3:5], vcc."""
+    return ["s_mov_b32 %s, 0" % s(S_T0),
+            ".Lcp%s:" % T,
+            "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(n)),
+            "s_cbranch_scc1 .Lcpe%s" % T,
+            "v_add_co_u32 %s, vcc, %s, v%d" % (v(H[0]), s(S_T0), src),
+            "v_addc_co_u32 %s, vcc, 0, v%d, vcc" % (v(H[1]), src + 1),
+            "flat_load_ubyte %s, %s" % (v(H[3]), vp(H[0])),
+            "s_add_u32 %s, %s, %s" % (s(S_T1), s(S_T0), s(off)),
+            "v_add_co_u32 %s, vcc, %s, %s" % (v(H[4]), s(S_T1), v(R[4])),
+            "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(H[5]), v(R[5])),
+            "s_waitcnt vmcnt(0) lgkmcnt(0)",
+            "global_store_byte %s, %s, off" % (vp(H[4]), v(H[3])),
+            "s_add_u32 %s, %s, 1" % (s(S_T0), s(S_T0)),
+            "s_branch .Lcp%s" % T,
+            ".Lcpe%s:" % T]
 
 
 def update_routine():
@@ -968,9 +1054,12 @@ def update_routine():
     the reference's (EINVAL for a NULL key / value or flags > EBPF_EXIST, EEXIST for
     EBPF_NOEXIST, EINVAL for a key >= max_entries, else 0) and the write itself goes to the
     launch's log (dp_launch.upd_log: {u64 packet, u32 entry | map << 20, u32 key, value}),
-    applied after the batch in packet order.  Key and value are region-checked like loads.  A
-    hashtable faults HELPER_UNSUPPORTED.  Uses s[8:9] (return address), s[10:11] (entry exec),
-    R[*], H[*]; compiled programs treat s10..s11 as clobbered after it."""
+    applied after the batch in packet order.  Key and value are region-checked like loads.
+    A hashtable (.Lup_hash): the return code against the batch-start table (EEXIST / ENOENT by
+    the key's presence, ebpf_map_hashtable.c:87-100; EBUSY for a new key when the table was
+    full, :371-377) and, for 0, a record {packet, entry | map << 20, flags << 8, key, value}
+    replayed on the host after the batch.  Uses s[8:9] (return address), s[10:11] (entry exec),
+    R[*], H[*], v63 (restored); compiled programs treat s10..s11 as clobbered after it."""
     key = v(H[2])
     L = [".Lr_update:",
          "s_mov_b64 s[8:9], %s" % sp(S_LINK),
@@ -986,12 +1075,8 @@ def update_routine():
          "s_cbranch_execz .Lup_ret",
          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
          "s_waitcnt lgkmcnt(0)",
-         "s_bitcmp1_b32 s71, 31",                       # a hashtable: no device form
-         "s_cbranch_scc0 .Lup_array",
-         "s_mov_b64 %s, exec" % sp(S_MASK),
-         "s_mov_b32 %s, 6" % s(S_CODE)] + call(".Lr_fault") + [
-         "s_branch .Lup_ret",
-         ".Lup_array:",
+         "s_bitcmp1_b32 s71, 31",
+         "s_cbranch_scc1 .Lup_hash",
          # EBPF_NOEXIST: every key of an array exists -> EEXIST (ebpf_map_array.c:188-189)
          "v_and_b32 %s, 1, v8" % v(R[0]),
          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(R[0]),
@@ -1018,53 +1103,7 @@ def update_routine():
           "v_mov_b32 %s, v6" % v(H[0]), "v_mov_b32 %s, v7" % v(H[1]),
           "s_mov_b32 %s, s68" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check") + [
           "s_cbranch_execz .Lup_ret",
-          "v_mov_b32 v0, 0",
-          # a log slot per lane: one atomic add on the log's counter for the wave
-          "s_load_dwordx4 s[64:67], s[0:1], 0x80",         # upd_log, upd_cap, upd_stride
-          "s_load_dwordx2 s[68:69], s[0:1], 0x90",         # pkt_base
-          "s_waitcnt lgkmcnt(0)",
-          "s_bcnt1_i32_b64 %s, exec" % s(S_T0),
-          "v_mbcnt_lo_u32_b32 %s, exec_lo, 0" % v(R[0]),
-          "v_mbcnt_hi_u32_b32 %s, exec_hi, %s" % (v(R[0]), v(R[0])),
-          "s_mov_b64 %s, exec" % sp(S_MASK),
-          "s_ff1_i32_b64 %s, exec" % s(S_T1),
-          "s_lshl_b64 exec, 1, %s" % s(S_T1),
-          "v_mov_b32 %s, %s" % (v(R[1]), s(S_T0)),
-          "v_mov_b32 %s, 0" % v(R[2]),
-          "global_atomic_add %s, %s, %s, s[64:65] sc0" % (v(R[3]), v(R[2]), v(R[1])),
-          "s_waitcnt vmcnt(0)",
-          "v_readfirstlane_b32 %s, %s" % (s(S_T2), v(R[3])),
-          "s_mov_b64 exec, %s" % sp(S_MASK),
-          "v_add_u32 %s, %s, %s" % (v(R[0]), s(S_T2), v(R[0])),      # this lane's slot
-          # (the host sizes the log for the program's most updates per path; a full log is a
-          # library bug: MEM fault, loudly, rather than a lost write)
-          "v_cmp_gt_u32_e64 vcc, s66, %s" % v(R[0]),
-          "s_andn2_b64 %s, exec, vcc" % sp(S_MASK),
-          "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
-          "s_cbranch_scc1 .Lup_room",
-          "s_mov_b32 %s, 3" % s(S_CODE)] + call(".Lr_fault") + [
-          "s_cbranch_execz .Lup_ret",
-          "s_load_dwordx4 s[64:67], s[0:1], 0x80",
-          "s_load_dwordx2 s[68:69], s[0:1], 0x90",
-          "s_waitcnt lgkmcnt(0)",
-          ".Lup_room:",
-          # the record: log + 64 + slot * stride
-          "s_add_u32 s64, s64, 64",
-          "s_addc_u32 s65, s65, 0",
-          "v_mov_b32 %s, s67" % v(R[1]),
-          "v_mad_u64_u32 %s, %s, %s, %s, s[64:65]" % (vp(R[4]), sp(S_JUNK), v(R[0]), v(R[1])),
-          # packet index (pkt_base = this launch's first packet in its batch)
-          ] + lane_pkt_index(R[2]) + [
-          "v_mov_b32 %s, s69" % v(R[3]),
-          "v_add_co_u32 %s, vcc, s68, %s" % (v(R[2]), v(R[2])),
-          "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[3]), v(R[3])),
-          "global_store_dwordx2 %s, %s, off" % (vp(R[4]), vp(R[2])),
-          "s_lshr_b32 %s, s14, 5" % s(S_T0),                  # map index
-          "s_lshl_b32 %s, %s, 20" % (s(S_T0), s(S_T0)),
-          "s_or_b32 %s, %s, s15" % (s(S_T0), s(S_T0)),        # | entry index
-          "v_mov_b32 %s, %s" % (v(R[6]), s(S_T0)),
-          "v_mov_b32 %s, %s" % (v(R[7]), key),
-          "global_store_dwordx2 %s, %s, off offset:8" % (vp(R[4]), vp(R[6])),
+          "v_mov_b32 v0, 0"] + log_record("", key, ".Lup_ret") + [
           # the value, byte by byte (r3 may point at the stack, the packet or a map value)
           "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
           "s_waitcnt lgkmcnt(0)",
@@ -1080,12 +1119,103 @@ def update_routine():
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "global_store_byte %s, %s, off offset:16" % (vp(H[4]), v(H[3])),
           "s_add_u32 %s, %s, 1" % (s(S_T0), s(S_T0)),
-          "s_branch .Lup_copy",
+          "s_branch .Lup_copy"]
+    # hashtable: the lanes probing are marked in v63 (the probe leaves no mask register alone)
+    L += [".Lup_hash:",
+          "s_mov_b64 %s, exec" % sp(S_JUNK),
+          "s_mov_b64 exec, s[10:11]",
+          "v_mov_b32 v%d, 0" % V_SEL,
+          "s_mov_b64 exec, %s" % sp(S_JUNK),
+          "v_mov_b32 v%d, 1" % V_SEL] + hprobe_body("U") + [
+          ".Lhl_retU:",
+          "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
+          "v_cmp_eq_u32_e64 vcc, 1, v%d" % V_SEL,
+          "s_and_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lup_hret",
+          "v_cmp_ne_u64_e64 %s, 0, v[0:1]" % sp(S_MASK),         # the key is in the table
+          "v_mov_b32 v0, 0", "v_mov_b32 v1, 0",
+          "v_and_b32 %s, 1, v8" % v(R[0]),                        # EBPF_NOEXIST: EEXIST
+          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(R[0]),
+          "s_and_b64 vcc, vcc, %s" % sp(S_MASK),
+          "v_cndmask_b32_e64 v0, v0, 17, vcc",
+          "v_and_b32 %s, 2, v8" % v(R[0]),                        # EBPF_EXIST: ENOENT
+          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(R[0]),
+          "s_andn2_b64 vcc, vcc, %s" % sp(S_MASK),
+          "v_cndmask_b32_e64 v0, v0, 2, vcc",
+          # a new key with the table full (the trailer: live entries, max_entries): EBUSY
+          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_bfe_u32 %s, s71, 0x50010" % s(S_T1),
+          "s_mov_b32 s64, s69",
+          "s_mov_b32 s65, 0",
+          "s_lshl_b64 s[64:65], s[64:65], %s" % s(S_T1),
+          "s_add_u32 s64, s64, s66",
+          "s_addc_u32 s65, s65, s67",
+          "s_load_dwordx2 s[64:65], s[64:65], 0x0",
+          "s_waitcnt lgkmcnt(0)",
+          "s_cmp_lt_u32 s64, s65",
+          "s_cbranch_scc1 .Lup_hroom",
+          "v_cmp_eq_u32_e64 vcc, 0, v0",
+          "s_andn2_b64 vcc, vcc, %s" % sp(S_MASK),
+          "v_cndmask_b32_e64 v0, v0, 16, vcc",
+          ".Lup_hroom:",
+          "v_cmp_eq_u32_e64 vcc, 0, v0",
+          "s_and_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lup_hret",
+          # the value is read only by a call that succeeds (ebpf_map_hashtable.c:380-381)
+          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "v_mov_b32 %s, v6" % v(H[0]), "v_mov_b32 %s, v7" % v(H[1]),
+          "s_mov_b32 %s, s68" % s(S_T0), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check") + [
+          "s_cbranch_execz .Lup_hret",
+          "v_lshlrev_b32 %s, 8, v8" % v(H[2])] + log_record("h", v(H[2]), ".Lup_hret") + [
+          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_and_b32 %s, s71, 0xffff" % s(S_T2),                  # key size
+          "s_mov_b32 %s, 16" % s(S_T3)] + copy_record("uk", 4, S_T2, S_T3) + [
+          "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_and_b32 %s, s71, 0xffff" % s(S_T3),
+          "s_add_u32 %s, %s, 23" % (s(S_T3), s(S_T3)),
+          "s_and_b32 %s, %s, -8" % (s(S_T3), s(S_T3)),            # 16 + round8(key size)
+          "s_mov_b32 %s, s68" % s(S_T2)] + copy_record("uv", 6, S_T2, S_T3) + [
+          ".Lup_hret:",
+          "s_mov_b64 exec, s[10:11]",
+          "v_mov_b32 v%d, 0x00010203" % V_SEL,
           ".Lup_ret:",
           # every lane that entered and did not fault (S_ALIVE lost the faulted ones)
           "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
           "s_setpc_b64 s[8:9]"]
     return L
+
+
+def hdelete_routine():
+    """HDELETE (called): r0 = map_delete_elem(map, r2) on the hashtable whose dp_map record is at
+    s14 (ebpf_map.c:126-132 -> ebpf_map_hashtable.c:475-502): EINVAL for a NULL key, else 0 with
+    the key region-checked (the reference hashes it) and a record {packet, entry | map << 20, 1,
+    key} for the host's replay after the batch."""
+    return [".Lr_hdelete:",
+            "s_mov_b64 s[8:9], %s" % sp(S_LINK),
+            "s_mov_b64 s[10:11], exec",
+            "v_mov_b32 v0, 22", "v_mov_b32 v1, 0",
+            "v_cmp_ne_u64_e64 vcc, 0, v[4:5]",
+            "s_and_b64 exec, exec, vcc",
+            "s_cbranch_execz .Lhd_ret",
+            "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+            "s_waitcnt lgkmcnt(0)",
+            "s_and_b32 %s, s71, 0xffff" % s(S_T0),
+            "s_mov_b32 %s, 0" % s(S_T1),
+            "v_mov_b32 %s, v4" % v(H[0]), "v_mov_b32 %s, v5" % v(H[1])] + call(".Lr_check") + [
+            "s_cbranch_execz .Lhd_ret",
+            "v_mov_b32 v0, 0",
+            "v_mov_b32 %s, 1" % v(H[2])] + log_record("d", v(H[2]), ".Lhd_ret") + [
+            "s_load_dwordx8 s[%d:%d], %s, s14" % (S_REC, S_REC + 7, sp(S_MAPS)),
+            "s_waitcnt lgkmcnt(0)",
+            "s_and_b32 %s, s71, 0xffff" % s(S_T2),
+            "s_mov_b32 %s, 16" % s(S_T3)] + copy_record("dk", 4, S_T2, S_T3) + [
+            ".Lhd_ret:",
+            "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
+            "s_setpc_b64 s[8:9]"]
 
 
 # ---------------------------------------------------------------- handler emission
@@ -1147,6 +1277,8 @@ def handler_body(name, d, sr):
         return call(".Lr_hlookup"), False
     if name == "UPDATE":
         return call(".Lr_update"), False
+    if name == "HDELETE":
+        return call(".Lr_hdelete"), False
     if name == "LOOPINIT":
         return ["v_mov_b32 %s, 0" % v(H[0]), "ds_write_b32 v%d, %s" % (V_STK, v(H[0]))], False
     if name == "LOOPCNT":
@@ -1457,6 +1589,7 @@ def routines():
           ".Llk_sched:"] + goto(".Lr_schedule")
     L += hlookup_routine()
     L += update_routine()
+    L += hdelete_routine()
     if not STAGED_IMAGE:
         # BATCH (regrouping; called by the compiled drain code): make the first n = S_T1 lanes the
         # running batch of the queue at s[64:65] from ring slot head = S_T2 on: their packet
@@ -2354,7 +2487,7 @@ def generate(out_s, staged_image):
                 m |= 1 << 2      # the routine resumes at s12
             if name == "HLOOKUP":
                 m |= 1 << 4      # the routine reads the map record offset from s14
-            if name == "UPDATE":
+            if name in ("UPDATE", "HDELETE"):
                 m |= (1 << 4) | (1 << 5)   # map record offset (s14), entry index (s15)
             reads.append(m)
             # an LDS read whose result the interpreter's dispatch wait (lgkmcnt) covered

@@ -42,6 +42,10 @@ enum dp_kind : uint16_t {
 	// 4 bytes of the lane's stack slice, below the frame the program can address.
 	DK_LOOPINIT = 0x10e,
 	DK_LOOPCNT = 0x10f,
+	// r0 = map_delete_elem(map, r2) on a hashtable map known at translation time (aux = its
+	// table index): 0, the delete logged for after the batch (ebpf_map.c:130-136 ->
+	// ebpf_map_hashtable.c:475-502); a NULL key is EINVAL
+	DK_CALL_HDELETE = 0x110,
 };
 #define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
@@ -91,6 +95,13 @@ DP_FN uint32_t dp_hash_key_bytes(uint32_t key_size) { return (key_size + 7u) & ~
 // offset of the value in a slot
 DP_FN uint32_t dp_hash_value_off(uint32_t key_size) { return 8u + dp_hash_key_bytes(key_size); }
 static_assert(sizeof(dp_map) == 32, "dp_map is 32 bytes");
+// A hashtable's device table is followed by a 16-byte trailer: u32 live entries of the table the
+// mirror was built from, u32 the map's max_entries (a device batch's map_update_elem of a new
+// key is EBUSY when the batch-start table is full, ebpf_map_hashtable.c:371-375)
+DP_FN uint64_t dp_hash_trailer_off(uint32_t slots, uint32_t flags)
+{
+	return (uint64_t)slots << dp_hash_stride_log2(flags);
+}
 
 // Kernel arguments (passed by value).
 struct dp_launch {

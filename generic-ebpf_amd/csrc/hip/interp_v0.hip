@@ -101,6 +101,43 @@ cond_taken(uint16_t op, uint64_t d, uint64_t s)
 	return false;
 }
 
+// hashtable_map_lookup_elem's search (ebpf_map_hashtable.c:285-301) over the device table:
+// linear probing from jhash(key) to the key or an empty slot; the value's address or 0
+__device__ inline uint64_t
+hash_find(const dp_map &mp, const uint8_t *kp, uint32_t ks)
+{
+	const uint32_t hv = ebpf_jhash(kp, ks, 0);
+	const uint32_t lg = dp_hash_stride_log2(mp.flags), mask = mp.max_entries - 1;
+	for (uint32_t i = hv & mask;; i = (i + 1) & mask) {
+		const uint8_t *slot = reinterpret_cast<const uint8_t *>(mp.dev_base + ((uint64_t)i << lg));
+		const uint32_t *hdr = reinterpret_cast<const uint32_t *>(slot);
+		if (hdr[0] == 0)
+			return 0;
+		if (hdr[1] != hv)
+			continue;
+		uint32_t b = 0;
+		while (b < ks && slot[8 + b] == kp[b])
+			b++;
+		if (b == ks)
+			return (uint64_t)(uintptr_t)(slot + dp_hash_value_off(ks));
+	}
+}
+
+// A record in the batch's write log (dp_launch.upd_log): {u64 packet, u32 entry | map << 20,
+// u32 word}, the rest for the caller; NULL when the log is full (the host sizes it: never)
+__device__ inline uint8_t *
+log_record(const dp_launch &L, uint64_t gid, uint32_t entry, uint32_t map, uint32_t word)
+{
+	const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t *>(L.upd_log), 1u);
+	if (slot >= L.upd_cap)
+		return nullptr;
+	uint8_t *rec = L.upd_log + 64 + (uint64_t)slot * L.upd_stride;
+	*reinterpret_cast<uint64_t *>(rec) = L.pkt_base + gid;
+	*reinterpret_cast<uint32_t *>(rec + 8) = entry | (map << 20);
+	*reinterpret_cast<uint32_t *>(rec + 12) = word;
+	return rec;
+}
+
 __global__ __launch_bounds__(kWG) void
 ebpf_interp_v0(dp_launch L)
 {
@@ -199,27 +236,7 @@ ebpf_interp_v0(dp_launch L)
 					continue;
 				}
 				if (mp.flags & DP_MAP_HASH) {
-					// hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301) over the
-					// device table: linear probing from jhash(key) to the key or an empty slot
-					const uint8_t *kp = reinterpret_cast<const uint8_t *>(r2);
-					const uint32_t hv = ebpf_jhash(kp, ks, 0);
-					const uint32_t lg = dp_hash_stride_log2(mp.flags), mask = mp.max_entries - 1;
-					for (uint32_t i = hv & mask;; i = (i + 1) & mask) {
-						const uint8_t *slot =
-						    reinterpret_cast<const uint8_t *>(mp.dev_base + ((uint64_t)i << lg));
-						const uint32_t *hdr = reinterpret_cast<const uint32_t *>(slot);
-						if (hdr[0] == 0)
-							break;
-						if (hdr[1] != hv)
-							continue;
-						uint32_t b = 0;
-						while (b < ks && slot[8 + b] == kp[b])
-							b++;
-						if (b == ks) {
-							res = (uint64_t)(uintptr_t)(slot + dp_hash_value_off(ks));
-							break;
-						}
-					}
+					res = hash_find(mp, reinterpret_cast<const uint8_t *>(r2), ks);
 				} else {
 					uint32_t key = (uint32_t)load_bytes(r2, 4);
 					if (key < mp.max_entries)
@@ -238,8 +255,41 @@ ebpf_interp_v0(dp_launch L)
 			if (r2 != 0 && r3 != 0 && r4 <= 2) {
 				const dp_map &mp = L.maps[e.aux];
 				if (mp.flags & DP_MAP_HASH) {
-					fault = F_HELPER_UNSUPPORTED;
-					active = false;
+					// against the batch-start table (ebpf_map_hashtable.c:346-390): EEXIST /
+					// ENOENT by the key's presence, EBUSY for a new key when the table was full;
+					// a call that succeeds logs {flags << 8, key, value} for the host's replay
+					const uint32_t ks = dp_hash_key_size(mp.flags);
+					int f = check(rg, L, r2, ks, false);
+					if (f) {
+						fault = f;
+						active = false;
+						continue;
+					}
+					const uint8_t *kp = reinterpret_cast<const uint8_t *>(r2);
+					const bool exists = hash_find(mp, kp, ks) != 0;
+					const uint32_t *trailer = reinterpret_cast<const uint32_t *>(
+					    mp.dev_base + dp_hash_trailer_off(mp.max_entries, mp.flags));
+					res = exists && (r4 & 1) ? 17 : !exists && (r4 & 2) ? 2
+					    : !exists && trailer[0] >= trailer[1] ? 16 : 0;
+					if (res == 0) {
+						if ((f = check(rg, L, r3, mp.value_size, false))) {
+							fault = f;
+							active = false;
+							continue;
+						}
+						uint8_t *rec = log_record(L, gid, t, e.aux, (uint32_t)r4 << 8);
+						if (!rec) {
+							fault = F_MEM;
+							active = false;
+							continue;
+						}
+						const uint8_t *v = reinterpret_cast<const uint8_t *>(r3);
+						for (uint32_t b = 0; b < ks; b++)
+							rec[16 + b] = kp[b];
+						for (uint32_t b = 0; b < mp.value_size; b++)
+							rec[16 + dp_hash_key_bytes(ks) + b] = v[b];
+					}
+					R[0][tid] = res;
 					continue;
 				}
 				if (r4 & 1) {
@@ -255,22 +305,41 @@ ebpf_interp_v0(dp_launch L)
 						continue;
 					}
 					if (key < mp.max_entries) {
-						const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t *>(L.upd_log), 1u);
-						if (slot >= L.upd_cap) {
+						uint8_t *rec = log_record(L, gid, t, e.aux, key);
+						if (!rec) {
 							fault = F_MEM; // (the host sizes the log: never)
 							active = false;
 							continue;
 						}
-						uint8_t *rec = L.upd_log + 64 + (uint64_t)slot * L.upd_stride;
-						*reinterpret_cast<uint64_t *>(rec) = L.pkt_base + gid;
-						*reinterpret_cast<uint32_t *>(rec + 8) = t | ((uint32_t)e.aux << 20);
-						*reinterpret_cast<uint32_t *>(rec + 12) = key;
 						const uint8_t *v = reinterpret_cast<const uint8_t *>(r3);
 						for (uint32_t b = 0; b < mp.value_size; b++)
 							rec[16 + b] = v[b];
 						res = 0;
 					}
 				}
+			}
+			R[0][tid] = res;
+			continue;
+		}
+		if (k == DK_CALL_HDELETE) {
+			// map_delete_elem on a hashtable (ebpf_map.c:126-132 -> ebpf_map_hashtable.c:
+			// 475-502): EINVAL for a NULL key, else 0 with {1, key} logged for the host's replay
+			const uint64_t r2 = R[2][tid];
+			uint64_t res = 22;
+			if (r2 != 0) {
+				const dp_map &mp = L.maps[e.aux];
+				const uint32_t ks = dp_hash_key_size(mp.flags);
+				int f = check(rg, L, r2, ks, false);
+				uint8_t *rec = f ? nullptr : log_record(L, gid, t, e.aux, 1);
+				if (f || !rec) {
+					fault = f ? f : F_MEM;
+					active = false;
+					continue;
+				}
+				const uint8_t *kp = reinterpret_cast<const uint8_t *>(r2);
+				for (uint32_t b = 0; b < ks; b++)
+					rec[16 + b] = kp[b];
+				res = 0;
 			}
 			R[0][tid] = res;
 			continue;

@@ -36,6 +36,8 @@ upd_offer(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 			continue; // the packet faulted after this write: no write of it lands
 		const uint32_t mi = *reinterpret_cast<const uint32_t *>(r + 8) >> 20;
 		const uint32_t key = *reinterpret_cast<const uint32_t *>(r + 12);
+		if (maps[mi].is_hash)
+			continue; // (replayed on the host)
 		atomicMax(&win[maps[mi].win_off + key], (unsigned long long)rec_order(r));
 	}
 }
@@ -49,6 +51,8 @@ upd_apply(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 		const uint8_t *r = log + 64 + (uint64_t)i * stride;
 		const uint32_t mi = *reinterpret_cast<const uint32_t *>(r + 8) >> 20;
 		const uint32_t key = *reinterpret_cast<const uint32_t *>(r + 12);
+		if (maps[mi].is_hash)
+			continue;
 		unsigned long long *w = &win[maps[mi].win_off + key];
 		if (*w != (unsigned long long)rec_order(r))
 			continue;

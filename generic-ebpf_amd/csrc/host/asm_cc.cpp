@@ -1486,7 +1486,7 @@ int
 written_reg(int fam, int d)
 {
 	switch (fam) {
-	case AHF_LOOKUPSTK: case AHF_LOOKUPGEN: case AHF_HLOOKUP: case AHF_UPDATE:
+	case AHF_LOOKUPSTK: case AHF_LOOKUPGEN: case AHF_HLOOKUP: case AHF_UPDATE: case AHF_HDELETE:
 		return 0;
 	case AHF_EXIT: case AHF_FAULT: case AHF_NOP:
 	case AHF_STXGEN1: case AHF_STXGEN2: case AHF_STXGEN4: case AHF_STXGEN8:
@@ -1509,7 +1509,7 @@ copied_uses(int fam, int d, int s)
 	switch (fam) {
 	case AHF_EXIT: return 1;
 	case AHF_LOOKUPGEN: return (1u << 1) | (1u << 2);
-	case AHF_HLOOKUP: return 1u << 2;
+	case AHF_HLOOKUP: case AHF_HDELETE: return 1u << 2;
 	case AHF_UPDATE: return (1u << 2) | (1u << 3) | (1u << 4);
 	case AHF_FAULT: case AHF_NOP: case AHF_LOOKUPSTK: return 0;
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8: return 0;
@@ -2338,7 +2338,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				const int fam = ah_fam[(uint32_t)low[e].handler];
 				if (!out[e].fast &&
 				    ((fam >= AHF_LDXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
-				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN))
+				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN ||
+				     fam == AHF_UPDATE || fam == AHF_HDELETE))
 					needs_pkt = true;
 			}
 			if (xl.start < n) {

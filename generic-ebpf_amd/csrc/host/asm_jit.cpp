@@ -348,7 +348,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			}
 			pre_mask[e] = m;
 			if (ah_fam[(uint32_t)low[e].handler] == AHF_HLOOKUP ||
-			    ah_fam[(uint32_t)low[e].handler] == AHF_UPDATE) // (their routines use s10/s11)
+			    ah_fam[(uint32_t)low[e].handler] == AHF_UPDATE ||
+			    ah_fam[(uint32_t)low[e].handler] == AHF_HDELETE) // (their routines use s10/s11)
 				for (bool &x : known)
 					x = false;
 		}

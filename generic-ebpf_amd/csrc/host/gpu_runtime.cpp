@@ -464,20 +464,26 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 	if (ep->xlated->max_updates) {
 		// map writes: the apply step's view of the table (map_writes.h), winner words for
 		// every key of every written map, the log record size
+		// (hashtable records: {u64 packet, u32 entry | map << 20, u32 op, key, value}, the key
+		// and the value each padded to 8 bytes)
 		std::vector<upd_map> um(nd->table.size());
-		uint32_t vmax = 8;
+		uint32_t rmax = 8;
+		const std::vector<uint16_t> &arr = ep->xlated->upd_maps, &hash = ep->xlated->hupd_maps;
 		for (size_t t = 0; t < nd->table.size(); t++) {
 			um[t].dev_base = nd->table[t].dev_base;
 			um[t].value_size = nd->table[t].value_size;
 			um[t].max_entries = nd->table[t].max_entries;
 			um[t].win_off = nd->win_words;
-			if (std::find(ep->xlated->upd_maps.begin(), ep->xlated->upd_maps.end(), (uint16_t)t) !=
-			    ep->xlated->upd_maps.end()) {
+			um[t].is_hash = (nd->table[t].flags & DP_MAP_HASH) ? 1u : 0u;
+			if (std::find(arr.begin(), arr.end(), (uint16_t)t) != arr.end()) {
 				nd->win_words += nd->table[t].max_entries;
-				vmax = std::max(vmax, nd->table[t].value_size);
+				rmax = std::max(rmax, (nd->table[t].value_size + 7) & ~7u);
 			}
+			if (std::find(hash.begin(), hash.end(), (uint16_t)t) != hash.end())
+				rmax = std::max(rmax, dp_hash_key_bytes(dp_hash_key_size(nd->table[t].flags)) +
+							  ((nd->table[t].value_size + 7) & ~7u));
 		}
-		nd->upd_stride = 16 + ((vmax + 7) & ~7u);
+		nd->upd_stride = 16 + rmax;
 		if ((e = hipMalloc(&nd->d_upd, um.size() * sizeof(upd_map))) != hipSuccess ||
 		    (e = hipMemcpy(nd->d_upd, um.data(), um.size() * sizeof(upd_map),
 				   hipMemcpyHostToDevice)) != hipSuccess)
@@ -736,18 +742,21 @@ upd_fetch(const dprog_device *dp, const upd_plan &P, hipStream_t stream, uint64_
 		e = hipMemcpy(out->rec.data(), P.log + 64, out->rec.size(), hipMemcpyDeviceToHost);
 	if (e == hipSuccess && P.faulted_bytes)
 		e = hipMemcpy(out->faulted.data(), P.faulted, P.faulted_bytes, hipMemcpyDeviceToHost);
-	// the log's counter is re-armed for the stream's next batch (upd_plan_for zeroes it too)
-	if (e == hipSuccess)
-		e = hipMemset(P.log, 0, 4);
+	// (the log's counter is re-armed by the apply step, or by the next batch's upd_plan_for)
 	return e == hipSuccess ? 0 : hip_fail(e, "map-write log copy");
 }
 
-// The merged logs of a batch applied to the host copies of the written maps: every record of a
-// packet that did not fault, in (global packet, call) order, so the last write of a key wins —
-// the same rule as the device apply step (map_writes.hip).  Then every device mirror of those
-// maps is stale (the host copy is the newest).
+// The logs of a batch applied on the host, every record of a packet that did not fault in
+// (global packet, call) order:
+//   - hashtable records (always): replayed through the map's own update / delete (the program
+//     side of ebpf_map_hashtable.c:346-431 / :475-502, percpu: the submitting CPU's value) with
+//     the call's arguments; a replayed call that fails against the table as it then is (EEXIST,
+//     ENOENT, EBUSY) leaves it unchanged;
+//   - array records (`arrays`: a batch whose shards ran on several devices): the value copied
+//     into the host copy, so the last write of a key wins — the device apply step's rule
+//     (map_writes.hip); every device mirror of those maps is then stale.
 int
-upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs)
+upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arrays)
 {
 	struct ref {
 		uint64_t order;
@@ -761,28 +770,58 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs)
 			uint32_t em;
 			memcpy(&pkt, r, 8);
 			memcpy(&em, r + 8, 4);
+			if ((em >> 20) >= ep->xlated->maps.size())
+				return fail(EIO, "map-write log: a record names no map of the program");
 			if (pkt / 32 < h.faulted.size() && ((h.faulted[pkt / 32] >> (pkt % 32)) & 1))
 				continue; // the packet faulted: none of its writes land
-			all.push_back(ref{((h.first + pkt) << 20) | (em & 0xfffff), r});
+			const bool hash = ep->xlated->maps[em >> 20]->is_hashtable();
+			if (hash || arrays)
+				all.push_back(ref{((h.first + pkt) << 20) | (em & 0xfffff), r});
 		}
 	std::stable_sort(all.begin(), all.end(), [](const ref &a, const ref &b) { return a.order < b.order; });
 	const uint16_t cpu = map_current_cpu();
-	for (uint16_t t : ep->xlated->upd_maps)
-		if (map_pull_device_writes(ep->xlated->maps[t]) != 0)
-			return fail(EIO, "copying a device batch's map writes back failed");
+	if (arrays)
+		for (uint16_t t : ep->xlated->upd_maps)
+			if (map_pull_device_writes(ep->xlated->maps[t]) != 0)
+				return fail(EIO, "copying a device batch's map writes back failed");
 	for (const ref &x : all) {
-		uint32_t em, key;
+		uint32_t em, word;
 		memcpy(&em, x.r + 8, 4);
-		memcpy(&key, x.r + 12, 4);
+		memcpy(&word, x.r + 12, 4);
 		struct ebpf_map *m = ep->xlated->maps[em >> 20];
-		if (key >= m->max_entries)
+		if (m->is_hashtable()) {
+			void *key = const_cast<uint8_t *>(x.r + 16);
+			void *value = const_cast<uint8_t *>(x.r + 16 + dp_hash_key_bytes(m->key_size));
+			if ((word & 0xff) == 1)
+				m->emt->ops.delete_elem(m, key);
+			else
+				m->emt->ops.update_elem(m, key, value, (word >> 8) & 0xff);
+			continue;
+		}
+		if (word >= m->max_entries)
 			continue; // (never: the routine checked it)
 		uint8_t *img = const_cast<uint8_t *>(map_array_image(m, m->percpu ? cpu : 0));
-		memcpy(img + (size_t)m->value_size * key, x.r + 16, m->value_size);
+		memcpy(img + (size_t)m->value_size * word, x.r + 16, m->value_size);
 	}
-	for (uint16_t t : ep->xlated->upd_maps)
-		ep->xlated->maps[t]->version.fetch_add(1);
+	if (arrays)
+		for (uint16_t t : ep->xlated->upd_maps)
+			ep->xlated->maps[t]->version.fetch_add(1);
 	return 0;
+}
+
+// The end of a map-writing batch on one device: array writes applied on the device
+// (upd_apply), hashtable writes copied to the host and replayed there (synchronous).
+int
+upd_finish(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
+{
+	const bool hash = !ep->xlated->hupd_maps.empty();
+	std::vector<host_log> logs(hash ? 1 : 0);
+	int err;
+	if (hash && (err = upd_fetch(dp, P, stream, 0, &logs[0])))
+		return err;
+	if (!ep->xlated->upd_maps.empty() && (err = upd_apply(ep, dp, P, stream)))
+		return err;
+	return hash ? upd_apply_host(ep, logs, false) : 0;
 }
 
 int
@@ -884,7 +923,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	if (e != hipSuccess)
 		return hip_fail(e, "kernel launch");
 	if (ep->xlated->max_updates && plan == nullptr)
-		return upd_apply(ep, dp, own, stream);
+		return upd_finish(ep, dp, own, stream);
 	return 0;
 }
 
@@ -1412,7 +1451,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	if (ep->xlated->max_updates && hi > lo) {
 		if (log_out) // (several shards: the caller merges the logs)
 			return upd_fetch(dp, plan, S.stream[0], lo, log_out);
-		if ((err = upd_apply(ep, dp, plan, S.stream[0])))
+		if ((err = upd_finish(ep, dp, plan, S.stream[0])))
 			return drain(err);
 		if ((e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
 			return hip_fail(e, "map writes");
@@ -1543,7 +1582,7 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 		if (s)
 			staging_release(s);
 	if (!err && merge)
-		err = upd_apply_host(ep, logs);
+		err = upd_apply_host(ep, logs, true);
 	if (err || !stats)
 		return err;
 	// the results came back over PCIe anyway: the per-shard histograms are summed here
@@ -1601,7 +1640,7 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 		for (int d = 0; d < ndev; d++)
 			if ((err = run_shard(d, &shards[d], nullptr)))
 				return err;
-		return merge ? upd_apply_host(ep, logs) : 0;
+		return merge ? upd_apply_host(ep, logs, true) : 0;
 	}
 	// The histogram: every shard's launch SETS its row of the scratch of its device's leading
 	// stream (the first shard on that device); the rows of one device are summed into row 0,
@@ -1686,5 +1725,5 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 				return hip_fail(e, "hipStreamWaitEvent");
 		}
 	}
-	return merge ? upd_apply_host(ep, logs) : 0;
+	return merge ? upd_apply_host(ep, logs, true) : 0;
 }

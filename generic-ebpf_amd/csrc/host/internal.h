@@ -176,6 +176,7 @@ struct dprog_host {
 	uint32_t max_updates = 0;            // most map_update_elem calls on one path (0: none)
 	bool has_loops = false;              // standard semantics: backward jumps (LOOPCNT entries)
 	std::vector<uint16_t> upd_maps;      // table indices of the array maps those calls write
+	std::vector<uint16_t> hupd_maps;     // ... and of the hashtables update / delete calls write
 	int error = 0;
 	std::string error_msg;
 };

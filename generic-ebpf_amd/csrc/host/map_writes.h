@@ -3,12 +3,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// One array map a program writes, as the apply kernels see it.
+// One map of a map-writing program, as the apply kernels see it.  Hashtable records
+// (is_hash) are replayed on the host after the batch (gpu_runtime.cpp upd_apply_host): the
+// kernels leave them alone.
 struct upd_map {
 	uint64_t dev_base;    // the device mirror
 	uint32_t value_size;
 	uint32_t max_entries;
 	uint64_t win_off;     // first winner word of this map (one u64 per key)
+	uint32_t is_hash;
+	uint32_t pad;
 };
 
 // Apply the log's records to the mirrors (last write per key, packet order) but those of the

@@ -564,7 +564,7 @@ map_device_layout_of(const struct ebpf_map *em)
 		slots <<= 1;
 	if (lg > 31 || slots > (1ull << 31) || slots * stride > (1ull << 36))
 		return l;
-	l.bytes = (size_t)(slots * stride);
+	l.bytes = (size_t)(slots * stride) + 16; // (+ the trailer, dprog.h dp_hash_trailer_off)
 	l.slots = (uint32_t)slots;
 	l.flags = DP_MAP_HASH | (lg << 16) | em->key_size;
 	return l;
@@ -592,6 +592,8 @@ map_device_image(struct ebpf_map *em, std::vector<uint8_t> &out, uint16_t cpu)
 			memcpy(slot + 8, h->key(e), em->key_size);
 			memcpy(slot + voff, h->val(e, h->percpu ? cpu % h->ncpu : 0), em->value_size);
 		}
+	const uint32_t trailer[2] = {(uint32_t)h->nlive, em->max_entries};
+	memcpy(out.data() + dp_hash_trailer_off(l.slots, l.flags), trailer, sizeof(trailer));
 }
 
 EBPF_EXPORT const struct ebpf_map_type emt_array = {

@@ -478,6 +478,10 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 	}
 	if (k == DK_LOOPINIT || k == DK_LOOPCNT)
 		return;
+	if (k == DK_CALL_HDELETE) {
+		r[0] = av();
+		return;
+	}
 	const uint8_t cls = k & 7;
 	if (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32 || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
 		return;
@@ -750,9 +754,9 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		if (grew)
 			dataflow(out);
 	}
-	// Map-writing helpers: the map must be a translation-time constant of the table.  delete
-	// on an array map is EINVAL whatever its arguments (ebpf_map.c delete -> ebpf_map_array.c:
-	// 246-250): a constant; on a hashtable it has no device form.  update keeps its entry,
+	// Map-writing helpers, the map now a translation-time constant of the table.  delete on an
+	// array map is EINVAL whatever its arguments (ebpf_map.c delete -> ebpf_map_array.c:
+	// 246-250): a constant; on a hashtable it becomes DK_CALL_HDELETE.  update keeps its entry,
 	// aux = the map's table index (its routine checks the arguments at run time).
 	for (size_t i = 0; i < out.entries.size(); i++) {
 		dp_entry &e = out.entries[i];
@@ -771,26 +775,11 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		}
 		if (e.aux == 1) { // delete
 			if (out.maps[mi]->is_hashtable()) {
-				// a NULL key is EINVAL before the map is touched (ebpf_map.c:130-136)
-				dp_entry j, a, f;
-				memset(&j, 0, sizeof(j));
-				memset(&a, 0, sizeof(a));
-				memset(&f, 0, sizeof(f));
-				a.kind = EBPF_OP_LDDW;
-				a.imm = EINVAL;
-				a.next = e.next;
-				f.kind = DK_FAULT;
-				f.aux = EBPF_FAULT_HELPER_UNSUPPORTED;
-				j.kind = EBPF_OP_JEQ_IMM;
-				j.dst = EBPF_R2;
-				j.imm = 0;
-				out.entries.push_back(a);
-				j.target = (uint32_t)(out.entries.size() - 1);
-				out.entries.push_back(f);
-				j.next = (uint32_t)(out.entries.size() - 1);
-				out.entries[i] = j; // (no reference into entries is held across the pushes)
-				out.annot.resize(out.entries.size());
-				out.annot[j.target] = out.annot[j.next] = out.annot[i];
+				e.kind = DK_CALL_HDELETE; // (the key is logged; the routine checks it)
+				e.aux = (uint16_t)mi;
+				if (std::find(out.hupd_maps.begin(), out.hupd_maps.end(), (uint16_t)mi) ==
+				    out.hupd_maps.end())
+					out.hupd_maps.push_back((uint16_t)mi);
 			} else {
 				e.kind = EBPF_OP_LDDW;
 				e.dst = 0;
@@ -799,14 +788,15 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 			continue;
 		}
 		e.aux = (uint16_t)mi;
-		if (!out.maps[mi]->is_hashtable() &&
-		    std::find(out.upd_maps.begin(), out.upd_maps.end(), (uint16_t)mi) == out.upd_maps.end())
-			out.upd_maps.push_back((uint16_t)mi); // (a hashtable's update faults instead)
+		std::vector<uint16_t> &written = out.maps[mi]->is_hashtable() ? out.hupd_maps : out.upd_maps;
+		if (std::find(written.begin(), written.end(), (uint16_t)mi) == written.end())
+			written.push_back((uint16_t)mi);
 	}
 	// a map write inside a loop has no per-packet bound for the batch's write log
 	if (out.has_loops)
 		for (size_t i = 0; i < out.entries.size(); i++)
-			if (out.entries[i].kind == DK_CALL_UPDATE && out.annot[i].reached) {
+			if ((out.entries[i].kind == DK_CALL_UPDATE || out.entries[i].kind == DK_CALL_HDELETE) &&
+			    out.annot[i].reached) {
 				out.error = EOPNOTSUPP;
 				out.error_msg = "device batches run map_update_elem only in loop-free programs "
 						"(run this one with ebpf_prog_run)";
@@ -850,7 +840,8 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 				if (sx < n)
 					m = std::max(m, best[sx]);
 			}
-			best[id] = m + (out.entries[id].kind == DK_CALL_UPDATE ? 1u : 0u);
+			best[id] = m + (out.entries[id].kind == DK_CALL_UPDATE ||
+					out.entries[id].kind == DK_CALL_HDELETE ? 1u : 0u);
 			state[id] = 2;
 		}
 		out.max_updates = best[out.start];

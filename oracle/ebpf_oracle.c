@@ -247,8 +247,8 @@ struct wrec {
 	uint64_t pkt;
 	uint32_t seq;
 	uint32_t map;
-	uint32_t key;
-	uint64_t voff; /* value bytes in the log's arena */
+	uint32_t key;  /* array: the key; hashtable: op (1 update, 2 delete) | flags << 8 */
+	uint64_t voff; /* value bytes in the log's arena (hashtable: key_size bytes, then the value) */
 };
 struct wlog {
 	struct wrec *rec;
@@ -261,7 +261,7 @@ static __thread uint64_t t_pkt;
 static __thread uint32_t t_seq;
 
 static void
-wlog_push(uint32_t map, uint32_t key, const uint8_t *value, uint32_t vs)
+wlog_push2(uint32_t map, uint32_t key, const uint8_t *a, uint32_t na, const uint8_t *b, uint32_t nb)
 {
 	struct wlog *w = t_wlog;
 	if (w == NULL)
@@ -270,13 +270,21 @@ wlog_push(uint32_t map, uint32_t key, const uint8_t *value, uint32_t vs)
 		w->cap = w->cap ? 2 * w->cap : 1024;
 		w->rec = realloc(w->rec, w->cap * sizeof(*w->rec));
 	}
-	if (w->used + vs > w->arena_cap) {
-		w->arena_cap = (w->arena_cap ? 2 * w->arena_cap : 65536) + vs;
+	if (w->used + na + nb > w->arena_cap) {
+		w->arena_cap = (w->arena_cap ? 2 * w->arena_cap : 65536) + na + nb;
 		w->arena = realloc(w->arena, w->arena_cap);
 	}
-	memcpy(w->arena + w->used, value, vs);
+	memcpy(w->arena + w->used, a, na);
+	if (nb)
+		memcpy(w->arena + w->used + na, b, nb);
 	w->rec[w->n++] = (struct wrec){t_pkt, t_seq++, map, key, w->used};
-	w->used += vs;
+	w->used += na + nb;
+}
+
+static void
+wlog_push(uint32_t map, uint32_t key, const uint8_t *value, uint32_t vs)
+{
+	wlog_push2(map, key, value, vs, NULL, 0);
 }
 
 static const struct oracle_map *
@@ -304,8 +312,22 @@ helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_
 		return 0;
 	}
 	if (m->kind == ORACLE_MAP_HASH) {
-		*fault = F_HELPER_UNSUPPORTED;
-		return 0;
+		/* hashtable_map_update_elem (ebpf_map_hashtable.c:346-390) against the batch-start
+		 * table: check_update_flags (:87-100) by the key's presence, EBUSY for a new key when
+		 * the table is full (:371-377); the value is read only by a call that succeeds */
+		if (checked && (*fault = check_access(re, r2, m->key_size, 0)))
+			return 0;
+		const int exists = helper_map_lookup(re, 0, r1, r2, fault) != 0;
+		const uint32_t cap = m->capacity ? m->capacity : m->max_entries;
+		uint64_t rc = exists && (r4 & 1) ? 17 : !exists && (r4 & 2) ? 2
+			      : !exists && m->max_entries >= cap ? 16 : 0;
+		if (rc == 0) {
+			if (checked && (*fault = check_access(re, r3, m->value_size, 0)))
+				return 0;
+			wlog_push2(mi, 1u | (uint32_t)r4 << 8, (const uint8_t *)(uintptr_t)r2, m->key_size,
+				   (const uint8_t *)(uintptr_t)r3, m->value_size);
+		}
+		return rc;
 	}
 	if (r4 & 1)  /* EBPF_NOEXIST: every key of an array exists */
 		return 17; /* EEXIST */
@@ -322,7 +344,7 @@ helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_
 
 /* ebpf_map_delete_elem (ebpf_map.c) -> array_map_delete_elem (ebpf_map_array.c:246-250) */
 static inline uint64_t
-helper_map_delete(const struct region_env *re, uint64_t r1, uint64_t r2, int *fault)
+helper_map_delete(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
 {
 	uint32_t mi;
 	if (r1 == 0 || r2 == 0) /* ebpf_map.c:130-136: checked before the map is touched */
@@ -332,11 +354,15 @@ helper_map_delete(const struct region_env *re, uint64_t r1, uint64_t r2, int *fa
 		*fault = F_BAD_MAP;
 		return 0;
 	}
-	if (m && m->kind == ORACLE_MAP_HASH) {
-		*fault = F_HELPER_UNSUPPORTED;
+	if (m->kind == ORACLE_MAP_HASH) {
+		/* hashtable_map_delete_elem (ebpf_map_hashtable.c:475-502): 0 whatever the table
+		 * holds; the key is hashed (read) first */
+		if (checked && (*fault = check_access(re, r2, m->key_size, 0)))
+			return 0;
+		wlog_push2(mi, 2u, (const uint8_t *)(uintptr_t)r2, m->key_size, NULL, 0);
 		return 0;
 	}
-	return 22; /* EINVAL: NULL map / key, or an array map (no delete) */
+	return 22; /* EINVAL: an array map (no delete) */
 }
 
 /* CALL :282-284 — helper id imm of the configured table */
@@ -354,7 +380,7 @@ helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_
 	case ORACLE_HELPER_MAP_UPDATE:
 		return helper_map_update(re, checked, reg[1], reg[2], reg[3], reg[4], fault);
 	case ORACLE_HELPER_MAP_DELETE:
-		return helper_map_delete(re, reg[1], reg[2], fault);
+		return helper_map_delete(re, checked, reg[1], reg[2], fault);
 	default:
 		*fault = F_HELPER_UNSUPPORTED;
 		return 0;
@@ -1006,12 +1032,23 @@ uint64_t
 oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *offsets,
 		 uint64_t count, uint32_t stride, uint64_t *ret, uint8_t *faults, int nthreads)
 {
+	return oracle_run_batch_hlog(p, data, offsets, count, stride, ret, faults, nthreads, NULL, 0,
+				     NULL);
+}
+
+uint64_t
+oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t *offsets,
+		      uint64_t count, uint32_t stride, uint64_t *ret, uint8_t *faults, int nthreads,
+		      uint8_t *hlog, uint64_t hlog_cap, uint64_t *hlog_used)
+{
 	uint64_t total = 0;
+	uint64_t hused = 0;
 	if (nthreads <= 0)
 		nthreads = 1;
 	int writes = 0;
 	for (int i = 0; i < 64; i++)
-		writes |= p->helper_kind[i] == ORACLE_HELPER_MAP_UPDATE;
+		writes |= p->helper_kind[i] == ORACLE_HELPER_MAP_UPDATE ||
+			  p->helper_kind[i] == ORACLE_HELPER_MAP_DELETE;
 	struct wlog *logs = writes ? calloc((size_t)nthreads, sizeof(struct wlog)) : NULL;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(+ : total)
@@ -1066,6 +1103,19 @@ oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *off
 		qsort(all, n, sizeof(*all), wrec_cmp);
 		for (size_t j = 0; j < n; j++) {
 			const struct oracle_map *m = &p->maps[all[j].map];
+			if (m->kind == ORACLE_MAP_HASH) {
+				/* for the caller's replay: {u32 map, u32 op | flags << 8, key, value} */
+				const uint64_t sz = 8 + m->key_size + m->value_size;
+				if (hlog && hused + sz <= hlog_cap) {
+					memcpy(hlog + hused, &all[j].map, 4);
+					memcpy(hlog + hused + 4, &all[j].key, 4);
+					memset(hlog + hused + 8, 0, m->key_size + m->value_size);
+					memcpy(hlog + hused + 8, (const void *)(uintptr_t)all[j].voff,
+					       (all[j].key & 0xff) == 1 ? m->key_size + m->value_size : m->key_size);
+				}
+				hused += sz;
+				continue;
+			}
 			memcpy(m->data + (uint64_t)m->value_size * all[j].key,
 			       (const void *)(uintptr_t)all[j].voff, m->value_size);
 		}
@@ -1076,5 +1126,7 @@ oracle_run_batch(const struct oracle_prog *p, uint8_t *data, const uint64_t *off
 		}
 		free(logs);
 	}
+	if (hlog_used)
+		*hlog_used = hused;
 	return total;
 }

@@ -3,6 +3,7 @@
 Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker or the
 timed CPU baseline; the product (generic-ebpf_amd/) never imports this module.
 """
+import copy
 import ctypes
 import os
 import subprocess
@@ -24,15 +25,18 @@ class _Map(ctypes.Structure):
                 ("value_size", ctypes.c_uint32), ("max_entries", ctypes.c_uint32),
                 ("kind", ctypes.c_uint32), ("key_size", ctypes.c_uint32),
                 ("keys", ctypes.c_void_p), ("nbuckets", ctypes.c_uint32),
-                ("bucket_head", ctypes.c_void_p), ("bucket_next", ctypes.c_void_p)]
+                ("bucket_head", ctypes.c_void_p), ("bucket_next", ctypes.c_void_p),
+                ("capacity", ctypes.c_uint32)]
 
 
 class HashSpec:
     """A hashtable map for the oracle: ``items`` = [(key bytes, value bytes)] (live entries), or
-    ``keys``/``values`` as uint8 arrays [n, key_size] / [n, value_size] (large tables)."""
+    ``keys``/``values`` as uint8 arrays [n, key_size] / [n, value_size] (large tables);
+    ``capacity`` = the map's max_entries (None: the entries given, i.e. a full table)."""
 
-    def __init__(self, key_size, value_size, items=None, keys=None, values=None):
+    def __init__(self, key_size, value_size, items=None, keys=None, values=None, capacity=None):
         self.key_size, self.value_size = key_size, value_size
+        self.capacity = capacity
         if items is not None:
             items = [(bytes(k), bytes(v)) for k, v in items]
             assert all(len(k) == key_size and len(v) == value_size for k, v in items)
@@ -48,6 +52,23 @@ class HashSpec:
 
     def __len__(self):
         return len(self.keys)
+
+    def model(self):
+        """The table as a HashtableModel (entries inserted in order, as a test fills the
+        engine's map; a spec made by from_model: that model)."""
+        if getattr(self, "_model", None) is not None:
+            return copy.deepcopy(self._model)
+        m = HashtableModel(self.capacity or max(1, len(self)))
+        for k, v in self.items:
+            m.update(k, v)
+        return m
+
+    @classmethod
+    def from_model(cls, model, key_size, value_size):
+        """The model's live entries (the table a next batch starts from)."""
+        spec = cls(key_size, value_size, items=model.items(), capacity=model.cap)
+        spec._model = copy.deepcopy(model)
+        return spec
 
 
 class _Prog(ctypes.Structure):
@@ -75,6 +96,11 @@ def lib():
         _lib.oracle_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]
+        _lib.oracle_run_batch_hlog.restype = ctypes.c_uint64
+        _lib.oracle_run_batch_hlog.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_void_p]
         _lib.oracle_hash_build.restype = None
         _lib.oracle_hash_build.argtypes = [ctypes.c_void_p]
         _lib.oracle_jhash.restype = ctypes.c_uint32
@@ -101,6 +127,8 @@ class OracleProgram:
         self.code = np.frombuffer(bytes(b), dtype=np.uint8).copy()
         u8 = lambda d: np.ascontiguousarray(np.frombuffer(bytes(d) or b"\0", dtype=np.uint8)).copy()
         self.map_data, self.map_keys, self.map_index = [], [], []
+        self.specs = list(maps)
+        self.hash_models = {}   # k -> HashtableModel: the tables after the batches run so far
         self.maps_arr = (_Map * max(1, len(maps)))()
         for k, m in enumerate(maps):
             self.maps_arr[k].handle = oracle_handle(k)
@@ -112,6 +140,8 @@ class OracleProgram:
                 self.maps_arr[k].keys = self.map_keys[-1].ctypes.data
                 self.maps_arr[k].value_size = m.value_size
                 self.maps_arr[k].max_entries = len(m)
+                self.maps_arr[k].capacity = m.capacity or len(m)
+                self.hash_models[k] = m.model()
                 # the reference's bucket index (nbuckets = entries rounded up to a power of two)
                 nb = 1
                 while nb < max(1, len(m)):
@@ -151,10 +181,36 @@ class OracleProgram:
         ret = np.zeros(count, dtype=np.uint64)
         faults = np.zeros(count, dtype=np.uint8)
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
-        steps = lib().oracle_run_batch(ctypes.addressof(self.p), work.ctypes.data,
-                                       None if offs is None else offs.ctypes.data,
-                                       count, stride, ret.ctypes.data, faults.ctypes.data,
-                                       nthreads)
+        args = (ctypes.addressof(self.p), work.ctypes.data, None if offs is None else offs.ctypes.data,
+                count, stride, ret.ctypes.data, faults.ctypes.data, nthreads)
+        if not self.hash_models:
+            steps = lib().oracle_run_batch(*args)
+            return ret, faults, work, int(steps)
+        # hashtable writes: the batch-start table stays in the oracle's maps (every packet sees
+        # it); the successful calls come back in (packet, call) order and are replayed on
+        # hash_models (a replay that fails leaves the model unchanged)
+        used = ctypes.c_uint64(0)
+        rmax = max(8 + m.key_size + m.value_size for m in self.specs if isinstance(m, HashSpec))
+        cap = max(4096, 4 * count * rmax)    # (up to 4 hashtable writes per packet)
+        buf = np.zeros(cap, dtype=np.uint8)
+        steps = lib().oracle_run_batch_hlog(*args, buf.ctypes.data, cap, ctypes.byref(used))
+        if used.value > cap:
+            raise RuntimeError("oracle: more hashtable writes than the replay buffer holds")
+        self.last_hlog = []
+        if used.value:
+            raw, pos = buf[:used.value].tobytes(), 0
+            while pos < len(raw):
+                k = int.from_bytes(raw[pos:pos + 4], "little")
+                word = int.from_bytes(raw[pos + 4:pos + 8], "little")
+                spec = self.specs[k]
+                key = raw[pos + 8:pos + 8 + spec.key_size]
+                val = raw[pos + 8 + spec.key_size:pos + 8 + spec.key_size + spec.value_size]
+                pos += 8 + spec.key_size + spec.value_size
+                self.last_hlog.append((k, word & 0xff, word >> 8, key, val))
+                if word & 0xff == 1:
+                    self.hash_models[k].update(key, val, word >> 8)
+                else:
+                    self.hash_models[k].delete(key)
         return ret, faults, work, int(steps)
 
     def map_bytes(self, k):
@@ -284,3 +340,7 @@ class HashtableModel:
 
     def keys_in_order(self):
         return [k for b in self.buckets for k, _ in b]
+
+    def items(self):
+        """(key, value) of every live entry in bucket order (percpu: CPU 0's value)."""
+        return [(k, v[0] if self.percpu else v) for b in self.buckets for k, v in b]

@@ -6,7 +6,7 @@ the maps as they were when the batch started; an update returns the reference's 
 (ebpf_map.c:101-108 -> ebpf_map_array.c:185-211: EINVAL for a NULL key / value or flags >
 EBPF_EXIST, EEXIST for EBPF_NOEXIST, EINVAL for a key >= max_entries, else 0) and its write
 lands after the batch in packet order (within a packet in call order); delete on an array map
-is EINVAL (ebpf_map_array.c:246-250).  Hashtable maps: both helpers fault HELPER_UNSUPPORTED.
+is EINVAL (ebpf_map_array.c:246-250).  Hashtable maps: tests/test_hash_writes.py.
 
 CPU tests pin the oracle mode with hand-computed answers and check the translator; GPU tests
 compare every device variant (results, faults and the map's contents after the batch, read back
@@ -73,18 +73,6 @@ def prog_generic():
          LdDw(R1, MapRef(0)),
          I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
          I("call", imm=2), I("lsh64_imm", R0, imm=8), I("or64_reg", R0, R9), I("exit")]
-    return layout.assemble(n)
-
-
-def prog_hash_update():
-    """An update on a hashtable map: HELPER_UNSUPPORTED on the device (and in the oracle)."""
-    from generic_ebpf_amd import layout
-    I, LdDw, MapRef, Branch = _nodes()
-    n = [I("ldxw", R6, R1, 0), I("stxw", R10, R6, -4), I("stxdw", R10, R6, -16),
-         LdDw(R1, MapRef(0)),
-         I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
-         I("mov_imm", R3, imm=0), I("mov64_reg", R3, R10), I("add64_imm", R3, imm=-16),
-         I("mov_imm", R4, imm=0), I("call", imm=1), I("exit")]
     return layout.assemble(n)
 
 
@@ -193,14 +181,6 @@ def test_oracle_generic_pointers_and_delete():
         if rc == 0:
             vals[int(p[0]) & 15] = np.frombuffer(p[16:24].tobytes(), dtype=np.uint64)[0]
     assert op.map_bytes(0) == vals.tobytes()
-
-
-def test_oracle_hash_update_faults():
-    lay = prog_hash_update()
-    spec = pyoracle.HashSpec(4, 8, items=[(b"\0\0\0\0", b"\1" * 8)])
-    op = pyoracle.OracleProgram(lay.code, lay.relocs, [spec])
-    ret, faults, _, _ = op.run(_packets(64, 3), 64, 64)
-    assert (faults == 6).all() and not ret.any()
 
 
 def prog_runtime_map():
@@ -380,24 +360,6 @@ def test_device_map_writes_across_batches(gpu, env):
         p.destroy()
         for m in maps:
             m.destroy()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2])
-def test_device_hash_update_faults(gpu, env, variant):
-    lay = prog_hash_update()
-    hm = gpu.HashMap(env, 4, 8, 16)
-    hm.fill(np.zeros((1, 4), np.uint8), np.ones((1, 8), np.uint8))
-    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [hm.handle]))
-    try:
-        gpu.set_variant(variant)
-        pk = _packets(256, 4)
-        ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), 256, 64)
-        assert (faults == 6).all() and not ret.any()
-    finally:
-        gpu.set_variant(0)
-        p.destroy()
-        hm.destroy()
 
 
 @pytest.mark.gpu
