@@ -1126,7 +1126,8 @@ def update_routine():
           "s_mov_b64 exec, s[10:11]",
           "v_mov_b32 v%d, 0" % V_SEL,
           "s_mov_b64 exec, %s" % sp(S_JUNK),
-          "v_mov_b32 v%d, 1" % V_SEL] + hprobe_body("U") + [
+          "v_mov_b32 v%d, 1" % V_SEL,
+          "v_mov_b32 v0, 0", "v_mov_b32 v1, 0"] + hprobe_body("U") + [
           ".Lhl_retU:",
           "s_and_b64 exec, s[10:11], %s" % sp(S_ALIVE),
           "v_cmp_eq_u32_e64 vcc, 1, v%d" % V_SEL,

@@ -43,8 +43,16 @@ struct ebpf_map;
  *     write of a key wins; a packet that faults (any code, even after its writes) leaves no
  *     write behind;
  *   - map_delete_elem on an array map returns EINVAL (ebpf_map_array.c:246-250);
- *   - on a hashtable map both helpers fault EBPF_FAULT_HELPER_UNSUPPORTED (after the
- *     reference's NULL-argument checks, which return EINVAL);
+ *   - on a hashtable map, map_update_elem returns the reference's code against the batch-start
+ *     table: EINVAL as above, EEXIST (EBPF_NOEXIST, the key present) / ENOENT (EBPF_EXIST, the
+ *     key absent) (ebpf_map_hashtable.c:87-100), EBUSY for a new key when the table was full
+ *     (:371-377), else 0; map_delete_elem returns 0 (:475-502; EINVAL for a NULL key).  The key
+ *     is read (region-checked) before the flags are judged, the value only by a call returning
+ *     0.  The calls that returned 0 are replayed on the host table after the batch, in the same
+ *     packet / call order, through the map's own update / delete (percpu: the submitting CPU's
+ *     value): the table is the one the reference would hold after those calls in that order; a
+ *     replayed call that fails against the table as it then is (EEXIST, ENOENT, EBUSY) leaves it
+ *     unchanged.  A batch with hashtable writes synchronises with the host before it returns;
  *   - the map may be known only at run time (r1 computed or loaded): the helper then checks r1
  *     against the maps of the program; r1 NULL (or a NULL key / value, or flags > EBPF_EXIST)
  *     is EINVAL as in ebpf_map.c:101-108 / :130-136, a pointer that is no map of them faults
@@ -65,8 +73,7 @@ enum ebpf_fault {
 	EBPF_FAULT_MEM = 3,          /* load/store outside this packet, its stack or a map value */
 	EBPF_FAULT_SLOT = 4,         /* stepping left the program (reference reads past the buffer) */
 	EBPF_FAULT_HELPER = 5,       /* CALL id outside [0,64) or an unset helper slot (:283) */
-	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation (incl. map writes
-	                                      to a hashtable: see "Map writes in a device batch") */
+	EBPF_FAULT_HELPER_UNSUPPORTED = 6, /* helper with no device implementation */
 	EBPF_FAULT_BAD_REG = 7,      /* dst/src register nibble >= 11 (reference overflows reg[]) */
 	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns;
 	                                standard semantics: the loop budget is spent (see below) */

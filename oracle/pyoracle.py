@@ -71,6 +71,18 @@ class HashSpec:
         return spec
 
 
+class _LazyModels(dict):
+    """{map index: HashtableModel}, each built from its HashSpec when first asked for."""
+
+    def __init__(self, specs):
+        super().__init__()
+        self.specs = specs
+
+    def __missing__(self, k):
+        m = self[k] = self.specs[k].model()
+        return m
+
+
 class _Prog(ctypes.Structure):
     _fields_ = [("insns", ctypes.c_void_p), ("nslots", ctypes.c_uint64),
                 ("helper_kind", ctypes.c_uint8 * 64), ("maps", ctypes.c_void_p),
@@ -128,7 +140,8 @@ class OracleProgram:
         u8 = lambda d: np.ascontiguousarray(np.frombuffer(bytes(d) or b"\0", dtype=np.uint8)).copy()
         self.map_data, self.map_keys, self.map_index = [], [], []
         self.specs = list(maps)
-        self.hash_models = {}   # k -> HashtableModel: the tables after the batches run so far
+        # k -> HashtableModel: the hashtables after the batches run so far (built on first use)
+        self.hash_models = _LazyModels(self.specs)
         self.maps_arr = (_Map * max(1, len(maps)))()
         for k, m in enumerate(maps):
             self.maps_arr[k].handle = oracle_handle(k)
@@ -141,7 +154,6 @@ class OracleProgram:
                 self.maps_arr[k].value_size = m.value_size
                 self.maps_arr[k].max_entries = len(m)
                 self.maps_arr[k].capacity = m.capacity or len(m)
-                self.hash_models[k] = m.model()
                 # the reference's bucket index (nbuckets = entries rounded up to a power of two)
                 nb = 1
                 while nb < max(1, len(m)):
@@ -165,6 +177,11 @@ class OracleProgram:
         kinds = helper_kinds or DEFAULT_HELPER_KINDS
         for i, v in kinds.items():
             self.p.helper_kind[i] = v
+        # does the program call a map-writing helper (a CALL whose id is one) on a hashtable?
+        ins = self.code[: len(self.code) // 8 * 8].reshape(-1, 8)
+        ids = ins[ins[:, 0] == 0x85, 4:8].copy().view(np.int32).reshape(-1)
+        self.hash_writes = any(isinstance(m, HashSpec) for m in maps) and any(
+            kinds.get(int(i)) in (HELPER_MAP_UPDATE, HELPER_MAP_DELETE) for i in ids)
         self.p.maps = ctypes.addressof(self.maps_arr)
         self.p.nmaps = len(maps)
         self.p.reg_init = reg_init
@@ -183,7 +200,7 @@ class OracleProgram:
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
         args = (ctypes.addressof(self.p), work.ctypes.data, None if offs is None else offs.ctypes.data,
                 count, stride, ret.ctypes.data, faults.ctypes.data, nthreads)
-        if not self.hash_models:
+        if not self.hash_writes:
             steps = lib().oracle_run_batch(*args)
             return ret, faults, work, int(steps)
         # hashtable writes: the batch-start table stays in the oracle's maps (every packet sees
