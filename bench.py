@@ -96,7 +96,12 @@ def parse(argv=None):
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
                    "c4": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24, "c5lit": 1 << 22}
-C4H_SLOT_BYTES = 32  # device table slot: u32 used | u32 hash | 4-B key (8-B padded) | 8-B value
+# C4H: bytes one lookup must move.  The device table's slot is 32 B (u32 used | u32 hash | 4-B key
+# 8-B padded | 8-B value), but a random probe cannot fetch less than one 64-B line from HBM: the
+# PMC passes measured 64 B per lookup (FETCH_SIZE, profiles/r02/s3/all/bench_c4h_slots8.json:
+# 7.79 GB per launch = 4.29 GB packets + 0.54 GB results + 64 B x 46.1M lookups), so the roofline
+# counts the line (round 2 counted the slot's 32 B)
+C4H_PROBE_BYTES = 64
 DISTINCT = 1 << 22  # distinct synthetic packets generated on the host, tiled in HBM
 
 
@@ -150,11 +155,11 @@ class Workload:
                 lens = np.minimum(lens, (w + 63) // 64 * 64)
             return int(lens.sum()) + 8 * (self.n + 1)
         b = self.n * 64
-        if self.cfg == "c4h":  # + one table slot per packet that reaches the lookup (IPv4, not ICMP)
+        if self.cfg == "c4h":  # + one table line per packet that reaches the lookup (IPv4, not ICMP)
             pk = self.pk
             et = (pk[:, 12].astype(np.uint32) << 8) | pk[:, 13]
             reach = float(np.mean((et == 0x0800) & (pk[:, 23] != 1)))
-            b += int(round(self.n * reach) * C4H_SLOT_BYTES)
+            b += int(round(self.n * reach) * C4H_PROBE_BYTES)
         return b
 
     def oracle_maps(self):

@@ -18,6 +18,7 @@ Execution model (one lane = one packet, wavefront-lockstep dispatch):
     the running group retires; retirement writes r0, the fault code and an LDS histogram.
 """
 import os
+import re
 import sys
 
 NREG = 11
@@ -228,6 +229,10 @@ for c in CONDS:
 fam("LOOPINIT", 0)
 fam("LOOPCNT", 0)
 fam("HDELETE", 0)              # map_delete_elem on a hashtable known at translation time (s14, s15)
+# interpreter superinstructions (asm_runtime.cpp asm_fuse_interp; staged kernels): a packet load at
+# a constant offset fused with the BE16 / BE32 of its destination (dst, offset)
+fam("LDXPKBE16", 3)
+fam("LDXPKBE32", 3)
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 
 
@@ -276,6 +281,31 @@ def dispatch(next_reg=12):
     return ["s_load_dwordx8 s[8:15], s[%d:%d], s%d" % (S_PROG, S_PROG + 1, next_reg),
             "s_waitcnt lgkmcnt(0)",
             "s_setpc_b64 s[8:9]"]
+
+
+_ENT_REF = re.compile(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]")
+
+
+def early_fetch_point(body):
+    """Interpreter image: where in a straight-line handler body the next entry's fetch can issue
+    — right after the body's last reference to the entry SGPRs s[8:15] (the load overwrites them
+    when it lands; its offset s12 is read at issue) — so that the fetch's latency overlaps the
+    rest of the body.  None when the body branches, calls, or waits on a partial lgkmcnt."""
+    last = -1
+    for i, ln in enumerate(body):
+        if ln.endswith(":") or ln.split(" ")[0] in ("s_cbranch_scc0", "s_cbranch_scc1", "s_cbranch_vccz",
+                                                    "s_cbranch_vccnz", "s_cbranch_execz",
+                                                    "s_cbranch_execnz", "s_branch", "s_setpc_b64",
+                                                    "s_swappc_b64"):
+            return None
+        for a, b, c in _ENT_REF.findall(ln):
+            lo_, hi_ = (int(a), int(a)) if a else (int(b), int(c))
+            if lo_ <= 15 and hi_ >= 8:
+                last = i
+    rest = body[last + 1:]
+    if any("lgkmcnt(" in ln and "lgkmcnt(0)" not in ln for ln in rest):
+        return None
+    return last + 1
 
 
 def raddr(label, pair_):
@@ -550,6 +580,24 @@ def h_ldx_pkt_const(z, d, off):
             out.append("v_mov_b32 %s, 0" % hi(d))
         return out + ["s_mov_b64 exec, %s" % sp(S_JUNK), ".Lst_{uid}:"]
     return _pkc_extract(z, d, off)
+
+
+def h_ldx_pkt_be(w, d, off):
+    """LDXH / LDXW at a constant packet offset followed by BE16 / BE32 of the same register
+    (ebpf_interpreter.c:327-338 then the byte swap of :164-185): one v_perm_b32 gathers the
+    bytes in big-endian order from the staged packet dwords (staged kernels only)."""
+    z = w // 8
+    if not STAGED_IMAGE or off + z > 64:
+        return []          # never selected
+    k, sh = off >> 2, off & 3
+    lo_ = "v%d" % (PKT0 + k)
+    hi_ = "v%d" % (PKT0 + k + 1) if k + 1 < 16 else lo_   # (then no byte of it is selected)
+    sel = 0
+    for i in range(4):
+        sel |= ((sh + z - 1 - i) if i < z else 0x0c) << (8 * i)
+    return ["s_mov_b32 %s, 0x%x" % (s(S_JUNK), sel),
+            "v_perm_b32 %s, %s, %s, %s" % (lo(d), hi_, lo_, s(S_JUNK)),
+            "v_mov_b32 %s, 0" % hi(d)]
 
 
 def _pkc_extract(z, d, off):
@@ -1239,6 +1287,8 @@ def handler_body(name, d, sr):
             return h_cond(c, d, None, True)
     if name.startswith("LDXPKC"):
         return h_ldx_pkt_const(int(name[6:]), d, sr), False
+    if name.startswith("LDXPKBE"):
+        return h_ldx_pkt_be(int(name[7:]), d, sr), False
     if name.startswith("LDXPKTG"):
         return h_ldx_pkt_general(int(name[7:]), d), False
     if name.startswith("LDXSTK"):
@@ -2420,15 +2470,30 @@ def jit_templates():
     return L
 
 
+# The staged image the assembly interpreter (variant 2) launches from (m3): one result group per
+# burst (64 VGPRs) and an interpreter kernel that declares only the SGPRs the image's own code
+# touches (s0..s73; compiled programs' join masks start at s74), so that 8 workgroups of 256
+# lanes fit a CU (MI355X_MICROARCH.md "Residency": .sgpr_count <= 80 -> 8; 98 -> 6).  The
+# interpreter is bound by its dependent dispatch chain (s_load -> s_waitcnt -> s_setpc per
+# entry) and scales with resident waves (C4: 2 workgroups per CU 3.19 ms ... 6: 1.25 ms).
+NSGPR_INTERP = S_JOIN
+INTERP_IMAGE = False
+RETK_INTERP = int(os.environ.get("EBPF_ASM_RETK_INTERP", "1"))
+assert RETK_INTERP in (1, 2, 4, 8)
+
+
 def main():
-    """gen_interp.py <staged.s> <general.s> <span.s> <handlers.h>"""
-    out_s1, out_s0, out_s2, out_h = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
+    """gen_interp.py <staged.s> <general.s> <span.s> <staged-interpreter.s> <handlers.h>"""
+    out_s1, out_s0, out_s2, out_s3, out_h = sys.argv[1:6]
     header = None
-    global SPAN_IMAGE, NVGPR
-    for out_s, k, staged, span in ((out_s1, RETK_STAGED, True, False), (out_s0, 1, False, False),
-                                   (out_s2, 1, False, True)):
+    global SPAN_IMAGE, NVGPR, INTERP_IMAGE
+    for out_s, k, staged, span, interp in ((out_s1, RETK_STAGED, True, False, False),
+                                           (out_s0, 1, False, False, False),
+                                           (out_s2, 1, False, True, False),
+                                           (out_s3, RETK_INTERP, True, False, True)):
         set_retk(k)
         SPAN_IMAGE = span
+        INTERP_IMAGE = interp
         if not staged:
             NVGPR += SPAN_HOIST_REGS if span else GEN_HOIST_REGS
         h = generate(out_s, staged)
@@ -2440,7 +2505,10 @@ def main():
                             "#define AH_RET_GROUPS_GENERAL 1",
                             "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS),
                             "#define AH_SPAN_HOIST_REGS %d  // span image: hoisted-load VGPRs from v64" % SPAN_HOIST_REGS,
-                            "#define AH_NVGPR_SPAN %d" % (64 + SPAN_HOIST_REGS)]
+                            "#define AH_NVGPR_SPAN %d" % (64 + SPAN_HOIST_REGS),
+                            "#define AH_NVGPR_INTERP %d  // the interpreter's staged image (m3)"
+                            % (64 if RETK_INTERP == 1 else 64 + 2 * RETK_INTERP),
+                            "#define AH_RET_GROUPS_INTERP %d" % RETK_INTERP]
     with open(out_h, "w") as f:
         f.write("\n".join(header) + "\n")
 
@@ -2480,9 +2548,15 @@ def generate(out_s, staged_image):
                 A += copy + [".Lhe_%d:" % hid] + body[k + 1:]
             else:
                 copy = body
-                A += body + [".Lhe_%d:" % hid]
-                if not own:
-                    A += dispatch(12)
+                k = early_fetch_point(body) if (INTERP_IMAGE and not own) else None
+                if k is not None and k < len(body):
+                    # (this image never feeds the code generator, which copies label..Lhe_)
+                    d = dispatch(12)
+                    A += body[:k] + [d[0]] + body[k:] + [".Lhe_%d:" % hid] + d[1:]
+                else:
+                    A += body + [".Lhe_%d:" % hid]
+                    if not own:
+                        A += dispatch(12)
             m = entry_reads(copy)
             if name == "LOOKUPGEN":
                 m |= 1 << 2      # the routine resumes at s12
@@ -2532,7 +2606,14 @@ def generate(out_s, staged_image):
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
     kernarg = 208
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
-    ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, nsg, 256),
+    if INTERP_IMAGE:
+        # the interpreter kernel declares s0..s73 only: check that the image's code uses no more
+        top = 0
+        for ln in A:
+            for a, b, c in re.findall(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]", ln.split(";")[0].split("//")[0]):
+                top = max(top, int(a or c))
+        assert top < NSGPR_INTERP, "interpreter image uses s%d" % top
+    ks = [("ebpf_interp_s64", kernarg, 0, NVGPR, NSGPR_INTERP if INTERP_IMAGE else nsg, 256),
           ("ebpf_interp_gen", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_jit_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_jit_gen", kernarg, 0, NVGPR, nsg, 256),

@@ -99,19 +99,26 @@ constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 
-// The assembly interpreter's three code objects (build/asm_image.cpp): mode 1 = staged 64-B
-// kernels, mode 0 = general kernels, mode 2 = general kernels of span-staged (length-bucketed)
-// launches, whose packets sit in LDS (compiled programs only).
+// The assembly interpreter's code objects (build/asm_image.cpp): mode 1 = staged 64-B kernels,
+// mode 0 = general kernels, mode 2 = general kernels of span-staged (length-bucketed) launches,
+// whose packets sit in LDS (compiled programs only).  Image 3 is mode 1 for the interpreter
+// itself (variant 2): one result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU
+// are resident instead of 6 (gen_interp.py NSGPR_INTERP).
 constexpr int kModes = 3;
-extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[];
-extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len;
+constexpr int kInterpStagedImage = 3;
+extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
+    ebpf_asm_hsaco_m3[];
+extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len,
+    ebpf_asm_hsaco_m3_len;
 inline const unsigned char *asm_image(int mode)
 {
-	return mode == 1 ? ebpf_asm_hsaco_m1 : mode == 2 ? ebpf_asm_hsaco_m2 : ebpf_asm_hsaco_m0;
+	return mode == 1 ? ebpf_asm_hsaco_m1 : mode == 2 ? ebpf_asm_hsaco_m2
+		: mode == 3 ? ebpf_asm_hsaco_m3 : ebpf_asm_hsaco_m0;
 }
 inline size_t asm_image_len(int mode)
 {
-	return mode == 1 ? ebpf_asm_hsaco_m1_len : mode == 2 ? ebpf_asm_hsaco_m2_len : ebpf_asm_hsaco_m0_len;
+	return mode == 1 ? ebpf_asm_hsaco_m1_len : mode == 2 ? ebpf_asm_hsaco_m2_len
+		: mode == 3 ? ebpf_asm_hsaco_m3_len : ebpf_asm_hsaco_m0_len;
 }
 
 // Per (program, device): entries for each interpreter variant and the map table.
