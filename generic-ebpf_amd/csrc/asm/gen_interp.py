@@ -1925,7 +1925,9 @@ def store_prev_results(tag, final):
     # R0 = byte offset of the superblock's first packet result for this lane; R1 = its index
     # (all lanes: the current group's live mask says nothing about the stored groups)
     L += ["s_mov_b64 exec, -1",
-          "s_andn2_b32 %s, %s, %s" % (s(S_T0), s(S_PREVG), s(S_KMASK)),
+          # (one result slot: the group itself, whatever the superblock size the host chose)
+          "s_andn2_b32 %s, %s, %s" % (s(S_T0), s(S_PREVG), s(S_KMASK)) if RETK > 1 else
+          "s_mov_b32 %s, %s" % (s(S_T0), s(S_PREVG)),
           ] + (["v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),
                 "v_lshl_add_u32 %s, %s, 6, %s" % (v(R[1]), s(S_T0), v(R[1]))] if STAGED_IMAGE else
                ["v_mov_b32 %s, v%d" % (v(R[1]), V_IDX)]) + [

@@ -15,7 +15,7 @@ for cfg in "$@"; do
     mkdir -p $d
     timeout -s KILL 120 rocprofv3 --pmc $p --kernel-trace --kernel-include-regex 'ebpf_(interp|jit)' \
       --output-format csv -d $d -o pmc -- python3 bench.py --config $cfg --no-cpu-baseline \
-      --steps 3 --warmup 1 > $d/bench.json 2> $d/err.log || { tail -5 $d/err.log; exit 1; }
+      --steps 3 --warmup 1 ${BENCH_ARGS:-} > $d/bench.json 2> $d/err.log || { tail -5 $d/err.log; exit 1; }
     i=$((i+1))
   done
 done
