@@ -6,8 +6,12 @@ length 16..79 at CSR offsets (general kernels, short packets fault), and with re
 subtrees are queued and batched).
 Odd-numbered programs also call map_update_elem / map_delete_elem (the device batch semantics).
 Compares results, fault codes, post-run packet bytes and the maps after the batch.
+--hash: the programs' two maps are hashtables instead (4-byte keys, a random live subset of a
+key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts can hit EBUSY):
+lookups, updates and deletes against the oracle's replay model; the tables are compared through
+get_next_key's walk (order and values).
 
-  python tools/fuzz_gpu.py [--programs N] [--seed S] [--out DIR]
+  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
 import argparse
 import os
@@ -37,36 +41,75 @@ def ragged_packets(n, seed):
     return data, offs
 
 
-def case(k, seed, layout):
+def hash_spec(g, vs):
+    cap = int(g.choice([16, 256]))
+    universe = np.unique(np.concatenate([np.arange(8), g.integers(0, 256, 64),
+                                         g.integers(0, 2**32, 64)]).astype(np.uint64))
+    keys = g.permutation(universe)[:int(g.integers(0, cap + 1))]
+    items = [(int(x).to_bytes(4, "little"), g.bytes(vs)) for x in keys]
+    return pyoracle.HashSpec(4, vs, items=items, capacity=cap)
+
+
+def case(k, seed, layout, hashed=False):
     g = np.random.default_rng(seed * 7919 + k)
     vs = int(g.choice([8, 16]))
     me = int(g.choice([16, 256]))
     lay = randprog.random_program(seed * 100000 + k, length=int(g.integers(10, 120)), nmaps=2,
-                                  map_value_size=vs, writes=bool(k & 1))
-    maps = [(vs, me, g.integers(0, 256, vs * me, dtype=np.uint8).tobytes()) for _ in range(2)]
+                                  map_value_size=vs, writes=bool(k & 1) or hashed)
+    if hashed:
+        maps = [hash_spec(g, vs) for _ in range(2)]
+    else:
+        maps = [(vs, me, g.integers(0, 256, vs * me, dtype=np.uint8).tobytes()) for _ in range(2)]
     n = int(g.choice([1, 63, 64, 65, 777, 2048]))
     if layout == "staged":
-        return goldens.Case("r%d" % k, lay.code, lay.relocs, maps,
-                            workloads.packets_random(n, 64, seed=k), n, 64, None)
-    data, offs = ragged_packets(n, seed * 31 + k)
-    return goldens.Case("r%d" % k, lay.code, lay.relocs, maps, data, n, 0, offs)
+        c = goldens.Case("r%d" % k, lay.code, lay.relocs, [] if hashed else maps,
+                         workloads.packets_random(n, 64, seed=k), n, 64, None)
+    else:
+        data, offs = ragged_packets(n, seed * 31 + k)
+        c = goldens.Case("r%d" % k, lay.code, lay.relocs, [] if hashed else maps, data, n, 0, offs)
+    if hashed:
+        c.maps = maps
+    return c
 
 
 def oracle(c):
-    """(ret, faults, packet bytes after, map bytes after the batch)"""
+    """(ret, faults, packet bytes after, maps after the batch: array bytes / hashtable items)"""
     op = pyoracle.OracleProgram(c.code, c.relocs, c.maps)
     ret, faults, data, _ = op.run(c.data, c.count, c.stride, c.offsets, nthreads=8)
-    return ret, faults, data, [op.map_bytes(i) for i in range(len(c.maps))]
+    return ret, faults, data, [op.hash_models[i].items() if isinstance(m, pyoracle.HashSpec)
+                               else op.map_bytes(i) for i, m in enumerate(c.maps)]
+
+
+def walk(m):
+    """A device-side hashtable through the host API: get_next_key's walk with the values."""
+    import ctypes
+    out, prev = [], None
+    while True:
+        nk = ctypes.create_string_buffer(m.key_size)
+        k = None if prev is None else ctypes.create_string_buffer(prev, m.key_size)
+        if native.lib().ebpf_map_get_next_key_from_user(m.ptr, k, nk) != 0:
+            return out
+        prev = nk.raw
+        out.append((prev, m.lookup(prev)[1]))
 
 
 def device(env, c, variant):
-    maps = make_maps(native, env, c)
+    if isinstance(c.maps[0], pyoracle.HashSpec):
+        maps = []
+        for spec in c.maps:
+            m = native.HashMap(env, spec.key_size, spec.value_size, spec.capacity)
+            for kk, vv in spec.items:
+                assert m.update(kk, vv) == 0
+            maps.append(m)
+    else:
+        maps = make_maps(native, env, c)
     p = native.Prog(env, native.patch_relocs(c.code, c.relocs, [m.handle for m in maps]))
     try:
         native.set_variant(variant)
         data = np.ascontiguousarray(c.data.copy())
         ret, faults, _ = p.run_batch(data, c.count, c.stride, c.offsets)
-        after = [b"".join(m.lookup(i)[1] for i in range(m.max_entries)) for m in maps]
+        after = [walk(m) if isinstance(m, native.HashMap) else
+                 b"".join(m.lookup(i)[1] for i in range(m.max_entries)) for m in maps]
         return ret, faults, data, after
     finally:
         native.set_variant(0)
@@ -79,11 +122,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=500)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--hash", action="store_true", help="hashtable maps (lookups and writes)")
     a = ap.parse_args()
     env = native.Env()
     failed = False
     configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
-    configs += [(0, "general", 2), (0, "general", 1)]   # regrouping, size threshold 2 / 1
+    if not a.hash:
+        configs += [(0, "general", 2), (0, "general", 1)]   # regrouping, size threshold 2 / 1
     for variant, layout, rg in configs:
         if rg:
             os.environ["EBPF_CC_REGROUP"] = "1"
@@ -91,17 +136,19 @@ def main():
         t0 = time.time()
         bad, faults = [], 0
         for k in range(a.programs):
-            c = case(k, a.seed, layout)
+            c = case(k, a.seed, layout, a.hash)
             want, wf, wdata, wmaps = oracle(c)
             got, gf, gdata, gmaps = device(env, c, variant)
             faults += int(np.count_nonzero(wf))
             if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
                     np.array_equal(wdata, gdata) and wmaps == gmaps):
                 bad.append(k)
+            if k % 100 == 99:
+                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
         os.environ.pop("EBPF_CC_REGROUP", None)
         os.environ.pop("EBPF_CC_RG_MIN", None)
-        print("variant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            variant, layout, " regroup>=%d" % rg if rg else "", a.programs, faults, len(bad), bad[:20],
+        print("%svariant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+            "hash " if a.hash else "", variant, layout, " regroup>=%d" % rg if rg else "", a.programs, faults, len(bad), bad[:20],
             time.time() - t0), flush=True)
         failed = failed or bool(bad)
     env.destroy()
