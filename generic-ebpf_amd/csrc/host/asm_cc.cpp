@@ -245,6 +245,25 @@ struct facts {
 				r[q].hfwd = -1;
 		}
 	}
+	// d's VGPRs are overwritten with something else while its value facts stay true (a register
+	// dead from here on, reused as a scratch): nothing may read those VGPRs for d any more
+	void clobber_phys(int d)
+	{
+		pv[d] = false;
+		uint8_t k = 0;
+		for (uint8_t i = 0; i < nst; i++)
+			if (st[i].reg != d)
+				st[k++] = st[i];
+		nst = k;
+		for (int q = 0; q < AH_NREGS; q++) {
+			if (r[q].mreg == d) {
+				r[q].mp = -1;
+				r[q].mreg = -1;
+			}
+			if (r[q].hfwd == d)
+				r[q].hfwd = -1;
+		}
+	}
 	void store(uint32_t off, int size, int reg)
 	{
 		uint8_t k = 0;
@@ -2236,7 +2255,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 						em.call_routine(rt.hlookup, 0);
 						em.E.vop1(V1_MOV_B64, 2 * D, vreg(50));
 						f.def(0, rf());
-						f.def(D, rf());
+						// (D's value facts stay: the liveness that picked D was computed with
+						// them, so a compare they decided must stay decided — dropping them
+						// made such a compare read D's VGPRs, now the forwarded value)
+						f.clobber_phys(D);
 						f.r[0].hfwd = (int8_t)D;
 						f.t2zero = false;
 						ok = true;

@@ -50,12 +50,13 @@ def hash_spec(g, vs):
     return pyoracle.HashSpec(4, vs, items=items, capacity=cap)
 
 
-def case(k, seed, layout, hashed=False):
+def case(k, seed, layout, hashed=False, writes=None):
     g = np.random.default_rng(seed * 7919 + k)
     vs = int(g.choice([8, 16]))
     me = int(g.choice([16, 256]))
     lay = randprog.random_program(seed * 100000 + k, length=int(g.integers(10, 120)), nmaps=2,
-                                  map_value_size=vs, writes=bool(k & 1) or hashed)
+                                  map_value_size=vs,
+                                  writes=(bool(k & 1) or hashed) if writes is None else writes)
     if hashed:
         maps = [hash_spec(g, vs) for _ in range(2)]
     else:
