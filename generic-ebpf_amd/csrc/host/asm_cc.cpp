@@ -2244,9 +2244,23 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				// result (LDXHV) become register extracts (one memory round trip less)
 				if (!ok && final_pass && mi < (int)table.size() && (table[mi].flags & DP_MAP_HASH) &&
 				    dp_hash_key_size(table[mi].flags) <= 8 && getenv("EBPF_CC_NOHFWD") == nullptr) {
+					// D must also be free of every fact that reads its VGPRs through another name
+					// (a stack word forwarded from D, a map pointer indexed by D): dropping such a
+					// fact here, where the pass that computed liveness kept it, changes the facts
+					// downstream (a load forwarded there, a constant exit, dead code removed for
+					// it) — found by the hashtable fuzz mode
+					auto aliased = [&](int r) {
+						for (uint8_t i = 0; i < f.nst; i++)
+							if (f.st[i].reg == r)
+								return true;
+						for (int q = 0; q < AH_NREGS; q++)
+							if (f.r[q].mreg == r)
+								return true;
+						return false;
+					};
 					int D = -1;
 					for (int r = 9; r >= 2 && D < 0; r--)
-						if (!(live_out[e] & (1u << r)))
+						if (!(live_out[e] & (1u << r)) && !aliased(r))
 							D = r;
 					if (D >= 0) {
 						blk.reads |= (uint8_t)(1u << 4); // s14 = the map record offset
@@ -2257,7 +2271,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 						f.def(0, rf());
 						// (D's value facts stay: the liveness that picked D was computed with
 						// them, so a compare they decided must stay decided — dropping them
-						// made such a compare read D's VGPRs, now the forwarded value)
+						// made such a compare read D's VGPRs, now the forwarded value; with D
+						// unaliased, clobber_phys drops nothing else)
 						f.clobber_phys(D);
 						f.r[0].hfwd = (int8_t)D;
 						f.t2zero = false;

@@ -19,7 +19,8 @@
 
 enum {
 	F_NONE = 0, F_BAD_OPCODE = 1, F_DIV_ZERO = 2, F_MEM = 3, F_SLOT = 4, F_HELPER = 5,
-	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10
+	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10,
+	F_UNDEF = 100 /* oracle only (oracle_prog.track_undef): a read of a stack byte no store wrote */
 };
 
 #define STACK_BYTES 512
@@ -28,6 +29,7 @@ struct region_env {
 	uint64_t pkt_lo, pkt_hi;
 	uint64_t stk_lo, stk_hi;
 	const struct oracle_prog *p;
+	uint8_t *sdef; /* track_undef: 1 per stack byte a store wrote (NULL: not tracked) */
 };
 
 /* 0 = ok, else a fault code. write=1 for stores. */
@@ -39,8 +41,15 @@ check_access(const struct region_env *re, uint64_t addr, uint64_t size, int writ
 		return F_MEM;
 	if (addr >= re->pkt_lo && end <= re->pkt_hi)
 		return 0;
-	if (addr >= re->stk_lo && end <= re->stk_hi)
+	if (addr >= re->stk_lo && end <= re->stk_hi) {
+		if (re->sdef) {
+			uint8_t *d = re->sdef + (addr - re->stk_lo);
+			for (uint64_t i = 0; i < size; i++)
+				if (!write && !d[i]) /* (stores mark their bytes in taint_pre) */
+					return F_UNDEF;
+		}
 		return 0;
+	}
 	for (uint32_t m = 0; m < re->p->nmaps; m++) {
 		const struct oracle_map *mp = &re->p->maps[m];
 		uint64_t lo = (uint64_t)(uintptr_t)mp->data;
@@ -387,12 +396,95 @@ helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_
 	}
 }
 
+
+/* track_undef (test tooling): taint[r] = r holds a value derived from an address (r1, r10, a
+ * map handle, a lookup result), whose bits differ between the reference, this oracle and the
+ * device; a result, a packet byte, a branch or a map key that depends on one is undefined.
+ * The stack shadow sdef holds 2 for a byte of a stored tainted value.  Returns F_UNDEF or 0;
+ * called before the instruction executes (CALL results are tainted after it). */
+static int
+taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s, int16_t off,
+	  int32_t imm, const uint64_t *reg)
+{
+	const struct oracle_prog *p = re->p;
+	const int cls = op & 7;
+	if (d >= 11 || s >= 11)
+		return 0;
+	if (cls == 4 || cls == 7) { /* ALU32 / ALU64 */
+		const int x = op & 0x08, code = op & 0xf0;
+		if (code == 0xb0 && cls == 4) /* MOV32 */
+			taint[d] = x ? taint[s] : 0;
+		else if (code == 0x80 && cls == 4) /* NEG32 = -imm */
+			taint[d] = 0;
+		else if (x && code == 0x10 && taint[d] && taint[s]) /* pointer - pointer */
+			taint[d] = 0;
+		else if (x)
+			taint[d] |= taint[s];
+		return 0;
+	}
+	if (op == 0x18)
+		return 0; /* (taint_lddw after it executes: a map handle is an address) */
+	if (cls == 5) { /* JMP */
+		if (op == 0x05 || op == 0x95 || op == 0x85) {
+			if (op == 0x95 && taint[0])
+				return F_UNDEF;
+			if (op == 0x85 && imm >= 0 && imm < 64 && re->sdef) {
+				const int k = p->helper_kind[imm];
+				uint32_t ks = 4, vs = 0;
+				for (uint32_t m = 0; m < p->nmaps; m++)
+					if (p->maps[m].handle == reg[1]) {
+						if (p->maps[m].kind == ORACLE_MAP_HASH)
+							ks = p->maps[m].key_size;
+						vs = p->maps[m].value_size;
+					}
+				uint64_t rg[2] = {reg[2], reg[3]};
+				uint32_t sz[2] = {ks, k == ORACLE_HELPER_MAP_UPDATE ? vs : 0};
+				for (int q = 0; q < 2; q++)
+					for (uint32_t i = 0; i < sz[q]; i++) {
+						uint64_t a = rg[q] + i;
+						if (a >= re->stk_lo && a < re->stk_hi && re->sdef[a - re->stk_lo] == 2)
+							return F_UNDEF;
+					}
+			}
+			return 0;
+		}
+		const int x = op & 0x08;
+		if (taint[d] && !(x == 0 && imm == 0 && ((op & 0xf0) == 0x10 || (op & 0xf0) == 0x50)))
+			return F_UNDEF; /* (a NULL test of a lookup result is defined) */
+		if (x && taint[s])
+			return F_UNDEF;
+		return 0;
+	}
+	if (cls == 1) { /* LDX: a tainted stack byte taints the loaded value */
+		const int sz = (op & 0x18) == 0x10 ? 1 : (op & 0x18) == 0x08 ? 2 : (op & 0x18) == 0 ? 4 : 8;
+		uint64_t a = reg[s] + (uint64_t)(int64_t)off;
+		uint8_t t = 0;
+		if (re->sdef && a >= re->stk_lo && a + sz <= re->stk_hi)
+			for (int i = 0; i < sz; i++)
+				t |= re->sdef[a - re->stk_lo + i] == 2;
+		taint[d] = t;
+		return 0;
+	}
+	if (cls == 3 || cls == 2) { /* STX / ST */
+		const int sz = (op & 0x18) == 0x10 ? 1 : (op & 0x18) == 0x08 ? 2 : (op & 0x18) == 0 ? 4 : 8;
+		const uint8_t t = cls == 3 ? taint[s] : 0;
+		uint64_t a = reg[d] + (uint64_t)(int64_t)off;
+		if (re->sdef && a >= re->stk_lo && a + sz <= re->stk_hi) {
+			for (int i = 0; i < sz; i++)
+				re->sdef[a - re->stk_lo + i] = t ? 2 : 1;
+			return 0;
+		}
+		return t ? F_UNDEF : 0;
+	}
+	return 0;
+}
+
 static inline uint64_t
 run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, uint8_t *fault_out,
 	uint64_t *steps_out)
 {
 	uint64_t reg[11];
-	uint8_t stack[STACK_BYTES];
+	uint8_t stack[STACK_BYTES], sdef[STACK_BYTES];
 	struct region_env re;
 	uint64_t idx = 0; /* slot index; the reference keeps a pointer (inst) */
 	uint32_t pc = 0;  /* u32 as in ebpf_interpreter.c:26 */
@@ -410,6 +502,11 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	re.pkt_hi = re.pkt_lo + len;
 	re.stk_lo = (uint64_t)(uintptr_t)stack;
 	re.stk_hi = re.stk_lo + STACK_BYTES;
+	re.sdef = p->track_undef ? sdef : NULL;
+	if (re.sdef)
+		memset(sdef, 0, sizeof(sdef));
+	uint8_t taint[11] = {0};
+	taint[1] = taint[10] = 1;
 	re.p = p;
 
 	for (;;) {
@@ -444,6 +541,8 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		int taken = -1;                        /* -1: not a conditional jump */
 		int msize = 0;
 
+		if (re.sdef && (fault = taint_pre(&re, taint, op, d, s, off, imm, reg)))
+			break;
 		switch (op) {
 		/* ---- ALU32 :41-133 — operands truncated to u32, result zero-extended ---- */
 		case 0x0c: reg[d] = (uint32_t)(D32 + S32); break;
@@ -586,6 +685,13 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		}
 		if (fault)
 			break;
+		if (re.sdef && op == 0x85) /* a lookup result is an address (NULL is not) */
+			taint[0] = p->helper_kind[imm] == ORACLE_HELPER_MAP_LOOKUP && reg[0] != 0;
+		if (re.sdef && op == 0x18) {
+			taint[d] = 0;
+			for (uint32_t m = 0; m < p->nmaps; m++)
+				taint[d] |= p->maps[m].handle == reg[d];
+		}
 		if (taken > 0) {
 			uint32_t npc = pc + (uint32_t)(int32_t)off; /* pc += inst->offset (u32 wrap) */
 			/* next state (idx + npc, npc + 1) == current (idx, pc) → the reference spins forever */
@@ -621,7 +727,7 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	uint64_t *steps_out)
 {
 	uint64_t reg[11];
-	uint8_t stack[STACK_BYTES];
+	uint8_t stack[STACK_BYTES], sdef[STACK_BYTES];
 	struct region_env re;
 	uint64_t pc = 0, steps = 0, r0 = 0, back = 0;
 	int fault = F_NONE;
@@ -636,6 +742,9 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	re.pkt_hi = re.pkt_lo + len;
 	re.stk_lo = (uint64_t)(uintptr_t)stack;
 	re.stk_hi = re.stk_lo + STACK_BYTES;
+	re.sdef = p->track_undef ? sdef : NULL;
+	if (re.sdef)
+		memset(sdef, 0, sizeof(sdef));
 	re.p = p;
 
 	for (;;) {
@@ -887,7 +996,7 @@ run_raw(const struct oracle_prog *p, uint8_t *pkt, uint64_t *steps_out)
 	const struct raw_inst *ip = (const struct raw_inst *)p->insns;
 	uint32_t pc = 0;
 	uint64_t steps = 0;
-	struct region_env re = {0, 0, 0, 0, p};
+	struct region_env re = {0, 0, 0, 0, p, NULL};
 	for (int i = 0; i < 11; i++)
 		reg[i] = p->reg_init;
 	reg[1] = (uint64_t)(uintptr_t)pkt;

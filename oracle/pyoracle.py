@@ -88,7 +88,7 @@ class _Prog(ctypes.Structure):
                 ("helper_kind", ctypes.c_uint8 * 64), ("maps", ctypes.c_void_p),
                 ("nmaps", ctypes.c_uint32), ("reg_init", ctypes.c_uint64),
                 ("stack_init", ctypes.c_uint8), ("checked", ctypes.c_uint8),
-                ("semantics", ctypes.c_uint8)]
+                ("semantics", ctypes.c_uint8), ("track_undef", ctypes.c_uint8)]
 
 
 _lib = None
@@ -130,7 +130,7 @@ class OracleProgram:
     [(slot, map_index)] are patched with oracle handles here."""
 
     def __init__(self, code, relocs=(), maps=(), helper_kinds=None, checked=True,
-                 reg_init=0, stack_init=0, semantics=0):
+                 reg_init=0, stack_init=0, semantics=0, track_undef=False):
         b = bytearray(code)
         for slot, k in relocs:
             h = oracle_handle(k)
@@ -188,6 +188,7 @@ class OracleProgram:
         self.p.stack_init = stack_init
         self.p.checked = 1 if checked else 0
         self.p.semantics = semantics
+        self.p.track_undef = 1 if track_undef else 0
 
     def run(self, data, count, stride=0, offsets=None, nthreads=1):
         """Runs in place on a COPY of ``data``; returns (ret u64[count], faults u8[count],

@@ -243,3 +243,24 @@ def test_run_mask_code_shape(native, env):
     cmps_on = sum(ln.startswith("v_cmp_") for ln in on)
     cmps_off = sum(ln.startswith("v_cmp_") for ln in off)
     assert cmps_on < cmps_off, (cmps_on, cmps_off)
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+def test_hash_forwarding_register_alias_code(native, env):
+    """The register that receives a hashtable probe's value bytes is not one a stack word was
+    stored from: the fall-through exit of test_gpu_hash._forward_alias_program stays the
+    constant the liveness pass proved (0x5bd1e995 + 3), so no code it removed is read."""
+    import hashprogs
+    from test_gpu_hash import _forward_alias_program
+    lay = _forward_alias_program()
+    m = hashprogs.NativeHash(native, env, 4, 8, 16, [])
+    try:
+        p = native.Prog(env, native.patch_relocs(lay.code, lay.relocs, [m.handle]))
+        try:
+            out, _ = _decode(p.device_code(1))
+        finally:
+            p.destroy()
+    finally:
+        m.destroy()
+    assert "v_mov_b32_e32 v44, 0x5bd1e998" in out
+    assert "v_mov_b64_e32 v[14:15], v[50:51]" not in out   # (r7: the key was stored from it)

@@ -271,3 +271,44 @@ def test_hash_long_keys(gpu, env, variant, ks, src, stride):
     np.testing.assert_array_equal(gf, wf)
     np.testing.assert_array_equal(got, want)
     assert (want != 0xdead).any() and (want == 0xdead).any()
+
+
+def _forward_alias_program():
+    """Hashtable value forwarding (asm_cc.cpp AHF_HLOOKUP) must not reuse a register whose value
+    another name still reaches: r7 is dead after the lookup as a register, but the key's stack
+    word was stored from it and a later stack load is forwarded from r7.  Reusing r7 for the
+    probe's value bytes dropped that forwarding in the final pass only, so the exit the
+    liveness pass had proven constant read a register it had removed the code for (fuzz_gpu.py
+    --hash case 126, shrunk)."""
+    I, Branch, LdDw, MapRef, assemble = hashprogs._mods()
+    R0, R1, R2, R3, R6, R7, R8, R9, R10 = 0, 1, 2, 3, 6, 7, 8, 9, 10
+    nodes = [
+        I("ldxb", R8, R1, 3), I("ldxb", R9, R1, 4),   # live across the lookup
+        I("mov_imm", R7, imm=3), I("stxw", R10, R7, -4),
+        LdDw(R1, MapRef(0)),
+        I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+        I("call", imm=0),
+        Branch(I("jeq_imm", R0, imm=0), [I("mov_imm", R0, imm=1), I("exit")]),
+        I("ldxb", R6, R0, 5),
+        Branch(I("jeq_reg", R8, R9), [I("mov64_reg", R0, R6), I("exit")]),
+        # r0 = a constant + the key's low byte, read back through the stack (forwarded from r7)
+        I("mov_imm", R0, imm=0x5bd1e995), I("ldxb", R3, R10, -4), I("add64_reg", R0, R3),
+        I("exit"),
+    ]
+    return assemble(nodes)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_hash_forwarding_register_alias(gpu, env, variant):
+    lay = _forward_alias_program()
+    rng = np.random.default_rng(126)
+    items = [(int(k).to_bytes(4, "little"), rng.bytes(8)) for k in range(8) if k != 5]
+    spec = pyoracle.HashSpec(4, 8, items=items, capacity=16)
+    n = 777
+    pk = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    pk[::3, 4] = pk[::3, 3]   # both exits taken
+    want, wf, _ = hashprogs.oracle(lay, [spec], pk.reshape(-1), n, 64)
+    got, gf = run_device(gpu, env, lay, [spec], pk.reshape(-1), n, 64, variant=variant, max_entries=16)
+    assert not wf.any()
+    assert np.array_equal(wf, gf)
+    assert np.array_equal(want, got), int((want != got).sum())
