@@ -10,6 +10,10 @@
 // longer than the last limit, or not 16-byte aligned (the span DMA reads aligned 16-B blocks).
 // Class k >= 1: lim[k-1] < length <= lim[k], 16-B aligned.
 //
+// Path-sorted launches (gpu_runtime.cpp launch_pathsorted) sort by a byte per packet instead: the
+// fault code the classifying run left (code_base + q at cut point q: class q + 1; anything else:
+// class 0).
+//
 // Two kernels over contiguous tiles of the batch: bucket_count (per tile and class counts), then
 // bucket_scatter (each tile's base per class from the counts before it; ranks in packet order by
 // wave ballots), which also writes the class table cls[k] = {start, count} the launches read.
@@ -24,6 +28,10 @@ constexpr int kThreads = 256;
 __device__ inline uint32_t
 klass(const bucket_args &a, uint64_t i)
 {
+	if (a.code) {
+		const uint32_t c = (uint32_t)a.code[i] - a.code_base; // (below code_base: wraps, class 0)
+		return c + 1 < a.nclass ? c + 1 : 0;
+	}
 	const uint64_t o0 = a.offsets[i], o1 = a.offsets[i + 1];
 	const uint64_t len = o1 - o0; // (a decreasing offset is a huge length: class 0)
 	const uint64_t addr = (uint64_t)(uintptr_t)a.data + (o0 - a.off_base);
@@ -91,6 +99,10 @@ bucket_scatter(bucket_args a)
 				a.cls[2 * k + 1] = t;
 			}
 			start += t;
+		}
+		if (blockIdx.x == 0) { // (the whole batch as one slot range: path-sorted launches)
+			a.cls[2 * kBucketMaxClass] = 0;
+			a.cls[2 * kBucketMaxClass + 1] = (uint32_t)a.count;
 		}
 	}
 	__syncthreads();

@@ -1835,6 +1835,75 @@ cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const st
 }
 
 void
+cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
+		 uint32_t max_cuts, std::vector<uint32_t> &cuts)
+{
+	uint32_t min_size = 96; // (as regrouping: both sides of the divergent conditional this long)
+	if (const char *m = getenv("EBPF_PATHSORT_MIN"))
+		min_size = (uint32_t)atoi(m);
+	const size_t n = low.size();
+	auto fam_of = [&](uint32_t e) { return (int)ah_fam[(uint32_t)low[e].handler]; };
+	auto is_term = [&](uint32_t e) { return fam_of(e) == AHF_EXIT || fam_of(e) == AHF_FAULT; };
+	auto is_cond = [&](uint32_t e) { return (ah_flags[(uint32_t)low[e].handler] & 1) != 0; };
+	// what the classifying run may execute: no store that can reach the packet or a map value,
+	// no map write (the main run executes it again from the packet as the caller gave it)
+	auto prefix_ok = [&](int fam) {
+		return !((fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) ||
+			 fam == AHF_UPDATE || fam == AHF_HDELETE || fam == AHF_LOOPINIT || fam == AHF_LOOPCNT);
+	};
+	std::vector<uint32_t> parent(n, UINT32_MAX), npred(n, 0), sz(n, 0);
+	for (uint32_t e : order) {
+		if (is_term(e))
+			continue;
+		const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
+		for (uint32_t c : ch)
+			if (c < n) {
+				npred[c]++;
+				parent[c] = e;
+			}
+	}
+	for (size_t k = order.size(); k-- > 0;) {
+		const uint32_t e = order[k];
+		uint32_t size = 1;
+		if (!is_term(e)) {
+			const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
+			for (uint32_t c : ch)
+				if (c < n)
+					size += sz[c];
+		}
+		sz[e] = size;
+	}
+	// pre[e]: every entry on the path from the start to e (e excluded) is prefix_ok
+	std::vector<char> pre(n, 0), cand(n, 0), below(n, 0);
+	for (uint32_t e : order) {
+		const uint32_t p = parent[e];
+		pre[e] = e == xl.start ? 1 : (p < n && npred[e] == 1 && pre[p] && prefix_ok(fam_of(p)));
+		if (e != xl.start && pre[e] && p < n && is_cond(p) && sz[e] >= min_size) {
+			const uint32_t o = xl.entries[p].next == e ? xl.entries[p].target : xl.entries[p].next;
+			cand[e] = o < n && sz[o] >= min_size;
+		}
+	}
+	for (size_t k = order.size(); k-- > 0;) {
+		const uint32_t e = order[k];
+		if (is_term(e))
+			continue;
+		const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
+		for (uint32_t c : ch)
+			if (c < n)
+				below[e] = below[e] || cand[c] || below[c];
+	}
+	for (uint32_t e : order)
+		if (cand[e] && !below[e])
+			cuts.push_back(e);
+	if (cuts.size() > max_cuts) { // the heaviest keep their class; the rest run as "other"
+		std::stable_sort(cuts.begin(), cuts.end(), [&](uint32_t a, uint32_t b) { return sz[a] > sz[b]; });
+		cuts.resize(max_cuts);
+	}
+	if (cuts.size() < 2)
+		cuts.clear();
+}
+
+void
 cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t sched_off,
 	     std::vector<uint8_t> &out)
 {

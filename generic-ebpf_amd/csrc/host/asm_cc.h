@@ -56,6 +56,14 @@ struct cc_regroup_point {
 void cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low,
 		     const std::vector<uint32_t> &order, std::vector<cc_regroup_point> &points);
 
+// Path-sorted launches (gpu_runtime.cpp launch_pathsorted; general kernels, compiled programs):
+// the cut points of the classifying run — heads of subtrees that both sides of a divergent
+// conditional make heavy, the deepest, none inside another, at most max_cuts (the heaviest) —
+// whose path from the start holds no store that may reach the packet or a map and no map write.
+// Empty when fewer than two qualify.
+void cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low,
+		      const std::vector<uint32_t> &order, uint32_t max_cuts, std::vector<uint32_t> &cuts);
+
 // Bytes of one queue: u32 packet indices [128], then u64 [128] per live-register slot.
 inline uint32_t
 cc_queue_bytes(uint32_t live_slots)

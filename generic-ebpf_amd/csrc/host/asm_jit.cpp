@@ -140,7 +140,66 @@ fits_simm16(int64_t bytes)
 	return (bytes % 4) == 0 && w >= -32768 && w <= 32767;
 }
 
+// Layout order of the lowered entries: depth-first from the start, the not-taken successor
+// falls through (parents before their children).
+std::vector<uint32_t>
+layout_order(const dprog_host &xl, const std::vector<dp_entry> &low)
+{
+	const size_t n = low.size();
+	std::vector<uint32_t> order;
+	order.reserve(n);
+	std::vector<char> placed(n, 0);
+	std::vector<uint32_t> stack{xl.start};
+	while (!stack.empty()) {
+		uint32_t cur = stack.back();
+		stack.pop_back();
+		while (cur < n && !placed[cur]) {
+			placed[cur] = 1;
+			order.push_back(cur);
+			const uint32_t h = (uint32_t)low[cur].handler;
+			if (is_terminal(h))
+				break;
+			if (ah_flags[h] & 1) {
+				const uint32_t tk = xl.entries[cur].target;
+				if (tk < n && !placed[tk])
+					stack.push_back(tk);
+			}
+			cur = xl.entries[cur].next;
+		}
+	}
+	return order;
+}
+
 } // namespace
+
+// Path-sorted launches (gpu_runtime.cpp launch_pathsorted): the classifying prefix of the
+// program, as a program of its own — the translation with every cut point of
+// cc_pathsort_plan (on the general kernels' lowering) replaced by a FAULT entry of code
+// kPathCutCode + q, so that a lane's fault byte says which heavy subtree it reaches (0 or a real
+// fault code: none, it exits or faults before).  ENOENT: fewer than two cut points.
+int
+asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint32_t max_cuts,
+		    dprog_host *prefix, uint32_t *ncuts, std::string *err)
+{
+	std::vector<dp_entry> low;
+	uint32_t stride = 0;
+	int e = asm_lower(xl, 0, table, low, &stride, err);
+	if (e)
+		return e;
+	std::vector<uint32_t> cuts;
+	cc_pathsort_plan(xl, low, layout_order(xl, low), max_cuts, cuts);
+	if (cuts.empty())
+		return ENOENT;
+	*prefix = xl;
+	for (size_t q = 0; q < cuts.size(); q++) {
+		dp_entry &x = prefix->entries[cuts[q]];
+		memset(&x, 0, sizeof(x));
+		x.kind = DK_FAULT;
+		x.aux = (uint16_t)(kPathCutCode + q);
+	}
+	*ncuts = (uint32_t)cuts.size();
+	return 0;
+}
 
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
@@ -173,28 +232,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	const uint32_t cs_len = tsize(JT_CS, JT_CS_END), cl_len = tsize(JT_CL, JT_CL_END);
 	const uint32_t jl_len = tsize(JT_JL, JT_JL_END);
 
-	// layout order: depth-first, not-taken successor falls through
-	std::vector<uint32_t> order;
-	order.reserve(n);
+	const std::vector<uint32_t> order = layout_order(xl, low);
 	std::vector<char> placed(n, 0);
-	std::vector<uint32_t> stack{xl.start};
-	while (!stack.empty()) {
-		uint32_t cur = stack.back();
-		stack.pop_back();
-		while (cur < n && !placed[cur]) {
-			placed[cur] = 1;
-			order.push_back(cur);
-			const uint32_t h = (uint32_t)low[cur].handler;
-			if (is_terminal(h))
-				break;
-			if (ah_flags[h] & 1) {
-				const uint32_t tk = xl.entries[cur].target;
-				if (tk < n && !placed[tk])
-					stack.push_back(tk);
-			}
-			cur = xl.entries[cur].next;
-		}
-	}
+	for (uint32_t e : order)
+		placed[e] = 1;
 	// successor that must follow each block (UINT32_MAX: none)
 	auto succ = [&](uint32_t e) -> uint32_t {
 		const uint32_t h = (uint32_t)low[e].handler;

@@ -39,6 +39,8 @@ int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<
 		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
 		  uint32_t *rq_wave_bytes);
 void asm_jit_release(void *mod);
+int asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint32_t max_cuts,
+			dprog_host *prefix, uint32_t *ncuts, std::string *err);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
 		 uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes = nullptr);
@@ -714,6 +716,123 @@ launch_bucketed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 	return 0;
 }
 
+// Path-sorted launch of a large batch (offsets form) of a compiled program on the general kernels
+// whose tree splits into heavy subtrees (cc_pathsort_plan).  Three steps on the stream:
+//   1. the classifying run: the program's prefix, compiled with every cut point a FAULT of code
+//      kPathCutCode + q (asm_pathsort_prefix), over the batch, into scratch results and faults;
+//   2. bucket.hip sorts the packet indices by that byte (class q + 1 for cut q, class 0 for a
+//      packet that exits or faults before any cut), stable, so a class keeps packet order;
+//   3. the whole program over the sorted order (slot mode, 64 packets per group): a group's
+//      lanes follow one path through the prefix into one subtree, instead of every subtree its
+//      packets take (C5: about 12 per group).
+// The main run re-executes the prefix from the packets as given: the prefix holds no store
+// that may reach the packet or a map and no map write, and maps are read-only during a batch,
+// so it takes the same path.  Every packet keeps its own result, fault and verdict.
+constexpr uint64_t kPathMin = 1u << 16; // smaller batches: one plain launch
+
+bool
+pathsort_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
+{
+	// opt-in (EBPF_PATHSORT=1) until it beats the plain launch on C5;
+	// EBPF_PATHSORT_MINBATCH=n lowers the batch threshold (tests)
+	const char *on = getenv("EBPF_PATHSORT");
+	if (!(on && *on == '1'))
+		return false;
+	uint64_t min = kPathMin;
+	if (const char *m = getenv("EBPF_PATHSORT_MINBATCH"))
+		min = strtoull(m, nullptr, 0);
+	return L.offsets != nullptr && L.count >= min && L.count < kBucketMax &&
+	       ep->xlated->max_updates == 0 && dp->jit_rq_bytes[0] == 0 && dp->ps_err == 0;
+}
+
+int
+pathsort_entries(struct ebpf_prog *ep, dprog_device *dp)
+{
+	std::lock_guard<std::mutex> g(ep->dlock);
+	if (dp->ps_fn)
+		return 0;
+	if (dp->ps_err)
+		return dp->ps_err;
+	std::string msg;
+	dprog_host prefix;
+	int err = asm_pathsort_prefix(*ep->xlated, dp->table, kPathMaxCuts, &prefix, &dp->ps_ncuts, &msg);
+	uint32_t rq = 0;
+	if (err == 0)
+		err = asm_jit_build(dp->device, prefix, 0, dp->table, &dp->ps_mod, &dp->ps_fn, &dp->ps_stride,
+				    &msg, &rq);
+	if (err == 0 && rq != 0)
+		err = ENOENT; // (regroup queues in the prefix: not combined)
+	dp->ps_err = err;
+	return err;
+}
+
+int
+launch_pathsorted(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
+		  hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
+		  bool *done)
+{
+	*done = false;
+	if (pathsort_entries(ep, dp) != 0)
+		return 0; // (no cut points: the plain launch)
+	uint32_t tile;
+	const uint32_t tiles = bucket_tiles(L.count, &tile);
+	const size_t perm_bytes = (L.count * 4 + 255) & ~(size_t)255;
+	const size_t blk_bytes = (size_t)kBucketMaxTiles * kBucketMaxClass * 4;
+	const size_t ret_bytes = L.count * 8, flt_bytes = (L.count + 255) & ~(size_t)255;
+	uint8_t *bk;
+	int err = bk_acquire(dp->device, stream, perm_bytes + blk_bytes + 256 + ret_bytes + flt_bytes, &bk);
+	if (err)
+		return fail(err, "path-sort buffer");
+	bucket_args a;
+	memset(&a, 0, sizeof(a));
+	a.offsets = L.offsets;
+	a.off_base = L.off_base;
+	a.data = L.data;
+	a.count = L.count;
+	a.nclass = dp->ps_ncuts + 1;
+	a.tile = tile;
+	a.perm = reinterpret_cast<uint32_t *>(bk);
+	a.blk_cnt = reinterpret_cast<uint32_t *>(bk + perm_bytes);
+	a.cls = reinterpret_cast<uint32_t *>(bk + perm_bytes + blk_bytes);
+	uint64_t *pret = reinterpret_cast<uint64_t *>(bk + perm_bytes + blk_bytes + 256);
+	uint8_t *pflt = bk + perm_bytes + blk_bytes + 256 + ret_bytes;
+	a.code = pflt;
+	a.code_base = kPathCutCode;
+	hipError_t e;
+	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	// 1. the classifying run (no verdicts: scratch results and fault bytes only)
+	dp_launch Lp = L;
+	Lp.ret = pret;
+	Lp.faults = pflt;
+	Lp.hist = nullptr;
+	Lp.hist_rows = nullptr;
+	Lp.stack_stride = dp->ps_stride;
+	e = launch_interp_asm(Lp, stream, dp->device, 0, dp->map_lds_bytes, dp->ps_fn, 0, nullptr, nullptr,
+			      nullptr, false);
+	if (e != hipSuccess)
+		return hip_fail(e, "path-sort classifying launch");
+	// 2. the packet indices by class
+	if ((e = launch_bucket(a, tiles, stream)) != hipSuccess)
+		return hip_fail(e, "path-sort bucketing kernels");
+	// 3. the program over the sorted order: one slot range, the whole batch (cls[kBucketMaxClass])
+	dp_launch Lm = L;
+	Lm.perm = a.perm;
+	Lm.perm_cls = a.cls + 2 * kBucketMaxClass;
+	Lm.span_slot = 0;
+	Lm.span_g = 64;
+	Lm.span_magic_g = (uint32_t)((0x100000000ull + 63) / 64);
+	e = launch_interp_asm(Lm, stream, dp->device, 0, dp->map_lds_bytes, dp->jit_fn[0], 0, nullptr,
+			      nullptr, user_hist, overwrite);
+	if (e != hipSuccess)
+		return hip_fail(e, "path-sorted launch");
+	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	dp->last_layout = 3;
+	*done = true;
+	return 0;
+}
+
 // A shard's write log brought to the host (a batch whose shards ran on several devices: the
 // logs are merged there, in global packet order).  Records as on the device (map_writes.h);
 // `first` = the global index of the shard's packet 0.
@@ -902,6 +1021,10 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		    (err = launch_bucketed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
 					   &done)))
 			return err;
+		if (!done && fn && mode == 0 && pathsort_wanted(ep, dp, L) &&
+		    (err = launch_pathsorted(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
+					     &done)))
+			return err;
 		e = done ? hipSuccess
 			 : launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
 					     (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
@@ -1049,6 +1172,7 @@ prog_release_device_state(struct ebpf_prog *ep)
 					hipFree(a);
 			for (auto *m : dp->jit_mod)
 				asm_jit_release(m);
+			asm_jit_release(dp->ps_mod);
 		}
 	}
 	ep->dev.clear();
@@ -1241,7 +1365,7 @@ ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *
 EBPF_EXPORT int
 ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 {
-	if (ep == nullptr || len == nullptr || layout < 0 || layout > 2)
+	if (ep == nullptr || len == nullptr || layout < 0 || layout > 3)
 		return fail(EINVAL, "bad argument");
 	std::lock_guard<std::mutex> g(ep->dlock);
 	int err = ensure_translated(ep);
@@ -1256,7 +1380,15 @@ ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 	std::vector<unsigned char> img, code;
 	uint32_t stride = 0;
 	std::string msg;
-	err = asm_jit_emit(*ep->xlated, layout, table, &img, &code, &stride, &msg);
+	if (layout == 3) { // the classifying prefix of a path-sorted launch (general kernels)
+		dprog_host prefix;
+		uint32_t ncuts = 0;
+		err = asm_pathsort_prefix(*ep->xlated, table, kPathMaxCuts, &prefix, &ncuts, &msg);
+		if (err == 0)
+			err = asm_jit_emit(prefix, 0, table, &img, &code, &stride, &msg);
+	} else {
+		err = asm_jit_emit(*ep->xlated, layout, table, &img, &code, &stride, &msg);
+	}
 	if (err)
 		return fail(err, msg);
 	const size_t cap = *len;

@@ -105,6 +105,11 @@ constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 // itself (variant 2): one result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU
 // are resident instead of 6 (gen_interp.py NSGPR_INTERP).
 constexpr int kModes = 3;
+// Path-sorted launches: the fault code a lane of the classifying run retires with at cut point q
+// (kPathCutCode + q; real fault codes are below), and the most cut points (classes 1..15 of
+// bucket.hip, class 0 = no cut reached)
+constexpr uint32_t kPathCutCode = 64;
+constexpr uint32_t kPathMaxCuts = 15;
 constexpr int kInterpStagedImage = 3;
 extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
     ebpf_asm_hsaco_m3[];
@@ -138,6 +143,13 @@ struct dprog_device {
 	uint32_t jit_stride[kModes] = {};
 	uint32_t jit_rq_bytes[kModes] = {};      // regroup queue bytes per wave (0: none)
 	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
+	// path-sorted launches (gpu_runtime.cpp launch_pathsorted): the classifying prefix, compiled
+	// for the general kernels (asm_pathsort_prefix), built on first use
+	void *ps_mod = nullptr;
+	void *ps_fn = nullptr;
+	uint32_t ps_stride = 0;
+	uint32_t ps_ncuts = 0;
+	int ps_err = 0;                          // ENOENT: no cut points (plain launches)
 	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
 	uint64_t win_words = 0;                  // winner words the apply step needs

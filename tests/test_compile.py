@@ -264,3 +264,28 @@ def test_hash_forwarding_register_alias_code(native, env):
         m.destroy()
     assert "v_mov_b32_e32 v44, 0x5bd1e998" in out
     assert "v_mov_b64_e32 v[14:15], v[50:51]" not in out   # (r7: the key was stored from it)
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+def test_pathsort_prefix_code(native, env):
+    """The classifying prefix of a path-sorted launch (layout 3): C5's tree is cut at its 12
+    leaf subtrees (fault codes 64..75 through s14, the fault routine's operand), the code is a
+    small fraction of the whole program's, and a program without heavy subtrees has none."""
+    import re
+    from generic_ebpf_amd import workloads
+    p = native.Prog(env, workloads.prog_c5().code)
+    try:
+        whole = p.device_code(0)
+        prefix = p.device_code(3)
+        out, err = _decode(prefix)
+        assert "invalid" not in err
+        assert len(prefix) * 10 < len(whole)
+        assert len(re.findall(r"s_mov_b32 s52, s14", out)) == 12
+    finally:
+        p.destroy()
+    p = native.Prog(env, workloads.prog_c3().code)
+    try:
+        with pytest.raises(native.EbpfError):
+            p.device_code(3)
+    finally:
+        p.destroy()
