@@ -290,7 +290,7 @@ def _forward_alias_program():
         I("call", imm=0),
         Branch(I("jeq_imm", R0, imm=0), [I("mov_imm", R0, imm=1), I("exit")]),
         I("ldxb", R6, R0, 5),
-        Branch(I("jeq_reg", R8, R9), [I("mov64_reg", R0, R6), I("exit")]),
+        Branch(I("jeq_reg", R8, R9), [I("mov_reg", R0, R6), I("exit")]),
         # r0 = a constant + the key's low byte, read back through the stack (forwarded from r7)
         I("mov_imm", R0, imm=0x5bd1e995), I("ldxb", R3, R10, -4), I("add64_reg", R0, R3),
         I("exit"),
