@@ -455,3 +455,54 @@ def test_literal_slot_programs(gpu, env, variant):
             got, gf, _ = device_run(gpu, env, c, variant)
             np.testing.assert_array_equal(want, got)
             np.testing.assert_array_equal(wf, gf)
+
+
+def test_per_thread_stream_histograms(gpu, env):
+    """hipStreamPerThread is one handle naming a different stream in each thread: two threads
+    launching on it concurrently, each into its own histogram, must each get exact counts (the
+    library keys its per-stream verdict partials by (handle, thread) for that handle)."""
+    import threading
+    import torch
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c4()
+    n = 1 << 20
+    pk = workloads.packets_l2l3(n, 64, seed=43)
+    vals = workloads.c4_map_values()
+    case = goldens.Case("c4", lay.code, lay.relocs, [(8, 256, vals.tobytes())], pk, n, 64, None)
+    want, _, _, _ = oracle_run(case, nthreads=8)
+    maps = make_maps(gpu, env, case)
+    p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle for m in maps]))
+    per_thread = 2  # hipStreamPerThread
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        rounds, nthr = 20, 2
+        rets = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(nthr)]
+        hists = [torch.zeros(257, dtype=torch.int64, device=dev) for _ in range(nthr)]
+        torch.cuda.synchronize()
+        errors = []
+
+        def worker(t):
+            try:
+                gpu.lib().ebpf_gpu_set_device(0)
+                for r in range(rounds):
+                    p.run_batch_dev(0, d_pk.data_ptr(), n, 64, rets[t].data_ptr(), None, None,
+                                    hists[t].data_ptr(), per_thread, hist_overwrite=(r == 0))
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthr)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        torch.cuda.synchronize()
+        assert not errors, errors
+        exp = np.bincount(np.minimum(want, 255).astype(np.int64), minlength=257) * rounds
+        for d_ret, h in zip(rets, hists):
+            np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+            np.testing.assert_array_equal(h.cpu().numpy(), exp)
+    finally:
+        p.destroy()
+        for m in maps:
+            m.destroy()
