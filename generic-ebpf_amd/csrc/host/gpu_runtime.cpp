@@ -693,14 +693,18 @@ launch_bucketed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 		return hip_fail(e, "hipEventRecord");
 	if ((e = launch_bucket(a, tiles, stream)) != hipSuccess)
 		return hip_fail(e, "bucketing kernels");
+	// (EBPF_BUCKET_NOSPAN=1, A/B: every class on the general kernels, 64 packets per group —
+	// length-sorted groups without the LDS staging)
+	const bool nospan = getenv("EBPF_BUCKET_NOSPAN") != nullptr;
 	for (uint32_t k = 0; k < nclass; k++) {
-		const int mode = k ? 2 : 0;
+		const int mode = k && !nospan ? 2 : 0;
+		const uint32_t g = mode == 2 ? G[k] : 64;
 		dp_launch Lk = L;
 		Lk.perm = a.perm;
 		Lk.perm_cls = a.cls + 2 * k;
-		Lk.span_slot = kSpanClasses[k].slot;
-		Lk.span_g = G[k];
-		Lk.span_magic_g = (uint32_t)((0x100000000ull + G[k] - 1) / G[k]);
+		Lk.span_slot = mode == 2 ? kSpanClasses[k].slot : 0;
+		Lk.span_g = g;
+		Lk.span_magic_g = (uint32_t)((0x100000000ull + g - 1) / g);
 		Lk.stack_stride = dp->jit_stride[mode];
 		if (mode == 2)
 			Lk.lds_pkt_base = 0; // (no header staging: every load reads the LDS slot)
