@@ -292,6 +292,10 @@ def cpu_baseline(w, budget_s):
                           mp, thr, mel, sp, core, sel)}
 
 
+DIST_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
 def pmc_traffic(a, w, total, layout, cfg=None):
     """HBM bytes per launch of the engine's kernel, from two rocprofv3 --pmc child passes of
     this script on the same workload (each counter group in a run of its own, kernel trace
@@ -318,7 +322,10 @@ def pmc_traffic(a, w, total, layout, cfg=None):
         cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc"] + list(group) + ["--kernel-trace",
                "--kernel-include-regex", "ebpf_(interp|jit)", "--output-format", "csv",
                "-d", d, "-o", "pmc", "--"] + child
-        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+        # (a single-process child: at N > 1 rank 0 measures its own shard's launch on its GPU, so
+        # the launcher's rendezvous variables are not passed on)
+        env = {k: v for k, v in os.environ.items() if k not in DIST_ENV and not k.startswith("TORCHELASTIC_")}
+        env["TMPDIR"] = os.environ.get("TMPDIR", "/tmp")
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
         if r.returncode != 0:
             return None, "%s pass exited %d: %s" % (counter, r.returncode,
@@ -533,8 +540,8 @@ def main():
         except Exception as e:  # reported in the line; the primary measurement stands
             also[c] = {"error": "%s: %s" % (type(e).__name__, e)}
             continue
-        if rank == 0 and not a.no_pmc and world == 1:  # the same PMC passes as the primary line
-            t, err = pmc_traffic(a, S["w"], S["total"], S["layout"], c)
+        if rank == 0 and not a.no_pmc:  # the same PMC passes as the primary line
+            t, err = pmc_traffic(a, S["w"], S["n"] if world > 1 else S["total"], S["layout"], c)
             S["traffic"], S["traffic_note"] = (t["bytes"], t["note"]) if t else (None, err)
             S["issue"] = (issue_roofline(t["insts"], S["kern_ms"], (S["n"] + 63) // 64)
                           if t and t["insts"] else None)
@@ -546,7 +553,7 @@ def main():
                                 "unit": "GB/s", "frac": round(S["achieved"] / PEAK_HBM_GBS, 4),
                                 "kernel_ms": round(S["kern_ms"], 4), "kernel_ms_stats": S["kern_stats"],
                                 "traffic": S.get("traffic"),
-                                "traffic_note": S.get("traffic_note", "not collected (N > 1 or --no-pmc)"),
+                                "traffic_note": S.get("traffic_note", "disabled (--no-pmc)"),
                                 "algorithmic_bytes_per_launch": S["bytes_per_launch"],
                                 "issue": S.get("issue")},
                    "desc": workloads.CONFIGS[c]["desc"]}
@@ -555,10 +562,10 @@ def main():
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(w, a.cpu_seconds)
-        traffic, pmc_note = None, "not collected (N > 1)" if world > 1 else "disabled (--no-pmc)"
+        traffic, pmc_note = None, "disabled (--no-pmc)"
         issue = None
-        if not a.no_pmc and world == 1:
-            t, err = pmc_traffic(a, w, total, layout)
+        if not a.no_pmc:   # (N > 1: rank 0's shard, one launch on its GPU, as the roofline's)
+            t, err = pmc_traffic(a, w, n if world > 1 else total, layout)
             traffic, pmc_note = (t["bytes"], t["note"]) if t else (None, err)
             if t and t["insts"]:
                 issue = issue_roofline(t["insts"], kern_ms, (n + 63) // 64)
