@@ -136,6 +136,22 @@ int main(int argc, char **argv) {
 	(void)hipMalloc(&out, npk * 8);
 	(void)hipMemset(in, 1, npk * 64);
 	const int cus = 256;
+	if (argc > 1 && argv[1][0] == 'k') {
+		// result-burst length K beyond the kernel's 8 (round 3): 8, 16, 32 groups per burst,
+		// u64 per lane (ST 0) or staged in LDS and written as 16-B lanes (ST 3), 16 / 24 waves
+		for (int rep = 0; rep < 2; rep++) {
+			run<1, 8, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 16, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 32, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 3, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 16, 3, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<2, 16, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 24);
+			run<1, 16, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 24);
+			run<1, 8, 2, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+		}
+		return 0;
+	}
 	if (argc > 1 && argv[1][0] == 'o') {
 		// occupancy x prefetch depth, with a little per-group work (the staged kernel at 4
 		// workgroups per CU, round 1)
