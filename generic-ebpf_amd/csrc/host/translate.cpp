@@ -404,6 +404,21 @@ struct Translator {
 			di++;
 			out.entries[from].target = get(k >> 32, (uint32_t)k, &created);
 		}
+		// A conditional jump of offset 0 goes to the same state taken or not (reference: pc += 0
+		// leaves the next state (idx + pc, pc + 1) unchanged, ebpf_interpreter.c:209-211;
+		// standard: pc + 1 + 0).  Its compare has no effect, so it becomes ADD64 dst, 0: the
+		// state graph keeps one edge per entry (the device's structured control flow and every
+		// pass that walks the tree rely on that; fuzz_gpu.py --standard found it).
+		for (dp_entry &x : out.entries) {
+			const uint8_t cls = x.kind < 0x100 ? (x.kind & 7) : 0xff;
+			if ((cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32) && x.kind != EBPF_OP_JA &&
+			    x.kind != EBPF_OP_CALL && x.kind != EBPF_OP_EXIT && x.target == x.next) {
+				x.kind = EBPF_OP_ADD64_IMM;
+				x.imm = 0;
+				x.src = 0;
+				x.off = 0;
+			}
+		}
 		if (!overflow && out.has_loops) { // every lane's loop count starts at 0
 			const uint32_t init = new_entry();
 			out.entries[init].kind = DK_LOOPINIT;

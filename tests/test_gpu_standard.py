@@ -116,3 +116,46 @@ def test_loop_programs_vs_oracle(gpu, env, variant):
         if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
             bad.append((seed, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("stride", [64, 72])
+def test_zero_offset_conditionals(gpu, env, variant, stride):
+    """Conditional jumps of offset 0 (64- and 32-bit) go to the next slot taken or not: r0 = 6
+    for every packet (fuzz_gpu.py --standard found the compiled staged path losing such groups'
+    results before the translator turned these compares into no-ops)."""
+    code, rel = stdprogs.asm([
+        stdprogs.I("mov64_imm", 0, imm=5), (stdprogs.JMP64["jeq"], 0, 0, 0, 5),
+        stdprogs.I("add64_imm", 0, imm=1),
+        (stdprogs.JMP32["jset"], 0, 0, 0, 7), (stdprogs.JMP64["jgt"] + 8, 1, 0, 0, 0),
+        (stdprogs.JMP64["jne"], 1, 0, 0, 0), stdprogs.I("exit")])
+    n = 777
+    pk = np.random.default_rng(1).integers(0, 256, (n, stride), dtype=np.uint8)
+    got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), n, stride, variant)
+    assert not gf.any()
+    assert (got == 6).all()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("stride", [64, 72])
+def test_zero_offset_conditionals_reference(gpu, env, variant, stride):
+    """The same under the reference's cumulative stepping (ebpf_interpreter.c:209-211: pc += 0
+    leaves the next state unchanged): slots 0 (r0 = 5), 1 (JEQ r0, 5, +0), 3 (r0 += 1), 6 (EXIT)."""
+    from generic_ebpf_amd import isa
+    E = isa.encode
+    filler = E(0xb4, 9, 0, 0, 77)
+    code = b"".join([E(0xb4, 0, 0, 0, 5), E(0x15, 0, 0, 0, 5), filler, E(0x04, 0, 0, 0, 1), filler,
+                     filler, E(0x95, 0, 0, 0, 0)])
+    n = 777
+    pk = np.random.default_rng(2).integers(0, 256, (n, stride), dtype=np.uint8)
+    want, wf, _, _ = pyoracle.OracleProgram(code, [], []).run(pk.reshape(-1), n, stride)
+    assert not wf.any() and (want == 6).all()
+    p = gpu.Prog(env, code)
+    try:
+        gpu.set_variant(variant)
+        got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, stride)
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+    assert not gf.any()
+    assert (got == 6).all()

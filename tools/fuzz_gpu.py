@@ -12,7 +12,7 @@ key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts
 lookups, updates and deletes against the oracle's replay model; the tables are compared through
 get_next_key's walk (order and values).
 
-  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash]
+  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
 import argparse
 import os
@@ -120,13 +120,66 @@ def device(env, c, variant):
             m.destroy()
 
 
+def standard(a, env):
+    """--standard: random programs under standard eBPF semantics (tests/stdprogs.py: loop-free
+    programs with every ALU op, JMP32, stack, packet and array-lookup access; programs with counted
+    loops) against the oracle's run_std, 64-B packets (staged) and 72-B (general kernels)."""
+    import stdprogs
+    failed = False
+    for variant in (0, 1, 2):
+        for stride in (64, 72):
+            t0, bad = time.time(), []
+            for k in range(a.programs):
+                seed = a.seed * 100000 + k
+                g = np.random.default_rng(seed)
+                specs = []
+                if k % 2:
+                    code, rel = stdprogs.gen_loop_program(seed, length=int(g.integers(10, 40)))
+                else:
+                    code, rel = stdprogs.gen_program(seed, length=int(g.integers(10, 80)), with_map=k % 4 == 0)
+                    if k % 4 == 0:
+                        specs = [(8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
+                n = int(g.choice([1, 64, 65, 777, 2048]))
+                pk = g.integers(0, 256, (n, stride), dtype=np.uint8)
+                want, wf, _, _ = pyoracle.OracleProgram(code, rel, specs, semantics=1).run(
+                    pk.reshape(-1), n, stride, nthreads=8)
+                maps = []
+                for vs, me, d in specs:
+                    m = native.Map(env, me, vs)
+                    m.fill(d)
+                    maps.append(m)
+                p = native.Prog(env, native.patch_relocs(code, rel, [m.handle for m in maps]))
+                try:
+                    p.set_semantics(native.SEM_STANDARD)
+                    native.set_variant(variant)
+                    got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, stride)
+                finally:
+                    native.set_variant(0)
+                    p.destroy()
+                    for m in maps:
+                        m.destroy()
+                if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+                    bad.append(k)
+                if k % 200 == 199:
+                    print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
+            print("standard variant %d stride %d: %d programs, %d mismatches %s (%.0f s)" % (
+                variant, stride, a.programs, len(bad), bad[:20], time.time() - t0), flush=True)
+            failed = failed or bool(bad)
+    return failed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=500)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--hash", action="store_true", help="hashtable maps (lookups and writes)")
+    ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (loops too)")
     a = ap.parse_args()
     env = native.Env()
+    if a.standard:
+        failed = standard(a, env)
+        env.destroy()
+        sys.exit(1 if failed else 0)
     failed = False
     configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
     if not a.hash:
