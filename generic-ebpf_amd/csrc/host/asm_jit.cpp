@@ -296,7 +296,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			const uint32_t nx = xl.entries[e].next;
 			if (ah_flags[h] & 1) {
 				const uint32_t tk = xl.entries[e].target;
-				if (jdepth[e] >= AH_JOIN_LEVELS || nx >= n || tk >= n || seen[nx] || seen[tk]) {
+				if (jdepth[e] >= AH_JOIN_LEVELS || nx >= n || tk >= n || nx == tk || seen[nx] || seen[tk]) {
 					structured = false;
 					break;
 				}
