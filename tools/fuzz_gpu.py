@@ -12,7 +12,7 @@ key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts
 lookups, updates and deletes against the oracle's replay model; the tables are compared through
 get_next_key's walk (order and values).
 
-  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard]
+  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
 import argparse
 import os
@@ -168,14 +168,84 @@ def standard(a, env):
     return failed
 
 
+def mutate(code, g):
+    """4-15 random edits of a program (reference semantics): a conditional jump's offset set to 0
+    or to a small value, a slot replaced by JA +0 / JA +1, an immediate changed."""
+    b = bytearray(code)
+    n = len(b) // 8
+    conds = [i for i in range(n) if (b[8 * i] & 7) == 5 and b[8 * i] not in (0x05, 0x85, 0x95)]
+    for _ in range(int(g.integers(4, 16))):
+        kind = int(g.integers(0, 4))
+        if kind <= 1 and conds:
+            i = int(g.choice(conds))
+            off = 0 if kind == 0 else int(g.integers(-3, 4))
+            b[8 * i + 2:8 * i + 4] = (off & 0xffff).to_bytes(2, "little")
+        elif kind == 2:
+            i = int(g.integers(0, n))
+            b[8 * i:8 * i + 8] = bytes([0x05, 0]) + int(g.integers(0, 2)).to_bytes(2, "little") + bytes(4)
+        else:
+            i = int(g.integers(0, n))
+            if b[8 * i] != 0x18 and (i == 0 or b[8 * i - 8] != 0x18):
+                b[8 * i + 4:8 * i + 8] = int(g.integers(-2**31, 2**31)).to_bytes(4, "little", signed=True)
+    return bytes(b)
+
+
+def defined(c):
+    """The oracle's results do not depend on the uninitialised stack or on addresses
+    (track_undef, two stack fills, two thread counts)."""
+    outs = []
+    for si, nt in ((0, 1), (0xa5, 3)):
+        op = pyoracle.OracleProgram(c.code, c.relocs, c.maps, stack_init=si, track_undef=True)
+        ret, faults, data, _ = op.run(c.data, c.count, c.stride, c.offsets, nthreads=nt)
+        if (faults == 100).any():
+            return False
+        outs.append((ret.tobytes(), faults.tobytes(), data.tobytes()))
+    return outs[0] == outs[1]
+
+
+def mutated(a, env):
+    """--mutate: random programs edited at random (zero and small jump offsets, JA +0 / +1 slots,
+    new immediates), kept only when the oracle finds them defined, on every variant and both
+    kernels."""
+    failed = False
+    for variant, layout in [(v, lay) for v in (0, 1, 2) for lay in ("staged", "general")]:
+        t0, bad, kept = time.time(), [], 0
+        for k in range(a.programs):
+            c = case(k, a.seed, layout, writes=False)
+            c.code = mutate(c.code, np.random.default_rng(a.seed * 7777 + k))
+            if not defined(c):
+                continue
+            kept += 1
+            want, wf, wdata, wmaps = oracle(c)
+            try:
+                got, gf, gdata, gmaps = device(env, c, variant)
+            except Exception as e:  # noqa: BLE001
+                bad.append((k, str(e)[:60]))
+                continue
+            if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
+                    np.array_equal(wdata, gdata) and wmaps == gmaps):
+                bad.append(k)
+            if k % 500 == 499:
+                print("  ... %d programs, %d kept, %d mismatches" % (k + 1, kept, len(bad)), flush=True)
+        print("mutated variant %d %-7s: %d programs, %d defined, %d mismatches %s (%.0f s)" % (
+            variant, layout, a.programs, kept, len(bad), bad[:20], time.time() - t0), flush=True)
+        failed = failed or bool(bad)
+    return failed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=500)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--hash", action="store_true", help="hashtable maps (lookups and writes)")
     ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (loops too)")
+    ap.add_argument("--mutate", action="store_true", help="randomly edited programs (defined ones)")
     a = ap.parse_args()
     env = native.Env()
+    if a.mutate:
+        failed = mutated(a, env)
+        env.destroy()
+        sys.exit(1 if failed else 0)
     if a.standard:
         failed = standard(a, env)
         env.destroy()
