@@ -111,8 +111,13 @@ struct Translator {
 	{
 		const uint32_t id = new_entry();
 		out.entries[id].kind = DK_LOOPCNT;
-		loop_next.push_back({id, key(idx, 0)});
 		out.has_loops = true;
+		if (idx >= nslots) { // (a jump before slot 0 wraps: past the program, not a state key)
+			const uint32_t f = fault(EBPF_FAULT_SLOT);
+			out.entries[id].next = f;
+			return id;
+		}
+		loop_next.push_back({id, key(idx, 0)});
 		return id;
 	}
 
@@ -351,6 +356,11 @@ struct Translator {
 				uint32_t tpc = std_mode ? 0 : np + 1;
 				if (tidx == idx && tpc == pc) {
 					uint32_t f = fault(EBPF_FAULT_LOOP); // may grow entries: no `e` after this
+					out.entries[id].target = f;
+				} else if (tidx >= nslots) {
+					// (before it becomes a state key: key() keeps 32 bits of the slot, and a
+					// taken jump whose u32 pc wrapped lands 2^32 slots on — past the program)
+					uint32_t f = fault(EBPF_FAULT_SLOT);
 					out.entries[id].target = f;
 				} else if (std_mode && in.offset < 0) {
 					const uint32_t c = loop_edge(tidx); // (grows entries too)
@@ -612,6 +622,17 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 	int err = t.run();
 	if (err)
 		return err;
+	if (const char *dump = getenv("EBPF_XLATE_DUMP")) { // (debugging: the entries, one a line)
+		if (FILE *f = fopen(dump, "w")) {
+			fprintf(f, "start %u\n", out.start);
+			for (size_t i = 0; i < out.entries.size(); i++) {
+				const dp_entry &e = out.entries[i];
+				fprintf(f, "%zu kind %#x dst %u src %u off %d imm %#llx next %u target %u aux %u\n", i,
+					e.kind, e.dst, e.src, e.off, (unsigned long long)e.imm, e.next, e.target, e.aux);
+			}
+			fclose(f);
+		}
+	}
 
 	// Resolve LDDW immediates that are live maps of this env: the device map table.
 	struct ebpf_env *ee = ep->eo.eo_ee;

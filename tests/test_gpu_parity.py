@@ -506,3 +506,23 @@ def test_per_thread_stream_histograms(gpu, env):
         p.destroy()
         for m in maps:
             m.destroy()
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_taken_jump_pc_wrap_leaves_program(gpu, env, variant):
+    """A taken jump that wraps the reference's u32 pc (ebpf_interpreter.c:26, pc += off) lands
+    2^32 slots on, past the program: SLOT for every packet.  Slot 1 (JNE r0, 0, -2) at pc 2 goes
+    to (1, 1), then at pc 1 to pc 0xffffffff (fuzz_gpu.py --mutate found the translator folding
+    that target back onto slot 0: a state key kept 32 bits of the slot)."""
+    from generic_ebpf_amd import isa
+    E = isa.encode
+    code = b"".join([E(0xb4, 0, 0, 0, 1), E(0x55, 0, 0, -2, 0), E(0xb4, 9, 0, 0, 1), E(0x95)])
+    pk = np.zeros((130, 64), dtype=np.uint8)
+    p = gpu.Prog(env, code)
+    try:
+        gpu.set_variant(variant)
+        ret, faults, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), 130, 64)
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+    assert (faults == 4).all() and (ret == 0).all()
