@@ -404,7 +404,7 @@ helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_
  * called before the instruction executes (CALL results are tainted after it). */
 static int
 taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s, int16_t off,
-	  int32_t imm, const uint64_t *reg)
+	  int32_t imm, const uint64_t *reg, int std)
 {
 	const struct oracle_prog *p = re->p;
 	const int cls = op & 7;
@@ -414,6 +414,10 @@ taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s,
 		const int x = op & 0x08, code = op & 0xf0;
 		if (code == 0xb0 && cls == 4) /* MOV32 */
 			taint[d] = x ? taint[s] : 0;
+		else if (std && code == 0xb0) /* standard MOV64 moves (the reference's adds) */
+			taint[d] = x ? taint[s] : 0;
+		else if (std && code == 0x80) /* standard NEG / NEG64: -dst */
+			;
 		else if (code == 0x80 && cls == 4) /* NEG32 = -imm */
 			taint[d] = 0;
 		else if (x && code == 0x10 && taint[d] && taint[s]) /* pointer - pointer */
@@ -541,7 +545,7 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		int taken = -1;                        /* -1: not a conditional jump */
 		int msize = 0;
 
-		if (re.sdef && (fault = taint_pre(&re, taint, op, d, s, off, imm, reg)))
+		if (re.sdef && (fault = taint_pre(&re, taint, op, d, s, off, imm, reg, 0)))
 			break;
 		switch (op) {
 		/* ---- ALU32 :41-133 — operands truncated to u32, result zero-extended ---- */
@@ -745,6 +749,8 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	re.sdef = p->track_undef ? sdef : NULL;
 	if (re.sdef)
 		memset(sdef, 0, sizeof(sdef));
+	uint8_t taint[11] = {0};
+	taint[1] = taint[10] = 1;
 	re.p = p;
 
 	for (;;) {
@@ -781,6 +787,9 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		uint64_t IS = (uint64_t)(int64_t)imm;
 		int taken = -1;
 		int msize = 0;
+		if (re.sdef && (fault = taint_pre(&re, taint, jmp32 ? (uint8_t)((op & 0xf8) | 5) : op, d, s,
+						   off, imm, reg, 1)))
+			break;
 		if (jmp32) {
 			const uint32_t B = (op & 0x08) ? S32 : I32;
 			switch (op & 0xf0) {
@@ -936,6 +945,13 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		}
 		if (fault)
 			break;
+		if (re.sdef && op == 0x85) /* a lookup result is an address (NULL is not) */
+			taint[0] = p->helper_kind[imm] == ORACLE_HELPER_MAP_LOOKUP && reg[0] != 0;
+		if (re.sdef && op == 0x18) {
+			taint[d] = 0;
+			for (uint32_t m = 0; m < p->nmaps; m++)
+				taint[d] |= p->maps[m].handle == reg[d];
+		}
 		if (taken > 0) {
 			int64_t npc = (int64_t)pc + off;
 			if (off < 0 && ++back > (1u << 20)) {

@@ -141,6 +141,15 @@ def standard(a, env):
                         specs = [(8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
                 n = int(g.choice([1, 64, 65, 777, 2048]))
                 pk = g.integers(0, 256, (n, stride), dtype=np.uint8)
+                if a.mutate:  # (forward offsets only: a new backward edge would loop to the budget)
+                    code = mutate(code, np.random.default_rng(seed + 1), forward=True)
+                    outs = []
+                    for si in (0, 0xa5):
+                        r, f, _, _ = pyoracle.OracleProgram(code, rel, specs, semantics=1, stack_init=si,
+                                                            track_undef=True).run(pk.reshape(-1), n, stride, nthreads=8)
+                        outs.append((r.tobytes(), f.tobytes(), bool((f == 100).any())))
+                    if outs[0][2] or outs[0] != outs[1]:
+                        continue
                 want, wf, _, _ = pyoracle.OracleProgram(code, rel, specs, semantics=1).run(
                     pk.reshape(-1), n, stride, nthreads=8)
                 maps = []
@@ -162,13 +171,14 @@ def standard(a, env):
                     bad.append(k)
                 if k % 200 == 199:
                     print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-            print("standard variant %d stride %d: %d programs, %d mismatches %s (%.0f s)" % (
-                variant, stride, a.programs, len(bad), bad[:20], time.time() - t0), flush=True)
+            print("standard%s variant %d stride %d: %d programs, %d mismatches %s (%.0f s)" % (
+                " mutated" if a.mutate else "", variant, stride, a.programs, len(bad), bad[:20],
+                time.time() - t0), flush=True)
             failed = failed or bool(bad)
     return failed
 
 
-def mutate(code, g):
+def mutate(code, g, forward=False):
     """4-15 random edits of a program (reference semantics): a conditional jump's offset set to 0
     or to a small value, a slot replaced by JA +0 / JA +1, an immediate changed."""
     b = bytearray(code)
@@ -178,7 +188,7 @@ def mutate(code, g):
         kind = int(g.integers(0, 4))
         if kind <= 1 and conds:
             i = int(g.choice(conds))
-            off = 0 if kind == 0 else int(g.integers(-3, 4))
+            off = 0 if kind == 0 else int(g.integers(0 if forward else -3, 4))
             b[8 * i + 2:8 * i + 4] = (off & 0xffff).to_bytes(2, "little")
         elif kind == 2:
             i = int(g.integers(0, n))
@@ -243,7 +253,7 @@ def main():
     ap.add_argument("--mutate", action="store_true", help="randomly edited programs (defined ones)")
     a = ap.parse_args()
     env = native.Env()
-    if a.mutate:
+    if a.mutate and not a.standard:
         failed = mutated(a, env)
         env.destroy()
         sys.exit(1 if failed else 0)
