@@ -463,7 +463,7 @@ taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s,
 		const int sz = (op & 0x18) == 0x10 ? 1 : (op & 0x18) == 0x08 ? 2 : (op & 0x18) == 0 ? 4 : 8;
 		uint64_t a = reg[s] + (uint64_t)(int64_t)off;
 		uint8_t t = 0;
-		if (re->sdef && a >= re->stk_lo && a + sz <= re->stk_hi)
+		if (re->sdef && a >= re->stk_lo && a + sz >= a && a + sz <= re->stk_hi)
 			for (int i = 0; i < sz; i++)
 				t |= re->sdef[a - re->stk_lo + i] == 2;
 		taint[d] = t;
@@ -473,7 +473,7 @@ taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s,
 		const int sz = (op & 0x18) == 0x10 ? 1 : (op & 0x18) == 0x08 ? 2 : (op & 0x18) == 0 ? 4 : 8;
 		const uint8_t t = cls == 3 ? taint[s] : 0;
 		uint64_t a = reg[d] + (uint64_t)(int64_t)off;
-		if (re->sdef && a >= re->stk_lo && a + sz <= re->stk_hi) {
+		if (re->sdef && a >= re->stk_lo && a + sz >= a && a + sz <= re->stk_hi) {
 			for (int i = 0; i < sz; i++)
 				re->sdef[a - re->stk_lo + i] = t ? 2 : 1;
 			return 0;

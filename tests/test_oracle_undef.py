@@ -50,3 +50,14 @@ def test_address_difference_is_defined():
                      E(0x0f, 0, 2, 0, 0), E(0xb4, 9, 0, 0, 1), E(0xb4, 9, 0, 0, 1), E(0x95)])
     ret, faults = _run(code)
     assert not faults.any() and (ret == 0).all()
+
+
+def test_wrapping_address_faults_mem():
+    # r2 = -4 (all ones but the low bits); r0 = *(u64 *)(r2 + 0): an access whose end wraps past
+    # 2^64 is no region's (MEM), in the shadow bookkeeping too (it crashed the tracker once)
+    code = b"".join([E(0xb7, 2, 0, 0, -4), E(0x79, 0, 2, 0, 0), E(0xb4, 9, 0, 0, 1), E(0x95)])
+    pk = np.zeros((4, 64), dtype=np.uint8)
+    for sem in (0, 1):
+        op = pyoracle.OracleProgram(code, [], [], track_undef=True, semantics=sem)
+        ret, faults = op.run(pk.reshape(-1), 4, 64)[:2]
+        assert (faults == 3).all()
