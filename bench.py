@@ -28,9 +28,14 @@ the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them
 the general kernel (divergent, any packet size: C5) get a third pass (SQ_INSTS_VALU / _SALU /
 _VMEM_RD) for roofline.issue, the VALU-issue floor that divergence puts under such a launch.
 
-The same run also measures BASELINE config 5 (C5: the 256-insn filter over IMIX packets; --also),
-sharded the same way and verified the same way, reported under "also" — so the driver's 1/2/4/8-GPU
-runs carry the C5 line at every N too.
+The same run also measures the other BASELINE configs (--also, default c2,c3,c5,c4h: C2 the
+8-insn ALU program over 1M packets, C3 the 64-insn classifier over 16M, C5 the 256-insn filter over
+IMIX packets, C4H the classifier with a hashtable lookup), each sharded and verified the same way and
+reported under "also" with its own roofline -- so the driver's 1/2/4/8-GPU runs carry every config
+at every N.
+
+`bench.py --gpus N` with N > 1 and no launcher around it starts its N ranks itself
+(torch.distributed.run in a child process, self_launch); under a launcher WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0.
 """
@@ -86,9 +91,10 @@ def parse(argv=None):
                     help="event-time the kernel of every k-th timed step (default 2: the events come from the kernel's own dispatch packet, ebpf_gpu_time_next_launch, so a timed step costs no extra GPU-side marker)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every step (launches never queue)")
-    ap.add_argument("--also", default="c5",
+    ap.add_argument("--also", default="c2,c3,c5,c4h",
                     help="comma-separated further configs measured in the same run (sharded the same way) "
-                         "and reported under 'also' (default c5: BASELINE config 5, the IMIX filter); '' for none")
+                         "and reported under 'also' (default: every other BASELINE config -- C2, C3, C5 "
+                         "the IMIX filter -- and C4H, the hashtable form of C4); '' for none")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)
@@ -509,8 +515,40 @@ def kernel_stats(samples, ms_per_step):
             "median_exceeds_step": bool(med > ms_per_step)}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(a):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks, one process per
+    GPU, as `python -m torch.distributed.run --nproc-per-node N bench.py ...` in a fresh child
+    process (nothing here has touched the GPU yet: torch.cuda.device_count() does not initialise
+    it), let rank 0's JSON line through on the inherited stdout and return the child's exit
+    code.  Fewer visible GPUs than N is an error, except in the gloo rehearsal
+    (EBPF_BENCH_BACKEND=gloo), where the ranks share the visible GPUs."""
+    import torch
+    ngpu = torch.cuda.device_count()
+    backend = os.environ.get("EBPF_BENCH_BACKEND", "nccl")
+    if ngpu < a.gpus and not (backend == "gloo" and ngpu >= 1):
+        print("bench.py: --gpus %d but %d GPU(s) visible" % (a.gpus, ngpu), file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % a.gpus, "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(self_launch(a))
+    if world_env is not None and int(world_env) != a.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (world_env, a.gpus), file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 

@@ -3,8 +3,8 @@
 // During the batch every packet reads the maps as they were when it started; each
 // map_update_elem that succeeds appends a record to the batch's log (dprog.h dp_launch.upd_log:
 // {u64 packet, u32 entry | map << 20, u32 key, value}).  After the batch the writes land in the
-// array-map mirrors in packet order — within a packet in call order (state-tree entry indices
-// grow along a path) — so the last write of a key wins, as if the packets had run one after the
+// array-map mirrors in packet order — within a packet in call order (a lane takes its log
+// slots call by call) — so the last write of a key wins, as if the packets had run one after the
 // other (ebpf_map_array.c:173-183 memcpy).  Two passes over the log: every record offers its
 // order for its key (atomicMax), then the record holding the maximum copies its value and
 // re-arms the key's winner word; the log's counter is re-armed by the host (memset).
@@ -15,12 +15,15 @@
 
 namespace {
 
+// A record's order: (packet, log slot).  A lane takes its log slots one call after the other,
+// so within a packet the slot index is the call order (the state-tree entry index is not: a
+// run-time-map compare chain's copies and standard-semantics merge points are numbered after
+// entries that a path reaches later).
 __device__ inline uint64_t
-rec_order(const uint8_t *r)
+rec_order(const uint8_t *r, uint32_t slot)
 {
 	const uint64_t pkt = *reinterpret_cast<const uint64_t *>(r);
-	const uint32_t em = *reinterpret_cast<const uint32_t *>(r + 8);
-	return ((pkt << 20) | (em & 0xfffffu)) + 1; // 0 = no write
+	return ((pkt << 32) | slot) + 1; // 0 = no write
 }
 
 __global__ void __launch_bounds__(256)
@@ -38,7 +41,7 @@ upd_offer(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 		const uint32_t key = *reinterpret_cast<const uint32_t *>(r + 12);
 		if (maps[mi].is_hash)
 			continue; // (replayed on the host)
-		atomicMax(&win[maps[mi].win_off + key], (unsigned long long)rec_order(r));
+		atomicMax(&win[maps[mi].win_off + key], (unsigned long long)rec_order(r, i));
 	}
 }
 
@@ -54,7 +57,7 @@ upd_apply(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 		if (maps[mi].is_hash)
 			continue;
 		unsigned long long *w = &win[maps[mi].win_off + key];
-		if (*w != (unsigned long long)rec_order(r))
+		if (*w != (unsigned long long)rec_order(r, i))
 			continue;
 		const upd_map &m = maps[mi];
 		uint8_t *dst = reinterpret_cast<uint8_t *>(m.dev_base) + (uint64_t)m.value_size * key;

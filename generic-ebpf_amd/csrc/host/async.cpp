@@ -7,6 +7,18 @@
 // the life of the process) fed by a bounded FIFO of kQueueDepth jobs: two workers keep one job's
 // copies overlapping the next one's, and a consumer that submits faster than PCIe drains gets
 // EAGAIN instead of an unbounded pile of threads.  Jobs on one device share its staging pool.
+//
+// Two properties of ebpf_prog_run_batch that a worker thread would otherwise lose:
+//   * percpu maps index the CPU the batch is submitted from (map_current_cpu: the first CPU of the
+//     calling thread's affinity mask, ebpf_linux_user.c:83-112).  A job carries its submitter's
+//     mask and the worker runs it under that mask;
+//   * jobs of map-writing programs behave as if run one after the other in submission order (each
+//     batch reads what the earlier ones wrote; ebpf_gpu.h "Map writes in a device batch"): such a
+//     job takes a ticket when it is queued, and a worker runs it only when every writing job with
+//     an earlier ticket has finished, on whichever device it was queued.
+#include <pthread.h>
+#include <sched.h>
+
 #include <cerrno>
 #include <condition_variable>
 #include <deque>
@@ -26,6 +38,9 @@ struct ebpf_batch_job {
 	ebpf_batch_stats stats;
 	int rc = 0;
 	std::string msg;
+	cpu_set_t affinity;      // the submitting thread's CPU mask
+	bool has_affinity = false;
+	uint64_t writer = 0;     // map-writing program: its ticket (1, 2, ...), else 0
 	std::mutex m;
 	std::condition_variable cv;
 	bool done = false;
@@ -41,11 +56,26 @@ struct device_pool {
 	std::mutex m;
 	std::condition_variable cv;
 	std::deque<ebpf_batch_job *> q;
-	bool started = false;
+	int nworkers = 0; // workers running (kWorkers once every start succeeded)
 };
 
 std::mutex g_pools_lock;
 std::vector<device_pool *> g_pools; // per device; never freed (its workers live until exit)
+
+// Tickets of map-writing jobs, across devices: the next one to hand out, the next one to run.
+// (A queue is FIFO and a ticket is taken as the job is queued, so the earliest unfinished writer
+// is at its queue's front once the jobs ahead of it are done: waiting for it cannot deadlock.)
+std::mutex g_writers_lock;
+std::condition_variable g_writers_cv;
+uint64_t g_writer_next_ticket = 1, g_writer_next_run = 1;
+
+bool
+writes_maps(struct ebpf_prog *ep)
+{
+	if (prog_ensure_translated(ep) != 0)
+		return false; // (the job fails with the same error when it runs)
+	return ep->xlated->max_updates != 0;
+}
 
 void
 worker(device_pool *P)
@@ -59,9 +89,20 @@ worker(device_pool *P)
 			j = P->q.front();
 			P->q.pop_front();
 		}
+		if (j->has_affinity)
+			pthread_setaffinity_np(pthread_self(), sizeof(j->affinity), &j->affinity);
+		if (j->writer) {
+			std::unique_lock<std::mutex> g(g_writers_lock);
+			g_writers_cv.wait(g, [j] { return g_writer_next_run == j->writer; });
+		}
 		j->rc = ebpf_prog_run_batch(j->ep, &j->batch, j->ret, j->faults, &j->stats);
 		if (j->rc)
 			j->msg = ebpf_gpu_last_error();
+		if (j->writer) {
+			std::lock_guard<std::mutex> g(g_writers_lock);
+			g_writer_next_run++;
+			g_writers_cv.notify_all();
+		}
 		// (notified under the lock: once it is released the waiter may free the job)
 		std::lock_guard<std::mutex> g(j->m);
 		j->done = true;
@@ -83,15 +124,18 @@ pool_for(int device, device_pool **out)
 		g_pools[device]->device = device;
 	}
 	device_pool *P = g_pools[device];
-	if (!P->started) {
+	// top the pool up to kWorkers (a start that failed earlier is retried; the threads that
+	// did start keep serving the queue)
+	while (P->nworkers < kWorkers) {
 		try {
-			for (int w = 0; w < kWorkers; w++)
-				std::thread(worker, P).detach();
+			std::thread(worker, P).detach();
 		} catch (...) {
-			return EAGAIN; // (threads already started keep serving the queue)
+			break;
 		}
-		P->started = true;
+		P->nworkers++;
 	}
+	if (P->nworkers == 0)
+		return EAGAIN;
 	*out = P;
 	return 0;
 }
@@ -124,12 +168,18 @@ ebpf_prog_run_batch_async(struct ebpf_prog *ep, const struct ebpf_pkt_batch *bat
 	j->batch = *batch;
 	j->ret = ret;
 	j->faults = faults;
+	j->has_affinity = pthread_getaffinity_np(pthread_self(), sizeof(j->affinity), &j->affinity) == 0;
+	const bool writer = writes_maps(ep);
 	{
 		std::lock_guard<std::mutex> g(P->m);
 		if (P->q.size() >= kQueueDepth) {
 			delete j;
 			set_last_error("the device's job queue is full (wait for earlier jobs)");
 			return EAGAIN;
+		}
+		if (writer) { // (taken with the queue slot: a ticket is never left unused)
+			std::lock_guard<std::mutex> w(g_writers_lock);
+			j->writer = g_writer_next_ticket++;
 		}
 		P->q.push_back(j);
 	}

@@ -369,6 +369,67 @@ ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 	return 0;
 }
 
+// Cross-stream order of one mirror's users (internal.h map_mirror; callers hold mirror_lock).
+// Nothing is enqueued while every user of the mirror is on one stream.
+bool
+has_stream(const std::vector<void *> &v, hipStream_t s)
+{
+	return std::find(v.begin(), v.end(), static_cast<void *>(s)) != v.end();
+}
+
+// A launch on `s` is about to read the mirror: after the last write made on another stream.
+void
+mirror_read(map_mirror &m, hipStream_t s)
+{
+	if (m.wr_ev && !has_stream(m.synced, s)) {
+		hipStreamWaitEvent(s, static_cast<hipEvent_t>(m.wr_ev), 0);
+		m.synced.push_back(s);
+	}
+	if (!has_stream(m.readers, s))
+		m.readers.push_back(s);
+}
+
+// A write of the mirror is about to be enqueued on `w`: after every launch that read it on
+// another stream since the last write (an event recorded on that stream now covers all of
+// them), and after the last write itself.
+void
+mirror_write_begin(map_mirror &m, hipStream_t w)
+{
+	for (void *r : m.readers) {
+		if (r == static_cast<void *>(w))
+			continue;
+		hipEvent_t ev;
+		if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+			hipStreamSynchronize(static_cast<hipStream_t>(r)); // (no event: wait on the host)
+			continue;
+		}
+		hipEventRecord(ev, static_cast<hipStream_t>(r));
+		hipStreamWaitEvent(w, ev, 0);
+		hipEventDestroy(ev); // (released once it completes)
+	}
+	if (m.wr_ev && !has_stream(m.synced, w))
+		hipStreamWaitEvent(w, static_cast<hipEvent_t>(m.wr_ev), 0);
+}
+
+// ... and it is enqueued: later users on other streams wait for it.
+void
+mirror_write_end(map_mirror &m, hipStream_t w)
+{
+	if (m.wr_ev == nullptr) {
+		hipEvent_t ev;
+		if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+			hipStreamSynchronize(w);
+			m.synced.clear();
+			m.readers.clear();
+			return;
+		}
+		m.wr_ev = ev;
+	}
+	hipEventRecord(static_cast<hipEvent_t>(m.wr_ev), w);
+	m.synced.assign(1, static_cast<void *>(w));
+	m.readers.clear();
+}
+
 int
 sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 {
@@ -393,6 +454,7 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 		uint64_t v = em->version.load();
 		if (m.version != v || m.cpu != c) {
 			hipError_t e;
+			mirror_write_begin(m, stream);
 			if (em->is_hashtable()) {
 				// a fresh snapshot of the table; the staging copy must outlive the transfer
 				map_device_image(em, m.image, c);
@@ -401,18 +463,40 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 				if (e == hipSuccess)
 					e = hipStreamSynchronize(stream);
 			} else {
-				e = hipMemcpyAsync(m.dev, map_array_image(em, c),
-						   (size_t)em->value_size * em->max_entries,
-						   hipMemcpyHostToDevice, stream);
+				// from a snapshot: the upload may wait on the stream for other streams'
+				// readers (mirror_write_begin) while the host writes the map again.  The
+				// previous upload from the snapshot has finished once the last write has
+				// (every write of the mirror is ordered after the one before it).
+				if (m.wr_ev)
+					hipEventSynchronize(static_cast<hipEvent_t>(m.wr_ev));
+				const size_t bytes = (size_t)em->value_size * em->max_entries;
+				const uint8_t *src = map_array_image(em, c);
+				m.image.assign(src, src + bytes);
+				e = hipMemcpyAsync(m.dev, m.image.data(), bytes, hipMemcpyHostToDevice, stream);
 			}
 			if (e != hipSuccess)
 				return hip_fail(e, "hipMemcpyAsync(map mirror)");
+			mirror_write_end(m, stream);
 			m.version = v;
 			m.cpu = c;
 		}
+		mirror_read(m, stream); // (the launch that follows reads it)
 	}
 	return 0;
 }
+
+// The maps' order locks, taken in address order for the span of one launch (internal.h
+// ebpf_map.order_lock).
+struct launch_order {
+	std::vector<std::unique_lock<std::mutex>> held;
+	explicit launch_order(const std::vector<struct ebpf_map *> &maps)
+	{
+		std::vector<struct ebpf_map *> v(maps);
+		std::sort(v.begin(), v.end());
+		for (struct ebpf_map *m : v)
+			held.emplace_back(m->order_lock);
+	}
+};
 
 int
 prepare(struct ebpf_prog *ep, int device, dprog_device **out)
@@ -597,6 +681,11 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 int
 upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
 {
+	for (uint16_t t : ep->xlated->upd_maps) { // (the writes land after other streams' readers)
+		struct ebpf_map *em = ep->xlated->maps[t];
+		std::lock_guard<std::mutex> g(em->mirror_lock);
+		mirror_write_begin(em->mirrors[dp->device], stream);
+	}
 	hipError_t e = launch_map_writes(P.log, P.cap, dp->upd_stride,
 					 static_cast<const upd_map *>(dp->d_upd), P.win, P.faulted, stream);
 	if (e != hipSuccess)
@@ -899,8 +988,12 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 				continue; // the packet faulted: none of its writes land
 			const bool hash = ep->xlated->maps[em >> 20]->is_hashtable();
 			if (hash || arrays)
-				all.push_back(ref{((h.first + pkt) << 20) | (em & 0xfffff), r});
+				all.push_back(ref{h.first + pkt, r});
 		}
+	// Within a packet the records are already in call order: a lane takes its log slots one call
+	// after the other and every log is gathered in slot order.  (The entry index is no order: a
+	// run-time-map compare chain's copies, and merge points under standard semantics, are
+	// numbered after entries that a path reaches later.)  So sort by packet only, stably.
 	std::stable_sort(all.begin(), all.end(), [](const ref &a, const ref &b) { return a.order < b.order; });
 	const uint16_t cpu = map_current_cpu();
 	if (arrays)
@@ -957,6 +1050,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	L.nmaps = dp->nmaps;
 	L.nentries = dp->nentries;
 	L.start = ep->xlated->start;
+	launch_order order(ep->xlated->maps);
 	int err = sync_map_mirrors(ep, dp->device, stream);
 	if (err)
 		return err;
@@ -1138,6 +1232,12 @@ stage_alloc(void **p, size_t *cap, size_t need)
 
 } // namespace
 
+int
+prog_ensure_translated(struct ebpf_prog *ep)
+{
+	return ensure_translated_locked(ep);
+}
+
 void
 set_last_error(const std::string &msg)
 {
@@ -1191,9 +1291,14 @@ map_release_device_state(struct ebpf_map *em)
 		hipEventDestroy(static_cast<hipEvent_t>(em->wb_event));
 		em->wb_event = nullptr;
 	}
-	for (size_t d = 0; d < em->mirrors.size(); d++)
-		if (em->mirrors[d].dev && hipSetDevice((int)d) == hipSuccess)
+	for (size_t d = 0; d < em->mirrors.size(); d++) {
+		if (hipSetDevice((int)d) != hipSuccess)
+			continue;
+		if (em->mirrors[d].wr_ev)
+			hipEventDestroy(static_cast<hipEvent_t>(em->mirrors[d].wr_ev));
+		if (em->mirrors[d].dev)
 			hipFree(em->mirrors[d].dev);
+	}
 	em->mirrors.clear();
 }
 
@@ -1216,8 +1321,10 @@ map_mark_device_write(struct ebpf_map *em, int device, void *stream)
 	}
 	hipEventRecord(static_cast<hipEvent_t>(em->wb_event), static_cast<hipStream_t>(stream));
 	const uint64_t v = em->version.fetch_add(1) + 1;
-	if ((int)em->mirrors.size() > device)
+	if ((int)em->mirrors.size() > device) {
 		em->mirrors[device].version = v;
+		mirror_write_end(em->mirrors[device], static_cast<hipStream_t>(stream));
+	}
 	em->dev_dirty.store(device, std::memory_order_release);
 }
 

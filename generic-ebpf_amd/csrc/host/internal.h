@@ -48,7 +48,14 @@ struct map_mirror {
 	void *dev = nullptr;
 	uint64_t version = ~0ull; // host version last uploaded
 	uint16_t cpu = 0;         // percpu maps: the CPU whose copy was uploaded
-	std::vector<uint8_t> image; // hashtable: host staging copy of the device table
+	std::vector<uint8_t> image; // host staging copy of the last upload (hashtable: the device table)
+	// Cross-stream order of the mirror's users on its device (gpu_runtime.cpp mirror_read /
+	// mirror_write_*): a write (an upload, or a batch's map writes landing) waits for every
+	// launch that read the mirror on another stream since the previous write, and a launch on a
+	// stream waits for the last write made on another stream.
+	void *wr_ev = nullptr;         // hipEvent_t recorded after the last write
+	std::vector<void *> synced;    // streams ordered after that write
+	std::vector<void *> readers;   // streams whose launches read the mirror since that write
 };
 
 // The device mirror of a map (maps.cpp).  Array maps mirror their value array, hashtables a
@@ -82,6 +89,9 @@ struct ebpf_map {
 	std::atomic<uint64_t> version{0}; // bumped on every host-side write
 	std::mutex mirror_lock;
 	std::vector<map_mirror> mirrors;  // indexed by device
+	// held by a launch from its mirror sync to its last enqueue, so that the reads and writes it
+	// registers (map_mirror.readers / wr_ev) match the order its work reaches the streams
+	std::mutex order_lock;
 	// a device batch wrote the map (map_update_elem): that device's mirror is newer than the
 	// host copy until map_pull_device_writes copies it back (after wb_event, a hipEvent_t)
 	std::atomic<int> dev_dirty{-1};
@@ -224,6 +234,8 @@ int translate_program(struct ebpf_prog *ep, dprog_host &out);
 
 // gpu_runtime.cpp
 void set_last_error(const std::string &msg);
+// Translate the program (once; thread-safe).  0, or the translation's error.
+int prog_ensure_translated(struct ebpf_prog *ep);
 // the calling thread's device for the host-buffer entry points (ebpf_gpu_set_device)
 int current_device();
 // Copy a device batch's map writes back into the host copy (no-op unless em->dev_dirty).

@@ -245,17 +245,23 @@ def test_two_ranks_gloo_equal_one_launch(gpu, cfg, total):
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_two_ranks_gloo(launcher):
     """bench.py's own N > 1 path (the driver's scaling run uses it with RCCL on 8 GPUs): two
     ranks on cuda:0 over gloo, strong sharding of one C4 batch; rank 0 prints one verified line
-    counting both shards, with C5 (BASELINE config 5) measured the same way under "also"."""
+    counting both shards, with C5 (BASELINE config 5) measured the same way under "also".
+    "self": plain `bench.py --gpus 2` with no launcher around it starts its own two ranks."""
     import json
     total = (1 << 21) + 77
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", "29631",
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
-           "--packets", str(total), "--no-cpu-baseline", "--no-pmc"]
-    env = dict(os.environ, OMP_NUM_THREADS="4", EBPF_BENCH_BACKEND="gloo")
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+            "--packets", str(total), "--no-cpu-baseline", "--no-pmc", "--also", "c5"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr", "127.0.0.1", "--master-port", "29631"] + args
+    else:
+        cmd = [sys.executable] + args
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="4", EBPF_BENCH_BACKEND="gloo")
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240, env=env)
     assert r.returncode == 0, (r.stdout.decode()[-2000:], r.stderr.decode()[-3000:])
     lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
@@ -267,3 +273,24 @@ def test_bench_two_ranks_gloo():
     # BASELINE config 5 in the same run, sharded the same way
     c5 = d["also"]["c5"]
     assert c5["verified"] is True and c5["packets_total"] == 1 << 22, c5
+
+
+def _bench_rc(args, **extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(extra)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120, env=env)
+    return r.returncode, r.stderr.decode()
+
+
+def test_bench_gpus_checks():
+    """`bench.py --gpus N` refuses to run a line it cannot honour (CPU here: no GPU visible):
+    fewer visible GPUs than N, and a launcher whose WORLD_SIZE disagrees with --gpus."""
+    import torch
+    if torch.cuda.device_count() == 0:
+        rc, err = _bench_rc(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+        assert rc == 2 and "--gpus 2 but 0 GPU(s) visible" in err, err
+    rc, err = _bench_rc(["--gpus", "2", "--steps", "1"], WORLD_SIZE="1")
+    assert rc == 2 and "WORLD_SIZE=1 but --gpus 2" in err, err
+    rc, err = _bench_rc(["--gpus", "1", "--steps", "1"], WORLD_SIZE="4")
+    assert rc == 2 and "WORLD_SIZE=4 but --gpus 1" in err, err
