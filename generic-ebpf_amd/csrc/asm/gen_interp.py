@@ -233,7 +233,22 @@ fam("HDELETE", 0)              # map_delete_elem on a hashtable known at transla
 # a constant offset fused with the BE16 / BE32 of its destination (dst, offset)
 fam("LDXPKBE16", 3)
 fam("LDXPKBE32", 3)
+# stores into map values (ebpf_gpu.h "Stores into map values"; dprog.h DK_CNT_STORE / DK_XADD):
+# the STX of a counter update (d = the pointer, s = the value), XADD (d = the pointer, s = the
+# addend) and XADD | FETCH (d = the addend, which receives the old value; s = the pointer)
+for z in (4, 8):
+    fam("CNTST%d" % z, 2)
+for z in (4, 8):
+    fam("XADD%d" % z, 2)
+for z in (4, 8):
+    fam("XADDF%d" % z, 2)
+fam("OVLINIT", 0)              # dprog.h DK_OVLINIT: the lane's overlay count = 0
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
+# the lane's stack slice below the frame (dprog.h DP_OVL_*): loop count, overlay count, the
+# scratch a store into a map value is redirected to, the overlay entries
+OVL_COUNT, VST_SCRATCH, OVL_ENTRIES = 4, 8, 16
+VFLAGS_OFF = 0xcc              # dp_launch.vflags: bit 0 overlay, bit 1 value stores provided for
+SPILL = 51                     # v51 (H[5]): .Lr_check's SGPR spill lanes around .Lr_vstore
 
 
 def variants(arity):
@@ -695,21 +710,42 @@ def h_st_stk(z):
     return out
 
 
+def gather(a0, acc, tmp, z, tag=None):
+    """acc (two VGPRs) = the z bytes at the flat address v[a0:a0+1], little-endian, byte by byte
+    (alignment-agnostic).  z: an int, or None for S_T0 bytes (4 or 8 at run time; `tag` names
+    the label)."""
+    out = ["v_mov_b32 %s, 0" % v(acc[0]), "v_mov_b32 %s, 0" % v(acc[1])]
+    for b in range(z or 8):
+        if z is None and b == 4:
+            out += ["s_cmp_le_u32 %s, %d" % (s(S_T0), b), "s_cbranch_scc1 .Lg_done_%s" % tag]
+        out.append("flat_load_ubyte %s, %s offset:%d" % (v(tmp), vp(a0), b))
+        out.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        tgt = v(acc[b // 4])
+        out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(tmp), 8 * (b % 4), tgt))
+    if z is None:
+        out.append(".Lg_done_%s:" % tag)
+    return out
+
+
+def vflags_test(bit, skip):
+    """scc = dp_launch.vflags bit `bit`; branches to `skip` when it is clear.  Clobbers S_T3."""
+    return ["s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
+            "s_waitcnt lgkmcnt(0)",
+            "s_bitcmp1_b32 %s, %d" % (s(S_T3), bit),
+            "s_cbranch_scc0 %s" % skip]
+
+
 def h_ldx_gen(z, d, sr):
     """Generic load: address = r_src + sext(off) (s[10:11]); region check, then byte-wise
-    flat loads (packet/map in global memory, stack in LDS via the shared aperture)."""
+    flat loads (packet/map in global memory, stack in LDS via the shared aperture); a program
+    that reads its own stores into map values (dp_launch.vflags bit 0) then takes the bytes it
+    stored from its overlay (.Lr_ovlfix)."""
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
            "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check")
-    # byte-wise gather (alignment-agnostic)
-    acc = [v(H[2]), v(H[3])]
-    out += ["v_mov_b32 %s, 0" % acc[0], "v_mov_b32 %s, 0" % acc[1]]
-    for b in range(z):
-        out.append("flat_load_ubyte %s, %s offset:%d" % (v(H[4]), vp(a0), b))
-        out.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        tgt = acc[b // 4]
-        out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(H[4]), 8 * (b % 4), tgt))
-    out += ["v_mov_b32 %s, %s" % (lo(d), acc[0]), "v_mov_b32 %s, %s" % (hi(d), acc[1])]
+    out += gather(a0, (H[2], H[3]), H[4], z)
+    out += vflags_test(0, ".Lnovl_{uid}") + call(".Lr_ovlfix") + [".Lnovl_{uid}:"]
+    out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3]))]
     return out
 
 
@@ -769,22 +805,44 @@ def store_bytes(a0, vals, z):
     return out
 
 
-def h_stx_gen(z, d, sr):
+def h_stx_gen(z, d, sr, kind=1):
+    """Generic store: the value in H[2:3] before the region check, which hands stores into map
+    values to .Lr_vstore (kind 1: plain, 2: a counter update's STX) and points those lanes'
+    address at their scratch; then byte-wise flat stores."""
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(d)),
-           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(".Lr_check")
-    out += ["v_mov_b32 %s, %s" % (v(H[2]), lo(sr)), "v_mov_b32 %s, %s" % (v(H[3]), hi(sr))]
+           "v_mov_b32 %s, %s" % (v(H[2]), lo(sr)), "v_mov_b32 %s, %s" % (v(H[3]), hi(sr)),
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, %d" % (s(S_T1), kind)] + call(".Lr_check")
     return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
 
 
+def h_xadd(z, p, x, fetch):
+    """XADD: *(u32 / u64 *)(r_p + off) += r_x (fetch: r_x = the old value).  The check hands a
+    map value's lanes to .Lr_vstore (kind 3), which leaves the old value the packet sees in the
+    lane's scratch and points the address there; the read-modify-write below then serves every
+    lane alike."""
+    a0 = H[0]
+    old, nv = (R[0], R[1]), (R[2], R[3])
+    out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(p)),
+           "v_mov_b32 %s, %s" % (v(H[2]), lo(x)), "v_mov_b32 %s, %s" % (v(H[3]), hi(x)),
+           "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 3" % s(S_T1)] + call(".Lr_check")
+    out += gather(a0, old, H[4], z)
+    out += ["v_lshl_add_u64 %s, %s, 0, %s" % (vp(nv[0]), vp(old[0]), vp(H[2]))]
+    out += store_bytes(a0, [v(nv[0]), v(nv[1])], z)
+    if fetch:
+        out += ["v_mov_b32 %s, %s" % (lo(x), v(old[0])),
+                "v_mov_b32 %s, %s" % (hi(x), v(old[1]) if z == 8 else "0")]
+    return out
+
+
 def h_st_gen(z, d):
-    """s[10:11] = value, s14 = sign-extended... no: offset comes in s15 (aux1, s16 off)."""
+    """s[10:11] = the value (sign-extended imm), s15 = the offset (aux1)."""
     a0 = H[0]
     out = ["s_ashr_i32 %s, s15, 31" % s(S_T3),
            "v_mov_b32 %s, s15" % v(H[2]), "v_mov_b32 %s, %s" % (v(H[3]), s(S_T3)),
            "v_lshl_add_u64 %s, %s, 0, %s" % (vp(a0), vp(H[2]), pair(d)),
+           "v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3]),
            "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 1" % s(S_T1)] + call(".Lr_check")
-    out += ["v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3])]
     return out + store_bytes(a0, [v(H[2]), v(H[3])], z)
 
 
@@ -1095,6 +1153,303 @@ def copy_record(T, src, n, off):
             ".Lcpe%s:" % T]
 
 
+def ovl_fix(T, acc):
+    """The packet's own stores into map values over the z = S_T0 bytes just read at H[0:1] into
+    acc (two VGPRs): every byte whose 8-byte word has an overlay entry (dprog.h DP_OVL_*) comes
+    from that entry.  For the lanes in exec; clobbers R[6:10], H[4], S_T3, S_BYTES, S_MASK, vcc."""
+    E, D0, D1, X, Y, C = R[10], R[6], R[7], R[8], R[9], H[4]   # (pairs start even: gfx950)
+    L = ["v_add_u32 %s, %d, v%d" % (v(C), OVL_COUNT, V_STK),
+         "ds_read_b32 %s, %s" % (v(C), v(C)),
+         "s_mov_b32 %s, 0" % s(S_T3),
+         ".Lof%s_loop:" % T,
+         "s_waitcnt lgkmcnt(0)",
+         "v_cmp_lt_u32_e64 vcc, %s, %s" % (s(S_T3), v(C)),
+         "s_and_b64 vcc, vcc, exec",
+         "s_cbranch_scc0 .Lof%s_done" % T,
+         "s_mov_b64 %s, exec" % sp(S_MASK),
+         "s_mov_b64 exec, vcc",
+         "s_lshl_b32 %s, %s, 4" % (s(S_BYTES), s(S_T3)),
+         "s_add_u32 %s, %s, %d" % (s(S_BYTES), s(S_BYTES), OVL_ENTRIES),
+         "v_add_u32 %s, %s, v%d" % (v(E), s(S_BYTES), V_STK),
+         "ds_read2_b32 %s, %s offset1:1" % (vp(D0), v(E)),          # the entry's word address
+         "v_and_b32 %s, -8, %s" % (v(X), v(H[0])),
+         "s_waitcnt lgkmcnt(0)",
+         # d = entry word - (address & ~7): 0 or 8 when it is a word of this load
+         "v_sub_co_u32 %s, vcc, %s, %s" % (v(D0), v(D0), v(X)),
+         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(D1), v(D1), v(H[1])),
+         "v_cmp_ne_u32_e64 vcc, 0, %s" % v(D1),
+         "v_cndmask_b32_e64 %s, %s, 16, vcc" % (v(D0), v(D0))]
+    for b in range(8):
+        if b in (1, 2, 4):
+            L += ["s_cmp_le_u32 %s, %d" % (s(S_T0), b), "s_cbranch_scc1 .Lof%s_next" % T]
+        k = 8 * (b % 4)
+        a = v(acc[b // 4])
+        L += ["v_and_b32 %s, 7, %s" % (v(X), v(H[0])),
+              "v_add_u32 %s, %d, %s" % (v(X), b, v(X)),               # j = (a & 7) + b
+              "v_and_b32 %s, 8, %s" % (v(Y), v(X)),                   # 8 * (j >> 3)
+              "v_cmp_eq_u32_e64 vcc, %s, %s" % (v(Y), v(D0)),
+              "v_and_b32 %s, 7, %s" % (v(X), v(X)),
+              "v_add3_u32 %s, %s, %s, 8" % (v(X), v(X), v(E)),
+              "ds_read_u8 %s, %s" % (v(Y), v(X)),
+              "s_waitcnt lgkmcnt(0)",
+              "v_lshlrev_b32 %s, %d, %s" % (v(Y), k, v(Y)),
+              "v_and_b32 %s, 0x%x, %s" % (v(X), 0xffffffff ^ (0xff << k), a),
+              "v_or_b32 %s, %s, %s" % (v(X), v(X), v(Y)),
+              "v_cndmask_b32 %s, %s, %s, vcc" % (a, a, v(X))]
+    L += [".Lof%s_next:" % T,
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "s_add_u32 %s, %s, 1" % (s(S_T3), s(S_T3)),
+          "s_branch .Lof%s_loop" % T,
+          ".Lof%s_done:" % T]
+    return L
+
+
+def ovl_store(T, nv):
+    """Remember, in the lanes' overlays, the z = S_T0 bytes of nv (two VGPRs) stored at H[0:1]:
+    for each of the (one or two) 8-byte words the store touches, its entry — made on first use
+    with the word's batch-start bytes from the mirror — gets the bytes.  For the lanes in exec;
+    clobbers R[0:3], R[8:10], H[2:4], S_T3, S_BYTES, S_MASK, S_JUNK (saved exec), vcc."""
+    W0, W1, CNT, IDX, E, X, Y = R[0], R[1], R[2], R[3], R[8], H[2], H[3]
+    L = ["s_mov_b64 %s, exec" % sp(S_JUNK),
+         "v_add_u32 %s, %d, v%d" % (v(X), OVL_COUNT, V_STK),
+         "ds_read_b32 %s, %s" % (v(CNT), v(X)),
+         "s_waitcnt lgkmcnt(0)"]
+    for wi in (0, 1):
+        t = "%s%d" % (T, wi)
+        L += ["s_mov_b64 exec, %s" % sp(S_JUNK)]
+        if wi:  # only lanes whose store reaches past its first word
+            L += ["v_and_b32 %s, 7, %s" % (v(X), v(H[0])),
+                  "v_add_u32 %s, %s, %s" % (v(X), s(S_T0), v(X)),
+                  "v_cmp_lt_u32_e64 vcc, 8, %s" % v(X),
+                  "s_and_b64 exec, exec, vcc",
+                  "s_cbranch_execz .Los%s_end" % t]
+        L += ["v_and_b32 %s, -8, %s" % (v(W0), v(H[0])),
+              "v_mov_b32 %s, %s" % (v(W1), v(H[1]))]
+        if wi:
+            L += ["v_add_co_u32 %s, vcc, 8, %s" % (v(W0), v(W0)),
+                  "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(W1), v(W1))]
+        # the word's entry (IDX), if any
+        L += ["v_mov_b32 %s, -1" % v(IDX),
+              "s_mov_b32 %s, 0" % s(S_T3),
+              ".Los%s_find:" % t,
+              "v_cmp_lt_u32_e64 vcc, %s, %s" % (s(S_T3), v(CNT)),
+              "s_and_b64 vcc, vcc, exec",
+              "s_cbranch_scc0 .Los%s_found" % t,
+              "s_mov_b64 %s, exec" % sp(S_MASK),
+              "s_mov_b64 exec, vcc",
+              "s_lshl_b32 %s, %s, 4" % (s(S_BYTES), s(S_T3)),
+              "s_add_u32 %s, %s, %d" % (s(S_BYTES), s(S_BYTES), OVL_ENTRIES),
+              "v_add_u32 %s, %s, v%d" % (v(E), s(S_BYTES), V_STK),
+              "ds_read2_b32 %s, %s offset1:1" % (vp(X), v(E)),
+              "v_mov_b32 %s, %s" % (v(E), s(S_T3)),
+              "s_waitcnt lgkmcnt(0)",
+              "v_cmp_eq_u64_e64 vcc, %s, %s" % (vp(X), vp(W0)),
+              "v_cndmask_b32 %s, %s, %s, vcc" % (v(IDX), v(IDX), v(E)),
+              "s_mov_b64 exec, %s" % sp(S_MASK),
+              "s_add_u32 %s, %s, 1" % (s(S_T3), s(S_T3)),
+              "s_branch .Los%s_find" % t,
+              ".Los%s_found:" % t,
+              # none: a new entry with the word's batch-start bytes
+              "v_cmp_eq_u32_e64 vcc, -1, %s" % v(IDX),
+              "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+              "s_cbranch_execz .Los%s_have" % t,
+              "v_mov_b32 %s, %s" % (v(IDX), v(CNT)),
+              "v_add_u32 %s, 1, %s" % (v(CNT), v(CNT)),
+              "v_lshl_add_u32 %s, %s, 4, v%d" % (v(E), v(IDX), V_STK),
+              "v_add_u32 %s, %d, %s" % (v(E), OVL_ENTRIES, v(E)),
+              "global_load_dwordx2 %s, %s, off" % (vp(X), vp(W0)),
+              "ds_write2_b32 %s, %s, %s offset1:1" % (v(E), v(W0), v(W1)),
+              "s_waitcnt vmcnt(0)",
+              "ds_write2_b32 %s, %s, %s offset0:2 offset1:3" % (v(E), v(X), v(Y)),
+              "v_add_u32 %s, %d, v%d" % (v(X), OVL_COUNT, V_STK),
+              "ds_write_b32 %s, %s" % (v(X), v(CNT)),
+              ".Los%s_have:" % t,
+              "s_or_b64 exec, exec, %s" % sp(S_MASK),
+              "v_lshl_add_u32 %s, %s, 4, v%d" % (v(E), v(IDX), V_STK),
+              "v_add_u32 %s, %d, %s" % (v(E), OVL_ENTRIES + 8, v(E))]   # the entry's bytes
+        # the bytes of the store that fall in this word
+        for b in range(8):
+            if b in (1, 2, 4):
+                L += ["s_cmp_le_u32 %s, %d" % (s(S_T0), b), "s_cbranch_scc1 .Los%s_end" % t]
+            L += ["v_and_b32 %s, 7, %s" % (v(X), v(H[0])),
+                  "v_add_u32 %s, %d, %s" % (v(X), b, v(X)),          # j = (a & 7) + b
+                  "v_and_b32 %s, 8, %s" % (v(Y), v(X)),
+                  "v_cmp_eq_u32_e64 vcc, %d, %s" % (8 * wi, v(Y)),
+                  "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+                  "v_and_b32 %s, 7, %s" % (v(X), v(X)),
+                  "v_add_u32 %s, %s, %s" % (v(X), v(X), v(E)),
+                  "v_lshrrev_b32 %s, %d, %s" % (v(Y), 8 * (b % 4), v(nv[b // 4])),
+                  "ds_write_b8 %s, %s" % (v(X), v(Y)),
+                  "s_or_b64 exec, exec, %s" % sp(S_MASK)]
+        L += [".Los%s_end:" % t]
+    L += ["s_mov_b64 exec, %s" % sp(S_JUNK),
+          "s_waitcnt lgkmcnt(0)"]
+    return L
+
+
+def vstore_routine():
+    """VSTORE (called by .Lr_check for the lanes of one map, exec = those lanes): a store into
+    that map's values (ebpf_gpu.h "Stores into map values"), S_T1 = kind (1 a plain store of
+    H[2:3]; 2 a counter update's STX of H[2:3]; 3 XADD of the addend H[2:3]), S_T0 = bytes,
+    H[0:1] = the address, S_T2 = the map's index, s[64:71] its dp_map record.
+      * kinds 2 and 3 read the value the packet sees there (L: the mirror's bytes under its
+        overlay); kind 3 leaves L in the lane's scratch (the handler's own read-modify-write,
+        pointed there, then fetches it); kind 2 adds X - L, kind 3 the addend;
+      * the overlay (dp_launch.vflags bit 0) remembers the stored value;
+      * an addition aligned to its width within the values of a DP_MAP_ATOMIC map goes into its
+        delta area (a device atomic); everything else is a record in the batch's log
+        {packet, map << 20 | DP_REC_VALUE | add << 16 | size, offset, data, hashtable slot}.
+    Returns S_JUNK = the lanes to fault (code S_CODE): the log full, or value stores not provided
+    for (vflags bit 1 clear: the translator saw none).  Preserves S_T0..S_T2 and v51 (SPILL);
+    clobbers R[*], H[2:4], S_T3, S_BYTES, S_MASK, s[64:71], vcc."""
+    L_, NV, OFF, VOFF, SLOT, WORD, ADD = (R[4], R[5]), (R[6], R[7]), R[0], R[2], R[3], R[8], R[10]
+    L = [".Lr_vstore:",
+         "v_writelane_b32 v%d, %s, 11" % (SPILL, s(S_LINK)),
+         "v_writelane_b32 v%d, %s, 12" % (SPILL, s(S_LINK + 1)),
+         "s_mov_b64 %s, 0" % sp(S_JUNK),
+         "s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
+         "s_waitcnt lgkmcnt(0)",
+         "s_bitcmp1_b32 %s, 1" % s(S_T3),
+         "s_cbranch_scc1 .Lvs_go",
+         "s_mov_b64 %s, exec" % sp(S_JUNK),
+         "s_mov_b32 %s, 9" % s(S_CODE),          # EBPF_FAULT_MAP_WRITE
+         "s_branch .Lvs_ret",
+         ".Lvs_go:",
+         "s_cmp_eq_u32 %s, 1" % s(S_T1),
+         "s_cbranch_scc1 .Lvs_plain"] + gather(H[0], L_, H[4], None, "vs") + \
+        vflags_test(0, ".Lvs_noovl") + ovl_fix("vs", L_) + [
+         ".Lvs_noovl:",
+         "s_cmp_eq_u32 %s, 3" % s(S_T1),
+         "s_cbranch_scc0 .Lvs_cnt",
+         # XADD: new = L + addend, L to the scratch, delta = the addend
+         "v_lshl_add_u64 %s, %s, 0, %s" % (vp(NV[0]), vp(L_[0]), vp(H[2])),
+         "v_add_u32 %s, %d, v%d" % (v(R[9]), VST_SCRATCH, V_STK),
+         "ds_write2_b32 %s, %s, %s offset1:1" % (v(R[9]), v(L_[0]), v(L_[1])),
+         "v_mov_b32 %s, %s" % (v(L_[0]), v(H[2])),
+         "v_mov_b32 %s, %s" % (v(L_[1]), v(H[3])),
+         "s_branch .Lvs_have",
+         ".Lvs_cnt:",                             # a counter's STX: delta = X - L
+         "v_mov_b32 %s, %s" % (v(NV[0]), v(H[2])),
+         "v_mov_b32 %s, %s" % (v(NV[1]), v(H[3])),
+         "v_sub_co_u32 %s, vcc, %s, %s" % (v(L_[0]), v(H[2]), v(L_[0])),
+         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(L_[1]), v(H[3]), v(L_[1])),
+         "s_branch .Lvs_have",
+         ".Lvs_plain:",
+         "v_mov_b32 %s, %s" % (v(NV[0]), v(H[2])),
+         "v_mov_b32 %s, %s" % (v(NV[1]), v(H[3])),
+         "v_mov_b32 %s, 0" % v(L_[0]),
+         "v_mov_b32 %s, 0" % v(L_[1]),
+         ".Lvs_have:"] + vflags_test(0, ".Lvs_noovl2") + ovl_store("vs", NV) + [
+         ".Lvs_noovl2:",
+         "s_mov_b64 %s, 0" % sp(S_JUNK),          # (ovl_store kept exec there)
+         # offsets: OFF = address - the mirror (hashtables: SLOT, VOFF = in the value)
+         "v_sub_co_u32 %s, vcc, %s, s66" % (v(OFF), v(H[0])),
+         "v_mov_b32 %s, s67" % v(R[9]),
+         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(H[1]), v(R[9])),
+         "v_mov_b32 %s, %s" % (v(VOFF), v(OFF)),
+         "v_mov_b32 %s, 0" % v(SLOT),
+         "s_bitcmp1_b32 s71, 31",
+         "s_cbranch_scc0 .Lvs_arr",
+         "s_bfe_u32 %s, s71, 0x50010" % s(S_T3),                    # log2 of the slot stride
+         "v_lshrrev_b64 %s, %s, %s" % (vp(R[8]), s(S_T3), vp(OFF)),
+         "v_mov_b32 %s, %s" % (v(SLOT), v(R[8])),
+         "s_lshl_b32 %s, 1, %s" % (s(S_BYTES), s(S_T3)),
+         "s_sub_u32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
+         "v_and_b32 %s, %s, %s" % (v(VOFF), s(S_BYTES), v(OFF)),
+         "s_and_b32 %s, s71, 0xffff" % s(S_T3),                    # value offset in the slot:
+         "s_add_u32 %s, %s, 15" % (s(S_T3), s(S_T3)),               # 8 + round8(key size)
+         "s_and_b32 %s, %s, -8" % (s(S_T3), s(S_T3)),
+         "v_subrev_u32 %s, %s, %s" % (v(VOFF), s(S_T3), v(VOFF)),
+         ".Lvs_arr:",
+         # ADD = an addition (kinds 2, 3) aligned to its width within the values
+         "s_sub_u32 %s, %s, 1" % (s(S_T3), s(S_T0)),
+         "v_and_b32 %s, %s, %s" % (v(ADD), s(S_T3), v(VOFF)),
+         "v_cmp_eq_u32_e64 vcc, 0, %s" % v(ADD),
+         "s_cmp_eq_u32 %s, 1" % s(S_T1),
+         "s_cselect_b64 vcc, 0, vcc",
+         "v_cndmask_b32_e64 %s, 0, 1, vcc" % v(ADD),
+         # a DP_MAP_ATOMIC map: the additions into its delta area
+         "s_bitcmp1_b32 s71, 30",
+         "s_cbranch_scc0 .Lvs_rec",
+         "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+         "s_cbranch_execz .Lvs_atom_done",
+         "s_mul_i32 %s, s68, s69" % s(S_BYTES),
+         "s_add_u32 %s, %s, 63" % (s(S_BYTES), s(S_BYTES)),
+         "s_and_b32 %s, %s, -64" % (s(S_BYTES), s(S_BYTES)),      # dprog.h dp_delta_off
+         "v_lshl_add_u64 %s, %s, 0, s[66:67]" % (vp(R[8]), vp(OFF)),
+         "v_add_co_u32 %s, vcc, %s, %s" % (v(R[8]), s(S_BYTES), v(R[8])),
+         "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[9]), v(R[9])),
+         "s_cmp_eq_u32 %s, 8" % s(S_T0),
+         "s_cbranch_scc0 .Lvs_atom4",
+         "global_atomic_add_x2 %s, %s, off" % (vp(R[8]), vp(L_[0])),
+         "s_branch .Lvs_atom_done",
+         ".Lvs_atom4:",
+         "global_atomic_add %s, %s, off" % (vp(R[8]), v(L_[0])),
+         ".Lvs_atom_done:",
+         "s_andn2_b64 exec, %s, exec" % sp(S_MASK),                # the lanes left: records
+         ".Lvs_rec:",
+         "s_cbranch_execz .Lvs_ret",
+         # the record's word and data (an addition: the addend; else the stored bytes)
+         "s_lshl_b32 %s, %s, 20" % (s(S_T3), s(S_T2)),
+         "s_or_b32 %s, %s, 0x%x" % (s(S_T3), s(S_T3), 0x80000),
+         "s_or_b32 %s, %s, %s" % (s(S_T3), s(S_T3), s(S_T0)),
+         "v_mov_b32 %s, %s" % (v(WORD), s(S_T3)),
+         "v_cmp_ne_u32_e64 vcc, 0, %s" % v(ADD),
+         "v_or_b32 %s, 0x%x, %s" % (v(R[9]), 0x10000, v(WORD)),
+         "v_cndmask_b32 %s, %s, %s, vcc" % (v(WORD), v(WORD), v(R[9])),
+         "v_cndmask_b32 %s, %s, %s, vcc" % (v(L_[0]), v(NV[0]), v(L_[0])),
+         "v_cndmask_b32 %s, %s, %s, vcc" % (v(L_[1]), v(NV[1]), v(L_[1])),
+         # a log slot per lane: one atomic add on the log's counter for the wave
+         "s_load_dwordx4 s[64:67], s[0:1], 0x80",                # upd_log, upd_cap, upd_stride
+         "s_load_dwordx2 s[68:69], s[0:1], 0x90",                # pkt_base
+         "s_waitcnt lgkmcnt(0)",
+         "s_cmp_eq_u64 s[64:65], 0",
+         "s_cbranch_scc0 .Lvs_log",
+         "s_mov_b64 %s, exec" % sp(S_JUNK),                       # (no log: a library bug)
+         "s_mov_b32 %s, 3" % s(S_CODE),
+         "s_branch .Lvs_ret",
+         ".Lvs_log:",
+         "s_bcnt1_i32_b64 %s, exec" % s(S_T3),
+         "v_mbcnt_lo_u32_b32 %s, exec_lo, 0" % v(OFF),
+         "v_mbcnt_hi_u32_b32 %s, exec_hi, %s" % (v(OFF), v(OFF)),
+         "s_mov_b64 %s, exec" % sp(S_MASK),
+         "s_ff1_i32_b64 %s, exec" % s(S_BYTES),
+         "s_lshl_b64 exec, 1, %s" % s(S_BYTES),
+         "v_mov_b32 %s, %s" % (v(R[1]), s(S_T3)),
+         "v_mov_b32 %s, 0" % v(R[9]),
+         "global_atomic_add %s, %s, %s, s[64:65] sc0" % (v(R[6]), v(R[9]), v(R[1])),
+         "s_waitcnt vmcnt(0)",
+         "v_readfirstlane_b32 %s, %s" % (s(S_T3), v(R[6])),
+         "s_mov_b64 exec, %s" % sp(S_MASK),
+         "v_add_u32 %s, %s, %s" % (v(OFF), s(S_T3), v(OFF)),      # this lane's slot
+         # a full log (the host sizes it for the program's records per path: a library bug)
+         # faults MEM, loudly, rather than losing a write
+         "v_cmp_gt_u32_e64 vcc, s66, %s" % v(OFF),
+         "s_andn2_b64 %s, exec, vcc" % sp(S_JUNK),
+         "s_mov_b32 %s, 3" % s(S_CODE),
+         "s_and_b64 exec, exec, vcc",
+         "s_cbranch_execz .Lvs_ret",
+         # the record: log + 64 + slot * stride
+         "s_add_u32 s64, s64, 64",
+         "s_addc_u32 s65, s65, 0",
+         "v_mov_b32 %s, s67" % v(R[1]),
+         "v_mad_u64_u32 %s, vcc, %s, %s, s[64:65]" % (vp(NV[0]), v(OFF), v(R[1]))] + \
+        lane_pkt_index(R[0]) + [
+         "v_mov_b32 %s, s69" % v(R[1]),
+         "v_add_co_u32 %s, vcc, s68, %s" % (v(R[0]), v(R[0])),
+         "v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(R[1]), v(R[1])),
+         "global_store_dwordx2 %s, %s, off" % (vp(NV[0]), vp(R[0])),
+         "v_mov_b32 %s, %s" % (v(R[9]), v(VOFF)),
+         "global_store_dwordx2 %s, %s, off offset:8" % (vp(NV[0]), vp(WORD)),
+         "global_store_dwordx2 %s, %s, off offset:16" % (vp(NV[0]), vp(L_[0])),
+         "global_store_dword %s, %s, off offset:24" % (vp(NV[0]), v(SLOT)),
+         ".Lvs_ret:",
+         "v_readlane_b32 %s, v%d, 11" % (s(S_LINK), SPILL),
+         "v_readlane_b32 %s, v%d, 12" % (s(S_LINK + 1), SPILL),
+         "s_setpc_b64 %s" % sp(S_LINK)]
+    return L
+
+
 def update_routine():
     """UPDATE (called): r0 = map_update_elem(map, r2, r3, r4) for the map whose dp_map record is
     at byte offset s14 of the map table (ebpf_map.c:101-108 -> ebpf_map_array.c:185-211), with
@@ -1311,6 +1666,12 @@ def handler_body(name, d, sr):
         return h_cond32(c, d, sr, name.endswith("_I"))
     if name.startswith("STXGEN"):
         return h_stx_gen(int(name[6:]), d, sr), False
+    if name.startswith("CNTST"):
+        return h_stx_gen(int(name[5:]), d, sr, kind=2), False
+    if name.startswith("XADDF"):
+        return h_xadd(int(name[5:]), sr, d, True), False
+    if name.startswith("XADD"):
+        return h_xadd(int(name[4:]), d, sr, False), False
     if name.startswith("STGEN"):
         return h_st_gen(int(name[5:]), d), False
     if name == "EXIT":
@@ -1330,6 +1691,9 @@ def handler_body(name, d, sr):
         return call(".Lr_update"), False
     if name == "HDELETE":
         return call(".Lr_hdelete"), False
+    if name == "OVLINIT":
+        return ["v_mov_b32 %s, 0" % v(H[0]), "v_add_u32 %s, %d, v%d" % (v(H[1]), OVL_COUNT, V_STK),
+                "ds_write_b32 %s, %s" % (v(H[1]), v(H[0]))], False
     if name == "LOOPINIT":
         return ["v_mov_b32 %s, 0" % v(H[0]), "ds_write_b32 v%d, %s" % (V_STK, v(H[0]))], False
     if name == "LOOPCNT":
@@ -1532,13 +1896,37 @@ def routines():
           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
           "s_cmp_eq_u32 %s, 0" % s(S_T1),
           "s_cbranch_scc1 .Lck_map_ok",
-          # a store into a map value: MAP_WRITE fault for those lanes
+          # a store into a map value (ebpf_gpu.h "Stores into map values"): .Lr_vstore for those
+          # lanes (SGPRs it clobbers spilled to lanes of v51), whose address then points at the
+          # lane's scratch, so the handler's own store leaves the map alone
           "s_cmp_eq_u64 %s, 0" % sp(S_JUNK),
-          "s_cbranch_scc1 .Lck_map_next",
-          "s_mov_b64 %s, %s" % (sp(S_MASK), sp(S_JUNK)),
-          "s_mov_b32 %s, 9" % s(S_CODE),
-          "s_mov_b64 %s, %s" % (sp(S_REC + 6), sp(S_LINK))] + call(".Lr_fault") + [
-          "s_mov_b64 %s, %s" % (sp(S_LINK), sp(S_REC + 6)),
+          "s_cbranch_scc1 .Lck_map_next"]
+    spill = [(S_LINK, 0), (S_LINK + 1, 1), ("exec_lo", 2), ("exec_hi", 3), (S_T0, 4), (S_T1, 5),
+             (S_T2, 6), (S_OK, 7), (S_OK + 1, 8), (S_JUNK, 9), (S_JUNK + 1, 10)]
+    L += ["v_writelane_b32 v%d, %s, %d" % (SPILL, r if isinstance(r, str) else s(r), k) for r, k in spill]
+    L += ["s_mov_b64 exec, %s" % sp(S_JUNK)] + call(".Lr_vstore") + [
+          # the lanes that stored: ok, their address the scratch
+          "v_readlane_b32 %s, v%d, 9" % (s(S_MASK), SPILL),
+          "v_readlane_b32 %s, v%d, 10" % (s(S_MASK + 1), SPILL),
+          "s_andn2_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
+          "v_readlane_b32 %s, v%d, 7" % (s(S_OK), SPILL),
+          "v_readlane_b32 %s, v%d, 8" % (s(S_OK + 1), SPILL),
+          "s_or_b64 %s, %s, %s" % (sp(S_OK), sp(S_OK), sp(S_MASK)),
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "v_add_u32 %s, %d, v%d" % (v(H[0]), VST_SCRATCH, V_STK),
+          "v_mov_b32 %s, %s" % (v(H[1]), s(S_SHARED + 1)),
+          "v_readlane_b32 %s, v%d, 4" % (s(S_T0), SPILL),
+          "v_readlane_b32 %s, v%d, 5" % (s(S_T1), SPILL),
+          "v_readlane_b32 %s, v%d, 6" % (s(S_T2), SPILL),
+          "v_readlane_b32 exec_lo, v%d, 2" % SPILL,
+          "v_readlane_b32 exec_hi, v%d, 3" % SPILL,
+          # the lanes .Lr_vstore could not serve fault (S_CODE)
+          "s_cmp_eq_u64 %s, 0" % sp(S_JUNK),
+          "s_cbranch_scc1 .Lck_vs_ok",
+          "s_mov_b64 %s, %s" % (sp(S_MASK), sp(S_JUNK))] + call(".Lr_fault") + [
+          ".Lck_vs_ok:",
+          "v_readlane_b32 %s, v%d, 0" % (s(S_LINK), SPILL),
+          "v_readlane_b32 %s, v%d, 1" % (s(S_LINK + 1), SPILL),
           "s_branch .Lck_map_next",
           ".Lck_map_ok:",
           "s_or_b64 %s, %s, %s" % (ok, ok, sp(S_JUNK)),
@@ -1641,6 +2029,10 @@ def routines():
     L += hlookup_routine()
     L += update_routine()
     L += hdelete_routine()
+    L += vstore_routine()
+    # OVLFIX (called by generic loads when dp_launch.vflags bit 0): the packet's own stores over
+    # the S_T0 bytes at H[0:1] just read into H[2:3]
+    L += [".Lr_ovlfix:"] + ovl_fix("L", (H[2], H[3])) + ["s_setpc_b64 %s" % sp(S_LINK)]
     if not STAGED_IMAGE:
         # BATCH (regrouping; called by the compiled drain code): make the first n = S_T1 lanes the
         # running batch of the queue at s[64:65] from ring slot head = S_T2 on: their packet

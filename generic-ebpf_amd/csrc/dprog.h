@@ -46,6 +46,18 @@ enum dp_kind : uint16_t {
 	// table index): 0, the delete logged for after the batch (ebpf_map.c:130-136 ->
 	// ebpf_map_hashtable.c:475-502); a NULL key is EINVAL
 	DK_CALL_HDELETE = 0x110,
+	// Stores into map values with the device batch's counter semantics (ebpf_gpu.h "Stores into
+	// map values"): the STX of a counter update — the translator found LDX{W,DW} X = [P + off];
+	// ADD/SUB X; STX [P + off] = X on one path — stores X like the STX (dst = P, src = X, off;
+	// aux = 4 or 8 bytes) and, into a map value, adds X minus the value it re-reads there
+	// (the packet's own view: nothing stored in between) instead of overwriting it
+	DK_CNT_STORE = 0x111,
+	// XADD (standard semantics, BPF_STX | BPF_XADD): *(u32 / u64 *)(dst + off) += src; aux = 4
+	// or 8 bytes, | 0x100 when imm was BPF_FETCH (src = the old value)
+	DK_XADD = 0x112,
+	// A program that reads its own stores into map values starts here: the lane's overlay is
+	// emptied (dprog.h DP_OVL_COUNT = 0)
+	DK_OVLINIT = 0x113,
 };
 #define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
@@ -83,6 +95,12 @@ struct dp_map {
 	uint32_t flags;       // DP_MAP_HASH | log2(stride) << 16 | key_size (hashtable), else 0
 };
 #define DP_MAP_HASH 0x80000000u
+// Array maps the program changes only by counter updates, all aligned and of one width (the
+// translator proves it): those land as device atomics into the map's delta area, right after its
+// values in the mirror (dp_delta_off), added into the mirror after the batch.  Bit 28: 8-byte
+// counters (else 4-byte).
+#define DP_MAP_ATOMIC 0x40000000u
+#define DP_MAP_ATOMIC64 0x10000000u
 #define DP_HASH_MAX_KEY 65535u // (the key size field of dp_map.flags)
 #if defined(__HIPCC__)
 #define DP_FN __host__ __device__ static inline
@@ -95,6 +113,12 @@ DP_FN uint32_t dp_hash_key_bytes(uint32_t key_size) { return (key_size + 7u) & ~
 // offset of the value in a slot
 DP_FN uint32_t dp_hash_value_off(uint32_t key_size) { return 8u + dp_hash_key_bytes(key_size); }
 static_assert(sizeof(dp_map) == 32, "dp_map is 32 bytes");
+// An array mirror's bytes are padded to 64 (loads of whole 8-byte words stay inside it), then the
+// delta area of a DP_MAP_ATOMIC map (as many bytes again)
+DP_FN uint64_t dp_delta_off(uint32_t value_size, uint32_t max_entries)
+{
+	return ((uint64_t)value_size * max_entries + 63u) & ~(uint64_t)63u;
+}
 // A hashtable's device table is followed by a 16-byte trailer: u32 live entries of the table the
 // mirror was built from, u32 the map's max_entries (a device batch's map_update_elem of a new
 // key is EBUSY when the batch-start table is full, ebpf_map_hashtable.c:371-375)
@@ -157,11 +181,30 @@ struct dp_launch {
 	uint32_t span_slot;
 	uint32_t span_g;
 	uint32_t span_magic_g;    // ceil(2^32 / span_g)
-	uint32_t span_pad;
+	// stores into map values (ebpf_gpu.h "Stores into map values"): bit 0 = the program reads
+	// its own stores (an overlay of the words it stored, per lane: DP_OVL_* below); bits 8..15 =
+	// the overlay's entries per lane
+	uint32_t vflags;
 };
 static_assert(sizeof(dp_launch) == 208, "dp_launch layout is shared with the assembly kernels");
 static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_slot) == 192,
 	      "gen_interp.py loads these fields at fixed offsets");
+
+// The lane's LDS stack slice, below the frame the program addresses: the loop count (+0), the
+// overlay's entry count (+4), an 8-byte scratch a store into a map value is redirected to (+8)
+// and the overlay entries (+16: {u64 word address, u64 word as the packet sees it}, 16 B each).
+// Programs with value stores keep at least the first 16 bytes.
+#define DP_OVL_COUNT 4u
+#define DP_OVL_SCRATCH 8u
+#define DP_OVL_ENTRIES 16u
+#define DP_OVL_MAX 32u // overlay entries per lane at most (more: the program runs on the CPU)
+
+// Value-store records in the batch's write log: {u64 packet, u32 map << 20 | DP_REC_VALUE |
+// kind << 16 | size, u32 byte offset (array: in the map's values; hashtable: in the value),
+// u64 data (the stored bytes, or a counter's addend), u32 hashtable slot}
+#define DP_REC_VALUE 0x80000u
+#define DP_REC_ADD 0x10000u
+#define DP_REC_VALUE_BYTES 32u
 
 // Verdict partials of one assembly-kernel launch (gen_interp.py .Lfinish): 8 replicas of
 // EBPF_HIST_BINS u64 (workgroup w adds to replica w & 7), then 9 u32 arrival tickets on 64-B

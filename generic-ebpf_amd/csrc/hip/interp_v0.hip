@@ -38,30 +38,84 @@ struct regions {
 	uint64_t pkt_lo, pkt_len, stk_lo;
 };
 
-// 0 = ok, else fault code.  Ranges: [pkt_lo, pkt_lo+len), [stk_lo, stk_lo+512), map mirrors.
+// 0 = ok, else fault code.  Ranges: [pkt_lo, pkt_lo+len), [stk_lo, stk_lo+512), map mirrors'
+// values (*map = the map's table index when the access lies there, else -1).
 __device__ inline int
-check(const regions &rg, const dp_launch &L, uint64_t a, uint32_t size, bool write)
+check(const regions &rg, const dp_launch &L, uint64_t a, uint32_t size, bool write, int *map = nullptr)
 {
+	if (map)
+		*map = -1;
 	if (rg.pkt_len >= size && a - rg.pkt_lo <= rg.pkt_len - size)
 		return F_NONE;
 	if (a - rg.stk_lo <= (uint64_t)(kStack - size))
 		return F_NONE;
 	for (uint32_t m = 0; m < L.nmaps; m++) {
 		const dp_map &mp = L.maps[m];
+		bool in;
 		if (mp.flags & DP_MAP_HASH) { // only the value of an occupied-or-not slot
 			const uint32_t lg = dp_hash_stride_log2(mp.flags);
 			const uint64_t off = a - mp.dev_base;
 			const uint64_t vo = dp_hash_value_off(dp_hash_key_size(mp.flags));
 			const uint64_t so = off & ((1ull << lg) - 1);
-			if (off < ((uint64_t)mp.max_entries << lg) && so >= vo && so - vo + size <= mp.value_size)
-				return write ? F_MAP_WRITE : F_NONE;
-			continue;
+			in = off < ((uint64_t)mp.max_entries << lg) && so >= vo && so - vo + size <= mp.value_size;
+		} else {
+			const uint64_t bytes = (uint64_t)mp.value_size * mp.max_entries;
+			in = bytes >= size && a - mp.dev_base <= bytes - size;
 		}
-		uint64_t bytes = (uint64_t)mp.value_size * mp.max_entries;
-		if (bytes >= size && a - mp.dev_base <= bytes - size)
-			return write ? F_MAP_WRITE : F_NONE;
+		if (in) {
+			if (map)
+				*map = (int)m;
+			return F_NONE; // (stores too: ebpf_interpreter.c:343-366 writes the value in place)
+		}
 	}
 	return F_MEM;
+}
+
+// The packet's own stores into map values (dp_launch.vflags bit 0): whole 8-byte words of the
+// mirror as the packet sees them (dprog.h DP_OVL_*), newest last.
+struct overlay {
+	uint32_t n = 0;
+	uint64_t addr[DP_OVL_MAX];
+	uint64_t data[DP_OVL_MAX];
+};
+
+// `size` bytes at a: the mirror's (the batch-start values) with the packet's own stores over them
+__device__ inline uint64_t
+load_ovl(const overlay &o, uint64_t a, uint32_t size)
+{
+	uint64_t v = 0;
+	for (uint32_t i = 0; i < size; i++) {
+		const uint64_t b = a + i, w = b & ~7ull;
+		uint8_t x = *reinterpret_cast<const uint8_t *>(b);
+		for (uint32_t k = 0; k < o.n; k++)
+			if (o.addr[k] == w)
+				x = (uint8_t)(o.data[k] >> (8 * (b & 7)));
+		v |= (uint64_t)x << (8 * i);
+	}
+	return v;
+}
+
+// Remember a store of `size` bytes of v at a; false when the overlay is full (the translator
+// sizes it: never)
+__device__ inline bool
+ovl_store(overlay &o, uint64_t a, uint32_t size, uint64_t v)
+{
+	for (uint32_t i = 0; i < size; i++) {
+		const uint64_t b = a + i, w = b & ~7ull;
+		uint32_t k = 0;
+		while (k < o.n && o.addr[k] != w)
+			k++;
+		if (k == o.n) {
+			if (o.n == DP_OVL_MAX)
+				return false;
+			o.addr[k] = w;
+			o.data[k] = *reinterpret_cast<const uint64_t *>(w); // (mirrors are padded to 8)
+			o.n++;
+		}
+		const uint32_t sh = 8 * (uint32_t)(b & 7);
+		o.data[k] = (o.data[k] & ~(0xffull << sh)) | ((uint64_t)(uint8_t)(v >> (8 * i)) << sh);
+	}
+	return true;
 }
 
 __device__ inline uint64_t
@@ -123,19 +177,59 @@ hash_find(const dp_map &mp, const uint8_t *kp, uint32_t ks)
 	}
 }
 
-// A record in the batch's write log (dp_launch.upd_log): {u64 packet, u32 entry | map << 20,
-// u32 word}, the rest for the caller; NULL when the log is full (the host sizes it: never)
+// A record in the batch's write log (dp_launch.upd_log): {u64 packet, u32 map << 20, u32 word},
+// the rest for the caller; NULL when the log is full (the host sizes it: never)
 __device__ inline uint8_t *
-log_record(const dp_launch &L, uint64_t gid, uint32_t entry, uint32_t map, uint32_t word)
+log_record(const dp_launch &L, uint64_t gid, uint32_t map, uint32_t word)
 {
+	if (L.upd_log == nullptr)
+		return nullptr;
 	const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t *>(L.upd_log), 1u);
 	if (slot >= L.upd_cap)
 		return nullptr;
 	uint8_t *rec = L.upd_log + 64 + (uint64_t)slot * L.upd_stride;
 	*reinterpret_cast<uint64_t *>(rec) = L.pkt_base + gid;
-	*reinterpret_cast<uint32_t *>(rec + 8) = entry | (map << 20);
+	*reinterpret_cast<uint32_t *>(rec + 8) = map << 20;
 	*reinterpret_cast<uint32_t *>(rec + 12) = word;
 	return rec;
+}
+
+// A store of `size` bytes of v at a, inside the values of map mi (ebpf_gpu.h "Stores into map
+// values"): `add` for a counter update adding `delta` (an addition when aligned to its width
+// within the values, else a plain store of v).  UPD_ATOMIC maps take the addition into their
+// delta area; the rest log a record for after the batch.  The packet's overlay remembers v.
+// Returns 0 or a fault code.
+__device__ inline int
+value_store(const dp_launch &L, uint64_t gid, overlay &o, int mi, uint64_t a, uint32_t size,
+	    uint64_t v, bool add, uint64_t delta)
+{
+	const dp_map &mp = L.maps[mi];
+	uint64_t off = a - mp.dev_base, voff = off;
+	uint32_t slot = 0;
+	if (mp.flags & DP_MAP_HASH) {
+		const uint32_t lg = dp_hash_stride_log2(mp.flags);
+		slot = (uint32_t)(off >> lg);
+		voff = (off & ((1ull << lg) - 1)) - dp_hash_value_off(dp_hash_key_size(mp.flags));
+	}
+	add = add && voff % size == 0;
+	if ((L.vflags & 1) && !ovl_store(o, a, size, v))
+		return F_MEM;
+	if (add && (mp.flags & DP_MAP_ATOMIC)) {
+		uint8_t *d = reinterpret_cast<uint8_t *>(mp.dev_base) + dp_delta_off(mp.value_size, mp.max_entries) + off;
+		if (size == 8)
+			atomicAdd(reinterpret_cast<unsigned long long *>(d), (unsigned long long)delta);
+		else
+			atomicAdd(reinterpret_cast<uint32_t *>(d), (uint32_t)delta);
+		return F_NONE;
+	}
+	uint8_t *rec = log_record(L, gid, (uint32_t)mi, (uint32_t)voff);
+	if (rec == nullptr)
+		return F_MEM;
+	const uint64_t mask = size == 8 ? ~0ull : (1ull << (8 * size)) - 1;
+	*reinterpret_cast<uint32_t *>(rec + 8) = ((uint32_t)mi << 20) | DP_REC_VALUE | (add ? DP_REC_ADD : 0u) | size;
+	*reinterpret_cast<uint64_t *>(rec + 16) = (add ? delta : v) & mask;
+	*reinterpret_cast<uint32_t *>(rec + 24) = slot;
+	return F_NONE;
 }
 
 __global__ __launch_bounds__(kWG) void
@@ -174,6 +268,7 @@ ebpf_interp_v0(dp_launch L)
 	int fault = F_NONE;
 	uint64_t result = 0;
 	uint32_t back = 0; // taken backward jumps (DK_LOOPCNT, standard semantics)
+	overlay ovl;       // stores into map values the packet reads back (dp_launch.vflags)
 
 	for (;;) {
 		const uint64_t am = __ballot(active);
@@ -203,6 +298,10 @@ ebpf_interp_v0(dp_launch L)
 		}
 		if (k == DK_LOOPINIT) {
 			back = 0;
+			continue;
+		}
+		if (k == DK_OVLINIT) {
+			ovl.n = 0;
 			continue;
 		}
 		if (k == DK_LOOPCNT) {
@@ -277,7 +376,7 @@ ebpf_interp_v0(dp_launch L)
 							active = false;
 							continue;
 						}
-						uint8_t *rec = log_record(L, gid, t, e.aux, (uint32_t)r4 << 8);
+						uint8_t *rec = log_record(L, gid, e.aux, (uint32_t)r4 << 8);
 						if (!rec) {
 							fault = F_MEM;
 							active = false;
@@ -305,7 +404,7 @@ ebpf_interp_v0(dp_launch L)
 						continue;
 					}
 					if (key < mp.max_entries) {
-						uint8_t *rec = log_record(L, gid, t, e.aux, key);
+						uint8_t *rec = log_record(L, gid, e.aux, key);
 						if (!rec) {
 							fault = F_MEM; // (the host sizes the log: never)
 							active = false;
@@ -330,7 +429,7 @@ ebpf_interp_v0(dp_launch L)
 				const dp_map &mp = L.maps[e.aux];
 				const uint32_t ks = dp_hash_key_size(mp.flags);
 				int f = check(rg, L, r2, ks, false);
-				uint8_t *rec = f ? nullptr : log_record(L, gid, t, e.aux, 1);
+				uint8_t *rec = f ? nullptr : log_record(L, gid, e.aux, 1);
 				if (f || !rec) {
 					fault = f ? f : F_MEM;
 					active = false;
@@ -382,28 +481,51 @@ ebpf_interp_v0(dp_launch L)
 				T = e.target;
 			continue;
 		}
-		if (cls == 0x1) { // LDX
+		if (k < 0x100 && cls == 0x1) { // LDX
 			const uint32_t size = (k & 0x18) == 0x00 ? 4 : (k & 0x18) == 0x08 ? 2 : (k & 0x18) == 0x10 ? 1 : 8;
 			const uint64_t a = R[e.src][tid] + (uint64_t)(int64_t)e.off;
-			int f = check(rg, L, a, size, false);
+			int mi;
+			int f = check(rg, L, a, size, false, &mi);
 			if (f) {
 				fault = f;
 				active = false;
 				continue;
 			}
-			R[e.dst][tid] = load_bytes(a, size);
+			R[e.dst][tid] = mi >= 0 && ovl.n ? load_ovl(ovl, a, size) : load_bytes(a, size);
 			continue;
 		}
-		if (cls == 0x2 || cls == 0x3) { // ST / STX
-			const uint32_t size = (k & 0x18) == 0x00 ? 4 : (k & 0x18) == 0x08 ? 2 : (k & 0x18) == 0x10 ? 1 : 8;
+		if (k == DK_CNT_STORE || k == DK_XADD || cls == 0x2 || cls == 0x3) {
+			// ST / STX; the STX of a counter update; XADD (standard semantics)
+			const uint32_t size = k >= 0x100 ? (e.aux & 0xff)
+					      : (k & 0x18) == 0x00 ? 4 : (k & 0x18) == 0x08 ? 2 : (k & 0x18) == 0x10 ? 1 : 8;
 			const uint64_t a = R[e.dst][tid] + (uint64_t)(int64_t)e.off;
-			int f = check(rg, L, a, size, true);
+			int mi;
+			int f = check(rg, L, a, size, true, &mi);
 			if (f) {
 				fault = f;
 				active = false;
 				continue;
 			}
-			store_bytes(a, size, cls == 0x2 ? e.imm : R[e.src][tid]);
+			const uint64_t mask = size == 8 ? ~0ull : (1ull << (8 * size)) - 1;
+			uint64_t v = cls == 0x2 ? e.imm : R[e.src][tid], delta = 0, old = 0;
+			const bool add = k == DK_CNT_STORE || k == DK_XADD;
+			if (add) {
+				old = mi >= 0 && ovl.n ? load_ovl(ovl, a, size) : load_bytes(a, size);
+				delta = k == DK_XADD ? v : v - old; // (a counter update: what the ADD / SUB added)
+				if (k == DK_XADD)
+					v = old + v;
+			}
+			if (mi >= 0)
+				f = value_store(L, gid, ovl, mi, a, size, v, add, delta & mask);
+			else
+				store_bytes(a, size, v);
+			if (f) {
+				fault = f;
+				active = false;
+				continue;
+			}
+			if (k == DK_XADD && (e.aux & 0x100)) // BPF_FETCH: src = the old value
+				R[e.src][tid] = old & mask;
 			continue;
 		}
 		if (k == 0x18) { // LDDW

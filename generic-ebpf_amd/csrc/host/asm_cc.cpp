@@ -1493,6 +1493,14 @@ struct emitter {
 	}
 };
 
+// the STX of a counter update, XADD (ebpf_gpu.h "Stores into map values"): generic stores
+bool
+is_value_store_fam(int fam)
+{
+	return fam == AHF_CNTST4 || fam == AHF_CNTST8 || fam == AHF_XADD4 || fam == AHF_XADD8 ||
+	       fam == AHF_XADDF4 || fam == AHF_XADDF8;
+}
+
 bool
 is_cond_fam(int fam)
 {
@@ -1512,6 +1520,7 @@ written_reg(int fam, int d)
 	case AHF_STXSTK1: case AHF_STXSTK2: case AHF_STXSTK4: case AHF_STXSTK8:
 	case AHF_STGEN1: case AHF_STGEN2: case AHF_STGEN4: case AHF_STGEN8:
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8:
+	case AHF_CNTST4: case AHF_CNTST8: case AHF_XADD4: case AHF_XADD8: case AHF_OVLINIT:
 		return -1;
 	default:
 		if (is_cond_fam(fam))
@@ -1530,7 +1539,7 @@ copied_uses(int fam, int d, int s)
 	case AHF_LOOKUPGEN: return (1u << 1) | (1u << 2);
 	case AHF_HLOOKUP: case AHF_HDELETE: return 1u << 2;
 	case AHF_UPDATE: return (1u << 2) | (1u << 3) | (1u << 4);
-	case AHF_FAULT: case AHF_NOP: case AHF_LOOKUPSTK: return 0;
+	case AHF_FAULT: case AHF_NOP: case AHF_LOOKUPSTK: case AHF_OVLINIT: return 0;
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8: return 0;
 	case AHF_LDXPKTG1: case AHF_LDXPKTG2: case AHF_LDXPKTG4: case AHF_LDXPKTG8: return 0;
 	case AHF_LDXSTK1: case AHF_LDXSTK2: case AHF_LDXSTK4: case AHF_LDXSTK8: return 0;
@@ -1552,7 +1561,7 @@ copied_result(int fam)
 	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: case AHF_LDXHV2:
 	case AHF_LDXPKC2: return kbits(16);
 	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: case AHF_LDXHV4:
-	case AHF_LDXPKC4: return kbits(32);
+	case AHF_LDXPKC4: case AHF_XADDF4: return kbits(32);
 	default:
 		if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
 			return kbits(32);
@@ -1849,7 +1858,8 @@ cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const s
 	// no map write (the main run executes it again from the packet as the caller gave it)
 	auto prefix_ok = [&](int fam) {
 		return !((fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) ||
-			 fam == AHF_UPDATE || fam == AHF_HDELETE || fam == AHF_LOOPINIT || fam == AHF_LOOPCNT);
+			 fam == AHF_UPDATE || fam == AHF_HDELETE || fam == AHF_LOOPINIT || fam == AHF_LOOPCNT ||
+			 is_value_store_fam(fam));
 	};
 	std::vector<uint32_t> parent(n, UINT32_MAX), npred(n, 0), sz(n, 0);
 	for (uint32_t e : order) {
@@ -2054,7 +2064,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				return (ah_flags[(uint32_t)low[e].handler] & 1) || fam == AHF_EXIT ||
 				       fam == AHF_FAULT || fam == AHF_LOOKUPGEN ||
 				       (fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8) ||
-				       (fam >= AHF_STGEN1 && fam <= AHF_STGEN8);
+				       (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || is_value_store_fam(fam);
 			};
 			while (j + 1 < order.size() && !breaks_after(order[j]) &&
 			       xl.entries[order[j]].next == order[j + 1] && !entry_point[order[j + 1]])
@@ -2389,7 +2399,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				// stores through unknown pointers may hit the stack
 				if (fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8)
 					f.nst = 0;
-				if (fam >= AHF_STGEN1 && fam <= AHF_STGEN8)
+				if ((fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || is_value_store_fam(fam))
 					f.nst = 0;
 				if (fam >= AHF_STSTK1 && fam <= AHF_STSTK8)
 					f.store(aux0, 1 << (fam - AHF_STSTK1), -1);
@@ -2445,6 +2455,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				if (!out[e].fast &&
 				    ((fam >= AHF_LDXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
 				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN ||
+				     is_value_store_fam(fam) ||
 				     fam == AHF_UPDATE || fam == AHF_HDELETE))
 					needs_pkt = true;
 			}

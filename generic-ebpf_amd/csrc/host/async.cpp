@@ -74,7 +74,7 @@ writes_maps(struct ebpf_prog *ep)
 {
 	if (prog_ensure_translated(ep) != 0)
 		return false; // (the job fails with the same error when it runs)
-	return ep->xlated->max_updates != 0;
+	return prog_writes_maps(*ep->xlated);
 }
 
 void

@@ -352,6 +352,12 @@ ensure_translated_locked(struct ebpf_prog *ep)
 	return ensure_translated(ep);
 }
 
+bool
+in_list(const std::vector<uint16_t> &v, size_t t)
+{
+	return std::find(v.begin(), v.end(), (uint16_t)t) != v.end();
+}
+
 int
 ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 {
@@ -360,7 +366,13 @@ ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 		em->mirrors.resize(device + 1);
 	map_mirror &m = em->mirrors[device];
 	if (m.dev == nullptr) {
-		hipError_t e = hipMalloc(&m.dev, map_device_layout_of(em).bytes);
+		// an array: its values padded to 64 bytes, then the delta area of counter updates
+		// (dprog.h dp_delta_off), both zero until the first upload
+		const size_t bytes = em->is_hashtable() ? map_device_layout_of(em).bytes
+							: 2 * dp_delta_off(em->value_size, em->max_entries);
+		hipError_t e = hipMalloc(&m.dev, bytes);
+		if (e == hipSuccess && !em->is_hashtable())
+			e = hipMemset(m.dev, 0, bytes);
 		if (e != hipSuccess)
 			return hip_fail(e, "hipMalloc(map mirror)");
 		m.version = ~0ull;
@@ -537,6 +549,10 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		m.dev_base = (uint64_t)(uintptr_t)mdev;
 		nd->table.push_back(m);
 	}
+	// arrays changed only by counter updates: device atomics into their delta areas
+	for (size_t k = 0; k < ep->xlated->atomic_maps.size(); k++)
+		nd->table[ep->xlated->atomic_maps[k]].flags |=
+		    DP_MAP_ATOMIC | (ep->xlated->atomic_width[k] == 8 ? DP_MAP_ATOMIC64 : 0u);
 	if (!nd->table.empty()) {
 		e = hipMalloc(&nd->d_maps, nd->table.size() * sizeof(dp_map));
 		if (e != hipSuccess)
@@ -547,29 +563,44 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 			return hip_fail(e, "hipMemcpy(map table)");
 	}
 	nd->nmaps = (uint32_t)nd->table.size();
-	if (ep->xlated->max_updates) {
-		// map writes: the apply step's view of the table (map_writes.h), winner words for
-		// every key of every written map, the log record size
-		// (hashtable records: {u64 packet, u32 entry | map << 20, u32 op, key, value}, the key
-		// and the value each padded to 8 bytes)
+	if (prog_writes_maps(*ep->xlated)) {
+		// map writes: the apply step's view of the table (map_writes.h), winner words for every
+		// byte of every map whose records land on the device, the log record size
+		// (update records: {u64 packet, u32 map << 20, u32 key, value}; hashtable update records
+		// {u64 packet, u32 map << 20, u32 op, key, value}, the key and the value each padded to
+		// 8 bytes; value-store records DP_REC_VALUE_BYTES)
+		const dprog_host &xl = *ep->xlated;
 		std::vector<upd_map> um(nd->table.size());
 		uint32_t rmax = 8;
-		const std::vector<uint16_t> &arr = ep->xlated->upd_maps, &hash = ep->xlated->hupd_maps;
 		for (size_t t = 0; t < nd->table.size(); t++) {
 			um[t].dev_base = nd->table[t].dev_base;
 			um[t].value_size = nd->table[t].value_size;
 			um[t].max_entries = nd->table[t].max_entries;
 			um[t].win_off = nd->win_words;
-			um[t].is_hash = (nd->table[t].flags & DP_MAP_HASH) ? 1u : 0u;
-			if (std::find(arr.begin(), arr.end(), (uint16_t)t) != arr.end()) {
-				nd->win_words += nd->table[t].max_entries;
+			um[t].cls = UPD_NONE;
+			if (in_list(xl.upd_maps, t)) {
+				um[t].cls = UPD_DEVICE;
+				nd->win_words += (uint64_t)nd->table[t].value_size * nd->table[t].max_entries;
 				rmax = std::max(rmax, (nd->table[t].value_size + 7) & ~7u);
 			}
-			if (std::find(hash.begin(), hash.end(), (uint16_t)t) != hash.end())
-				rmax = std::max(rmax, dp_hash_key_bytes(dp_hash_key_size(nd->table[t].flags)) +
-							  ((nd->table[t].value_size + 7) & ~7u));
+			if (in_list(xl.hupd_maps, t)) {
+				um[t].cls = UPD_HOST;
+				if (nd->table[t].flags & DP_MAP_HASH)
+					rmax = std::max(rmax, dp_hash_key_bytes(dp_hash_key_size(nd->table[t].flags)) +
+								  ((nd->table[t].value_size + 7) & ~7u));
+				else
+					rmax = std::max(rmax, (nd->table[t].value_size + 7) & ~7u);
+			}
+			for (size_t k = 0; k < xl.atomic_maps.size(); k++)
+				if (xl.atomic_maps[k] == t) {
+					um[t].cls = UPD_ATOMIC;
+					um[t].width = xl.atomic_width[k];
+				}
 		}
+		if (xl.vstore_sites)
+			rmax = std::max(rmax, DP_REC_VALUE_BYTES - 16);
 		nd->upd_stride = 16 + rmax;
+		nd->upd_host = um;
 		if ((e = hipMalloc(&nd->d_upd, um.size() * sizeof(upd_map))) != hipSuccess ||
 		    (e = hipMemcpy(nd->d_upd, um.data(), um.size() * sizeof(upd_map),
 				   hipMemcpyHostToDevice)) != hipSuccess)
@@ -681,16 +712,19 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 int
 upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
 {
-	for (uint16_t t : ep->xlated->upd_maps) { // (the writes land after other streams' readers)
+	std::vector<uint16_t> dev = ep->xlated->upd_maps;
+	dev.insert(dev.end(), ep->xlated->atomic_maps.begin(), ep->xlated->atomic_maps.end());
+	for (uint16_t t : dev) { // (the writes land after other streams' readers)
 		struct ebpf_map *em = ep->xlated->maps[t];
 		std::lock_guard<std::mutex> g(em->mirror_lock);
 		mirror_write_begin(em->mirrors[dp->device], stream);
 	}
 	hipError_t e = launch_map_writes(P.log, P.cap, dp->upd_stride,
-					 static_cast<const upd_map *>(dp->d_upd), P.win, P.faulted, stream);
+					 static_cast<const upd_map *>(dp->d_upd), dp->upd_host.data(),
+					 (uint32_t)dp->upd_host.size(), P.win, P.faulted, stream);
 	if (e != hipSuccess)
 		return hip_fail(e, "map writes");
-	for (uint16_t t : ep->xlated->upd_maps)
+	for (uint16_t t : dev)
 		map_mark_device_write(ep->xlated->maps[t], dp->device, static_cast<void *>(stream));
 	return 0;
 }
@@ -717,7 +751,7 @@ bucket_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launc
 	// opt-in (EBPF_BUCKET=1) until it beats the plain launch on C5
 	const char *on = getenv("EBPF_BUCKET");
 	return on && *on == '1' && L.offsets != nullptr && L.count >= kBucketMin && L.count < kBucketMax &&
-	       ep->xlated->asm_span && ep->xlated->max_updates == 0 && dp->jit_rq_bytes[0] == 0;
+	       ep->xlated->asm_span && !prog_writes_maps(*ep->xlated) && dp->jit_rq_bytes[0] == 0;
 }
 
 int
@@ -835,7 +869,7 @@ pathsort_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_lau
 	if (const char *m = getenv("EBPF_PATHSORT_MINBATCH"))
 		min = strtoull(m, nullptr, 0);
 	return L.offsets != nullptr && L.count >= min && L.count < kBucketMax &&
-	       ep->xlated->max_updates == 0 && dp->jit_rq_bytes[0] == 0 && dp->ps_err == 0;
+	       !prog_writes_maps(*ep->xlated) && dp->jit_rq_bytes[0] == 0 && dp->ps_err == 0;
 }
 
 int
@@ -935,6 +969,7 @@ struct host_log {
 	uint32_t stride = 0;
 	std::vector<uint32_t> faulted;
 	uint64_t first = 0;
+	int device = -1;
 };
 
 // Copy the plan's log (its records and faulted-packet bitmap) to the host.  Synchronous.
@@ -943,11 +978,12 @@ upd_fetch(const dprog_device *dp, const upd_plan &P, hipStream_t stream, uint64_
 {
 	hipError_t e = hipStreamSynchronize(stream);
 	uint32_t n = 0;
-	if (e == hipSuccess)
+	if (e == hipSuccess && P.cap)
 		e = hipMemcpy(&n, P.log, 4, hipMemcpyDeviceToHost);
 	out->count = std::min(n, P.cap);
 	out->stride = dp->upd_stride;
 	out->first = first;
+	out->device = dp->device;
 	out->rec.resize((size_t)out->count * out->stride);
 	out->faulted.resize(P.faulted_bytes / 4);
 	if (e == hipSuccess && out->count)
@@ -958,21 +994,41 @@ upd_fetch(const dprog_device *dp, const upd_plan &P, hipStream_t stream, uint64_
 	return e == hipSuccess ? 0 : hip_fail(e, "map-write log copy");
 }
 
-// The logs of a batch applied on the host, every record of a packet that did not fault in
-// (global packet, call) order:
-//   - hashtable records (always): replayed through the map's own update / delete (the program
-//     side of ebpf_map_hashtable.c:346-431 / :475-502, percpu: the submitting CPU's value) with
-//     the call's arguments; a replayed call that fails against the table as it then is (EEXIST,
-//     ENOENT, EBUSY) leaves it unchanged;
-//   - array records (`arrays`: a batch whose shards ran on several devices): the value copied
-//     into the host copy, so the last write of a key wins — the device apply step's rule
-//     (map_writes.hip); every device mirror of those maps is then stale.
+// A counter update, a store, or an update / delete call, applied to the host copy of a map.
+void
+apply_value(uint8_t *at, uint32_t size, bool add, const uint8_t *data)
+{
+	if (!add) {
+		memcpy(at, data, size);
+		return;
+	}
+	uint64_t v = 0, d = 0;
+	memcpy(&v, at, size);
+	memcpy(&d, data, size);
+	v += d;
+	memcpy(at, &v, size);
+}
+
+// The logs of a batch applied on the host, every record of a packet that did not fault (a
+// counter update's record even then: ebpf_gpu.h) in (global packet, call) order:
+//   - records of hupd_maps (hashtables; arrays mixing counter updates and stores), always:
+//     hashtable update / delete calls replayed through the map's own update / delete (the
+//     program side of ebpf_map_hashtable.c:346-431 / :475-502, percpu: the submitting CPU's
+//     value), a replayed call that fails against the table as it then is (EEXIST, ENOENT, EBUSY)
+//     leaving it unchanged; stores and counter updates into a hashtable value applied to the
+//     element with the slot's key (the device table's image) if it still exists; array stores
+//     and counter updates applied to the host copy;
+//   - records of upd_maps (`arrays`: a batch whose shards ran on several devices) too, so the
+//     last write of a byte wins — the device apply step's rule (map_writes.hip); every device
+//     mirror of the maps changed here is then stale.
 int
 upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arrays)
 {
+	const dprog_host &xl = *ep->xlated;
 	struct ref {
 		uint64_t order;
 		const uint8_t *r;
+		int device;
 	};
 	std::vector<ref> all;
 	for (const host_log &h : logs)
@@ -982,13 +1038,13 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 			uint32_t em;
 			memcpy(&pkt, r, 8);
 			memcpy(&em, r + 8, 4);
-			if ((em >> 20) >= ep->xlated->maps.size())
+			if ((em >> 20) >= xl.maps.size())
 				return fail(EIO, "map-write log: a record names no map of the program");
-			if (pkt / 32 < h.faulted.size() && ((h.faulted[pkt / 32] >> (pkt % 32)) & 1))
-				continue; // the packet faulted: none of its writes land
-			const bool hash = ep->xlated->maps[em >> 20]->is_hashtable();
-			if (hash || arrays)
-				all.push_back(ref{h.first + pkt, r});
+			const bool add = (em & DP_REC_VALUE) && (em & DP_REC_ADD);
+			if (!add && pkt / 32 < h.faulted.size() && ((h.faulted[pkt / 32] >> (pkt % 32)) & 1))
+				continue; // the packet faulted: none of its writes land (counter updates do)
+			if (in_list(xl.hupd_maps, em >> 20) || (arrays && in_list(xl.upd_maps, em >> 20)))
+				all.push_back(ref{h.first + pkt, r, h.device});
 		}
 	// Within a packet the records are already in call order: a lane takes its log slots one call
 	// after the other and every log is gathered in slot order.  (The entry index is no order: a
@@ -996,15 +1052,45 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 	// numbered after entries that a path reaches later.)  So sort by packet only, stably.
 	std::stable_sort(all.begin(), all.end(), [](const ref &a, const ref &b) { return a.order < b.order; });
 	const uint16_t cpu = map_current_cpu();
-	if (arrays)
-		for (uint16_t t : ep->xlated->upd_maps)
-			if (map_pull_device_writes(ep->xlated->maps[t]) != 0)
-				return fail(EIO, "copying a device batch's map writes back failed");
+	std::vector<uint16_t> host_arrays; // the array maps whose host copy changes here
+	for (size_t t = 0; t < xl.maps.size(); t++)
+		if (!xl.maps[t]->is_hashtable() &&
+		    (in_list(xl.hupd_maps, t) || (arrays && in_list(xl.upd_maps, t))))
+			host_arrays.push_back((uint16_t)t);
+	for (uint16_t t : host_arrays)
+		if (map_pull_device_writes(xl.maps[t]) != 0)
+			return fail(EIO, "copying a device batch's map writes back failed");
 	for (const ref &x : all) {
 		uint32_t em, word;
 		memcpy(&em, x.r + 8, 4);
 		memcpy(&word, x.r + 12, 4);
-		struct ebpf_map *m = ep->xlated->maps[em >> 20];
+		struct ebpf_map *m = xl.maps[em >> 20];
+		if (em & DP_REC_VALUE) {
+			const uint32_t size = em & 0xf;
+			const bool add = (em & DP_REC_ADD) != 0;
+			if (m->is_hashtable()) {
+				uint32_t slot;
+				memcpy(&slot, x.r + 24, 4);
+				const map_device_layout l = map_device_layout_of(m);
+				std::lock_guard<std::mutex> g(m->mirror_lock);
+				if (x.device < 0 || x.device >= (int)m->mirrors.size() || slot >= l.slots)
+					continue;
+				const std::vector<uint8_t> &img = m->mirrors[x.device].image;
+				const size_t so = (size_t)slot << dp_hash_stride_log2(l.flags);
+				if (so + 8 + m->key_size > img.size())
+					continue;
+				uint8_t *v = static_cast<uint8_t *>(
+				    m->emt->ops.lookup_elem(m, const_cast<uint8_t *>(img.data() + so + 8)));
+				if (v != nullptr && word + size <= m->value_size) // (deleted before: nothing)
+					apply_value(v + word, size, add, x.r + 16);
+				continue;
+			}
+			if ((uint64_t)word + size > (uint64_t)m->value_size * m->max_entries)
+				continue;
+			uint8_t *img = const_cast<uint8_t *>(map_array_image(m, m->percpu ? cpu : 0));
+			apply_value(img + word, size, add, x.r + 16);
+			continue;
+		}
 		if (m->is_hashtable()) {
 			void *key = const_cast<uint8_t *>(x.r + 16);
 			void *value = const_cast<uint8_t *>(x.r + 16 + dp_hash_key_bytes(m->key_size));
@@ -1019,25 +1105,76 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 		uint8_t *img = const_cast<uint8_t *>(map_array_image(m, m->percpu ? cpu : 0));
 		memcpy(img + (size_t)m->value_size * word, x.r + 16, m->value_size);
 	}
-	if (arrays)
-		for (uint16_t t : ep->xlated->upd_maps)
-			ep->xlated->maps[t]->version.fetch_add(1);
+	for (uint16_t t : host_arrays)
+		xl.maps[t]->version.fetch_add(1);
 	return 0;
 }
 
-// The end of a map-writing batch on one device: array writes applied on the device
-// (upd_apply), hashtable writes copied to the host and replayed there (synchronous).
+// A batch sharded over several devices: the counter updates of its UPD_ATOMIC maps, summed in
+// each device's delta area (one area per device, however many shards ran there), go into the
+// host copy — after every shard is done — and the areas are zeroed.  The device mirrors are then
+// stale.
+int
+delta_merge_host(struct ebpf_prog *ep, int ndev, const int *devices)
+{
+	const dprog_host &xl = *ep->xlated;
+	if (xl.atomic_maps.empty())
+		return 0;
+	const uint16_t cpu = map_current_cpu();
+	for (size_t k = 0; k < xl.atomic_maps.size(); k++) {
+		struct ebpf_map *m = xl.maps[xl.atomic_maps[k]];
+		if (map_pull_device_writes(m) != 0)
+			return fail(EIO, "copying a device batch's map writes back failed");
+		const uint32_t w = xl.atomic_width[k];
+		const size_t bytes = (size_t)m->value_size * m->max_entries;
+		uint8_t *img = const_cast<uint8_t *>(map_array_image(m, m->percpu ? cpu : 0));
+		std::vector<uint8_t> d(bytes);
+		for (int q = 0; q < ndev; q++) {
+			bool seen = false;
+			for (int q2 = 0; q2 < q; q2++)
+				seen = seen || devices[q2] == devices[q];
+			if (seen)
+				continue;
+			void *mdev = nullptr;
+			{
+				std::lock_guard<std::mutex> g(m->mirror_lock);
+				if (devices[q] < (int)m->mirrors.size())
+					mdev = m->mirrors[devices[q]].dev;
+			}
+			if (mdev == nullptr)
+				continue;
+			device_guard g2;
+			hipError_t e = hipSetDevice(devices[q]);
+			uint8_t *da = static_cast<uint8_t *>(mdev) + dp_delta_off(m->value_size, m->max_entries);
+			if (e == hipSuccess)
+				e = hipMemcpy(d.data(), da, bytes, hipMemcpyDeviceToHost);
+			if (e == hipSuccess)
+				e = hipMemset(da, 0, bytes);
+			if (e != hipSuccess)
+				return hip_fail(e, "counter updates copy");
+			for (size_t o = 0; o < bytes; o += w)
+				apply_value(img + o, w, true, d.data() + o);
+		}
+		m->version.fetch_add(1);
+	}
+	return 0;
+}
+
+// The end of a map-writing batch on one device: records of upd_maps and the counter updates of
+// atomic_maps applied on the device (upd_apply), records of hupd_maps copied to the host and
+// replayed there (synchronous).
 int
 upd_finish(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t stream)
 {
-	const bool hash = !ep->xlated->hupd_maps.empty();
-	std::vector<host_log> logs(hash ? 1 : 0);
+	const bool host = !ep->xlated->hupd_maps.empty();
+	std::vector<host_log> logs(host ? 1 : 0);
 	int err;
-	if (hash && (err = upd_fetch(dp, P, stream, 0, &logs[0])))
+	if (host && (err = upd_fetch(dp, P, stream, 0, &logs[0])))
 		return err;
-	if (!ep->xlated->upd_maps.empty() && (err = upd_apply(ep, dp, P, stream)))
+	if ((!ep->xlated->upd_maps.empty() || !ep->xlated->atomic_maps.empty()) &&
+	    (err = upd_apply(ep, dp, P, stream)))
 		return err;
-	return hash ? upd_apply_host(ep, logs, false) : 0;
+	return host ? upd_apply_host(ep, logs, false) : 0;
 }
 
 int
@@ -1050,13 +1187,15 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	L.nmaps = dp->nmaps;
 	L.nentries = dp->nentries;
 	L.start = ep->xlated->start;
+	L.vflags = (ep->xlated->vstore_overlay ? 1u : 0u) | (ep->xlated->vstore_sites ? 2u : 0u) |
+		   (ep->xlated->ovl_entries << 8);
 	launch_order order(ep->xlated->maps);
 	int err = sync_map_mirrors(ep, dp->device, stream);
 	if (err)
 		return err;
 	hipError_t e;
 	upd_plan own;
-	if (ep->xlated->max_updates) {
+	if (prog_writes_maps(*ep->xlated)) {
 		if (plan == nullptr && (err = upd_plan_for(ep, dp, L0.count, stream, &own)))
 			return err; // (this launch is the whole batch: its own log, applied below)
 		const upd_plan &P = plan ? *plan : own;
@@ -1143,7 +1282,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	}
 	if (e != hipSuccess)
 		return hip_fail(e, "kernel launch");
-	if (ep->xlated->max_updates && plan == nullptr)
+	if (prog_writes_maps(*ep->xlated) && plan == nullptr)
 		return upd_finish(ep, dp, own, stream);
 	return 0;
 }
@@ -1561,7 +1700,7 @@ batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch, 
 	L.count = batch->count;
 	L.stride = batch->stride;
 	hipStream_t st = static_cast<hipStream_t>(stream);
-	if (keep && ep->xlated->max_updates) {
+	if (keep && prog_writes_maps(*ep->xlated)) {
 		if ((err = sync_map_mirrors(ep, device, st)) ||
 		    (err = upd_plan_for(ep, dp, batch->count, st, keep)))
 			return err;
@@ -1604,7 +1743,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	// a map-writing program: one log for the whole shard, applied after its last chunk (every
 	// chunk reads the maps as they were when the batch started)
 	upd_plan plan;
-	if (ep->xlated->max_updates) {
+	if (prog_writes_maps(*ep->xlated)) {
 		// the log is set up on stream 0; the odd chunks run on stream 1 and log into it too
 		if ((err = upd_plan_for(ep, dp, hi - lo, S.stream[0], &plan)))
 			return err;
@@ -1691,7 +1830,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 		if ((e = hipStreamSynchronize(S.stream[i])) != hipSuccess || (e = collect(i)) != hipSuccess)
 			return drain(hip_fail(e, "batch"));
 	}
-	if (ep->xlated->max_updates && hi > lo) {
+	if (prog_writes_maps(*ep->xlated) && hi > lo) {
 		if (log_out) // (several shards: the caller merges the logs)
 			return upd_fetch(dp, plan, S.stream[0], lo, log_out);
 		if ((err = upd_finish(ep, dp, plan, S.stream[0])))
@@ -1786,7 +1925,7 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 	device_guard dg;
 	// a map-writing program: each shard's writes stay in its log, merged and applied on the host
 	// in global packet order after every shard is done
-	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates;
+	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && prog_writes_maps(*ep->xlated);
 	std::vector<host_log> logs(merge ? ndev : 0);
 	std::vector<dprog_device *> dps(ndev);
 	std::vector<staging *> S(ndev, nullptr);
@@ -1824,7 +1963,7 @@ ebpf_prog_run_batch_multi(struct ebpf_prog *ep, int ndev, const int *devices,
 	for (staging *s : S)
 		if (s)
 			staging_release(s);
-	if (!err && merge)
+	if (!err && merge && !(err = delta_merge_host(ep, ndev, devices)))
 		err = upd_apply_host(ep, logs, true);
 	if (err || !stats)
 		return err;
@@ -1860,7 +1999,7 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 	// A map-writing program on several shards: the batch is the shards in list order; each
 	// shard's writes stay in its log, copied to the host after its launch (synchronous), and
 	// the merged logs are applied there in global packet order when every shard is done.
-	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && ep->xlated->max_updates;
+	const bool merge = ndev > 1 && ensure_translated_locked(ep) == 0 && prog_writes_maps(*ep->xlated);
 	std::vector<host_log> logs(merge ? ndev : 0);
 	auto run_shard = [&](int d, const struct ebpf_pkt_batch *b, uint64_t *hist) -> int {
 		if (!merge)
@@ -1883,7 +2022,9 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 		for (int d = 0; d < ndev; d++)
 			if ((err = run_shard(d, &shards[d], nullptr)))
 				return err;
-		return merge ? upd_apply_host(ep, logs, true) : 0;
+		if (!merge)
+			return 0;
+		return (err = delta_merge_host(ep, ndev, devices)) ? err : upd_apply_host(ep, logs, true);
 	}
 	// The histogram: every shard's launch SETS its row of the scratch of its device's leading
 	// stream (the first shard on that device); the rows of one device are summed into row 0,
@@ -1968,5 +2109,7 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 				return hip_fail(e, "hipStreamWaitEvent");
 		}
 	}
-	return merge ? upd_apply_host(ep, logs, true) : 0;
+	if (!merge)
+		return 0;
+	return (err = delta_merge_host(ep, ndev, devices)) ? err : upd_apply_host(ep, logs, true);
 }

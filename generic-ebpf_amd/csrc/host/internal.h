@@ -24,6 +24,7 @@
 #include "ebpf_gpu.h"
 #include "ebpf_vm_isa.h"
 #include "../dprog.h"
+#include "map_writes.h"
 
 #define EBPF_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -162,11 +163,16 @@ struct dprog_device {
 	int ps_err = 0;                          // ENOENT: no cut points (plain launches)
 	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
+	std::vector<struct upd_map> upd_host;    // ... and its host copy
 	uint64_t win_words = 0;                  // winner words the apply step needs
 	uint32_t upd_stride = 0;                 // log record bytes
 	int last_exec = -1;                      // ebpf_dexec_info.exec of the last launch
 	int last_layout = -1;                    // its mode
 };
+
+// Whether a batch of the program writes maps (a log, or counter updates into delta areas).
+struct dprog_host;
+bool prog_writes_maps(const dprog_host &xl);
 
 // Abstract value of a register (pointer provenance), computed by translate.cpp's dataflow pass
 // over the state tree.  Used to specialise device handlers: packet loads at known offsets come
@@ -202,10 +208,20 @@ struct dprog_host {
 	bool asm_span = false;               // length-bucketed launches pay (asm_program_span)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
-	uint32_t max_updates = 0;            // most map_update_elem calls on one path (0: none)
+	// Map writes of a device batch (ebpf_gpu.h): the write log holds max_updates records per
+	// packet — the most update / delete calls and logged stores into map values on one path
+	// (0: no log).  Every written map is in exactly one of:
+	std::vector<uint16_t> upd_maps;      // arrays whose records land on the device (byte winners)
+	std::vector<uint16_t> hupd_maps;     // maps whose records replay on the host in order
+	                                     // (hashtables; arrays mixing counter updates and stores)
+	std::vector<uint16_t> atomic_maps;   // arrays changed only by aligned counter updates of one
+	                                     // width: device atomics into the delta area (DP_MAP_ATOMIC)
+	std::vector<uint8_t> atomic_width;   // ... their counter bytes (4 or 8), in that order
+	uint32_t max_updates = 0;
 	bool has_loops = false;              // standard semantics: backward jumps (LOOPCNT entries)
-	std::vector<uint16_t> upd_maps;      // table indices of the array maps those calls write
-	std::vector<uint16_t> hupd_maps;     // ... and of the hashtables update / delete calls write
+	uint32_t vstore_sites = 0;           // stores into map values / counter updates / XADD (reached)
+	bool vstore_overlay = false;         // a load may read what the packet stored into a map value
+	uint32_t ovl_entries = 0;            // ... overlay words per lane (2 per store on a path)
 	int error = 0;
 	std::string error_msg;
 };

@@ -209,6 +209,7 @@ struct Translator {
 				return false;
 			e.kind = EBPF_OP_ADD64_IMM;
 			e.imm = 0;
+			e.aux = 1; // (not an ADD of the program's: no counter update, fuse_counters)
 			return true;
 		case EBPF_OP_DIV_IMM: // 32-bit: dst = 0
 			if (zx != 0)
@@ -253,7 +254,10 @@ struct Translator {
 			x.aux = (uint16_t)c;
 		};
 		const bool jmp32 = std_mode && (op & 7) == DP_CLS_JMP32;
-		if (jmp32 ? !valid_jmp32(op) : !valid_op(op)) {
+		// XADD (standard semantics only: the reference has no case for it, ebpf_interpreter.c:
+		// 367-369): imm BPF_ADD (0) or BPF_ADD | BPF_FETCH (1)
+		const bool xadd = std_mode && (op == 0xc3 || op == 0xdb);
+		if (jmp32 ? !valid_jmp32(op) : !(valid_op(op) || xadd) || (xadd && in.imm != 0 && in.imm != 1)) {
 			make_fault(EBPF_FAULT_BAD_OPCODE);
 			return;
 		}
@@ -324,6 +328,11 @@ struct Translator {
 		case EBPF_CLS_STX:
 			if (in.dst != EBPF_R10)
 				out.writes_memory = true;
+			if (xadd) {
+				e.kind = DK_XADD;
+				e.aux = (uint16_t)((op == 0xdb ? 8 : 4) | (in.imm == 1 ? 0x100 : 0));
+				out.writes_memory = true;
+			}
 			break;
 		case EBPF_CLS_LDX:
 			break;
@@ -427,6 +436,7 @@ struct Translator {
 				x.imm = 0;
 				x.src = 0;
 				x.off = 0;
+				x.aux = 1; // (not an ADD of the program's: no counter update, fuse_counters)
 			}
 		}
 		if (!overflow && out.has_loops) { // every lane's loop count starts at 0
@@ -501,10 +511,17 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		r[0] = av();
 		return;
 	}
-	if (k == DK_LOOPINIT || k == DK_LOOPCNT)
+	if (k == DK_LOOPINIT || k == DK_LOOPCNT || k == DK_OVLINIT)
 		return;
 	if (k == DK_CALL_HDELETE) {
 		r[0] = av();
+		return;
+	}
+	if (k == DK_CNT_STORE)
+		return;
+	if (k == DK_XADD) {
+		if (e.aux & 0x100) // BPF_FETCH: src = the old value
+			r[e.src] = av();
 		return;
 	}
 	const uint8_t cls = k & 7;
@@ -610,7 +627,274 @@ dataflow(dprog_host &out)
 	}
 }
 
+// Successors of an entry in the state graph (UINT32_MAX: none).
+uint32_t
+succ_of(const dprog_host &out, uint32_t id, int k)
+{
+	const dp_entry &e = out.entries[id];
+	if (e.kind == DK_FAULT || e.kind == EBPF_OP_EXIT)
+		return UINT32_MAX;
+	if (k == 0)
+		return e.next;
+	if (e.kind < 0x100 && ((e.kind & 7) == EBPF_CLS_JMP || (e.kind & 7) == DP_CLS_JMP32))
+		return e.target;
+	return UINT32_MAX;
+}
+
+// Counter updates (ebpf_gpu.h "Stores into map values"): three consecutive entries
+//   LDX{W,DW} X = [P + off] (X != P);  ADD / SUB to X of an immediate or of a register other than
+//   X (64-bit; 32-bit too for W; the reference's MOV64, which adds); STX [P + off] = X, same width
+// make the STX a DK_CNT_STORE.  The pattern is on executed instructions, JA aside (the graph has
+// JA folded): where the ALU or the STX entry has other predecessors (standard semantics), the
+// pattern's path gets copies of its own.  Returns whether entries were added.
+bool
+fuse_counters(dprog_host &out, bool std_mode)
+{
+	const size_t n0 = out.entries.size();
+	std::vector<uint32_t> preds(n0, 0);
+	for (uint32_t i = 0; i < n0; i++) {
+		if (!out.annot[i].reached)
+			continue;
+		for (int k = 0; k < 2; k++) {
+			const uint32_t s = succ_of(out, i, k);
+			if (s < n0)
+				preds[s]++;
+		}
+	}
+	bool grew = false;
+	for (uint32_t i = 0; i < n0; i++) {
+		const dp_entry e1 = out.entries[i];
+		if (!out.annot[i].reached || !(e1.kind == EBPF_OP_LDXW || e1.kind == EBPF_OP_LDXDW) ||
+		    e1.dst == e1.src)
+			continue;
+		const uint32_t w = e1.kind == EBPF_OP_LDXDW ? 8 : 4;
+		const uint32_t j = e1.next;
+		if (j >= n0)
+			continue;
+		const dp_entry e2 = out.entries[j];
+		bool ok = false;
+		if (e2.dst == e1.dst && e2.aux == 0)
+			switch (e2.kind) {
+			case EBPF_OP_ADD64_IMM: case EBPF_OP_SUB64_IMM: ok = true; break;
+			case EBPF_OP_ADD64_REG: case EBPF_OP_SUB64_REG: ok = e2.src != e1.dst; break;
+			case EBPF_OP_MOV64_IMM: ok = !std_mode; break; // (standard MOV64s are rewritten)
+			case EBPF_OP_MOV64_REG: ok = !std_mode && e2.src != e1.dst; break;
+			case EBPF_OP_ADD_IMM: case EBPF_OP_SUB_IMM: ok = w == 4; break;
+			case EBPF_OP_ADD_REG: case EBPF_OP_SUB_REG: ok = w == 4 && e2.src != e1.dst; break;
+			default: break;
+			}
+		if (!ok || e2.next >= n0)
+			continue;
+		const uint32_t k3 = e2.next;
+		const dp_entry e3 = out.entries[k3];
+		if (e3.kind != (w == 8 ? EBPF_OP_STXDW : EBPF_OP_STXW) || e3.dst != e1.src ||
+		    e3.src != e1.dst || e3.off != e1.off)
+			continue;
+		dp_entry st = e3;
+		st.kind = DK_CNT_STORE;
+		st.aux = (uint16_t)w;
+		if (preds[j] == 1 && preds[k3] == 1) {
+			out.entries[k3] = st;
+			continue;
+		}
+		// (a merge point under standard semantics: the pattern's own copies)
+		dp_entry alu = e2;
+		out.entries.push_back(st);
+		alu.next = (uint32_t)(out.entries.size() - 1);
+		out.entries.push_back(alu);
+		out.entries[i].next = (uint32_t)(out.entries.size() - 1);
+		grew = true;
+	}
+	return grew;
+}
+
+// Stores into map values (ebpf_gpu.h "Stores into map values"): which maps they may reach and
+// how each written map's writes land (dprog_host upd_maps / hupd_maps / atomic_maps), whether
+// the packet may read its own stores back (the overlay), and the write log's records per path.
+int
+analyze_writes(dprog_host &out)
+{
+	const size_t n = out.entries.size(), nm = out.maps.size();
+	auto is_vsite = [&](size_t i, bool *add, av *base) {
+		const dp_entry &e = out.entries[i];
+		const uint8_t cls = e.kind < 0x100 ? (e.kind & 7) : 0xff;
+		*add = e.kind == DK_CNT_STORE || e.kind == DK_XADD;
+		if (!*add && cls != EBPF_CLS_ST && cls != EBPF_CLS_STX)
+			return false;
+		*base = out.annot[i].in[e.dst];
+		// (the stack and the packet are never a map's values)
+		return base->kind != AV_STACK && base->kind != AV_CTX;
+	};
+	auto size_of = [](const dp_entry &e) -> uint32_t {
+		if (e.kind == DK_CNT_STORE || e.kind == DK_XADD)
+			return e.aux & 0xff;
+		const uint32_t z = e.kind & 0x18;
+		return z == 0x00 ? 4 : z == 0x08 ? 2 : z == 0x10 ? 1 : 8;
+	};
+	// per map: stores, counter updates, counter widths, and whether every counter update is
+	// through that map's lookup result at an offset aligned for every key
+	std::vector<uint32_t> nset(nm, 0), nadd(nm, 0), widths(nm, 0);
+	std::vector<char> exact(nm, 1);
+	out.vstore_sites = 0;
+	for (size_t i = 0; i < n; i++) {
+		bool add;
+		av b;
+		if (!out.annot[i].reached || !is_vsite(i, &add, &b))
+			continue;
+		out.vstore_sites++;
+		const dp_entry &e = out.entries[i];
+		const uint32_t w = size_of(e);
+		const bool one = (b.kind == AV_MAPVAL || b.kind == AV_MAPVAL_NULL) && b.map >= 0 &&
+				 (size_t)b.map < nm;
+		for (size_t m = 0; m < nm; m++) {
+			if (one && (size_t)b.map != m)
+				continue;
+			if (!add) {
+				nset[m]++;
+				continue;
+			}
+			nadd[m]++;
+			widths[m] |= w;
+			const int64_t o = b.off + e.off;
+			if (!one || out.maps[m]->value_size % w || ((o % w) + w) % w)
+				exact[m] = 0;
+		}
+	}
+	if (out.vstore_sites && out.has_loops) {
+		out.error = EOPNOTSUPP;
+		out.error_msg = "device batches run stores into map values only in loop-free programs "
+				"(run this one with ebpf_prog_run)";
+		return EOPNOTSUPP;
+	}
+	for (size_t m = 0; m < nm; m++) {
+		const uint16_t t = (uint16_t)m;
+		const bool helper = std::find(out.upd_maps.begin(), out.upd_maps.end(), t) != out.upd_maps.end();
+		const bool hash = out.maps[m]->is_hashtable();
+		auto drop = [&](std::vector<uint16_t> &v) { v.erase(std::remove(v.begin(), v.end(), t), v.end()); };
+		auto put = [&](std::vector<uint16_t> &v) {
+			if (std::find(v.begin(), v.end(), t) == v.end())
+				v.push_back(t);
+		};
+		if (nset[m] == 0 && nadd[m] == 0)
+			continue;
+		if (hash) {
+			put(out.hupd_maps);
+		} else if (nadd[m] == 0) {
+			put(out.upd_maps); // stores (and update calls): byte winners on the device
+		} else if (nset[m] == 0 && !helper && exact[m] && (widths[m] == 4 || widths[m] == 8)) {
+			put(out.atomic_maps);
+			out.atomic_width.push_back((uint8_t)widths[m]);
+		} else {
+			drop(out.upd_maps);
+			put(out.hupd_maps);
+		}
+	}
+	// sites that log: every store, and counter updates unless all their maps are atomic
+	auto logs = [&](size_t i) {
+		const dp_entry &e = out.entries[i];
+		if (e.kind == DK_CALL_UPDATE || e.kind == DK_CALL_HDELETE)
+			return true;
+		bool add;
+		av b;
+		if (!out.annot[i].reached || !is_vsite(i, &add, &b))
+			return false;
+		if (!add)
+			return true;
+		for (size_t m = 0; m < nm; m++) {
+			if ((b.kind == AV_MAPVAL || b.kind == AV_MAPVAL_NULL) && b.map >= 0 && (size_t)b.map != m)
+				continue;
+			if (std::find(out.atomic_maps.begin(), out.atomic_maps.end(), (uint16_t)m) ==
+			    out.atomic_maps.end())
+				return true;
+		}
+		return false;
+	};
+	// may a load read a value the packet stored before it?  (a forward pass: `stored` after an
+	// entry when any path to it passed a store into a map value)
+	std::vector<char> stored(n, 0), seen(n, 0);
+	{
+		std::vector<uint32_t> work{out.start};
+		seen[out.start] = 1;
+		while (!work.empty()) {
+			const uint32_t id = work.back();
+			work.pop_back();
+			bool add;
+			av b;
+			const char after = stored[id] || (out.annot[id].reached && is_vsite(id, &add, &b));
+			for (int k = 0; k < 2; k++) {
+				const uint32_t s = succ_of(out, id, k);
+				if (s >= n)
+					continue;
+				if (!seen[s] || (after && !stored[s])) {
+					seen[s] = 1;
+					stored[s] = stored[s] || after;
+					work.push_back(s);
+				}
+			}
+		}
+	}
+	out.vstore_overlay = false;
+	for (size_t i = 0; i < n && !out.vstore_overlay; i++) {
+		const dp_entry &e = out.entries[i];
+		if (!out.annot[i].reached || !stored[i])
+			continue;
+		if (e.kind == DK_CNT_STORE || e.kind == DK_XADD) {
+			out.vstore_overlay = true; // (they read the value back first)
+		} else if (e.kind < 0x100 && (e.kind & 7) == EBPF_CLS_LDX) {
+			const av &b = out.annot[i].in[e.src];
+			out.vstore_overlay = b.kind != AV_STACK && b.kind != AV_CTX;
+		}
+	}
+	// per path: records the log needs, stores the overlay holds
+	std::vector<uint32_t> best(n, 0), bests(n, 0);
+	std::vector<uint8_t> state(n, 0);
+	std::vector<uint32_t> st{out.start};
+	while (!st.empty()) {
+		const uint32_t id = st.back();
+		if (state[id] == 0) {
+			state[id] = 1;
+			for (int k = 0; k < 2; k++) {
+				const uint32_t sx = succ_of(out, id, k);
+				if (sx < n && state[sx] == 0)
+					st.push_back(sx);
+			}
+			continue;
+		}
+		st.pop_back();
+		if (state[id] == 2)
+			continue;
+		uint32_t m = 0, ms = 0;
+		for (int k = 0; k < 2; k++) {
+			const uint32_t sx = succ_of(out, id, k);
+			if (sx < n) {
+				m = std::max(m, best[sx]);
+				ms = std::max(ms, bests[sx]);
+			}
+		}
+		bool add;
+		av b;
+		best[id] = m + (logs(id) ? 1u : 0u);
+		bests[id] = ms + (out.annot[id].reached && is_vsite(id, &add, &b) ? 1u : 0u);
+		state[id] = 2;
+	}
+	out.max_updates = best[out.start];
+	out.ovl_entries = out.vstore_overlay ? 2 * bests[out.start] : 0;
+	if (out.ovl_entries > DP_OVL_MAX) {
+		out.error = EOPNOTSUPP;
+		out.error_msg = "the program stores into map values and reads them back more often on one "
+				"path than the device overlay holds (run it with ebpf_prog_run)";
+		return EOPNOTSUPP;
+	}
+	return 0;
+}
+
 } // namespace
+
+bool
+prog_writes_maps(const dprog_host &xl)
+{
+	return xl.max_updates != 0 || !xl.atomic_maps.empty();
+}
 
 int
 translate_program(struct ebpf_prog *ep, dprog_host &out)
@@ -839,48 +1123,28 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 				out.maps.clear();
 				return EOPNOTSUPP;
 			}
-	// most update calls on one path from the start (the graph is a tree under the reference's
-	// stepping, a DAG under loop-free standard semantics): the per-packet bound of the write log
-	{
-		const size_t n = out.entries.size();
-		std::vector<uint32_t> best(n, 0);
-		std::vector<uint8_t> state(n, 0); // 0 new, 1 open, 2 done
-		std::vector<uint32_t> st{out.start};
-		auto succ_of = [&](uint32_t id, int k) -> uint32_t {
-			const dp_entry &e = out.entries[id];
-			if (e.kind == DK_FAULT || e.kind == EBPF_OP_EXIT)
-				return UINT32_MAX;
-			if (k == 0)
-				return e.next;
-			if (e.kind < 0x100 && ((e.kind & 7) == EBPF_CLS_JMP || (e.kind & 7) == DP_CLS_JMP32))
-				return e.target;
-			return UINT32_MAX;
-		};
-		while (!st.empty()) {
-			const uint32_t id = st.back();
-			if (state[id] == 0) {
-				state[id] = 1;
-				for (int k = 0; k < 2; k++) {
-					const uint32_t sx = succ_of(id, k);
-					if (sx < n && state[sx] == 0)
-						st.push_back(sx);
-				}
-				continue;
-			}
-			st.pop_back();
-			if (state[id] == 2)
-				continue;
-			uint32_t m = 0;
-			for (int k = 0; k < 2; k++) {
-				const uint32_t sx = succ_of(id, k);
-				if (sx < n)
-					m = std::max(m, best[sx]);
-			}
-			best[id] = m + (out.entries[id].kind == DK_CALL_UPDATE ||
-					out.entries[id].kind == DK_CALL_HDELETE ? 1u : 0u);
-			state[id] = 2;
+	// counter updates, then how the program's map writes land and the log's records per path
+	if (fuse_counters(out, std_sem)) {
+		if (out.entries.size() >= kMaxEntries) {
+			out.error = E2BIG;
+			out.error_msg = "program state graph exceeds the device translation limit";
+			out.maps.clear();
+			return E2BIG;
 		}
-		out.max_updates = best[out.start];
+		dataflow(out);
+	}
+	if (analyze_writes(out) != 0) {
+		out.maps.clear();
+		return out.error;
+	}
+	if (out.vstore_overlay) { // every lane's overlay starts empty
+		dp_entry x;
+		memset(&x, 0, sizeof(x));
+		x.kind = DK_OVLINIT;
+		x.next = out.start;
+		out.entries.push_back(x);
+		out.start = (uint32_t)(out.entries.size() - 1);
+		dataflow(out);
 	}
 	// The program now pins its maps (released in prog_dtor): a device mirror must not outlive
 	// its map while a later batch may still read it.

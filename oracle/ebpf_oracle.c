@@ -30,12 +30,15 @@ struct region_env {
 	uint64_t stk_lo, stk_hi;
 	const struct oracle_prog *p;
 	uint8_t *sdef; /* track_undef: 1 per stack byte a store wrote (NULL: not tracked) */
+	int map_hit;   /* check_access: the map whose values hold the access, else -1 */
 };
 
-/* 0 = ok, else a fault code. write=1 for stores. */
+/* 0 = ok, else a fault code. write=1 for stores (into map values too: ebpf_interpreter.c:343-366
+ * writes through whatever pointer the program holds; re->map_hit tells the caller). */
 static inline int
-check_access(const struct region_env *re, uint64_t addr, uint64_t size, int write)
+check_access(struct region_env *re, uint64_t addr, uint64_t size, int write)
 {
+	re->map_hit = -1;
 	uint64_t end = addr + size;
 	if (end < addr)
 		return F_MEM;
@@ -60,7 +63,8 @@ check_access(const struct region_env *re, uint64_t addr, uint64_t size, int writ
 		 * an access that leaves it reads stray memory, which stops the packet like any other */
 		if (mp->kind == ORACLE_MAP_HASH && (addr - lo) / mp->value_size != (end - 1 - lo) / mp->value_size)
 			continue;
-		return write ? F_MAP_WRITE : 0;
+		re->map_hit = (int)m;
+		return 0;
 	}
 	return F_MEM;
 }
@@ -199,7 +203,7 @@ oracle_hash_build(struct oracle_map *m)
 /* ebpf_map_lookup_elem (ebpf_map.c:77-84) → array_map_lookup_elem (ebpf_map_array.c:115-124)
  * or hashtable_map_lookup_elem (ebpf_map_hashtable.c:285-301) */
 static inline uint64_t
-helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
+helper_map_lookup(struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
 {
 	const struct oracle_prog *p = re->p;
 	if (r1 == 0 || r2 == 0) /* em == NULL || key == NULL → NULL (ebpf_map.c:80-81) */
@@ -252,12 +256,18 @@ helper_map_lookup(const struct region_env *re, int checked, uint64_t r1, uint64_
 }
 
 /* ---- map-writing helpers, device-batch semantics (ebpf_oracle.h) ---- */
+enum { WR_HELPER = 0, WR_STORE = 1, WR_ADD = 2 };
 struct wrec {
 	uint64_t pkt;
 	uint32_t seq;
 	uint32_t map;
-	uint32_t key;  /* array: the key; hashtable: op (1 update, 2 delete) | flags << 8 */
+	uint32_t key;  /* array: the key; hashtable: op (1 update, 2 delete) | flags << 8;
+			* WR_STORE / WR_ADD into a hashtable: the element's index */
 	uint64_t voff; /* value bytes in the log's arena (hashtable: key_size bytes, then the value) */
+	uint8_t kind;  /* WR_HELPER: update / delete; WR_STORE / WR_ADD: a store into a value */
+	uint8_t size;  /* WR_STORE / WR_ADD: bytes */
+	uint32_t off;  /* ... byte offset in the map's values (hashtable: in the element's value) */
+	uint64_t data; /* ... the stored bytes (WR_ADD: the addend), little-endian */
 };
 struct wlog {
 	struct wrec *rec;
@@ -268,6 +278,7 @@ struct wlog {
 static __thread struct wlog *t_wlog; /* set by oracle_run_batch per thread */
 static __thread uint64_t t_pkt;
 static __thread uint32_t t_seq;
+static __thread int t_sequential; /* oracle_prog.sequential: writes land at once */
 
 static void
 wlog_push2(uint32_t map, uint32_t key, const uint8_t *a, uint32_t na, const uint8_t *b, uint32_t nb)
@@ -286,8 +297,166 @@ wlog_push2(uint32_t map, uint32_t key, const uint8_t *a, uint32_t na, const uint
 	memcpy(w->arena + w->used, a, na);
 	if (nb)
 		memcpy(w->arena + w->used + na, b, nb);
-	w->rec[w->n++] = (struct wrec){t_pkt, t_seq++, map, key, w->used};
+	w->rec[w->n++] = (struct wrec){t_pkt, t_seq++, map, key, w->used, WR_HELPER, 0, 0, 0};
 	w->used += na + nb;
+}
+
+/* ---- stores into map values, batch semantics (ebpf_oracle.h) ----
+ * The packet's own stores: one entry per byte it stored into a map value (addresses in the
+ * oracle's map storage), newest last.  Its loads read them back; the maps stay the batch-start
+ * bytes until the batch's records are applied. */
+#define OVL_MAX 8192
+struct ovl {
+	uint32_t n;
+	uint64_t addr[OVL_MAX];
+	uint8_t byte[OVL_MAX];
+};
+static __thread struct ovl *t_ovl; /* batch mode (not sequential): the packet's overlay */
+
+static int
+ovl_find(uint64_t a)
+{
+	for (uint32_t i = t_ovl->n; i-- > 0;)
+		if (t_ovl->addr[i] == a)
+			return (int)i;
+	return -1;
+}
+
+/* 0, or F_MEM when the packet stored more bytes than the overlay holds (never in the tests;
+ * the device bounds its overlay by the program's stores per path) */
+static int
+ovl_put(uint64_t a, uint8_t b)
+{
+	int k = ovl_find(a);
+	if (k < 0) {
+		if (t_ovl->n == OVL_MAX)
+			return F_MEM;
+		k = (int)t_ovl->n++;
+		t_ovl->addr[k] = a;
+	}
+	t_ovl->byte[k] = b;
+	return 0;
+}
+
+/* A load of map-value bytes: the packet's own stores over the batch-start bytes. */
+static inline uint64_t
+load_mem(uint64_t addr, int size)
+{
+	if (t_ovl == NULL || t_ovl->n == 0)
+		return load_n(addr, size);
+	uint64_t v = 0;
+	for (int i = 0; i < size; i++) {
+		const int k = ovl_find(addr + (uint64_t)i);
+		const uint8_t b = k >= 0 ? t_ovl->byte[k] : *(const uint8_t *)(uintptr_t)(addr + (uint64_t)i);
+		v |= (uint64_t)b << (8 * i);
+	}
+	return v;
+}
+
+/* A store of `size` bytes of v at addr inside the values of map mi (check_access): in place when
+ * the run is sequential (or a lone oracle_run), else into the packet's overlay and the batch's
+ * log.  `add`: a counter update adding `delta` (the caller checked the alignment).  Returns 0 or
+ * a fault code. */
+static int
+value_store(const struct region_env *re, int mi, uint64_t addr, int size, uint64_t v, int add,
+	    uint64_t delta)
+{
+	const struct oracle_map *m = &re->p->maps[mi];
+	struct wlog *w = t_wlog;
+	if (t_sequential || w == NULL || t_ovl == NULL) {
+		store_n(addr, size, v);
+		return 0;
+	}
+	for (int i = 0; i < size; i++) {
+		int f = ovl_put(addr + (uint64_t)i, (uint8_t)(v >> (8 * i)));
+		if (f)
+			return f;
+	}
+	uint64_t off = addr - (uint64_t)(uintptr_t)m->data;
+	uint32_t elem = 0;
+	if (m->kind == ORACLE_MAP_HASH) {
+		elem = (uint32_t)(off / m->value_size);
+		off %= m->value_size;
+	}
+	if (w->n == w->cap) {
+		w->cap = w->cap ? 2 * w->cap : 1024;
+		w->rec = realloc(w->rec, w->cap * sizeof(*w->rec));
+	}
+	const uint64_t mask = size == 8 ? ~0ull : (1ull << (8 * size)) - 1;
+	w->rec[w->n++] = (struct wrec){t_pkt, t_seq++, (uint32_t)mi, elem, 0, add ? WR_ADD : WR_STORE,
+				       (uint8_t)size, (uint32_t)off, (add ? delta : v) & mask};
+	return 0;
+}
+
+/* Is a counter update at addr (map mi) aligned to its width within the map's values? */
+static inline int
+value_aligned(const struct region_env *re, int mi, uint64_t addr, int size)
+{
+	const struct oracle_map *m = &re->p->maps[mi];
+	uint64_t off = addr - (uint64_t)(uintptr_t)m->data;
+	if (m->kind == ORACLE_MAP_HASH)
+		off %= m->value_size;
+	return off % (uint64_t)size == 0;
+}
+
+/* Counter-update tracking (ebpf_oracle.h): LDX{W,DW} X = [P + off]; ADD/SUB X; STX [P + off] = X,
+ * consecutive (JA aside).  cnt_next() is called with every executed instruction before it runs;
+ * it returns 1 when this instruction is the pattern's store. */
+struct cnt_track {
+	int stage; /* 0 none, 1 after the load, 2 after the add */
+	uint8_t x, p;
+	int16_t off;
+	int size;
+	uint64_t loaded;
+};
+
+static inline int
+cnt_next(struct cnt_track *ct, uint8_t op, uint8_t d, uint8_t s, int16_t off, int std)
+{
+	if (op == 0x05)
+		return 0; /* JA: not a step (the device folds it into the state graph) */
+	if (ct->stage == 1 && d == ct->x) {
+		int ok = 0;
+		switch (op) {
+		case 0x07: case 0x17: ok = 1; break;                    /* ADD64 / SUB64 imm */
+		case 0x0f: case 0x1f: ok = s != ct->x; break;           /* ... reg */
+		case 0xb7: ok = !std; break;                            /* reference MOV64 = add */
+		case 0xbf: ok = !std && s != ct->x; break;
+		case 0x04: case 0x14: ok = ct->size == 4; break;        /* ALU32 ADD / SUB imm */
+		case 0x0c: case 0x1c: ok = ct->size == 4 && s != ct->x; break;
+		}
+		ct->stage = ok ? 2 : 0;
+		return 0;
+	}
+	if (ct->stage == 2) {
+		ct->stage = 0;
+		const uint8_t stx = ct->size == 8 ? 0x7b : 0x63;
+		return op == stx && d == ct->p && s == ct->x && off == ct->off;
+	}
+	ct->stage = 0;
+	return 0;
+}
+
+/* after an LDX of `size` bytes into d from [s + off] that loaded v */
+static inline void
+cnt_load(struct cnt_track *ct, uint8_t d, uint8_t s, int16_t off, int size, uint64_t v)
+{
+	if ((size == 4 || size == 8) && d != s)
+		*ct = (struct cnt_track){1, d, s, off, size, v};
+}
+
+/* STX / ST / XADD of `size` bytes of v at a (already region-checked, re->map_hit set) */
+static inline int
+mem_store(const struct region_env *re, int checked, uint64_t a, int size, uint64_t v, int add,
+	  uint64_t delta)
+{
+	if (checked && re->map_hit >= 0) {
+		if (add && !value_aligned(re, re->map_hit, a, size))
+			add = 0;
+		return value_store(re, re->map_hit, a, size, v, add, delta);
+	}
+	store_n(a, size, v);
+	return 0;
 }
 
 static void
@@ -309,7 +478,7 @@ find_map(const struct oracle_prog *p, uint64_t handle, uint32_t *idx)
 
 /* ebpf_map_update_elem (ebpf_map.c:101-108) -> array_map_update_elem (ebpf_map_array.c:185-211) */
 static inline uint64_t
-helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, uint64_t r3,
+helper_map_update(struct region_env *re, int checked, uint64_t r1, uint64_t r2, uint64_t r3,
 		  uint64_t r4, int *fault)
 {
 	if (r1 == 0 || r2 == 0 || r3 == 0 || r4 > 2) /* EBPF_EXIST = 2 */
@@ -347,13 +516,17 @@ helper_map_update(const struct region_env *re, int checked, uint64_t r1, uint64_
 		return 22;
 	if (checked && (*fault = check_access(re, r3, m->value_size, 0)))
 		return 0;
+	if (t_sequential) { /* the reference: memcpy into the value now (ebpf_map_array.c:173-183) */
+		memmove(m->data + (uint64_t)m->value_size * k, (const void *)(uintptr_t)r3, m->value_size);
+		return 0;
+	}
 	wlog_push(mi, k, (const uint8_t *)(uintptr_t)r3, m->value_size);
 	return 0;
 }
 
 /* ebpf_map_delete_elem (ebpf_map.c) -> array_map_delete_elem (ebpf_map_array.c:246-250) */
 static inline uint64_t
-helper_map_delete(const struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
+helper_map_delete(struct region_env *re, int checked, uint64_t r1, uint64_t r2, int *fault)
 {
 	uint32_t mi;
 	if (r1 == 0 || r2 == 0) /* ebpf_map.c:130-136: checked before the map is touched */
@@ -376,7 +549,7 @@ helper_map_delete(const struct region_env *re, int checked, uint64_t r1, uint64_
 
 /* CALL :282-284 — helper id imm of the configured table */
 static inline uint64_t
-helper_call(const struct region_env *re, int checked, int32_t imm, const uint64_t *reg, int *fault)
+helper_call(struct region_env *re, int checked, int32_t imm, const uint64_t *reg, int *fault)
 {
 	const struct oracle_prog *p = re->p;
 	if (imm < 0 || imm >= 64 || p->helper_kind[imm] == ORACLE_HELPER_UNSET) {
@@ -512,6 +685,8 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	uint8_t taint[11] = {0};
 	taint[1] = taint[10] = 1;
 	re.p = p;
+	re.map_hit = -1;
+	struct cnt_track ct = {0, 0, 0, 0, 0, 0};
 
 	for (;;) {
 		/* :39  inst = inst + pc++;  (cumulative stepping) */
@@ -547,6 +722,7 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 
 		if (re.sdef && (fault = taint_pre(&re, taint, op, d, s, off, imm, reg, 0)))
 			break;
+		const int cnt = cnt_next(&ct, op, d, s, off, 0);
 		switch (op) {
 		/* ---- ALU32 :41-133 — operands truncated to u32, result zero-extended ---- */
 		case 0x0c: reg[d] = (uint32_t)(D32 + S32); break;
@@ -649,7 +825,8 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = S + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 0)))
 				break;
-			reg[d] = load_n(a, msize);
+			reg[d] = checked && re.map_hit >= 0 ? load_mem(a, msize) : load_n(a, msize);
+			cnt_load(&ct, d, s, off, msize, reg[d]);
 			break;
 		}
 		case 0x18:                                                  /* :339-342 LDDW */
@@ -669,7 +846,7 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = D + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 1)))
 				break;
-			store_n(a, msize, S);
+			fault = mem_store(&re, checked, a, msize, S, cnt, S - ct.loaded);
 			break;
 		}
 		case 0x72: msize = 1; goto st;
@@ -680,7 +857,7 @@ run_ref(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = D + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 1)))
 				break;
-			store_n(a, msize, IS);
+			fault = mem_store(&re, checked, a, msize, IS, 0, 0);
 			break;
 		}
 		default:                                                    /* :367-369 */
@@ -752,6 +929,8 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 	uint8_t taint[11] = {0};
 	taint[1] = taint[10] = 1;
 	re.p = p;
+	re.map_hit = -1;
+	struct cnt_track ct = {0, 0, 0, 0, 0, 0};
 
 	for (;;) {
 		if (pc >= p->nslots) {
@@ -768,8 +947,9 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		memcpy(&imm, ip + 4, 4);
 		pc++;
 		const int jmp32 = (op & 7) == 6;
-		if (!(valid_op(op) || (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 &&
-				       op != 0x86 && op != 0x96))) {
+		if (!(valid_op(op) || op == 0xc3 || op == 0xdb ||
+		      (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 && op != 0x86 &&
+		       op != 0x96))) {
 			fault = F_BAD_OPCODE;
 			break;
 		}
@@ -790,6 +970,7 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 		if (re.sdef && (fault = taint_pre(&re, taint, jmp32 ? (uint8_t)((op & 0xf8) | 5) : op, d, s,
 						   off, imm, reg, 1)))
 			break;
+		const int cnt = cnt_next(&ct, op, d, s, off, 1);
 		if (jmp32) {
 			const uint32_t B = (op & 0x08) ? S32 : I32;
 			switch (op & 0xf0) {
@@ -905,7 +1086,8 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = S + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 0)))
 				break;
-			reg[d] = load_n(a, msize);
+			reg[d] = checked && re.map_hit >= 0 ? load_mem(a, msize) : load_n(a, msize);
+			cnt_load(&ct, d, s, off, msize, reg[d]);
 			break;
 		}
 		case 0x18:
@@ -925,7 +1107,7 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = D + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 1)))
 				break;
-			store_n(a, msize, S);
+			fault = mem_store(&re, checked, a, msize, S, cnt, S - ct.loaded);
 			break;
 		}
 		case 0x72: msize = 1; goto st;
@@ -936,7 +1118,26 @@ run_std(const struct oracle_prog *p, int checked, uint8_t *pkt, uint64_t len, ui
 			uint64_t a = D + (uint64_t)(int64_t)off;
 			if (checked && (fault = check_access(&re, a, msize, 1)))
 				break;
-			store_n(a, msize, IS);
+			fault = mem_store(&re, checked, a, msize, IS, 0, 0);
+			break;
+		}
+		/* XADD (standard eBPF, BPF_STX | BPF_XADD): *(u32 / u64 *)(dst + off) += src; imm 1
+		 * (BPF_ADD | BPF_FETCH) also sets src to the old value.  In a batch: a counter update
+		 * (ebpf_oracle.h). */
+		case 0xc3: msize = 4; goto xadd;
+		case 0xdb: msize = 8;
+		xadd: {
+			if (imm != 0 && imm != 1) {
+				fault = F_BAD_OPCODE;
+				break;
+			}
+			uint64_t a = D + (uint64_t)(int64_t)off;
+			if (checked && (fault = check_access(&re, a, msize, 1)))
+				break;
+			const uint64_t old = checked && re.map_hit >= 0 ? load_mem(a, msize) : load_n(a, msize);
+			fault = mem_store(&re, checked, a, msize, old + S, 1, S);
+			if (!fault && imm == 1)
+				reg[s] = old;
 			break;
 		}
 		default:
@@ -1012,7 +1213,7 @@ run_raw(const struct oracle_prog *p, uint8_t *pkt, uint64_t *steps_out)
 	const struct raw_inst *ip = (const struct raw_inst *)p->insns;
 	uint32_t pc = 0;
 	uint64_t steps = 0;
-	struct region_env re = {0, 0, 0, 0, p, NULL};
+	struct region_env re = {0, 0, 0, 0, p, NULL, -1};
 	for (int i = 0; i < 11; i++)
 		reg[i] = p->reg_init;
 	reg[1] = (uint64_t)(uintptr_t)pkt;
@@ -1170,10 +1371,14 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 	uint64_t hused = 0;
 	if (nthreads <= 0)
 		nthreads = 1;
-	int writes = 0;
+	/* a checked run may store into map values: every thread keeps a log (and, batch mode, the
+	 * packet's overlay); a sequential run writes in place on one thread */
+	int writes = p->checked && p->nmaps > 0;
 	for (int i = 0; i < 64; i++)
 		writes |= p->helper_kind[i] == ORACLE_HELPER_MAP_UPDATE ||
 			  p->helper_kind[i] == ORACLE_HELPER_MAP_DELETE;
+	if (p->sequential)
+		nthreads = 1;
 	struct wlog *logs = writes ? calloc((size_t)nthreads, sizeof(struct wlog)) : NULL;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(+ : total)
@@ -1185,6 +1390,8 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		const int tid = 0;
 #endif
 		t_wlog = logs ? &logs[tid] : NULL;
+		t_sequential = p->sequential;
+		t_ovl = logs && p->checked && !p->sequential ? malloc(sizeof(struct ovl)) : NULL;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
 #endif
@@ -1202,15 +1409,25 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 			uint64_t st = 0;
 			t_pkt = (uint64_t)i;
 			t_seq = 0;
+			if (t_ovl)
+				t_ovl->n = 0;
 			size_t n0 = t_wlog ? t_wlog->n : 0;
 			ret[i] = oracle_run(p, pkt, len, &f, &st);
-			if (f && t_wlog) /* a packet that faults leaves no write behind */
-				t_wlog->n = n0;
+			if (f && t_wlog) { /* a packet that faults leaves no write behind but its counter updates */
+				size_t w = n0;
+				for (size_t r = n0; r < t_wlog->n; r++)
+					if (t_wlog->rec[r].kind == WR_ADD)
+						t_wlog->rec[w++] = t_wlog->rec[r];
+				t_wlog->n = w;
+			}
 			if (faults)
 				faults[i] = f;
 			total += st;
 		}
 		t_wlog = NULL;
+		free(t_ovl);
+		t_ovl = NULL;
+		t_sequential = 0;
 	}
 	if (logs) {
 		/* after the batch: every write in packet order (last writer of a key wins) */
@@ -1228,6 +1445,30 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		qsort(all, n, sizeof(*all), wrec_cmp);
 		for (size_t j = 0; j < n; j++) {
 			const struct oracle_map *m = &p->maps[all[j].map];
+			if (all[j].kind != WR_HELPER) {
+				const int sz = all[j].size;
+				if (m->kind == ORACLE_MAP_HASH) {
+					/* {u32 map, u32 op (3 store, 4 add) | size << 8 | offset << 16, key, data} */
+					const uint64_t rs = 8 + m->key_size + m->value_size;
+					if (hlog && hused + rs <= hlog_cap) {
+						const uint32_t w = (all[j].kind == WR_ADD ? 4u : 3u) | (uint32_t)sz << 8 |
+								   all[j].off << 16;
+						memcpy(hlog + hused, &all[j].map, 4);
+						memcpy(hlog + hused + 4, &w, 4);
+						memcpy(hlog + hused + 8, m->keys + (uint64_t)m->key_size * all[j].key,
+						       m->key_size);
+						memset(hlog + hused + 8 + m->key_size, 0, m->value_size);
+						memcpy(hlog + hused + 8 + m->key_size, &all[j].data, (size_t)sz);
+					}
+					hused += rs;
+					continue;
+				}
+				uint8_t *at = m->data + all[j].off;
+				const uint64_t v = all[j].kind == WR_ADD ? load_n((uint64_t)(uintptr_t)at, sz) + all[j].data
+								       : all[j].data;
+				store_n((uint64_t)(uintptr_t)at, sz, v);
+				continue;
+			}
 			if (m->kind == ORACLE_MAP_HASH) {
 				/* for the caller's replay: {u32 map, u32 op | flags << 8, key, value} */
 				const uint64_t sz = 8 + m->key_size + m->value_size;

@@ -88,7 +88,8 @@ class _Prog(ctypes.Structure):
                 ("helper_kind", ctypes.c_uint8 * 64), ("maps", ctypes.c_void_p),
                 ("nmaps", ctypes.c_uint32), ("reg_init", ctypes.c_uint64),
                 ("stack_init", ctypes.c_uint8), ("checked", ctypes.c_uint8),
-                ("semantics", ctypes.c_uint8), ("track_undef", ctypes.c_uint8)]
+                ("semantics", ctypes.c_uint8), ("track_undef", ctypes.c_uint8),
+                ("sequential", ctypes.c_uint8)]
 
 
 _lib = None
@@ -130,7 +131,7 @@ class OracleProgram:
     [(slot, map_index)] are patched with oracle handles here."""
 
     def __init__(self, code, relocs=(), maps=(), helper_kinds=None, checked=True,
-                 reg_init=0, stack_init=0, semantics=0, track_undef=False):
+                 reg_init=0, stack_init=0, semantics=0, track_undef=False, sequential=False):
         b = bytearray(code)
         for slot, k in relocs:
             h = oracle_handle(k)
@@ -180,8 +181,9 @@ class OracleProgram:
         # does the program call a map-writing helper (a CALL whose id is one) on a hashtable?
         ins = self.code[: len(self.code) // 8 * 8].reshape(-1, 8)
         ids = ins[ins[:, 0] == 0x85, 4:8].copy().view(np.int32).reshape(-1)
-        self.hash_writes = any(isinstance(m, HashSpec) for m in maps) and any(
-            kinds.get(int(i)) in (HELPER_MAP_UPDATE, HELPER_MAP_DELETE) for i in ids)
+        # (or a store into a hashtable value: any checked program with a hashtable may make one)
+        self.hash_writes = any(isinstance(m, HashSpec) for m in maps) and (checked or any(
+            kinds.get(int(i)) in (HELPER_MAP_UPDATE, HELPER_MAP_DELETE) for i in ids))
         self.p.maps = ctypes.addressof(self.maps_arr)
         self.p.nmaps = len(maps)
         self.p.reg_init = reg_init
@@ -189,6 +191,9 @@ class OracleProgram:
         self.p.checked = 1 if checked else 0
         self.p.semantics = semantics
         self.p.track_undef = 1 if track_undef else 0
+        # the reference's own run, one packet after the other: stores into map values and array
+        # map_update_elem land at once (ebpf_oracle.h); batches run on one thread
+        self.p.sequential = 1 if sequential else 0
 
     def run(self, data, count, stride=0, offsets=None, nthreads=1):
         """Runs in place on a COPY of ``data``; returns (ret u64[count], faults u8[count],
@@ -225,10 +230,14 @@ class OracleProgram:
                 val = raw[pos + 8 + spec.key_size:pos + 8 + spec.key_size + spec.value_size]
                 pos += 8 + spec.key_size + spec.value_size
                 self.last_hlog.append((k, word & 0xff, word >> 8, key, val))
-                if word & 0xff == 1:
+                op = word & 0xff
+                if op == 1:
                     self.hash_models[k].update(key, val, word >> 8)
-                else:
+                elif op == 2:
                     self.hash_models[k].delete(key)
+                else:   # a store into the element's value (3), or a counter update (4)
+                    size, off = (word >> 8) & 0xff, word >> 16
+                    self.hash_models[k].store(key, off, val[:size], add=op == 4)
         return ret, faults, work, int(steps)
 
     def map_bytes(self, k):
@@ -342,6 +351,25 @@ class HashtableModel:
         if i >= 0:
             del bk[i]
         return 0
+
+    def store(self, key, off, data, add=False):
+        """A program's store into the value of ``key`` through a lookup result, in place (the
+        element keeps its place in its bucket); ``add``: a counter update adding ``data``
+        (little-endian, mod 2^(8 len(data))).  No element: nothing (it was deleted before)."""
+        bk, i = self._find(key)
+        if i < 0:
+            return
+        cur = bk[i][1][0] if self.percpu else bk[i][1]
+        v = bytearray(cur)
+        n = len(data)
+        if add:
+            x = (int.from_bytes(v[off:off + n], "little") + int.from_bytes(data, "little")) % (1 << (8 * n))
+            data = x.to_bytes(n, "little")
+        v[off:off + n] = data
+        if self.percpu:
+            bk[i][1][0] = bytes(v)
+        else:
+            bk[i][1] = bytes(v)
 
     def get_next_key(self, key=None):
         start = 0

@@ -39,7 +39,8 @@ def key_nodes(ks, src, key_off, stk_off, I):
 def lookup_program(ks, src="stack", key_off=0, stk_off=None, read=(8, 0), miss=0xdead,
                    store=False, second=None):
     """r0 = value bytes [read[1], read[1] + read[0]) of map 0's value for the packet's key, or
-    `miss`.  store: write r6 into the value first (a MAP_WRITE fault on the device).  second:
+    `miss`.  store: write the packet's first 8 bytes into the value first (read back by the
+    load: the packet's own store, ebpf_gpu.h "Stores into map values").  second:
     (ks2, key_off2) looks up map 1 too and XORs its first 8 value bytes in (or 0x77 on a miss)."""
     I, Branch, LdDw, MapRef, assemble = _mods()
     if stk_off is None:
@@ -50,7 +51,7 @@ def lookup_program(ks, src="stack", key_off=0, stk_off=None, read=(8, 0), miss=0
     nodes += [LdDw(R1, MapRef(0)), I("call", imm=0),
               Branch(I("jeq_imm", R0, imm=0), [I("mov_imm", R0, imm=miss), I("exit")])]
     if store:
-        nodes += [I("stxdw", R0, R6, 0)]
+        nodes += [I("ldxdw", R9, R6, 0), I("stxdw", R0, R9, 0)]
     nodes += [I(ldx, R8, R0, read[1])]
     if second is not None:
         ks2, off2 = second
