@@ -101,7 +101,8 @@ def parse(argv=None):
 
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
-                   "c4": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24, "c5lit": 1 << 22}
+                   "c4": 1 << 26, "c4c": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24,
+                   "c5lit": 1 << 22}
 # C4H: bytes one lookup must move.  The device table's slot is 32 B (u32 used | u32 hash | 4-B key
 # 8-B padded | 8-B value), but a random probe cannot fetch less than one 64-B line from HBM: the
 # PMC passes measured 64 B per lookup (FETCH_SIZE, profiles/r02/s3/all/bench_c4h_slots8.json:
@@ -129,6 +130,8 @@ class Workload:
         self.D = min(total, DISTINCT)
         if cfg == "c4":
             self.maps = [(8, 256, workloads.c4_map_values().tobytes())]
+        if cfg == "c4c":  # + the per-key packet counters, from zero
+            self.maps = [(8, 256, workloads.c4_map_values().tobytes()), (8, 256, bytes(8 * 256))]
         if cfg == "c4h":  # ("hash", key_size, value_size, max_entries, keys, values)
             universe, keys, values = workloads.c4h_table()
             self.maps = [("hash", 4, 8, len(keys), keys, values)]
@@ -238,6 +241,27 @@ def verify(w, torch, d_ret, d_hist_total, world, dev):
             "hist_mismatched_bins": hist_bad,
             "oracle_packets": int(w.n if w.offs is not None else w.D)}
     return info["verified"], info
+
+
+def verify_counters(w, maps, launches):
+    """C4C: the counters map after `launches` launches over the shard equals the oracle's count of
+    the packets that reached the counter update (ebpf_gpu.h: counter updates are additions, so
+    the map ends as the reference's sequential run leaves it), for every key."""
+    import pyoracle
+    s, (k, r) = w.lo % w.D, divmod(w.n, w.D)
+
+    def once(pk):
+        spec = [w.maps[0], (8, 256, bytes(8 * 256))]
+        op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, spec)
+        op.run(pk, len(pk), 64, nthreads=oracle_threads())
+        return np.frombuffer(op.map_bytes(1), dtype=np.uint64).astype(object)
+    per = once(w.pk) * k if k else 0
+    if r:
+        per = per + once(w.pk[(s + np.arange(r)) % w.D])
+    want = [int(x) * launches % (1 << 64) for x in per]
+    got = [int(np.frombuffer(maps[1].lookup(key)[1], dtype=np.uint64)[0]) for key in range(256)]
+    return {"counters_verified": got == want, "counted_per_launch": int(sum(int(x) for x in per)),
+            "counter_mismatches": sum(1 for a, b in zip(got, want) if a != b)}
 
 
 def cpu_model():
@@ -490,6 +514,11 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
     ok = True
     if not a.no_verify:  # the last timed launch against the oracle (outside the timing)
         ok, vinfo = verify(w, torch, d_ret, d_hist, world, dev)
+        if cfg == "c4c":
+            c = verify_counters(w, maps, a.warmup + a.steps + (1 if graphs is not None else 0))
+            vinfo.update(c)
+            ok = ok and c["counters_verified"]
+            vinfo["verified"] = ok
     elif int(hist.sum()) != total:
         ok = False
         vinfo = {"verified": False, "hist_total": int(hist.sum())}

@@ -243,6 +243,15 @@ for z in (4, 8):
 for z in (4, 8):
     fam("XADDF%d" % z, 2)
 fam("OVLINIT", 0)              # dprog.h DK_OVLINIT: the lane's overlay count = 0
+# a counter update the translator resolved completely (asm_runtime.cpp): an immediate addend
+# (s[10:11]) into a DP_MAP_ATOMIC map's delta area at r_d + s14 (d = the value pointer, a
+# non-NULL lookup result; s14 = the offset + the map's delta-area offset)
+for z in (4, 8):
+    fam("CNTAI%d" % z, 1)
+# ... into the workgroup's LDS sums of a DP_MAP_LDSDELTA map: at (r_d - s15) + s14 (s15 = the
+# mirror's address, low word; s14 = the offset + the table's LDS address)
+for z in (4, 8):
+    fam("CNTAL%d" % z, 1)
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 # the lane's stack slice below the frame (dprog.h DP_OVL_*): loop count, overlay count, the
 # scratch a store into a map value is redirected to, the overlay entries
@@ -1373,6 +1382,19 @@ def vstore_routine():
          "s_cbranch_scc0 .Lvs_rec",
          "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
          "s_cbranch_execz .Lvs_atom_done",
+         # the workgroup's LDS sums (DP_MAP_LDSDELTA: table at s71 & 0xffff)
+         "s_bitcmp1_b32 s71, 29",
+         "s_cbranch_scc0 .Lvs_atom_g",
+         "s_and_b32 %s, s71, 0xffff" % s(S_BYTES),
+         "v_add_u32 %s, %s, %s" % (v(R[8]), s(S_BYTES), v(OFF)),
+         "s_cmp_eq_u32 %s, 8" % s(S_T0),
+         "s_cbranch_scc0 .Lvs_lds4",
+         "ds_add_u64 %s, %s" % (v(R[8]), vp(L_[0])),
+         "s_branch .Lvs_atom_done",
+         ".Lvs_lds4:",
+         "ds_add_u32 %s, %s" % (v(R[8]), v(L_[0])),
+         "s_branch .Lvs_atom_done",
+         ".Lvs_atom_g:",
          "s_mul_i32 %s, s68, s69" % s(S_BYTES),
          "s_add_u32 %s, %s, 63" % (s(S_BYTES), s(S_BYTES)),
          "s_and_b32 %s, %s, -64" % (s(S_BYTES), s(S_BYTES)),      # dprog.h dp_delta_off
@@ -1386,6 +1408,7 @@ def vstore_routine():
          ".Lvs_atom4:",
          "global_atomic_add %s, %s, off" % (vp(R[8]), v(L_[0])),
          ".Lvs_atom_done:",
+         "s_waitcnt lgkmcnt(0)",
          "s_andn2_b64 exec, %s, exec" % sp(S_MASK),                # the lanes left: records
          ".Lvs_rec:",
          "s_cbranch_execz .Lvs_ret",
@@ -1691,6 +1714,22 @@ def handler_body(name, d, sr):
         return call(".Lr_update"), False
     if name == "HDELETE":
         return call(".Lr_hdelete"), False
+    if name.startswith("CNTAI"):
+        z = int(name[5:])
+        out = ["v_mov_b32 %s, s14" % v(H[2]), "v_mov_b32 %s, 0" % v(H[3]),
+               "v_lshl_add_u64 %s, %s, 0, %s" % (vp(H[0]), vp(H[2]), pair(d)),
+               "v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3])]
+        if z == 8:
+            return out + ["global_atomic_add_x2 %s, %s, off" % (vp(H[0]), vp(H[2]))], False
+        return out + ["global_atomic_add %s, %s, off" % (vp(H[0]), v(H[2]))], False
+    if name.startswith("CNTAL"):
+        z = int(name[5:])
+        out = ["v_subrev_u32 %s, s15, %s" % (v(H[0]), lo(d)),
+               "v_add_u32 %s, s14, %s" % (v(H[0]), v(H[0])),
+               "v_mov_b32 %s, s10" % v(H[2]), "v_mov_b32 %s, s11" % v(H[3])]
+        if z == 8:
+            return out + ["ds_add_u64 %s, %s" % (v(H[0]), vp(H[2]))], False
+        return out + ["ds_add_u32 %s, %s" % (v(H[0]), v(H[2]))], False
     if name == "OVLINIT":
         return ["v_mov_b32 %s, 0" % v(H[0]), "v_add_u32 %s, %d, v%d" % (v(H[1]), OVL_COUNT, V_STK),
                 "ds_write_b32 %s, %s" % (v(H[1]), v(H[0]))], False
@@ -2376,7 +2415,7 @@ def common_group_code():
           "s_mov_b32 %s, 0" % s(S_T0),
           ".Lmc_chunk:",
           "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_T1)),
-          "s_cbranch_scc1 .Lmc_loop",
+          "s_cbranch_scc1 .Lmc_zero",
           "v_add_u32 %s, %s, %s" % (v(H[5]), s(S_T0), v(H[4])),
           "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T1), v(H[5])),
           "s_mov_b64 exec, vcc",
@@ -2387,6 +2426,24 @@ def common_group_code():
           "s_mov_b64 exec, -1",
           "s_add_u32 %s, %s, 1024" % (s(S_T0), s(S_T0)),
           "s_branch .Lmc_chunk",
+          # a DP_MAP_LDSDELTA map: its workgroup sums start at zero
+          ".Lmc_zero:",
+          "s_bitcmp1_b32 s71, 29",
+          "s_cbranch_scc0 .Lmc_loop",
+          "s_and_b32 %s, s71, 0xffff" % s(S_T3),
+          "v_mov_b32 %s, 0" % v(H[3]),
+          "s_mov_b32 %s, 0" % s(S_T0),
+          ".Lmc_zchunk:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_T1)),
+          "s_cbranch_scc1 .Lmc_loop",
+          "v_add_u32 %s, %s, %s" % (v(H[5]), s(S_T0), v(H[4])),
+          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T1), v(H[5])),
+          "s_mov_b64 exec, vcc",
+          "v_add_u32 %s, %s, %s" % (v(H[5]), s(S_T3), v(H[5])),
+          "ds_write_b32 %s, %s" % (v(H[5]), v(H[3])),
+          "s_mov_b64 exec, -1",
+          "s_add_u32 %s, %s, 1024" % (s(S_T0), s(S_T0)),
+          "s_branch .Lmc_zchunk",
           ".Lmc_done:",
           "s_waitcnt lgkmcnt(0)",
           "s_barrier"]
@@ -2591,7 +2648,66 @@ def common_group_code():
     L += [".Lfinish_body:",
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
-          "s_barrier",
+          "s_barrier"]
+    # DP_MAP_LDSDELTA maps: the workgroup's sums into the delta areas (a global atomic per
+    # non-zero word; lane tid takes words tid, tid + 256, ...)
+    L += lane_index(H[0]) + [
+          "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_T0), v(H[0])),       # tid
+          "s_mov_b32 %s, 0" % s(S_T2),
+          ".Lfd_loop:",
+          "s_cmp_ge_u32 %s, %s" % (s(S_T2), s(S_NMAPS)),
+          "s_cbranch_scc1 .Lfd_done",
+          "s_lshl_b32 %s, %s, 5" % (s(S_T3), s(S_T2)),
+          "s_load_dwordx8 s[%d:%d], %s, %s" % (S_REC, S_REC + 7, sp(S_MAPS), s(S_T3)),
+          "s_waitcnt lgkmcnt(0)",
+          "s_add_u32 %s, %s, 1" % (s(S_T2), s(S_T2)),
+          "s_bitcmp1_b32 s71, 29",
+          "s_cbranch_scc0 .Lfd_loop",
+          "s_mul_i32 %s, s68, s69" % s(S_T1),                          # bytes
+          "s_add_u32 %s, %s, 63" % (s(S_BYTES), s(S_T1)),
+          "s_and_b32 %s, %s, -64" % (s(S_BYTES), s(S_BYTES)),          # dp_delta_off
+          "s_add_u32 s66, s66, %s" % s(S_BYTES),
+          "s_addc_u32 s67, s67, 0",                                    # the delta area
+          "s_and_b32 %s, s71, 0xffff" % s(S_T3),                       # the LDS sums
+          "s_bitcmp1_b32 s71, 28",
+          "s_cselect_b32 %s, 3, 2" % s(S_CODE),                        # log2 of the word
+          "v_lshlrev_b32 %s, %s, %s" % (v(H[2]), s(S_CODE), v(H[1])),  # first byte offset
+          "s_lshl_b32 %s, 256, %s" % (s(S_BYTES), s(S_CODE)),          # bytes per round
+          ".Lfd_word:",
+          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T1), v(H[2])),
+          "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+          "s_cbranch_execz .Lfd_next",
+          "v_add_u32 %s, %s, %s" % (v(H[3]), s(S_T3), v(H[2])),
+          "v_mov_b32 %s, 0" % v(R[3]),
+          "s_cmp_eq_u32 %s, 3" % s(S_CODE),
+          "s_cbranch_scc0 .Lfd_r4",
+          "ds_read_b64 %s, %s" % (vp(R[2]), v(H[3])),
+          "s_branch .Lfd_r",
+          ".Lfd_r4:",
+          "ds_read_b32 %s, %s" % (v(R[2]), v(H[3])),
+          ".Lfd_r:",
+          "s_waitcnt lgkmcnt(0)",
+          "v_cmp_ne_u64_e64 vcc, 0, %s" % vp(R[2]),
+          "s_and_b64 exec, exec, vcc",
+          "s_cbranch_execz .Lfd_next",
+          "v_mov_b32 %s, %s" % (v(R[0]), v(H[2])),
+          "s_cmp_eq_u32 %s, 3" % s(S_CODE),
+          "s_cbranch_scc0 .Lfd_w4",
+          "global_atomic_add_x2 %s, %s, s[66:67]" % (v(R[0]), vp(R[2])),
+          "s_branch .Lfd_next",
+          ".Lfd_w4:",
+          "global_atomic_add %s, %s, s[66:67]" % (v(R[0]), v(R[2])),
+          ".Lfd_next:",
+          "s_mov_b64 exec, %s" % sp(S_MASK),
+          "v_add_u32 %s, %s, %s" % (v(H[2]), s(S_BYTES), v(H[2])),
+          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T1), v(H[2])),
+          "s_and_b64 vcc, vcc, exec",
+          "s_cbranch_scc1 .Lfd_word",
+          "s_mov_b64 exec, -1",
+          "s_branch .Lfd_loop",
+          ".Lfd_done:",
+          "s_mov_b64 exec, -1",
           "s_cmp_eq_u64 %s, 0" % sp(S_HIST),
           "s_cbranch_scc1 .Lfin_end",
           ] + lane_index(H[0]) + [

@@ -50,7 +50,8 @@ enum dp_kind : uint16_t {
 	// map values"): the STX of a counter update — the translator found LDX{W,DW} X = [P + off];
 	// ADD/SUB X; STX [P + off] = X on one path — stores X like the STX (dst = P, src = X, off;
 	// aux = 4 or 8 bytes) and, into a map value, adds X minus the value it re-reads there
-	// (the packet's own view: nothing stored in between) instead of overwriting it
+	// (the packet's own view: nothing stored in between) instead of overwriting it.  aux bit 9:
+	// the update's addend is an immediate, in imm (what the ADD / SUB adds)
 	DK_CNT_STORE = 0x111,
 	// XADD (standard semantics, BPF_STX | BPF_XADD): *(u32 / u64 *)(dst + off) += src; aux = 4
 	// or 8 bytes, | 0x100 when imm was BPF_FETCH (src = the old value)
@@ -101,6 +102,10 @@ struct dp_map {
 // counters (else 4-byte).
 #define DP_MAP_ATOMIC 0x40000000u
 #define DP_MAP_ATOMIC64 0x10000000u
+// ... whose counter updates the assembly kernels first sum per workgroup in an LDS table (at the
+// LDS address in flags bits 0..15, zeroed at kernel start), added into the delta area when the
+// workgroup ends: one global atomic per touched word and workgroup instead of one per update
+#define DP_MAP_LDSDELTA 0x20000000u
 #define DP_HASH_MAX_KEY 65535u // (the key size field of dp_map.flags)
 #if defined(__HIPCC__)
 #define DP_FN __host__ __device__ static inline

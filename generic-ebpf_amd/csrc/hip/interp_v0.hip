@@ -507,7 +507,7 @@ ebpf_interp_v0(dp_launch L)
 				continue;
 			}
 			const uint64_t mask = size == 8 ? ~0ull : (1ull << (8 * size)) - 1;
-			uint64_t v = cls == 0x2 ? e.imm : R[e.src][tid], delta = 0, old = 0;
+			uint64_t v = (k < 0x100 && cls == 0x2) ? e.imm : R[e.src][tid], delta = 0, old = 0;
 			const bool add = k == DK_CNT_STORE || k == DK_XADD;
 			if (add) {
 				old = mi >= 0 && ovl.n ? load_ovl(ovl, a, size) : load_bytes(a, size);

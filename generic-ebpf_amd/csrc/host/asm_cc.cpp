@@ -1521,6 +1521,7 @@ written_reg(int fam, int d)
 	case AHF_STGEN1: case AHF_STGEN2: case AHF_STGEN4: case AHF_STGEN8:
 	case AHF_STSTK1: case AHF_STSTK2: case AHF_STSTK4: case AHF_STSTK8:
 	case AHF_CNTST4: case AHF_CNTST8: case AHF_XADD4: case AHF_XADD8: case AHF_OVLINIT:
+	case AHF_CNTAI4: case AHF_CNTAI8: case AHF_CNTAL4: case AHF_CNTAL8:
 		return -1;
 	default:
 		if (is_cond_fam(fam))

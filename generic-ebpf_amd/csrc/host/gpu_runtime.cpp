@@ -550,9 +550,17 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 		nd->table.push_back(m);
 	}
 	// arrays changed only by counter updates: device atomics into their delta areas
-	for (size_t k = 0; k < ep->xlated->atomic_maps.size(); k++)
-		nd->table[ep->xlated->atomic_maps[k]].flags |=
-		    DP_MAP_ATOMIC | (ep->xlated->atomic_width[k] == 8 ? DP_MAP_ATOMIC64 : 0u);
+	for (size_t k = 0; k < ep->xlated->atomic_maps.size(); k++) {
+		dp_map &m = nd->table[ep->xlated->atomic_maps[k]];
+		m.flags |= DP_MAP_ATOMIC | (ep->xlated->atomic_width[k] == 8 ? DP_MAP_ATOMIC64 : 0u);
+		// an LDS-resident map: its workgroup-local sums too (DP_MAP_LDSDELTA), if they fit
+		const uint32_t bytes = m.value_size * m.max_entries;
+		const uint32_t at = (nd->map_lds_bytes + 7) & ~7u;
+		if (m.lds_off != ~0u && at + bytes <= kMapLdsBudget && kMapLdsBase + at < 0x10000u) {
+			m.flags |= DP_MAP_LDSDELTA | (kMapLdsBase + at);
+			nd->map_lds_bytes = at + ((bytes + 15) & ~15u);
+		}
+	}
 	if (!nd->table.empty()) {
 		e = hipMalloc(&nd->d_maps, nd->table.size() * sizeof(dp_map));
 		if (e != hipSuccess)

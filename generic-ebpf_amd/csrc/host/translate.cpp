@@ -600,6 +600,16 @@ dataflow(dprog_host &out)
 			rt[i] = r[i];
 		if (e.kind == EBPF_OP_JEQ_IMM && e.dst < EBPF_REG_MAX)
 			rt[e.dst] = mk(AV_CONST, (int64_t)e.imm);
+		// a NULL test of a lookup result: past it (JEQ 0 not taken, JNE 0 taken) it is non-NULL
+		if ((e.kind == EBPF_OP_JEQ_IMM || e.kind == EBPF_OP_JNE_IMM) && e.imm == 0 &&
+		    e.dst < EBPF_REG_MAX && r[e.dst].kind == AV_MAPVAL_NULL) {
+			av nn = r[e.dst];
+			nn.kind = AV_MAPVAL;
+			if (e.kind == EBPF_OP_JEQ_IMM)
+				r[e.dst] = nn; // (r feeds the fall-through edge below)
+			else
+				rt[e.dst] = nn;
+		}
 		for (int k = 0; k < 2; k++) {
 			const uint32_t sx = succ[k];
 			const av *re = k ? rt : r;
@@ -693,6 +703,20 @@ fuse_counters(dprog_host &out, bool std_mode)
 		dp_entry st = e3;
 		st.kind = DK_CNT_STORE;
 		st.aux = (uint16_t)w;
+		// an immediate addend (the ALU's): aux bit 9, imm = what the update adds
+		switch (e2.kind) {
+		case EBPF_OP_ADD64_IMM: case EBPF_OP_MOV64_IMM: case EBPF_OP_ADD_IMM:
+			st.imm = e2.imm;
+			st.aux |= 0x200;
+			break;
+		case EBPF_OP_SUB64_IMM: case EBPF_OP_SUB_IMM:
+			st.imm = 0 - e2.imm;
+			st.aux |= 0x200;
+			break;
+		default:
+			st.imm = 0;
+			break;
+		}
 		if (preds[j] == 1 && preds[k3] == 1) {
 			out.entries[k3] = st;
 			continue;

@@ -22,11 +22,12 @@ _SPECIAL_IMM = [0, 1, -1, 2, 7, 8, 15, 16, 31, 32, 33, 48, 63, 64, 65, 127, 255,
 
 
 class _Gen:
-    def __init__(self, seed, nmaps, map_value_size, writes=False):
+    def __init__(self, seed, nmaps, map_value_size, writes=False, vstores=False):
         self.g = np.random.default_rng(seed)
         self.nmaps = nmaps
         self.vs = map_value_size
         self.writes = writes
+        self.vstores = vstores
         self.scalars = [0, 2, 3, 4, 5, 6, 7, 8, 9]
         self.ctx = 1
         self.stack_ok = set()   # initialised stack byte offsets (negative, relative to r10)
@@ -146,10 +147,41 @@ class _Gen:
         vsz = self.pick([s for s in (1, 2, 4, 8) if s <= self.vs])
         voff = self.r(self.vs - vsz + 1)
         dst = self.pick([3, 4, 5, 8, 9])
-        out += [Branch(I("jeq_imm", 0, imm=0), miss),
-                I({1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[vsz], dst, 0, voff),
+        out += [Branch(I("jeq_imm", 0, imm=0), miss)]
+        if self.vstores:
+            out += self.value_stores()
+        out += [I({1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[vsz], dst, 0, voff),
                 I("mov_imm", 0, imm=self.imm()), I("mov_imm", 1, imm=self.imm()),
                 I("mov_imm", 2, imm=self.imm())]
+        return out
+
+    def value_stores(self):
+        """Stores through the lookup result in r0 (ebpf_gpu.h "Stores into map values"): plain
+        STX / ST of 1-8 bytes anywhere in the value, and counter updates (LDX{W,DW} X; ADD/SUB
+        (32- or 64-bit, immediate or register; the reference's MOV64, which adds); STX back),
+        aligned or not.  The lookup's own load follows (the packet reads its stores back)."""
+        out = []
+        safe = [3, 4, 5, 7, 8, 9]   # (r0 holds the value's address, r1 the map, r2 the key's)
+        for _ in range(self.r(3) + 1):
+            k = self.r(4)
+            if k < 2 or self.vs < 4:
+                size = self.pick([z for z in (1, 2, 4, 8) if z <= self.vs])
+                off = self.r(self.vs - size + 1)
+                if k == 0:
+                    out.append(I({1: "stb", 2: "sth", 4: "stw", 8: "stdw"}[size], 0, 0, off, self.imm()))
+                else:
+                    out.append(I({1: "stxb", 2: "stxh", 4: "stxw", 8: "stxdw"}[size], 0,
+                                 self.pick(safe), off))
+                continue
+            size = self.pick([z for z in (4, 8) if z <= self.vs])
+            off = self.r(self.vs - size + 1)
+            x = self.pick([3, 4, 5, 8, 9])
+            y = self.pick([s for s in safe if s != x])
+            alu = self.pick(["add64_imm", "sub64_imm", "add64_reg", "sub64_reg", "mov64_reg"] +
+                            (["add_imm", "sub_imm", "add_reg"] if size == 4 else []))
+            a = I(alu, x, imm=self.imm()) if alu.endswith("imm") else I(alu, x, y)
+            out += [I({4: "ldxw", 8: "ldxdw"}[size], x, 0, off), a,
+                    I({4: "stxw", 8: "stxdw"}[size], 0, x, off)]
         return out
 
     def update(self):
@@ -243,10 +275,12 @@ class _Gen:
         return out + [I("exit")]
 
 
-def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None, writes=False):
+def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None, writes=False,
+                   vstores=False):
     """writes: half the map helper calls are map_update_elem / map_delete_elem (the device
-    batch semantics: ebpf_gpu.h "Map writes in a device batch")."""
-    gen = _Gen(seed, nmaps, map_value_size, writes)
+    batch semantics: ebpf_gpu.h "Map writes in a device batch"); vstores: every lookup hit
+    stores into the value first (ebpf_gpu.h "Stores into map values")."""
+    gen = _Gen(seed, nmaps, map_value_size, writes, vstores)
     nodes = gen.prologue() + gen.block(length) + gen.epilogue()
     rs = reset_stride if reset_stride is not None else int(gen.g.integers(3, 12))
     return assemble(nodes, reset_stride=rs)

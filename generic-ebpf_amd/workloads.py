@@ -130,7 +130,7 @@ def prog_c2():
     return assemble(nodes)
 
 
-def _classify_program(with_lookup, pad, reset, hash_key=False):
+def _classify_program(with_lookup, pad, reset, hash_key=False, counter=False):
     """Ethernet → IPv4 (TCP/UDP main path) | IPv6 | ICMP | other.  The flow hash and the
     verdict arithmetic run first and the ACL decisions sit at the end of the path, so nearly
     every IPv4 packet executes the full main path (no early-exit shortcut)."""
@@ -185,6 +185,14 @@ def _classify_program(with_lookup, pad, reset, hash_key=False):
             Branch(I("jeq_imm", R0, imm=0), _exit_with(2)),
             I("ldxdw", R6, R0, 0), I("xor64_reg", R8, R6),
         ]
+        if counter:   # counters[key] += 1: the per-port packet counter (map 1)
+            lookup += [
+                LdDw(R1, MapRef(1)),
+                I("mov_imm", R2, imm=0), I("mov64_reg", R2, R10), I("add64_imm", R2, imm=-4),
+                I("call", imm=0),
+                Branch(I("jeq_imm", R0, imm=0), _exit_with(2)),
+                I("ldxdw", R6, R0, 0), I("add64_imm", R6, imm=1), I("stxdw", R0, R6, 0),
+            ]
     verdict = [
         I("mov_reg", R0, R8), I("rsh_imm", R0, imm=13), I("and_imm", R0, imm=7),
         I("add_imm", R0, imm=8),
@@ -200,11 +208,11 @@ def _classify_program(with_lookup, pad, reset, hash_key=False):
     return assemble(head + pads + lookup + verdict, reset_stride=reset)
 
 
-def _fit(with_lookup, target, exact=True, hash_key=False):
+def _fit(with_lookup, target, exact=True, hash_key=False, counter=False):
     """Smallest padding whose main path executes ``target`` instructions (JA resets included)."""
     for reset in (8, 7, 9, 6, 10):
         for pad in range(0, 64):
-            lay = _classify_program(with_lookup, pad, reset, hash_key)
+            lay = _classify_program(with_lookup, pad, reset, hash_key, counter)
             if lay.main_path_steps == target or (not exact and lay.main_path_steps >= target):
                 return lay
             if lay.main_path_steps > target:
@@ -222,6 +230,13 @@ def prog_c4():
     path (64) plus STXW key, LDDW map, r2 = r10-4 (3 insns), CALL, NULL check, LDXDW value and
     XOR into the hash — 75 executed instructions on the main path."""
     return _fit(True, 75, exact=False)
+
+
+def prog_c4c():
+    """C4 + a per-key packet counter: after the array lookup, counters[key] += 1 through a second
+    array map's lookup result (LDDW, r2 = r10-4, CALL, NULL check, LDXDW / ADD64 1 / STXDW — the
+    counter update the device runs as an atomic addition, ebpf_gpu.h "Stores into map values")."""
+    return _fit(True, 84, exact=False, counter=True)
 
 
 def prog_c4h():
@@ -366,6 +381,9 @@ CONFIGS = {
                pkt="l2l3"),
     "c5": dict(desc="256-insn branch-heavy filter, IMIX 64-1500 B packets", prog=prog_c5,
                pkt="imix"),
+    "c4c": dict(desc="64-insn classify + array-map lookup + per-key packet counter "
+                     "(counters[key] += 1 through a lookup result), 64 B packets", prog=prog_c4c,
+                pkt="l2l3"),
     "c4h": dict(desc="64-insn classify + hashtable lookup (1M-entry table keyed by IPv4 dst), "
                      "64 B packets", prog=prog_c4h, pkt="c4h"),
     "c3lit": dict(desc="literal 64-slot classify (11 executed), 64 B packets",

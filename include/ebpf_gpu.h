@@ -63,7 +63,35 @@ struct ebpf_map;
  *     one batch on one device (ebpf_prog_run_batch_multi_dev then synchronises its streams).
  * The written values live in the device's mirror of the map until the host API touches the map
  * (lookup / update / delete / get_next_key, or a helper call from ebpf_prog_run), which copies
- * them back first.  ebpf_prog_run itself keeps the reference's immediate writes. */
+ * them back first.  ebpf_prog_run itself keeps the reference's immediate writes.
+ *
+ * Stores into map values.  The reference hands the program a pointer into the map's storage
+ * (array_map_lookup_elem, ebpf_map_array.c:115-124; a hashtable element's value,
+ * ebpf_map_hashtable.c:285-301) and ST / STX write through it in place
+ * (ebpf_interpreter.c:343-366).  In a device batch:
+ *   - a packet's loads (LDX, and the load of a counter update or XADD below) see its own
+ *     earlier stores into map values; other packets of the batch see the batch-start maps.
+ *     Helper calls read keys and values as the batch started;
+ *   - after the batch the stores land in packet order, a packet's own in program order, byte by
+ *     byte: the last store of each byte wins (together with map_update_elem's whole values);
+ *   - counter updates land as additions: three consecutive instructions (JA aside)
+ *     LDX{W,DW} X = [P + off] (X != P); ADD or SUB to X of an immediate or of a register other
+ *     than X (64-bit; 32-bit too for W; under the reference's semantics MOV64, which adds);
+ *     STX [P + off] = X of the same width — and, under standard semantics, XADD
+ *     (BPF_STX | BPF_XADD, W / DW; imm 0, or 1 = BPF_FETCH: src receives the old value) — add
+ *     (stored - loaded) mod 2^width when the address is aligned to the width within the map's
+ *     values (arrays: from the first value; hashtables: from the value's start), else land as
+ *     plain stores.  Additions commute, so a map that only counter updates touch in a batch ends
+ *     as the reference's sequential run leaves it (per-packet counters, byte counts);
+ *   - a packet that faults leaves no write behind except its counter updates, which are atomic
+ *     operations: they take effect when executed;
+ *   - EBPF_FAULT_MAP_WRITE is left for a store into a map value the translation did not provide
+ *     for (a packet-relative pointer that lands in a map); programs with loops cannot store into
+ *     map values on the device (EOPNOTSUPP, as for map_update_elem).
+ * How it runs: arrays changed only by aligned counter updates of one width take device atomics
+ * into a delta area next to their mirror (added into the values after the batch); other arrays'
+ * stores land on the device (per-byte winners); hashtables, and arrays that mix counter updates
+ * with stores, replay the batch's records on the host in order. */
 
 /* Per-packet fault codes (0 = the program reached EXIT). */
 enum ebpf_fault {
@@ -77,8 +105,8 @@ enum ebpf_fault {
 	EBPF_FAULT_BAD_REG = 7,      /* dst/src register nibble >= 11 (reference overflows reg[]) */
 	EBPF_FAULT_LOOP = 8,         /* a jump that re-enters its own state: the reference never returns;
 	                                standard semantics: the loop budget is spent (see below) */
-	EBPF_FAULT_MAP_WRITE = 9,    /* store into map value memory through a lookup result (values
-	                                change only through map_update_elem during a batch) */
+	EBPF_FAULT_MAP_WRITE = 9,    /* store into a map value through a pointer the translation did
+	                                not see reach a map ("Stores into map values" above) */
 	EBPF_FAULT_BAD_MAP = 10,     /* map helper called with r1 not a map of this program's env */
 	EBPF_FAULT_MAX
 };

@@ -324,3 +324,58 @@ def test_counter_full_size_equals_sequential_reference(gpu, env, variant):
         gpu.set_variant(0)
         p.destroy()
         m.destroy()
+
+
+# ---------------------------------------------------------------- random programs
+
+
+def _random_case(k):
+    from generic_ebpf_amd import randprog
+    g = np.random.default_rng(9000 + k)
+    vs = int(g.choice([4, 8, 12, 16]))
+    me = int(g.choice([8, 256]))
+    lay = randprog.random_program(7000 + k, length=int(g.integers(10, 60)), nmaps=2,
+                                  map_value_size=vs, writes=k % 3 == 0, vstores=True)
+    maps = [(vs, me, g.integers(0, 256, vs * me, dtype=np.uint8).tobytes()) for _ in range(2)]
+    return lay, maps
+
+
+def test_oracle_one_packet_batches_are_the_reference_run():
+    """For random programs with value stores: a one-packet batch (overlay, records applied after
+    the batch) leaves the same results, faults, packet bytes and maps as the sequential run that
+    writes in place — the rules reduce to the reference's behaviour for one packet."""
+    from generic_ebpf_amd import workloads
+    for k in range(40):
+        lay, maps = _random_case(k)
+        pk = workloads.packets_random(8, 64, seed=k)
+        for i in range(len(pk)):
+            a = pyoracle.OracleProgram(lay.code, lay.relocs, maps)
+            b = pyoracle.OracleProgram(lay.code, lay.relocs, maps, sequential=True)
+            ra, fa, da, _ = a.run(pk[i:i + 1], 1, 64)
+            rb, fb, db, _ = b.run(pk[i:i + 1], 1, 64)
+            assert (ra == rb).all() and (fa == fb).all() and (da == db).all(), (k, i)
+            if not fa.any():
+                assert a.map_bytes(0) == b.map_bytes(0) and a.map_bytes(1) == b.map_bytes(1), (k, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_random_value_store_programs_vs_oracle(gpu, env, variant):
+    """Random programs whose lookups store into the values (plain stores, counter updates,
+    read back), a third with map_update_elem / delete too: results, faults, packet bytes and
+    both maps against the oracle's batch mode."""
+    import goldens
+    from helpers import device_run
+    from generic_ebpf_amd import workloads
+    bad = []
+    for k in range(60):
+        lay, maps = _random_case(k)
+        n = 2048
+        pk = workloads.packets_random(n, 64, seed=300 + k)
+        op = pyoracle.OracleProgram(lay.code, lay.relocs, maps)
+        want, wf, wdata, _ = op.run(pk.reshape(-1), n, 64, nthreads=8)
+        ret, faults, after = _device(gpu, env, lay, maps, pk, variant, False)
+        if not (np.array_equal(want, ret) and np.array_equal(wf, faults) and
+                after[0] == op.map_bytes(0) and after[1] == op.map_bytes(1)):
+            bad.append(k)
+    assert not bad, bad
