@@ -101,7 +101,7 @@ def parse(argv=None):
 
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
-                   "c4": 1 << 26, "c4c": 1 << 26, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24,
+                   "c4": 1 << 26, "c4c": 1 << 26, "c3l": 1 << 24, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24,
                    "c5lit": 1 << 22}
 # C4H: bytes one lookup must move.  The device table's slot is 32 B (u32 used | u32 hash | 4-B key
 # 8-B padded | 8-B value), but a random probe cannot fetch less than one 64-B line from HBM: the
@@ -121,6 +121,8 @@ class Workload:
         self.cfg, self.lo, self.hi = cfg, lo, hi
         self.n = hi - lo
         self.lay = workloads.CONFIGS[cfg]["prog"]()
+        # 0: the reference's stepping; 1: standard eBPF (ebpf_prog_set_semantics: C3L's loop)
+        self.semantics = workloads.CONFIGS[cfg].get("semantics", 0)
         self.maps = []
         self.offs = None
         if workloads.CONFIGS[cfg]["pkt"] == "imix":
@@ -136,6 +138,9 @@ class Workload:
             universe, keys, values = workloads.c4h_table()
             self.maps = [("hash", 4, 8, len(keys), keys, values)]
             self.pk = workloads.packets_c4h(self.D, universe, seed=4)
+            return
+        if cfg == "c3l":
+            self.pk = workloads.packets_ipv4opt(self.D)
             return
         rnd = cfg in ("c0", "c2", "nop200", "alu200")
         gen = workloads.packets_random if rnd else workloads.packets_l2l3
@@ -206,7 +211,8 @@ def oracle_threads():
 def verify(w, torch, d_ret, d_hist_total, world, dev):
     """Compare the last launch's results on the device with the oracle.  Returns (ok, info)."""
     import pyoracle
-    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=True)
+    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=True,
+                                semantics=w.semantics)
     thr = oracle_threads()
     if w.offs is not None:
         want, wf, _, _ = op.run(w.pk, w.n, 0, w.offs, nthreads=thr)
@@ -290,7 +296,8 @@ def cpu_baseline(w, budget_s):
         data = np.ascontiguousarray(w.pk[:n].reshape(-1))
         offsets, stride = None, 64
     # no configured program stores to packet bytes, so passes over the same buffer are identical
-    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=False)
+    op = pyoracle.OracleProgram(w.lay.code, w.lay.relocs, w.oracle_maps(), checked=False,
+                                semantics=w.semantics)
     ret = np.zeros(n, dtype=np.uint64)
 
     def timed(threads, seconds):
@@ -419,6 +426,8 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
     env = native.Env()
     maps = make_maps(env, w.maps)
     prog = native.Prog(env, native.patch_relocs(w.lay.code, w.lay.relocs, [m.handle for m in maps]))
+    if w.semantics:
+        prog.set_semantics(native.SEM_STANDARD)
     native.set_variant(a.variant)
     prog.prepare(local)
 

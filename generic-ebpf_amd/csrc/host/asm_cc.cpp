@@ -1738,7 +1738,7 @@ cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const st
 	points.clear();
 	// opt-in (EBPF_CC_REGROUP=1): measured slower than per-group divergence on C5
 	const char *on = getenv("EBPF_CC_REGROUP");
-	if (on == nullptr || atoi(on) == 0)
+	if (on == nullptr || atoi(on) == 0 || xl.has_loops) // (the plan walks a tree)
 		return;
 	// entries each side of the divergent conditional at least holds: a queued lane costs its
 	// push, a batch slot and the batch set-up (packet address, header), worth it for long paths
@@ -1848,6 +1848,9 @@ void
 cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 		 uint32_t max_cuts, std::vector<uint32_t> &cuts)
 {
+	cuts.clear();
+	if (xl.has_loops) // (the plan walks a tree)
+		return;
 	uint32_t min_size = 96; // (as regrouping: both sides of the divergent conditional this long)
 	if (const char *m = getenv("EBPF_PATHSORT_MIN"))
 		min_size = (uint32_t)atoi(m);

@@ -1218,11 +1218,11 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		const int mode =
 		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
 		// variant 0: the compiled program; a program too large for the code area runs on the
-		// assembly interpreter instead (still the device path)
-		// (a program with loops runs on the interpreter: the code generator's liveness and
-		// facts assume an acyclic graph)
+		// assembly interpreter instead (still the device path).  Programs with loops compile
+		// too: the code generator keeps facts and liveness only across single-predecessor
+		// edges, and a loop head (an entry point, >= 2 predecessors) starts from nothing known
 		void *fn = nullptr;
-		const bool compile = variant == 0 && !ep->xlated->has_loops;
+		const bool compile = variant == 0;
 		if (compile && (err = jit_entries(ep, dp, mode)) == 0) {
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];

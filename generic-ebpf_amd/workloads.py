@@ -355,6 +355,102 @@ def prog_literal(nslots):
     return Layout(b"".join(code), [], len(execd), nslots)
 
 
+def _asm_std(items):
+    """Standard-semantics code (pc += off + 1) from Insn and ("label", name) items; a jump's
+    ``off`` may name a label."""
+    at, k = {}, 0
+    for it in items:
+        if isinstance(it, tuple):
+            at[it[1]] = k
+        else:
+            k += 1
+    code, k = [], 0
+    for it in items:
+        if isinstance(it, tuple):
+            continue
+        off = at[it.off] - (k + 1) if isinstance(it.off, str) else it.off
+        code.append(isa.encode(it.op, it.dst, it.src, off, it.imm))
+        k += 1
+    from .layout import Layout
+    return Layout(b"".join(code), [], None, len(code))
+
+
+def packets_ipv4opt(n, seed=6):
+    """C3L packets: the C3 frames (packets_l2l3) with IPv4 header lengths of 5 words (half) or
+    6-12 (options, the rest of the header random bytes), and a correct header checksum on 90 %
+    of the IPv4 frames (the others keep random checksum bytes)."""
+    p = packets_l2l3(n, 64, seed)
+    g = _rng(seed + 1)
+    v4 = (p[:, 12] == 0x08) & (p[:, 13] == 0x00)
+    ihl = np.where(g.random(n) < 0.5, 5, g.integers(6, 13, n)).astype(np.uint8)
+    p[v4, 14] = 0x40 | ihl[v4]
+    fix = v4 & (g.random(n) < 0.9)
+    for h in range(5, 13):
+        sel = np.nonzero(fix & (ihl == h))[0]
+        if len(sel) == 0:
+            continue
+        hdr = p[sel, 14:14 + 4 * h].astype(np.uint32)
+        hdr[:, 10:12] = 0
+        s = ((hdr[:, 0::2] << 8) | hdr[:, 1::2]).sum(axis=1)
+        while (s >> 16).any():
+            s = (s & 0xffff) + (s >> 16)
+        c = (~s) & 0xffff
+        p[sel, 24] = (c >> 8).astype(np.uint8)
+        p[sel, 25] = (c & 0xff).astype(np.uint8)
+    return p
+
+
+def prog_c3l():
+    """IPv4 header check with a bounded loop (standard semantics, ebpf_prog_set_semantics): not
+    IPv4 -> 0; IHL outside 5..12 -> 3; a loop over the IHL 32-bit header words (LDXW through a
+    cursor, 5 instructions per word, one backward jump per word) sums them, four folds reduce the
+    sum to the 16-bit one's-complement sum; != 0xffff (bad checksum) -> 2; TTL <= 1 -> 4; else
+    16 + (protocol & 15).  Accepted frames execute 34 + 5 x IHL instructions (59-94)."""
+    L = "label"
+    items = [I("mov64_reg", R6, R1), I("mov64_imm", R0, imm=0), I("ldxh", R2, R6, 12),
+             I("jne_imm", R2, imm=0x0008, off="out"), I("ldxb", R3, R6, 14),
+             I("and64_imm", R3, imm=15), I("jlt_imm", R3, imm=5, off="mal"),
+             I("jgt_imm", R3, imm=12, off="mal"), I("mov64_imm", R4, imm=0),
+             I("mov64_reg", R5, R6), I("add64_imm", R5, imm=14), (L, "word"),
+             I("ldxw", R7, R5, 0), I("add64_reg", R4, R7), I("add64_imm", R5, imm=4),
+             I("sub64_imm", R3, imm=1), I("jne_imm", R3, imm=0, off="word"),
+             I("mov64_reg", R7, R4), I("rsh64_imm", R7, imm=32), I("mov_reg", R4, R4),
+             I("add64_reg", R4, R7)]
+    for _ in range(3):
+        items += [I("mov64_reg", R7, R4), I("rsh64_imm", R7, imm=16), I("and64_imm", R4, imm=0xffff),
+                  I("add64_reg", R4, R7)]
+    items += [I("jne_imm", R4, imm=0xffff, off="bad"), I("ldxb", R2, R6, 22),
+              I("jle_imm", R2, imm=1, off="ttl"), I("ldxb", R0, R6, 23), I("and64_imm", R0, imm=15),
+              I("add64_imm", R0, imm=16), I("exit"),
+              (L, "out"), I("exit"),
+              (L, "mal"), I("mov64_imm", R0, imm=3), I("exit"),
+              (L, "bad"), I("mov64_imm", R0, imm=2), I("exit"),
+              (L, "ttl"), I("mov64_imm", R0, imm=4), I("exit")]
+    return _asm_std(items)
+
+
+def c3l_expected(p):
+    """numpy restatement of prog_c3l's verdict per packet (tests; input generation aside,
+    nothing here executes eBPF)."""
+    v4 = (p[:, 12] == 0x08) & (p[:, 13] == 0x00)
+    ihl = (p[:, 14] & 15).astype(np.int64)
+    out = np.zeros(len(p), dtype=np.uint64)
+    mal = v4 & ((ihl < 5) | (ihl > 12))
+    out[mal] = 3
+    ok = v4 & ~mal
+    for h in range(5, 13):
+        sel = np.nonzero(ok & (ihl == h))[0]
+        hdr = p[sel, 14:14 + 4 * h].astype(np.uint64)
+        s = ((hdr[:, 0::2] << 8) | hdr[:, 1::2]).sum(axis=1)
+        while (s >> 16).any():
+            s = (s & 0xffff) + (s >> 16)
+        good = s == 0xffff
+        ttl = p[sel, 22]
+        v = np.where(~good, 2, np.where(ttl <= 1, 4, 16 + (p[sel, 23] & 15).astype(np.uint64)))
+        out[sel] = v
+    return out
+
+
 def prog_c0():
     """Floor: MOV r0, 2; EXIT (2 executed instructions) — measures staging + retirement."""
     return assemble([I("mov_imm", R0, imm=2), I("exit")])
@@ -384,6 +480,9 @@ CONFIGS = {
     "c4c": dict(desc="64-insn classify + array-map lookup + per-key packet counter "
                      "(counters[key] += 1 through a lookup result), 64 B packets", prog=prog_c4c,
                 pkt="l2l3"),
+    "c3l": dict(desc="IPv4 header checksum over IHL words in a bounded loop (standard "
+                     "semantics; 59-94 executed insns), 64 B packets", prog=prog_c3l,
+                pkt="ipv4opt", semantics=1),
     "c4h": dict(desc="64-insn classify + hashtable lookup (1M-entry table keyed by IPv4 dst), "
                      "64 B packets", prog=prog_c4h, pkt="c4h"),
     "c3lit": dict(desc="literal 64-slot classify (11 executed), 64 B packets",

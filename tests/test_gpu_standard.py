@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 VARIANTS = [0, 1, 2]
 
 
-def run_device(native, env, code, rel, specs, data, count, stride, variant, offsets=None):
+def run_device(native, env, code, rel, specs, data, count, stride, variant, offsets=None,
+               want_exec=None):
     maps = []
     for vs, me, d in specs:
         m = native.Map(env, me, vs)
@@ -24,6 +25,8 @@ def run_device(native, env, code, rel, specs, data, count, stride, variant, offs
         native.set_variant(variant)
         d = np.ascontiguousarray(data.copy())
         ret, faults, _ = p.run_batch(d, count, stride, offsets)
+        if want_exec is not None:  # what the launch ran (variant 0: the compiled program)
+            assert p.exec_info(0)[0] == want_exec
         return ret, faults
     finally:
         native.set_variant(0)
@@ -90,7 +93,8 @@ def test_loop_budget_on_device(gpu, env, variant, extra, fault):
     n = stdprogs.LOOP_BUDGET + 1 + extra
     code, rel = stdprogs.countdown(n)
     pk = np.zeros((64, 64), dtype=np.uint8)
-    got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), 64, 64, variant)
+    got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), 64, 64, variant,
+                         want_exec="compiled" if variant == 0 else None)
     assert (gf == fault).all()
     assert (got == (0 if fault else n * (n + 1) // 2)).all()
 
@@ -112,10 +116,30 @@ def test_loop_programs_vs_oracle(gpu, env, variant):
             pk.reshape(-1), n, stride, nthreads=8)
         if forever:
             assert (wf == 8).any()
-        got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), n, stride, variant)
+        got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), n, stride, variant,
+                             want_exec="compiled" if variant == 0 else None)
         if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
             bad.append((seed, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_c3l_full_size(gpu, env, variant):
+    """The bench's loop workload (C3L: IPv4 header checksum over IHL words, 5-12 trips) over 16M
+    packets tiled from 256k distinct: result i equals the oracle's for its distinct packet (and
+    the numpy restatement of the rule); variant 0 runs it compiled."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c3l()
+    distinct, tiles = 1 << 18, 64
+    pk = workloads.packets_ipv4opt(distinct)
+    want, wf, _, _ = pyoracle.OracleProgram(lay.code, [], [], semantics=1).run(
+        pk.reshape(-1), distinct, 64, nthreads=8)
+    assert not wf.any()
+    np.testing.assert_array_equal(want, workloads.c3l_expected(pk))
+    got, gf = run_device(gpu, env, lay.code, [], [], np.tile(pk.reshape(-1), tiles), distinct * tiles,
+                         64, variant, want_exec="compiled" if variant == 0 else None)
+    assert not gf.any()
+    np.testing.assert_array_equal(got.reshape(tiles, distinct), np.broadcast_to(want, (tiles, distinct)))
 
 
 @pytest.mark.parametrize("variant", VARIANTS)

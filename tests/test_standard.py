@@ -153,3 +153,40 @@ def test_loop_programs_oracle_vs_cpu_path(native, env, seed):
         p.info()
     finally:
         p.destroy()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_loop_programs_compile(native, env, seed):
+    """Programs with loops compile for variant 0 (both layouts): the code generator's facts and
+    liveness cross only single-predecessor edges, so a loop head starts from nothing known."""
+    code, rel = stdprogs.gen_loop_program(9000 + seed, forever_every=97 if seed % 8 == 0 else 0)
+    p = native.Prog(env, code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        for layout in (0, 1):
+            assert len(p.device_code(layout)) > 0
+    finally:
+        p.destroy()
+
+
+def test_c3l_workload_oracle_and_cpu_path(native, env):
+    """C3L (workloads.prog_c3l, the bench's loop workload): the oracle's standard restatement,
+    a numpy restatement of the header checksum rule and the CPU ebpf_prog_run agree; every
+    verdict class occurs."""
+    from generic_ebpf_amd import workloads
+    lay = workloads.prog_c3l()
+    pk = workloads.packets_ipv4opt(1 << 14)
+    want = workloads.c3l_expected(pk)
+    got, gf, _, _ = pyoracle.OracleProgram(lay.code, [], [], semantics=1).run(pk.reshape(-1), len(pk), 64)
+    assert not gf.any()
+    np.testing.assert_array_equal(got, want)
+    assert {0, 2, 4} <= set(int(x) for x in np.unique(want)) and (want >= 16).mean() > 0.5
+    p = native.Prog(env, lay.code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        for i in range(0, len(pk), 37):
+            assert p.run_cpu(pk[i].tobytes())[0] == int(want[i]), i
+        for layout in (0, 1):
+            assert len(p.device_code(layout)) > 0
+    finally:
+        p.destroy()
