@@ -190,8 +190,18 @@ struct dp_launch {
 	// its own stores (an overlay of the words it stored, per lane: DP_OVL_* below); bits 8..15 =
 	// the overlay's entries per lane
 	uint32_t vflags;
+	// window launches (span image; gen_interp.py "Window mode"): LDS bytes of a window (0: not
+	// a window launch), packets per workgroup, the LDS offset of the per-window arrays, and the
+	// overflow slot list {0, n, packet indices...} the general kernels run after it
+	uint32_t win_bytes;
+	uint32_t win_chunk;
+	uint32_t win_arr;
+	uint32_t win_pad;
+	uint32_t *win_ovf;
 };
-static_assert(sizeof(dp_launch) == 208, "dp_launch layout is shared with the assembly kernels");
+static_assert(sizeof(dp_launch) == 232, "dp_launch layout is shared with the assembly kernels");
+static_assert(offsetof(dp_launch, win_bytes) == 0xd0 && offsetof(dp_launch, win_ovf) == 0xe0,
+	      "gen_interp.py loads the window fields at fixed offsets");
 static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_slot) == 192,
 	      "gen_interp.py loads these fields at fixed offsets");
 

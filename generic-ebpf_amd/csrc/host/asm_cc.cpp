@@ -1694,7 +1694,7 @@ enum : uint32_t {
 	S2_ADD_U32 = 0x00, S2_SUB_U32 = 0x01, S2_ADDC_U32 = 0x04, S2_MIN_U32 = 0x07, S2_CSELECT_B32 = 0x0a,
 	S2_AND_B32 = 0x0c, S2_OR_B32 = 0x0e, S2_OR_B64 = 0x0f, S2_ANDN2_B64 = 0x13, S2_LSHL_B32 = 0x1c,
 	S2_BFE_U32 = 0x25,
-	S1_BCNT1_I32_B64 = 0x0d, S1_SETPC_B64 = 0x1d, S1_SWAPPC_B64 = 0x1e,
+	S1_MOV_B32 = 0x00, S1_BCNT1_I32_B64 = 0x0d, S1_SETPC_B64 = 0x1d, S1_SWAPPC_B64 = 0x1e,
 	SC_CMP_GE_U32 = 0x09, SC_BITCMP1_B32 = 0x0d,
 	V3_MBCNT_LO = 0x28c, V3_MBCNT_HI = 0x28d,
 	G_LOAD_DWORDX2 = 0x15, G_STORE_DWORD = 0x1c, G_STORE_DWORDX2 = 0x1d,
@@ -1946,6 +1946,16 @@ cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t 
 	E.sop2(S2_OR_B64, AH_S_DEFER, opnd{(uint32_t)AH_S_DEFER}, opnd{SRC_EXEC});  // queued, not stored
 	E.sop2(S2_ANDN2_B64, 16, opnd{16}, opnd{SRC_EXEC});                        // S_ALIVE
 	jump_cb(E, sched_off, false);
+}
+
+void
+cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out)
+{
+	enc E{out};
+	sopc(E, SC_BITCMP1_B32, opnd{7}, opnd{128 + 12});              // s_bitcmp1_b32 s7, 12
+	E.w(0xbf840000u | 5u);                                        // s_cbranch_scc0 +5 (past the jump)
+	E.sop1(S1_MOV_B32, 52, opnd{128 + cls});                      // s_mov_b32 S_CODE, class
+	jump_cb(E, cut_off, false);                                   // (4 dwords) -> .Lr_cut
 }
 
 void

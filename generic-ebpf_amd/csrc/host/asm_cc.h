@@ -76,6 +76,11 @@ cc_queue_bytes(uint32_t live_slots)
 void cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t sched_off,
 		  std::vector<uint8_t> &out);
 
+// Window launches (gen_interp.py "Window mode"; span image): code at the head of cut point q,
+// class cls = q + 1.  In phase A (s7 bit 12) the running lanes record their class and leave the
+// group (.Lr_cut at cut_off from .Lcb); otherwise it falls through (2 SALU).  Cls <= 64.
+void cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out);
+
 // The drain code (entered at ebpf_jit_area + 0): run the first queue holding a batch (>= 64
 // entries, or any with s7 bit 8) through .Lr_batch (batch_off) and its point's code (resume[q]),
 // or return to the kernel (drain_ret_off) when none does.

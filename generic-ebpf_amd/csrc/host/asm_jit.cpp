@@ -34,7 +34,7 @@ enum jt_index {
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
 	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE, JT_RBATCH,
-	JT_SCHED, JT_DRAINRET, JT_AREA, JT_AREA_BYTES,
+	JT_SCHED, JT_DRAINRET, JT_CUT, JT_AREA, JT_AREA_BYTES,
 	JT_COUNT
 };
 
@@ -210,10 +210,12 @@ asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-	     uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes)
+	     uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes, uint32_t *win_cuts)
 {
 	if (rq_wave_bytes)
 		*rq_wave_bytes = 0;
+	if (win_cuts)
+		*win_cuts = 0;
 	const uint32_t HDR = 16;
 	// mode 2 (span-staged general launches) compiles as mode 0 but for its packet loads (asm_cc)
 	const int gm = mode == 2 ? 0 : mode;
@@ -340,6 +342,20 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		}
 		if (rq_wave_bytes)
 			*rq_wave_bytes = (uint32_t)rg.size() * qbytes;
+	}
+	// window launches (mode 2, the span image; gen_interp.py "Window mode"): the cut points of
+	// phase A, class q + 1 at cut q, each block headed by its cut code (an entry point: the
+	// lanes that leave there end its hoisted-load run)
+	if (mode == 2 && getenv("EBPF_WINDOW_NOCUT") == nullptr) {
+		std::vector<uint32_t> cuts;
+		cc_pathsort_plan(xl, low, order, kPathMaxCuts, cuts);
+		for (size_t q = 0; q < cuts.size(); q++) {
+			const uint32_t e = cuts[q];
+			entry_point[e] = 1;
+			cc_cut_code((uint32_t)q + 1, T[JT_CUT], push[e]);
+		}
+		if (win_cuts)
+			*win_cuts = (uint32_t)cuts.size();
 	}
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
@@ -719,10 +735,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 int
 asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-	      uint32_t *rq_wave_bytes)
+	      uint32_t *rq_wave_bytes, uint32_t *win_cuts)
 {
 	std::vector<unsigned char> img;
-	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, rq_wave_bytes);
+	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, rq_wave_bytes, win_cuts);
 	if (e)
 		return e;
 	if (hipSetDevice(device) != hipSuccess)

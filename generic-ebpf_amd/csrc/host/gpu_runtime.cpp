@@ -37,13 +37,14 @@ int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vec
 // asm_jit.cpp
 int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-		  uint32_t *rq_wave_bytes);
+		  uint32_t *rq_wave_bytes, uint32_t *win_cuts = nullptr);
 void asm_jit_release(void *mod);
 int asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint32_t max_cuts,
 			dprog_host *prefix, uint32_t *ncuts, std::string *err);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-		 uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes = nullptr);
+		 uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes = nullptr,
+		 uint32_t *win_cuts = nullptr);
 
 
 namespace {
@@ -632,7 +633,8 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	std::string msg;
 	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
-				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_rq_bytes[mode]);
+				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_rq_bytes[mode],
+				&dp->jit_cuts[mode]);
 	dp->build_ms[mode] =
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
@@ -968,6 +970,83 @@ launch_pathsorted(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hi
 	return 0;
 }
 
+// Window launch of a large batch (offsets form) of a compiled program that reads past the
+// packets' first 64 bytes (gen_interp.py "Window mode"): the span image walks each workgroup's
+// share of the batch in windows of up to 256 packets staged in LDS as one contiguous DMA, runs
+// every packet to its exit or to the head of a heavy subtree (a cut point, asm_jit.cpp), sorts
+// the cut packets by subtree in LDS and runs them again from the start 64 per group, so a group
+// takes one subtree.  The packets that cannot open a window (not 16-B aligned, longer than a
+// window) are listed on the device and run next on the general kernels (slot mode), so every
+// packet keeps its own result, fault byte and verdict.  No map writes (a rerun packet must see
+// what it saw the first time; maps are read-only during a batch).
+constexpr uint64_t kWinMin = 1u << 14;     // smaller batches: one plain launch
+constexpr bool kWindowDefault = false;     // opt-in (EBPF_WINDOW=1) until measured
+constexpr uint64_t kWinMax = 1u << 28;     // (one chunk of launch_interp_asm)
+
+bool
+window_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
+{
+	// (EBPF_WINDOW=0 / 1: force off / on whatever the batch; EBPF_WINDOW_MINBATCH=n: the
+	// smallest batch that is windowed, for tests)
+	const char *on = getenv("EBPF_WINDOW");
+	if (on && *on == '0')
+		return false;
+	uint64_t min = kWinMin;
+	if (const char *m = getenv("EBPF_WINDOW_MINBATCH"))
+		min = strtoull(m, nullptr, 0);
+	// (the staged copy is not written back: no store that may reach the packet)
+	const bool fits = L.offsets != nullptr && L.count >= min && L.count <= kWinMax &&
+			  !ep->xlated->asm_needs_general && !prog_writes_maps(*ep->xlated) &&
+			  dp->jit_rq_bytes[0] == 0;
+	if (on && *on == '1')
+		return fits;
+	return fits && ep->xlated->asm_span && kWindowDefault;
+}
+
+int
+launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
+		hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
+		bool *done)
+{
+	*done = false;
+	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 || dp->jit_rq_bytes[0] != 0)
+		return 0; // (no span code for this program: the plain launch)
+	const size_t ovf_bytes = (8 + 4 * (size_t)L.count + 255) & ~(size_t)255;
+	uint8_t *ovf;
+	int err = bk_acquire(dp->device, stream, ovf_bytes, &ovf);
+	if (err)
+		return fail(err, "window overflow list");
+	hipError_t e;
+	if ((e = hipMemsetAsync(ovf, 0, 8, stream)) != hipSuccess)
+		return hip_fail(e, "hipMemsetAsync(window overflow)");
+	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	dp_launch Lw = L;
+	Lw.win_ovf = reinterpret_cast<uint32_t *>(ovf);
+	Lw.stack_stride = dp->jit_stride[2];
+	Lw.win_bytes = 1; // (launch_interp_asm sizes the window)
+	e = launch_interp_asm(Lw, stream, dp->device, 2, dp->map_lds_bytes, dp->jit_fn[2], 0, nullptr,
+			      nullptr, user_hist, overwrite);
+	if (e != hipSuccess)
+		return hip_fail(e, "window launch");
+	dp_launch Lo = L;
+	Lo.perm = reinterpret_cast<const uint32_t *>(ovf) + 2;
+	Lo.perm_cls = reinterpret_cast<const uint32_t *>(ovf);
+	Lo.span_slot = 0;
+	Lo.span_g = 64;
+	Lo.span_magic_g = (uint32_t)((0x100000000ull + 63) / 64);
+	Lo.stack_stride = dp->jit_stride[0];
+	e = launch_interp_asm(Lo, stream, dp->device, 0, dp->map_lds_bytes, dp->jit_fn[0], 0, nullptr,
+			      nullptr, user_hist, false);
+	if (e != hipSuccess)
+		return hip_fail(e, "window overflow launch");
+	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
+		return hip_fail(e, "hipEventRecord");
+	dp->last_layout = 4;
+	*done = true;
+	return 0;
+}
+
 // A shard's write log brought to the host (a batch whose shards ran on several devices: the
 // logs are merged there, in global packet order).  Records as on the device (map_writes.h);
 // `first` = the global index of the shard's packet 0.
@@ -1262,7 +1341,11 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
 		bool done = false;
-		if (fn && mode == 0 && bucket_wanted(ep, dp, L) &&
+		if (fn && mode == 0 && window_wanted(ep, dp, L) &&
+		    (err = launch_windowed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
+					   &done)))
+			return err;
+		if (!done && fn && mode == 0 && bucket_wanted(ep, dp, L) &&
 		    (err = launch_bucketed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
 					   &done)))
 			return err;

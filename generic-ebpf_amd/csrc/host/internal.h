@@ -153,6 +153,7 @@ struct dprog_device {
 	void *jit_fn[kModes] = {};               // its kernel
 	uint32_t jit_stride[kModes] = {};
 	uint32_t jit_rq_bytes[kModes] = {};      // regroup queue bytes per wave (0: none)
+	uint32_t jit_cuts[kModes] = {};          // mode 2: the window launches' cut points
 	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
 	// path-sorted launches (gpu_runtime.cpp launch_pathsorted): the classifying prefix, compiled
 	// for the general kernels (asm_pathsort_prefix), built on first use
