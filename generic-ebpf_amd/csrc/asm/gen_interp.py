@@ -2246,7 +2246,7 @@ def kernel(name, staged, jit=False):
               "s_waitcnt lgkmcnt(0)",
               "s_cmp_eq_u32 s80, 0",
               "s_cbranch_scc1 .L%s_nowin" % k,
-              "s_or_b32 s7, s7, 2048",
+              "s_or_b32 s7, s7, 0xc00",     # (bit 10 too: the packets are in LDS)
               ".L%s_nowin:" % k]
     L += ["s_branch .Lprologue"]
     return L
