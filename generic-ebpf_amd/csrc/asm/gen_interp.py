@@ -169,7 +169,11 @@ SPAN_HOIST_REGS = int(os.environ.get("EBPF_ASM_SPANHOIST", "48"))
 # Packets are LDS-aperture pointers throughout (their loads LDS reads).  A packet that cannot
 # open a window (unaligned, or longer than win_bytes) goes to dp_launch.win_ovf (a slot list the
 # general kernels run next).  No map writes (the host only windows programs without them).
-S_WP, S_WHI, S_WC = 76, 77, 78   # window's first packet; the workgroup's end; phase C count
+# (s[74:77] are the compiled program's short-lane and run masks: window state lives above them,
+# and the span image declares s0..s95)
+S_WC = 78            # phase C: the window's cut packets
+S_WP, S_WHI = 88, 89 # the window's first packet; the workgroup's end
+NSGPR_SPAN = 96
 S_WB, S_WG, S_WARR, S_WN = 80, 81, 82, 83   # window bytes; phase C group; LDS arrays; window count
 S_WDEF = 84          # s[84:85] lanes of the running group that reached a cut point
 S_GINIT = 86         # s[86:87] lanes the running group started with
@@ -3453,7 +3457,7 @@ def generate(out_s, staged_image):
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
     kernarg = 232
-    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
+    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_SPAN if SPAN_IMAGE else NSGPR_GEN
     if INTERP_IMAGE:
         # the interpreter kernel declares s0..s73 only: check that the image's code uses no more
         top = 0
