@@ -29,6 +29,7 @@ hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device,
 			     bool hist_overwrite);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
+bool asm_window_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_program_needs_general(const dprog_host &xl);
 bool asm_program_gstage(const dprog_host &xl);
 bool asm_program_span(const dprog_host &xl);
@@ -1009,8 +1010,9 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 		bool *done)
 {
 	*done = false;
-	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 || dp->jit_rq_bytes[0] != 0)
-		return 0; // (no span code for this program: the plain launch)
+	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 || dp->jit_rq_bytes[0] != 0 ||
+	    !asm_window_fits(dp->map_lds_bytes, dp->jit_stride[2]))
+		return 0; // (no span code for this program, or no room for a window: the plain launch)
 	const size_t ovf_bytes = (8 + 4 * (size_t)L.count + 255) & ~(size_t)255;
 	uint8_t *ovf;
 	int err = bk_acquire(dp->device, stream, ovf_bytes, &ovf);

@@ -109,6 +109,8 @@ constexpr uint32_t kHistLds = 1024; // bins 0..255 (bin 256 is counted in global
 constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
+// window launches: the smallest window worth staging (gen_interp.py "Window mode")
+constexpr uint32_t kWinMinBytes = 4096;
 
 // The assembly interpreter's code objects (build/asm_image.cpp): mode 1 = staged 64-B kernels,
 // mode 0 = general kernels, mode 2 = general kernels of span-staged (length-bucketed) launches,
