@@ -276,11 +276,14 @@ class _Gen:
 
 
 def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None, writes=False,
-                   vstores=False):
+                   vstores=False, pkt_stores=True):
     """writes: half the map helper calls are map_update_elem / map_delete_elem (the device
     batch semantics: ebpf_gpu.h "Map writes in a device batch"); vstores: every lookup hit
-    stores into the value first (ebpf_gpu.h "Stores into map values")."""
+    stores into the value first (ebpf_gpu.h "Stores into map values"); pkt_stores=False: packet
+    loads where stores into the packet would be (programs the window launches take)."""
     gen = _Gen(seed, nmaps, map_value_size, writes, vstores)
+    if not pkt_stores:
+        gen.pkt_store = gen.ldx_pkt
     nodes = gen.prologue() + gen.block(length) + gen.epilogue()
     rs = reset_stride if reset_stride is not None else int(gen.g.integers(3, 12))
     return assemble(nodes, reset_stride=rs)

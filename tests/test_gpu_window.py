@@ -134,7 +134,8 @@ def test_window_off_is_plain(gpu, env, monkeypatch):
 def test_window_random_programs(gpu, env, monkeypatch):
     """Random stepping-aware programs with two array maps (lookups, stack traffic, every ALU and
     jump quirk) on packets of random sizes, 16-B aligned or not, with the cut threshold at 2
-    entries and the batch threshold at 1 packet: cut points anywhere in the trees."""
+    entries and the batch threshold at 1 packet: cut points anywhere in the trees.  Every fourth
+    program stores into its packets (no window: the plain launch)."""
     from generic_ebpf_amd import randprog
     monkeypatch.setenv("EBPF_PATHSORT_MIN", "2")
     monkeypatch.setenv("EBPF_WINDOW_MINBATCH", "1")
@@ -142,7 +143,7 @@ def test_window_random_programs(gpu, env, monkeypatch):
     for k in range(60):
         g = np.random.default_rng(6000 + k)
         lay = randprog.random_program(78000 + k, length=int(g.integers(20, 120)), nmaps=2,
-                                      map_value_size=8)
+                                      map_value_size=8, pkt_stores=k % 4 == 3)
         maps = [(8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes()) for _ in range(2)]
         n = int(g.choice([1, 63, 64, 65, 257, 777, 3000]))
         sizes = g.integers(16, 200, n).astype(np.uint64)
