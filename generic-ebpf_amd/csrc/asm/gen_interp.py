@@ -1810,7 +1810,10 @@ def routines():
           "v_cmp_lt_u64_e64 vcc, v[0:1], %s" % vp(R[8]),
           "v_cndmask_b32 %s, %s, v0, vcc" % (v(R[8]), v(R[8])),
           # one LDS atomic per wave when every exiting lane has the same verdict (the usual
-          # case); per-lane adds to one address would serialise
+          # case); per-lane adds to one address would serialise.  (s_nop: a VALU write, then
+          # v_readfirstlane of it, needs one wait state; without it the read can see the
+          # previous value and every exit took the per-lane path)
+          "s_nop 0",
           "v_readfirstlane_b32 %s, %s" % (s(S_BYTES), v(R[8])),
           "v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_MASK), s(S_BYTES), v(R[8])),
           "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
@@ -2366,6 +2369,42 @@ def span_stage(tag):
             "s_branch .Lps_done_%s" % tag]
 
 
+def window_debug():
+    """(diagnostics, dp_launch.win_pad bit 0; wave 0 after B5 of the workgroup's first window)
+    the window's classes, W, the cut count, s7 and the class counts (v0..v15) into the words
+    after the overflow list (win_ovf + 8 + 4 * count): cls[0..63], W, WC, s7, cnt[0..15]."""
+    return ["s_load_dword s64, s[0:1], 0xdc",
+            "s_waitcnt lgkmcnt(0)",
+            "s_bitcmp1_b32 s64, 0",
+            "s_cbranch_scc0 .Lwin_dbg_end",
+            "s_cmp_eq_u32 s2, 0",
+            "s_cbranch_scc0 .Lwin_dbg_end",
+            "s_load_dwordx2 s[64:65], s[0:1], 0xe0",
+            "s_waitcnt lgkmcnt(0)",
+            "s_lshl_b32 s66, %s, 2" % s(S_COUNT),
+            "s_add_u32 s66, s66, 8",
+            "s_add_u32 s64, s64, s66",
+            "s_addc_u32 s65, s65, 0",
+            "s_mov_b64 exec, -1"] + lane_index(H[0]) + [
+            "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[0])),
+            "v_add_u32 %s, %s, %s" % (v(H[3]), s(S_WARR), v(H[2])),
+            "ds_read_b32 %s, %s offset:%d" % (v(R[0]), v(H[3]), W_CLS),
+            "s_waitcnt lgkmcnt(0)",
+            "global_store_dword %s, %s, s[64:65]" % (v(H[2]), v(R[0])),
+            "s_mov_b64 exec, 1",
+            "v_mov_b32 %s, 0" % v(H[2]),
+            "v_mov_b32 %s, %s" % (v(R[0]), s(S_WN)),
+            "global_store_dword %s, %s, s[64:65] offset:256" % (v(H[2]), v(R[0])),
+            "v_mov_b32 %s, %s" % (v(R[0]), s(S_WC)),
+            "global_store_dword %s, %s, s[64:65] offset:260" % (v(H[2]), v(R[0])),
+            "v_mov_b32 %s, s7" % v(R[0]),
+            "global_store_dword %s, %s, s[64:65] offset:264" % (v(H[2]), v(R[0]))] + [
+            "global_store_dword %s, v%d, s[64:65] offset:%d" % (v(H[2]), k, 268 + 4 * k)
+            for k in range(16)] + [
+            "s_waitcnt vmcnt(0)",
+            ".Lwin_dbg_end:"]
+
+
 def window_code():
     """Window mode (span image, s7 bit 11; see "Window mode" at the top).  Entered by every wave
     of the workgroup after the prologue; ends at .Lfinish.  Six workgroup barriers per window:
@@ -2587,7 +2626,8 @@ def window_code():
               "v_cndmask_b32 v18, 0, v%d, vcc" % k,
               "v_add_u32 v16, v16, v18",
               "v_add_u32 v17, v17, v%d" % k]
-    L += ["v_readfirstlane_b32 %s, v17" % s(S_WC),
+    L += ["s_nop 0",                  # (a VALU write, then v_readfirstlane of it: 1 wait state)
+          "v_readfirstlane_b32 %s, v17" % s(S_WC),
           "s_mov_b64 exec, %s" % sp(S_SAVE),
           "s_cbranch_execz .Lwin_b_noperm",
           "v_add_u32 v16, v16, %s" % v(R[3]),
@@ -2600,7 +2640,8 @@ def window_code():
           "s_barrier",                                                    # B5
           # wave 0 re-arms the class counts (every wave read them before B5)
           "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lwin_c",
+          "s_cbranch_scc0 .Lwin_c"] + window_debug() + [
+          "s_mov_b64 exec, -1"] + tid_code() + [
           "v_cmp_gt_u32_e64 vcc, 16, %s" % v(tid),
           "s_mov_b64 exec, vcc"] + arr_addr(H[2], tid) + [
           "v_mov_b32 %s, 0" % v(H[3]),

@@ -1013,7 +1013,8 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 || dp->jit_rq_bytes[0] != 0 ||
 	    !asm_window_fits(dp->map_lds_bytes, dp->jit_stride[2]))
 		return 0; // (no span code for this program, or no room for a window: the plain launch)
-	const size_t ovf_bytes = (8 + 4 * (size_t)L.count + 255) & ~(size_t)255;
+	// (+ 512 bytes: EBPF_WIN_DEBUG's record after the list, gen_interp.py window_debug)
+	const size_t ovf_bytes = (8 + 4 * (size_t)L.count + 512 + 255) & ~(size_t)255;
 	uint8_t *ovf;
 	int err = bk_acquire(dp->device, stream, ovf_bytes, &ovf);
 	if (err)
@@ -1027,6 +1028,8 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 	Lw.win_ovf = reinterpret_cast<uint32_t *>(ovf);
 	Lw.stack_stride = dp->jit_stride[2];
 	Lw.win_bytes = 1; // (launch_interp_asm sizes the window)
+	static const bool dbg = getenv("EBPF_WIN_DEBUG") != nullptr;
+	Lw.win_pad = dbg ? 1u : 0u;
 	e = launch_interp_asm(Lw, stream, dp->device, 2, dp->map_lds_bytes, dp->jit_fn[2], 0, nullptr,
 			      nullptr, user_hist, overwrite);
 	if (e != hipSuccess)
@@ -1044,6 +1047,18 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 		return hip_fail(e, "window overflow launch");
 	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
 		return hip_fail(e, "hipEventRecord");
+	if (dbg) {
+		uint32_t rec[64 + 3 + 16];
+		hipStreamSynchronize(stream);
+		hipMemcpy(rec, ovf + 8 + 4 * L.count, sizeof(rec), hipMemcpyDeviceToHost);
+		fprintf(stderr, "window dbg: W %u WC %u s7 %#x cnt", rec[64], rec[65], rec[66]);
+		for (int k = 0; k < 16; k++)
+			fprintf(stderr, " %u", rec[67 + k]);
+		fprintf(stderr, "\n  cls");
+		for (int k = 0; k < 64; k++)
+			fprintf(stderr, " %u", rec[k]);
+		fprintf(stderr, "\n");
+	}
 	dp->last_layout = 4;
 	*done = true;
 	return 0;

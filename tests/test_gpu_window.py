@@ -36,6 +36,23 @@ def _check(gpu, env, lay, data, offs, n, relocs=(), maps=()):
         d = np.ascontiguousarray(data.copy())
         ret, faults, st = p.run_batch(d, n, 0, offs)
         layout = p.exec_info(0)[1]
+        # device-resident, results and fault bytes pre-filled with sentinels: a packet whose
+        # result is never stored cannot pass on what an earlier batch left in a pooled buffer
+        if n:
+            import torch
+            dev = torch.device("cuda:0")
+            d_pk = torch.from_numpy(np.ascontiguousarray(data)).to(dev)
+            d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+            d_ret = torch.full((n,), 0x5eed, dtype=torch.int64, device=dev)
+            d_flt = torch.full((n,), 77, dtype=torch.uint8, device=dev)
+            d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 0, d_ret.data_ptr(), d_off.data_ptr(),
+                            d_flt.data_ptr(), d_hist.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                            hist_overwrite=True)
+            torch.cuda.synchronize()
+            dev_ret = d_ret.cpu().numpy().view(np.uint64)
+            dev_flt = d_flt.cpu().numpy()
+            dev_hist = d_hist.cpu().numpy()
     finally:
         p.destroy()
         for m in mp:
@@ -45,6 +62,10 @@ def _check(gpu, env, lay, data, offs, n, relocs=(), maps=()):
     np.testing.assert_array_equal(d, wdata)
     bins = np.where(wf != 0, 256, np.minimum(want, 255)).astype(np.int64)
     np.testing.assert_array_equal(np.array(st.hist[:], dtype=np.int64), np.bincount(bins, minlength=257))
+    if n:
+        np.testing.assert_array_equal(dev_flt, wf)
+        np.testing.assert_array_equal(dev_ret, want)
+        np.testing.assert_array_equal(dev_hist, np.bincount(bins, minlength=257))
     return layout
 
 
