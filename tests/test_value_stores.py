@@ -282,7 +282,7 @@ def test_one_packet_batch_equals_cpu_run(gpu, env, variant, case):
         m.fill(init)
         p = gpu.Prog(env, gpu.patch_relocs(lay.code, lay.relocs, [m.handle]))
         try:
-            r = p.run_cpu(np.ascontiguousarray(pk[0]))
+            r = p.run_cpu(np.ascontiguousarray(pk[0]))[0]
             cpu_after = b"".join(m.lookup(k)[1] for k in range(vp.NKEYS))
         finally:
             p.destroy()
