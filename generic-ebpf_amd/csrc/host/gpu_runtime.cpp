@@ -30,6 +30,7 @@ hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device,
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
 bool asm_window_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
+bool asm_lds_fits(int mode, uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_program_needs_general(const dprog_host &xl);
 bool asm_program_gstage(const dprog_host &xl);
 bool asm_program_span(const dprog_host &xl);
@@ -1310,16 +1311,31 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		L.upd_faulted = P.faulted;
 	}
 	const int variant = effective_variant(dp->device);
+	const int mode = (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
+	// the assembly kernels keep 256 lanes' stack slices in LDS: a program whose slice (stack
+	// depth, loop count, value-store overlay) leaves them no room runs on the portable HIP
+	// interpreter instead (its stack is per-thread memory)
+	bool asm_fits = true;
 	if (variant == 0 || variant == 2) {
-		const int mode =
-		    (L.offsets == nullptr && L.stride == 64 && !ep->xlated->asm_needs_general) ? 1 : 0;
+		const bool compile = variant == 0;
+		if (compile && (err = jit_entries(ep, dp, mode)) == 0) {
+			asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, dp->jit_stride[mode]);
+		} else {
+			if (compile && err != E2BIG)
+				return err;
+			if ((err = asm_entries(ep, dp, mode)))
+				return err;
+			asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, dp->asm_stride[mode]);
+		}
+	}
+	if ((variant == 0 || variant == 2) && asm_fits) {
 		// variant 0: the compiled program; a program too large for the code area runs on the
 		// assembly interpreter instead (still the device path).  Programs with loops compile
 		// too: the code generator keeps facts and liveness only across single-predecessor
 		// edges, and a loop head (an entry point, >= 2 predecessors) starts from nothing known
 		void *fn = nullptr;
 		const bool compile = variant == 0;
-		if (compile && (err = jit_entries(ep, dp, mode)) == 0) {
+		if (compile && dp->jit_fn[mode]) {
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];
 			fn = dp->jit_fn[mode];
@@ -1330,10 +1346,6 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 				L.rq_wave_bytes = dp->jit_rq_bytes[mode];
 			}
 		} else {
-			if (compile && err != E2BIG)
-				return err;
-			if ((err = asm_entries(ep, dp, mode)))
-				return err;
 			L.prog = dp->d_asm[mode];
 			L.stack_stride = dp->asm_stride[mode];
 		}
