@@ -44,8 +44,7 @@ V_LEN = 40           # packet length (bytes)
 V_T = 41             # parked entry byte offset
 V_STK = 42           # lane stack bottom (LDS byte address)
 V_L16 = 43           # staged image: lane * 16 (LDS-DMA staging offset)
-V_IDX = 43           # general image: the lane's packet index in the launch (its group's, or in
-                     # a regrouped batch the queued packet's; see "Regrouping" below)
+V_IDX = 43           # general image: the lane's packet index in the launch
 # v[44:45] (RETK == 1) or v[64:64+2*RETK]: r0 of the lanes that retired, per group of the
 # current superblock (stored together at the start of the next superblock)
 H = [46, 47, 48, 49, 50, 51]         # handler temporaries
@@ -107,21 +106,10 @@ S_KMASK = 73         # superblock size - 1 of this launch (K' <= RETK, a power o
 S_WAVE = 3
 NSGPR = 76           # + VCC, XNACK, FLAT_SCRATCH; s[74:75]: compiled programs' short-lane mask
                      # in the general image (asm_cc.cpp ldxpkc_general)
-# Regrouping (general image, compiled programs; asm_jit.cpp regroup plan).  Lanes that reach the
-# head of a heavy subtree the compiler chose (a "regroup point", at most RQ_MAX) do not run it
-# with the group: they push (packet index, live registers) onto that point's queue, a ring of 128
-# entries in the wave's slice of dp_launch.rq_buf, and leave the group.  After each group the
-# compiled program's drain code runs every queue holding >= 64 entries as a batch of 64 lanes
-# that all take the same subtree (at the end of the wave's groups: every non-empty queue), so a
-# divergent program runs each heavy path with full waves instead of once per group with a few
-# lanes.  Queue q: u32 packet index [128] at +0, then live register k: u64 [128] at +512 + 1024k.
-S_DEFER = 76         # s[76:77] lanes of the running group that were queued (no result stored)
-S_QBASE = 78         # s[78:79] this wave's queue slice
-S_BMASK = 80         # s[80:81] lanes of the running batch
-S_QS = 82            # s82..s87: queue states, two per SGPR (bits 0-6 tail, 8-15 count; +16 odd q)
-RQ_MAX = 12
-NSGPR_GEN = S_QS + RQ_MAX // 2
-# s7 flags of regrouping: bit 6 queues active, bit 7 a batch is running, bit 8 final drain
+# general image: s[76:77] = the run mask of a compiled program's hoisted packet loads (asm_cc.cpp
+# runmask: the running lanes whose packet holds every load of the run)
+S_RUNMASK = 76
+NSGPR_GEN = 88
 # staged image: s[74:75] .. s[96:97] hold the taken-lane masks of a structured compiled program's
 # pending branches (asm_jit.cpp; 12 levels); 98 SGPRs still allow the image's 6 waves per SIMD
 S_JOIN = 74
@@ -130,30 +118,23 @@ NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
 # general image with the join SGPRs too (structured compiled programs in the general kernels;
 # 98 SGPRs allow 7 instead of 8 waves per SIMD there)
 GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
-# (the join SGPRs s74..s97 would overlap the regroup SGPRs, and structured exits address the LDS
-# histogram through lane 0 of v43, which the general image uses for V_IDX)
-assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with regrouping (S_DEFER..) and V_IDX"
+# (the join SGPRs s74..s97 would overlap the run mask and the slot SGPRs, and structured exits
+# address the LDS histogram through lane 0 of v43, which the general image uses for V_IDX)
+assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with the run mask and V_IDX"
 # general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
 # hoist plan); 16 cost the general kernels 8 -> 6 waves per SIMD
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
 # A/B: XCD-major logical workgroup order (common_group_code)
 XCD_MAJOR = os.environ.get("EBPF_ASM_XCD") == "1"
-# Length-bucketed launches (general image; dp_launch.perm, gpu_runtime.cpp bucketing).  A launch
-# runs one length class of a batch: its slots are perm[start .. start + n) (packet indices,
-# bucket.hip), G per group (G <= 64 lanes; the rest idle).  These SGPRs share s78..s83 with the
-# regroup queues: the host never combines the two (a regrouping program is not bucketed).
+# Slot mode (general image; dp_launch.perm, s7 bit 9: a window launch's overflow list).  The
+# launch's slots are perm[start .. start + n) (packet indices on the device), G per group.
 S_PERM = 78          # s[78:79] this launch's slots (perm + start); 0 = slot i is packet i
-S_SPAN = 80          # span image: bytes of LDS per lane slot (dp_launch.span_slot, a multiple of
-                     # 16 with an odd number of 16-B blocks: ds_read_b128 at one offset is
-                     # conflict-free), 0 = no span staging
-S_G = 81             # packets per group (64 unless the slots are large)
-S_NSLOT = 82         # slots in this launch (the class's packet count)
-S_MAGN = 83          # (spare)
-# Span image (the third code object, interp_m2): every packet of a group is DMA'd whole into the
-# wave's slice of LDS before the program runs (one LDS-DMA per packet, 16 B per lane), and its
-# packet pointer is the slot's LDS-aperture address: constant-offset packet loads become LDS
-# reads (the compiler's b128 hoisted loads, asm_cc.cpp mode 2) instead of per-lane gathers of
-# 64 distinct lines each.  Bigger hoist ring: the launch is LDS-bound to one workgroup per CU.
+S_G = 81             # packets per group (64)
+S_NSLOT = 82         # slots in this launch
+# Span image (the third code object, interp_m2; window launches): packets sit in LDS (s7 bit
+# 10), so the packet pointer is an LDS-aperture address and constant-offset packet loads are LDS
+# reads (the compiler's b128 hoisted loads, asm_cc.cpp mode 2).  Bigger hoist ring: the launch
+# is LDS-bound to a few workgroups per CU.
 SPAN_IMAGE = False
 SPAN_HOIST_REGS = int(os.environ.get("EBPF_ASM_SPANHOIST", "48"))
 # Window mode (span image, dp_launch.win_bytes != 0; gpu_runtime.cpp launch_windowed).  A
@@ -2101,34 +2082,6 @@ def routines():
     # the S_T0 bytes at H[0:1] just read into H[2:3]
     L += [".Lr_ovlfix:"] + ovl_fix("L", (H[2], H[3])) + ["s_setpc_b64 %s" % sp(S_LINK)]
     if not STAGED_IMAGE:
-        # BATCH (regrouping; called by the compiled drain code): make the first n = S_T1 lanes the
-        # running batch of the queue at s[64:65] from ring slot head = S_T2 on: their packet
-        # indices (V_IDX), packet address / length and staged header; s7 bit 7 set.  Returns with
-        # exec = S_ALIVE = S_BMASK = the batch and H[2] = each lane's slot * 8 (the compiled code
-        # then loads the live registers: +512 + 1024k).  The wait first: the pushes (and this
-        # wave's earlier result and fault stores) have landed before a batch reads or rewrites.
-        L += [".Lr_batch:",
-              "s_waitcnt vmcnt(0)",
-              "s_bfm_b64 %s, %s, 0" % (sp(S_BMASK), s(S_T1)),
-              "s_cmp_eq_u32 %s, 64" % s(S_T1),
-              "s_cselect_b64 %s, -1, %s" % (sp(S_BMASK), sp(S_BMASK)),
-              "s_mov_b64 exec, %s" % sp(S_BMASK),
-              "s_mov_b64 %s, %s" % (sp(S_ALIVE), sp(S_BMASK)),
-              "s_or_b32 s7, s7, 128"] + lane_index(H[0]) + [
-              "v_add_u32 %s, %s, %s" % (v(H[0]), s(S_T2), v(H[0])),
-              "v_and_b32 %s, 0x7f, %s" % (v(H[0]), v(H[0])),
-              "v_lshlrev_b32 %s, 2, %s" % (v(H[1]), v(H[0])),
-              "v_lshlrev_b32 %s, 3, %s" % (v(H[2]), v(H[0])),
-              "global_load_dword v%d, %s, s[64:65]" % (V_IDX, v(H[1])),
-              "s_waitcnt vmcnt(0)",
-              # (defensive: a lane whose index is not a packet of this launch drops out rather
-              # than reading outside the batch)
-              "v_cmp_gt_u32_e64 vcc, %s, v%d" % (s(S_COUNT), V_IDX),
-              "s_and_b64 %s, %s, vcc" % (sp(S_BMASK), sp(S_BMASK)),
-              "s_mov_b64 exec, %s" % sp(S_BMASK),
-              "s_mov_b64 %s, %s" % (sp(S_ALIVE), sp(S_BMASK))] + pkt_setup(V_IDX, "b") + [
-              "s_setpc_b64 %s" % sp(S_LINK)]
-    if not STAGED_IMAGE:
         # CUT (window launches, phase A; entered by a cut point's code with S_CODE = its class):
         # the running lanes record the class of their window slot and leave the group
         L += [".Lr_cut:",
@@ -2204,30 +2157,12 @@ def kernel(name, staged, jit=False):
               "s_cbranch_scc0 .L%s_nogs" % k,
               "s_or_b32 s7, s7, 8",
               ".L%s_nogs:" % k]
-    if not staged and jit and not STAGED_IMAGE:
-        # regroup queues (dp_launch.rq_buf != 0): this wave's slice, empty queues
-        L += ["s_load_dwordx2 %s, s[0:1], 0x98" % sp(S_QBASE),
-              "s_load_dword %s, s[0:1], 0xa0" % s(S_BMASK),
-              "s_mov_b64 %s, 0" % sp(S_DEFER)] + [
-              "s_mov_b64 %s, 0" % sp(S_QS + 2 * i) for i in range(RQ_MAX // 4)] + [
-              "s_waitcnt lgkmcnt(0)",
-              "s_cmp_eq_u64 %s, 0" % sp(S_QBASE),
-              "s_cbranch_scc1 .L%s_norq" % k,
-              "s_lshl_b32 %s, s2, 2" % s(S_T0),
-              "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_WAVE)),
-              "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_BMASK)),
-              "s_add_u32 %s, %s, %s" % (s(S_QBASE), s(S_QBASE), s(S_T0)),
-              "s_addc_u32 %s, %s, 0" % (s(S_QBASE + 1), s(S_QBASE + 1)),
-              "s_or_b32 s7, s7, 64",
-              ".L%s_norq:" % k]
     if not staged and not STAGED_IMAGE:
-        # length-bucketed launch (dp_launch.perm != 0): s7 bit 9 = slot mode (this launch's slots
-        # are perm[start .. start + n), G per group), bit 10 = span staging (span image)
-        L += ["s_bitcmp1_b32 s7, 6",                 # (regrouping: s78.. hold the queues)
-              "s_cbranch_scc1 .L%s_noperm" % k,
-              "s_load_dwordx2 %s, s[0:1], 0xb0" % sp(S_PERM),
+        # slot launch (dp_launch.perm != 0): s7 bit 9 = slot mode (this launch's slots are
+        # perm[start .. start + n), G per group)
+        L += ["s_load_dwordx2 %s, s[0:1], 0xb0" % sp(S_PERM),
               "s_load_dwordx2 s[54:55], s[0:1], 0xb8",
-              "s_load_dwordx4 s[80:83], s[0:1], 0xc0",   # span_slot, G, magic(G), pad
+              "s_load_dwordx4 s[80:83], s[0:1], 0xc0",   # reserved, G, magic(G), pad
               "s_waitcnt lgkmcnt(0)",
               "s_cmp_eq_u64 %s, 0" % sp(S_PERM),
               "s_cbranch_scc1 .L%s_noperm" % k,
@@ -2243,9 +2178,6 @@ def kernel(name, staged, jit=False):
               "s_mul_hi_u32 s83, s83, s82",
               "s_mov_b32 %s, s55" % s(S_NSLOT),
               "s_or_b32 s7, s7, 512",
-              "s_cmp_eq_u32 %s, 0" % s(S_SPAN),
-              "s_cbranch_scc1 .L%s_noperm" % k,
-              "s_or_b32 s7, s7, 1024",
               ".L%s_noperm:" % k]
     if SPAN_IMAGE and jit:
         # window mode (dp_launch.win_bytes, win_chunk, win_arr at 0xd0): s7 bit 11
@@ -2270,8 +2202,7 @@ def lane_index(dst):
 
 
 def lane_pkt_index(dst):
-    """dst = the packet index of this lane in the launch (general image: V_IDX, which a
-    regrouped batch sets to the queued packet's)."""
+    """dst = the packet index of this lane in the launch (general image: V_IDX)."""
     if STAGED_IMAGE:
         return ["v_lshrrev_b32 %s, 4, v%d" % (v(dst), V_L16),
                 "v_lshl_add_u32 %s, %s, 6, %s" % (v(dst), s(S_GROUP), v(dst))]
@@ -2301,7 +2232,7 @@ def pkt_setup(idx, tag):
             "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
             "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),
             "v_lshl_add_u64 v[%d:%d], %s, 0, %s" % (V_PKT, V_PKT + 1, vp(H[4]), sp(S_DATA)),
-            ] + (span_stage(tag) if SPAN_IMAGE else []) + [
+            ] + [
             # header staging: the first 64 bytes of every packet at least that long into
             # v22..v37 (what the staged kernels' LDS DMA provides)
             ".Lps_stage_%s:" % tag,
@@ -2316,57 +2247,6 @@ def pkt_setup(idx, tag):
             "s_waitcnt vmcnt(0)",
             ".Lps_done_%s:" % tag,
             "s_mov_b64 exec, %s" % sp(S_MASK)]
-
-
-def span_stage(tag):
-    """Span image, s7 bit 10: the group's packets (16-B aligned, at most S_SPAN bytes: the host's
-    length class) are DMA'd whole into the wave's LDS slots, packet p at S_PKTLDS + p * S_SPAN,
-    one LDS-DMA of 16 B per lane per 1 KB of packet (coalesced: consecutive lanes, consecutive
-    bytes of one packet); then V_PKT = the slot's LDS-aperture address.  The last 16-B block of a
-    packet is read whole: an aligned block holding a packet byte never leaves its page.
-    Entered with exec = s[S_MASK] (the running lanes, V_PKT / V_LEN set); clobbers R[3:5],
-    s[64:65], S_T1, S_T2, m0."""
-    return ["s_bitcmp1_b32 s7, 10",
-            "s_cbranch_scc0 .Lps_stage_%s" % tag,
-            "v_add_u32 %s, 15, v%d" % (v(R[3]), V_LEN),
-            "v_lshrrev_b32 %s, 4, %s" % (v(R[3]), v(R[3])),       # 16-B blocks of the lane's packet
-            "s_not_b64 exec, %s" % sp(S_MASK),
-            "v_mov_b32 %s, 0" % v(R[3]),
-            "s_mov_b64 exec, -1",
-            "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(R[5]),
-            "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(R[5]), v(R[5])),
-            "v_lshlrev_b32 %s, 4, %s" % (v(R[4]), v(R[5])),
-            "s_mov_b32 %s, 0" % s(S_T1),
-            "s_mov_b32 m0, %s" % s(S_PKTLDS),
-            ".Lsp_loop_%s:" % tag,
-            "v_readlane_b32 s64, v%d, %s" % (V_PKT, s(S_T1)),
-            "v_readlane_b32 s65, v%d, %s" % (V_PKT + 1, s(S_T1)),
-            "v_readlane_b32 %s, %s, %s" % (s(S_T2), v(R[3]), s(S_T1)),
-            "s_nop 4",                        # (VALU-written SGPRs read by a memory instruction)
-            "s_cmp_eq_u32 %s, 0" % s(S_T2),
-            "s_cbranch_scc1 .Lsp_next_%s" % tag,
-            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T2), v(R[5])),
-            "s_mov_b64 exec, vcc",
-            "global_load_lds_dwordx4 %s, s[64:65] offset:0%s" % (v(R[4]), LD_POLICY),
-            "s_sub_u32 %s, %s, 64" % (s(S_T2), s(S_T2)),
-            "s_cmp_le_i32 %s, 0" % s(S_T2),
-            "s_cbranch_scc1 .Lsp_one_%s" % tag,
-            "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T2), v(R[5])),
-            "s_mov_b64 exec, vcc",
-            "global_load_lds_dwordx4 %s, s[64:65] offset:1024%s" % (v(R[4]), LD_POLICY),
-            ".Lsp_one_%s:" % tag,
-            "s_mov_b64 exec, -1",
-            ".Lsp_next_%s:" % tag,
-            "s_add_u32 m0, m0, %s" % s(S_SPAN),
-            "s_add_u32 %s, %s, 1" % (s(S_T1), s(S_T1)),
-            "s_cmp_lt_u32 %s, %s" % (s(S_T1), s(S_G)),
-            "s_cbranch_scc1 .Lsp_loop_%s" % tag,
-            "s_waitcnt vmcnt(0)",
-            "s_mov_b64 exec, %s" % sp(S_MASK),
-            "v_mul_u32_u24 %s, %s, %s" % (v(R[4]), s(S_SPAN), v(R[5])),
-            "v_add_u32 v%d, %s, %s" % (V_PKT, s(S_PKTLDS), v(R[4])),
-            "v_mov_b32 v%d, %s" % (V_PKT + 1, s(S_SHARED + 1)),
-            "s_branch .Lps_done_%s" % tag]
 
 
 def window_debug():
@@ -2860,13 +2740,6 @@ def common_group_code():
           "s_sub_u32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_KMASK)),
           # this wave's packet buffer (staged kernel); first group's prefetch
           "s_lshl_b32 %s, %s, 12" % (s(S_T0), s(S_WAVE)),
-          ] + ([] if STAGED_IMAGE else [
-          # (span staging: G slots of S_SPAN bytes per wave)
-          "s_bitcmp1_b32 s7, 10",
-          "s_cbranch_scc0 .Lpk_std",
-          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_G), s(S_SPAN)),
-          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_WAVE)),
-          ".Lpk_std:"]) + [
           "s_add_u32 %s, %s, %s" % (s(S_PKTLDS), s(S_PKTLDS), s(S_T0)),
           "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgroup_check",
@@ -2876,17 +2749,10 @@ def common_group_code():
     if SPAN_IMAGE:
         L += ["s_bitcmp1_b32 s7, 11",
               "s_cbranch_scc1 .Lwin_gdone"]
-    if not STAGED_IMAGE:
-        L += ["s_bitcmp1_b32 s7, 6",
-              "s_cbranch_scc1 .Lrg_done"]
     L += ["s_and_b32 %s, s7, 48" % s(S_BYTES),
           "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
           "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
-          ".Lgd_dma_ok:"] + slot_commit() + [
-          ".Ldrain_ret:"] + ([] if STAGED_IMAGE else [
-          # (the compiled drain code returns here when no queue holds a batch to run)
-          "s_bitcmp1_b32 s7, 8",
-          "s_cbranch_scc1 .Lfinish_body"]) + next_group(S_T0) + [
+          ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
@@ -2962,12 +2828,9 @@ def common_group_code():
           "s_mov_b64 exec, %s" % sp(S_ALIVE)] + pkt_setup(H[3], "g") + [
           ".Lgs_init:"] + store_prev_results("g", False) + [
           "s_mov_b32 %s, %s" % (s(S_PREVG), s(S_GROUP))] + ([] if STAGED_IMAGE else [
-          # V_IDX: this group's packet indices (after the previous group's store read them);
-          # with queues the group's results are stored when it is done, not here
+          # V_IDX: this group's packet indices (after the previous group's store read them)
           "s_mov_b64 exec, -1",
-          "v_mov_b32 v%d, v%d" % (V_IDX, H[3]),
-          "s_bitcmp1_b32 s7, 6",
-          "s_cselect_b32 %s, -1, %s" % (s(S_PREVG), s(S_PREVG))]) + [
+          "v_mov_b32 v%d, v%d" % (V_IDX, H[3])]) + [
           "s_mov_b64 exec, %s" % sp(S_ALIVE),
           # fault code 0 for the whole group up front (a faulting lane overwrites its byte)
           "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
@@ -2997,35 +2860,10 @@ def common_group_code():
     # histogram (stored, or added), then re-arms the ticket.  One kernel per launch: no
     # second-stage reduce (hand-off form: 8-B agent atomics on both sides, MI355X_MICROARCH.md
     # "Valid forms")
-    if not STAGED_IMAGE:
-        # Regrouping.  A group is done: store its results but the queued lanes', then let the
-        # compiled drain code (ebpf_jit_area + 0) run the full queues.  A batch is done: store its
-        # lanes' results at their packets, back to the drain code.
-        L += [".Lrg_done:",
-              "s_bitcmp1_b32 s7, 7",
-              "s_cbranch_scc1 .Lrg_batch_done",
-              "s_mov_b64 exec, -1",
-              "v_cmp_gt_u32_e64 vcc, %s, v%d" % (s(S_COUNT), V_IDX),
-              "s_andn2_b64 exec, vcc, %s" % sp(S_DEFER),
-              "v_lshlrev_b32 %s, 3, v%d" % (v(R[0]), V_IDX),
-              "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RES, V_RES + 1, sp(S_RET),
-                                                          ST_POLICY),
-              "s_mov_b64 %s, 0" % sp(S_DEFER)] + goto("ebpf_jit_area") + [
-              ".Lrg_batch_done:",
-              "s_mov_b64 exec, %s" % sp(S_BMASK),
-              "v_lshlrev_b32 %s, 3, v%d" % (v(R[0]), V_IDX),
-              "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RES, V_RES + 1, sp(S_RET),
-                                                          ST_POLICY),
-              "s_and_b32 s7, s7, ~128"] + goto("ebpf_jit_area")
     if SPAN_IMAGE:
         L += window_code()
     HR = HIST_REPLICA_BYTES
     L += [".Lfinish:"] + store_prev_results("f", True)
-    if not STAGED_IMAGE:
-        # every group done: the drain code runs what the queues still hold (bit 8: any count)
-        L += ["s_bitcmp1_b32 s7, 6",
-              "s_cbranch_scc0 .Lfinish_body",
-              "s_or_b32 s7, s7, 256"] + goto("ebpf_jit_area")
     L += [".Lfinish_body:",
           "s_mov_b64 exec, -1",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
@@ -3354,8 +3192,8 @@ def jit_templates():
         ".Ljt_cs", ".Ljt_cs_br", ".Ljt_cs_vt", ".Ljt_cs_end",
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
         ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", ".Lr_exit", ".Lr_fault",
-        ".Lr_hlookup", ".Lgroup_done", ".Lr_batch" if not STAGED_IMAGE else ".Lgroup_done",
-        ".Lr_schedule", ".Ldrain_ret", ".Lr_cut" if not STAGED_IMAGE else ".Lgroup_done",
+        ".Lr_hlookup", ".Lgroup_done",
+        ".Lr_schedule", ".Lr_cut" if not STAGED_IMAGE else ".Lgroup_done",
         "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
@@ -3482,10 +3320,7 @@ def generate(out_s, staged_image):
     header.append("#define AH_GEN_JOIN %d  // the general image holds the join SGPRs too" % GEN_JOIN)
     header.append("#define AH_GEN_HOIST_BASE 64  // general image: spare VGPRs for hoisted loads")
     header.append("#define AH_GEN_HOIST_REGS %d" % GEN_HOIST_REGS)
-    header.append("#define AH_S_DEFER %d  // regrouping (general image): queued lanes of the group" % S_DEFER)
-    header.append("#define AH_S_QBASE %d  // the wave's queue slice" % S_QBASE)
-    header.append("#define AH_S_QS %d  // queue states, two per SGPR" % S_QS)
-    header.append("#define AH_RQ_MAX %d" % RQ_MAX)
+    header.append("#define AH_S_RUNMASK %d  // general image: s[76:77], a hoisted-load run's lanes" % S_RUNMASK)
     header.append("#define AH_V_IDX %d  // general image: the lane's packet index" % V_IDX)
     header.append("#define AH_WIN_ARR_BYTES %d  // window launches: LDS per-window arrays" % W_ARR_BYTES)
     header.append("#define AH_RET_GROUPS %d" % RETK)

@@ -166,24 +166,19 @@ struct dp_launch {
 	uint32_t upd_cap;         // records the log holds
 	uint32_t upd_stride;
 	uint64_t pkt_base;        // index of this launch's first packet in its batch
-	// regrouping (compiled programs, general kernels; gen_interp.py "Regrouping"): the queue
-	// buffer, rq_wave_bytes per wave of the launch (wave w = workgroup * 4 + wave in it); NULL:
-	// no queues
-	uint8_t *rq_buf;
-	uint32_t rq_wave_bytes;
-	uint32_t rq_pad;
+	uint8_t *reserved0;       // (unused; keeps the offsets the assembly kernels load)
+	uint32_t reserved1;
+	uint32_t reserved2;
 	// map writes: one bit per packet of the batch (index pkt_base + i, cleared by the host before
 	// the batch), set when the packet faults; the apply step skips a faulted packet's logged
 	// writes (a packet that faults leaves no write behind).  NULL for programs without map writes
 	uint32_t *upd_faulted;
-	// length-bucketed launches (general kernels; gen_interp.py "Length-bucketed launches"):
-	// this launch runs slots perm[perm_cls[0] .. perm_cls[0] + perm_cls[1]) (packet indices, both
-	// on the device: written by the bucketing kernels, bucket.hip), span_g per group; NULL = every
-	// packet, 64 per group.  span_slot != 0 (span image only): each packet is staged whole in
-	// LDS, span_slot bytes per lane (a multiple of 16 with an odd number of 16-B blocks)
+	// slot launches (general kernels; gen_interp.py "Slot mode": a window launch's overflow
+	// list): this launch runs slots perm[perm_cls[0] .. perm_cls[0] + perm_cls[1]) (packet
+	// indices, both on the device), span_g per group; NULL = every packet, 64 per group
 	const uint32_t *perm;
 	const uint32_t *perm_cls;
-	uint32_t span_slot;
+	uint32_t reserved3;
 	uint32_t span_g;
 	uint32_t span_magic_g;    // ceil(2^32 / span_g)
 	// stores into map values (ebpf_gpu.h "Stores into map values"): bit 0 = the program reads
@@ -202,7 +197,7 @@ struct dp_launch {
 static_assert(sizeof(dp_launch) == 232, "dp_launch layout is shared with the assembly kernels");
 static_assert(offsetof(dp_launch, win_bytes) == 0xd0 && offsetof(dp_launch, win_ovf) == 0xe0,
 	      "gen_interp.py loads the window fields at fixed offsets");
-static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_slot) == 192,
+static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_g) == 196,
 	      "gen_interp.py loads these fields at fixed offsets");
 
 // The lane's LDS stack slice, below the frame the program addresses: the loop count (+0), the

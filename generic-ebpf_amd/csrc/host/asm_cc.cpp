@@ -1272,7 +1272,7 @@ struct emitter {
 		const int S_MASK = 48, S_CODE = 52, V_LEN = 40, S_JUNK_ = 60, V_PKT = 38;
 		size_t br = 0, from = 0;
 		if (runmask) {
-			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_DEFER}); // s_andn2_b64
+			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_RUNMASK}); // s_andn2_b64
 			br = E.b.size();
 			E.w(0xbf840000u); // s_cbranch_scc0 over the block below (its length set at its end)
 			from = E.b.size();
@@ -1285,7 +1285,7 @@ struct emitter {
 		if (runmask) {
 			static const uint32_t gop[4] = {0x10, 0x12, 0x14, 0x15};
 			const int zi = z == 1 ? 0 : z == 2 ? 1 : z == 4 ? 2 : 3;
-			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_DEFER}); // in bounds, unmasked
+			E.sop2(0x13, S_MASK, opnd{SRC_EXEC}, opnd{(uint32_t)AH_S_RUNMASK}); // in bounds, unmasked
 			E.w(0xbf840000u | 6u);                                           // s_cbranch_scc0 +6
 			E.sop1(0x01, S_JUNK_, opnd{SRC_EXEC});                           // s_mov_b64 s60, exec
 			E.sop1(0x01, 126, opnd{(uint32_t)S_MASK});                       // s_mov_b64 exec, s48
@@ -1670,26 +1670,7 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vecto
 
 namespace {
 
-// families a regroup point's subtree may hold: they read and write registers and the packet
-// (through V_PKT / the staged header, never r1), nothing lane-position dependent
-bool
-regroup_safe(int fam)
-{
-	if ((fam >= AHF_A64R_ADD && fam <= AHF_A64R_MOD) || (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD) ||
-	    (fam >= AHF_A64I_ADD && fam <= AHF_A64I_MOV) || (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD) ||
-	    (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) || (fam >= AHF_LDXPKC1 && fam <= AHF_LDXPKC8) ||
-	    (fam >= AHF_MOV64R && fam <= AHF_MOD32Z) || is_cond_fam(fam))
-		return true;
-	switch (fam) {
-	case AHF_BSWAP16: case AHF_BSWAP32: case AHF_BSWAP64:
-	case AHF_EXIT: case AHF_FAULT: case AHF_NOP:
-		return true;
-	default:
-		return false;
-	}
-}
-
-// SOP2 / SOP1 / SOPC / SOPP opcodes used by the regroup code (llvm-mc, gfx950)
+// SOP2 / SOP1 / SOPC / SOPP opcodes used by the cut code (llvm-mc, gfx950)
 enum : uint32_t {
 	S2_ADD_U32 = 0x00, S2_SUB_U32 = 0x01, S2_ADDC_U32 = 0x04, S2_MIN_U32 = 0x07, S2_CSELECT_B32 = 0x0a,
 	S2_AND_B32 = 0x0c, S2_OR_B32 = 0x0e, S2_OR_B64 = 0x0f, S2_ANDN2_B64 = 0x13, S2_LSHL_B32 = 0x1c,
@@ -1699,8 +1680,6 @@ enum : uint32_t {
 	V3_MBCNT_LO = 0x28c, V3_MBCNT_HI = 0x28d,
 	G_LOAD_DWORDX2 = 0x15, G_STORE_DWORD = 0x1c, G_STORE_DWORDX2 = 0x1d,
 };
-const int RG_T0 = 53, RG_T1 = 54, RG_T2 = 55, RG_T3 = 56; // gen_interp.py S_T0..S_T3
-const int RG_REC = 64;                                    // s[64:65]: the queue's base
 
 void
 sopc(enc &E, uint32_t op, opnd a, opnd b)
@@ -1708,15 +1687,6 @@ sopc(enc &E, uint32_t op, opnd a, opnd b)
 	E.w(0xbf000000u | (op << 16) | (b.code << 8) | a.code);
 	E.lit(a);
 	E.lit(b);
-}
-
-// global load/store, SGPR base s[sbase:+1] + VGPR byte offset voff + imm
-void
-gmem(enc &E, uint32_t op, int voff, int data_or_vdst, int sbase, uint32_t imm, bool store)
-{
-	E.w(0xdc000000u | (op << 18) | 0x8000u | (imm & 0x1fffu));
-	E.w((uint32_t)voff | (store ? ((uint32_t)data_or_vdst << 8) : ((uint32_t)data_or_vdst << 24)) |
-	    ((uint32_t)sbase << 16));
 }
 
 // jump (or call, link s[50:51]) to .Lcb + off
@@ -1732,127 +1702,14 @@ jump_cb(enc &E, uint32_t off, bool call)
 } // namespace
 
 void
-cc_regroup_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
-		std::vector<cc_regroup_point> &points)
-{
-	points.clear();
-	// opt-in (EBPF_CC_REGROUP=1): measured slower than per-group divergence on C5
-	const char *on = getenv("EBPF_CC_REGROUP");
-	if (on == nullptr || atoi(on) == 0 || xl.has_loops) // (the plan walks a tree)
-		return;
-	// entries each side of the divergent conditional at least holds: a queued lane costs its
-	// push, a batch slot and the batch set-up (packet address, header), worth it for long paths
-	uint32_t rg_min = 96;
-	if (const char *m = getenv("EBPF_CC_RG_MIN"))
-		rg_min = (uint32_t)atoi(m);
-	const size_t n = low.size();
-	auto fam_of = [&](uint32_t e) { return (int)ah_fam[(uint32_t)low[e].handler]; };
-	auto is_term = [&](uint32_t e) { return fam_of(e) == AHF_EXIT || fam_of(e) == AHF_FAULT; };
-	auto is_cond = [&](uint32_t e) { return (ah_flags[(uint32_t)low[e].handler] & 1) != 0; };
-	std::vector<uint32_t> parent(n, UINT32_MAX), npred(n, 0);
-	for (uint32_t e : order) {
-		if (is_term(e))
-			continue;
-		const uint32_t nx = xl.entries[e].next;
-		if (nx < n) {
-			npred[nx]++;
-			parent[nx] = e;
-		}
-		if (is_cond(e) && xl.entries[e].target < n) {
-			npred[xl.entries[e].target]++;
-			parent[xl.entries[e].target] = e;
-		}
-	}
-	// backward over the tree (children follow their parent in `order`): subtree size, safety,
-	// conservative liveness (every register a copied handler body would read)
-	std::vector<uint32_t> sz(n, 0);
-	std::vector<char> safe(n, 0), cand(n, 0), below(n, 0);
-	std::vector<uint16_t> live(n, 0);
-	for (size_t k = order.size(); k-- > 0;) {
-		const uint32_t e = order[k];
-		const int fam = fam_of(e);
-		const int d = ah_dst[(uint32_t)low[e].handler], sr = ah_src[(uint32_t)low[e].handler];
-		uint32_t size = 1;
-		bool ok = regroup_safe(fam);
-		uint16_t lo = 0;
-		if (!is_term(e)) {
-			uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
-			for (uint32_t c : ch) {
-				if (c >= n)
-					continue;
-				size += sz[c];
-				ok = ok && safe[c];
-				lo |= live[c];
-			}
-		}
-		const int wr = written_reg(fam, d);
-		uint16_t li = lo;
-		if (wr >= 0)
-			li &= (uint16_t)~(1u << wr);
-		li |= copied_uses(fam, d, sr);
-		sz[e] = size;
-		safe[e] = ok;
-		live[e] = li;
-	}
-	// candidates: the entry heads one side of a conditional whose both sides are heavy (sizes
-	// complete now: a taken subtree is laid out after its fall-through sibling)
-	for (uint32_t e : order) {
-		const uint32_t p = parent[e];
-		if (safe[e] && e != xl.start && npred[e] == 1 && p < n && is_cond(p) && sz[e] >= rg_min &&
-		    __builtin_popcount(live[e]) <= 3) {
-			const uint32_t o = xl.entries[p].next == e ? xl.entries[p].target : xl.entries[p].next;
-			cand[e] = o < n && sz[o] >= rg_min;
-		}
-	}
-	for (size_t k = order.size(); k-- > 0;) {
-		const uint32_t e = order[k];
-		if (is_term(e))
-			continue;
-		uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
-		for (uint32_t c : ch)
-			if (c < n)
-				below[e] = below[e] || cand[c] || below[c];
-	}
-	std::vector<uint32_t> pick;
-	for (uint32_t e : order)
-		if (cand[e] && !below[e])
-			pick.push_back(e);
-	if (pick.size() > (size_t)AH_RQ_MAX) {
-		std::stable_sort(pick.begin(), pick.end(), [&](uint32_t a, uint32_t b) { return sz[a] > sz[b]; });
-		pick.resize(AH_RQ_MAX);
-	}
-	if (getenv("EBPF_CC_RG_DEBUG")) {
-		for (uint32_t e : order)
-			if (cand[e])
-				fprintf(stderr, "regroup candidate %u size %u live %#x below %d\n", e, sz[e], live[e],
-					(int)below[e]);
-		fprintf(stderr, "regroup points: %zu\n", pick.size());
-		int shown = 0;
-		for (uint32_t e : order)
-			if (!regroup_safe(fam_of(e)) && shown++ < 10)
-				fprintf(stderr, "unsafe entry %u family %d\n", e, fam_of(e));
-	}
-	if (pick.size() < 2)
-		return;
-	for (uint32_t e : pick) {
-		cc_regroup_point pt;
-		pt.entry = e;
-		for (int r = 0; r < AH_NREGS; r++)
-			if (live[e] & (1u << r))
-				pt.live.push_back((uint8_t)r);
-		points.push_back(pt);
-	}
-}
-
-void
-cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
+cc_cut_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 		 uint32_t max_cuts, std::vector<uint32_t> &cuts)
 {
 	cuts.clear();
 	if (xl.has_loops) // (the plan walks a tree)
 		return;
-	uint32_t min_size = 96; // (as regrouping: both sides of the divergent conditional this long)
-	if (const char *m = getenv("EBPF_PATHSORT_MIN"))
+	uint32_t min_size = 96; // (both sides of the divergent conditional at least this long)
+	if (const char *m = getenv("EBPF_WIN_CUT_MIN"))
 		min_size = (uint32_t)atoi(m);
 	const size_t n = low.size();
 	auto fam_of = [&](uint32_t e) { return (int)ah_fam[(uint32_t)low[e].handler]; };
@@ -1918,37 +1775,6 @@ cc_pathsort_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const s
 }
 
 void
-cc_push_code(int q, const std::vector<uint8_t> &live, uint32_t qbytes, uint32_t sched_off,
-	     std::vector<uint8_t> &out)
-{
-	enc E{out};
-	const int QS = AH_S_QS + q / 2, sh = 16 * (q & 1);
-	E.sop1(S1_BCNT1_I32_B64, RG_T0, opnd{SRC_EXEC});                          // n
-	E.vop3(V3_MBCNT_LO, T0, SRC_EXEC, 128, 0);                                 // rank in exec
-	E.vop3(V3_MBCNT_HI, T0, SRC_EXEC + 1, VGPR0 + T0, 0);
-	E.sop2(S2_BFE_U32, RG_T1, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)sh | (7u << 16)}); // tail
-	E.vop2(V2_ADD_U32, T0, opnd{(uint32_t)RG_T1}, T0);
-	E.vop2(V2_AND, T0, opnd{SRC_LIT, 0x7f}, T0);                               // slot
-	E.vop2(V2_LSHLREV_B32, T1, opnd{128 + 2}, T0);
-	E.vop2(V2_LSHLREV_B32, T0, opnd{128 + 3}, T0);
-	E.sop2(S2_ADD_U32, RG_REC, opnd{(uint32_t)AH_S_QBASE}, opnd{SRC_LIT, (uint32_t)q * qbytes});
-	E.sop2(S2_ADDC_U32, RG_REC + 1, opnd{(uint32_t)AH_S_QBASE + 1}, opnd{128});
-	gmem(E, G_STORE_DWORD, T1, AH_V_IDX, RG_REC, 0, true);
-	for (size_t k = 0; k < live.size(); k++)
-		gmem(E, G_STORE_DWORDX2, T0, 2 * live[k], RG_REC, 512u + 1024u * (uint32_t)k, true);
-	// tail += n (mod 128), count += n
-	E.sop2(S2_LSHL_B32, RG_T2, opnd{(uint32_t)RG_T0}, opnd{128 + 8});
-	E.sop2(S2_OR_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{(uint32_t)RG_T0});
-	if (sh)
-		E.sop2(S2_LSHL_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{128 + 16});
-	E.sop2(S2_ADD_U32, QS, opnd{(uint32_t)QS}, opnd{(uint32_t)RG_T2});
-	E.sop2(S2_AND_B32, QS, opnd{(uint32_t)QS}, opnd{SRC_LIT, ~(0x80u << sh)});
-	E.sop2(S2_OR_B64, AH_S_DEFER, opnd{(uint32_t)AH_S_DEFER}, opnd{SRC_EXEC});  // queued, not stored
-	E.sop2(S2_ANDN2_B64, 16, opnd{16}, opnd{SRC_EXEC});                        // S_ALIVE
-	jump_cb(E, sched_off, false);
-}
-
-void
 cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out)
 {
 	enc E{out};
@@ -1959,51 +1785,9 @@ cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out)
 }
 
 void
-cc_drain_code(const std::vector<cc_regroup_point> &points, uint32_t qbytes,
-	      const std::vector<uint32_t> &resume, uint32_t batch_off, uint32_t drain_ret_off,
-	      std::vector<uint8_t> &out)
-{
-	enc E{out};
-	const size_t nq = points.size();
-	sopc(E, SC_BITCMP1_B32, opnd{7}, opnd{128 + 8});                             // final drain?
-	E.sop2(S2_CSELECT_B32, RG_T3, opnd{128 + 1}, opnd{128 + 64});             // threshold
-	std::vector<size_t> br(nq);
-	for (size_t q = 0; q < nq; q++) {
-		const int QS = AH_S_QS + (int)q / 2, sh = 16 * (int)(q & 1);
-		E.sop2(S2_BFE_U32, RG_T0, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)(8 + sh) | (8u << 16)});
-		sopc(E, SC_CMP_GE_U32, opnd{(uint32_t)RG_T0}, opnd{(uint32_t)RG_T3});
-		br[q] = out.size();
-		E.w(0xbf850000u);                                                  // s_cbranch_scc1 run_q
-	}
-	jump_cb(E, drain_ret_off, false);
-	for (size_t q = 0; q < nq; q++) {
-		const int QS = AH_S_QS + (int)q / 2, sh = 16 * (int)(q & 1);
-		const uint32_t rel = (uint32_t)((out.size() - br[q] - 4) / 4);
-		out[br[q]] = (uint8_t)(rel & 0xff);
-		out[br[q] + 1] = (uint8_t)(rel >> 8);
-		E.sop2(S2_MIN_U32, RG_T1, opnd{(uint32_t)RG_T0}, opnd{128 + 64});      // n
-		E.sop2(S2_BFE_U32, RG_T2, opnd{(uint32_t)QS}, opnd{SRC_LIT, (uint32_t)sh | (7u << 16)});
-		E.sop2(S2_SUB_U32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{(uint32_t)RG_T0});
-		E.sop2(S2_AND_B32, RG_T2, opnd{(uint32_t)RG_T2}, opnd{SRC_LIT, 0x7f});   // head
-		E.sop2(S2_LSHL_B32, RG_T0, opnd{(uint32_t)RG_T1}, opnd{128 + 8 + (uint32_t)sh});
-		E.sop2(S2_SUB_U32, QS, opnd{(uint32_t)QS}, opnd{(uint32_t)RG_T0});        // count -= n
-		E.sop2(S2_ADD_U32, RG_REC, opnd{(uint32_t)AH_S_QBASE}, opnd{SRC_LIT, (uint32_t)q * qbytes});
-		E.sop2(S2_ADDC_U32, RG_REC + 1, opnd{(uint32_t)AH_S_QBASE + 1}, opnd{128});
-		jump_cb(E, batch_off, true);                                     // .Lr_batch
-		for (size_t k = 0; k < points[q].live.size(); k++)
-			gmem(E, G_LOAD_DWORDX2, T2, 2 * points[q].live[k], RG_REC, 512u + 1024u * (uint32_t)k,
-			     false);
-		// (the lanes whose packet is shorter than 64 bytes, as the prologue sets them)
-		E.vop3(VC_U32 + P_GT, 74, 128 + 64, VGPR0 + 40, 0);
-		E.w(0xbf8c0f70u);                                                  // s_waitcnt vmcnt(0)
-		jump_cb(E, resume[q], false);
-	}
-}
-
-void
 cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 	   const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
-	   const std::vector<dp_map> &table, const std::vector<char> &regroup, std::vector<cc_block> &out)
+	   const std::vector<dp_map> &table, std::vector<cc_block> &out)
 {
 	// mode 2: the general kernels of a span-staged launch (the packet is in LDS: its constant-
 	// offset loads are LDS reads, hoisted as one ds_read_b128 of the 16-B block each); otherwise
@@ -2035,15 +1819,13 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	std::vector<uint16_t> hoist_later(n, 0);
 	std::vector<std::vector<uint32_t>> hoist_at(n);
 	std::vector<uint32_t> hoist_next(n, UINT32_MAX); // the load to issue after this one is used
-	// Run mask (general kernels, programs without regroup points, whose s[76:77] is then free):
+	// Run mask (general kernels: s[76:77]):
 	// the run head tests every running lane against the run's largest load extent once (one
 	// VALU compare into s[76:77]); the run's loads are issued for those lanes with no per-load
 	// compare, and a use only compares (bounds check, fault, direct load) when some running
 	// lane missed the mask.  Two VALU per hoisted load fewer; EBPF_CC_NORUNMASK=1 keeps the
 	// per-load compares (A/B).
-	const bool runmask = mode == 0 &&
-			     std::none_of(regroup.begin(), regroup.end(), [](char c) { return c != 0; }) &&
-			     getenv("EBPF_CC_NORUNMASK") == nullptr;
+	const bool runmask = mode == 0 && getenv("EBPF_CC_NORUNMASK") == nullptr;
 	std::vector<uint32_t> run_ext(n, 0); // run head: the largest off + size of its hoisted loads
 	const int hoist_regs = span ? AH_SPAN_HOIST_REGS : AH_GEN_HOIST_REGS;
 	const int slot_regs = span ? 4 : 2;
@@ -2148,7 +1930,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 		std::vector<int16_t> movfuse_fam(n, -1); // ... as this 32-bit operation
 		for (size_t k = 0; k < order.size(); k++) {
 			const uint32_t e = order[k];
-			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u) && !regroup[e];
+			const bool valid = have[e] && npred[e] == (e == xl.start ? 0u : 1u);
 			facts f = valid ? in[e] : facts();
 			if (!valid)
 				for (bool &p : f.pv)
@@ -2175,7 +1957,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				static const uint32_t gop[4] = {0x10, 0x12, 0x14, 0x15};
 				if (masked) {
 				} else if (runmask) {
-					Hq.sop1(0x20, S_JUNK_, opnd{(uint32_t)AH_S_DEFER}); // s_and_saveexec_b64
+					Hq.sop1(0x20, S_JUNK_, opnd{(uint32_t)AH_S_RUNMASK}); // s_and_saveexec_b64
 				} else {
 					Hq.vopc(VC_U32 + P_LE, k32(K32 + (uint32_t)z), V_LEN); // vcc = off+z <= len
 					Hq.sop1(0x20, S_JUNK_, opnd{SRC_VCC});                  // s_and_saveexec_b64
@@ -2193,7 +1975,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				enc Hq{blk.hoist};
 				if (runmask) { // s[76:77] = the running lanes whose packet holds every load of the run
 					Hq.vopc(VC_U32 + P_LE, k32(run_ext[e]), 40); // vcc = ext <= len (v40)
-					Hq.sop1(0x01, AH_S_DEFER, opnd{SRC_VCC});    // s_mov_b64
+					Hq.sop1(0x01, AH_S_RUNMASK, opnd{SRC_VCC});    // s_mov_b64
 					Hq.sop1(0x20, 60, opnd{SRC_VCC});            // s_and_saveexec_b64 s[60:61]
 					for (uint32_t x : hoist_at[e])
 						issue(Hq, x, true);

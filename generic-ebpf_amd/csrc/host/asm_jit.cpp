@@ -33,8 +33,8 @@ enum jt_index {
 	JT_MOV_S10 = 0, // .. JT_MOV_S10 + 5
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
-	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE, JT_RBATCH,
-	JT_SCHED, JT_DRAINRET, JT_CUT, JT_AREA, JT_AREA_BYTES,
+	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE,
+	JT_SCHED, JT_CUT, JT_AREA, JT_AREA_BYTES,
 	JT_COUNT
 };
 
@@ -172,48 +172,16 @@ layout_order(const dprog_host &xl, const std::vector<dp_entry> &low)
 
 } // namespace
 
-// Path-sorted launches (gpu_runtime.cpp launch_pathsorted): the classifying prefix of the
-// program, as a program of its own — the translation with every cut point of
-// cc_pathsort_plan (on the general kernels' lowering) replaced by a FAULT entry of code
-// kPathCutCode + q, so that a lane's fault byte says which heavy subtree it reaches (0 or a real
-// fault code: none, it exits or faults before).  ENOENT: fewer than two cut points.
-int
-asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint32_t max_cuts,
-		    dprog_host *prefix, uint32_t *ncuts, std::string *err)
-{
-	std::vector<dp_entry> low;
-	uint32_t stride = 0;
-	int e = asm_lower(xl, 0, table, low, &stride, err);
-	if (e)
-		return e;
-	std::vector<uint32_t> cuts;
-	cc_pathsort_plan(xl, low, layout_order(xl, low), max_cuts, cuts);
-	if (cuts.empty())
-		return ENOENT;
-	*prefix = xl;
-	for (size_t q = 0; q < cuts.size(); q++) {
-		dp_entry &x = prefix->entries[cuts[q]];
-		memset(&x, 0, sizeof(x));
-		x.kind = DK_FAULT;
-		x.aux = (uint16_t)(kPathCutCode + q);
-	}
-	*ncuts = (uint32_t)cuts.size();
-	return 0;
-}
-
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
-// *rq_wave_bytes: the regroup queue bytes each wave of a launch needs (0: the program has no
-// regroup point; gen_interp.py "Regrouping").
-// Area layout: +0 the drain entry (16 bytes: a jump to the drain code, or s_endpgm), +16 the
-// program's start block (where the kernel enters each group), the blocks, the drain code.
+// *win_cuts (mode 2): the cut points of the window launches' phase A.
+// Area layout: +0 16 bytes of s_endpgm, +16 the program's start block (where the kernel enters
+// each group), then the blocks.
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-	     uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes, uint32_t *win_cuts)
+	     uint32_t *stack_stride, std::string *err, uint32_t *win_cuts)
 {
-	if (rq_wave_bytes)
-		*rq_wave_bytes = 0;
 	if (win_cuts)
 		*win_cuts = 0;
 	const uint32_t HDR = 16;
@@ -319,36 +287,14 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			}
 		}
 	}
-	// regroup points (general kernels, unstructured compiled programs): each block starts with
-	// its push code; the drain code resumes a batch right after it (an entry point)
-	std::vector<cc_regroup_point> rg;
-	std::vector<char> regroup(n, 0);
-	std::vector<int> rq_of(n, -1);
+	// code heading a block (window cut points)
 	std::vector<std::vector<uint8_t>> push(n);
-	uint32_t qbytes = 0;
-	if (mode == 0 && !structured && getenv("EBPF_JIT_NOCC") == nullptr)
-		cc_regroup_plan(xl, low, order, rg); // (never in span launches: s78.. are theirs)
-	if (!rg.empty()) {
-		size_t slots = 0;
-		for (const cc_regroup_point &p : rg)
-			slots = std::max(slots, p.live.size());
-		qbytes = cc_queue_bytes((uint32_t)slots);
-		for (size_t q = 0; q < rg.size(); q++) {
-			const uint32_t e = rg[q].entry;
-			regroup[e] = 1;
-			entry_point[e] = 1;
-			rq_of[e] = (int)q;
-			cc_push_code((int)q, rg[q].live, qbytes, T[JT_SCHED], push[e]);
-		}
-		if (rq_wave_bytes)
-			*rq_wave_bytes = (uint32_t)rg.size() * qbytes;
-	}
 	// window launches (mode 2, the span image; gen_interp.py "Window mode"): the cut points of
 	// phase A, class q + 1 at cut q, each block headed by its cut code (an entry point: the
 	// lanes that leave there end its hoisted-load run)
 	if (mode == 2 && getenv("EBPF_WINDOW_NOCUT") == nullptr) {
 		std::vector<uint32_t> cuts;
-		cc_pathsort_plan(xl, low, order, kPathMaxCuts, cuts);
+		cc_cut_plan(xl, low, order, kPathMaxCuts, cuts);
 		for (size_t q = 0; q < cuts.size(); q++) {
 			const uint32_t e = cuts[q];
 			entry_point[e] = 1;
@@ -361,7 +307,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<cc_block> cb;
 	if (getenv("EBPF_JIT_NOCC") == nullptr)
 		cc_compile(xl, low, order, entry_point, mode, structured,
-			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, regroup, cb);
+			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, cb);
 	else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
 		cc_prologue(gm, 0x7ff, true, false, cb[xl.start].prologue);
@@ -529,13 +475,6 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		}
 		if (!changed)
 			break;
-	}
-	// the drain code (its size does not depend on the offsets it jumps to)
-	const uint32_t drain_pos = total;
-	if (!rg.empty()) {
-		std::vector<uint8_t> probe;
-		cc_drain_code(rg, qbytes, std::vector<uint32_t>(rg.size(), 0), 0, 0, probe);
-		total += (uint32_t)probe.size();
 	}
 	if (total > (uint32_t)AH_JIT_AREA_BYTES) {
 		*err = "compiled program exceeds the code area";
@@ -709,22 +648,6 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
 		put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
 	}
-	if (!rg.empty()) { // the drain entry at +0 and the drain code
-		std::vector<uint32_t> resume(rg.size());
-		for (size_t q = 0; q < rg.size(); q++)
-			resume[q] = code_off(rg[q].entry) + (uint32_t)push[rg[q].entry].size();
-		std::vector<uint8_t> dr;
-		cc_drain_code(rg, qbytes, resume, T[JT_RBATCH], T[JT_DRAINRET], dr);
-		if (drain_pos + dr.size() != total) {
-			*err = "internal error: drain code size mismatch";
-			return EINVAL;
-		}
-		memcpy(&img[area + drain_pos], dr.data(), dr.size());
-		put32(0, 0x80000000u | (60u << 16) | (255u << 8) | 4u);           // s_add_u32 s60, s4, lit
-		put32(4, T[JT_AREA] + drain_pos);
-		put32(8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
-		put32(12, 0xbe800000u | (0x1du << 8) | 60u);                        // s_setpc_b64 s[60:61]
-	}
 	if (code)
 		code->assign(img.begin() + area, img.begin() + area + total);
 	return 0;
@@ -735,10 +658,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 int
 asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-	      uint32_t *rq_wave_bytes, uint32_t *win_cuts)
+	      uint32_t *win_cuts)
 {
 	std::vector<unsigned char> img;
-	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, rq_wave_bytes, win_cuts);
+	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, win_cuts);
 	if (e)
 		return e;
 	if (hipSetDevice(device) != hipSuccess)

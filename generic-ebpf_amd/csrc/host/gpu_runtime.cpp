@@ -16,7 +16,6 @@
 #include <functional>
 #include <thread>
 
-#include "bucket.h"
 #include "hist_ops.h"
 #include "internal.h"
 #include "map_writes.h"
@@ -39,14 +38,11 @@ int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vec
 // asm_jit.cpp
 int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-		  uint32_t *rq_wave_bytes, uint32_t *win_cuts = nullptr);
+		  uint32_t *win_cuts = nullptr);
 void asm_jit_release(void *mod);
-int asm_pathsort_prefix(const dprog_host &xl, const std::vector<dp_map> &table, uint32_t max_cuts,
-			dprog_host *prefix, uint32_t *ncuts, std::string *err);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-		 uint32_t *stack_stride, std::string *err, uint32_t *rq_wave_bytes = nullptr,
-		 uint32_t *win_cuts = nullptr);
+		 uint32_t *stack_stride, std::string *err, uint32_t *win_cuts = nullptr);
 
 
 namespace {
@@ -100,10 +96,7 @@ struct rows_slot {
 	size_t log_bytes = 0;
 	void *win = nullptr;
 	size_t win_bytes = 0;
-	// compiled programs with regroup points: the stream's queue buffer (any contents)
-	void *rq = nullptr;
-	size_t rq_bytes = 0;
-	// length-bucketed launches: perm, per-tile counts and the class table (bucket.h)
+	// window launches: the overflow slot list (any contents but its count, set per launch)
 	void *bk = nullptr;
 	size_t bk_bytes = 0;
 	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
@@ -238,7 +231,7 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 	return 0;
 }
 
-// The stream's bucketing buffer (>= bytes, any contents).
+// The stream's window scratch buffer (>= bytes, any contents).
 int
 bk_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
 {
@@ -249,20 +242,6 @@ bk_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
 		err = grow_zeroed(&r->bk, &r->bk_bytes, bytes);
 	if (!err)
 		*out = static_cast<uint8_t *>(r->bk);
-	return err;
-}
-
-// The stream's regroup queue buffer (>= bytes).
-int
-rq_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
-{
-	std::lock_guard<std::mutex> g(g_rows_lock);
-	rows_slot *r;
-	int err = slot_for(device, stream, &r);
-	if (!err)
-		err = grow_zeroed(&r->rq, &r->rq_bytes, bytes);
-	if (!err)
-		*out = static_cast<uint8_t *>(r->rq);
 	return err;
 }
 
@@ -635,8 +614,7 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	std::string msg;
 	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
-				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_rq_bytes[mode],
-				&dp->jit_cuts[mode]);
+				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_cuts[mode]);
 	dp->build_ms[mode] =
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
@@ -741,237 +719,6 @@ upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t
 	return 0;
 }
 
-// Length-bucketed launch of a mixed-size batch (offsets form) of a compiled program that reads
-// past the packets' first 64 bytes (asm_program_span): bucket.hip sorts the packet indices into
-// length classes, then one launch per class runs the class's packets G per wave — class 0 (up to
-// 64 bytes, longer than the last class, or not 16-B aligned) on the general kernels, classes 1..
-// on the span-staged kernels (mode 2: each packet DMA'd whole into an LDS slot of `slot` bytes,
-// its loads LDS reads).  Every packet keeps its own result and fault slot (ret[i], faults[i]).
-// Returns 0 with *done set when it ran the batch; 0 with *done clear when the batch should run
-// as one plain launch instead (no span code, LDS too small); else an error.
-struct span_class {
-	uint32_t lim;  // longest packet of the class
-	uint32_t slot; // LDS bytes per packet (a multiple of 16, an odd count of 16-B blocks)
-};
-const span_class kSpanClasses[3] = {{64, 0}, {576, 592}, {1536, 1552}};
-constexpr uint64_t kBucketMin = 1u << 16;  // smaller batches: one plain launch
-constexpr uint64_t kBucketMax = 1u << 26;  // (the kernels' group-count division is exact below)
-
-bool
-bucket_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
-{
-	// opt-in (EBPF_BUCKET=1) until it beats the plain launch on C5
-	const char *on = getenv("EBPF_BUCKET");
-	return on && *on == '1' && L.offsets != nullptr && L.count >= kBucketMin && L.count < kBucketMax &&
-	       ep->xlated->asm_span && !prog_writes_maps(*ep->xlated) && dp->jit_rq_bytes[0] == 0;
-}
-
-int
-launch_bucketed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
-		hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
-		bool *done)
-{
-	*done = false;
-	if (jit_entries(ep, dp, 2) != 0)
-		return 0; // (no span code for this program: the plain launch)
-	const uint32_t pkt_base = kMapLdsBase + dp->map_lds_bytes;
-	const uint32_t stack = 256 * std::max(dp->jit_stride[0], dp->jit_stride[2]);
-	if (pkt_base + stack >= 160 * 1024)
-		return 0;
-	// packets per group of each span class: as many slots as the LDS left by the stacks and
-	// maps holds (a program with generic memory accesses has the reference's 512-B stack per
-	// lane); a class that would get fewer than 8 is left out (its packets go to class 0, as
-	// "longer than the last class")
-	uint32_t nclass = 1;
-	uint32_t G[3] = {64, 0, 0};
-	// (EBPF_SPAN_WAVES=w: size G for w workgroups per CU; EBPF_SPAN_G<k>: force G of class k)
-	static const char *sw = getenv("EBPF_SPAN_WAVES");
-	const uint32_t wgs = sw && atoi(sw) > 0 ? (uint32_t)atoi(sw) : 1;
-	for (uint32_t k = 1; k < 3; k++) {
-		const uint32_t per_wg = 160 * 1024 / wgs;
-		if (per_wg <= pkt_base + stack)
-			break;
-		G[k] = std::min<uint32_t>(64, (per_wg - pkt_base - stack) / (4 * kSpanClasses[k].slot));
-		char nm[16];
-		snprintf(nm, sizeof(nm), "EBPF_SPAN_G%u", k);
-		if (const char *g = getenv(nm))
-			G[k] = std::min<uint32_t>((uint32_t)atoi(g), G[k]);
-		if (G[k] < 4)
-			break;
-		nclass = k + 1;
-	}
-	if (nclass == 1)
-		return 0;
-	uint32_t tile;
-	const uint32_t tiles = bucket_tiles(L.count, &tile);
-	const size_t perm_bytes = (L.count * 4 + 255) & ~(size_t)255;
-	const size_t blk_bytes = (size_t)kBucketMaxTiles * kBucketMaxClass * 4;
-	uint8_t *bk;
-	int err = bk_acquire(dp->device, stream, perm_bytes + blk_bytes + 256, &bk);
-	if (err)
-		return fail(err, "bucketing buffer");
-	bucket_args a;
-	memset(&a, 0, sizeof(a));
-	a.offsets = L.offsets;
-	a.off_base = L.off_base;
-	a.data = L.data;
-	a.count = L.count;
-	for (uint32_t k = 0; k < nclass; k++)
-		a.lim[k] = kSpanClasses[k].lim;
-	a.nclass = nclass;
-	a.tile = tile;
-	a.perm = reinterpret_cast<uint32_t *>(bk);
-	a.blk_cnt = reinterpret_cast<uint32_t *>(bk + perm_bytes);
-	a.cls = reinterpret_cast<uint32_t *>(bk + perm_bytes + blk_bytes);
-	hipError_t e;
-	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	if ((e = launch_bucket(a, tiles, stream)) != hipSuccess)
-		return hip_fail(e, "bucketing kernels");
-	// (EBPF_BUCKET_NOSPAN=1, A/B: every class on the general kernels, 64 packets per group —
-	// length-sorted groups without the LDS staging)
-	const bool nospan = getenv("EBPF_BUCKET_NOSPAN") != nullptr;
-	for (uint32_t k = 0; k < nclass; k++) {
-		const int mode = k && !nospan ? 2 : 0;
-		const uint32_t g = mode == 2 ? G[k] : 64;
-		dp_launch Lk = L;
-		Lk.perm = a.perm;
-		Lk.perm_cls = a.cls + 2 * k;
-		Lk.span_slot = mode == 2 ? kSpanClasses[k].slot : 0;
-		Lk.span_g = g;
-		Lk.span_magic_g = (uint32_t)((0x100000000ull + g - 1) / g);
-		Lk.stack_stride = dp->jit_stride[mode];
-		if (mode == 2)
-			Lk.lds_pkt_base = 0; // (no header staging: every load reads the LDS slot)
-		e = launch_interp_asm(Lk, stream, dp->device, mode, dp->map_lds_bytes, dp->jit_fn[mode], 0,
-				      nullptr, nullptr, user_hist, overwrite && k == 0);
-		if (e != hipSuccess)
-			return hip_fail(e, "length-class launch");
-	}
-	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	dp->last_layout = 2;
-	*done = true;
-	return 0;
-}
-
-// Path-sorted launch of a large batch (offsets form) of a compiled program on the general kernels
-// whose tree splits into heavy subtrees (cc_pathsort_plan).  Three steps on the stream:
-//   1. the classifying run: the program's prefix, compiled with every cut point a FAULT of code
-//      kPathCutCode + q (asm_pathsort_prefix), over the batch, into scratch results and faults;
-//   2. bucket.hip sorts the packet indices by that byte (class q + 1 for cut q, class 0 for a
-//      packet that exits or faults before any cut), stable, so a class keeps packet order;
-//   3. the whole program over the sorted order (slot mode, 64 packets per group): a group's
-//      lanes follow one path through the prefix into one subtree, instead of every subtree its
-//      packets take (C5: about 12 per group).
-// The main run re-executes the prefix from the packets as given: the prefix holds no store
-// that may reach the packet or a map and no map write, and maps are read-only during a batch,
-// so it takes the same path.  Every packet keeps its own result, fault and verdict.
-constexpr uint64_t kPathMin = 1u << 16; // smaller batches: one plain launch
-
-bool
-pathsort_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
-{
-	// opt-in (EBPF_PATHSORT=1) until it beats the plain launch on C5;
-	// EBPF_PATHSORT_MINBATCH=n lowers the batch threshold (tests)
-	const char *on = getenv("EBPF_PATHSORT");
-	if (!(on && *on == '1'))
-		return false;
-	uint64_t min = kPathMin;
-	if (const char *m = getenv("EBPF_PATHSORT_MINBATCH"))
-		min = strtoull(m, nullptr, 0);
-	return L.offsets != nullptr && L.count >= min && L.count < kBucketMax &&
-	       !prog_writes_maps(*ep->xlated) && dp->jit_rq_bytes[0] == 0 && dp->ps_err == 0;
-}
-
-int
-pathsort_entries(struct ebpf_prog *ep, dprog_device *dp)
-{
-	std::lock_guard<std::mutex> g(ep->dlock);
-	if (dp->ps_fn)
-		return 0;
-	if (dp->ps_err)
-		return dp->ps_err;
-	std::string msg;
-	dprog_host prefix;
-	int err = asm_pathsort_prefix(*ep->xlated, dp->table, kPathMaxCuts, &prefix, &dp->ps_ncuts, &msg);
-	uint32_t rq = 0;
-	if (err == 0)
-		err = asm_jit_build(dp->device, prefix, 0, dp->table, &dp->ps_mod, &dp->ps_fn, &dp->ps_stride,
-				    &msg, &rq);
-	if (err == 0 && rq != 0)
-		err = ENOENT; // (regroup queues in the prefix: not combined)
-	dp->ps_err = err;
-	return err;
-}
-
-int
-launch_pathsorted(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
-		  hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
-		  bool *done)
-{
-	*done = false;
-	if (pathsort_entries(ep, dp) != 0)
-		return 0; // (no cut points: the plain launch)
-	uint32_t tile;
-	const uint32_t tiles = bucket_tiles(L.count, &tile);
-	const size_t perm_bytes = (L.count * 4 + 255) & ~(size_t)255;
-	const size_t blk_bytes = (size_t)kBucketMaxTiles * kBucketMaxClass * 4;
-	const size_t ret_bytes = L.count * 8, flt_bytes = (L.count + 255) & ~(size_t)255;
-	uint8_t *bk;
-	int err = bk_acquire(dp->device, stream, perm_bytes + blk_bytes + 256 + ret_bytes + flt_bytes, &bk);
-	if (err)
-		return fail(err, "path-sort buffer");
-	bucket_args a;
-	memset(&a, 0, sizeof(a));
-	a.offsets = L.offsets;
-	a.off_base = L.off_base;
-	a.data = L.data;
-	a.count = L.count;
-	a.nclass = dp->ps_ncuts + 1;
-	a.tile = tile;
-	a.perm = reinterpret_cast<uint32_t *>(bk);
-	a.blk_cnt = reinterpret_cast<uint32_t *>(bk + perm_bytes);
-	a.cls = reinterpret_cast<uint32_t *>(bk + perm_bytes + blk_bytes);
-	uint64_t *pret = reinterpret_cast<uint64_t *>(bk + perm_bytes + blk_bytes + 256);
-	uint8_t *pflt = bk + perm_bytes + blk_bytes + 256 + ret_bytes;
-	a.code = pflt;
-	a.code_base = kPathCutCode;
-	hipError_t e;
-	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	// 1. the classifying run (no verdicts: scratch results and fault bytes only)
-	dp_launch Lp = L;
-	Lp.ret = pret;
-	Lp.faults = pflt;
-	Lp.hist = nullptr;
-	Lp.hist_rows = nullptr;
-	Lp.stack_stride = dp->ps_stride;
-	e = launch_interp_asm(Lp, stream, dp->device, 0, dp->map_lds_bytes, dp->ps_fn, 0, nullptr, nullptr,
-			      nullptr, false);
-	if (e != hipSuccess)
-		return hip_fail(e, "path-sort classifying launch");
-	// 2. the packet indices by class
-	if ((e = launch_bucket(a, tiles, stream)) != hipSuccess)
-		return hip_fail(e, "path-sort bucketing kernels");
-	// 3. the program over the sorted order: one slot range, the whole batch (cls[kBucketMaxClass])
-	dp_launch Lm = L;
-	Lm.perm = a.perm;
-	Lm.perm_cls = a.cls + 2 * kBucketMaxClass;
-	Lm.span_slot = 0;
-	Lm.span_g = 64;
-	Lm.span_magic_g = (uint32_t)((0x100000000ull + 63) / 64);
-	e = launch_interp_asm(Lm, stream, dp->device, 0, dp->map_lds_bytes, dp->jit_fn[0], 0, nullptr,
-			      nullptr, user_hist, overwrite);
-	if (e != hipSuccess)
-		return hip_fail(e, "path-sorted launch");
-	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	dp->last_layout = 3;
-	*done = true;
-	return 0;
-}
-
 // Window launch of a large batch (offsets form) of a compiled program that reads past the
 // packets' first 64 bytes (gen_interp.py "Window mode"): the span image walks each workgroup's
 // share of the batch in windows of up to 256 packets staged in LDS as one contiguous DMA, runs
@@ -998,8 +745,7 @@ window_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launc
 		min = strtoull(m, nullptr, 0);
 	// (the staged copy is not written back: no store that may reach the packet)
 	const bool fits = L.offsets != nullptr && L.count >= min && L.count <= kWinMax &&
-			  !ep->xlated->asm_needs_general && !prog_writes_maps(*ep->xlated) &&
-			  dp->jit_rq_bytes[0] == 0;
+			  !ep->xlated->asm_needs_general && !prog_writes_maps(*ep->xlated);
 	if (on && *on == '1')
 		return fits;
 	return fits && ep->xlated->asm_span && kWindowDefault;
@@ -1011,7 +757,7 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 		bool *done)
 {
 	*done = false;
-	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 || dp->jit_rq_bytes[0] != 0 ||
+	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 ||
 	    !asm_window_fits(dp->map_lds_bytes, dp->jit_stride[2]))
 		return 0; // (no span code for this program, or no room for a window: the plain launch)
 	// (+ 512 bytes: EBPF_WIN_DEBUG's record after the list, gen_interp.py window_debug)
@@ -1038,7 +784,6 @@ launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipS
 	dp_launch Lo = L;
 	Lo.perm = reinterpret_cast<const uint32_t *>(ovf) + 2;
 	Lo.perm_cls = reinterpret_cast<const uint32_t *>(ovf);
-	Lo.span_slot = 0;
 	Lo.span_g = 64;
 	Lo.span_magic_g = (uint32_t)((0x100000000ull + 63) / 64);
 	Lo.stack_stride = dp->jit_stride[0];
@@ -1339,12 +1084,6 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.prog = nullptr;
 			L.stack_stride = dp->jit_stride[mode];
 			fn = dp->jit_fn[mode];
-			if (dp->jit_rq_bytes[mode]) { // regroup queues: a slice per wave the launch can have
-				const size_t bytes = (size_t)asm_max_workgroups(dp->device) * 4 * dp->jit_rq_bytes[mode];
-				if ((err = rq_acquire(dp->device, stream, bytes, &L.rq_buf)))
-					return fail(err, "regroup queues");
-				L.rq_wave_bytes = dp->jit_rq_bytes[mode];
-			}
 		} else {
 			L.prog = dp->d_asm[mode];
 			L.stack_stride = dp->asm_stride[mode];
@@ -1373,14 +1112,6 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		if (fn && mode == 0 && window_wanted(ep, dp, L) &&
 		    (err = launch_windowed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
 					   &done)))
-			return err;
-		if (!done && fn && mode == 0 && bucket_wanted(ep, dp, L) &&
-		    (err = launch_bucketed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
-					   &done)))
-			return err;
-		if (!done && fn && mode == 0 && pathsort_wanted(ep, dp, L) &&
-		    (err = launch_pathsorted(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
-					     &done)))
 			return err;
 		e = done ? hipSuccess
 			 : launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
@@ -1535,7 +1266,6 @@ prog_release_device_state(struct ebpf_prog *ep)
 					hipFree(a);
 			for (auto *m : dp->jit_mod)
 				asm_jit_release(m);
-			asm_jit_release(dp->ps_mod);
 		}
 	}
 	ep->dev.clear();
@@ -1735,7 +1465,7 @@ ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *
 EBPF_EXPORT int
 ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 {
-	if (ep == nullptr || len == nullptr || layout < 0 || layout > 3)
+	if (ep == nullptr || len == nullptr || layout < 0 || layout > 2)
 		return fail(EINVAL, "bad argument");
 	std::lock_guard<std::mutex> g(ep->dlock);
 	int err = ensure_translated(ep);
@@ -1750,15 +1480,7 @@ ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 	std::vector<unsigned char> img, code;
 	uint32_t stride = 0;
 	std::string msg;
-	if (layout == 3) { // the classifying prefix of a path-sorted launch (general kernels)
-		dprog_host prefix;
-		uint32_t ncuts = 0;
-		err = asm_pathsort_prefix(*ep->xlated, table, kPathMaxCuts, &prefix, &ncuts, &msg);
-		if (err == 0)
-			err = asm_jit_emit(prefix, 0, table, &img, &code, &stride, &msg);
-	} else {
-		err = asm_jit_emit(*ep->xlated, layout, table, &img, &code, &stride, &msg);
-	}
+	err = asm_jit_emit(*ep->xlated, layout, table, &img, &code, &stride, &msg);
 	if (err)
 		return fail(err, msg);
 	const size_t cap = *len;

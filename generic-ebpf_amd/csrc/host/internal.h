@@ -113,15 +113,12 @@ constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 constexpr uint32_t kWinMinBytes = 4096;
 
 // The assembly interpreter's code objects (build/asm_image.cpp): mode 1 = staged 64-B kernels,
-// mode 0 = general kernels, mode 2 = general kernels of span-staged (length-bucketed) launches,
-// whose packets sit in LDS (compiled programs only).  Image 3 is mode 1 for the interpreter
+// mode 0 = general kernels, mode 2 = general kernels of window launches, whose packets sit in
+// LDS (compiled programs only).  Image 3 is mode 1 for the interpreter
 // itself (variant 2): one result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU
 // are resident instead of 6 (gen_interp.py NSGPR_INTERP).
 constexpr int kModes = 3;
-// Path-sorted launches: the fault code a lane of the classifying run retires with at cut point q
-// (kPathCutCode + q; real fault codes are below), and the most cut points (classes 1..15 of
-// bucket.hip, class 0 = no cut reached)
-constexpr uint32_t kPathCutCode = 64;
+// Window launches: the most cut points of a program (classes 1..15; 0 = no cut reached)
 constexpr uint32_t kPathMaxCuts = 15;
 constexpr int kInterpStagedImage = 3;
 extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
@@ -154,16 +151,8 @@ struct dprog_device {
 	void *jit_mod[kModes] = {};              // variant 0: compiled program module, per mode
 	void *jit_fn[kModes] = {};               // its kernel
 	uint32_t jit_stride[kModes] = {};
-	uint32_t jit_rq_bytes[kModes] = {};      // regroup queue bytes per wave (0: none)
 	uint32_t jit_cuts[kModes] = {};          // mode 2: the window launches' cut points
 	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
-	// path-sorted launches (gpu_runtime.cpp launch_pathsorted): the classifying prefix, compiled
-	// for the general kernels (asm_pathsort_prefix), built on first use
-	void *ps_mod = nullptr;
-	void *ps_fn = nullptr;
-	uint32_t ps_stride = 0;
-	uint32_t ps_ncuts = 0;
-	int ps_err = 0;                          // ENOENT: no cut points (plain launches)
 	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
 	std::vector<struct upd_map> upd_host;    // ... and its host copy
@@ -208,7 +197,7 @@ struct dprog_host {
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
-	bool asm_span = false;               // length-bucketed launches pay (asm_program_span)
+	bool asm_span = false;               // window launches pay (asm_program_span)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
 	// Map writes of a device batch (ebpf_gpu.h): the write log holds max_updates records per

@@ -267,25 +267,31 @@ def test_hash_forwarding_register_alias_code(native, env):
 
 
 @pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
-def test_pathsort_prefix_code(native, env):
-    """The classifying prefix of a path-sorted launch (layout 3): C5's tree is cut at its 12
-    leaf subtrees (fault codes 64..75 through s14, the fault routine's operand), the code is a
-    small fraction of the whole program's, and a program without heavy subtrees has none."""
+def test_window_cut_code(native, env):
+    """The window kernels' code (layout 2): C5's tree gets its 12 leaf subtrees' cut code
+    (s_bitcmp1 s7, 12: phase A only; class 1..12 into s52, a jump to the cut routine), the code
+    decodes and re-encodes exactly, and a program without heavy subtrees has no cut code.
+    Layout 3 (the retired path-sorted prefix) is rejected."""
     import re
     from generic_ebpf_amd import workloads
     p = native.Prog(env, workloads.prog_c5().code)
     try:
-        whole = p.device_code(0)
-        prefix = p.device_code(3)
-        out, err = _decode(prefix)
+        code = p.device_code(2)
+        out, err = _decode(code)
         assert "invalid" not in err
-        assert len(prefix) * 10 < len(whole)
-        assert len(re.findall(r"s_mov_b32 s52, s14", out)) == 12
+        assert len(re.findall(r"s_bitcmp1_b32 s7, 12", out)) == 12
+        lines = [ln.strip() for ln in out.splitlines()]
+        cls = [int(lines[i + 2].split(",")[1]) for i, ln in enumerate(lines)
+               if ln == "s_bitcmp1_b32 s7, 12" and lines[i + 2].startswith("s_mov_b32 s52,")]
+        assert sorted(cls) == list(range(1, 13))
+        enc, _ = _encodings(code)
+        assert enc == code
+        with pytest.raises(native.EbpfError):
+            p.device_code(3)
     finally:
         p.destroy()
     p = native.Prog(env, workloads.prog_c3().code)
     try:
-        with pytest.raises(native.EbpfError):
-            p.device_code(3)
+        assert "s_bitcmp1_b32 s7, 12" not in _decode(p.device_code(2))[0]
     finally:
         p.destroy()

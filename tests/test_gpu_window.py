@@ -1,5 +1,5 @@
 """Window launches (gpu_runtime.cpp launch_windowed, gen_interp.py "Window mode", asm_jit.cpp cut
-code, asm_cc.cpp cc_pathsort_plan cut points).
+code, asm_cc.cpp cc_cut_plan cut points).
 
 A batch in offsets form run by a compiled program that reads past the first 64 bytes goes
 through the span image in windows: up to 256 packets staged in LDS by one contiguous DMA, every
@@ -158,7 +158,7 @@ def test_window_random_programs(gpu, env, monkeypatch):
     entries and the batch threshold at 1 packet: cut points anywhere in the trees.  Every fourth
     program stores into its packets (no window: the plain launch)."""
     from generic_ebpf_amd import randprog
-    monkeypatch.setenv("EBPF_PATHSORT_MIN", "2")
+    monkeypatch.setenv("EBPF_WIN_CUT_MIN", "2")
     monkeypatch.setenv("EBPF_WINDOW_MINBATCH", "1")
     windowed = 0
     for k in range(60):

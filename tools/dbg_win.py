@@ -27,7 +27,7 @@ data = g.integers(0, 256, int(offs[-1]) + 64, dtype=np.uint8)
 c = goldens.Case("w", lay.code, list(lay.relocs), maps, data, n, 0, offs)
 want, wf, _, _ = oracle_run(c, nthreads=4)
 print("oracle", want[:4], wf[:4])
-os.environ["EBPF_PATHSORT_MIN"] = "2"
+os.environ["EBPF_WIN_CUT_MIN"] = "2"
 os.environ["EBPF_WINDOW_MINBATCH"] = "1"
 for name, envs, variant in (("plain", {"EBPF_WINDOW": "0"}, 0), ("window", {"EBPF_WINDOW": "1"}, 0),
                             ("window-nocut", {"EBPF_WINDOW": "1", "EBPF_WINDOW_NOCUT": "1"}, 0),

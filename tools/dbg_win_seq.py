@@ -13,7 +13,7 @@ import goldens  # noqa: E402
 from helpers import oracle_run, make_maps  # noqa: E402
 from generic_ebpf_amd import randprog, native  # noqa: E402
 
-os.environ["EBPF_PATHSORT_MIN"] = "2"
+os.environ["EBPF_WIN_CUT_MIN"] = "2"
 os.environ["EBPF_WINDOW_MINBATCH"] = "1"
 env = native.Env()
 

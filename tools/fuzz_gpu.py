@@ -1,10 +1,9 @@
 """Randomised parity sweep on the GPU (a longer run than tests/test_gpu_parity.py): seeded random
 programs (generic-ebpf_amd/randprog.py: every opcode and reference quirk) on the device against the
 oracle, for every device variant, on both kernels: 64-B packets (staged) and packets of random
-length 16..79 at CSR offsets (general kernels, short packets fault), and with regrouping forced
-(EBPF_CC_REGROUP=1, size thresholds 2 and 1: most random programs get regroup points, so random
-subtrees are queued and batched), and path-sorted (EBPF_PATHSORT=1 with cut threshold 2 and no
-batch threshold: random programs are cut anywhere, their packets sorted by the subtree reached).
+length 16..79 at CSR offsets (general kernels, short packets fault), and as window launches
+(EBPF_WINDOW=1 with cut threshold 2 and no batch threshold: random programs are cut anywhere,
+their packets staged in LDS windows and sorted by the subtree reached).
 Odd-numbered programs also call map_update_elem / map_delete_elem (the device batch semantics).
 Compares results, fault codes, post-run packet bytes and the maps after the batch.
 --hash: the programs' two maps are hashtables instead (4-byte keys, a random live subset of a
@@ -266,20 +265,15 @@ def main():
         sys.exit(1 if failed else 0)
     failed = False
     configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
-    if not a.hash:
-        configs += [(0, "general", 2), (0, "general", 1)]   # regrouping, size threshold 2 / 1
-    configs += [(0, "general", "ps")]   # path-sorted launches, cut threshold 2, any batch size
+    configs += [(0, "general", "win")]   # window launches, cut threshold 2, any batch size
     for variant, layout, rg in configs:
-        if rg == "ps":
-            os.environ.update(EBPF_PATHSORT="1", EBPF_PATHSORT_MIN="2", EBPF_PATHSORT_MINBATCH="1")
-        elif rg:
-            os.environ["EBPF_CC_REGROUP"] = "1"
-            os.environ["EBPF_CC_RG_MIN"] = str(rg)
+        if rg == "win":
+            os.environ.update(EBPF_WINDOW="1", EBPF_WIN_CUT_MIN="2", EBPF_WINDOW_MINBATCH="1")
         t0 = time.time()
         bad, faults = [], 0
         for k in range(a.programs):
-            # (path-sorted launches take programs without map writes: those get none here)
-            c = case(k, a.seed, layout, a.hash, writes=False if rg == "ps" else None)
+            # (window launches take programs without map writes: those get none here)
+            c = case(k, a.seed, layout, a.hash, writes=False if rg == "win" else None)
             want, wf, wdata, wmaps = oracle(c)
             got, gf, gdata, gmaps = device(env, c, variant)
             faults += int(np.count_nonzero(wf))
@@ -288,12 +282,11 @@ def main():
                 bad.append(k)
             if k % 100 == 99:
                 print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        for k in ("EBPF_CC_REGROUP", "EBPF_CC_RG_MIN", "EBPF_PATHSORT", "EBPF_PATHSORT_MIN",
-                  "EBPF_PATHSORT_MINBATCH"):
+        for k in ("EBPF_WINDOW", "EBPF_WIN_CUT_MIN", "EBPF_WINDOW_MINBATCH"):
             os.environ.pop(k, None)
         print("%svariant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
             "hash " if a.hash else "", variant, layout,
-            " path-sorted" if rg == "ps" else " regroup>=%d" % rg if rg else "", a.programs, faults, len(bad), bad[:20],
+            " window" if rg == "win" else "", a.programs, faults, len(bad), bad[:20],
             time.time() - t0), flush=True)
         failed = failed or bool(bad)
     env.destroy()
