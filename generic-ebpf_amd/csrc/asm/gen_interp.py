@@ -725,10 +725,38 @@ def h_st_stk(z):
     return out
 
 
+FLAT_LOAD = {1: "flat_load_ubyte", 2: "flat_load_ushort", 4: "flat_load_dword", 8: "flat_load_dwordx2"}
+
+
 def gather(a0, acc, tmp, z, tag=None):
-    """acc (two VGPRs) = the z bytes at the flat address v[a0:a0+1], little-endian, byte by byte
-    (alignment-agnostic).  z: an int, or None for S_T0 bytes (4 or 8 at run time; `tag` names
-    the label)."""
+    """acc (two VGPRs) = the z bytes at the flat address v[a0:a0+1], little-endian.  z: an int
+    (tmp a list of z VGPRs: when every running lane's address is z-aligned, one flat load of z
+    bytes; else z byte loads issued together, one wait), or None for S_T0 bytes (4 or 8 at run
+    time, byte by byte; tmp one VGPR, `tag` names the label)."""
+    if z is not None:
+        t = tmp
+        out = []
+        if z > 1:
+            out += ["v_and_b32 %s, %d, %s" % (v(t[0]), z - 1, lo(a0)),
+                    "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(t[0])),
+                    "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+                    "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
+                    "s_cbranch_scc0 .Lg_una_%s" % tag]
+        out += ["%s %s, %s" % (FLAT_LOAD[z], vp(acc[0]) if z == 8 else v(acc[0]), vp(a0)),
+                "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+        if z < 8:
+            out.append("v_mov_b32 %s, 0" % v(acc[1]))
+        if z == 1:
+            return out
+        out += ["s_branch .Lg_done_%s" % tag, ".Lg_una_%s:" % tag]
+        out += ["flat_load_ubyte %s, %s offset:%d" % (v(t[b]), vp(a0), b) for b in range(z)]
+        out += ["s_waitcnt vmcnt(0) lgkmcnt(0)",
+                "v_mov_b32 %s, %s" % (v(acc[0]), v(t[0])), "v_mov_b32 %s, 0" % v(acc[1])]
+        for b in range(1, z):
+            tgt = v(acc[b // 4])
+            out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(t[b]), 8 * (b % 4), tgt))
+        out.append(".Lg_done_%s:" % tag)
+        return out
     out = ["v_mov_b32 %s, 0" % v(acc[0]), "v_mov_b32 %s, 0" % v(acc[1])]
     for b in range(z or 8):
         if z is None and b == 4:
@@ -743,7 +771,10 @@ def gather(a0, acc, tmp, z, tag=None):
 
 
 def vflags_test(bit, skip):
-    """scc = dp_launch.vflags bit `bit`; branches to `skip` when it is clear.  Clobbers S_T3."""
+    """Branches to `skip` when dp_launch.vflags bit `bit` is clear (bit 0, the overlay: s7 bit 13,
+    copied at kernel start; other bits: loaded, clobbering S_T3)."""
+    if bit == 0:
+        return ["s_bitcmp1_b32 s7, 13", "s_cbranch_scc0 %s" % skip]
     return ["s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
             "s_waitcnt lgkmcnt(0)",
             "s_bitcmp1_b32 %s, %d" % (s(S_T3), bit),
@@ -758,7 +789,7 @@ def h_ldx_gen(z, d, sr):
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
            "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 0" % s(S_T1)] + call(".Lr_check")
-    out += gather(a0, (H[2], H[3]), H[4], z)
+    out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}")
     out += vflags_test(0, ".Lnovl_{uid}") + call(".Lr_ovlfix") + [".Lnovl_{uid}:"]
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3]))]
     return out
@@ -841,7 +872,7 @@ def h_xadd(z, p, x, fetch):
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(p)),
            "v_mov_b32 %s, %s" % (v(H[2]), lo(x)), "v_mov_b32 %s, %s" % (v(H[3]), hi(x)),
            "s_mov_b32 %s, %d" % (s(S_T0), z), "s_mov_b32 %s, 3" % s(S_T1)] + call(".Lr_check")
-    out += gather(a0, old, H[4], z)
+    out += gather(a0, old, [H[4]] + R[4:11], z, "{uid}")
     out += ["v_lshl_add_u64 %s, %s, 0, %s" % (vp(nv[0]), vp(old[0]), vp(H[2]))]
     out += store_bytes(a0, [v(nv[0]), v(nv[1])], z)
     if fetch:
@@ -2151,7 +2182,14 @@ def kernel(name, staged, jit=False):
           "v_lshlrev_b32 v%d, 4, %s" % (V_L16, v(H[0])),
           "s_mov_b32 %s, -1" % s(S_PREVG),
           "s_waitcnt lgkmcnt(0)",
-          "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0))]
+          "s_mov_b32 s7, %d" % ((1 if staged else 0) | (2 if jit else 0)),
+          # s7 bit 13: the program reads its own stores into map values (dp_launch.vflags bit 0)
+          "s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
+          "s_waitcnt lgkmcnt(0)",
+          "s_bitcmp1_b32 %s, 0" % s(S_T3),
+          "s_cbranch_scc0 .L%s_noovl" % k,
+          "s_or_b32 s7, s7, 0x2000",
+          ".L%s_noovl:" % k]
     if not staged:   # header staging requested by the host (dp_launch.lds_pkt_base bit 31)
         L += ["s_bitcmp1_b32 %s, 31" % s(S_PKTLDS),
               "s_cbranch_scc0 .L%s_nogs" % k,
