@@ -258,6 +258,11 @@ for z in (4, 8):
 # mirror's address, low word; s14 = the offset + the table's LDS address)
 for z in (4, 8):
     fam("CNTAL%d" % z, 1)
+# a load through a packet pointer at an offset only known at run time (translate.cpp AV_CTXV:
+# a cursor advanced in a loop): one bounds check against the lane's packet, one load; lanes whose
+# address leaves the packet take the generic path (s[10:11] = the offset)
+for z in SIZES:
+    fam("LDXPKTV%d" % z, 2)
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 # the lane's stack slice below the frame (dprog.h DP_OVL_*): loop count, overlay count, the
 # scratch a store into a map value is redirected to, the overlay entries
@@ -737,7 +742,7 @@ def gather(a0, acc, tmp, z, tag=None):
         t = tmp
         out = []
         if z > 1:
-            out += ["v_and_b32 %s, %d, %s" % (v(t[0]), z - 1, lo(a0)),
+            out += ["v_and_b32 %s, %d, %s" % (v(t[0]), z - 1, v(a0)),
                     "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(t[0])),
                     "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
                     "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
@@ -792,6 +797,32 @@ def h_ldx_gen(z, d, sr):
     out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}")
     out += vflags_test(0, ".Lnovl_{uid}") + call(".Lr_ovlfix") + [".Lnovl_{uid}:"]
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3]))]
+    return out
+
+
+def h_ldx_pktv(z, d, sr):
+    """LDXPKTV: address = r_src + sext(off); when every running lane's address holds z bytes of
+    its own packet ([V_PKT, V_PKT + V_LEN)), one flat load (or z byte loads when unaligned);
+    otherwise the generic load (region check, faults) for all of them."""
+    a0 = H[0]
+    out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
+           "v_sub_co_u32 %s, vcc, %s, v%d" % (v(H[2]), v(a0), V_PKT),
+           "v_subb_co_u32 %s, vcc, %s, v%d, vcc" % (v(H[3]), v(a0 + 1), V_PKT + 1),
+           "v_subrev_u32 %s, %d, v%d" % (v(H[4]), z, V_LEN),
+           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[3])),
+           "v_cmp_le_u32_e64 vcc, %s, %s" % (v(H[2]), v(H[4])),
+           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+           "v_cmp_le_u32_e64 vcc, %d, v%d" % (z, V_LEN),
+           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+           "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
+           "s_cbranch_scc0 .Lpv_gen_{uid}"]
+    out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}f")
+    out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3])),
+            "s_branch .Lpv_done_{uid}",
+            ".Lpv_gen_{uid}:"]
+    out += h_ldx_gen(z, d, sr)
+    out.append(".Lpv_done_{uid}:")
     return out
 
 
@@ -1714,6 +1745,8 @@ def handler_body(name, d, sr):
         return h_st_stk(int(name[5:])), False
     if name.startswith("LDXGEN"):
         return h_ldx_gen(int(name[6:]), d, sr), False
+    if name.startswith("LDXPKTV"):
+        return h_ldx_pktv(int(name[7:]), d, sr), False
     if name.startswith("LDXMAP"):
         return h_ldx_map(int(name[6:]), d, sr), False
     if name.startswith("LDXHV"):
@@ -3370,6 +3403,14 @@ def generate(out_s, staged_image):
     A += [".p2align 2", "ebpf_jit_meta:"] + meta
     A += jit_templates()
     A += [".p2align 8", "ebpf_jit_area:", "  .fill %d, 4, 0xbf810000" % (JIT_AREA_BYTES // 4)]
+    # every VGPR the image's code names lies inside the kernels' allocation (a register past it
+    # assembles but reads whatever the hardware holds there)
+    vtop = 0
+    for ln in A:
+        code = ln.split(";")[0].split("//")[0]
+        for a, b, c in re.findall(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]", code):
+            vtop = max(vtop, int(a or c))
+    assert vtop < NVGPR, "image code uses v%d, the kernels allocate %d VGPRs" % (vtop, NVGPR)
     kernarg = 232
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_SPAN if SPAN_IMAGE else NSGPR_GEN
     if INTERP_IMAGE:

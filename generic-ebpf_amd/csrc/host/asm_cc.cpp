@@ -1558,11 +1558,11 @@ copied_result(int fam)
 {
 	switch (fam) {
 	case AHF_LDXGEN1: case AHF_LDXMAP1: case AHF_LDXPKTG1: case AHF_LDXSTK1: case AHF_LDXHV1:
-	case AHF_LDXPKC1: return kbits(8);
+	case AHF_LDXPKC1: case AHF_LDXPKTV1: return kbits(8);
 	case AHF_LDXGEN2: case AHF_LDXMAP2: case AHF_LDXPKTG2: case AHF_LDXSTK2: case AHF_LDXHV2:
-	case AHF_LDXPKC2: return kbits(16);
+	case AHF_LDXPKC2: case AHF_LDXPKTV2: return kbits(16);
 	case AHF_LDXGEN4: case AHF_LDXMAP4: case AHF_LDXPKTG4: case AHF_LDXSTK4: case AHF_LDXHV4:
-	case AHF_LDXPKC4: case AHF_XADDF4: return kbits(32);
+	case AHF_LDXPKC4: case AHF_XADDF4: case AHF_LDXPKTV4: return kbits(32);
 	default:
 		if (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)
 			return kbits(32);
@@ -2251,7 +2251,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				if (!out[e].fast &&
 				    ((fam >= AHF_LDXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
 				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN ||
-				     is_value_store_fam(fam) ||
+				     (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8) || is_value_store_fam(fam) ||
 				     fam == AHF_UPDATE || fam == AHF_HDELETE))
 					needs_pkt = true;
 			}

@@ -176,6 +176,8 @@ enum av_kind : uint8_t {
 	AV_STACK,       // stack top (r10 at entry) + off
 	AV_MAPVAL,      // value of map #map (dp_map table index) + off, never NULL
 	AV_MAPVAL_NULL, // as AV_MAPVAL, or NULL (a lookup result not yet NULL-checked)
+	AV_CTXV,        // packet start + an offset not known at translation time (a cursor advanced
+	                // in a loop, merged paths): a packet pointer, never the stack or a map value
 };
 struct av {
 	uint8_t kind = AV_UNKNOWN;

@@ -481,7 +481,20 @@ add_av(const av &d, const av &s)
 		return mk(d.kind, (int64_t)((uint64_t)d.off + (uint64_t)s.off), d.map);
 	if (d.kind == AV_CONST && is_ptr(s))
 		return mk(s.kind, (int64_t)((uint64_t)s.off + (uint64_t)d.off), s.map);
+	if ((d.kind == AV_CTXV && s.kind == AV_CONST) || (d.kind == AV_CONST && s.kind == AV_CTXV))
+		return mk(AV_CTXV);
 	return av();
+}
+
+// Two paths meet: the same value, or two packet pointers (one with an unknown offset), else
+// unknown
+av
+meet_av(const av &a, const av &b)
+{
+	if (a == b)
+		return a;
+	const bool pa = a.kind == AV_CTX || a.kind == AV_CTXV, pb = b.kind == AV_CTX || b.kind == AV_CTXV;
+	return pa && pb ? mk(AV_CTXV) : av();
 }
 
 void
@@ -623,11 +636,13 @@ dataflow(dprog_host &out)
 				a.reached = true;
 				changed = true;
 			} else {
-				for (int i = 0; i < EBPF_REG_MAX; i++)
-					if (a.in[i] != re[i] && a.in[i].kind != AV_UNKNOWN) {
-						a.in[i] = av();
+				for (int i = 0; i < EBPF_REG_MAX; i++) {
+					const av m = meet_av(a.in[i], re[i]);
+					if (m != a.in[i]) {
+						a.in[i] = m;
 						changed = true;
 					}
+				}
 			}
 			if (changed && !queued[sx]) {
 				queued[sx] = 1;
@@ -747,7 +762,7 @@ analyze_writes(dprog_host &out)
 			return false;
 		*base = out.annot[i].in[e.dst];
 		// (the stack and the packet are never a map's values)
-		return base->kind != AV_STACK && base->kind != AV_CTX;
+		return base->kind != AV_STACK && base->kind != AV_CTX && base->kind != AV_CTXV;
 	};
 	auto size_of = [](const dp_entry &e) -> uint32_t {
 		if (e.kind == DK_CNT_STORE || e.kind == DK_XADD)
@@ -866,7 +881,7 @@ analyze_writes(dprog_host &out)
 			out.vstore_overlay = true; // (they read the value back first)
 		} else if (e.kind < 0x100 && (e.kind & 7) == EBPF_CLS_LDX) {
 			const av &b = out.annot[i].in[e.src];
-			out.vstore_overlay = b.kind != AV_STACK && b.kind != AV_CTX;
+			out.vstore_overlay = b.kind != AV_STACK && b.kind != AV_CTX && b.kind != AV_CTXV;
 		}
 	}
 	// per path: records the log needs, stores the overlay holds
