@@ -91,10 +91,11 @@ def parse(argv=None):
                     help="event-time the kernel of every k-th timed step (default 2: the events come from the kernel's own dispatch packet, ebpf_gpu_time_next_launch, so a timed step costs no extra GPU-side marker)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every step (launches never queue)")
-    ap.add_argument("--also", default="c2,c3,c5,c4h",
+    ap.add_argument("--also", default="c2,c3,c5,c4h,c4c,c3l",
                     help="comma-separated further configs measured in the same run (sharded the same way) "
                          "and reported under 'also' (default: every other BASELINE config -- C2, C3, C5 "
-                         "the IMIX filter -- and C4H, the hashtable form of C4); '' for none")
+                         "the IMIX filter -- C4H, the hashtable form of C4, C4C, C4 with a per-key "
+                         "counter update, and C3L, a bounded loop under standard semantics); '' for none")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)
