@@ -817,6 +817,37 @@ def h_ldx_pktv(z, d, sr):
            "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
            "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
            "s_cbranch_scc0 .Lpv_gen_{uid}"]
+    if STAGED_IMAGE:
+        # keep mode (s7 bit 14): the group's packets stay in the wave's LDS packet buffer while
+        # the program runs (lane l's 64 bytes at S_PKTLDS + 64 l), so read them there: one
+        # ds_read when every lane's offset is z-aligned, else z byte reads issued together
+        out += ["s_bitcmp1_b32 s7, 14",
+                "s_cbranch_scc0 .Lpv_flat_{uid}",
+                "v_lshl_add_u32 %s, v%d, 2, %s" % (v(H[4]), V_L16, v(H[2])),
+                "v_add_u32 %s, %s, %s" % (v(H[4]), s(S_PKTLDS), v(H[4]))]
+        if z > 1:
+            out += ["v_and_b32 %s, %d, %s" % (v(H[5]), z - 1, v(H[2])),
+                    "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[5])),
+                    "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+                    "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
+                    "s_cbranch_scc0 .Lpv_lu_{uid}"]
+        rd = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[z]
+        out += ["%s %s, %s" % (rd, pair(d) if z == 8 else lo(d), v(H[4])),
+                "s_waitcnt lgkmcnt(0)"]
+        if z < 8:
+            out.append("v_mov_b32 %s, 0" % hi(d))
+        out.append("s_branch .Lpv_done_{uid}")
+        if z > 1:
+            t = [H[5]] + R[:7]
+            out.append(".Lpv_lu_{uid}:")
+            out += ["ds_read_u8 %s, %s offset:%d" % (v(t[b]), v(H[4]), b) for b in range(z)]
+            out += ["s_waitcnt lgkmcnt(0)", "v_mov_b32 %s, 0" % hi(d),
+                    "v_mov_b32 %s, %s" % (lo(d), v(t[0]))]
+            for b in range(1, z):
+                tgt = lo(d) if b < 4 else hi(d)
+                out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(t[b]), 8 * (b % 4), tgt))
+            out.append("s_branch .Lpv_done_{uid}")
+        out.append(".Lpv_flat_{uid}:")
     out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}f")
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3])),
             "s_branch .Lpv_done_{uid}",
@@ -2223,6 +2254,17 @@ def kernel(name, staged, jit=False):
           "s_cbranch_scc0 .L%s_noovl" % k,
           "s_or_b32 s7, s7, 0x2000",
           ".L%s_noovl:" % k]
+    if staged and jit:
+        # s7 bit 14 (keep mode): the compiled program reads its packet at run-time offsets from
+        # the LDS packet buffer (LDXPKTV), so the next group's DMA waits for the group's end
+        # (flags word at the head of the code area, asm_jit.cpp JIT_HDR_KEEP_PKT)
+        L += raddr("ebpf_jit_area", S_JUNK) + [
+            "s_load_dword %s, %s, 0x0" % (s(S_T3), sp(S_JUNK)),
+            "s_waitcnt lgkmcnt(0)",
+            "s_bitcmp1_b32 %s, 0" % s(S_T3),
+            "s_cbranch_scc0 .L%s_nokeep" % k,
+            "s_or_b32 s7, s7, 0x4000",
+            ".L%s_nokeep:" % k]
     if not staged:   # header staging requested by the host (dp_launch.lds_pkt_base bit 31)
         L += ["s_bitcmp1_b32 %s, 31" % s(S_PKTLDS),
               "s_cbranch_scc0 .L%s_nogs" % k,
@@ -2824,6 +2866,11 @@ def common_group_code():
           "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
           "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
           ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
+          # keep mode (s7 bit 14): the next group's DMA, now that the program is done with the
+          # packet buffer
+          "s_bitcmp1_b32 s7, 14",
+          "s_cbranch_scc0 .Lgd_nokeep"] + call(".Lr_prefetch") + [
+          ".Lgd_nokeep:",
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),
           ".Lgroup_check:",
           "s_mov_b64 exec, -1",
@@ -2864,8 +2911,12 @@ def common_group_code():
     # group through the masking routine
     # (s7 bit 4: a program that probes memory issues this DMA itself right after its first
     # probe, so the two latencies overlap — see .Lr_dma_next; bit 5: issued for this group)
+    # (keep mode, s7 bit 14: none here; .Lgroup_done issues it once the program is done with
+    # the buffer)
     L += ["s_waitcnt lgkmcnt(0)",
-          "s_or_b32 s7, s7, 32"] + next_group(S_T0) + [
+          "s_or_b32 s7, s7, 32",
+          "s_bitcmp1_b32 s7, 14",
+          "s_cbranch_scc1 .Lgs_pf_keep"] + next_group(S_T0) + [
           "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),        # full groups
           "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
           "s_cbranch_scc0 .Lgs_pf_slow",
@@ -2883,6 +2934,9 @@ def common_group_code():
           "s_nop 0"] + [
           "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
           for qq in range(4)] + [
+          "s_branch .Lgs_pf_done",
+          ".Lgs_pf_keep:",
+          "s_and_b32 s7, s7, ~32",
           "s_branch .Lgs_pf_done",
           ".Lgs_pf_slow:"] + call(".Lr_prefetch") + [
           ".Lgs_pf_done:",

@@ -175,7 +175,7 @@ layout_order(const dprog_host &xl, const std::vector<dp_entry> &low)
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
 // *win_cuts (mode 2): the cut points of the window launches' phase A.
-// Area layout: +0 16 bytes of s_endpgm, +16 the program's start block (where the kernel enters
+// Area layout: +0 a flags word (JIT_HDR_*) and 12 bytes of s_endpgm, +16 the program's start block (where the kernel enters
 // each group), then the blocks.
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
@@ -235,6 +235,24 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		if (needs_branch(e))
 			entry_point[succ(e)] = 1;
 	}
+	// Loop back edges (standard semantics: a conditional whose taken side is a LOOPCNT entry)
+	// split the other way round: the lanes that stay in the loop continue, the lanes that leave
+	// it park at the fall-through block, and when no lane loops any more the scheduler resumes
+	// every parked lane of that exit together.  (The forward split would run the loop's tail
+	// once per distinct trip count in the group.)  The fall-through block becomes an entry point.
+	std::vector<char> rev_cond(n, 0);
+	if (getenv("EBPF_JIT_NOREVLOOP") == nullptr)
+		for (uint32_t e : order) {
+			const uint32_t h = (uint32_t)low[e].handler;
+			if (!(ah_flags[h] & 1))
+				continue;
+			const uint32_t tk = xl.entries[e].target, nx = xl.entries[e].next;
+			if (tk < n && nx < n && nx != tk && xl.entries[tk].kind == DK_LOOPCNT) {
+				rev_cond[e] = 1;
+				entry_point[nx] = 1;
+			}
+		}
+	const uint32_t RC = 48; // the reversed split up to its jump to the loop (see the emitter)
 	// Structured control flow (staged programs without generic lookups): every conditional
 	// splits exec into its fall-through lanes, which run first, and its taken lanes, whose mask
 	// waits in s[74 + 2d] (d = branches pending on the path) and which run when the fall-through
@@ -408,7 +426,9 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		if (structured && (ah_flags[h] & 1)) {
 			sz += long_cond[e] ? 12 + LJ : 12;
 		} else if (ah_flags[h] & 1) {
-			if (cb[e].sdir < 0)
+			if (cb[e].sdir < 0 && rev_cond[e])
+				sz += RC + (long_cond[e] ? LJ : 4);
+			else if (cb[e].sdir < 0)
 				sz += long_cond[e] ? cl_len : cs_len;
 			else if (cb[e].sdir == 1)
 				sz += long_cond[e] ? jl_len : 4; // always taken: a jump
@@ -458,7 +478,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				}
 			}
 			if (!structured && (ah_flags[h] & 1) && !long_cond[e] && cb[e].sdir != 0) {
-				const uint32_t br_at = pos[e] + be + (cb[e].sdir == 1 ? 0 : T[JT_CS_BR] - T[JT_CS]);
+				const uint32_t br_at = pos[e] + be + (cb[e].sdir == 1 ? 0 : rev_cond[e] ? RC :
+								      T[JT_CS_BR] - T[JT_CS]);
 				const uint32_t tk = xl.entries[e].target;
 				if (!fits_simm16((int64_t)pos[tk] - (int64_t)(br_at + 4))) {
 					long_cond[e] = 1;
@@ -518,7 +539,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			const int32_t d = ((int32_t)target_pos - (int32_t)(a + 4)) / 4;
 			put32(a, 0xbf800000u | (op << 16) | ((uint32_t)d & 0xffffu));
 		};
-		const uint32_t OP_BRANCH = 0x02, OP_EXECZ = 0x08, OP_EXECNZ = 0x09;
+		const uint32_t OP_BRANCH = 0x02, OP_SCC0 = 0x04, OP_EXECZ = 0x08, OP_EXECNZ = 0x09;
 		if (!push[e].empty()) {
 			memcpy(&img[area + at], push[e].data(), push[e].size());
 			at += push[e].size();
@@ -600,6 +621,38 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				put32(at + 4, code_off(tk));
 				at += jl_len;
 			}
+		} else if ((ah_flags[h] & 1) && cb[e].sdir < 0 && rev_cond[e]) {
+			// s_and_b64 s[48:49], vcc, exec          (lanes that loop)
+			// s_andn2_b64 s[18:19], exec, vcc        (lanes that leave; SCC = any)
+			// s_cbranch_scc0 .Lloop
+			// s_mov_b64 exec, s[18:19]
+			// v_mov_b32 v41, <code offset of the fall-through block>   (park them there)
+			// s_mov_b64 exec, s[48:49]
+			// s_cbranch_execnz .Lloop
+			// (long jump to .Lr_schedule)
+			// .Lloop: s_branch <taken block> (or a long jump)
+			const uint32_t tk = xl.entries[e].target, nx = xl.entries[e].next;
+			const size_t loop_at = at + RC;
+			put32(at, 0x80000000u | (0x0du << 23) | (48u << 16) | (126u << 8) | 106u);
+			put32(at + 4, 0x80000000u | (0x13u << 23) | (18u << 16) | (106u << 8) | 126u);
+			sopp(at + 8, OP_SCC0, (uint32_t)loop_at);
+			put32(at + 12, 0xbe800000u | (126u << 16) | (0x01u << 8) | 18u);
+			put32(at + 16, 0x7e000000u | (41u << 17) | (0x01u << 9) | 255u);
+			put32(at + 20, code_off(nx));
+			put32(at + 24, 0xbe800000u | (126u << 16) | (0x01u << 8) | 48u);
+			sopp(at + 28, OP_EXECNZ, (uint32_t)loop_at);
+			put32(at + 32, 0x80000000u | (60u << 16) | (255u << 8) | 4u);
+			put32(at + 36, T[JT_SCHED]);
+			put32(at + 40, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
+			put32(at + 44, 0xbe800000u | (0x1du << 8) | 60u);
+			at = loop_at;
+			if (!long_cond[e]) {
+				sopp(at, OP_BRANCH, pos[tk]);
+				at += 4;
+			} else {
+				long_jump(at, pos[tk]);
+				at += LJ;
+			}
 		} else if ((ah_flags[h] & 1) && cb[e].sdir < 0) {
 			const uint32_t tk = xl.entries[e].target;
 			if (!long_cond[e]) {
@@ -648,6 +701,17 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
 		put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
 	}
+	// the area's first word (never executed: code starts at +16) is read by the staged kernel's
+	// start: bit 0 = keep mode (gen_interp.py, s7 bit 14), when a packet load at a run-time
+	// offset (LDXPKTV) reads the wave's LDS packet buffer, so the next group's DMA waits
+	if (gm == 1 && getenv("EBPF_JIT_NOKEEP") == nullptr)
+		for (uint32_t e : order) {
+			const int fam = ah_fam[(uint32_t)low[e].handler];
+			if (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8) {
+				put32(0, JIT_HDR_KEEP_PKT);
+				break;
+			}
+		}
 	if (code)
 		code->assign(img.begin() + area, img.begin() + area + total);
 	return 0;

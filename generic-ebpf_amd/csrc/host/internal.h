@@ -120,6 +120,9 @@ constexpr uint32_t kWinMinBytes = 4096;
 constexpr int kModes = 3;
 // Window launches: the most cut points of a program (classes 1..15; 0 = no cut reached)
 constexpr uint32_t kPathMaxCuts = 15;
+// Staged compiled programs: flags word at the head of the code area (asm_jit.cpp), bit 0 = keep
+// the group's packets in the LDS buffer until the program is done (LDXPKTV reads them there)
+constexpr uint32_t JIT_HDR_KEEP_PKT = 1;
 constexpr int kInterpStagedImage = 3;
 extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
     ebpf_asm_hsaco_m3[];
@@ -177,7 +180,11 @@ enum av_kind : uint8_t {
 	AV_MAPVAL,      // value of map #map (dp_map table index) + off, never NULL
 	AV_MAPVAL_NULL, // as AV_MAPVAL, or NULL (a lookup result not yet NULL-checked)
 	AV_CTXV,        // packet start + an offset not known at translation time (a cursor advanced
-	                // in a loop, merged paths): a packet pointer, never the stack or a map value
+	                // in a loop, merged paths, advanced by an AV_SCALAR): a packet pointer, never
+	                // the stack or a map value
+	AV_SCALAR,      // a number not derived from any pointer: packet bytes, constants and ALU on
+	                // them (a TLV length).  (Stack and map-value loads may return spilled
+	                // pointers: they stay AV_UNKNOWN.)
 };
 struct av {
 	uint8_t kind = AV_UNKNOWN;

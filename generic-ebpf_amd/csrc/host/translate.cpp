@@ -471,6 +471,13 @@ is_ptr(const av &a)
 	return a.kind == AV_CTX || a.kind == AV_STACK || a.kind == AV_MAPVAL;
 }
 
+// a number (a constant or an AV_SCALAR): nothing in it came from a pointer
+bool
+is_num(const av &a)
+{
+	return a.kind == AV_CONST || a.kind == AV_SCALAR;
+}
+
 // dst + src for ADD64 / MOV64 (which adds, ebpf_interpreter.c:197-202)
 av
 add_av(const av &d, const av &s)
@@ -481,20 +488,27 @@ add_av(const av &d, const av &s)
 		return mk(d.kind, (int64_t)((uint64_t)d.off + (uint64_t)s.off), d.map);
 	if (d.kind == AV_CONST && is_ptr(s))
 		return mk(s.kind, (int64_t)((uint64_t)s.off + (uint64_t)d.off), s.map);
-	if ((d.kind == AV_CTXV && s.kind == AV_CONST) || (d.kind == AV_CONST && s.kind == AV_CTXV))
+	// a packet pointer moved by a number no pointer went into (a TLV walk's length field) is
+	// still a packet pointer; numbers combine into numbers
+	const bool pd = d.kind == AV_CTX || d.kind == AV_CTXV, ps = s.kind == AV_CTX || s.kind == AV_CTXV;
+	if ((pd && is_num(s)) || (is_num(d) && ps))
 		return mk(AV_CTXV);
+	if (is_num(d) && is_num(s))
+		return mk(AV_SCALAR);
 	return av();
 }
 
-// Two paths meet: the same value, or two packet pointers (one with an unknown offset), else
-// unknown
+// Two paths meet: the same value, two packet pointers (one with an unknown offset), two numbers,
+// else unknown
 av
 meet_av(const av &a, const av &b)
 {
 	if (a == b)
 		return a;
 	const bool pa = a.kind == AV_CTX || a.kind == AV_CTXV, pb = b.kind == AV_CTX || b.kind == AV_CTXV;
-	return pa && pb ? mk(AV_CTXV) : av();
+	if (pa && pb)
+		return mk(AV_CTXV);
+	return is_num(a) && is_num(b) ? mk(AV_SCALAR) : av();
 }
 
 void
@@ -507,8 +521,10 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		r[e.dst] = r[e.src];
 		return;
 	}
-	if (k >= DK_NEG64 && k <= DK_MOD32Z) {
-		r[e.dst] = av();
+	if (k >= DK_NEG64 && k <= DK_MOD32Z) { // (numbers stay numbers)
+		const bool reads_src = k == DK_ARSH64R || k == DK_ARSH32R || k >= DK_DIV64Z;
+		const bool num = is_num(r[e.dst]) && (!reads_src || is_num(r[e.src]));
+		r[e.dst] = num ? mk(AV_SCALAR) : av();
 		return;
 	}
 	if (k == DK_CALL_LOOKUP) {
@@ -540,8 +556,9 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 	const uint8_t cls = k & 7;
 	if (cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32 || cls == EBPF_CLS_ST || cls == EBPF_CLS_STX)
 		return;
-	if (cls == EBPF_CLS_LDX) {
-		r[e.dst] = av();
+	if (cls == EBPF_CLS_LDX) { // packet bytes are numbers; the stack and map values may hold pointers
+		const uint8_t b = r[e.src].kind;
+		r[e.dst] = (b == AV_CTX || b == AV_CTXV) ? mk(AV_SCALAR) : av();
 		return;
 	}
 	if (k == EBPF_OP_LDDW) {
@@ -559,6 +576,8 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		if (s.kind == AV_CONST) {
 			av neg = mk(AV_CONST, (int64_t)(0 - (uint64_t)s.off));
 			d = add_av(d, neg);
+		} else if (s.kind == AV_SCALAR && (d.kind == AV_CTX || d.kind == AV_CTXV || is_num(d))) {
+			d = add_av(d, s); // (the sign does not matter to the kind)
 		} else {
 			d = av();
 		}
@@ -567,13 +586,13 @@ transfer(const dp_entry &e, const dprog_host &out, av r[EBPF_REG_MAX])
 		d = mk(AV_CONST, (int64_t)(uint32_t)e.imm);
 		break;
 	case EBPF_OP_MOV_REG:
-		d = s.kind == AV_CONST ? mk(AV_CONST, (int64_t)(uint32_t)s.off) : av();
+		d = s.kind == AV_CONST ? mk(AV_CONST, (int64_t)(uint32_t)s.off) : is_num(s) ? mk(AV_SCALAR) : av();
 		break;
 	case EBPF_OP_NEG:
 		d = mk(AV_CONST, (int64_t)(uint32_t)(0u - (uint32_t)e.imm));
 		break;
-	default:
-		d = av();
+	default: // other ALU: numbers in, a number out
+		d = is_num(d) && ((k & 0x08) == 0 || is_num(s)) ? mk(AV_SCALAR) : av();
 		break;
 	}
 }

@@ -256,3 +256,32 @@ def gen_loop_program(seed, length=30, forever_every=0):
                   I("ja", off="H"), ("label", "F")]
     items += [I("xor64_reg", 0, int(g.choice(regs))), I("exit")]
     return asm(items)
+
+
+def gen_cursor_program(seed):
+    """A standard program that walks the packet with a cursor in a loop (the C3L / TLV shape:
+    packet loads at run-time offsets): r7 = ctx + a start offset, a trip count of 1-16 from a
+    packet byte, and per trip 1-3 loads of 1/2/4/8 bytes at small offsets from the cursor (any
+    alignment) mixed into r0, then the cursor advances by a constant or by a packet byte (0-7).
+    Cursors that run past the packet end fault MEM, as in the reference's bounds check."""
+    g = np.random.default_rng(seed)
+    items = [I("mov64_reg", 6, 1), I("mov64_imm", 0, imm=int(g.integers(0, 2**31))),
+             I("mov64_reg", 7, 6), I("add64_imm", 7, imm=int(g.integers(0, 9))),
+             I("ldxb", 8, 6, int(g.integers(0, 64))), I("and64_imm", 8, imm=15),
+             I("add64_imm", 8, imm=1), ("label", "L")]
+    for _ in range(int(g.integers(1, 4))):
+        z = int(g.choice([1, 2, 4, 8]))
+        op = {1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[z]
+        items += [I(op, 2, 7, int(g.integers(0, 4))), I("mul64_imm", 0, imm=31),
+                  I("add64_reg", 0, 2)]
+    if g.random() < 0.5:
+        items.append(I("add64_imm", 7, imm=int(g.integers(3, 8))))
+    else:
+        items += [I("ldxb", 3, 7, 0), I("and64_imm", 3, imm=7), I("add64_reg", 7, 3)]
+    items.append(I("sub64_imm", 8, imm=1))
+    if g.random() < 0.7:
+        items.append(I("jne_imm", 8, imm=0, off="L"))
+    else:   # exit test forward, JA back
+        items += [I("jeq_imm", 8, imm=0, off="E"), I("ja", off="L"), ("label", "E")]
+    items += [I("ldxb", 2, 6, 1), I("xor64_reg", 0, 2), I("exit")]
+    return asm(items)

@@ -124,6 +124,30 @@ def test_loop_programs_vs_oracle(gpu, env, variant):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
+def test_cursor_loops_vs_oracle(gpu, env, variant):
+    """Packet walks with a cursor in a loop (LDXPKTV: loads at run-time offsets, any alignment,
+    cursors running off the end fault MEM) against the oracle.  Staged 64-B batches of 600,001
+    packets (many groups per wave: the compiled program reads the LDS packet buffer, whose next
+    DMA waits for the group's end; a partial last group) and general 72-B batches."""
+    bad, outcomes = [], set()
+    for seed in range(12):
+        code, rel = stdprogs.gen_cursor_program(7000 + seed)
+        g = np.random.default_rng(seed)
+        stride = 64 if seed % 3 else 72
+        n = 600001 if stride == 64 else 20011
+        pk = g.integers(0, 256, (n, stride), dtype=np.uint8)
+        want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(
+            pk.reshape(-1), n, stride, nthreads=8)
+        got, gf = run_device(gpu, env, code, rel, [], pk.reshape(-1), n, stride, variant,
+                             want_exec="compiled" if variant == 0 else None)
+        if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+            bad.append((seed, int(np.count_nonzero(want != got)), int(np.count_nonzero(wf != gf))))
+        outcomes |= set(int(x) for x in np.unique(wf))
+    assert not bad, bad
+    assert {0, 3} <= outcomes
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_c3l_full_size(gpu, env, variant):
     """The bench's loop workload (C3L: IPv4 header checksum over IHL words, 5-12 trips) over 16M
     packets tiled from 256k distinct: result i equals the oracle's for its distinct packet (and
