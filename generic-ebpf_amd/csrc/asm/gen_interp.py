@@ -802,52 +802,54 @@ def h_ldx_gen(z, d, sr):
 
 def h_ldx_pktv(z, d, sr):
     """LDXPKTV: address = r_src + sext(off); when every running lane's address holds z bytes of
-    its own packet ([V_PKT, V_PKT + V_LEN)), one flat load (or z byte loads when unaligned);
-    otherwise the generic load (region check, faults) for all of them."""
+    its own packet ([V_PKT, V_PKT + V_LEN)), one flat load (or z byte loads when unaligned) —
+    in the staged kernel's keep mode from the LDS packet buffer instead; otherwise the generic
+    load (region check, faults) for all of them."""
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
            "v_sub_co_u32 %s, vcc, %s, v%d" % (v(H[2]), v(a0), V_PKT),
            "v_subb_co_u32 %s, vcc, %s, v%d, vcc" % (v(H[3]), v(a0 + 1), V_PKT + 1),
-           "v_subrev_u32 %s, %d, v%d" % (v(H[4]), z, V_LEN),
-           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[3])),
-           "v_cmp_le_u32_e64 vcc, %s, %s" % (v(H[2]), v(H[4])),
-           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-           "v_cmp_le_u32_e64 vcc, %d, v%d" % (z, V_LEN),
-           "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-           "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
-           "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
-           "s_cbranch_scc0 .Lpv_gen_{uid}"]
+           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[3]))]
+    if STAGED_IMAGE:   # (every packet is 64 bytes)
+        out += ["v_cmp_ge_u32_e64 vcc, %d, %s" % (64 - z, v(H[2]))]
+    else:
+        out += ["v_subrev_u32 %s, %d, v%d" % (v(H[4]), z, V_LEN),
+                "v_cmp_le_u32_e64 vcc, %s, %s" % (v(H[2]), v(H[4])),
+                "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+                "v_cmp_le_u32_e64 vcc, %d, v%d" % (z, V_LEN)]
+    out += ["s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+            "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+            "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
+            "s_cbranch_scc0 .Lpv_gen_{uid}"]
     if STAGED_IMAGE:
         # keep mode (s7 bit 14): the group's packets stay in the wave's LDS packet buffer while
-        # the program runs (lane l's 64 bytes at S_PKTLDS + 64 l), so read them there: one
-        # ds_read when every lane's offset is z-aligned, else z byte reads issued together
+        # the program runs (lane l's 64 bytes at S_PKTLDS + 64 l), so read them there: the
+        # dwords around the bytes from the aligned address below them, then one byte align by
+        # the address's low bits (any alignment, no branch; a dword past the lane's 64 bytes is
+        # read but never selected)
+        A, B = v(H[4]), v(H[5])
         out += ["s_bitcmp1_b32 s7, 14",
                 "s_cbranch_scc0 .Lpv_flat_{uid}",
-                "v_lshl_add_u32 %s, v%d, 2, %s" % (v(H[4]), V_L16, v(H[2])),
-                "v_add_u32 %s, %s, %s" % (v(H[4]), s(S_PKTLDS), v(H[4]))]
-        if z > 1:
-            out += ["v_and_b32 %s, %d, %s" % (v(H[5]), z - 1, v(H[2])),
-                    "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[5])),
-                    "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
-                    "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
-                    "s_cbranch_scc0 .Lpv_lu_{uid}"]
-        rd = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[z]
-        out += ["%s %s, %s" % (rd, pair(d) if z == 8 else lo(d), v(H[4])),
-                "s_waitcnt lgkmcnt(0)"]
-        if z < 8:
-            out.append("v_mov_b32 %s, 0" % hi(d))
-        out.append("s_branch .Lpv_done_{uid}")
-        if z > 1:
-            t = [H[5]] + R[:7]
-            out.append(".Lpv_lu_{uid}:")
-            out += ["ds_read_u8 %s, %s offset:%d" % (v(t[b]), v(H[4]), b) for b in range(z)]
-            out += ["s_waitcnt lgkmcnt(0)", "v_mov_b32 %s, 0" % hi(d),
-                    "v_mov_b32 %s, %s" % (lo(d), v(t[0]))]
-            for b in range(1, z):
-                tgt = lo(d) if b < 4 else hi(d)
-                out.append("v_lshl_or_b32 %s, %s, %d, %s" % (tgt, v(t[b]), 8 * (b % 4), tgt))
-            out.append("s_branch .Lpv_done_{uid}")
-        out.append(".Lpv_flat_{uid}:")
+                "v_lshl_add_u32 %s, v%d, 2, %s" % (A, V_L16, v(H[2])),
+                "v_add_u32 %s, %s, %s" % (A, s(S_PKTLDS), A)]
+        if z == 1:
+            out += ["ds_read_u8 %s, %s" % (lo(d), A), "s_waitcnt lgkmcnt(0)",
+                    "v_mov_b32 %s, 0" % hi(d)]
+        else:
+            t0, t1, t2 = v(R[0]), v(R[1]), v(R[2])
+            out += ["v_and_b32 %s, -4, %s" % (B, A),
+                    "ds_read2_b32 v[%d:%d], %s offset1:1" % (R[0], R[1], B)]
+            if z == 8:
+                out.append("ds_read_b32 %s, %s offset:8" % (t2, B))
+            out += ["s_waitcnt lgkmcnt(0)",
+                    "v_alignbyte_b32 %s, %s, %s, %s" % (lo(d), t1, t0, A)]
+            if z == 8:
+                out.append("v_alignbyte_b32 %s, %s, %s, %s" % (hi(d), t2, t1, A))
+            else:
+                if z == 2:
+                    out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
+                out.append("v_mov_b32 %s, 0" % hi(d))
+        out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
     out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}f")
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3])),
             "s_branch .Lpv_done_{uid}",
@@ -1838,11 +1840,11 @@ def handler_body(name, d, sr):
         return ["v_mov_b32 %s, 0" % v(H[0]), "ds_write_b32 v%d, %s" % (V_STK, v(H[0]))], False
     if name == "LOOPCNT":
         # count the taken backward jump; lanes past the budget fault LOOP (EBPF_FAULT_LOOP = 8)
-        return ["ds_read_b32 %s, v%d" % (v(H[0]), V_STK),
+        # (one LDS add returning the count before it: past the budget when that is >= budget)
+        return ["v_mov_b32 %s, 1" % v(H[0]),
+                "ds_add_rtn_u32 %s, v%d, %s" % (v(H[0]), V_STK, v(H[0])),
                 "s_waitcnt lgkmcnt(0)",
-                "v_add_u32 %s, 1, %s" % (v(H[0]), v(H[0])),
-                "ds_write_b32 v%d, %s" % (V_STK, v(H[0])),
-                "v_cmp_lt_u32_e32 vcc, %d, %s" % (LOOP_BUDGET, v(H[0])),
+                "v_cmp_le_u32_e32 vcc, %d, %s" % (LOOP_BUDGET, v(H[0])),
                 "s_and_b64 %s, vcc, exec" % sp(S_MASK),
                 "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
                 "s_cbranch_scc1 .Lok_{uid}"] + fault_mask(S_MASK, 8) + [".Lok_{uid}:"], False

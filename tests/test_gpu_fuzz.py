@@ -1,0 +1,41 @@
+"""The GPU fuzzer (tools/fuzz_gpu.py) inside the suite, on seeds the fixed-seed parity tests do
+not use: random programs under the reference's semantics with array maps (every variant, staged
+and general kernels, window launches) and with hashtables, standard-semantics programs (loop-free,
+counted loops, cursor walks), and randomly edited programs the oracle finds defined.  Each mode
+compares results, fault codes, packet bytes after the batch and the maps with the oracle.  The
+long campaigns (thousands of programs per configuration) stay in tools/fuzz_gpu.py; their logs
+are under profiles/r03/fuzz/."""
+import argparse
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+
+def _args(**kw):
+    a = argparse.Namespace(programs=150, seed=11, hash=False, standard=False, mutate=False)
+    a.__dict__.update(kw)
+    return a
+
+
+@pytest.fixture(scope="module")
+def fuzz(gpu):
+    import fuzz_gpu
+    return fuzz_gpu
+
+
+@pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate"])
+def test_fuzz_campaign(fuzz, env, mode):
+    if mode == "reference":
+        failed = fuzz.reference(_args(seed=11), env)
+    elif mode == "hash":
+        failed = fuzz.reference(_args(seed=12, hash=True), env)
+    elif mode == "standard":
+        failed = fuzz.standard(_args(seed=13, programs=80, standard=True), env)
+    else:
+        failed = fuzz.mutated(_args(seed=14, programs=200, mutate=True), env)
+    assert not failed, "mismatches (see the captured output for the failing program numbers)"

@@ -122,7 +122,8 @@ def device(env, c, variant):
 def standard(a, env):
     """--standard: random programs under standard eBPF semantics (tests/stdprogs.py: loop-free
     programs with every ALU op, JMP32, stack, packet and array-lookup access; programs with counted
-    loops) against the oracle's run_std, 64-B packets (staged) and 72-B (general kernels)."""
+    loops; cursor walks over the packet) against the oracle's run_std, 64-B packets (staged) and
+    72-B (general kernels)."""
     import stdprogs
     failed = False
     for variant in (0, 1, 2):
@@ -132,7 +133,9 @@ def standard(a, env):
                 seed = a.seed * 100000 + k
                 g = np.random.default_rng(seed)
                 specs = []
-                if k % 2:
+                if k % 4 == 3:   # a packet walk with a cursor (loads at run-time offsets)
+                    code, rel = stdprogs.gen_cursor_program(seed)
+                elif k % 2:
                     code, rel = stdprogs.gen_loop_program(seed, length=int(g.integers(10, 40)))
                 else:
                     code, rel = stdprogs.gen_program(seed, length=int(g.integers(10, 80)), with_map=k % 4 == 0)
@@ -246,6 +249,40 @@ def mutated(a, env):
     return failed
 
 
+def reference(a, env):
+    """Random programs under the reference's semantics (array maps, or hashtables with --hash)
+    on every variant and both kernels, plus window launches; returns True on any mismatch."""
+    failed = False
+    configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
+    configs += [(0, "general", "win")]   # window launches, cut threshold 2, any batch size
+    for variant, layout, rg in configs:
+        if rg == "win":
+            os.environ.update(EBPF_WINDOW="1", EBPF_WIN_CUT_MIN="2", EBPF_WINDOW_MINBATCH="1")
+        t0 = time.time()
+        bad, faults = [], 0
+        try:
+            for k in range(a.programs):
+                # (window launches take programs without map writes: those get none here)
+                c = case(k, a.seed, layout, a.hash, writes=False if rg == "win" else None)
+                want, wf, wdata, wmaps = oracle(c)
+                got, gf, gdata, gmaps = device(env, c, variant)
+                faults += int(np.count_nonzero(wf))
+                if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
+                        np.array_equal(wdata, gdata) and wmaps == gmaps):
+                    bad.append(k)
+                if k % 100 == 99:
+                    print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
+        finally:
+            for k in ("EBPF_WINDOW", "EBPF_WIN_CUT_MIN", "EBPF_WINDOW_MINBATCH"):
+                os.environ.pop(k, None)
+        print("%svariant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+            "hash " if a.hash else "", variant, layout,
+            " window" if rg == "win" else "", a.programs, faults, len(bad), bad[:20],
+            time.time() - t0), flush=True)
+        failed = failed or bool(bad)
+    return failed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=500)
@@ -257,38 +294,10 @@ def main():
     env = native.Env()
     if a.mutate and not a.standard:
         failed = mutated(a, env)
-        env.destroy()
-        sys.exit(1 if failed else 0)
-    if a.standard:
+    elif a.standard:
         failed = standard(a, env)
-        env.destroy()
-        sys.exit(1 if failed else 0)
-    failed = False
-    configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
-    configs += [(0, "general", "win")]   # window launches, cut threshold 2, any batch size
-    for variant, layout, rg in configs:
-        if rg == "win":
-            os.environ.update(EBPF_WINDOW="1", EBPF_WIN_CUT_MIN="2", EBPF_WINDOW_MINBATCH="1")
-        t0 = time.time()
-        bad, faults = [], 0
-        for k in range(a.programs):
-            # (window launches take programs without map writes: those get none here)
-            c = case(k, a.seed, layout, a.hash, writes=False if rg == "win" else None)
-            want, wf, wdata, wmaps = oracle(c)
-            got, gf, gdata, gmaps = device(env, c, variant)
-            faults += int(np.count_nonzero(wf))
-            if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
-                    np.array_equal(wdata, gdata) and wmaps == gmaps):
-                bad.append(k)
-            if k % 100 == 99:
-                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        for k in ("EBPF_WINDOW", "EBPF_WIN_CUT_MIN", "EBPF_WINDOW_MINBATCH"):
-            os.environ.pop(k, None)
-        print("%svariant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            "hash " if a.hash else "", variant, layout,
-            " window" if rg == "win" else "", a.programs, faults, len(bad), bad[:20],
-            time.time() - t0), flush=True)
-        failed = failed or bool(bad)
+    else:
+        failed = reference(a, env)
     env.destroy()
     sys.exit(1 if failed else 0)
 
