@@ -240,14 +240,20 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	// it park at the fall-through block, and when no lane loops any more the scheduler resumes
 	// every parked lane of that exit together.  (The forward split would run the loop's tail
 	// once per distinct trip count in the group.)  The fall-through block becomes an entry point.
-	std::vector<char> rev_cond(n, 0);
+	// (a loop whose count translate.cpp dropped jumps to its head directly: a loop head placed
+	// before the conditional)
+	std::vector<char> rev_cond(n, 0), loop_head(n, 0);
+	for (uint32_t e = 0; e < n; e++)
+		if (xl.entries[e].kind == DK_LOOPCNT && xl.entries[e].next < n)
+			loop_head[xl.entries[e].next] = 1;
 	if (getenv("EBPF_JIT_NOREVLOOP") == nullptr)
 		for (uint32_t e : order) {
 			const uint32_t h = (uint32_t)low[e].handler;
 			if (!(ah_flags[h] & 1))
 				continue;
 			const uint32_t tk = xl.entries[e].target, nx = xl.entries[e].next;
-			if (tk < n && nx < n && nx != tk && xl.entries[tk].kind == DK_LOOPCNT) {
+			if (tk < n && nx < n && nx != tk &&
+			    (xl.entries[tk].kind == DK_LOOPCNT || (loop_head[tk] && idx[tk] < idx[e]))) {
 				rev_cond[e] = 1;
 				entry_point[nx] = 1;
 			}

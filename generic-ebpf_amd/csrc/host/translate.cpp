@@ -15,6 +15,7 @@
 #include "internal.h"
 
 #include <algorithm>
+#include <array>
 
 #include <unordered_map>
 
@@ -685,6 +686,283 @@ succ_of(const dprog_host &out, uint32_t id, int k)
 	return UINT32_MAX;
 }
 
+// Counted loops whose budget cannot run out (standard semantics).  A program with one loop —
+// one LOOPCNT entry L, reached from one conditional C on a counter X:
+//   JNE X, 0 taken into L (the back edge), or JEQ X, 0 whose fall-through is L (exit test, JA back)
+// — where every path from the loop head H = L.next to C decrements X by one exactly once
+// (SUB64 X, 1 / ADD64 X, -1), nothing else on those paths writes X or calls a helper, and X
+// enters the loop in [1, K]: the loop takes at most K - 1 backward jumps, so with K - 1 <=
+// DP_LOOP_BUDGET no lane can reach EBPF_FAULT_LOOP and the count is dropped (C jumps to H
+// directly; the oracle counts on and never faults either).  X's entry range comes from an
+// interval pass over the loop-free graph (the back edge removed): constants, loads (0 ..
+// 2^(8 size) - 1), AND / RSH / MOD / ADD / SUB with immediates, 64-bit compares with immediates
+// on their edges.  Returns whether the loop count was dropped.
+bool
+elide_loop_count(dprog_host &out)
+{
+	const size_t n = out.entries.size();
+	uint32_t L = UINT32_MAX;
+	for (uint32_t i = 0; i < n; i++)
+		if (out.entries[i].kind == DK_LOOPCNT && out.annot[i].reached) {
+			if (L != UINT32_MAX)
+				return false; // (several loops: their counts add up)
+			L = i;
+		}
+	if (L == UINT32_MAX)
+		return false;
+	const uint32_t H = out.entries[L].next;
+	if (H >= n || out.entries[H].kind == DK_FAULT)
+		return false;
+	// the one predecessor of L
+	uint32_t C = UINT32_MAX;
+	std::vector<std::vector<uint32_t>> preds(n);
+	for (uint32_t i = 0; i < n; i++) {
+		if (!out.annot[i].reached)
+			continue;
+		for (int k = 0; k < 2; k++) {
+			const uint32_t s = succ_of(out, i, k);
+			if (s >= n)
+				continue;
+			preds[s].push_back(i);
+			if (s == L) {
+				if (C != UINT32_MAX && C != i)
+					return false;
+				C = i;
+			}
+		}
+	}
+	if (C == UINT32_MAX)
+		return false;
+	const dp_entry &c = out.entries[C];
+	const bool jne_form = c.kind == EBPF_OP_JNE_IMM && c.target == L && c.next != L;
+	const bool jeq_form = c.kind == EBPF_OP_JEQ_IMM && c.next == L && c.target != L;
+	if (!(jne_form || jeq_form) || c.imm != 0 || c.dst >= EBPF_REG_MAX)
+		return false;
+	const uint8_t X = c.dst;
+	// the loop body: entries on a path H ->* C (not through L)
+	std::vector<char> fwd(n, 0), bwd(n, 0);
+	std::vector<uint32_t> st{H};
+	fwd[H] = 1;
+	while (!st.empty()) {
+		const uint32_t i = st.back();
+		st.pop_back();
+		for (int k = 0; k < 2; k++) {
+			const uint32_t s = succ_of(out, i, k);
+			if (s < n && s != L && !fwd[s]) {
+				fwd[s] = 1;
+				st.push_back(s);
+			}
+		}
+	}
+	if (!fwd[C])
+		return false;
+	st.push_back(C);
+	bwd[C] = 1;
+	while (!st.empty()) {
+		const uint32_t i = st.back();
+		st.pop_back();
+		if (i == H)
+			continue;
+		for (uint32_t p : preds[i])
+			if (fwd[p] && !bwd[p] && p != L) {
+				bwd[p] = 1;
+				st.push_back(p);
+			}
+	}
+	auto is_dec = [&](const dp_entry &e) {
+		return e.dst == X && ((e.kind == EBPF_OP_SUB64_IMM && e.imm == 1) ||
+				      (e.kind == EBPF_OP_ADD64_IMM && e.imm == ~0ull && e.aux == 0));
+	};
+	// (writes dst: ALU, ALU64, LDX, LDDW and the standard-semantics ALU kinds)
+	auto writes = [&](const dp_entry &e, uint8_t r) {
+		if (e.kind >= DK_MOV64R && e.kind <= DK_MOD32Z)
+			return e.dst == r;
+		if (e.kind >= 0x100)
+			return true; // (calls, stores into maps, loop entries: not in a counted body)
+		const uint8_t cls = e.kind & 7;
+		return (cls == EBPF_CLS_ALU || cls == EBPF_CLS_ALU64 || cls == EBPF_CLS_LDX ||
+			cls == EBPF_CLS_LD) && e.dst == r;
+	};
+	// decrements of X along the body's paths: every path H ->* C exactly one
+	std::vector<int> ndec(n, -1); // -1 unknown, 0 or 1, 2 = inconsistent
+	std::vector<uint32_t> order;  // topological over the body (a DAG: L is its only back edge)
+	{
+		std::vector<uint32_t> indeg(n, 0);
+		for (uint32_t i = 0; i < n; i++)
+			if (bwd[i])
+				for (int k = 0; k < 2; k++) {
+					const uint32_t s = succ_of(out, i, k);
+					if (s < n && bwd[s] && s != H)
+						indeg[s]++;
+				}
+		std::vector<uint32_t> q{H};
+		while (!q.empty()) {
+			const uint32_t i = q.back();
+			q.pop_back();
+			order.push_back(i);
+			for (int k = 0; k < 2; k++) {
+				const uint32_t s = succ_of(out, i, k);
+				if (s < n && bwd[s] && s != H && --indeg[s] == 0)
+					q.push_back(s);
+			}
+		}
+	}
+	size_t nbody = 0;
+	for (uint32_t i = 0; i < n; i++)
+		nbody += bwd[i] ? 1 : 0;
+	if (order.size() != nbody)
+		return false;
+	ndec[H] = 0;
+	for (uint32_t i : order) {
+		const dp_entry &e = out.entries[i];
+		int d = ndec[i];
+		if (d < 0 || d > 1)
+			return false;
+		if (i != C) {
+			if (is_dec(e))
+				d++;
+			else if (writes(e, X) || e.kind == DK_XADD)
+				return false;
+			if (e.kind == DK_CALL_LOOKUP || e.kind == DK_CALL_UPDATE || e.kind == DK_CALL_HDELETE)
+				return false;
+		}
+		for (int k = 0; k < 2; k++) {
+			const uint32_t s = succ_of(out, i, k);
+			if (s >= n || !bwd[s] || s == H)
+				continue;
+			if (ndec[s] < 0)
+				ndec[s] = d;
+			else if (ndec[s] != d)
+				return false;
+		}
+	}
+	if (ndec[C] != 1)
+		return false;
+	// X's range on the way in: intervals over the graph without the back edge
+	struct iv {
+		uint64_t lo = 0, hi = ~0ull;
+	};
+	std::vector<std::array<iv, EBPF_REG_MAX>> in(n);
+	std::vector<char> have(n, 0);
+	std::vector<uint32_t> indeg(n, 0);
+	for (uint32_t i = 0; i < n; i++)
+		if (out.annot[i].reached)
+			for (int k = 0; k < 2; k++) {
+				const uint32_t s = succ_of(out, i, k);
+				if (s < n && i != L)
+					indeg[s]++;
+			}
+	for (auto &r : in[out.start]) {
+		r.lo = 0;
+		r.hi = 0; // (the device zeroes r0, r2..r9, as the dataflow assumes)
+	}
+	in[out.start][1] = iv();
+	in[out.start][10] = iv();
+	have[out.start] = 1;
+	std::vector<uint32_t> q{out.start};
+	auto join = [&](uint32_t s, const std::array<iv, EBPF_REG_MAX> &r) {
+		if (!have[s]) {
+			in[s] = r;
+			have[s] = 1;
+		} else {
+			for (int k = 0; k < EBPF_REG_MAX; k++) {
+				in[s][k].lo = std::min(in[s][k].lo, r[k].lo);
+				in[s][k].hi = std::max(in[s][k].hi, r[k].hi);
+			}
+		}
+	};
+	while (!q.empty()) {
+		const uint32_t i = q.back();
+		q.pop_back();
+		if (i == L)
+			continue; // (the back edge)
+		const dp_entry &e = out.entries[i];
+		std::array<iv, EBPF_REG_MAX> r = in[i], t;
+		const uint8_t d = e.dst < EBPF_REG_MAX ? e.dst : 0;
+		const uint64_t K = e.imm;
+		const uint8_t cls = e.kind < 0x100 ? (e.kind & 7) : 0xff;
+		const iv full;
+		auto set = [&](uint64_t lo, uint64_t hi) {
+			r[d].lo = lo;
+			r[d].hi = hi;
+		};
+		switch (e.kind) {
+		case EBPF_OP_LDDW: set(K, K); break;
+		case EBPF_OP_MOV_IMM: set((uint32_t)K, (uint32_t)K); break;
+		case DK_MOV64R: r[d] = r[e.src]; break;
+		case EBPF_OP_LDXB: set(0, 0xff); break;
+		case EBPF_OP_LDXH: set(0, 0xffff); break;
+		case EBPF_OP_LDXW: set(0, 0xffffffffull); break;
+		case EBPF_OP_AND64_IMM: set(0, std::min(r[d].hi, K)); break;
+		case EBPF_OP_AND_IMM: set(0, std::min<uint64_t>(r[d].hi, K & 0xffffffffull)); break;
+		case EBPF_OP_RSH64_IMM: set(r[d].lo >> (K & 63), r[d].hi >> (K & 63)); break;
+		case EBPF_OP_MOD64_IMM: set(0, K - 1); break; // (K != 0: MOD by 0 was rewritten)
+		case EBPF_OP_ADD64_IMM:
+			if ((int64_t)K >= 0 && r[d].hi <= ~0ull - K)
+				set(r[d].lo + K, r[d].hi + K);
+			else if ((int64_t)K < 0 && r[d].lo >= 0 - K)
+				set(r[d].lo + K, r[d].hi + K);
+			else
+				r[d] = full;
+			break;
+		case EBPF_OP_SUB64_IMM:
+			if ((int64_t)K >= 0 && r[d].lo >= K)
+				set(r[d].lo - K, r[d].hi - K);
+			else
+				r[d] = full;
+			break;
+		default:
+			if (e.kind >= DK_MOV64R && e.kind <= DK_MOD32Z)
+				r[d] = full;
+			else if (e.kind >= 0x100 && e.kind != DK_LOOPINIT && e.kind != DK_OVLINIT &&
+				 e.kind != DK_LOOPCNT)
+				for (auto &x : r)
+					x = full; // (calls, XADD fetch, ...: nothing known after)
+			else if (e.kind < 0x100 && writes(e, d))
+				r[d] = (cls == EBPF_CLS_ALU) ? iv{0, 0xffffffffull} : full;
+			break;
+		}
+		t = r;
+		// 64-bit compares with an immediate refine their edges (taken: t, fall-through: r)
+		if (cls == EBPF_CLS_JMP && !(e.kind & 0x08)) {
+			iv &a = r[d], &b = t[d];
+			switch (e.kind) {
+			case EBPF_OP_JEQ_IMM: b.lo = std::max(b.lo, K); b.hi = std::min(b.hi, K); break;
+			case EBPF_OP_JGT_IMM: b.lo = std::max(b.lo, K + 1); a.hi = std::min(a.hi, K); break;
+			case EBPF_OP_JGE_IMM: b.lo = std::max(b.lo, K); if (K) a.hi = std::min(a.hi, K - 1); break;
+			case EBPF_OP_JLT_IMM: if (K) b.hi = std::min(b.hi, K - 1); a.lo = std::max(a.lo, K); break;
+			case EBPF_OP_JLE_IMM: b.hi = std::min(b.hi, K); a.lo = std::max(a.lo, K + 1); break;
+			default: break;
+			}
+			if (e.kind == EBPF_OP_JGT_IMM && K == ~0ull)
+				b = iv{1, 0}; // (never taken)
+		}
+		for (int k = 0; k < 2; k++) {
+			const uint32_t s = succ_of(out, i, k);
+			if (s >= n)
+				continue;
+			join(s, k ? t : r);
+			if (--indeg[s] == 0)
+				q.push_back(s);
+		}
+	}
+	if (!have[H])
+		return false;
+	// H's range joined the entry edges only (the back edge was skipped); every predecessor
+	// outside the loop must have been processed (indeg 0), else the graph has another cycle
+	if (indeg[H] != 0)
+		return false;
+	const iv x = in[H][X];
+	if (x.lo < 1 || x.hi - 1 > DP_LOOP_BUDGET)
+		return false;
+	dp_entry &cm = out.entries[C];
+	if (jne_form)
+		cm.target = H;
+	else
+		cm.next = H;
+	return true;
+}
+
 // Counter updates (ebpf_gpu.h "Stores into map values"): three consecutive entries
 //   LDX{W,DW} X = [P + off] (X != P);  ADD / SUB to X of an immediate or of a register other than
 //   X (64-bit; 32-bit too for W; the reference's MOV64, which adds); STX [P + off] = X, same width
@@ -1181,6 +1459,9 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 				out.maps.clear();
 				return EOPNOTSUPP;
 			}
+	// a counted loop that cannot reach the budget needs no count
+	if (out.has_loops && getenv("EBPF_XLATE_KEEP_LOOPCNT") == nullptr && elide_loop_count(out))
+		dataflow(out);
 	// counter updates, then how the program's map writes land and the log's records per path
 	if (fuse_counters(out, std_sem)) {
 		if (out.entries.size() >= kMaxEntries) {

@@ -219,3 +219,54 @@ def test_cursor_programs_cpu_and_code(native, env):
         assert int.from_bytes(p.device_code(1)[:4], "little") != 1
     finally:
         p.destroy()
+
+
+def _keeps_loop_count(native, env, code):
+    import subprocess
+    p = native.Prog(env, code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        c = p.device_code(1)
+    finally:
+        p.destroy()
+    r = subprocess.run(["/opt/rocm/llvm/bin/llvm-mc", "--disassemble", "-triple=amdgcn-amd-amdhsa",
+                        "-mcpu=gfx950"], input=" ".join("0x%02x" % b for b in c),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    return "ds_add_rtn_u32" in r.stdout   # (the LOOPCNT body: one LDS add per back edge)
+
+
+def test_counted_loop_needs_no_count(native, env):
+    """translate.cpp elide_loop_count: a single counted loop whose counter enters in [1, K] with
+    K - 1 <= 2^20 drops its per-lane count (C3L: IHL in [5, 12]; countdown(n) for n <= 2^20 + 1,
+    which takes exactly the budget); one more trip than the budget keeps it (the GPU budget test
+    then faults LOOP), and so do programs with two loops."""
+    import os
+    from generic_ebpf_amd import workloads
+    if not os.path.exists("/opt/rocm/llvm/bin/llvm-mc"):
+        pytest.skip("llvm-mc not available")
+    assert not _keeps_loop_count(native, env, workloads.prog_c3l().code)
+    assert not _keeps_loop_count(native, env, stdprogs.countdown(100)[0])
+    assert not _keeps_loop_count(native, env, stdprogs.countdown(stdprogs.LOOP_BUDGET + 1)[0])
+    assert _keeps_loop_count(native, env, stdprogs.countdown(stdprogs.LOOP_BUDGET + 2)[0])
+    # the counter may enter at 0 (r2 = packet byte & 15, no lower bound): 2^64 - 1 trips
+    code, _ = stdprogs.asm([stdprogs.I("ldxb", 2, 1, 5), stdprogs.I("and64_imm", 2, imm=15),
+                            ("label", "L"), stdprogs.I("add64_imm", 0, imm=1),
+                            stdprogs.I("sub64_imm", 2, imm=1), stdprogs.I("jne_imm", 2, imm=0, off="L"),
+                            stdprogs.I("exit")])
+    assert _keeps_loop_count(native, env, code)
+    # ... with the +1 the cursor/loop generators use it cannot
+    code, _ = stdprogs.asm([stdprogs.I("ldxb", 2, 1, 5), stdprogs.I("and64_imm", 2, imm=15),
+                            stdprogs.I("add64_imm", 2, imm=1),
+                            ("label", "L"), stdprogs.I("add64_imm", 0, imm=1),
+                            stdprogs.I("sub64_imm", 2, imm=1), stdprogs.I("jne_imm", 2, imm=0, off="L"),
+                            stdprogs.I("exit")])
+    assert not _keeps_loop_count(native, env, code)
+    # a second write of the counter in the body keeps the count
+    code, _ = stdprogs.asm([stdprogs.I("mov64_imm", 2, imm=9), ("label", "L"),
+                            stdprogs.I("sub64_imm", 2, imm=1), stdprogs.I("add64_imm", 2, imm=1),
+                            stdprogs.I("sub64_imm", 2, imm=1), stdprogs.I("jne_imm", 2, imm=0, off="L"),
+                            stdprogs.I("exit")])
+    assert _keeps_loop_count(native, env, code)
+    assert sum(_keeps_loop_count(native, env, stdprogs.gen_cursor_program(7000 + s)[0])
+               for s in range(6)) == 0
