@@ -152,6 +152,22 @@ int main(int argc, char **argv) {
 		}
 		return 0;
 	}
+	if (argc > 1 && argv[1][0] == 'm') {
+		// round 4: one contiguous range per wave (MAP 1) against interleaved superblocks, plain
+		// (ST 1) against nt result stores, the read ceiling (ST 2) beside them
+		for (int rep = 0; rep < 2; rep++) {
+			run<1, 8, 0, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 1, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 1, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 1, 1, 1, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 0, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 1, 0>(in, out, ngroups, npk, cus, 24);
+			run<2, 8, 0, 1, 1, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 2, 1, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 2, 1, 1, 0>(in, out, ngroups, npk, cus, 16);
+		}
+		return 0;
+	}
 	if (argc > 1 && argv[1][0] == 'o') {
 		// occupancy x prefetch depth, with a little per-group work (the staged kernel at 4
 		// workgroups per CU, round 1)
