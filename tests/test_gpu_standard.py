@@ -147,6 +147,52 @@ def test_cursor_loops_vs_oracle(gpu, env, variant):
     assert {0, 3} <= outcomes
 
 
+@pytest.mark.parametrize("variant", [0, 2])
+def test_cursor_walk_then_hash_probe(gpu, env, variant):
+    """A cursor walk (packet loads at run-time offsets: keep mode, the LDS packet buffer held
+    until the group ends) followed by a hashtable probe keyed by the walk's result (the probe's
+    routine and the group-end DMA on one wave), 200,001 staged packets against the oracle."""
+    I = stdprogs.I
+    code, rel = stdprogs.asm([
+        I("mov64_reg", 6, 1), I("mov64_imm", 0, imm=7), I("mov64_reg", 7, 6),
+        I("add64_imm", 7, imm=2), I("ldxb", 8, 6, 40), I("and64_imm", 8, imm=7),
+        I("add64_imm", 8, imm=1), ("label", "L"),
+        I("ldxh", 2, 7, 1), I("mul64_imm", 0, imm=31), I("add64_reg", 0, 2),
+        I("ldxb", 3, 7, 0), I("and64_imm", 3, imm=3), I("add64_reg", 7, 3), I("add64_imm", 7, imm=2),
+        I("sub64_imm", 8, imm=1), I("jne_imm", 8, imm=0, off="L"),
+        I("mov64_reg", 9, 0), I("and64_imm", 0, imm=63), I("stxw", 10, 0, -4),
+        ("lddw_map", 1, 0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+        I("call", imm=0), I("jeq_imm", 0, imm=0, off="M"),
+        I("ldxdw", 0, 0, 0), I("xor64_reg", 9, 0), ("label", "M"),
+        I("mov64_reg", 0, 9), I("exit")])
+    g = np.random.default_rng(77)
+    keys = np.arange(0, 64, 2, dtype=np.uint32)   # every other key present
+    vals = g.integers(0, 256, (len(keys), 8), dtype=np.uint8)
+    spec = pyoracle.HashSpec(4, 8, keys=keys.view(np.uint8).reshape(-1, 4), values=vals, capacity=64)
+    n = 200001
+    pk = g.integers(0, 256, (n, 64), dtype=np.uint8)
+    want, wf, _, _ = pyoracle.OracleProgram(code, rel, [spec], semantics=1).run(pk.reshape(-1), n, 64,
+                                                                                nthreads=8)
+    assert not wf.any()
+    m = gpu.HashMap(env, 4, 8, 64)
+    try:
+        m.fill(keys.view(np.uint8).reshape(-1, 4), vals)
+        p = gpu.Prog(env, gpu.patch_relocs(code, rel, [m.handle]))
+        try:
+            p.set_semantics(gpu.SEM_STANDARD)
+            gpu.set_variant(variant)
+            got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, 64)
+            if variant == 0:
+                assert p.exec_info(0)[0] == "compiled"
+        finally:
+            gpu.set_variant(0)
+            p.destroy()
+    finally:
+        m.destroy()
+    assert not gf.any()
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_c3l_full_size(gpu, env, variant):
     """The bench's loop workload (C3L: IPv4 header checksum over IHL words, 5-12 trips) over 16M
