@@ -2255,7 +2255,12 @@ def kernel(name, staged, jit=False):
           "s_bitcmp1_b32 %s, 0" % s(S_T3),
           "s_cbranch_scc0 .L%s_noovl" % k,
           "s_or_b32 s7, s7, 0x2000",
-          ".L%s_noovl:" % k]
+          ".L%s_noovl:" % k,
+          # s7 bit 15: dp_launch.offsets holds (start, end) pairs (vflags bit 2, DP_VF_EXTENTS)
+          "s_bitcmp1_b32 %s, 2" % s(S_T3),
+          "s_cbranch_scc0 .L%s_noext" % k,
+          "s_or_b32 s7, s7, 0x8000",
+          ".L%s_noext:" % k]
     if staged and jit:
         # s7 bit 14 (keep mode): the compiled program reads its packet at run-time offsets from
         # the LDS packet buffer (LDXPKTV), so the next group's DMA waits for the group's end
@@ -2337,12 +2342,20 @@ def pkt_setup(idx, tag):
             "v_mov_b32 v%d, %s" % (V_LEN, s(S_STRIDE)),
             "s_branch .Lps_stage_%s" % tag,
             ".Lps_offsets_%s:" % tag,
-            "v_mov_b32 %s, 8" % v(H[1]),
+            # offsets[i], offsets[i + 1]; extents batches (s7 bit 15): offsets[2i], offsets[2i + 1]
+            "s_bitcmp1_b32 s7, 15",
+            "s_cselect_b32 %s, 16, 8" % s(S_JUNK),
+            "v_mov_b32 %s, %s" % (v(H[1]), s(S_JUNK)),
             "v_mad_u64_u32 %s, %s, v%d, %s, %s" % (vp(H[4]), sp(S_JUNK), idx, v(H[1]), sp(S_OFFS)),
             "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[0]), vp(H[4])),
             "global_load_dwordx2 %s, %s, off" % (vp(H[4]), vp(H[4])),
             "s_waitcnt vmcnt(0)",
-            "v_sub_u32 v%d, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
+            # length = end - start; an end below its start or 4 GiB past it: length 0 (every load
+            # of the packet faults MEM)
+            "v_sub_co_u32 v%d, vcc, %s, %s" % (V_LEN, v(R[0]), v(H[4])),
+            "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(R[1]), v(H[5])),
+            "v_cmp_ne_u32_e32 vcc, 0, %s" % v(R[1]),
+            "v_cndmask_b32 v%d, v%d, 0, vcc" % (V_LEN, V_LEN),
             "v_mov_b32 %s, %s" % (v(R[2]), s(S_OFFBASE + 1)),
             "v_sub_co_u32 %s, vcc, %s, %s" % (v(H[4]), v(H[4]), s(S_OFFBASE)),
             "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(H[5]), v(H[5]), v(R[2])),

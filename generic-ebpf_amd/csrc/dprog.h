@@ -60,6 +60,7 @@ enum dp_kind : uint16_t {
 	// emptied (dprog.h DP_OVL_COUNT = 0)
 	DK_OVLINIT = 0x113,
 };
+#define DP_VF_EXTENTS 4u // dp_launch.vflags: offsets are (start, end) pairs
 #define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
 
@@ -182,8 +183,9 @@ struct dp_launch {
 	uint32_t span_g;
 	uint32_t span_magic_g;    // ceil(2^32 / span_g)
 	// stores into map values (ebpf_gpu.h "Stores into map values"): bit 0 = the program reads
-	// its own stores (an overlay of the words it stored, per lane: DP_OVL_* below); bits 8..15 =
-	// the overlay's entries per lane
+	// its own stores (an overlay of the words it stored, per lane: DP_OVL_* below); bit 1 = it
+	// has value-store sites; bit 2 (DP_VF_EXTENTS) = `offsets` holds (start, end) pairs
+	// (EBPF_BATCH_EXTENTS); bits 8..15 = the overlay's entries per lane
 	uint32_t vflags;
 	// window launches (span image; gen_interp.py "Window mode"): LDS bytes of a window (0: not
 	// a window launch), packets per workgroup, the LDS offset of the per-window arrays, and the

@@ -250,8 +250,13 @@ ebpf_interp_v0(dp_launch L)
 	rg.pkt_len = 0;
 	if (live) {
 		if (L.offsets) {
-			rg.pkt_lo = (uint64_t)L.data + (L.offsets[gid] - L.off_base);
-			rg.pkt_len = L.offsets[gid + 1] - L.offsets[gid];
+			// offsets[i], offsets[i + 1]; extents batches: offsets[2i], offsets[2i + 1].  An end
+			// below its start or 4 GiB past it gives length 0 (every packet load faults MEM),
+			// as in the assembly kernels
+			const uint64_t k = (L.vflags & DP_VF_EXTENTS) ? 2 * gid : gid;
+			const uint64_t lo = L.offsets[k], hi = L.offsets[k + 1];
+			rg.pkt_lo = (uint64_t)L.data + (lo - L.off_base);
+			rg.pkt_len = (hi >= lo && hi - lo < (1ull << 32)) ? hi - lo : 0;
 		} else {
 			rg.pkt_lo = (uint64_t)L.data + gid * L.stride;
 			rg.pkt_len = L.stride;

@@ -744,7 +744,9 @@ window_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launc
 	if (const char *m = getenv("EBPF_WINDOW_MINBATCH"))
 		min = strtoull(m, nullptr, 0);
 	// (the staged copy is not written back: no store that may reach the packet)
-	const bool fits = L.offsets != nullptr && L.count >= min && L.count <= kWinMax &&
+	// (extents batches: packets in any order, a window needs them back to back)
+	const bool fits = L.offsets != nullptr && !(L.vflags & DP_VF_EXTENTS) && L.count >= min &&
+			  L.count <= kWinMax &&
 			  !ep->xlated->asm_needs_general && !prog_writes_maps(*ep->xlated);
 	if (on && *on == '1')
 		return fits;
@@ -1038,7 +1040,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	L.nentries = dp->nentries;
 	L.start = ep->xlated->start;
 	L.vflags = (ep->xlated->vstore_overlay ? 1u : 0u) | (ep->xlated->vstore_sites ? 2u : 0u) |
-		   (ep->xlated->ovl_entries << 8);
+		   (ep->xlated->ovl_entries << 8) | (L0.vflags & DP_VF_EXTENTS);
 	launch_order order(ep->xlated->maps);
 	int err = sync_map_mirrors(ep, dp->device, stream);
 	if (err)
@@ -1143,9 +1145,10 @@ validate_batch(const struct ebpf_pkt_batch *b, uint32_t allowed_flags = 0)
 {
 	if (b == nullptr || (b->data == nullptr && b->count != 0))
 		return fail(EINVAL, "batch or batch->data is NULL");
-	if (b->flags & ~allowed_flags)
-		return fail(EINVAL, allowed_flags ? "batch->flags: unknown bits"
-						  : "batch->flags must be 0");
+	if (b->flags & ~(allowed_flags | EBPF_BATCH_EXTENTS))
+		return fail(EINVAL, "batch->flags: unknown bits");
+	if ((b->flags & EBPF_BATCH_EXTENTS) && b->offsets == nullptr && b->count != 0)
+		return fail(EINVAL, "extents batch without offsets");
 	if (b->offsets == nullptr && b->stride == 0 && b->count != 0)
 		return fail(EINVAL, "fixed-stride batch with stride 0");
 	return 0;
@@ -1536,6 +1539,7 @@ batch_dev(struct ebpf_prog *ep, int device, const struct ebpf_pkt_batch *batch, 
 	L.data = (uint8_t *)batch->data;
 	L.offsets = batch->offsets;
 	L.off_base = 0;
+	L.vflags = (batch->flags & EBPF_BATCH_EXTENTS) ? DP_VF_EXTENTS : 0;
 	L.ret = ret_dev;
 	L.faults = faults_dev;
 	L.hist = reinterpret_cast<unsigned long long *>(hist_dev);
@@ -1577,6 +1581,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	const bool copy_back = ep->xlated->writes_memory;
 	// Chunked, double-buffered: chunk k's H2D overlaps chunk k-1's kernel and D2H.
 	const uint64_t chunk = batch->offsets ? (1ull << 20) : (1ull << 22);
+	const bool ext = (batch->flags & EBPF_BATCH_EXTENTS) != 0;
 	if ((e = hipMemsetAsync(S.d_hist, 0, EBPF_HIST_BINS * sizeof(unsigned long long),
 				S.stream[0])) != hipSuccess ||
 	    (e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
@@ -1614,7 +1619,16 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 		hipStream_t st = S.stream[b];
 		const uint64_t cn = (hi - c0 < chunk) ? hi - c0 : chunk;
 		uint64_t byte0, byte1;
-		if (batch->offsets) {
+		if (ext) { // the bytes the chunk's packets span (in any order, gaps included)
+			byte0 = UINT64_MAX;
+			byte1 = 0;
+			for (uint64_t i = c0; i < c0 + cn; i++) {
+				byte0 = std::min(byte0, batch->offsets[2 * i]);
+				byte1 = std::max(byte1, batch->offsets[2 * i + 1]);
+			}
+			if (byte1 < byte0)
+				byte0 = byte1;
+		} else if (batch->offsets) {
 			byte0 = batch->offsets[c0];
 			byte1 = batch->offsets[c0 + cn];
 		} else {
@@ -1626,18 +1640,19 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 			return drain(hip_fail(e, "batch chunk"));
 		if ((err = stage_alloc(&S.d_data[b], &S.data_cap[b], byte1 - byte0 + 16)))
 			return drain(err);
-		const size_t small = cn * 9 + (batch->offsets ? (cn + 1) * 8 : 0) + 64;
+		const uint64_t noffs = ext ? 2 * cn : cn + 1;
+		const size_t small = cn * 9 + (batch->offsets ? noffs * 8 : 0) + 64;
 		if ((err = stage_alloc(&S.d_small[b], &S.small_cap[b], small)))
 			return drain(err);
 		uint8_t *sm = static_cast<uint8_t *>(S.d_small[b]);
 		uint64_t *d_ret = reinterpret_cast<uint64_t *>(sm);
 		uint64_t *d_offs = batch->offsets ? reinterpret_cast<uint64_t *>(sm + cn * 8) : nullptr;
-		uint8_t *d_faults = sm + cn * 8 + (batch->offsets ? (cn + 1) * 8 : 0);
+		uint8_t *d_faults = sm + cn * 8 + (batch->offsets ? noffs * 8 : 0);
 		const uint8_t *src = static_cast<const uint8_t *>(batch->data) + byte0;
 		if ((e = hipMemcpyAsync(S.d_data[b], src, byte1 - byte0, hipMemcpyHostToDevice, st)) !=
 		    hipSuccess)
 			return drain(hip_fail(e, "hipMemcpyAsync(packets H2D)"));
-		if (d_offs && (e = hipMemcpyAsync(d_offs, batch->offsets + c0, (cn + 1) * 8,
+		if (d_offs && (e = hipMemcpyAsync(d_offs, batch->offsets + (ext ? 2 * c0 : c0), noffs * 8,
 						  hipMemcpyHostToDevice, st)) != hipSuccess)
 			return drain(hip_fail(e, "hipMemcpyAsync(offsets H2D)"));
 		dp_launch L;
@@ -1645,6 +1660,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 		L.data = static_cast<uint8_t *>(S.d_data[b]);
 		L.offsets = d_offs;
 		L.off_base = byte0;
+		L.vflags = ext ? DP_VF_EXTENTS : 0;
 		L.ret = d_ret;
 		L.faults = d_faults;
 		L.hist = S.d_hist;

@@ -8,7 +8,9 @@
 // The records' captured bytes are gathered into one buffer in offsets form (ebpf_pkt_batch:
 // packet i = data[offsets[i], offsets[i+1])), which ebpf_prog_run_batch consumes directly; the
 // program sees each packet's captured bytes, as a caller that hands a record's buffer to the
-// reference's ebpf_prog_run would.
+// reference's ebpf_prog_run would.  ebpf_pcap_extents skips the gather: the batch is the capture
+// itself in extents form (each record's (start, end) in the capture; the 16-byte record headers
+// stay between the packets and are never part of one).
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -82,32 +84,37 @@ release(const void *p)
 		free(const_cast<void *>(p));
 }
 
-} // namespace
+// The capture's global header and a validating walk over its record headers.
+struct pcap_scan {
+	bool swap = false, nsec = false;
+	uint32_t snaplen = 0, linktype = 0;
+	uint64_t count = 0, bytes = 0, truncated = 0, cut = 0;
+};
 
-EBPF_EXPORT int
-ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
-		struct ebpf_pcap_info *info)
+int
+scan_capture(const void *capture, size_t len, pcap_scan *sc)
 {
-	if (!capture || !batch || len < 24) {
+	if (!capture || len < 24) {
 		set_last_error("pcap: NULL argument or shorter than the 24-byte global header");
 		return EINVAL;
 	}
 	const uint8_t *b = static_cast<const uint8_t *>(capture);
 	uint32_t magic;
 	memcpy(&magic, b, 4);
-	bool swap, nsec;
 	switch (magic) {
-	case 0xa1b2c3d4u: swap = false; nsec = false; break;
-	case 0xa1b23c4du: swap = false; nsec = true; break;
-	case 0xd4c3b2a1u: swap = true; nsec = false; break;
-	case 0x4d3cb2a1u: swap = true; nsec = true; break;
+	case 0xa1b2c3d4u: sc->swap = false; sc->nsec = false; break;
+	case 0xa1b23c4du: sc->swap = false; sc->nsec = true; break;
+	case 0xd4c3b2a1u: sc->swap = true; sc->nsec = false; break;
+	case 0x4d3cb2a1u: sc->swap = true; sc->nsec = true; break;
 	default:
 		set_last_error("pcap: unknown magic (not a classic libpcap capture)");
 		return EINVAL;
 	}
-	const uint32_t snaplen = rd32(b + 16, swap), linktype = rd32(b + 20, swap);
-	// pass 1: count the records and their bytes, validating every header
-	uint64_t count = 0, bytes = 0, truncated = 0, cut = 0;
+	const bool swap = sc->swap;
+	sc->snaplen = rd32(b + 16, swap);
+	sc->linktype = rd32(b + 20, swap);
+	const uint32_t snaplen = sc->snaplen;
+	// count the records and their bytes, validating every header
 	size_t at = 24;
 	while (at < len) {
 		if (len - at < 16) {
@@ -122,12 +129,46 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 		// a record longer than the header's snaplen (some writers get the snaplen wrong): as
 		// libpcap's reader does, the packet is its first snaplen bytes (counted as truncated)
 		const uint32_t keep = (snaplen && incl > snaplen) ? snaplen : incl;
-		cut += keep < incl;
-		truncated += keep < orig;
-		count++;
-		bytes += keep;
+		sc->cut += keep < incl;
+		sc->truncated += keep < orig;
+		sc->count++;
+		sc->bytes += keep;
 		at += 16 + (size_t)incl;
 	}
+	return 0;
+}
+
+void
+fill_info(const pcap_scan &sc, struct ebpf_pcap_info *info)
+{
+	if (!info)
+		return;
+	info->linktype = sc.linktype;
+	info->snaplen = sc.snaplen;
+	info->nanosecond = sc.nsec ? 1u : 0u;
+	info->byte_swapped = sc.swap ? 1u : 0u;
+	info->truncated = sc.truncated;
+	info->bytes = sc.bytes;
+}
+
+} // namespace
+
+EBPF_EXPORT int
+ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
+		struct ebpf_pcap_info *info)
+{
+	pcap_scan sc;
+	if (!batch) {
+		set_last_error("pcap: NULL batch");
+		return EINVAL;
+	}
+	if (int err = scan_capture(capture, len, &sc))
+		return err;
+	const uint8_t *b = static_cast<const uint8_t *>(capture);
+	const bool swap = sc.swap;
+	const uint32_t snaplen = sc.snaplen;
+	const uint64_t count = sc.count, bytes = sc.bytes, cut = sc.cut;
+	size_t at;
 	// pass 2: gather the captured bytes
 	uint8_t *data = static_cast<uint8_t *>(alloc((size_t)bytes, pinned != 0));
 	uint64_t *offs = static_cast<uint64_t *>(alloc((size_t)(count + 1) * sizeof(uint64_t), pinned != 0));
@@ -188,14 +229,40 @@ ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_bat
 	batch->data = data;
 	batch->offsets = offs;
 	batch->count = count;
-	if (info) {
-		info->linktype = linktype;
-		info->snaplen = snaplen;
-		info->nanosecond = nsec ? 1u : 0u;
-		info->byte_swapped = swap ? 1u : 0u;
-		info->truncated = truncated;
-		info->bytes = bytes;
+	fill_info(sc, info);
+	return 0;
+}
+
+EBPF_EXPORT int
+ebpf_pcap_extents(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
+		  struct ebpf_pcap_info *info)
+{
+	pcap_scan sc;
+	if (!batch) {
+		set_last_error("pcap: NULL batch");
+		return EINVAL;
 	}
+	if (int err = scan_capture(capture, len, &sc))
+		return err;
+	const uint8_t *b = static_cast<const uint8_t *>(capture);
+	uint64_t *ext = static_cast<uint64_t *>(alloc((size_t)sc.count * 2 * sizeof(uint64_t), pinned != 0));
+	if (!ext)
+		return ENOMEM;
+	// record i's captured bytes in place: (start, start + kept length)
+	uint64_t i = 0;
+	for (size_t at = 24; at < len; i++) {
+		const uint32_t incl = rd32(b + at + 8, sc.swap);
+		const uint32_t keep = (sc.snaplen && incl > sc.snaplen) ? sc.snaplen : incl;
+		ext[2 * i] = at + 16;
+		ext[2 * i + 1] = at + 16 + keep;
+		at += 16 + (size_t)incl;
+	}
+	memset(batch, 0, sizeof(*batch));
+	batch->data = capture;
+	batch->offsets = ext;
+	batch->count = sc.count;
+	batch->flags = EBPF_BATCH_EXTENTS;
+	fill_info(sc, info);
 	return 0;
 }
 
@@ -204,9 +271,10 @@ ebpf_pcap_batch_free(struct ebpf_pkt_batch *batch)
 {
 	if (!batch)
 		return;
-	release(batch->data);
+	release(batch->data); // (an extents batch's data is the caller's capture: not ours, kept)
 	release(batch->offsets);
 	batch->data = nullptr;
 	batch->offsets = nullptr;
 	batch->count = 0;
+	batch->flags = 0;
 }

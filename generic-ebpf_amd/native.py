@@ -121,6 +121,7 @@ FUNCS = {
     "ebpf_prog_set_semantics": (_I, [_VP, _I]),
     "ebpf_pcap_batch": (_I, [_VP, ctypes.c_size_t, _I, _VP, _VP]),
     "ebpf_pcap_batch_free": (None, [_VP]),
+    "ebpf_pcap_extents": (_I, [_VP, ctypes.c_size_t, _I, _VP, _VP]),
     "ebpf_prog_run_batch_async": (_I, [_VP, _VP, _VP, _VP, ctypes.POINTER(_VP)]),
     "ebpf_batch_wait": (_I, [_VP, _VP]),
 }
@@ -131,6 +132,7 @@ _lib = None
 
 
 BATCH_HIST_OVERWRITE = 0x1  # include/ebpf_gpu.h EBPF_BATCH_HIST_OVERWRITE
+BATCH_EXTENTS = 0x2         # EBPF_BATCH_EXTENTS: offsets holds (start, end) pairs
 
 
 class _AsyncJob:
@@ -155,23 +157,29 @@ class PcapBatch:
     form.  ``batch`` is the ebpf_pkt_batch to hand to the run functions; ``data()`` /
     ``offsets()`` copy it out; ``free()`` (or the context manager) releases it."""
 
-    def __init__(self, capture, pinned=False):
-        buf = np.frombuffer(bytes(capture), dtype=np.uint8)
+    def __init__(self, capture, pinned=False, extents=False):
+        # (extents: ebpf_pcap_extents, the batch is the capture itself; it is kept here)
+        self.buf = np.frombuffer(bytes(capture), dtype=np.uint8)
+        buf = self.buf
         self.batch = PktBatch()
         self.info = PcapInfo()
-        _check(lib().ebpf_pcap_batch(buf.ctypes.data if len(buf) else None, len(buf),
-                                     1 if pinned else 0, ctypes.byref(self.batch),
-                                     ctypes.byref(self.info)), "ebpf_pcap_batch")
+        fn = lib().ebpf_pcap_extents if extents else lib().ebpf_pcap_batch
+        _check(fn(buf.ctypes.data if len(buf) else None, len(buf), 1 if pinned else 0,
+                  ctypes.byref(self.batch), ctypes.byref(self.info)),
+               "ebpf_pcap_extents" if extents else "ebpf_pcap_batch")
 
     @property
     def count(self):
         return int(self.batch.count)
 
     def offsets(self):
-        return np.ctypeslib.as_array((ctypes.c_uint64 * (self.count + 1)).from_address(
+        n = 2 * self.count if self.batch.flags & BATCH_EXTENTS else self.count + 1
+        return np.ctypeslib.as_array((ctypes.c_uint64 * n).from_address(
             self.batch.offsets)).copy()
 
     def data(self):
+        if self.batch.flags & BATCH_EXTENTS:
+            return self.buf.copy()
         n = int(self.info.bytes)
         if n == 0:
             return np.zeros(0, dtype=np.uint8)
@@ -387,15 +395,16 @@ class Prog:
         buf = ctypes.create_string_buffer(bytes(packet), len(packet))
         return lib().ebpf_prog_run(buf, self.ptr), buf.raw
 
-    def run_batch(self, data, count, stride=0, offsets=None, want_faults=True):
+    def run_batch(self, data, count, stride=0, offsets=None, want_faults=True, extents=False):
         """Host buffers: returns (ret u64[count], faults u8[count], stats).  ``data`` (a
-        contiguous uint8 numpy array) is modified in place if the program stores to packets."""
+        contiguous uint8 numpy array) is modified in place if the program stores to packets.
+        ``extents``: ``offsets`` holds (start, end) pairs (EBPF_BATCH_EXTENTS)."""
         assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
         ret = np.zeros(count, dtype=np.uint64)
         faults = np.zeros(count, dtype=np.uint8) if want_faults else None
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
         b = PktBatch(data.ctypes.data, None if offs is None else offs.ctypes.data, count,
-                     stride, 0)
+                     stride, BATCH_EXTENTS if extents else 0)
         st = BatchStats()
         _check(lib().ebpf_prog_run_batch(self.ptr, ctypes.byref(b), ret.ctypes.data,
                                          None if faults is None else faults.ctypes.data,
@@ -428,7 +437,8 @@ class Prog:
                                          ctypes.byref(st)), "ebpf_prog_run_batch")
         return ret, faults, st
 
-    def run_batch_multi(self, devices, data, count, stride=0, offsets=None, want_faults=True):
+    def run_batch_multi(self, devices, data, count, stride=0, offsets=None, want_faults=True,
+                        extents=False):
         """ebpf_prog_run_batch_multi: host buffers sharded over ``devices`` (a list of device
         indices, repeats allowed).  Returns (ret, faults, stats) like run_batch."""
         assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
@@ -436,7 +446,7 @@ class Prog:
         faults = np.zeros(count, dtype=np.uint8) if want_faults else None
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
         b = PktBatch(data.ctypes.data, None if offs is None else offs.ctypes.data, count,
-                     stride, 0)
+                     stride, BATCH_EXTENTS if extents else 0)
         devs = (ctypes.c_int * len(devices))(*devices)
         st = BatchStats()
         _check(lib().ebpf_prog_run_batch_multi(self.ptr, len(devices), devs, ctypes.byref(b),
@@ -470,11 +480,13 @@ class Prog:
         return bytes(buf)[: n.value]
 
     def run_batch_dev(self, device, data_ptr, count, stride, ret_ptr, offsets_ptr=None,
-                      faults_ptr=None, hist_ptr=None, stream=None, hist_overwrite=False):
+                      faults_ptr=None, hist_ptr=None, stream=None, hist_overwrite=False,
+                      extents=False):
         """Device pointers (ints); asynchronous on ``stream`` (hipStream_t as int or None).
         ``hist_overwrite``: the histogram is set to this batch's counts instead of added to."""
         b = PktBatch(data_ptr, offsets_ptr, count, stride,
-                     BATCH_HIST_OVERWRITE if hist_overwrite else 0)
+                     (BATCH_HIST_OVERWRITE if hist_overwrite else 0) |
+                     (BATCH_EXTENTS if extents else 0))
         _check(lib().ebpf_prog_run_batch_dev(self.ptr, device, ctypes.byref(b), ret_ptr,
                                              faults_ptr, hist_ptr, stream),
                "ebpf_prog_run_batch_dev")

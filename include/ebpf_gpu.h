@@ -113,18 +113,24 @@ enum ebpf_fault {
 
 /* Batch descriptor.  Fixed-stride mode (offsets == NULL): packet i occupies
  * [data + i*stride, data + (i+1)*stride).  Offsets mode: packet i occupies
- * [data + offsets[i], data + offsets[i+1]) — offsets has count+1 entries. */
+ * [data + offsets[i], data + offsets[i+1]) — offsets has count+1 entries.  Extents mode
+ * (flags & EBPF_BATCH_EXTENTS): packet i occupies [data + offsets[2i], data + offsets[2i+1]) —
+ * offsets has 2*count entries, start <= end, packets in any order, with gaps between them or
+ * overlapping (a capture's records in place: ebpf_pcap_extents).  A program that stores into
+ * overlapping packets leaves their common bytes unspecified. */
 struct ebpf_pkt_batch {
 	const void *data;
 	const uint64_t *offsets;
 	uint64_t count;
 	uint32_t stride;
-	uint32_t flags; /* 0, or EBPF_BATCH_HIST_OVERWRITE (ebpf_prog_run_batch_dev only) */
+	uint32_t flags; /* EBPF_BATCH_* */
 };
 
 /* ebpf_prog_run_batch_dev: hist_dev receives this batch's counts instead of having them added,
  * so the caller need not zero it before each launch. */
 #define EBPF_BATCH_HIST_OVERWRITE 0x1u
+/* Every batch entry point: offsets holds (start, end) pairs (extents mode above). */
+#define EBPF_BATCH_EXTENTS 0x2u
 
 /* Verdict histogram: bin min(r0, 255) for packets that reached EXIT, bin 256 = faulted. */
 #define EBPF_HIST_BINS 257
@@ -158,6 +164,13 @@ struct ebpf_pcap_info {
 };
 int ebpf_pcap_batch(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
 		    struct ebpf_pcap_info *info);
+/* The same capture as an extents-mode batch over the capture itself: batch->data = capture (no
+ * copy; it must stay valid while the batch is used), batch->offsets = the library's (start, end)
+ * pair of every record's captured bytes (snaplen-truncated as above), flags =
+ * EBPF_BATCH_EXTENTS.  Only the offsets are allocated (pinned on request); release them with
+ * ebpf_pcap_batch_free, which leaves an extents batch's data alone.  Same errors. */
+int ebpf_pcap_extents(const void *capture, size_t len, int pinned, struct ebpf_pkt_batch *batch,
+		      struct ebpf_pcap_info *info);
 void ebpf_pcap_batch_free(struct ebpf_pkt_batch *batch);
 
 /* Number of visible GPUs (0 on a host without one). Never fails. */

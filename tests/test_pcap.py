@@ -122,3 +122,112 @@ def test_pcap_batch_on_device_vs_oracle(gpu, env, pinned):
     np.testing.assert_array_equal(wf, gf)
     np.testing.assert_array_equal(want, got)
     assert st.packets == n
+
+
+@pytest.mark.parametrize("magic,big", [(MAGIC_US, False), (MAGIC_NS, True)])
+def test_pcap_extents_layout(native, magic, big):
+    """ebpf_pcap_extents: the batch is the capture itself (no copy), offsets the (start, end) of
+    every record's captured bytes in it (snaplen-truncated), flags EBPF_BATCH_EXTENTS; the same
+    packets as ebpf_pcap_batch."""
+    pk = _packets(300, seed=5) + [b"", b"x" * 300]
+    cap = make_pcap(pk, magic, big, snaplen=256)
+    with native.PcapBatch(cap, extents=True) as e, native.PcapBatch(cap) as g:
+        assert e.batch.flags == native.BATCH_EXTENTS and e.count == g.count == len(pk)
+        ext = e.offsets().reshape(-1, 2)
+        raw = e.data()
+        assert raw.tobytes() == cap
+        assert b"".join(raw[s:t].tobytes() for s, t in ext) == g.data().tobytes()
+        assert np.array_equal(ext[:, 1] - ext[:, 0], np.diff(g.offsets()))
+        assert e.info.truncated == g.info.truncated == 1 and e.info.bytes == g.info.bytes
+
+
+def test_pcap_extents_rejects(native):
+    good = make_pcap(_packets(4, seed=3))
+    with pytest.raises(native.EbpfError) as ei:
+        native.PcapBatch(good[:-1], extents=True)
+    assert ei.value.code == errno.EINVAL
+
+
+def _gather(data, ext):
+    """An extents batch as the offsets form the oracle takes (its packets' bytes concatenated)."""
+    lens = (ext[:, 1] - ext[:, 0]).astype(np.int64)
+    offs = np.zeros(len(ext) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    flat = np.concatenate([data[s:t] for s, t in ext]) if len(ext) else np.zeros(0, np.uint8)
+    return flat.astype(np.uint8), offs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_extents_batch_vs_oracle(gpu, env, variant):
+    """EBPF_BATCH_EXTENTS on every variant: 40,000 packets of 0..127 bytes at random places in a
+    buffer, in random order, with gaps, overlapping each other, some empty and some with an end
+    below the start (length 0: every load faults MEM), against the oracle on the same packets
+    gathered back to back; host buffers (chunked uploads of each chunk's span) and the
+    device-resident entry point."""
+    import torch
+    from generic_ebpf_amd import workloads
+    g = np.random.default_rng(31 + variant)
+    n, size = 40000, 3 << 20
+    data = g.integers(0, 256, size, dtype=np.uint8)
+    frames = workloads.packets_l2l3(4096, 128, seed=3)
+    starts = g.integers(0, size - 128, n).astype(np.uint64)
+    lens = g.integers(0, 128, n).astype(np.uint64)
+    for i in range(0, n, 7):   # real L2/L3 frames at some of the places
+        data[int(starts[i]):int(starts[i]) + 128] = frames[i % 4096]
+    ext = np.stack([starts, starts + lens], axis=1)
+    bad = g.random(n) < 0.01
+    ext[bad, 1] = ext[bad, 0] - 1          # an end below its start
+    lay = workloads.prog_c3()
+    good = np.where(bad[:, None], np.stack([starts, starts], axis=1), ext)
+    flat, offs = _gather(data, good)
+    want, wf, _, _ = oracle_run(__import__("goldens").Case("ext", lay.code, [], [], flat, n, 0, offs),
+                                nthreads=8)
+    assert (wf[~bad] == 0).any() and (wf[~bad] == 3).any()
+    p = gpu.Prog(env, lay.code)
+    try:
+        gpu.set_variant(variant)
+        got, gf, st = p.run_batch(np.ascontiguousarray(data), n, 0, ext.reshape(-1), extents=True)
+        np.testing.assert_array_equal(gf, wf)
+        np.testing.assert_array_equal(got, want)
+        # device-resident
+        d_data = torch.from_numpy(data).cuda()
+        d_offs = torch.from_numpy(ext.reshape(-1).view(np.int64)).cuda()
+        d_ret = torch.zeros(n, dtype=torch.int64, device="cuda")
+        d_f = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        p.run_batch_dev(0, d_data.data_ptr(), n, 0, d_ret.data_ptr(), offsets_ptr=d_offs.data_ptr(),
+                        faults_ptr=d_f.data_ptr(), extents=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_f.cpu().numpy(), wf)
+        np.testing.assert_array_equal(d_ret.cpu().numpy().view(np.uint64), want)
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+
+
+@pytest.mark.gpu
+def test_pcap_extents_on_device_vs_gathered(gpu, env):
+    """The capture run in place (ebpf_pcap_extents, pinned offsets) gives the results of the
+    gathered batch (ebpf_pcap_batch), which test_pcap_batch_on_device_vs_oracle pins to the
+    oracle; also sharded over the device listed twice."""
+    from generic_ebpf_amd import workloads
+    n = 50000
+    frames = workloads.packets_l2l3(n, 128, seed=9)
+    lens = np.random.default_rng(10).integers(14, 129, n)
+    cap = make_pcap([frames[i, :lens[i]].tobytes() for i in range(n)])
+    lay = workloads.prog_c3()
+    p = gpu.Prog(env, lay.code)
+    try:
+        with gpu.PcapBatch(cap, pinned=True) as b, gpu.PcapBatch(cap, pinned=True, extents=True) as e:
+            want, wf, _ = p.run_pcap(b)
+            got, gf, st = p.run_pcap(e)
+            raw, ext = e.data(), e.offsets()
+        mg, mf, _ = p.run_batch_multi([0, 0], np.ascontiguousarray(raw), n, 0, ext, extents=True)
+    finally:
+        p.destroy()
+    assert wf.any() and not wf.all()
+    np.testing.assert_array_equal(gf, wf)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(mf, wf)
+    np.testing.assert_array_equal(mg, want)
+    assert st.packets == n
