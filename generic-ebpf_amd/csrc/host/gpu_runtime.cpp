@@ -1106,8 +1106,9 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		// a compiled program that probes hashtables is bound by their latency and wants every
 		// wave; the others stream packets at 4 workgroups per CU (asm_runtime.cpp, occupancy).
 		// The interpreter (fn == NULL) is bound by its scalar dispatch and wants every wave too:
-		// C4 1.86 -> 1.42 ms at 6 instead of 4 workgroups per CU (profiles/r02/v2occ)
-		bool probes = false;
+		// C4 1.86 -> 1.42 ms at 6 instead of 4 workgroups per CU (profiles/r02/v2occ).  So is a
+		// program with loops (C3L 0.305 -> 0.277 ms at 6, profiles/r04/c3l_occ)
+		bool probes = ep->xlated->has_loops;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
 		bool done = false;
