@@ -850,6 +850,41 @@ def h_ldx_pktv(z, d, sr):
                     out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
                 out.append("v_mov_b32 %s, 0" % hi(d))
         out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
+    elif not SPAN_IMAGE:
+        # general kernels with the headers kept in LDS (s7 bit 14, every lane's first 64 bytes
+        # at S_PKTLDS + 64 lane when its packet is at least that long): when every running lane's
+        # bytes lie in its first 64 and its packet has them staged, read them there
+        A, B = v(H[4]), v(H[5])
+        out += ["s_bitcmp1_b32 s7, 14",
+                "s_cbranch_scc0 .Lpv_flat_{uid}",
+                "v_cmp_ge_u32_e64 vcc, %d, %s" % (64 - z, v(H[2])),
+                "s_and_b64 %s, vcc, exec" % sp(S_MASK),
+                "v_cmp_le_u32_e64 vcc, 64, v%d" % V_LEN,
+                "s_and_b64 %s, %s, vcc" % (sp(S_MASK), sp(S_MASK)),
+                "s_cmp_eq_u64 %s, exec" % sp(S_MASK),
+                "s_cbranch_scc0 .Lpv_flat_{uid}",
+                "v_mbcnt_lo_u32_b32 %s, -1, 0" % A,
+                "v_mbcnt_hi_u32_b32 %s, -1, %s" % (A, A),
+                "v_lshl_add_u32 %s, %s, 6, %s" % (A, A, v(H[2])),
+                "v_add_u32 %s, %s, %s" % (A, s(S_PKTLDS), A)]
+        if z == 1:
+            out += ["ds_read_u8 %s, %s" % (lo(d), A), "s_waitcnt lgkmcnt(0)",
+                    "v_mov_b32 %s, 0" % hi(d)]
+        else:
+            t0, t1, t2 = v(R[0]), v(R[1]), v(R[2])
+            out += ["v_and_b32 %s, -4, %s" % (B, A),
+                    "ds_read2_b32 v[%d:%d], %s offset1:1" % (R[0], R[1], B)]
+            if z == 8:
+                out.append("ds_read_b32 %s, %s offset:8" % (t2, B))
+            out += ["s_waitcnt lgkmcnt(0)",
+                    "v_alignbyte_b32 %s, %s, %s, %s" % (lo(d), t1, t0, A)]
+            if z == 8:
+                out.append("v_alignbyte_b32 %s, %s, %s, %s" % (hi(d), t2, t1, A))
+            else:
+                if z == 2:
+                    out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
+                out.append("v_mov_b32 %s, 0" % hi(d))
+        out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
     out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}f")
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3])),
             "s_branch .Lpv_done_{uid}",
@@ -2276,7 +2311,14 @@ def kernel(name, staged, jit=False):
         L += ["s_bitcmp1_b32 %s, 31" % s(S_PKTLDS),
               "s_cbranch_scc0 .L%s_nogs" % k,
               "s_or_b32 s7, s7, 8",
-              ".L%s_nogs:" % k]
+              ".L%s_nogs:" % k,
+              # bit 30: the staged headers are kept in the wave's LDS packet buffer too, for the
+              # loads at run-time offsets (s7 bit 14 in the general kernels)
+              "s_bitcmp1_b32 %s, 30" % s(S_PKTLDS),
+              "s_cbranch_scc0 .L%s_nohl" % k,
+              "s_or_b32 s7, s7, 0x4000",
+              ".L%s_nohl:" % k,
+              "s_and_b32 %s, %s, 0x3fffffff" % (s(S_PKTLDS), s(S_PKTLDS))]
     if not staged and not STAGED_IMAGE:
         # slot launch (dp_launch.perm != 0): s7 bit 9 = slot mode (this launch's slots are
         # perm[start .. start + n), G per group)
@@ -2373,6 +2415,15 @@ def pkt_setup(idx, tag):
                                                                        V_PKT, V_PKT + 1, 16 * q)
             for q in range(4)] + [
             "s_waitcnt vmcnt(0)",
+            # (s7 bit 14: the headers also into the lane's 64 bytes of the wave's LDS packet
+            # buffer, S_PKTLDS + 64 lane, for loads at run-time offsets: h_ldx_pktv)
+            "s_bitcmp1_b32 s7, 14",
+            "s_cbranch_scc0 .Lps_done_%s" % tag,
+            "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[1]),
+            "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[1]), v(H[1])),
+            "v_lshl_add_u32 %s, %s, 6, %s" % (v(H[1]), v(H[1]), s(S_PKTLDS))] + [
+            "ds_write_b128 %s, v[%d:%d] offset:%d" % (v(H[1]), PKT0 + 4 * q, PKT0 + 4 * q + 3, 16 * q)
+            for q in range(4)] + [
             ".Lps_done_%s:" % tag,
             "s_mov_b64 exec, %s" % sp(S_MASK)]
 
@@ -2881,9 +2932,10 @@ def common_group_code():
           "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
           "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
           ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
-          # keep mode (s7 bit 14): the next group's DMA, now that the program is done with the
-          # packet buffer
-          "s_bitcmp1_b32 s7, 14",
+          # keep mode (s7 bits 14 and 0: staged kernels): the next group's DMA, now that the
+          # program is done with the packet buffer
+          "s_and_b32 %s, s7, 0x4001" % s(S_BYTES),
+          "s_cmp_eq_u32 %s, 0x4001" % s(S_BYTES),
           "s_cbranch_scc0 .Lgd_nokeep"] + call(".Lr_prefetch") + [
           ".Lgd_nokeep:",
           "s_mov_b32 %s, %s" % (s(S_GROUP), s(S_T0)),

@@ -32,6 +32,8 @@ bool asm_window_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_lds_fits(int mode, uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_program_needs_general(const dprog_host &xl);
 bool asm_program_gstage(const dprog_host &xl);
+bool asm_program_hdrlds(const dprog_host &xl);
+bool asm_hdrlds_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_program_span(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
@@ -319,6 +321,7 @@ ensure_translated(struct ebpf_prog *ep)
 	if (!x->error) {
 		x->asm_needs_general = asm_program_needs_general(*x);
 		x->asm_gstage = asm_program_gstage(*x);
+		x->asm_hdrlds = asm_program_hdrlds(*x) && getenv("EBPF_NOHDRLDS") == nullptr;
 		x->asm_span = asm_program_span(*x);
 	}
 	ep->xlated = std::move(x);
@@ -1092,7 +1095,11 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		}
 		dp->last_exec = fn ? EBPF_EXEC_COMPILED : EBPF_EXEC_INTERPRETER;
 		dp->last_layout = mode;
-		L.lds_pkt_base = (mode == 0 && ep->xlated->asm_gstage) ? 0x80000000u : 0;
+		// general kernels: header staging (bit 31), and the headers kept in LDS too (bit 30;
+		// when the 16 KB of packet buffers cost no resident workgroup: the VGPRs allow 6 per CU)
+		const bool hdrlds = ep->xlated->asm_hdrlds && asm_hdrlds_fits(dp->map_lds_bytes, L.stack_stride);
+		L.lds_pkt_base = mode != 0 ? 0 : hdrlds ? 0xc0000000u
+						 : ep->xlated->asm_gstage ? 0x80000000u : 0;
 		unsigned long long *user_hist = L.hist;
 		if (L.hist) {
 			void *part = nullptr;

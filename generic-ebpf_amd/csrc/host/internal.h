@@ -206,6 +206,8 @@ struct dprog_host {
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
+	bool asm_hdrlds = false;             // ... and keep them in LDS for run-time-offset loads
+	                                     // (asm_program_hdrlds)
 	bool asm_span = false;               // window launches pay (asm_program_span)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
