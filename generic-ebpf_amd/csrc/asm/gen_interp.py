@@ -808,17 +808,17 @@ def h_ldx_pktv(z, d, sr):
     a0 = H[0]
     out = ["v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(a0), pair(sr)),
            "v_sub_co_u32 %s, vcc, %s, v%d" % (v(H[2]), v(a0), V_PKT),
-           "v_subb_co_u32 %s, vcc, %s, v%d, vcc" % (v(H[3]), v(a0 + 1), V_PKT + 1),
-           "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[3]))]
-    if STAGED_IMAGE:   # (every packet is 64 bytes)
-        out += ["v_cmp_ge_u32_e64 vcc, %d, %s" % (64 - z, v(H[2]))]
+           "v_subb_co_u32 %s, vcc, %s, v%d, vcc" % (v(H[3]), v(a0 + 1), V_PKT + 1)]
+    if STAGED_IMAGE:   # (every packet is 64 bytes: one unsigned 64-bit compare of the offset)
+        out += ["v_cmp_ge_u64_e64 %s, %d, v[%d:%d]" % (sp(S_JUNK), 64 - z, H[2], H[3])]
     else:
-        out += ["v_subrev_u32 %s, %d, v%d" % (v(H[4]), z, V_LEN),
+        out += ["v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(H[3])),
+                "v_subrev_u32 %s, %d, v%d" % (v(H[4]), z, V_LEN),
                 "v_cmp_le_u32_e64 vcc, %s, %s" % (v(H[2]), v(H[4])),
                 "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-                "v_cmp_le_u32_e64 vcc, %d, v%d" % (z, V_LEN)]
-    out += ["s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
-            "s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
+                "v_cmp_le_u32_e64 vcc, %d, v%d" % (z, V_LEN),
+                "s_and_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK))]
+    out += ["s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
             "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
             "s_cbranch_scc0 .Lpv_gen_{uid}"]
     if STAGED_IMAGE:

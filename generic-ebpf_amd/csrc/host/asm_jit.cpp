@@ -639,14 +639,19 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			// .Lloop: s_branch <taken block> (or a long jump)
 			const uint32_t tk = xl.entries[e].target, nx = xl.entries[e].next;
 			const size_t loop_at = at + RC;
+			// (both branches go to the taken block itself when it is in reach, not through .Lloop)
+			auto to_loop = [&](size_t a) -> uint32_t {
+				return !long_cond[e] && fits_simm16((int64_t)pos[tk] - (int64_t)(a + 4)) ? pos[tk]
+													 : (uint32_t)loop_at;
+			};
 			put32(at, 0x80000000u | (0x0du << 23) | (48u << 16) | (126u << 8) | 106u);
 			put32(at + 4, 0x80000000u | (0x13u << 23) | (18u << 16) | (106u << 8) | 126u);
-			sopp(at + 8, OP_SCC0, (uint32_t)loop_at);
+			sopp(at + 8, OP_SCC0, to_loop(at + 8));
 			put32(at + 12, 0xbe800000u | (126u << 16) | (0x01u << 8) | 18u);
 			put32(at + 16, 0x7e000000u | (41u << 17) | (0x01u << 9) | 255u);
 			put32(at + 20, code_off(nx));
 			put32(at + 24, 0xbe800000u | (126u << 16) | (0x01u << 8) | 48u);
-			sopp(at + 28, OP_EXECNZ, (uint32_t)loop_at);
+			sopp(at + 28, OP_EXECNZ, to_loop(at + 28));
 			put32(at + 32, 0x80000000u | (60u << 16) | (255u << 8) | 4u);
 			put32(at + 36, T[JT_SCHED]);
 			put32(at + 40, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
