@@ -236,6 +236,53 @@ def _keeps_loop_count(native, env, code):
     return "ds_add_rtn_u32" in r.stdout   # (the LOOPCNT body: one LDS add per back edge)
 
 
+def _disasm(code):
+    """(byte offset, instruction text) pairs of gfx950 machine code (llvm-mc)."""
+    import subprocess
+    r = subprocess.run(["/opt/rocm/llvm/bin/llvm-mc", "--disassemble", "-triple=amdgcn-amd-amdhsa",
+                        "-mcpu=gfx950", "-show-encoding"], input=" ".join("0x%02x" % b for b in code),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    out, off = [], 0
+    for line in r.stdout.splitlines():
+        if "encoding:" not in line:
+            continue
+        ins, enc = line.split("encoding:", 1)
+        out.append((off, ins.strip().rstrip(";/").strip()))
+        off += enc.count("0x")
+    return out
+
+
+def test_loop_back_edge_code_shape(native, env):
+    """C3L's staged compiled code (asm_jit.cpp, the reversed split): both branches of a back edge
+    that keeps the looping lanes go to the loop block itself, never to an s_branch; the staged
+    packet load at a run-time offset checks the offset with one unsigned 64-bit compare
+    (gen_interp.py h_ldx_pktv)."""
+    import os
+    from generic_ebpf_amd import workloads
+    if not os.path.exists("/opt/rocm/llvm/bin/llvm-mc"):
+        pytest.skip("llvm-mc not available")
+    p = native.Prog(env, workloads.prog_c3l().code)
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+        ins = _disasm(p.device_code(1))
+    finally:
+        p.destroy()
+    at = dict(ins)
+    back = 0
+    for off, text in ins:
+        op = text.split()[0]
+        if op not in ("s_cbranch_execnz", "s_cbranch_scc0"):
+            continue
+        simm = int(text.split()[1])
+        tgt = off + 4 + 4 * (simm - 65536 if simm >= 32768 else simm)
+        if tgt < off:   # a back edge
+            back += 1
+            assert not at[tgt].startswith("s_branch"), (hex(off), at[tgt])
+    assert back == 2
+    assert any(t.startswith("v_cmp_ge_u64") for _, t in ins)
+
+
 def test_counted_loop_needs_no_count(native, env):
     """translate.cpp elide_loop_count: a single counted loop whose counter enters in [1, K] with
     K - 1 <= 2^20 drops its per-lane count (C3L: IHL in [5, 12]; countdown(n) for n <= 2^20 + 1,
