@@ -2296,10 +2296,12 @@ def kernel(name, staged, jit=False):
           "s_cbranch_scc0 .L%s_noext" % k,
           "s_or_b32 s7, s7, 0x8000",
           ".L%s_noext:" % k]
-    if staged and jit:
+    if staged and jit and RETK > 1:
         # s7 bit 14 (keep mode): the compiled program reads its packet at run-time offsets from
         # the LDS packet buffer (LDXPKTV), so the next group's DMA waits for the group's end
         # (flags word at the head of the code area, asm_jit.cpp JIT_HDR_KEEP_PKT)
+        # (not in an EBPF_ASM_RETK=1 build, an A/B knob: there C3L's results mismatched in keep
+        # mode, profiles/r04/retk/; such a build reads those loads from global memory)
         L += raddr("ebpf_jit_area", S_JUNK) + [
             "s_load_dword %s, %s, 0x0" % (s(S_T3), sp(S_JUNK)),
             "s_waitcnt lgkmcnt(0)",
