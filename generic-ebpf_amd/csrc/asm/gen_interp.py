@@ -2232,7 +2232,11 @@ def routines():
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
     # past the batch end masked off.  Clobbers s[64:68], m0, exec.
+    # The lane mask is a VALU compare, so it is computed under exec = all lanes: a caller may
+    # arrive with any exec (.Lgroup_done in keep mode comes from .Lr_schedule with exec = 0, and
+    # a compare under it would DMA no chunk, leaving the previous group's bytes in the buffer)
     L += [".Lr_prefetch:",
+          "s_mov_b64 exec, -1",
           "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_NGROUPS)),
           "s_cbranch_scc1 .Lpf_ret",
           "s_lshl_b32 s66, %s, 6" % s(S_T0),
@@ -2296,19 +2300,21 @@ def kernel(name, staged, jit=False):
           "s_cbranch_scc0 .L%s_noext" % k,
           "s_or_b32 s7, s7, 0x8000",
           ".L%s_noext:" % k]
-    if staged and jit and RETK > 1:
-        # s7 bit 14 (keep mode): the compiled program reads its packet at run-time offsets from
-        # the LDS packet buffer (LDXPKTV), so the next group's DMA waits for the group's end
-        # (flags word at the head of the code area, asm_jit.cpp JIT_HDR_KEEP_PKT)
-        # (not in an EBPF_ASM_RETK=1 build, an A/B knob: there C3L's results mismatched in keep
-        # mode, profiles/r04/retk/; such a build reads those loads from global memory)
-        L += raddr("ebpf_jit_area", S_JUNK) + [
-            "s_load_dword %s, %s, 0x0" % (s(S_T3), sp(S_JUNK)),
-            "s_waitcnt lgkmcnt(0)",
-            "s_bitcmp1_b32 %s, 0" % s(S_T3),
-            "s_cbranch_scc0 .L%s_nokeep" % k,
-            "s_or_b32 s7, s7, 0x4000",
-            ".L%s_nokeep:" % k]
+    if staged:
+        # s7 bit 14 (keep mode): the program reads its packet at run-time offsets from the LDS
+        # packet buffer (LDXPKTV), so the next group's DMA waits for the group's end.  Compiled
+        # code flags it in the word at the head of its code area (asm_jit.cpp JIT_HDR_KEEP_PKT),
+        # the interpreter's launch in dp_launch.vflags (DP_VF_KEEP, still in S_T3)
+        if jit:
+            L += raddr("ebpf_jit_area", S_JUNK) + [
+                "s_load_dword %s, %s, 0x0" % (s(S_T3), sp(S_JUNK)),
+                "s_waitcnt lgkmcnt(0)",
+                "s_bitcmp1_b32 %s, 0" % s(S_T3)]
+        else:
+            L += ["s_bitcmp1_b32 %s, 3" % s(S_T3)]
+        L += ["s_cbranch_scc0 .L%s_nokeep" % k,
+              "s_or_b32 s7, s7, 0x4000",
+              ".L%s_nokeep:" % k]
     if not staged:   # header staging requested by the host (dp_launch.lds_pkt_base bit 31)
         L += ["s_bitcmp1_b32 %s, 31" % s(S_PKTLDS),
               "s_cbranch_scc0 .L%s_nogs" % k,

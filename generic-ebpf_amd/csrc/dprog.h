@@ -61,6 +61,9 @@ enum dp_kind : uint16_t {
 	DK_OVLINIT = 0x113,
 };
 #define DP_VF_EXTENTS 4u // dp_launch.vflags: offsets are (start, end) pairs
+// dp_launch.vflags: the assembly interpreter's staged kernel keeps each group's packets in the
+// wave's LDS packet buffer until the group ends (keep mode: LDXPKTV reads them there)
+#define DP_VF_KEEP 8u
 #define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
 

@@ -11,7 +11,9 @@
 // as if the packets had run one after the other (ebpf_map_array.c:173-183 memcpy,
 // ebpf_interpreter.c:343-366 stores).  Two passes over the log: every record offers its order for
 // each byte it writes (atomicMax), then the record holding a byte's maximum copies that byte and
-// re-arms its winner word; the log's counter is re-armed by the host (memset).  Counter updates
+// re-arms its winner word; the log's counter is re-armed by the host (memset).  A map that
+// stores into its values never reach has one winner word per key instead of per byte (its
+// records all write whole values: upd_map.gran).  Counter updates
 // of UPD_ATOMIC maps were added into the map's delta area during the batch: a third kernel adds
 // that area into the values and zeroes it.
 #include <hip/hip_runtime.h>
@@ -67,8 +69,8 @@ upd_offer(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 		if (m.cls != UPD_DEVICE || !rec_span(r, m, &lo, &nb))
 			continue; // (replayed on the host, or an atomic map's)
 		const unsigned long long o = rec_order(r, i);
-		for (uint32_t b = 0; b < nb; b++)
-			atomicMax(&win[m.win_off + lo + b], o);
+		for (uint32_t b = 0; b < nb; b += m.gran)
+			atomicMax(&win[m.win_off + (lo + b) / m.gran], o);
 	}
 }
 
@@ -86,12 +88,13 @@ upd_apply(const uint8_t *__restrict__ log, uint32_t cap, uint32_t stride,
 			continue;
 		const unsigned long long o = rec_order(r, i);
 		uint8_t *dst = reinterpret_cast<uint8_t *>(m.dev_base) + lo;
-		for (uint32_t b = 0; b < nb; b++) {
-			unsigned long long *w = &win[m.win_off + lo + b];
+		for (uint32_t b = 0; b < nb; b += m.gran) {
+			unsigned long long *w = &win[m.win_off + (lo + b) / m.gran];
 			if (*w != o)
 				continue;
-			dst[b] = r[16 + b];
-			*w = 0; // the winner re-arms its byte (a later check by a loser sees 0 != its order)
+			for (uint32_t c = 0; c < m.gran; c++)
+				dst[b + c] = r[16 + b + c];
+			*w = 0; // the winner re-arms its word (a later check by a loser sees 0 != its order)
 		}
 	}
 }

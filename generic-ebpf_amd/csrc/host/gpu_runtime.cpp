@@ -321,7 +321,8 @@ ensure_translated(struct ebpf_prog *ep)
 	if (!x->error) {
 		x->asm_needs_general = asm_program_needs_general(*x);
 		x->asm_gstage = asm_program_gstage(*x);
-		x->asm_hdrlds = asm_program_hdrlds(*x) && getenv("EBPF_NOHDRLDS") == nullptr;
+		x->asm_pktv = asm_program_hdrlds(*x);
+		x->asm_hdrlds = x->asm_pktv && getenv("EBPF_NOHDRLDS") == nullptr;
 		x->asm_span = asm_program_span(*x);
 	}
 	ep->xlated = std::move(x);
@@ -571,9 +572,15 @@ prepare(struct ebpf_prog *ep, int device, dprog_device **out)
 			um[t].max_entries = nd->table[t].max_entries;
 			um[t].win_off = nd->win_words;
 			um[t].cls = UPD_NONE;
+			um[t].gran = nd->table[t].value_size;
 			if (in_list(xl.upd_maps, t)) {
 				um[t].cls = UPD_DEVICE;
-				nd->win_words += (uint64_t)nd->table[t].value_size * nd->table[t].max_entries;
+				// byte winners only where a store into a value may land; a map written only by
+				// map_update_elem (whole values) needs one word per key
+				if (in_list(xl.vstore_maps, t))
+					um[t].gran = 1;
+				nd->win_words += (uint64_t)nd->table[t].value_size * nd->table[t].max_entries /
+						 um[t].gran;
 				rmax = std::max(rmax, (nd->table[t].value_size + 7) & ~7u);
 			}
 			if (in_list(xl.hupd_maps, t)) {
@@ -690,13 +697,14 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 	P->faulted = reinterpret_cast<uint32_t *>(P->log + boff);
 	P->faulted_bytes = bbytes;
 	// (the buffer is reused at other sizes: whatever lies where the bitmap now starts is stale).
-	// The log's counter and the winner words are zero after every apply step; they are zeroed
-	// here too, so that a batch whose launch failed before its apply leaves nothing behind
+	// The log's counter is zero after every apply step; it is zeroed here too, so that a batch
+	// whose launch failed before its apply leaves nothing behind.  The winner words need no
+	// clearing: they are zeroed when allocated, only the apply step writes them (its first kernel
+	// offers, its second re-arms every word that received an offer), so they are zero between
+	// batches whatever happened to the launch before
 	hipError_t e = hipMemsetAsync(P->faulted, 0, bbytes, stream);
 	if (e == hipSuccess)
 		e = hipMemsetAsync(P->log, 0, 4, stream);
-	if (e == hipSuccess && dp->win_words)
-		e = hipMemsetAsync(P->win, 0, dp->win_words * 8, stream);
 	return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync(map-write log)");
 }
 
@@ -1095,6 +1103,10 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		}
 		dp->last_exec = fn ? EBPF_EXEC_COMPILED : EBPF_EXEC_INTERPRETER;
 		dp->last_layout = mode;
+		// the interpreter's staged kernel: keep mode when the program loads its packet at
+		// run-time offsets (compiled code flags it in its own area, asm_jit.cpp)
+		if (fn == nullptr && mode == 1 && ep->xlated->asm_pktv)
+			L.vflags |= DP_VF_KEEP;
 		// general kernels: header staging (bit 31), and the headers kept in LDS too (bit 30;
 		// when the 16 KB of packet buffers cost no resident workgroup: the VGPRs allow 6 per CU)
 		const bool hdrlds = ep->xlated->asm_hdrlds && asm_hdrlds_fits(dp->map_lds_bytes, L.stack_stride);

@@ -206,6 +206,7 @@ struct dprog_host {
 	bool writes_memory = false;          // any reachable ST/STX through a non-r10 base
 	bool asm_needs_general = false;      // a store may touch the packet: no staged mode
 	bool asm_gstage = false;             // general kernels stage packet headers (asm_program_gstage)
+	bool asm_pktv = false;               // packet loads at run-time offsets (LDXPKTV), no packet stores
 	bool asm_hdrlds = false;             // ... and keep them in LDS for run-time-offset loads
 	                                     // (asm_program_hdrlds)
 	bool asm_span = false;               // window launches pay (asm_program_span)
@@ -214,7 +215,9 @@ struct dprog_host {
 	// Map writes of a device batch (ebpf_gpu.h): the write log holds max_updates records per
 	// packet — the most update / delete calls and logged stores into map values on one path
 	// (0: no log).  Every written map is in exactly one of:
-	std::vector<uint16_t> upd_maps;      // arrays whose records land on the device (byte winners)
+	std::vector<uint16_t> upd_maps;      // arrays whose records land on the device (winner words)
+	std::vector<uint16_t> vstore_maps;   // ... of them, those a store into a map value may reach
+	                                     // (one winner word per byte; the others: one per key)
 	std::vector<uint16_t> hupd_maps;     // maps whose records replay on the host in order
 	                                     // (hashtables; arrays mixing counter updates and stores)
 	std::vector<uint16_t> atomic_maps;   // arrays changed only by aligned counter updates of one

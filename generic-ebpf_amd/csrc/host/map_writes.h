@@ -13,7 +13,10 @@ struct upd_map {
 	uint64_t dev_base;    // the device mirror
 	uint32_t value_size;
 	uint32_t max_entries;
-	uint64_t win_off;     // first winner word of this map (one u64 per byte of its values)
+	uint64_t win_off;     // first winner word of this map
+	uint32_t gran;        // value bytes per winner word: 1 when stores into its values may reach
+	                      // the map (byte winners), else value_size (whole-value updates: per key)
+	uint32_t pad;
 	uint32_t cls;         // UPD_*
 	uint32_t width;       // UPD_ATOMIC: counter bytes (4 or 8)
 };

@@ -1117,6 +1117,7 @@ analyze_writes(dprog_host &out)
 			put(out.hupd_maps);
 		} else if (nadd[m] == 0) {
 			put(out.upd_maps); // stores (and update calls): byte winners on the device
+			put(out.vstore_maps);
 		} else if (nset[m] == 0 && !helper && exact[m] && (widths[m] == 4 || widths[m] == 8)) {
 			put(out.atomic_maps);
 			out.atomic_width.push_back((uint8_t)widths[m]);

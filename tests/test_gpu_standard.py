@@ -147,6 +147,42 @@ def test_cursor_loops_vs_oracle(gpu, env, variant):
     assert {0, 3} <= outcomes
 
 
+def test_keep_mode_refill_on_interpreter(gpu, env):
+    """Keep mode on the assembly interpreter's staged kernel (one result slot per group, the
+    RETK = 1 image): every group of the interpreter ends with no live lane (.Lr_schedule reaches
+    .Lgroup_done with exec = 0), and only then is the wave's next group DMA'd into the LDS
+    packet buffer the program's run-time-offset loads read.  That DMA's lane mask must not
+    depend on the arriving exec (round 4: with it, refilled groups read the previous group's
+    bytes or a mix).  4M + 37 distinct packets (8 groups per wave and a partial last group), a
+    walk whose every load is at a run-time offset, against the oracle
+    (ebpf_interpreter.c:327-338: each packet reads its own bytes)."""
+    I = stdprogs.I
+    code, rel = stdprogs.asm([
+        I("mov64_reg", 6, 1), I("ldxb", 8, 6, 0), I("and64_imm", 8, imm=7), I("add64_imm", 8, imm=1),
+        I("mov64_imm", 0, imm=1), ("label", "L"),
+        I("ldxw", 2, 6, 3), I("mul64_imm", 0, imm=0x9e3779b1), I("xor64_reg", 0, 2),
+        I("add64_imm", 6, imm=5), I("sub64_imm", 8, imm=1), I("jne_imm", 8, imm=0, off="L"),
+        I("exit")])
+    n = (1 << 22) + 37
+    pk = np.random.default_rng(91).integers(0, 256, (n, 64), dtype=np.uint8)
+    want, wf, _, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(pk.reshape(-1), n, 64,
+                                                                            nthreads=16)
+    assert not wf.any()
+    p = gpu.Prog(env, code)
+    try:
+        p.set_semantics(gpu.SEM_STANDARD)
+        gpu.set_variant(2)
+        got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        ex, layout = p.exec_info(0)[:2]
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+    assert (ex, layout) == ("interpreter", 1)
+    assert not gf.any()
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (bad.size, bad[:8])
+
+
 @pytest.mark.parametrize("variant", [0, 2])
 def test_cursor_walk_then_hash_probe(gpu, env, variant):
     """A cursor walk (packet loads at run-time offsets: keep mode, the LDS packet buffer held

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 GPU session: the given pytest selection (TESTS), then optional bench lines (BENCH:
+# GPU session: the given pytest selection (TESTS), then optional bench lines (BENCH:
 # space-separated configs, each run with --also= and no PMC).  Each GPU step has its own limit;
 # the first failure ends the script.
 set -u
-OUT=gpurun_out/${TAG:-r4}
+OUT=gpurun_out/${TAG:-r5}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
