@@ -219,9 +219,10 @@ def verify(w, torch, d_ret, d_hist_total, world, dev):
         want, wf, _, _ = op.run(w.pk, w.n, 0, w.offs, nthreads=thr)
     else:
         want, wf, _, _ = op.run(w.pk, w.D, 64, None, nthreads=thr)
-    # per-packet results: the shard tiles want[] starting at lo % D
+    # per-packet results: a fixed-size config's shard tiles want[] starting at lo % D; an IMIX
+    # shard is its own packets (D = n: no rotation, whatever lo)
     wt = torch.from_numpy(want.view(np.int64)).to(dev)
-    s = w.lo % w.D
+    s = w.lo % w.D if w.offs is None else 0
     if s:
         wt = torch.cat([wt[s:], wt[:s]])
     got = d_ret[: w.n]
