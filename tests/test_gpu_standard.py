@@ -160,7 +160,7 @@ def test_keep_mode_refill_on_interpreter(gpu, env):
     code, rel = stdprogs.asm([
         I("mov64_reg", 6, 1), I("ldxb", 8, 6, 0), I("and64_imm", 8, imm=7), I("add64_imm", 8, imm=1),
         I("mov64_imm", 0, imm=1), ("label", "L"),
-        I("ldxw", 2, 6, 3), I("mul64_imm", 0, imm=0x9e3779b1), I("xor64_reg", 0, 2),
+        I("ldxw", 2, 6, 3), I("mul64_imm", 0, imm=0x1e3779b1), I("xor64_reg", 0, 2),
         I("add64_imm", 6, imm=5), I("sub64_imm", 8, imm=1), I("jne_imm", 8, imm=0, off="L"),
         I("exit")])
     n = (1 << 22) + 37
