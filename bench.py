@@ -96,6 +96,12 @@ def parse(argv=None):
                          "and reported under 'also' (default: every other BASELINE config -- C2, C3, C5 "
                          "the IMIX filter -- C4H, the hashtable form of C4, C4C, C4 with a per-key "
                          "counter update, and C3L, a bounded loop under standard semantics); '' for none")
+    ap.add_argument("--also-min-ms", type=float, default=60.0,
+                    help="an --also config whose --steps would time less than this many ms runs more "
+                         "steps (up to --also-max-steps; its line says how many): a 20-step timed region "
+                         "of a 15-us launch is 0.3 ms, where one host hiccup or the first launch's "
+                         "latency decides the number")
+    ap.add_argument("--also-max-steps", type=int, default=4000)
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="eager: direct launches (default); graph: each step replays a captured HIP graph (measured 1.6%% slower on C2-C4, profiles/r01/graph_ab)")
     return ap.parse_args(argv)
@@ -103,7 +109,7 @@ def parse(argv=None):
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
                    "c4": 1 << 26, "c4c": 1 << 26, "c3l": 1 << 24, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24,
-                   "c5lit": 1 << 22}
+                   "c5lit": 1 << 22, "c5d0": 1 << 22, "c5d1": 1 << 22}
 # C4H: bytes one lookup must move.  The device table's slot is 32 B (u32 used | u32 hash | 4-B key
 # 8-B padded | 8-B value), but a random probe cannot fetch less than one 64-B line from HBM: the
 # PMC passes measured 64 B per lookup (FETCH_SIZE, profiles/r02/s3/all/bench_c4h_slots8.json:
@@ -412,9 +418,10 @@ def issue_roofline(insts, kern_ms, groups):
                 VALU_ISSUE_CYCLES, SIMDS, CLOCK_GHZ)}
 
 
-def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
+def measure(a, cfg, packets, torch, dist, world, rank, local, dev, also=False):
     """One configuration on this rank: build its shard, warm up, time a.steps launches (barrier
-    and max over ranks), verify the last launch.  Returns the numbers of the JSON line."""
+    and max over ranks), verify the last launch.  Returns the numbers of the JSON line.  An
+    --also config (also=True) times at least --also-min-ms of steps (see parse)."""
     size = packets or DEFAULT_PACKETS[cfg]
     if a.scaling == "strong":
         total = size
@@ -486,7 +493,22 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
         step(i)
     red.finish()
     torch.cuda.synchronize()
-    timed = list(range(0, a.steps, max(1, a.time_every)))  # steps whose kernel is event-timed
+    steps = a.steps
+    if also and a.also_min_ms > 0:
+        # a few more warm steps estimate the step; the count is the same on every rank (max)
+        t_est = time.perf_counter()
+        for i in range(10):
+            step(i)
+        red.finish()
+        torch.cuda.synchronize()
+        est_ms = (time.perf_counter() - t_est) * 1e3 / 10
+        want = int(np.ceil(a.also_min_ms / max(est_ms, 1e-3)))
+        steps = max(a.steps, min(a.also_max_steps, want))
+        if world > 1:
+            t = torch.tensor([steps], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            steps = int(t[0])
+    timed = list(range(0, steps, max(1, a.time_every)))  # steps whose kernel is event-timed
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in timed]
     for e0, e1 in evs:  # torch creates its events at their first record
@@ -497,7 +519,7 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     k = 0
-    for i in range(a.steps):
+    for i in range(steps):
         if k < len(timed) and timed[k] == i:
             step(i, evs[k])
             k += 1
@@ -514,8 +536,8 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
-    ms_per_step = el * 1e3 / a.steps
-    value = total * a.steps / el / 1e6
+    ms_per_step = el * 1e3 / steps
+    value = total * steps / el / 1e6
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     exec_name, layout, translate_ms, build_ms = prog.exec_info(local)
 
@@ -526,7 +548,8 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
     if not a.no_verify:  # the last timed launch against the oracle (outside the timing)
         ok, vinfo = verify(w, torch, d_ret, d_hist, world, dev)
         if cfg == "c4c":
-            c = verify_counters(w, maps, a.warmup + a.steps + (1 if graphs is not None else 0))
+            c = verify_counters(w, maps, a.warmup + steps + (10 if also and a.also_min_ms > 0 else 0) +
+                                (1 if graphs is not None else 0))
             vinfo.update(c)
             ok = ok and c["counters_verified"]
             vinfo["verified"] = ok
@@ -542,7 +565,7 @@ def measure(a, cfg, packets, torch, dist, world, rank, local, dev):
                 achieved=achieved, bytes_per_launch=bytes_per_launch, exec_name=exec_name,
                 layout=layout, translate_ms=translate_ms, build_ms=build_ms, faulted=faulted,
                 vinfo=vinfo, ok=ok, nentries=info.nentries, graph=graphs is not None,
-                samples=len(evs), kern_stats=kernel_stats(kern_samples, ms_per_step))
+                samples=len(evs), kern_stats=kernel_stats(kern_samples, ms_per_step), steps=steps)
 
 
 def kernel_stats(samples, ms_per_step):
@@ -614,7 +637,7 @@ def main():
     also = {}
     for c in [x for x in a.also.split(",") if x and x != cfg]:
         try:
-            S = measure(a, c, 0, torch, dist, world, rank, local, dev)
+            S = measure(a, c, 0, torch, dist, world, rank, local, dev, also=True)
         except Exception as e:  # reported in the line; the primary measurement stands
             also[c] = {"error": "%s: %s" % (type(e).__name__, e)}
             continue
@@ -624,6 +647,7 @@ def main():
             S["issue"] = (issue_roofline(t["insts"], S["kern_ms"], (S["n"] + 63) // 64)
                           if t and t["insts"] else None)
         also[c] = {"value": round(S["value"], 1), "unit": "Mpkt/s", "ms_per_step": round(S["ms_per_step"], 4),
+                   "steps": S["steps"], "warmup": a.warmup + 10,
                    "packets_total": S["total"], "packets_per_gpu": S["n"], "verified": S["vinfo"].get("verified"),
                    "check": S["vinfo"], "exec": S["exec_name"],
                    "kernel_layout": "staged64" if S["layout"] == 1 else "general",

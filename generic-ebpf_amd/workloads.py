@@ -273,7 +273,7 @@ def c4_map_values(seed=11, entries=256):
     return _rng(seed).integers(0, 2**63, size=entries, dtype=np.uint64)
 
 
-def _c5_nodes(seed, body):
+def _c5_nodes(seed, body, depth=2):
     g = _rng(seed)
 
     def leaf(limit):
@@ -307,17 +307,17 @@ def _c5_nodes(seed, body):
         return test + [Branch(I("jne_imm", R6, imm=0), taken)] + tree(limit, depth - 1)
 
     head = [I("ldxh", R7, R1, 16), I("be", R7, imm=16), I("mov_imm", R8, imm=0x1234)]
-    return head + [Branch(I("jgt_imm", R7, imm=1000), tree(1500, 2)),
-                   Branch(I("jgt_imm", R7, imm=100), tree(576, 2))] + tree(64, 2)
+    return head + [Branch(I("jgt_imm", R7, imm=1000), tree(1500, depth)),
+                   Branch(I("jgt_imm", R7, imm=100), tree(576, depth))] + tree(64, depth)
 
 
-def prog_c5(seed=7, target=256):
+def prog_c5(seed=7, target=256, depth=2):
     """Branch-heavy filter over IMIX packets: a 3-way split on the IPv4 total length, then a
     depth-2 tree of data-dependent tests on payload bytes (within the size class) whose leaves
     are straight segments of loads + mixing with rare data-dependent early exits.  The leaf
     length is fitted so the main (all-not-taken) path executes ``target`` instructions."""
     for body in range(target // 2, target):
-        lay = assemble(_c5_nodes(seed, body))
+        lay = assemble(_c5_nodes(seed, body, depth))
         if lay.main_path_steps >= target:
             return lay
     raise ValueError("cannot fit C5")
@@ -477,6 +477,11 @@ CONFIGS = {
                pkt="l2l3"),
     "c5": dict(desc="256-insn branch-heavy filter, IMIX 64-1500 B packets", prog=prog_c5,
                pkt="imix"),
+    # (probes: C5's shape with shallower trees, fewer leaves per group)
+    "c5d0": dict(desc="probe: C5 with depth-0 trees (3 leaves)", prog=lambda: prog_c5(depth=0),
+                 pkt="imix"),
+    "c5d1": dict(desc="probe: C5 with depth-1 trees (6 leaves)", prog=lambda: prog_c5(depth=1),
+                 pkt="imix"),
     "c4c": dict(desc="64-insn classify + array-map lookup + per-key packet counter "
                      "(counters[key] += 1 through a lookup result), 64 B packets", prog=prog_c4c,
                 pkt="l2l3"),
