@@ -248,7 +248,7 @@ for z in (4, 8):
     fam("XADD%d" % z, 2)
 for z in (4, 8):
     fam("XADDF%d" % z, 2)
-fam("OVLINIT", 0)              # dprog.h DK_OVLINIT: the lane's overlay count = 0
+fam("OVLINIT", 0)              # dprog.h DK_OVLINIT: the lane's overlay and write counts = 0
 # a counter update the translator resolved completely (asm_runtime.cpp): an immediate addend
 # (s[10:11]) into a DP_MAP_ATOMIC map's delta area at r_d + s14 (d = the value pointer, a
 # non-NULL lookup result; s14 = the offset + the map's delta-area offset)
@@ -266,7 +266,9 @@ for z in SIZES:
 LOOP_BUDGET = 1 << 20          # dprog.h DP_LOOP_BUDGET
 # the lane's stack slice below the frame (dprog.h DP_OVL_*): loop count, overlay count, the
 # scratch a store into a map value is redirected to, the overlay entries
-OVL_COUNT, VST_SCRATCH, OVL_ENTRIES = 4, 8, 16
+OVL_COUNT, VST_SCRATCH, WCOUNT, OVL_ENTRIES = 4, 8, 16, 24
+WRITES_MAX = 16             # dprog.h DP_WRITES_MAX (dp_launch.vflags bit 4, DP_VF_WCAP)
+FAULT_WRITES = 11           # include/ebpf_gpu.h EBPF_FAULT_WRITES
 VFLAGS_OFF = 0xcc              # dp_launch.vflags: bit 0 overlay, bit 1 value stores provided for
 SPILL = 51                     # v51 (H[5]): .Lr_check's SGPR spill lanes around .Lr_vstore
 
@@ -1225,10 +1227,27 @@ def hprobe_body(tag):
 def log_record(T, word, ret):
     """For the lanes in exec: a slot in the launch's write log (one atomic add on its counter per
     wave), R[4:5] = the record's address (log + 64 + slot * stride), its first 16 bytes written:
-    {u64 packet index, u32 entry | map << 20, u32 `word`}.  A full log (the host sizes it for the
-    program's most writes per path: a library bug) faults MEM, loudly, rather than lose a write;
-    exec empty after that branches to `ret`.  Uses R[0:7], S_T0..2, S_MASK, S_JUNK, s[64:69]."""
+    {u64 packet index, u32 entry | map << 20, u32 `word`}.  With dp_launch.vflags bit 4
+    (DP_VF_WCAP) every lane first counts the write in its stack slice (DP_WCOUNT): a packet's
+    write past WRITES_MAX faults it EBPF_FAULT_WRITES instead.  A full log (the host sizes it for
+    the program's most writes per path: a library bug) faults MEM, loudly, rather than lose a
+    write; exec empty after that branches to `ret`.  Uses R[0:7], S_T0..2, S_MASK, S_JUNK,
+    s[64:69]."""
     return [
+        "s_load_dword %s, s[0:1], 0x%x" % (s(S_T0), VFLAGS_OFF),
+        "s_waitcnt lgkmcnt(0)",
+        "s_bitcmp1_b32 %s, 4" % s(S_T0),
+        "s_cbranch_scc0 .Lwc_ok%s" % T,
+        "v_add_u32 %s, %d, v%d" % (v(R[0]), WCOUNT, V_STK),
+        "v_mov_b32 %s, 1" % v(R[1]),
+        "ds_add_rtn_u32 %s, %s, %s" % (v(R[2]), v(R[0]), v(R[1])),
+        "s_waitcnt lgkmcnt(0)",
+        "v_cmp_le_u32_e64 %s, %d, %s" % (sp(S_MASK), WRITES_MAX, v(R[2])),
+        "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
+        "s_cbranch_scc0 .Lwc_ok%s" % T,
+        "s_mov_b32 %s, %d" % (s(S_CODE), FAULT_WRITES)] + call(".Lr_fault") + [
+        "s_cbranch_execz %s" % ret,
+        ".Lwc_ok%s:" % T,
         # a log slot per lane: one atomic add on the log's counter for the wave
         "s_load_dwordx4 s[64:67], s[0:1], 0x80",         # upd_log, upd_cap, upd_stride
         "s_load_dwordx2 s[68:69], s[0:1], 0x90",         # pkt_base
@@ -1548,6 +1567,28 @@ def vstore_routine():
          "s_andn2_b64 exec, %s, exec" % sp(S_MASK),                # the lanes left: records
          ".Lvs_rec:",
          "s_cbranch_execz .Lvs_ret",
+         # capped writes (vflags bit 4, DP_VF_WCAP): a plain store (ADD = 0; an aligned addition
+         # is not counted) counts in the lane's slice; the one past WRITES_MAX faults
+         "s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
+         "s_waitcnt lgkmcnt(0)",
+         "s_bitcmp1_b32 %s, 4" % s(S_T3),
+         "s_cbranch_scc0 .Lvs_wc_ok",
+         "v_cmp_eq_u32_e64 vcc, 0, %s" % v(ADD),
+         "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+         "s_cbranch_execz .Lvs_wc_none",
+         "v_add_u32 %s, %d, v%d" % (v(R[1]), WCOUNT, V_STK),
+         "v_mov_b32 %s, 1" % v(R[9]),
+         "ds_add_rtn_u32 %s, %s, %s" % (v(R[9]), v(R[1]), v(R[9])),
+         "s_waitcnt lgkmcnt(0)",
+         "v_cmp_le_u32_e64 vcc, %d, %s" % (WRITES_MAX, v(R[9])),
+         "s_and_b64 vcc, vcc, exec",
+         ".Lvs_wc_none:",                         # (vcc = the lanes past the cap, or none)
+         "s_mov_b64 exec, %s" % sp(S_MASK),
+         "s_andn2_b64 exec, exec, vcc",
+         "s_or_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),
+         "s_mov_b32 %s, %d" % (s(S_CODE), FAULT_WRITES),
+         "s_cbranch_execz .Lvs_ret",
+         ".Lvs_wc_ok:",
          # the record's word and data (an addition: the addend; else the stored bytes)
          "s_lshl_b32 %s, %s, 20" % (s(S_T3), s(S_T2)),
          "s_or_b32 %s, %s, 0x%x" % (s(S_T3), s(S_T3), 0x80000),
@@ -1564,7 +1605,7 @@ def vstore_routine():
          "s_waitcnt lgkmcnt(0)",
          "s_cmp_eq_u64 s[64:65], 0",
          "s_cbranch_scc0 .Lvs_log",
-         "s_mov_b64 %s, exec" % sp(S_JUNK),                       # (no log: a library bug)
+         "s_or_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),       # (no log: a library bug)
          "s_mov_b32 %s, 3" % s(S_CODE),
          "s_branch .Lvs_ret",
          ".Lvs_log:",
@@ -1584,8 +1625,10 @@ def vstore_routine():
          # a full log (the host sizes it for the program's records per path: a library bug)
          # faults MEM, loudly, rather than losing a write
          "v_cmp_gt_u32_e64 vcc, s66, %s" % v(OFF),
-         "s_andn2_b64 %s, exec, vcc" % sp(S_JUNK),
-         "s_mov_b32 %s, 3" % s(S_CODE),
+         "s_andn2_b64 %s, exec, vcc" % sp(S_MASK),
+         "s_or_b64 %s, %s, %s" % (sp(S_JUNK), sp(S_JUNK), sp(S_MASK)),
+         "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
+         "s_cselect_b32 %s, %s, 3" % (s(S_CODE), s(S_CODE)),
          "s_and_b64 exec, exec, vcc",
          "s_cbranch_execz .Lvs_ret",
          # the record: log + 64 + slot * stride
@@ -1868,9 +1911,10 @@ def handler_body(name, d, sr):
         if z == 8:
             return out + ["ds_add_u64 %s, %s" % (v(H[0]), vp(H[2]))], False
         return out + ["ds_add_u32 %s, %s" % (v(H[0]), v(H[2]))], False
-    if name == "OVLINIT":
+    if name == "OVLINIT":   # the overlay's count and the logged-write count
         return ["v_mov_b32 %s, 0" % v(H[0]), "v_add_u32 %s, %d, v%d" % (v(H[1]), OVL_COUNT, V_STK),
-                "ds_write_b32 %s, %s" % (v(H[1]), v(H[0]))], False
+                "ds_write_b32 %s, %s" % (v(H[1]), v(H[0])),
+                "ds_write_b32 %s, %s offset:%d" % (v(H[1]), v(H[0]), WCOUNT - OVL_COUNT)], False
     if name == "LOOPINIT":
         return ["v_mov_b32 %s, 0" % v(H[0]), "ds_write_b32 v%d, %s" % (V_STK, v(H[0]))], False
     if name == "LOOPCNT":

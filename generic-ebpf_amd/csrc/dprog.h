@@ -56,14 +56,16 @@ enum dp_kind : uint16_t {
 	// XADD (standard semantics, BPF_STX | BPF_XADD): *(u32 / u64 *)(dst + off) += src; aux = 4
 	// or 8 bytes, | 0x100 when imm was BPF_FETCH (src = the old value)
 	DK_XADD = 0x112,
-	// A program that reads its own stores into map values starts here: the lane's overlay is
-	// emptied (dprog.h DP_OVL_COUNT = 0)
+	// A program that reads its own stores into map values, or whose writes are capped, starts
+	// here: the lane's overlay is emptied and its write count zeroed (DP_OVL_COUNT, DP_WCOUNT = 0)
 	DK_OVLINIT = 0x113,
 };
 #define DP_VF_EXTENTS 4u // dp_launch.vflags: offsets are (start, end) pairs
 // dp_launch.vflags: the assembly interpreter's staged kernel keeps each group's packets in the
 // wave's LDS packet buffer until the group ends (keep mode: LDXPKTV reads them there)
 #define DP_VF_KEEP 8u
+// dp_launch.vflags: count each packet's logged writes and fault the one past DP_WRITES_MAX
+#define DP_VF_WCAP 16u
 #define DP_LOOP_BUDGET (1u << 20) // taken backward jumps a lane may make (standard semantics)
 #define DP_CLS_JMP32 6
 
@@ -206,13 +208,21 @@ static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_g) ==
 	      "gen_interp.py loads these fields at fixed offsets");
 
 // The lane's LDS stack slice, below the frame the program addresses: the loop count (+0), the
-// overlay's entry count (+4), an 8-byte scratch a store into a map value is redirected to (+8)
-// and the overlay entries (+16: {u64 word address, u64 word as the packet sees it}, 16 B each).
-// Programs with value stores keep at least the first 16 bytes.
+// overlay's entry count (+4), an 8-byte scratch a store into a map value is redirected to (+8),
+// the packet's logged writes (+16, dp_launch.vflags DP_VF_WCAP) and the overlay entries (+24:
+// {u64 word address, u64 word as the packet sees it}, 16 B each).  Programs with value stores or
+// capped writes keep at least the first 24 bytes.
 #define DP_OVL_COUNT 4u
 #define DP_OVL_SCRATCH 8u
-#define DP_OVL_ENTRIES 16u
+#define DP_WCOUNT 16u
+#define DP_OVL_ENTRIES 24u
 #define DP_OVL_MAX 32u // overlay entries per lane at most (more: the program runs on the CPU)
+// Logged writes a packet may make in a device batch (ebpf_gpu.h "Map writes in a device batch":
+// successful map_update_elem / map_delete_elem calls and stores into map values other than
+// aligned counter updates); the next one faults EBPF_FAULT_WRITES.  Checked on the device only
+// where a path can exceed it (programs with loops, dp_launch.vflags DP_VF_WCAP); 2 x this many
+// overlay words hold every store it allows (DP_OVL_MAX)
+#define DP_WRITES_MAX 16u
 
 // Value-store records in the batch's write log: {u64 packet, u32 map << 20 | DP_REC_VALUE |
 // kind << 16 | size, u32 byte offset (array: in the map's values; hashtable: in the value),

@@ -23,8 +23,17 @@ constexpr int kHistBins = 257;
 
 enum {
 	F_NONE = 0, F_BAD_OPCODE = 1, F_DIV_ZERO = 2, F_MEM = 3, F_SLOT = 4, F_HELPER = 5,
-	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10
+	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10,
+	F_WRITES = 11
 };
+
+// A logged write of the packet (dp_launch.vflags DP_VF_WCAP: counted; the one past
+// DP_WRITES_MAX faults EBPF_FAULT_WRITES before it happens)
+__device__ inline bool
+over_cap(const dp_launch &L, uint32_t &writes)
+{
+	return (L.vflags & DP_VF_WCAP) && ++writes > DP_WRITES_MAX;
+}
 
 __device__ inline uint32_t
 wave_min(uint32_t v)
@@ -200,8 +209,8 @@ log_record(const dp_launch &L, uint64_t gid, uint32_t map, uint32_t word)
 // delta area; the rest log a record for after the batch.  The packet's overlay remembers v.
 // Returns 0 or a fault code.
 __device__ inline int
-value_store(const dp_launch &L, uint64_t gid, overlay &o, int mi, uint64_t a, uint32_t size,
-	    uint64_t v, bool add, uint64_t delta)
+value_store(const dp_launch &L, uint64_t gid, overlay &o, uint32_t &writes, int mi, uint64_t a,
+	    uint32_t size, uint64_t v, bool add, uint64_t delta)
 {
 	const dp_map &mp = L.maps[mi];
 	uint64_t off = a - mp.dev_base, voff = off;
@@ -212,6 +221,8 @@ value_store(const dp_launch &L, uint64_t gid, overlay &o, int mi, uint64_t a, ui
 		voff = (off & ((1ull << lg) - 1)) - dp_hash_value_off(dp_hash_key_size(mp.flags));
 	}
 	add = add && voff % size == 0;
+	if (!add && over_cap(L, writes)) // (aligned additions are not counted)
+		return F_WRITES;
 	if ((L.vflags & 1) && !ovl_store(o, a, size, v))
 		return F_MEM;
 	if (add && (mp.flags & DP_MAP_ATOMIC)) {
@@ -274,6 +285,7 @@ ebpf_interp_v0(dp_launch L)
 	uint64_t result = 0;
 	uint32_t back = 0; // taken backward jumps (DK_LOOPCNT, standard semantics)
 	overlay ovl;       // stores into map values the packet reads back (dp_launch.vflags)
+	uint32_t writes = 0; // logged writes (DP_VF_WCAP)
 
 	for (;;) {
 		const uint64_t am = __ballot(active);
@@ -307,6 +319,7 @@ ebpf_interp_v0(dp_launch L)
 		}
 		if (k == DK_OVLINIT) {
 			ovl.n = 0;
+			writes = 0;
 			continue;
 		}
 		if (k == DK_LOOPCNT) {
@@ -376,7 +389,8 @@ ebpf_interp_v0(dp_launch L)
 					res = exists && (r4 & 1) ? 17 : !exists && (r4 & 2) ? 2
 					    : !exists && trailer[0] >= trailer[1] ? 16 : 0;
 					if (res == 0) {
-						if ((f = check(rg, L, r3, mp.value_size, false))) {
+						if ((f = check(rg, L, r3, mp.value_size, false)) ||
+						    (over_cap(L, writes) && (f = F_WRITES))) {
 							fault = f;
 							active = false;
 							continue;
@@ -409,6 +423,11 @@ ebpf_interp_v0(dp_launch L)
 						continue;
 					}
 					if (key < mp.max_entries) {
+						if (over_cap(L, writes)) {
+							fault = F_WRITES;
+							active = false;
+							continue;
+						}
 						uint8_t *rec = log_record(L, gid, e.aux, key);
 						if (!rec) {
 							fault = F_MEM; // (the host sizes the log: never)
@@ -434,6 +453,8 @@ ebpf_interp_v0(dp_launch L)
 				const dp_map &mp = L.maps[e.aux];
 				const uint32_t ks = dp_hash_key_size(mp.flags);
 				int f = check(rg, L, r2, ks, false);
+				if (!f && over_cap(L, writes))
+					f = F_WRITES;
 				uint8_t *rec = f ? nullptr : log_record(L, gid, e.aux, 1);
 				if (f || !rec) {
 					fault = f ? f : F_MEM;
@@ -521,7 +542,7 @@ ebpf_interp_v0(dp_launch L)
 					v = old + v;
 			}
 			if (mi >= 0)
-				f = value_store(L, gid, ovl, mi, a, size, v, add, delta & mask);
+				f = value_store(L, gid, ovl, writes, mi, a, size, v, add, delta & mask);
 			else
 				store_bytes(a, size, v);
 			if (f) {

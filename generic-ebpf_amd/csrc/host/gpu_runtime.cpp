@@ -1051,7 +1051,8 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	L.nentries = dp->nentries;
 	L.start = ep->xlated->start;
 	L.vflags = (ep->xlated->vstore_overlay ? 1u : 0u) | (ep->xlated->vstore_sites ? 2u : 0u) |
-		   (ep->xlated->ovl_entries << 8) | (L0.vflags & DP_VF_EXTENTS);
+		   (ep->xlated->ovl_entries << 8) | (L0.vflags & DP_VF_EXTENTS) |
+		   (ep->xlated->write_cap ? DP_VF_WCAP : 0u);
 	launch_order order(ep->xlated->maps);
 	int err = sync_map_mirrors(ep, dp->device, stream);
 	if (err)

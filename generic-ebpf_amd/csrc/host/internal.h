@@ -228,6 +228,8 @@ struct dprog_host {
 	uint32_t vstore_sites = 0;           // stores into map values / counter updates / XADD (reached)
 	bool vstore_overlay = false;         // a load may read what the packet stored into a map value
 	uint32_t ovl_entries = 0;            // ... overlay words per lane (2 per store on a path)
+	bool write_cap = false;              // a path may log more than DP_WRITES_MAX writes (loops):
+	                                     // the device counts them per packet (DP_VF_WCAP)
 	int error = 0;
 	std::string error_msg;
 };

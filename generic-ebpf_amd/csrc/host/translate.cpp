@@ -1044,6 +1044,87 @@ fuse_counters(dprog_host &out, bool std_mode)
 	return grew;
 }
 
+// Registers an entry reads and writes, for liveness (a read over-approximated, a write only where
+// certain; an entry kind not listed reads every register).
+void
+reg_rw(const dp_entry &e, uint16_t *rd, uint16_t *wr)
+{
+	const uint16_t k = e.kind, d = (uint16_t)(1u << (e.dst & 15)), s = (uint16_t)(1u << (e.src & 15));
+	*rd = 0;
+	*wr = 0;
+	switch (k) {
+	case DK_FAULT: case DK_LOOPINIT: case DK_LOOPCNT: case DK_OVLINIT:
+		return;
+	case EBPF_OP_EXIT:
+		*rd = 1;
+		return;
+	case DK_CALL_LOOKUP: case DK_CALL_HDELETE: // (map, key)
+		*rd = 0x6;
+		*wr = 1;
+		return;
+	case DK_CALL_UPDATE: // (map, key, value, flags)
+		*rd = 0x1e;
+		*wr = 1;
+		return;
+	case DK_CNT_STORE: case DK_XADD:
+		*rd = d | s;
+		return;
+	case DK_MOV64R:
+		*rd = s;
+		*wr = d;
+		return;
+	case EBPF_OP_LDDW:
+		*wr = d;
+		return;
+	default:
+		break;
+	}
+	if (k >= DK_NEG64 && k <= DK_MOD32Z) {
+		*rd = d | s;
+		*wr = d;
+		return;
+	}
+	if (k >= 0x100) {
+		*rd = 0x7ff;
+		return;
+	}
+	switch (k & 7) {
+	case EBPF_CLS_LDX: *rd = s; *wr = d; return;
+	case EBPF_CLS_ST: *rd = d; return;
+	case EBPF_CLS_STX: *rd = d | s; return;
+	case EBPF_CLS_JMP: case DP_CLS_JMP32: *rd = d | ((k & 0x08) ? s : 0); return;
+	default: *rd = d | ((k & 0x08) ? s : 0); *wr = d; return; // ALU / ALU64
+	}
+}
+
+// Registers live after each entry (a backward pass to a fixed point: the graph may have loops).
+std::vector<uint16_t>
+live_out(const dprog_host &out)
+{
+	const size_t n = out.entries.size();
+	std::vector<uint16_t> rd(n), wr(n), lin(n, 0), lout(n, 0);
+	for (size_t i = 0; i < n; i++)
+		reg_rw(out.entries[i], &rd[i], &wr[i]);
+	for (bool changed = true; changed;) {
+		changed = false;
+		for (size_t i = n; i-- > 0;) {
+			uint16_t o = 0;
+			for (int k = 0; k < 2; k++) {
+				const uint32_t sx = succ_of(out, (uint32_t)i, k);
+				if (sx < n)
+					o |= lin[sx];
+			}
+			const uint16_t in = rd[i] | (uint16_t)(o & ~wr[i]);
+			if (o != lout[i] || in != lin[i]) {
+				lout[i] = o;
+				lin[i] = in;
+				changed = true;
+			}
+		}
+	}
+	return lout;
+}
+
 // Stores into map values (ebpf_gpu.h "Stores into map values"): which maps they may reach and
 // how each written map's writes land (dprog_host upd_maps / hupd_maps / atomic_maps), whether
 // the packet may read its own stores back (the overlay), and the write log's records per path.
@@ -1095,12 +1176,6 @@ analyze_writes(dprog_host &out)
 			if (!one || out.maps[m]->value_size % w || ((o % w) + w) % w)
 				exact[m] = 0;
 		}
-	}
-	if (out.vstore_sites && out.has_loops) {
-		out.error = EOPNOTSUPP;
-		out.error_msg = "device batches run stores into map values only in loop-free programs "
-				"(run this one with ebpf_prog_run)";
-		return EOPNOTSUPP;
 	}
 	for (size_t m = 0; m < nm; m++) {
 		const uint16_t t = (uint16_t)m;
@@ -1170,17 +1245,70 @@ analyze_writes(dprog_host &out)
 			}
 		}
 	}
+	// A counter update whose register nobody reads after its STX needs no value the packet sees:
+	// its addition is the same whatever was loaded, so neither it nor the idiom's LDX makes the
+	// packet read its own stores back (the overlay)
+	const std::vector<uint16_t> lout = live_out(out);
+	auto cnt_dead = [&](size_t k) {
+		const dp_entry &c = out.entries[k];
+		return c.kind == DK_CNT_STORE && !((lout[k] >> c.src) & 1);
+	};
+	auto idiom_head_dead = [&](size_t i) { // LDX i -> ALU -> CNT_STORE with a dead register
+		const dp_entry &e = out.entries[i];
+		if (!(e.kind == EBPF_OP_LDXW || e.kind == EBPF_OP_LDXDW) || e.next >= n)
+			return false;
+		const uint32_t k = out.entries[e.next].next;
+		if (k >= n)
+			return false;
+		const dp_entry &c = out.entries[k];
+		return c.kind == DK_CNT_STORE && c.src == e.dst && c.dst == e.src && c.off == e.off && cnt_dead(k);
+	};
 	out.vstore_overlay = false;
 	for (size_t i = 0; i < n && !out.vstore_overlay; i++) {
 		const dp_entry &e = out.entries[i];
 		if (!out.annot[i].reached || !stored[i])
 			continue;
-		if (e.kind == DK_CNT_STORE || e.kind == DK_XADD) {
-			out.vstore_overlay = true; // (they read the value back first)
+		if (e.kind == DK_CNT_STORE) {
+			out.vstore_overlay = !cnt_dead(i); // (it loaded the value it adds to)
+		} else if (e.kind == DK_XADD) {
+			out.vstore_overlay = (e.aux & 0x100) != 0; // (BPF_FETCH returns the old value)
 		} else if (e.kind < 0x100 && (e.kind & 7) == EBPF_CLS_LDX) {
 			const av &b = out.annot[i].in[e.src];
-			out.vstore_overlay = b.kind != AV_STACK && b.kind != AV_CTX && b.kind != AV_CTXV;
+			out.vstore_overlay = b.kind != AV_STACK && b.kind != AV_CTX && b.kind != AV_CTXV &&
+					     !idiom_head_dead(i);
 		}
+	}
+	// Programs with loops: a path has no bound on its writes.  Counter updates must be device
+	// atomics (an array only aligned counter updates of one width change) the packet never reads
+	// back (no overlay entry each); the logged writes are capped per packet (DP_WRITES_MAX, the
+	// next one faults EBPF_FAULT_WRITES), which also bounds the overlay (two words per store)
+	bool counters = false;
+	for (size_t i = 0; i < n; i++) {
+		const dp_entry &e = out.entries[i];
+		if (!out.annot[i].reached || !(e.kind == DK_CNT_STORE || e.kind == DK_XADD))
+			continue;
+		counters = true;
+		if (!out.has_loops)
+			continue;
+		const av &b = out.annot[i].in[e.dst];
+		for (size_t m = 0; m < nm; m++) {
+			if ((b.kind == AV_MAPVAL || b.kind == AV_MAPVAL_NULL) && b.map >= 0 && (size_t)b.map != m)
+				continue;
+			if (std::find(out.atomic_maps.begin(), out.atomic_maps.end(), (uint16_t)m) ==
+			    out.atomic_maps.end()) {
+				out.error = EOPNOTSUPP;
+				out.error_msg = "in a program with loops, counter updates must go to an array map that "
+						"only aligned counter updates of one width change (run this one with "
+						"ebpf_prog_run)";
+				return EOPNOTSUPP;
+			}
+		}
+	}
+	if (out.has_loops && counters && out.vstore_overlay) {
+		out.error = EOPNOTSUPP;
+		out.error_msg = "in a program with loops, the packet may not read back the values its counter "
+				"updates change (run this one with ebpf_prog_run)";
+		return EOPNOTSUPP;
 	}
 	// per path: records the log needs, stores the overlay holds
 	std::vector<uint32_t> best(n, 0), bests(n, 0);
@@ -1216,6 +1344,15 @@ analyze_writes(dprog_host &out)
 	}
 	out.max_updates = best[out.start];
 	out.ovl_entries = out.vstore_overlay ? 2 * bests[out.start] : 0;
+	out.write_cap = out.max_updates > DP_WRITES_MAX;
+	if (out.has_loops) { // (the path counts above do not bound a loop)
+		bool logging = false;
+		for (size_t i = 0; i < n && !logging; i++)
+			logging = out.annot[i].reached && logs(i);
+		out.write_cap = logging;
+		out.max_updates = logging ? DP_WRITES_MAX : 0;
+		out.ovl_entries = out.vstore_overlay ? 2 * DP_WRITES_MAX : 0;
+	}
 	if (out.ovl_entries > DP_OVL_MAX) {
 		out.error = EOPNOTSUPP;
 		out.error_msg = "the program stores into map values and reads them back more often on one "
@@ -1449,17 +1586,6 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		if (std::find(written.begin(), written.end(), (uint16_t)mi) == written.end())
 			written.push_back((uint16_t)mi);
 	}
-	// a map write inside a loop has no per-packet bound for the batch's write log
-	if (out.has_loops)
-		for (size_t i = 0; i < out.entries.size(); i++)
-			if ((out.entries[i].kind == DK_CALL_UPDATE || out.entries[i].kind == DK_CALL_HDELETE) &&
-			    out.annot[i].reached) {
-				out.error = EOPNOTSUPP;
-				out.error_msg = "device batches run map_update_elem only in loop-free programs "
-						"(run this one with ebpf_prog_run)";
-				out.maps.clear();
-				return EOPNOTSUPP;
-			}
 	// a counted loop that cannot reach the budget needs no count
 	if (out.has_loops && getenv("EBPF_XLATE_KEEP_LOOPCNT") == nullptr && elide_loop_count(out))
 		dataflow(out);
@@ -1477,7 +1603,7 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		out.maps.clear();
 		return out.error;
 	}
-	if (out.vstore_overlay) { // every lane's overlay starts empty
+	if (out.vstore_overlay || out.write_cap) { // every lane's overlay and write count start at 0
 		dp_entry x;
 		memset(&x, 0, sizeof(x));
 		x.kind = DK_OVLINIT;

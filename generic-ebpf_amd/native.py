@@ -27,7 +27,7 @@ HELPER_LOOKUP, HELPER_UPDATE, HELPER_DELETE, HELPER_OTHER = range(4)
 EBPF_ANY, EBPF_NOEXIST, EBPF_EXIST = 0, 1, 2
 
 FAULT_NAMES = ["NONE", "BAD_OPCODE", "DIV_ZERO", "MEM", "SLOT", "HELPER", "HELPER_UNSUPPORTED",
-               "BAD_REG", "LOOP", "MAP_WRITE", "BAD_MAP"]
+               "BAD_REG", "LOOP", "MAP_WRITE", "BAD_MAP", "WRITES"]
 
 
 class ProgAttr(ctypes.Structure):

@@ -57,6 +57,11 @@ struct ebpf_map;
  *     against the maps of the program; r1 NULL (or a NULL key / value, or flags > EBPF_EXIST)
  *     is EINVAL as in ebpf_map.c:101-108 / :130-136, a pointer that is no map of them faults
  *     EBPF_FAULT_BAD_MAP (the reference dereferences it);
+ *   - a packet may make 16 logged writes: successful map_update_elem / map_delete_elem calls
+ *     and stores into map values, counter updates aligned to their width (below) not counted
+ *     (they are additions).  The 17th faults the packet with EBPF_FAULT_WRITES (a fault: its
+ *     writes do not land, its counter updates do).  A loop-free path of at most 16 such writes never meets the limit; programs
+ *     with loops (standard semantics) may write inside them under it;
  *   - a writing program sharded over several devices (ebpf_prog_run_batch_multi*): the batch is
  *     the shards in order, every shard reads the batch-start maps, and the shards' writes are
  *     merged on the host in that global packet order after the last shard — the same result as
@@ -86,8 +91,12 @@ struct ebpf_map;
  *   - a packet that faults leaves no write behind except its counter updates, which are atomic
  *     operations: they take effect when executed;
  *   - EBPF_FAULT_MAP_WRITE is left for a store into a map value the translation did not provide
- *     for (a packet-relative pointer that lands in a map); programs with loops cannot store into
- *     map values on the device (EOPNOTSUPP, as for map_update_elem).
+ *     for (a packet-relative pointer that lands in a map);
+ *   - in a program with loops (standard semantics) a counter update must go to an array that
+ *     only aligned counter updates of one width change, and may not be read back by the packet
+ *     (an XADD without BPF_FETCH, or the LDX / ADD / STX idiom whose register is dead after the
+ *     STX): the batch functions return EOPNOTSUPP otherwise.  Plain stores and map_update_elem /
+ *     map_delete_elem in loops are limited only by the 16 logged writes per packet.
  * How it runs: arrays changed only by aligned counter updates of one width take device atomics
  * into a delta area next to their mirror (added into the values after the batch); other arrays'
  * stores land on the device (per-byte winners); hashtables, and arrays that mix counter updates
@@ -108,6 +117,8 @@ enum ebpf_fault {
 	EBPF_FAULT_MAP_WRITE = 9,    /* store into a map value through a pointer the translation did
 	                                not see reach a map ("Stores into map values" above) */
 	EBPF_FAULT_BAD_MAP = 10,     /* map helper called with r1 not a map of this program's env */
+	EBPF_FAULT_WRITES = 11,      /* the packet's 17th logged map write in a device batch ("Map
+	                                writes in a device batch" above) */
 	EBPF_FAULT_MAX
 };
 
@@ -272,10 +283,9 @@ int ebpf_gpu_time_next_launch(void *start_event, void *stop_event);
  *       DIV by zero gives 0 and MOD by zero leaves dst (32-bit ops: truncated), and the JMP32
  *       class (opcode class 0x06, compares of the low 32 bits).  Loops: in a device batch a
  *       packet may take 2^20 backward jumps (taken jumps whose target is at or before their own
- *       slot); the next one stops it with EBPF_FAULT_LOOP.  Programs with loops run on the
- *       assembly interpreter (variant 0 compiles loop-free programs only); a map_update_elem in
- *       a program with loops makes the batch functions return EOPNOTSUPP.  ebpf_prog_run runs
- *       any program unbounded.
+ *       slot); the next one stops it with EBPF_FAULT_LOOP.  Map writes inside loops: see "Map
+ *       writes in a device batch" and "Stores into map values" above (16 logged writes per
+ *       packet; counter updates as additions).  ebpf_prog_run runs any program unbounded.
  * Applies to ebpf_prog_run and to device batches.  Returns 0, EINVAL (bad argument) or EBUSY
  * (the program was already translated for a device). */
 #define EBPF_SEM_REFERENCE 0

@@ -20,6 +20,7 @@
 enum {
 	F_NONE = 0, F_BAD_OPCODE = 1, F_DIV_ZERO = 2, F_MEM = 3, F_SLOT = 4, F_HELPER = 5,
 	F_HELPER_UNSUPPORTED = 6, F_BAD_REG = 7, F_LOOP = 8, F_MAP_WRITE = 9, F_BAD_MAP = 10,
+	F_WRITES = 11,
 	F_UNDEF = 100 /* oracle only (oracle_prog.track_undef): a read of a stack byte no store wrote */
 };
 
@@ -278,7 +279,20 @@ struct wlog {
 static __thread struct wlog *t_wlog; /* set by oracle_run_batch per thread */
 static __thread uint64_t t_pkt;
 static __thread uint32_t t_seq;
+static __thread uint32_t t_writes; /* the packet's logged writes (ebpf_oracle.h: at most 16) */
 static __thread int t_sequential; /* oracle_prog.sequential: writes land at once */
+#define ORACLE_WRITES_MAX 16u /* include/ebpf_gpu.h EBPF_FAULT_WRITES (dprog.h DP_WRITES_MAX) */
+
+/* A logged write of the batch (a map_update_elem / map_delete_elem that succeeds, a store into a
+ * map value other than an aligned counter update): 0, or F_WRITES for the packet's 17th.  Only in
+ * batch mode (the reference's own run, sequential or one packet, has no such limit). */
+static inline int
+count_write(void)
+{
+	if (t_sequential || t_wlog == NULL)
+		return 0;
+	return ++t_writes > ORACLE_WRITES_MAX ? F_WRITES : 0;
+}
 
 static void
 wlog_push2(uint32_t map, uint32_t key, const uint8_t *a, uint32_t na, const uint8_t *b, uint32_t nb)
@@ -366,6 +380,11 @@ value_store(const struct region_env *re, int mi, uint64_t addr, int size, uint64
 	if (t_sequential || w == NULL || t_ovl == NULL) {
 		store_n(addr, size, v);
 		return 0;
+	}
+	if (!add) {
+		int f = count_write();
+		if (f)
+			return f;
 	}
 	for (int i = 0; i < size; i++) {
 		int f = ovl_put(addr + (uint64_t)i, (uint8_t)(v >> (8 * i)));
@@ -502,6 +521,8 @@ helper_map_update(struct region_env *re, int checked, uint64_t r1, uint64_t r2, 
 		if (rc == 0) {
 			if (checked && (*fault = check_access(re, r3, m->value_size, 0)))
 				return 0;
+			if ((*fault = count_write()))
+				return 0;
 			wlog_push2(mi, 1u | (uint32_t)r4 << 8, (const uint8_t *)(uintptr_t)r2, m->key_size,
 				   (const uint8_t *)(uintptr_t)r3, m->value_size);
 		}
@@ -520,6 +541,8 @@ helper_map_update(struct region_env *re, int checked, uint64_t r1, uint64_t r2, 
 		memmove(m->data + (uint64_t)m->value_size * k, (const void *)(uintptr_t)r3, m->value_size);
 		return 0;
 	}
+	if ((*fault = count_write()))
+		return 0;
 	wlog_push(mi, k, (const uint8_t *)(uintptr_t)r3, m->value_size);
 	return 0;
 }
@@ -540,6 +563,8 @@ helper_map_delete(struct region_env *re, int checked, uint64_t r1, uint64_t r2, 
 		/* hashtable_map_delete_elem (ebpf_map_hashtable.c:475-502): 0 whatever the table
 		 * holds; the key is hashed (read) first */
 		if (checked && (*fault = check_access(re, r2, m->key_size, 0)))
+			return 0;
+		if ((*fault = count_write()))
 			return 0;
 		wlog_push2(mi, 2u, (const uint8_t *)(uintptr_t)r2, m->key_size, NULL, 0);
 		return 0;
@@ -1409,6 +1434,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 			uint64_t st = 0;
 			t_pkt = (uint64_t)i;
 			t_seq = 0;
+			t_writes = 0;
 			if (t_ovl)
 				t_ovl->n = 0;
 			size_t n0 = t_wlog ? t_wlog->n : 0;

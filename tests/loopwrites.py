@@ -1,0 +1,186 @@
+"""Map writes inside loops (standard semantics; include/ebpf_gpu.h "Map writes in a device
+batch", "Stores into map values"): option walks over a TLV area of the packet — the shape
+§8(f)'s standard-semantics row exists for — that count, update and store per option, and the
+Python restatement of the batch rules each is checked against:
+
+* counter updates (XADD, or the LDX / ADD / STX idiom whose register is dead afterwards) into an
+  array only counter updates change are additions, uncapped;
+* successful map_update_elem / map_delete_elem calls and plain stores into map values are
+  logged writes: 16 per packet, the 17th faults EBPF_FAULT_WRITES (11) and the packet's logged
+  writes do not land;
+* every packet reads the batch-start maps plus its own stores.
+
+The TLV area: options from byte 14 on, {u8 type, u8 len, data...}, type 0 ends the walk, the next
+option at + 2 + (len & 3); an option that runs past the packet's end faults MEM on its load, as
+the reference's bounds check would (here: the oracle's checked mode).  Every expectation below is
+worked out from those rules, not by the implementations under test."""
+import numpy as np
+
+import stdprogs
+
+I = stdprogs.I
+NKEYS = 16
+START = 14
+FAULT_MEM, FAULT_WRITES = 3, 11
+
+
+def _walk_head():
+    """r6 = packet, r7 = cursor (packet + START), r8 = options seen; loop head "L": r2 = type, r3
+    = len (the walk ends at type 0)."""
+    return [I("mov64_reg", 6, 1), I("mov64_reg", 7, 6), I("add64_imm", 7, imm=START),
+            I("mov64_imm", 8, imm=0), ("label", "L"),
+            I("ldxb", 2, 7, 0), I("jeq_imm", 2, imm=0, off="E"), I("ldxb", 3, 7, 1)]
+
+
+def _walk_tail(extra_exit=()):
+    """r8 += 1; cursor += 2 + (len & 3); back to L.  "E": r0 = r8 (+ extra), exit."""
+    return [I("add64_imm", 8, imm=1), I("and64_imm", 3, imm=3), I("add64_imm", 3, imm=2),
+            I("add64_reg", 7, 3), I("ja", off="L"), ("label", "E"), I("mov64_reg", 0, 8)] + \
+        list(extra_exit) + [I("exit")]
+
+
+def _key_lookup(k=0):
+    """stack[-4] = type & 15; r0 = lookup(map k, &stack[-4]); a miss skips to "N"."""
+    return [I("mov64_reg", 4, 2), I("and64_imm", 4, imm=NKEYS - 1), I("stxw", 10, 4, -4),
+            ("lddw_map", 1, k), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+            I("call", imm=0), I("ldxb", 3, 7, 1), I("jeq_imm", 0, imm=0, off="N")]
+
+
+def prog_xadd_counters():
+    """Per option: counters[type & 15].packets += 1 and .bytes += len (XADD, 8-byte words of a
+    16-B value).  r0 = options."""
+    return stdprogs.asm(_walk_head() + _key_lookup() + [
+        I("mov64_imm", 9, imm=1), (0xdb, 0, 9, 0, 0), (0xdb, 0, 3, 8, 0), ("label", "N")] +
+        _walk_tail())
+
+
+def prog_idiom_counters(live=False):
+    """Per option: counters[type & 15] += len through LDX / ADD / STX.  live=True: the loaded
+    register feeds r0 afterwards (the packet reads its own additions back: refused in a loop)."""
+    body = [I("ldxdw", 5, 0, 0), I("add64_reg", 5, 3), I("stxdw", 0, 5, 0)]
+    if live:
+        body.append(I("xor64_reg", 8, 5))
+    return stdprogs.asm(_walk_head() + _key_lookup() + body + [("label", "N")] + _walk_tail())
+
+
+def prog_updates():
+    """Per option: map_update_elem(map 0, &(type & 15), &option data (8 bytes at cursor + 2),
+    ANY); r9 ^= its return code << option number.  r0 = options | r9 << 8."""
+    return stdprogs.asm(_walk_head() + [
+        I("mov64_reg", 4, 2), I("and64_imm", 4, imm=NKEYS - 1), I("stxw", 10, 4, -4),
+        ("lddw_map", 1, 0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+        I("mov64_reg", 3, 7), I("add64_imm", 3, imm=2), I("mov64_imm", 4, imm=0),
+        I("call", imm=1), I("lsh64_reg", 0, 8), I("xor64_reg", 9, 0), I("ldxb", 3, 7, 1)] +
+        _walk_tail([I("lsh64_imm", 9, imm=8), I("or64_reg", 0, 9)]))
+
+
+def prog_stores():
+    """Per option: values[type & 15] bytes 4..8 = the option's 4 data bytes (a plain store), then
+    r9 += the value's first 8 bytes as the packet sees them (its own stores over the batch-start
+    map).  r0 = options ^ r9."""
+    return stdprogs.asm(_walk_head() + _key_lookup() + [
+        I("ldxw", 5, 7, 2), I("stxw", 0, 5, 4), I("ldxdw", 5, 0, 0), I("add64_reg", 9, 5),
+        ("label", "N")] + _walk_tail([I("xor64_reg", 0, 9)]))
+
+
+def packets(n, seed, max_opts=24):
+    """64-B packets whose TLV area holds 0..max_opts options, short ones mostly (len & 3 = 0 in
+    70 %): most walks end at a type-0 option, some run off the end of the packet (MEM)."""
+    g = np.random.default_rng(seed)
+    pk = g.integers(0, 256, (n, 64), dtype=np.uint8)
+    for i in range(n):
+        k = int(g.integers(0, max_opts + 1))
+        at = START
+        for _ in range(k):
+            if at + 1 >= 64:
+                break
+            pk[i, at] = int(g.integers(1, 256))
+            ln = int(g.choice([0, 1, 2, 3], p=[0.7, 0.1, 0.1, 0.1]))
+            pk[i, at + 1] = (int(pk[i, at + 1]) & ~3) | ln
+            at += 2 + ln
+        if at < 64:
+            pk[i, at] = 0
+    return pk
+
+
+def _u(b, at, w):
+    return int.from_bytes(bytes(b[at:at + w]), "little")
+
+
+def expect(kind, pk, init, vs):
+    """(r0, fault, map bytes after the batch) of prog_<kind> over pk, step by step in each
+    program's own order of loads, checks and writes."""
+    m = bytearray(init)
+    M64 = 2**64 - 1
+    ret, flt = [], []
+    for p in pk:
+        own = bytearray(init)   # the packet's view (its own stores over the batch start)
+        adds, writes, fault = [], [], 0
+        n, r9, at = 0, 0, START
+        while True:
+            if at >= 64:                      # ldxb type
+                fault = FAULT_MEM
+                break
+            t = int(p[at])
+            if t == 0:
+                break
+            k = (t & (NKEYS - 1)) * vs
+            if kind == "updates":
+                if at + 2 + vs > 64:          # the value, region-checked before the call counts
+                    fault = FAULT_MEM
+                    break
+                if len(writes) == 16:
+                    fault = FAULT_WRITES
+                    break
+                writes.append((k, bytes(p[at + 2:at + 2 + vs])))
+            if at + 1 >= 64:                  # ldxb len
+                fault = FAULT_MEM
+                break
+            ln = int(p[at + 1])
+            if kind == "xadd":
+                adds += [(k, 1), (k + 8, ln)]
+            elif kind == "idiom":
+                adds.append((k, ln))
+            elif kind == "stores":
+                if at + 6 > 64:               # ldxw data
+                    fault = FAULT_MEM
+                    break
+                if len(writes) == 16:
+                    fault = FAULT_WRITES
+                    break
+                writes.append((k + 4, bytes(p[at + 2:at + 6])))
+                own[k + 4:k + 8] = bytes(p[at + 2:at + 6])
+                r9 = (r9 + _u(own, k, 8)) & M64
+            n += 1
+            at += 2 + (ln & 3)
+        for k, a in adds:                     # atomic additions land even when the packet faults
+            m[k:k + 8] = ((_u(m, k, 8) + a) & M64).to_bytes(8, "little")
+        if not fault:
+            for k, b in writes:
+                m[k:k + len(b)] = b
+        r0 = n ^ r9 if kind == "stores" else n
+        ret.append(0 if fault else r0)
+        flt.append(fault)
+    return np.array(ret, dtype=np.uint64), np.array(flt, dtype=np.uint8), bytes(m)
+
+
+def walk_options(p):
+    """The options a walk of packet p visits before it ends (or runs off the packet)."""
+    out, at = [], START
+    while at + 1 < 64 and int(p[at]) != 0:
+        out.append(at)
+        at += 2 + (int(p[at + 1]) & 3)
+    return out
+
+
+def prog_mixed_counter_store():
+    """A counter update and a plain store into the same array inside the loop (refused: the
+    counter would need the ordered host replay, whose log a loop cannot bound)."""
+    return stdprogs.asm(_walk_head() + _key_lookup() + [
+        I("mov64_imm", 9, imm=1), (0xdb, 0, 9, 0, 0), I("stxb", 0, 3, 4), ("label", "N")] +
+        _walk_tail())
+
+
+VALUE_SIZE = {"xadd": 16, "idiom": 8, "updates": 8, "stores": 8}
+PROGS = {"xadd": prog_xadd_counters, "idiom": prog_idiom_counters, "updates": prog_updates,
+         "stores": prog_stores}

@@ -285,3 +285,67 @@ def gen_cursor_program(seed):
         items += [I("jeq_imm", 8, imm=0, off="E"), I("ja", off="L"), ("label", "E")]
     items += [I("ldxb", 2, 6, 1), I("xor64_reg", 0, 2), I("exit")]
     return asm(items)
+
+
+def gen_loop_write_program(seed, counters=False):
+    """A standard program that writes maps inside loops (include/ebpf_gpu.h "Map writes in a
+    device batch"): 1-2 counted loops (trip counts 1-24 from packet bytes, so some packets pass
+    the 16 logged writes a packet may make and fault EBPF_FAULT_WRITES), each trip looking up
+    map 0 (16 entries, 16-B values; the key from the trip counter and a packet byte) and then,
+    at random:
+      counters=False: plain stores of 1/2/4/8 bytes of a register into the value at any
+        offset, loads back from the value (the packet reads its own stores), and
+        map_update_elem of map 1 (8-B values) with a stack value (flags ANY or, rarely,
+        NOEXIST: EEXIST, not logged);
+      counters=True: XADD (W or DW, aligned, no fetch) into map 0's value, and the LDX / ADD /
+        STX idiom on another word whose register is overwritten right after (a dead counter
+        register), no loads back.
+    r0 mixes the trip count, loaded values and helper return codes."""
+    g = np.random.default_rng(seed)
+    items = [I("mov64_reg", 6, 1), I("mov64_imm", 0, imm=int(g.integers(0, 2**31))),
+             I("mov64_imm", 9, imm=0)]
+    cw = int(g.choice([4, 8]))   # counters: one width per program (a device-atomic array)
+    nloops = 1 + int(g.random() < 0.4)
+    for li in range(nloops):
+        t = "%d" % li
+        items += [I("ldxb", 8, 6, int(g.integers(0, 64))), I("mod64_imm", 8, imm=24),
+                  I("add64_imm", 8, imm=1), ("label", "L" + t),
+                  # key = (trip + pkt byte) & 15
+                  I("ldxb", 4, 6, int(g.integers(0, 64))), I("add64_reg", 4, 8),
+                  I("and64_imm", 4, imm=15), I("stxw", 10, 4, -4),
+                  ("lddw_map", 1, 0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                  I("call", imm=0), I("jeq_imm", 0, imm=0, off="M" + t)]
+        for j in range(int(g.integers(1, 4))):
+            r = g.random()
+            if counters:
+                off = int(g.integers(0, 16 // cw)) * cw
+                if r < 0.6:
+                    items += [I("mov64_reg", 3, 8), I("add64_imm", 3, imm=int(g.integers(0, 9))),
+                              (0xdb if cw == 8 else 0xc3, 0, 3, off, 0)]
+                else:
+                    ld, st = ("ldxdw", "stxdw") if cw == 8 else ("ldxw", "stxw")
+                    items += [I(ld, 5, 0, off), I("add64_imm", 5, imm=int(g.integers(1, 100))),
+                              I(st, 0, 5, off), I("mov64_imm", 5, imm=0)]
+            elif r < 0.45:
+                z = int(g.choice([1, 2, 4, 8]))
+                op = {1: "stxb", 2: "stxh", 4: "stxw", 8: "stxdw"}[z]
+                items += [I("mov64_reg", 3, 8), I("mul64_imm", 3, imm=int(g.integers(1, 2**20))),
+                          I(op, 0, 3, int(g.integers(0, 17 - z)))]
+            elif r < 0.75:
+                z = int(g.choice([1, 2, 4, 8]))
+                op = {1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[z]
+                items += [I(op, 3, 0, int(g.integers(0, 17 - z))), I("mul64_imm", 9, imm=33),
+                          I("add64_reg", 9, 3)]
+            else:   # map_update_elem(map 1, &key, &stack value, flags); r9 += the code
+                items += [I("stxdw", 10, 8, -16), I("mov64_reg", 7, 0),
+                          ("lddw_map", 1, 1), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                          I("mov64_reg", 3, 10), I("add64_imm", 3, imm=-16),
+                          I("mov64_imm", 4, imm=1 if g.random() < 0.15 else 0),
+                          I("call", imm=1), I("add64_reg", 9, 0), I("mov64_reg", 0, 7)]
+        items += [("label", "M" + t), I("sub64_imm", 8, imm=1)]
+        if g.random() < 0.5:
+            items.append(I("jne_imm", 8, imm=0, off="L" + t))
+        else:
+            items += [I("jeq_imm", 8, imm=0, off="E" + t), I("ja", off="L" + t), ("label", "E" + t)]
+    items += [I("mov64_reg", 0, 9), I("exit")]
+    return asm(items)

@@ -1,0 +1,215 @@
+"""Map writes inside loops (include/ebpf_gpu.h "Map writes in a device
+batch", "Stores into map values"; the reference writes anywhere: ebpf_interpreter.c:343-366,
+282-284, ebpf_map_array.c:198-211).  Option walks over a TLV area (tests/loopwrites.py) that
+count with XADD and with the LDX / ADD / STX idiom, call map_update_elem and store into map
+values inside the loop.
+
+CPU: the oracle's batch mode against the step-by-step restatement in loopwrites.py (16 logged
+writes per packet, the 17th faulting EBPF_FAULT_WRITES; counter updates uncapped additions), the
+oracle's sequential mode for the counters (additions commute: the reference's own run), and the
+translation rules for loops (counter updates only into atomic arrays, never read back).
+GPU: every device variant, host-buffer and device-resident, results + faults + the map against
+the oracle."""
+import ctypes
+import errno
+import os
+
+import numpy as np
+import pytest
+
+import loopwrites as lw
+import pyoracle
+
+VARIANTS = [int(v) for v in os.environ.get("EBPF_TEST_VARIANTS", "0,1,2").split(",")]
+
+
+def _init(vs, seed):
+    return np.random.default_rng(seed).integers(0, 256, lw.NKEYS * vs, dtype=np.uint8).tobytes()
+
+
+def _oracle(kind, pk, init, sequential=False):
+    code, rel = lw.PROGS[kind]()
+    op = pyoracle.OracleProgram(code, rel, [(lw.VALUE_SIZE[kind], lw.NKEYS, init)], semantics=1,
+                                sequential=sequential)
+    ret, flt, _, _ = op.run(pk.reshape(-1), len(pk), 64, nthreads=1 if sequential else 4)
+    return ret, flt, op.map_bytes(0)
+
+
+@pytest.mark.parametrize("kind", sorted(lw.PROGS))
+def test_oracle_loop_writes_known_answers(kind):
+    pk = lw.packets(4000, 11)
+    init = _init(lw.VALUE_SIZE[kind], 12)
+    ret, flt, after = _oracle(kind, pk, init)
+    want, wf, wafter = lw.expect(kind, pk, init, lw.VALUE_SIZE[kind])
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == wafter
+    assert (wf == 0).any() and (wf == lw.FAULT_MEM).any()
+    if kind in ("updates", "stores"):
+        assert (wf == lw.FAULT_WRITES).any()       # some walks pass 16 logged writes
+    if kind in ("xadd", "idiom"):
+        # counters: the batch ends where the reference's sequential run ends
+        _, _, seq = _oracle(kind, pk, init, sequential=True)
+        assert seq == after
+
+
+def test_oracle_write_cap_is_batch_only():
+    """The reference's own run (sequential mode) has no limit: a 20-update walk succeeds."""
+    pk = lw.packets(2000, 13)
+    opts = np.array([len(lw.walk_options(p)) for p in pk])
+    init = _init(8, 14)
+    ret, flt, _ = _oracle("updates", pk, init, sequential=True)
+    assert ((opts > 16) & (flt == 0)).any()
+
+
+def _translate_error(native, env, code, rel, maps):
+    p = native.Prog(env, native.patch_relocs(code, rel, [m.handle for m in maps]))
+    try:
+        p.set_semantics(native.SEM_STANDARD)
+
+        class Info(ctypes.Structure):
+            _fields_ = [("nslots", ctypes.c_uint32), ("nentries", ctypes.c_uint32),
+                        ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
+        i = Info()
+        return native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i))
+    finally:
+        p.destroy()
+
+
+def test_loop_translation_rules(native, env):
+    """Counter updates in a loop: into an atomic array, not read back (XADD; the idiom with a
+    dead register) translate; the idiom whose register is read afterwards, and a counter update
+    into a map that stores also change, return EOPNOTSUPP.  Updates and stores in loops
+    translate (capped)."""
+    m = native.Map(env, lw.NKEYS, 16)
+    m8 = native.Map(env, lw.NKEYS, 8)
+    try:
+        assert _translate_error(native, env, *lw.prog_xadd_counters(), [m]) == 0
+        assert _translate_error(native, env, *lw.prog_idiom_counters(), [m8]) == 0
+        assert _translate_error(native, env, *lw.prog_idiom_counters(live=True), [m8]) == errno.EOPNOTSUPP
+        assert _translate_error(native, env, *lw.prog_updates(), [m8]) == 0
+        assert _translate_error(native, env, *lw.prog_stores(), [m8]) == 0
+        code, rel = lw.prog_mixed_counter_store()
+        assert _translate_error(native, env, code, rel, [m8]) == errno.EOPNOTSUPP
+    finally:
+        m.destroy()
+        m8.destroy()
+
+
+def _device(gpu, env, kind, pk, init, variant, resident):
+    import torch
+    code, rel = lw.PROGS[kind]()
+    vs = lw.VALUE_SIZE[kind]
+    m = gpu.Map(env, lw.NKEYS, vs)
+    m.fill(init)
+    p = gpu.Prog(env, gpu.patch_relocs(code, rel, [m.handle]))
+    n = len(pk)
+    try:
+        p.set_semantics(gpu.SEM_STANDARD)
+        gpu.set_variant(variant)
+        if resident:
+            dev = torch.device("cuda:0")
+            d_pk = torch.from_numpy(np.ascontiguousarray(pk.reshape(-1))).to(dev)
+            d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+            d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+            p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, d_flt.data_ptr(),
+                            None, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            ret, flt = d_ret.cpu().numpy().view(np.uint64), d_flt.cpu().numpy()
+        else:
+            ret, flt, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+        ex = p.exec_info(0)[0]
+        after = b"".join(m.lookup(k)[1] for k in range(lw.NKEYS))
+        return ret, flt, after, ex
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("kind", sorted(lw.PROGS))
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_loop_writes_vs_oracle(gpu, env, variant, kind, resident):
+    pk = lw.packets((1 << 15) + 11, 21)
+    init = _init(lw.VALUE_SIZE[kind], 22)
+    want, wf, wafter = _oracle(kind, pk, init)
+    ret, flt, after, ex = _device(gpu, env, kind, pk, init, variant, resident)
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == wafter
+    if variant == 0:
+        assert ex == "compiled"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_device_xadd_walk_full_size_equals_sequential_reference(gpu, env, variant):
+    """1M packets of the per-option XADD counter walk: the counters equal the reference's
+    sequential run (oracle, sequential mode) bit-exact."""
+    pk = lw.packets(1 << 20 if variant != 1 else 1 << 18, 23)
+    init = _init(16, 24)
+    _, _, seq = _oracle("xadd", pk, init, sequential=True)
+    ret, flt, after, _ = _device(gpu, env, "xadd", pk, init, variant, True)
+    assert after == seq
+
+
+def _random_maps(k):
+    g = np.random.default_rng(500 + k)
+    return [(16, 16, g.integers(0, 256, 256, dtype=np.uint8).tobytes()),
+            (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
+
+
+def test_oracle_random_loop_write_programs_fault_writes_somewhere():
+    """The generator's programs exercise the cap: over 40 programs some packets fault WRITES,
+    some finish, and a one-packet batch equals the sequential run (no cap for the reference)
+    whenever the packet made at most 16 logged writes."""
+    import stdprogs
+    from generic_ebpf_amd import workloads
+    seen = set()
+    for k in range(40):
+        code, rel = stdprogs.gen_loop_write_program(800 + k, counters=k % 3 == 2)
+        pk = workloads.packets_random(256, 64, seed=900 + k)
+        op = pyoracle.OracleProgram(code, rel, _random_maps(k), semantics=1)
+        ret, flt, _, _ = op.run(pk.reshape(-1), len(pk), 64, nthreads=4)
+        seen |= set(int(x) for x in np.unique(flt))
+    assert {0, lw.FAULT_WRITES} <= seen
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_device_random_loop_write_programs_vs_oracle(gpu, env, variant):
+    """Random loop programs with stores, loads back, updates (and, every third, counter
+    updates) inside the loops: results, faults and both maps against the oracle's batch mode."""
+    import stdprogs
+    from generic_ebpf_amd import workloads
+    bad = []
+    for k in range(30):
+        code, rel = stdprogs.gen_loop_write_program(800 + k, counters=k % 3 == 2)
+        maps = _random_maps(k)
+        n = 4096 + k
+        pk = workloads.packets_random(n, 64, seed=900 + k)
+        op = pyoracle.OracleProgram(code, rel, maps, semantics=1)
+        want, wf, _, _ = op.run(pk.reshape(-1), n, 64, nthreads=8)
+        ms = []
+        for vs, me, d in maps:
+            m = gpu.Map(env, me, vs)
+            m.fill(d)
+            ms.append(m)
+        p = gpu.Prog(env, gpu.patch_relocs(code, rel, [m.handle for m in ms]))
+        try:
+            p.set_semantics(gpu.SEM_STANDARD)
+            gpu.set_variant(variant)
+            ret, flt, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+            after = [b"".join(m.lookup(key)[1] for key in range(m.max_entries)) for m in ms]
+        finally:
+            gpu.set_variant(0)
+            p.destroy()
+            for m in ms:
+                m.destroy()
+        if not (np.array_equal(ret, want) and np.array_equal(flt, wf) and
+                after[0] == op.map_bytes(0) and after[1] == op.map_bytes(1)):
+            bad.append((k, int((ret != want).sum()), int((flt != wf).sum()),
+                        after[0] == op.map_bytes(0), after[1] == op.map_bytes(1)))
+    assert not bad, bad
