@@ -140,7 +140,10 @@ def test_device_loop_writes_vs_oracle(gpu, env, variant, kind, resident):
     np.testing.assert_array_equal(ret, want)
     assert after == wafter
     if variant == 0:
-        assert ex == "compiled"
+        # (a loop program that reads its own stores back keeps 32 overlay words per lane: 256
+        # lanes' slices leave the assembly kernels no room, so it runs on the portable HIP
+        # interpreter, DESIGN.md "Out of scope")
+        assert ex == ("hip" if kind == "stores" else "compiled")
 
 
 @pytest.mark.gpu
