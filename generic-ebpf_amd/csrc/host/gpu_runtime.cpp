@@ -455,9 +455,10 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 			mirror_write_begin(m, stream);
 			if (em->is_hashtable()) {
 				// a fresh snapshot of the table; the staging copy must outlive the transfer
-				map_device_image(em, m.image, c);
-				e = hipMemcpyAsync(m.dev, m.image.data(), m.image.size(), hipMemcpyHostToDevice,
-						   stream);
+				auto img = std::make_shared<std::vector<uint8_t>>();
+				map_device_image(em, *img, c);
+				m.image = img;
+				e = hipMemcpyAsync(m.dev, img->data(), img->size(), hipMemcpyHostToDevice, stream);
 				if (e == hipSuccess)
 					e = hipStreamSynchronize(stream);
 			} else {
@@ -469,8 +470,9 @@ sync_map_mirrors(struct ebpf_prog *ep, int device, hipStream_t stream)
 					hipEventSynchronize(static_cast<hipEvent_t>(m.wr_ev));
 				const size_t bytes = (size_t)em->value_size * em->max_entries;
 				const uint8_t *src = map_array_image(em, c);
-				m.image.assign(src, src + bytes);
-				e = hipMemcpyAsync(m.dev, m.image.data(), bytes, hipMemcpyHostToDevice, stream);
+				auto img = std::make_shared<std::vector<uint8_t>>(src, src + bytes);
+				m.image = img;
+				e = hipMemcpyAsync(m.dev, img->data(), bytes, hipMemcpyHostToDevice, stream);
 			}
 			if (e != hipSuccess)
 				return hip_fail(e, "hipMemcpyAsync(map mirror)");
@@ -666,6 +668,9 @@ struct upd_plan {
 	uint64_t pkt_base = 0;
 	uint32_t *faulted = nullptr; // one bit per packet of the batch (after the records)
 	size_t faulted_bytes = 0;
+	// per table map, the device table its launches read (hashtables whose values the batch
+	// stores into: a record names a slot, and this is the slot's key whatever is uploaded later)
+	std::vector<std::shared_ptr<const std::vector<uint8_t>>> tables;
 };
 
 // Log capacity for `count` packets of a map-writing program (records, and bytes: the records,
@@ -833,6 +838,7 @@ struct host_log {
 	std::vector<uint32_t> faulted;
 	uint64_t first = 0;
 	int device = -1;
+	std::vector<std::shared_ptr<const std::vector<uint8_t>>> tables; // upd_plan.tables
 };
 
 // Copy the plan's log (its records and faulted-packet bitmap) to the host.  Synchronous.
@@ -847,6 +853,7 @@ upd_fetch(const dprog_device *dp, const upd_plan &P, hipStream_t stream, uint64_
 	out->stride = dp->upd_stride;
 	out->first = first;
 	out->device = dp->device;
+	out->tables = P.tables;
 	out->rec.resize((size_t)out->count * out->stride);
 	out->faulted.resize(P.faulted_bytes / 4);
 	if (e == hipSuccess && out->count)
@@ -891,7 +898,7 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 	struct ref {
 		uint64_t order;
 		const uint8_t *r;
-		int device;
+		const host_log *h;
 	};
 	std::vector<ref> all;
 	for (const host_log &h : logs)
@@ -907,7 +914,7 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 			if (!add && pkt / 32 < h.faulted.size() && ((h.faulted[pkt / 32] >> (pkt % 32)) & 1))
 				continue; // the packet faulted: none of its writes land (counter updates do)
 			if (in_list(xl.hupd_maps, em >> 20) || (arrays && in_list(xl.upd_maps, em >> 20)))
-				all.push_back(ref{h.first + pkt, r, h.device});
+				all.push_back(ref{h.first + pkt, r, &h});
 		}
 	// Within a packet the records are already in call order: a lane takes its log slots one call
 	// after the other and every log is gathered in slot order.  (The entry index is no order: a
@@ -932,13 +939,15 @@ upd_apply_host(struct ebpf_prog *ep, const std::vector<host_log> &logs, bool arr
 			const uint32_t size = em & 0xf;
 			const bool add = (em & DP_REC_ADD) != 0;
 			if (m->is_hashtable()) {
+				// the slot's key in the table the batch's launch read (upd_plan.tables), not in
+				// whatever a later upload left in the mirror
 				uint32_t slot;
 				memcpy(&slot, x.r + 24, 4);
 				const map_device_layout l = map_device_layout_of(m);
-				std::lock_guard<std::mutex> g(m->mirror_lock);
-				if (x.device < 0 || x.device >= (int)m->mirrors.size() || slot >= l.slots)
+				const uint16_t t = (uint16_t)(em >> 20);
+				if (t >= x.h->tables.size() || !x.h->tables[t] || slot >= l.slots)
 					continue;
-				const std::vector<uint8_t> &img = m->mirrors[x.device].image;
+				const std::vector<uint8_t> &img = *x.h->tables[t];
 				const size_t so = (size_t)slot << dp_hash_stride_log2(l.flags);
 				if (so + 8 + m->key_size > img.size())
 					continue;
@@ -1043,7 +1052,7 @@ upd_finish(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_
 int
 launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t stream,
        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, bool hist_overwrite = false,
-       const upd_plan *plan = nullptr)
+       upd_plan *plan = nullptr)
 {
 	dp_launch L = L0;
 	L.maps = dp->d_maps;
@@ -1062,7 +1071,17 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	if (prog_writes_maps(*ep->xlated)) {
 		if (plan == nullptr && (err = upd_plan_for(ep, dp, L0.count, stream, &own)))
 			return err; // (this launch is the whole batch: its own log, applied below)
-		const upd_plan &P = plan ? *plan : own;
+		upd_plan &P = plan ? *plan : own;
+		if (ep->xlated->vstore_sites) // (the slot -> key map of the tables this launch reads)
+			for (uint16_t t : ep->xlated->hupd_maps) {
+				struct ebpf_map *em = ep->xlated->maps[t];
+				if (!em->is_hashtable())
+					continue;
+				std::lock_guard<std::mutex> g(em->mirror_lock);
+				if (P.tables.size() <= t)
+					P.tables.resize(t + 1);
+				P.tables[t] = em->mirrors[dp->device].image;
+			}
 		L.upd_log = P.log;
 		L.upd_cap = P.cap;
 		L.upd_stride = dp->upd_stride;

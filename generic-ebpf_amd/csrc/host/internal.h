@@ -49,7 +49,9 @@ struct map_mirror {
 	void *dev = nullptr;
 	uint64_t version = ~0ull; // host version last uploaded
 	uint16_t cpu = 0;         // percpu maps: the CPU whose copy was uploaded
-	std::vector<uint8_t> image; // host staging copy of the last upload (hashtable: the device table)
+	// host staging copy of the last upload (hashtable: the device table); a new upload makes a
+	// new one, so a batch that captured it keeps the table its packets read
+	std::shared_ptr<const std::vector<uint8_t>> image;
 	// Cross-stream order of the mirror's users on its device (gpu_runtime.cpp mirror_read /
 	// mirror_write_*): a write (an upload, or a batch's map writes landing) waits for every
 	// launch that read the mirror on another stream since the previous write, and a launch on a

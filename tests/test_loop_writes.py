@@ -216,3 +216,45 @@ def test_device_random_loop_write_programs_vs_oracle(gpu, env, variant):
             bad.append((k, int((ret != want).sum()), int((flt != wf).sum()),
                         after[0] == op.map_bytes(0), after[1] == op.map_bytes(1)))
     assert not bad, bad
+
+
+def prog_spilled_packet_stores():
+    """A loop that stores through a packet pointer reloaded from a stack spill (the translator
+    cannot prove it is the packet: a possible store into a map value): trip k
+    writes byte k + 20 of the packet, then r0 = the packet's bytes 20..28 read back."""
+    import stdprogs
+    I = stdprogs.I
+    return stdprogs.asm([
+        I("stxdw", 10, 1, -8), I("ldxb", 8, 1, 3), I("and64_imm", 8, imm=7), I("add64_imm", 8, imm=1),
+        ("label", "L"), I("ldxdw", 7, 10, -8), I("add64_reg", 7, 8), I("stxb", 7, 8, 19),
+        I("sub64_imm", 8, imm=1), I("jne_imm", 8, imm=0, off="L"),
+        I("ldxdw", 0, 1, 20), I("exit")])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("stride", [64, 72])
+def test_device_loop_stores_through_spilled_packet_pointer(gpu, env, variant, stride):
+    from generic_ebpf_amd import workloads
+    code, rel = prog_spilled_packet_stores()
+    n = 20011
+    pk = workloads.packets_random(n, stride, seed=31)
+    want, wf, wdata, _ = pyoracle.OracleProgram(code, rel, [], semantics=1).run(pk.reshape(-1), n, stride)
+    assert not wf.any()
+    p = gpu.Prog(env, code)
+    try:
+        p.set_semantics(gpu.SEM_STANDARD)
+        gpu.set_variant(variant)
+        data = np.ascontiguousarray(pk.reshape(-1).copy())
+        ret, flt, _ = p.run_batch(data, n, stride)
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+    assert not flt.any()
+    np.testing.assert_array_equal(ret, want)
+    np.testing.assert_array_equal(data, wdata)
+
+
+def test_spilled_packet_pointer_store_loop_translates(native, env):
+    code, rel = prog_spilled_packet_stores()
+    assert _translate_error(native, env, code, rel, []) == 0
