@@ -109,7 +109,8 @@ def parse(argv=None):
 
 DEFAULT_PACKETS = {"nop200": 1 << 24, "alu200": 1 << 24, "c0": 1 << 26, "c2": 1 << 20, "c3": 1 << 24,
                    "c4": 1 << 26, "c4c": 1 << 26, "c3l": 1 << 24, "c5": 1 << 22, "c4h": 1 << 26, "c3lit": 1 << 24,
-                   "c5lit": 1 << 22, "c5d0": 1 << 22, "c5d1": 1 << 22}
+                   "c5lit": 1 << 22, "c5d0": 1 << 22, "c5d1": 1 << 22, "c5ms": 1 << 22,
+                   "c5b2": 1 << 22, "c5b0": 1 << 22}
 # C4H: bytes one lookup must move.  The device table's slot is 32 B (u32 used | u32 hash | 4-B key
 # 8-B padded | 8-B value), but a random probe cannot fetch less than one 64-B line from HBM: the
 # PMC passes measured 64 B per lookup (FETCH_SIZE, profiles/r02/s3/all/bench_c4h_slots8.json:
@@ -134,6 +135,9 @@ class Workload:
         self.offs = None
         if workloads.CONFIGS[cfg]["pkt"] == "imix":
             self.pk, self.offs, _ = workloads.packets_imix_range(lo, hi, seed=5)
+            if cfg == "c5ms":  # (probe: the melded leaves' operand table)
+                t = workloads.c5meldsim_table()
+                self.maps = [(4 * t.shape[1], 16, t.tobytes())]
             self.D = self.n
             return
         self.D = min(total, DISTINCT)

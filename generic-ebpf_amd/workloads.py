@@ -311,6 +311,85 @@ def _c5_nodes(seed, body, depth=2):
                    Branch(I("jgt_imm", R7, imm=100), tree(576, depth))] + tree(64, depth)
 
 
+def _meldsim_nodes(seed, body):
+    """Probe (round 5): what melding C5's isomorphic leaves could gain, as an optimistic bound.
+    C5's shape — the 3-way size split, then per class two data-dependent bit tests — but the
+    tests do not branch: they pick a per-lane row of an LDS-resident operand table (array map 0,
+    16 rows of 4-B words, row = class * 4 + the two test bits), and ONE leaf per class runs for
+    all its lanes with every ALU immediate and early-exit verdict read from the lane's row
+    (LDXMAP: an LDS read, then the register form of the operation), as a melding compiler would
+    emit them.  Packet loads stay at the class's constant offsets and widths (a melded load
+    would add a per-lane offset and a width mask: a few VALU each, not counted here)."""
+    g = _rng(seed)
+    limits = (64, 576, 1500)
+    cols = []   # per word: values[class][variant]
+
+    def col(draw):
+        cols.append([[draw(c) for _ in range(4)] for c in range(3)])
+        return 4 * (len(cols) - 1)
+
+    plan = []
+    for k in range(body):
+        if k % 4 == 0:
+            offs = [int(g.integers(18, limits[c] - 8)) for c in range(3)]
+            op = ("ldxb", "ldxh", "ldxw", "ldxdw")[int(g.integers(0, 4))]
+            plan.append(("ld", op, offs))
+        elif k % 24 == 23:
+            offs = [int(g.integers(18, limits[c] - 1)) for c in range(3)]
+            plan.append(("exit", offs, col(lambda c: int(g.integers(0, 16)))))
+        else:
+            plan.append(("alu", ("mul64_reg", "add64_reg", "xor64_reg")[k % 3],
+                         col(lambda c: int(g.integers(1, 1 << 30)))))
+
+    def leaf(cls):
+        n, acc = [], R8
+        for k, x in enumerate(plan):
+            if x[0] == "ld":
+                n += [I(x[1], R6, R7, x[2][cls]), I("xor64_reg", acc, R6)]
+            elif x[0] == "exit":
+                n += [I("ldxb", R6, R7, x[1][cls]), I("jne_imm", R6, imm=0x5a, off="c%dk%d" % (cls, k)),
+                      I("ldxw", R0, R0, x[2]), I("exit"), ("label", "c%dk%d" % (cls, k))]
+            else:
+                n += [I("ldxw", R4, R0, x[2]), I(x[1], acc, R4)]
+        n += [I("mov_reg", R0, acc), I("rsh_imm", R0, imm=7), I("and_imm", R0, imm=15), I("exit")]
+        return n
+
+    def cls_tree(cls):
+        t = [I("mov64_reg", R7, R1), I("mov64_imm", R5, imm=4 * cls)]
+        for j in range(2):   # two tests: bit j of the row
+            t += [I("ldxb", R6, R7, int(g.integers(18, limits[cls] - 1))),
+                  I("rsh_imm", R6, imm=int(g.integers(0, 8))), I("and_imm", R6, imm=1),
+                  I("xor64_reg", R8, R6), I("lsh64_imm", R6, imm=j), I("or64_reg", R5, R6)]
+        t += [I("stxw", R10, R5, -4), LdDw(R1, MapRef(0)), I("mov64_reg", R2, R10),
+              I("add64_imm", R2, imm=-4), I("call", imm=0)]
+        return t + leaf(cls)
+
+    head = [I("ldxh", R7, R1, 16), I("be", R7, imm=16), I("mov64_imm", R8, imm=0x1234)]
+    out = head + [I("jgt_imm", R7, imm=1000, off="C2"), I("jgt_imm", R7, imm=100, off="C1")] + \
+        cls_tree(0) + [("label", "C1")] + cls_tree(1) + [("label", "C2")] + cls_tree(2)
+    return out, cols
+
+
+def prog_c5meldsim(seed=7, body=96):
+    return _asm_std(_meldsim_nodes(seed, body)[0])
+
+
+def c5meldsim_table(seed=7, body=96):
+    """prog_c5meldsim's operand table: 16 rows x one 4-B word per column (row class * 4 + v)."""
+    cols = _meldsim_nodes(seed, body)[1]
+    t = np.zeros((16, len(cols)), dtype=np.uint32)
+    for ci, vals in enumerate(cols):
+        for c in range(3):
+            for v in range(4):
+                t[4 * c + v, ci] = vals[c][v]
+    return t
+
+
+def prog_c5d(depth, body=96, seed=7):
+    """C5's generator with a given leaf body and tree depth (the probes' same-size baselines)."""
+    return assemble(_c5_nodes(seed, body, depth))
+
+
 def prog_c5(seed=7, target=256, depth=2):
     """Branch-heavy filter over IMIX packets: a 3-way split on the IPv4 total length, then a
     depth-2 tree of data-dependent tests on payload bytes (within the size class) whose leaves
@@ -356,23 +435,30 @@ def prog_literal(nslots):
 
 
 def _asm_std(items):
-    """Standard-semantics code (pc += off + 1) from Insn and ("label", name) items; a jump's
-    ``off`` may name a label."""
+    """Standard-semantics code (pc += off + 1) from Insn, LdDw (two slots; a MapRef value is a
+    relocation) and ("label", name) items; a jump's ``off`` may name a label."""
     at, k = {}, 0
     for it in items:
         if isinstance(it, tuple):
             at[it[1]] = k
         else:
-            k += 1
-    code, k = [], 0
+            k += 2 if isinstance(it, LdDw) else 1
+    code, relocs, k = [], [], 0
     for it in items:
         if isinstance(it, tuple):
+            continue
+        if isinstance(it, LdDw):
+            v = 0 if isinstance(it.value, MapRef) else it.value & 0xffffffffffffffff
+            if isinstance(it.value, MapRef):
+                relocs.append((k, it.value.index))
+            code += [isa.encode(0x18, it.dst, 0, 0, isa.s32(v)), isa.encode(0, 0, 0, 0, isa.s32(v >> 32))]
+            k += 2
             continue
         off = at[it.off] - (k + 1) if isinstance(it.off, str) else it.off
         code.append(isa.encode(it.op, it.dst, it.src, off, it.imm))
         k += 1
     from .layout import Layout
-    return Layout(b"".join(code), [], None, len(code))
+    return Layout(b"".join(code), relocs, None, len(code))
 
 
 def packets_ipv4opt(n, seed=6):
@@ -482,6 +568,10 @@ CONFIGS = {
                  pkt="imix"),
     "c5d1": dict(desc="probe: C5 with depth-1 trees (6 leaves)", prog=lambda: prog_c5(depth=1),
                  pkt="imix"),
+    "c5ms": dict(desc="probe: C5's shape melded by hand (per-lane operands from an LDS table)",
+                 prog=prog_c5meldsim, pkt="imix", semantics=1),
+    "c5b2": dict(desc="probe: C5, body 96, depth 2", prog=lambda: prog_c5d(2), pkt="imix"),
+    "c5b0": dict(desc="probe: C5, body 96, depth 0", prog=lambda: prog_c5d(0), pkt="imix"),
     "c4c": dict(desc="64-insn classify + array-map lookup + per-key packet counter "
                      "(counters[key] += 1 through a lookup result), 64 B packets", prog=prog_c4c,
                 pkt="l2l3"),
