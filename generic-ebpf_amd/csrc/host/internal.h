@@ -126,9 +126,9 @@ constexpr uint32_t kPathMaxCuts = 15;
 // the group's packets in the LDS buffer until the program is done (LDXPKTV reads them there)
 constexpr uint32_t JIT_HDR_KEEP_PKT = 1;
 constexpr int kInterpStagedImage = 3;
-extern const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
+extern __attribute__((visibility("hidden"))) const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
     ebpf_asm_hsaco_m3[];
-extern const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len,
+extern __attribute__((visibility("hidden"))) const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len,
     ebpf_asm_hsaco_m3_len;
 inline const unsigned char *asm_image(int mode)
 {

@@ -311,7 +311,7 @@ def _c5_nodes(seed, body, depth=2):
                    Branch(I("jgt_imm", R7, imm=100), tree(576, depth))] + tree(64, depth)
 
 
-def _meldsim_nodes(seed, body):
+def _meldsim_nodes(seed, body, exits=True, table_alu=True, ops=("mul64_reg", "add64_reg", "xor64_reg"), classes=3):
     """Probe (round 5): what melding C5's isomorphic leaves could gain, as an optimistic bound.
     C5's shape — the 3-way size split, then per class two data-dependent bit tests — but the
     tests do not branch: they pick a per-lane row of an LDS-resident operand table (array map 0,
@@ -334,12 +334,11 @@ def _meldsim_nodes(seed, body):
             offs = [int(g.integers(18, limits[c] - 8)) for c in range(3)]
             op = ("ldxb", "ldxh", "ldxw", "ldxdw")[int(g.integers(0, 4))]
             plan.append(("ld", op, offs))
-        elif k % 24 == 23:
+        elif k % 24 == 23 and exits:
             offs = [int(g.integers(18, limits[c] - 1)) for c in range(3)]
             plan.append(("exit", offs, col(lambda c: int(g.integers(0, 16)))))
         else:
-            plan.append(("alu", ("mul64_reg", "add64_reg", "xor64_reg")[k % 3],
-                         col(lambda c: int(g.integers(1, 1 << 30)))))
+            plan.append(("alu", ops[k % len(ops)], col(lambda c: int(g.integers(1, 1 << 30)))))
 
     def leaf(cls):
         n, acc = [], R8
@@ -349,8 +348,10 @@ def _meldsim_nodes(seed, body):
             elif x[0] == "exit":
                 n += [I("ldxb", R6, R7, x[1][cls]), I("jne_imm", R6, imm=0x5a, off="c%dk%d" % (cls, k)),
                       I("ldxw", R0, R0, x[2]), I("exit"), ("label", "c%dk%d" % (cls, k))]
-            else:
+            elif table_alu:
                 n += [I("ldxw", R4, R0, x[2]), I(x[1], acc, R4)]
+            else:
+                n += [I(x[1].replace("_reg", "_imm"), acc, imm=cols[x[2] // 4][cls][0])]
         n += [I("mov_reg", R0, acc), I("rsh_imm", R0, imm=7), I("and_imm", R0, imm=15), I("exit")]
         return n
 

@@ -24,6 +24,20 @@ def test_exports_every_declared_symbol(native):
     assert declared <= set(native.FUNCS), declared - set(native.FUNCS)
 
 
+def test_exports_nothing_else(native):
+    """The dynamic symbol table holds exactly the headers' functions and data symbols
+    (generic-ebpf_amd/libebpf.map): no embedded code objects, no C++ runtime instantiations."""
+    import subprocess
+    path = os.path.join(native.HERE, "lib", "libebpf.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    # (+ ebpf_prog_attach_map: not in the public header, but the reference's libebpf.so exports
+    # it, sys/dev/ebpf/ebpf_prog.c:84-109)
+    want = set(native.FUNCS) | set(native.DATA_SYMBOLS) | {"ebpf_prog_attach_map"}
+    assert exported == want, exported ^ want
+
+
 def test_abi_layouts(native):
     assert ctypes.sizeof(native.ProgAttr) == 32
     assert native.ProgAttr.prog_len.offset == 16 and native.ProgAttr.data.offset == 24
