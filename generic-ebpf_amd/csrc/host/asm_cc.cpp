@@ -119,6 +119,17 @@ k32(uint32_t v)
 	return opnd{SRC_LIT, v};
 }
 
+// gfx9 (gfx950 included) VOP3 reads at most one SGPR (or VCC / EXEC / M0) through the constant
+// bus; a second one reads garbage and no assembler stands between this encoder and the hardware.
+// Every VOP3 the compiler emits is checked (cc_bus_violations, asm_jit_emit fails the build).
+thread_local unsigned g_bus_violations = 0;
+
+bool
+is_sgpr_src(uint32_t c)
+{
+	return c <= 127 || (c >= 251 && c <= 253);
+}
+
 struct enc {
 	std::vector<uint8_t> &b;
 	void w(uint32_t x)
@@ -149,6 +160,22 @@ struct enc {
 	// VOP3 (a and b forms); sources are 9-bit codes, never a literal on gfx9
 	void vop3(uint32_t op, int vdst, uint32_t s0, uint32_t s1, uint32_t s2, int sdst = 0)
 	{
+		const uint32_t src[3] = {s0, s1, s2};
+		// (two-source encodings: the compares, v_mul_lo_u32, the 64-bit shifts ignore src2)
+		const int nsrc = (op < 0x100 || op == V3_MUL_LO_U32 || op == V3_LSHLREV_B64 ||
+				  op == V3_LSHRREV_B64) ? 2 : 3;
+		uint32_t bus = UINT32_MAX;
+		for (int i = 0; i < nsrc; i++) {
+			const uint32_t x = src[i];
+			if (!is_sgpr_src(x) || x == bus)
+				continue;
+			if (bus != UINT32_MAX) {
+				g_bus_violations++;
+				if (getenv("EBPF_CC_BUS_DEBUG"))
+					fprintf(stderr, "VOP3 op %#x reads SGPRs %u and %u\n", op, bus, x);
+			}
+			bus = x;
+		}
 		w((0x34u << 26) | (op << 16) | ((uint32_t)sdst << 8) | (uint32_t)vdst);
 		w(s0 | (s1 << 9) | (s2 << 18));
 	}
@@ -345,6 +372,17 @@ struct emitter {
 		if (inline_i64((int64_t)(int32_t)v, &c))
 			return c;
 		return sconst(v);
+	}
+	// a 32-bit constant as a VOP3 source that does not use the constant bus: an inline
+	// constant, or the literal moved into VGPR `tmp` first (for an instruction that already reads
+	// an SGPR)
+	uint32_t vconst(uint32_t v, int tmp)
+	{
+		uint32_t c;
+		if (inline_i64((int64_t)(int32_t)v, &c))
+			return c;
+		mov32(tmp, v);
+		return VGPR0 + (uint32_t)tmp;
 	}
 	uint32_t c64(uint64_t v)
 	{
@@ -986,7 +1024,8 @@ struct emitter {
 		if (kmax >= m.max_entries || m.max_entries > (1u << 24))
 			return false;
 		use(R);
-		E.vop3(V3_MAD_U64_U32, L(0), VGPR0 + L(R), c3(m.value_size), spair(m.dev_base), S_JUNK);
+		// (the map base is an SGPR pair: the value size must not be a second SGPR)
+		E.vop3(V3_MAD_U64_U32, L(0), VGPR0 + L(R), vconst(m.value_size, T0), spair(m.dev_base), S_JUNK);
 		rf v;
 		v.nz = true;
 		v.mp = (int8_t)mi;
@@ -1109,7 +1148,10 @@ struct emitter {
 		E.vop1(V1_MOV_B64, 0, opnd{128});                                     // r0 = NULL
 		E.sop1(0x01, S_SAVE, opnd{SRC_EXEC});                                 // s_mov_b64 s[12:13], exec
 		E.sop1(0x01, S_PEND, opnd{SRC_EXEC});                                 // pending lanes
-		const uint32_t stride_src = c3(1u << lg), base_src = spair(m.dev_base);
+		uint32_t stride_src;
+		if (!inline_i64((int64_t)(1u << lg), &stride_src))
+			return false; // (one SGPR per VOP3: the base pair takes it)
+		const uint32_t base_src = spair(m.dev_base);
 		const size_t loop_at = blk.body.size();
 		E.vop3(V3_MAD_U64_U32, A, VGPR0 + ti, stride_src, base_src, S_JUNK);
 		E.w(0xdc5c8000u);                                                     // global_load_dwordx4
@@ -1184,7 +1226,9 @@ struct emitter {
 		const int R = xs.mreg;
 		use(R);
 		const uint32_t base = m.lds_off + (uint32_t)c;
-		E.vop3(V3_MAD_U32_U24, T0, VGPR0 + L(R), c3(m.value_size), c3(base));
+		// (base >= the map area's LDS offset is never an inline constant: an SGPR, so a value
+		// size that is none either goes through a VGPR)
+		E.vop3(V3_MAD_U32_U24, T0, VGPR0 + L(R), vconst(m.value_size, T1), c3(base));
 		if (z == 8) {
 			E.ds(DS_READ2_B32, T0, 0, 0, L(d), 0, 1);
 			E.wait_lgkm();
@@ -1782,6 +1826,13 @@ cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out)
 	E.w(0xbf840000u | 5u);                                        // s_cbranch_scc0 +5 (past the jump)
 	E.sop1(S1_MOV_B32, 52, opnd{128 + cls});                      // s_mov_b32 S_CODE, class
 	jump_cb(E, cut_off, false);                                   // (4 dwords) -> .Lr_cut
+}
+
+// VOP3 instructions this thread's compiler has emitted with two SGPR sources (a bug: see enc)
+unsigned
+cc_bus_violations()
+{
+	return g_bus_violations;
 }
 
 void

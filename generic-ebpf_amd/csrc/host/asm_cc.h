@@ -36,6 +36,8 @@ struct cc_routines {
 // mode 1 = staged 64-B packets (packet loads read v22..v37).  structured: the program runs with
 // structured control flow (asm_jit.cpp): exits and faults are calls that return, compares
 // always leave VCC.  table: the program's maps.
+// VOP3 instructions emitted with two SGPR sources so far on this thread (must stay 0)
+unsigned cc_bus_violations();
 void cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
 		const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 		const std::vector<dp_map> &table, std::vector<cc_block> &out);

@@ -329,12 +329,17 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	}
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
-	if (getenv("EBPF_JIT_NOCC") == nullptr)
+	const unsigned bus0 = cc_bus_violations();
+	if (getenv("EBPF_JIT_NOCC") == nullptr) {
 		cc_compile(xl, low, order, entry_point, mode, structured,
 			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, cb);
-	else {
+	} else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
 		cc_prologue(gm, 0x7ff, true, false, cb[xl.start].prologue);
+	}
+	if (cc_bus_violations() != bus0) {
+		*err = "internal error: the compiler emitted a VOP3 instruction reading two SGPRs";
+		return EINVAL;
 	}
 	auto reads_of = [&](uint32_t e) -> uint8_t {
 		return cb[e].fast ? cb[e].reads : ah_reads[(uint32_t)low[e].handler];

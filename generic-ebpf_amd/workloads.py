@@ -311,7 +311,8 @@ def _c5_nodes(seed, body, depth=2):
                    Branch(I("jgt_imm", R7, imm=100), tree(576, depth))] + tree(64, depth)
 
 
-def _meldsim_nodes(seed, body, exits=True, table_alu=True, ops=("mul64_reg", "add64_reg", "xor64_reg"), classes=3):
+def _meldsim_nodes(seed, body, exits=True, table_alu=True, ops=("mul64_reg", "add64_reg", "xor64_reg"),
+                   tests=2, split=True):
     """Probe (round 5): what melding C5's isomorphic leaves could gain, as an optimistic bound.
     C5's shape — the 3-way size split, then per class two data-dependent bit tests — but the
     tests do not branch: they pick a per-lane row of an LDS-resident operand table (array map 0,
@@ -357,7 +358,7 @@ def _meldsim_nodes(seed, body, exits=True, table_alu=True, ops=("mul64_reg", "ad
 
     def cls_tree(cls):
         t = [I("mov64_reg", R7, R1), I("mov64_imm", R5, imm=4 * cls)]
-        for j in range(2):   # two tests: bit j of the row
+        for j in range(tests):   # two tests: bit j of the row
             t += [I("ldxb", R6, R7, int(g.integers(18, limits[cls] - 1))),
                   I("rsh_imm", R6, imm=int(g.integers(0, 8))), I("and_imm", R6, imm=1),
                   I("xor64_reg", R8, R6), I("lsh64_imm", R6, imm=j), I("or64_reg", R5, R6)]
@@ -366,6 +367,8 @@ def _meldsim_nodes(seed, body, exits=True, table_alu=True, ops=("mul64_reg", "ad
         return t + leaf(cls)
 
     head = [I("ldxh", R7, R1, 16), I("be", R7, imm=16), I("mov64_imm", R8, imm=0x1234)]
+    if not split:
+        return head + cls_tree(0), cols
     out = head + [I("jgt_imm", R7, imm=1000, off="C2"), I("jgt_imm", R7, imm=100, off="C1")] + \
         cls_tree(0) + [("label", "C1")] + cls_tree(1) + [("label", "C2")] + cls_tree(2)
     return out, cols

@@ -295,3 +295,30 @@ def test_window_cut_code(native, env):
         assert "s_bitcmp1_b32 s7, 12" not in _decode(p.device_code(2))[0]
     finally:
         p.destroy()
+
+
+def test_no_vop3_reads_two_sgprs(native, env):
+    """gfx950's VOP3 reads at most one SGPR; the encoder counts violations and the build fails
+    on one (asm_cc.cpp enc::vop3).  Array maps whose value size is no inline constant (> 64)
+    were the round-5 case: the compiled lookup (map base pair + value size) and LDS loads (LDS
+    base + value size).  Both layouts compile, and the value size goes through a VGPR."""
+    import stdprogs
+    I = stdprogs.I
+    code, rel = stdprogs.asm([
+        I("ldxb", 5, 1, 3), I("and64_imm", 5, imm=15), I("stxw", 10, 5, -4),
+        ("lddw_map", 1, 0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4), I("call", imm=0),
+        I("ldxw", 4, 0, 100), I("mov64_reg", 3, 0), I("add64_reg", 3, 4), I("mov64_reg", 0, 3),
+        I("exit")])
+    for vs in (8, 200, 288):
+        m = native.Map(env, 16, vs)
+        p = native.Prog(env, native.patch_relocs(code, rel, [m.handle]))
+        try:
+            p.set_semantics(native.SEM_STANDARD)
+            for layout in (0, 1):
+                text, _ = _decode(p.device_code(layout))
+                if vs > 64 and os.path.exists(LLVM_MC):
+                    assert "v_mov_b32_e32 v46, 0x%x" % vs in text or \
+                        "v_mov_b32_e32 v47, 0x%x" % vs in text, text
+        finally:
+            p.destroy()
+            m.destroy()

@@ -7,13 +7,16 @@ from generic_ebpf_amd import native, workloads as w
 n = 1 << 14
 data, offs, sizes = w.packets_imix(n)
 env = native.Env()
+base = dict(ops=("add64_reg",), exits=False)
 cases = {
-    "full": {}, "noexit": dict(exits=False), "immalu": dict(table_alu=False),
-    "add": dict(ops=("add64_reg",)), "xor": dict(ops=("xor64_reg",)), "mul": dict(ops=("mul64_reg",)),
-    "add_noexit": dict(ops=("add64_reg",), exits=False), "imm_noexit": dict(table_alu=False, exits=False),
+    "add_noexit": dict(base), "nosplit": dict(base, split=False), "notests": dict(base, tests=0),
+    "onetest": dict(base, tests=1), "nosplit_notests": dict(base, split=False, tests=0),
+    "body8": dict(base, body=8), "body8_nosplit": dict(base, body=8, split=False),
 }
 for name, kw in cases.items():
-    nodes, cols = w._meldsim_nodes(7, 96, **kw)
+    kw = dict(kw)
+    body = kw.pop("body", 96)
+    nodes, cols = w._meldsim_nodes(7, body, **kw)
     lay = w._asm_std(nodes)
     t = np.zeros((16, max(1, len(cols))), dtype=np.uint32)
     for ci, vals in enumerate(cols):
@@ -32,6 +35,9 @@ for name, kw in cases.items():
         native.set_variant(variant)
         r, f, _ = p.run_batch(np.ascontiguousarray(data.copy()), n, 0, offs)
         out.append("v%d %s mism %d" % (variant, p.exec_info(0)[0], int((r != want).sum())))
+        if variant == 0 and (r != want).any():
+            i = np.flatnonzero(r != want)[:3]
+            out.append("e.g. %s got %s want %s sizes %s" % (i.tolist(), r[i].tolist(), want[i].tolist(), sizes[i].tolist()))
         native.set_variant(0)
         p.destroy()
         m.destroy()
