@@ -52,7 +52,7 @@ def hash_spec(g, vs):
 
 def case(k, seed, layout, hashed=False, writes=None):
     g = np.random.default_rng(seed * 7919 + k)
-    vs = int(g.choice([8, 16]))
+    vs = int(g.choice([8, 16, 72, 200]))   # (> 64: no inline constant, round 5)
     me = int(g.choice([16, 256]))
     lay = randprog.random_program(seed * 100000 + k, length=int(g.integers(10, 120)), nmaps=2,
                                   map_value_size=vs,
