@@ -118,7 +118,7 @@ NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
 # general image with the join SGPRs too (structured compiled programs in the general kernels;
 # 98 SGPRs allow 7 instead of 8 waves per SIMD there)
 GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
-# (the join SGPRs s74..s97 would overlap the run mask and the slot SGPRs, and structured exits
+# (the join SGPRs s74..s97 would overlap the run mask and the short-lane mask, and structured exits
 # address the LDS histogram through lane 0 of v43, which the general image uses for V_IDX)
 assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with the run mask and V_IDX"
 # general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
@@ -126,43 +126,6 @@ assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with the run mask and V_IDX"
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
 # A/B: XCD-major logical workgroup order (common_group_code)
 XCD_MAJOR = os.environ.get("EBPF_ASM_XCD") == "1"
-# Slot mode (general image; dp_launch.perm, s7 bit 9: a window launch's overflow list).  The
-# launch's slots are perm[start .. start + n) (packet indices on the device), G per group.
-S_PERM = 78          # s[78:79] this launch's slots (perm + start); 0 = slot i is packet i
-S_G = 81             # packets per group (64)
-S_NSLOT = 82         # slots in this launch
-# Span image (the third code object, interp_m2; window launches): packets sit in LDS (s7 bit
-# 10), so the packet pointer is an LDS-aperture address and constant-offset packet loads are LDS
-# reads (the compiler's b128 hoisted loads, asm_cc.cpp mode 2).  Bigger hoist ring: the launch
-# is LDS-bound to a few workgroups per CU.
-SPAN_IMAGE = False
-SPAN_HOIST_REGS = int(os.environ.get("EBPF_ASM_SPANHOIST", "48"))
-# Window mode (span image, dp_launch.win_bytes != 0; gpu_runtime.cpp launch_windowed).  A
-# workgroup walks its share of an offsets batch [S_WP, S_WHI) in windows: the longest run of at
-# most 256 packets, 16-B aligned, lying in [a0, a0 + win_bytes) from the first one's start a0, is
-# DMA'd into LDS as one contiguous span (coalesced, each byte once), then
-#   phase A  every packet of the window runs (lane t = packet S_WP + t) until it exits, faults or
-#            reaches a cut point q (the head of a heavy subtree, asm_jit.cpp): there it records
-#            class q + 1 and leaves (.Lr_cut; compiled cut code, s7 bit 12);
-#   phase B  a counting sort of the cut packets by class (LDS atomics) into perm;
-#   phase C  the cut packets run again from the start, 64 consecutive entries of perm per group,
-#            so a group's lanes take one heavy subtree instead of the ~12 an IMIX group takes.
-# Packets are LDS-aperture pointers throughout (their loads LDS reads).  A packet that cannot
-# open a window (unaligned, or longer than win_bytes) goes to dp_launch.win_ovf (a slot list the
-# general kernels run next).  No map writes (the host only windows programs without them).
-# (s[74:77] are the compiled program's short-lane and run masks: window state lives above them,
-# and the span image declares s0..s95)
-S_WC = 78            # phase C: the window's cut packets
-S_WP, S_WHI = 88, 89 # the window's first packet; the workgroup's end
-NSGPR_SPAN = 96
-S_WB, S_WG, S_WARR, S_WN = 80, 81, 82, 83   # window bytes; phase C group; LDS arrays; window count
-S_WDEF = 84          # s[84:85] lanes of the running group that reached a cut point
-S_GINIT = 86         # s[86:87] lanes the running group started with
-V_WSLOT = 22         # the lane's packet slot t in the window
-W_POFS, W_PLEN, W_CLS, W_PERM, W_CNT, W_SPAN, W_FF = 0, 1024, 2048, 3072, 4096, 4160, 4176
-W_ARR_BYTES = 4352   # LDS per-window arrays (u32 x 256 each, class counts, span, first fails)
-W_MAX = 256
-
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
 ALU64I = ["ADD", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD", "MOV"]   # MOV = LDDW
@@ -674,25 +637,12 @@ def h_ldx_pkt_general(z, d):
            "s_and_b64 %s, %s, exec" % (sp(S_MASK), sp(S_MASK)),
            "s_cmp_eq_u64 %s, 0" % sp(S_MASK),
            "s_cbranch_scc1 .Lok_{uid}"] + fault_mask(S_MASK, 3) + [".Lok_{uid}:"]
-    if SPAN_IMAGE:
-        # (the packet's slot in LDS when span-staged; else its global address: s7 bit 10)
-        out += ["s_bitcmp1_b32 s7, 10",
-                "s_cbranch_scc0 .Lpg_{uid}",
-                "v_add_u32 %s, s10, v%d" % (v(t[0]), V_PKT),
-                "%s %s, %s" % ({1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[z],
-                               pair(d) if z == 8 else lo(d), v(t[0])),
-                "s_waitcnt lgkmcnt(0)"]
-        if z < 8:
-            out.append("v_mov_b32 %s, 0" % hi(d))
-        out += ["s_branch .Lpd_{uid}", ".Lpg_{uid}:"]
     out.append("v_lshl_add_u64 %s, s[10:11], 0, %s" % (vp(t[0]), vp(V_PKT)))
     if z == 8:
         out.append("%s %s, %s, off" % (LOADS[8], pair(d), vp(t[0])))
     else:
         out += ["%s %s, %s, off" % (LOADS[z], lo(d), vp(t[0])), "v_mov_b32 %s, 0" % hi(d)]
     out.append("s_waitcnt vmcnt(0)")
-    if SPAN_IMAGE:
-        out.append(".Lpd_{uid}:")
     return out
 
 
@@ -852,7 +802,7 @@ def h_ldx_pktv(z, d, sr):
                     out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
                 out.append("v_mov_b32 %s, 0" % hi(d))
         out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
-    elif not SPAN_IMAGE:
+    else:
         # general kernels with the headers kept in LDS (s7 bit 14, every lane's first 64 bytes
         # at S_PKTLDS + 64 lane when its packet is at least that long): when every running lane's
         # bytes lie in its first 64 and its packet has them staged, read them there
@@ -2257,16 +2207,6 @@ def routines():
     # OVLFIX (called by generic loads when dp_launch.vflags bit 0): the packet's own stores over
     # the S_T0 bytes at H[0:1] just read into H[2:3]
     L += [".Lr_ovlfix:"] + ovl_fix("L", (H[2], H[3])) + ["s_setpc_b64 %s" % sp(S_LINK)]
-    if not STAGED_IMAGE:
-        # CUT (window launches, phase A; entered by a cut point's code with S_CODE = its class):
-        # the running lanes record the class of their window slot and leave the group
-        L += [".Lr_cut:",
-              "v_mov_b32 %s, %s" % (v(R[0]), s(S_CODE)),
-              "v_lshlrev_b32 %s, 2, v%d" % (v(R[1]), V_WSLOT),
-              "v_add_u32 %s, %s, %s" % (v(R[1]), s(S_WARR), v(R[1])),
-              "ds_write_b32 %s, %s offset:%d" % (v(R[1]), v(R[0]), W_CLS),
-              "s_or_b64 %s, %s, exec" % (sp(S_WDEF), sp(S_WDEF)),
-              "s_andn2_b64 %s, %s, exec" % (sp(S_ALIVE), sp(S_ALIVE))] + goto(".Lr_schedule")
     # DMA_NEXT (staged kernel, deferred mode s7 bit 4): issue the LDS DMA of this wave's next
     # group now, once per group (sets bit 5).  The group set-up defers only a full next group,
     # so this is always the 4-instruction full-group DMA.  Preserves exec, S_T*, s[66:71];
@@ -2371,36 +2311,6 @@ def kernel(name, staged, jit=False):
               "s_or_b32 s7, s7, 0x4000",
               ".L%s_nohl:" % k,
               "s_and_b32 %s, %s, 0x3fffffff" % (s(S_PKTLDS), s(S_PKTLDS))]
-    if not staged and not STAGED_IMAGE:
-        # slot launch (dp_launch.perm != 0): s7 bit 9 = slot mode (this launch's slots are
-        # perm[start .. start + n), G per group)
-        L += ["s_load_dwordx2 %s, s[0:1], 0xb0" % sp(S_PERM),
-              "s_load_dwordx2 s[54:55], s[0:1], 0xb8",
-              "s_load_dwordx4 s[80:83], s[0:1], 0xc0",   # reserved, G, magic(G), pad
-              "s_waitcnt lgkmcnt(0)",
-              "s_cmp_eq_u64 %s, 0" % sp(S_PERM),
-              "s_cbranch_scc1 .L%s_noperm" % k,
-              "s_load_dwordx2 s[54:55], s[54:55], 0x0",  # {start, n} of the class
-              "s_waitcnt lgkmcnt(0)",
-              "s_lshl_b32 s54, s54, 2",
-              "s_add_u32 %s, %s, s54" % (s(S_PERM), s(S_PERM)),
-              "s_addc_u32 %s, %s, 0" % (s(S_PERM + 1), s(S_PERM + 1)),
-              # groups = ceil(n / G) = mul_hi(n + G - 1, ceil(2^32 / G)), into s83 until
-              # common_group_code takes it
-              "s_add_u32 s83, s55, %s" % s(S_G),
-              "s_sub_u32 s83, s83, 1",
-              "s_mul_hi_u32 s83, s83, s82",
-              "s_mov_b32 %s, s55" % s(S_NSLOT),
-              "s_or_b32 s7, s7, 512",
-              ".L%s_noperm:" % k]
-    if SPAN_IMAGE and jit:
-        # window mode (dp_launch.win_bytes, win_chunk, win_arr at 0xd0): s7 bit 11
-        L += ["s_load_dwordx4 s[80:83], s[0:1], 0xd0",
-              "s_waitcnt lgkmcnt(0)",
-              "s_cmp_eq_u32 s80, 0",
-              "s_cbranch_scc1 .L%s_nowin" % k,
-              "s_or_b32 s7, s7, 0xc00",     # (bit 10 too: the packets are in LDS)
-              ".L%s_nowin:" % k]
     L += ["s_branch .Lprologue"]
     return L
 
@@ -2478,333 +2388,6 @@ def pkt_setup(idx, tag):
             for q in range(4)] + [
             ".Lps_done_%s:" % tag,
             "s_mov_b64 exec, %s" % sp(S_MASK)]
-
-
-def window_debug():
-    """(diagnostics, dp_launch.win_pad bit 0; wave 0 after B5 of the workgroup's first window)
-    the window's classes, W, the cut count, s7 and the class counts (v0..v15) into the words
-    after the overflow list (win_ovf + 8 + 4 * count): cls[0..63], W, WC, s7, cnt[0..15]."""
-    return ["s_load_dword s64, s[0:1], 0xdc",
-            "s_waitcnt lgkmcnt(0)",
-            "s_bitcmp1_b32 s64, 0",
-            "s_cbranch_scc0 .Lwin_dbg_end",
-            "s_cmp_eq_u32 s2, 0",
-            "s_cbranch_scc0 .Lwin_dbg_end",
-            "s_load_dwordx2 s[64:65], s[0:1], 0xe0",
-            "s_waitcnt lgkmcnt(0)",
-            "s_lshl_b32 s66, %s, 2" % s(S_COUNT),
-            "s_add_u32 s66, s66, 8",
-            "s_add_u32 s64, s64, s66",
-            "s_addc_u32 s65, s65, 0",
-            "s_mov_b64 exec, -1"] + lane_index(H[0]) + [
-            "v_lshlrev_b32 %s, 2, %s" % (v(H[2]), v(H[0])),
-            "v_add_u32 %s, %s, %s" % (v(H[3]), s(S_WARR), v(H[2])),
-            "ds_read_b32 %s, %s offset:%d" % (v(R[0]), v(H[3]), W_CLS),
-            "s_waitcnt lgkmcnt(0)",
-            "global_store_dword %s, %s, s[64:65]" % (v(H[2]), v(R[0])),
-            "s_mov_b64 exec, 1",
-            "v_mov_b32 %s, 0" % v(H[2]),
-            "v_mov_b32 %s, %s" % (v(R[0]), s(S_WN)),
-            "global_store_dword %s, %s, s[64:65] offset:256" % (v(H[2]), v(R[0])),
-            "v_mov_b32 %s, %s" % (v(R[0]), s(S_WC)),
-            "global_store_dword %s, %s, s[64:65] offset:260" % (v(H[2]), v(R[0])),
-            "v_mov_b32 %s, s7" % v(R[0]),
-            "global_store_dword %s, %s, s[64:65] offset:264" % (v(H[2]), v(R[0]))] + [
-            "global_store_dword %s, v%d, s[64:65] offset:%d" % (v(H[2]), k, 268 + 4 * k)
-            for k in range(16)] + [
-            "s_waitcnt vmcnt(0)",
-            ".Lwin_dbg_end:"]
-
-
-def window_code():
-    """Window mode (span image, s7 bit 11; see "Window mode" at the top).  Entered by every wave
-    of the workgroup after the prologue; ends at .Lfinish.  Six workgroup barriers per window:
-    B1 window formed (offsets, first fails, span), B2 its bytes in LDS, B3 phase A done (classes),
-    B4 class counts, B5 perm, B6 phase C done.  Between program runs v0..v21 (the eBPF registers),
-    H[], R[] are free."""
-    tid = H[1]
-
-    def tid_code():
-        return lane_index(H[0]) + [
-            "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WAVE)),
-            "v_add_u32 %s, %s, %s" % (v(tid), s(S_T0), v(H[0]))]
-
-    def arr_addr(dst, idx):   # dst = S_WARR + 4 * idx
-        return ["v_lshlrev_b32 %s, 2, %s" % (v(dst), v(idx)),
-                "v_add_u32 %s, %s, %s" % (v(dst), s(S_WARR), v(dst))]
-
-    L = [".Lwin_start:",
-         # the workgroup's packets: [wg * chunk, min((wg + 1) * chunk, count))
-         "s_mul_i32 %s, s2, s81" % s(S_WP),
-         "s_add_u32 %s, %s, s81" % (s(S_WHI), s(S_WP)),
-         "s_min_u32 %s, %s, %s" % (s(S_WHI), s(S_WHI), s(S_COUNT)),
-         "s_min_u32 %s, %s, %s" % (s(S_WP), s(S_WP), s(S_WHI)),
-         "s_mov_b64 exec, -1"] + tid_code() + [
-         # class counts and the span word start at zero
-         "v_cmp_gt_u32_e64 vcc, 17, %s" % v(tid),
-         "s_and_saveexec_b64 %s, vcc" % sp(S_SAVE)] + arr_addr(H[2], tid) + [
-         "v_mov_b32 %s, 0" % v(H[3]),
-         "ds_write_b32 %s, %s offset:%d" % (v(H[2]), v(H[3]), W_CNT),
-         "s_mov_b64 exec, -1",
-         "s_waitcnt lgkmcnt(0)",
-         "s_barrier",
-         ".Lwin_loop:",
-         "s_mov_b64 exec, -1",
-         "s_cmp_ge_u32 %s, %s" % (s(S_WP), s(S_WHI)),
-         "s_cbranch_scc1 .Lfinish",
-         # s[68:69] = offsets[S_WP]
-         "s_lshl_b32 s66, %s, 3" % s(S_WP),
-         "s_add_u32 s66, s66, %s" % s(S_OFFS),
-         "s_addc_u32 s67, %s, 0" % s(S_OFFS + 1),
-         "s_load_dwordx2 s[68:69], s[66:67], 0x0"] + tid_code() + [
-         # thread t: packet S_WP + t; R[0:1] = its offset, R[2:3] = the next one
-         "v_add_u32 %s, %s, %s" % (v(H[2]), s(S_WP), v(tid)),
-         "v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_MASK), s(S_WHI), v(H[2])),
-         "v_mov_b32 %s, 8" % v(H[3]),
-         "v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(H[4]), sp(S_JUNK), v(H[2]), v(H[3]), sp(S_OFFS)),
-         "s_mov_b64 exec, %s" % sp(S_MASK),
-         "global_load_dwordx2 %s, %s, off" % (vp(R[0]), vp(H[4])),
-         "global_load_dwordx2 %s, %s, off offset:8" % (vp(R[2]), vp(H[4])),
-         "s_mov_b64 exec, -1",
-         "s_waitcnt vmcnt(0) lgkmcnt(0)",
-         # relative to the window start: ra = R[0:1], re = R[2:3]
-         "v_mov_b32 %s, s69" % v(R[5]),
-         "v_subrev_co_u32 %s, vcc, s68, %s" % (v(R[0]), v(R[0])),
-         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[1]), v(R[1]), v(R[5])),
-         "v_subrev_co_u32 %s, vcc, s68, %s" % (v(R[2]), v(R[2])),
-         "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[3]), v(R[3]), v(R[5])),
-         # s[64:65] = the window start in memory (data + offsets[S_WP] - off_base)
-         "s_sub_u32 s64, s68, %s" % s(S_OFFBASE),
-         "s_subb_u32 s65, s69, %s" % s(S_OFFBASE + 1),
-         "s_add_u32 s64, s64, %s" % s(S_DATA),
-         "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
-         # in the window: ra, re < 2^32, ra <= re <= win_bytes, the packet 16-B aligned
-         "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[1])),
-         "s_and_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
-         "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[3])),
-         "s_and_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
-         "v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_JUNK), v(R[0]), v(R[2])),
-         "s_and_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
-         "v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_JUNK), s(S_WB), v(R[2])),
-         "s_and_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
-         "v_add_u32 %s, s64, %s" % (v(R[4]), v(R[0])),
-         "v_and_b32 %s, 15, %s" % (v(R[4]), v(R[4])),
-         "v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[4])),
-         "s_and_b64 %s, %s, %s" % (sp(S_MASK), sp(S_MASK), sp(S_JUNK)),
-         # this wave's first lane out of the window (64: none); its lanes before that record
-         # their packet's place and length, and the span they need
-         "s_not_b64 %s, %s" % (sp(S_JUNK), sp(S_MASK)),
-         "s_ff1_i32_b64 %s, %s" % (s(S_T0), sp(S_JUNK)),
-         "s_cmp_eq_u32 %s, -1" % s(S_T0),
-         "s_cselect_b32 %s, 64, %s" % (s(S_T0), s(S_T0)),
-         "s_bfm_b64 %s, %s, 0" % (sp(S_SAVE), s(S_T0)),
-         "s_cmp_eq_u32 %s, 64" % s(S_T0),
-         "s_cselect_b64 %s, -1, %s" % (sp(S_SAVE), sp(S_SAVE)),
-         "s_mov_b64 exec, %s" % sp(S_SAVE),
-         "s_cbranch_execz .Lwin_noprefix"] + arr_addr(H[2], tid) + [
-         "ds_write_b32 %s, %s offset:%d" % (v(H[2]), v(R[0]), W_POFS),
-         "v_sub_u32 %s, %s, %s" % (v(R[4]), v(R[2]), v(R[0])),
-         "ds_write_b32 %s, %s offset:%d" % (v(H[2]), v(R[4]), W_PLEN),
-         "v_mov_b32 %s, %s" % (v(R[5]), s(S_WARR)),
-         "ds_max_u32 %s, %s offset:%d" % (v(R[5]), v(R[2]), W_SPAN),
-         ".Lwin_noprefix:",
-         "s_mov_b64 exec, 1",
-         "s_lshl_b32 %s, %s, 2" % (s(S_T1), s(S_WAVE)),
-         "s_add_u32 %s, %s, %s" % (s(S_T1), s(S_T1), s(S_WARR)),
-         "v_mov_b32 %s, %s" % (v(R[5]), s(S_T1)),
-         "v_mov_b32 %s, %s" % (v(R[6]), s(S_T0)),
-         "ds_write_b32 %s, %s offset:%d" % (v(R[5]), v(R[6]), W_FF),
-         "s_mov_b64 exec, -1",
-         "s_waitcnt lgkmcnt(0)",
-         "s_barrier",                                                     # B1
-         "v_mov_b32 %s, %s" % (v(R[5]), s(S_WARR)),
-         "ds_read_b128 v[0:3], %s offset:%d" % (v(R[5]), W_FF),
-         "ds_read_b32 v4, %s offset:%d" % (v(R[5]), W_SPAN),
-         "s_waitcnt lgkmcnt(0)"] + [
-         "v_readfirstlane_b32 %s, v%d" % (s(S_T0 + w), w) for w in range(4)] + [
-         "v_readfirstlane_b32 %s, v4" % s(S_BYTES),
-         # W = the first packet out of the window, over the four waves
-         "s_mov_b32 %s, %d" % (s(S_WN), W_MAX)]
-    for w in (3, 2, 1, 0):
-        L += ["s_add_u32 %s, %s, %d" % (s(S_CODE), s(S_T0 + w), 64 * w),
-              "s_cmp_lt_u32 %s, 64" % s(S_T0 + w),
-              "s_cselect_b32 %s, %s, %s" % (s(S_WN), s(S_CODE), s(S_WN))]
-    L += ["s_cmp_eq_u32 %s, 0" % s(S_WN),
-          "s_cbranch_scc1 .Lwin_ovf",
-          # the window's bytes into LDS at S_PKTLDS: 16-B blocks, wave w the blocks w*64 + lane
-          # + 256k (global and LDS addresses advance together)
-          "s_add_u32 %s, %s, 15" % (s(S_BYTES), s(S_BYTES)),
-          "s_lshr_b32 %s, %s, 4" % (s(S_BYTES), s(S_BYTES)),
-          "s_lshl_b32 %s, %s, 10" % (s(S_T0), s(S_WAVE)),
-          "s_add_u32 s64, s64, %s" % s(S_T0),
-          "s_addc_u32 s65, s65, 0",
-          "s_add_u32 %s, %s, %s" % (s(S_T1), s(S_PKTLDS), s(S_T0))] + tid_code() + [
-          "v_lshlrev_b32 %s, 4, %s" % (v(R[7]), v(H[0])),
-          "v_mov_b32 %s, %s" % (v(R[6]), v(tid)),
-          ".Lwin_dma:",
-          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_BYTES), v(R[6])),
-          "s_mov_b64 exec, vcc",
-          "s_cbranch_execz .Lwin_dma_done",
-          "s_mov_b32 m0, %s" % s(S_T1),
-          "s_nop 0",
-          "global_load_lds_dwordx4 %s, s[64:65]%s" % (v(R[7]), LD_POLICY),
-          "s_add_u32 s64, s64, 0x1000",
-          "s_addc_u32 s65, s65, 0",
-          "s_add_u32 %s, %s, 0x1000" % (s(S_T1), s(S_T1)),
-          "s_mov_b64 exec, -1",
-          "v_add_u32 %s, 0x100, %s" % (v(R[6]), v(R[6])),
-          "s_branch .Lwin_dma",
-          ".Lwin_dma_done:",
-          "s_mov_b64 exec, -1",
-          "s_waitcnt vmcnt(0)",
-          "s_barrier",                                                    # B2
-          # wave 0 re-arms the span word (every wave read it before B2)
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lwin_a",
-          "s_mov_b64 exec, 1",
-          "v_mov_b32 %s, %s" % (v(R[5]), s(S_WARR)),
-          "v_mov_b32 %s, 0" % v(R[6]),
-          "ds_write_b32 %s, %s offset:%d" % (v(R[5]), v(R[6]), W_SPAN),
-          "s_mov_b64 exec, -1",
-          # phase A: lane t runs packet S_WP + t (t < W) with class 0 (exits or faults)
-          ".Lwin_a:"] + tid_code() + [
-          "v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_GINIT), s(S_WN), v(tid)),
-          "s_mov_b64 exec, %s" % sp(S_GINIT),
-          "s_cbranch_execz .Lwin_a_done",
-          "v_mov_b32 v%d, %s" % (V_WSLOT, v(tid))] + arr_addr(H[2], tid) + [
-          "v_mov_b32 %s, 0" % v(H[3]),
-          "ds_write_b32 %s, %s offset:%d" % (v(H[2]), v(H[3]), W_CLS),
-          "s_or_b32 s7, s7, 0x1000",
-          # run the group: exec = S_GINIT, V_WSLOT = each lane's window slot
-          ".Lwin_run:",
-          "v_add_u32 v%d, %s, v%d" % (V_IDX, s(S_WP), V_WSLOT),
-          "v_lshlrev_b32 %s, 2, v%d" % (v(H[2]), V_WSLOT),
-          "v_add_u32 %s, %s, %s" % (v(H[2]), s(S_WARR), v(H[2])),
-          "ds_read_b32 %s, %s offset:%d" % (v(H[3]), v(H[2]), W_POFS),
-          "ds_read_b32 v%d, %s offset:%d" % (V_LEN, v(H[2]), W_PLEN),
-          "s_waitcnt lgkmcnt(0)",
-          "v_add_u32 v%d, %s, %s" % (V_PKT, s(S_PKTLDS), v(H[3])),
-          "v_mov_b32 v%d, %s" % (V_PKT + 1, s(S_SHARED + 1)),
-          "s_mov_b64 %s, exec" % sp(S_ALIVE),
-          "s_mov_b64 %s, 0" % sp(S_WDEF),
-          "s_mov_b32 %s, -1" % s(S_PREVG),
-          "s_cmp_eq_u64 %s, 0" % sp(S_FAULTS),
-          "s_cbranch_scc1 .Lwin_nofz",
-          "v_mov_b32 %s, 0" % v(R[8]),
-          "global_store_byte v%d, %s, %s" % (V_IDX, v(R[8]), sp(S_FAULTS)),
-          ".Lwin_nofz:"] + goto("ebpf_jit_area+16") + [
-          # a group is done (.Lgroup_done): the results of its lanes that did not stop at a cut
-          ".Lwin_gdone:",
-          "s_andn2_b64 exec, %s, %s" % (sp(S_GINIT), sp(S_WDEF)),
-          "s_cbranch_execz .Lwin_gd_none",
-          "v_lshlrev_b32 %s, 3, v%d" % (v(R[0]), V_IDX),
-          "global_store_dwordx2 %s, v[%d:%d], %s%s" % (v(R[0]), V_RES, V_RES + 1, sp(S_RET), ST_POLICY),
-          ".Lwin_gd_none:",
-          "s_mov_b64 exec, -1",
-          "s_bitcmp1_b32 s7, 12",
-          "s_cbranch_scc0 .Lwin_c_more",
-          ".Lwin_a_done:",
-          "s_and_b32 s7, s7, 0xffffefff",
-          "s_mov_b64 exec, -1",
-          "s_waitcnt vmcnt(0) lgkmcnt(0)",
-          "s_barrier",                                                    # B3
-          # phase B: each cut packet's rank in its class
-          ] + tid_code() + [
-          "v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_SAVE), s(S_WN), v(tid)),
-          "s_mov_b64 exec, %s" % sp(S_SAVE)] + arr_addr(H[2], tid) + [
-          "ds_read_b32 %s, %s offset:%d" % (v(R[0]), v(H[2]), W_CLS),
-          "s_waitcnt lgkmcnt(0)",
-          "v_cmp_ne_u32_e64 vcc, 0, %s" % v(R[0]),
-          "s_and_b64 exec, exec, vcc",
-          "s_mov_b64 %s, exec" % sp(S_SAVE),
-          "s_cbranch_execz .Lwin_b_norank",
-          "v_lshlrev_b32 %s, 2, %s" % (v(R[1]), v(R[0])),
-          "v_add_u32 %s, %s, %s" % (v(R[1]), s(S_WARR), v(R[1])),
-          "v_mov_b32 %s, 1" % v(R[2]),
-          "ds_add_rtn_u32 %s, %s, %s offset:%d" % (v(R[3]), v(R[1]), v(R[2]), W_CNT),
-          ".Lwin_b_norank:",
-          "s_mov_b64 exec, -1",
-          "s_waitcnt lgkmcnt(0)",
-          "s_barrier",                                                    # B4
-          "v_mov_b32 %s, %s" % (v(R[4]), s(S_WARR))] + [
-          "ds_read_b128 v[%d:%d], %s offset:%d" % (4 * q, 4 * q + 3, v(R[4]), W_CNT + 16 * q)
-          for q in range(4)] + [
-          "s_waitcnt lgkmcnt(0)",
-          "v_mov_b32 v16, 0",          # the lane's class base
-          "v_mov_b32 v17, 0"]          # every cut packet of the window
-    for k in range(1, 16):
-        L += ["v_cmp_lt_u32_e64 vcc, %d, %s" % (k, v(R[0])),
-              "v_cndmask_b32 v18, 0, v%d, vcc" % k,
-              "v_add_u32 v16, v16, v18",
-              "v_add_u32 v17, v17, v%d" % k]
-    L += ["s_nop 0",                  # (a VALU write, then v_readfirstlane of it: 1 wait state)
-          "v_readfirstlane_b32 %s, v17" % s(S_WC),
-          "s_mov_b64 exec, %s" % sp(S_SAVE),
-          "s_cbranch_execz .Lwin_b_noperm",
-          "v_add_u32 v16, v16, %s" % v(R[3]),
-          "v_lshlrev_b32 v16, 2, v16",
-          "v_add_u32 v16, %s, v16" % s(S_WARR),
-          "ds_write_b32 v16, %s offset:%d" % (v(tid), W_PERM),
-          ".Lwin_b_noperm:",
-          "s_mov_b64 exec, -1",
-          "s_waitcnt lgkmcnt(0)",
-          "s_barrier",                                                    # B5
-          # wave 0 re-arms the class counts (every wave read them before B5)
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lwin_c"] + window_debug() + [
-          "s_mov_b64 exec, -1"] + tid_code() + [
-          "v_cmp_gt_u32_e64 vcc, 16, %s" % v(tid),
-          "s_mov_b64 exec, vcc"] + arr_addr(H[2], tid) + [
-          "v_mov_b32 %s, 0" % v(H[3]),
-          "ds_write_b32 %s, %s offset:%d" % (v(H[2]), v(H[3]), W_CNT),
-          "s_mov_b64 exec, -1",
-          # phase C: wave w runs perm groups w, w + 4, ...
-          ".Lwin_c:",
-          "s_mov_b32 %s, %s" % (s(S_WG), s(S_WAVE)),
-          ".Lwin_c_next:",
-          "s_mov_b64 exec, -1",
-          "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_WG)),
-          "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_WC)),
-          "s_cbranch_scc1 .Lwin_c_done"] + lane_index(H[0]) + [
-          "v_add_u32 %s, %s, %s" % (v(H[0]), s(S_T0), v(H[0])),
-          "v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_GINIT), s(S_WC), v(H[0])),
-          "s_mov_b64 exec, %s" % sp(S_GINIT)] + arr_addr(H[2], H[0]) + [
-          "ds_read_b32 v%d, %s offset:%d" % (V_WSLOT, v(H[2]), W_PERM),
-          "s_waitcnt lgkmcnt(0)",
-          "s_branch .Lwin_run",
-          ".Lwin_c_more:",
-          "s_add_u32 %s, %s, 4" % (s(S_WG), s(S_WG)),
-          "s_branch .Lwin_c_next",
-          ".Lwin_c_done:",
-          "s_mov_b64 exec, -1",
-          "s_waitcnt vmcnt(0) lgkmcnt(0)",
-          "s_barrier",                                                    # B6
-          "s_add_u32 %s, %s, %s" % (s(S_WP), s(S_WP), s(S_WN)),
-          "s_branch .Lwin_loop",
-          # the first packet cannot open a window: to the overflow list (wave 0), one packet on
-          ".Lwin_ovf:",
-          "s_cmp_eq_u32 %s, 0" % s(S_WAVE),
-          "s_cbranch_scc0 .Lwin_ovf_wait",
-          "s_load_dwordx2 s[64:65], s[0:1], 0xe0",
-          "s_mov_b64 exec, 1",
-          "v_mov_b32 %s, %s" % (v(R[5]), s(S_WARR)),
-          "v_mov_b32 %s, 0" % v(R[6]),
-          "ds_write_b32 %s, %s offset:%d" % (v(R[5]), v(R[6]), W_SPAN),
-          "v_mov_b32 %s, 4" % v(R[0]),
-          "v_mov_b32 %s, 1" % v(R[1]),
-          "s_waitcnt lgkmcnt(0)",
-          "global_atomic_add %s, %s, %s, s[64:65] sc0" % (v(R[2]), v(R[0]), v(R[1])),
-          "s_waitcnt vmcnt(0)",
-          "v_lshlrev_b32 %s, 2, %s" % (v(R[2]), v(R[2])),
-          "v_mov_b32 %s, %s" % (v(R[3]), s(S_WP)),
-          "global_store_dword %s, %s, s[64:65] offset:8" % (v(R[2]), v(R[3])),
-          "s_mov_b64 exec, -1",
-          ".Lwin_ovf_wait:",
-          "s_waitcnt vmcnt(0) lgkmcnt(0)",
-          "s_barrier",
-          "s_add_u32 %s, %s, 1" % (s(S_WP), s(S_WP)),
-          "s_branch .Lwin_loop"]
-    return L
 
 
 def ret_slot_write(x0, x1):
@@ -2931,9 +2514,6 @@ def common_group_code():
           ".Lmc_done:",
           "s_waitcnt lgkmcnt(0)",
           "s_barrier"]
-    if SPAN_IMAGE:
-        L += ["s_bitcmp1_b32 s7, 11",
-              "s_cbranch_scc1 .Lwin_start"]
     # groups of 64 packets: group = workgroup*4 + wave, stride = total waves
     L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
           "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
@@ -2962,10 +2542,7 @@ def common_group_code():
           "s_lshl_b32 %s, 1, %s" % (s(S_KMASK), s(S_T1)),
           "s_sub_u32 %s, %s, 1" % (s(S_KMASK), s(S_KMASK)),
           "s_lshl_b32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_T1)),
-          ] + ([] if STAGED_IMAGE else [
-          # slot mode: ceil(n / G) groups (prologue)
-          "s_bitcmp1_b32 s7, 9",
-          "s_cselect_b32 %s, s83, %s" % (s(S_NGROUPS), s(S_NGROUPS))]) + [
+          ] + [
           # superblock jump: (total waves - 1) * K' + 1
           "s_lshl_b32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_T1)),
           "s_sub_u32 %s, %s, %s" % (s(S_GSTRIDE), s(S_GSTRIDE), s(S_KMASK)),
@@ -2977,9 +2554,6 @@ def common_group_code():
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
     L += [".Lgroup_done:"]
-    if SPAN_IMAGE:
-        L += ["s_bitcmp1_b32 s7, 11",
-              "s_cbranch_scc1 .Lwin_gdone"]
     L += ["s_and_b32 %s, s7, 48" % s(S_BYTES),
           "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
           "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
@@ -2998,24 +2572,7 @@ def common_group_code():
           ] + lane_index(H[0]) + [
           "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
-          ] + ([] if STAGED_IMAGE else [
-          # slot mode: slot group * G + lane (lanes < G), its packet perm[slot]; the other lanes
-          # get index ~0 (no result, no fault byte)
-          "s_bitcmp1_b32 s7, 9",
-          "s_cbranch_scc0 .Lgc_slots_done",
-          "s_mul_i32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_G)),
-          "v_add_u32 v%d, %s, %s" % (H[3], s(S_T0), v(H[0])),
-          "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_NSLOT), H[3]),
-          "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_G), v(H[0])),
-          "s_and_b64 %s, %s, vcc" % (sp(S_ALIVE), sp(S_ALIVE)),
-          "v_lshlrev_b32 %s, 2, v%d" % (v(H[4]), H[3]),
-          "s_mov_b64 exec, %s" % sp(S_ALIVE),
-          "global_load_dword v%d, %s, %s" % (H[3], v(H[4]), sp(S_PERM)),
-          "s_waitcnt vmcnt(0)",
-          "s_not_b64 exec, %s" % sp(S_ALIVE),
-          "v_mov_b32 v%d, -1" % H[3],
-          "s_mov_b64 exec, -1",
-          ".Lgc_slots_done:"]) + [
+          ] + [
           "s_bitcmp1_b32 s7, 0",
           "s_cbranch_scc0 .Lgs_general",
           # staged: this group's packets are (or are being) DMA'd into the packet buffer
@@ -3104,8 +2661,6 @@ def common_group_code():
     # histogram (stored, or added), then re-arms the ticket.  One kernel per launch: no
     # second-stage reduce (hand-off form: 8-B agent atomics on both sides, MI355X_MICROARCH.md
     # "Valid forms")
-    if SPAN_IMAGE:
-        L += window_code()
     HR = HIST_REPLICA_BYTES
     L += [".Lfinish:"] + store_prev_results("f", True)
     L += [".Lfinish_body:",
@@ -3437,7 +2992,7 @@ def jit_templates():
         ".Ljt_cl", ".Ljt_cl_lit", ".Ljt_cl_vt", ".Ljt_cl_end",
         ".Ljt_br", ".Ljt_jl", ".Ljt_jl_end", ".Ljt_wait", ".Lr_exit_k", ".Lr_exit", ".Lr_fault",
         ".Lr_hlookup", ".Lgroup_done",
-        ".Lr_schedule", ".Lr_cut" if not STAGED_IMAGE else ".Lgroup_done",
+        ".Lr_schedule",
         "ebpf_jit_area"]
     L += [".p2align 2", "ebpf_jit_tmpl:"] + ["  .long %s-.Lcb" % n for n in names]
     L += ["  .long %d" % JIT_AREA_BYTES]
@@ -3457,19 +3012,17 @@ assert RETK_INTERP in (1, 2, 4, 8)
 
 
 def main():
-    """gen_interp.py <staged.s> <general.s> <span.s> <staged-interpreter.s> <handlers.h>"""
-    out_s1, out_s0, out_s2, out_s3, out_h = sys.argv[1:6]
+    """gen_interp.py <staged.s> <general.s> <staged-interpreter.s> <handlers.h>"""
+    out_s1, out_s0, out_s3, out_h = sys.argv[1:5]
     header = None
-    global SPAN_IMAGE, NVGPR, INTERP_IMAGE
-    for out_s, k, staged, span, interp in ((out_s1, RETK_STAGED, True, False, False),
-                                           (out_s0, 1, False, False, False),
-                                           (out_s2, 1, False, True, False),
-                                           (out_s3, RETK_INTERP, True, False, True)):
+    global NVGPR, INTERP_IMAGE
+    for out_s, k, staged, interp in ((out_s1, RETK_STAGED, True, False),
+                                     (out_s0, 1, False, False),
+                                     (out_s3, RETK_INTERP, True, True)):
         set_retk(k)
-        SPAN_IMAGE = span
         INTERP_IMAGE = interp
         if not staged:
-            NVGPR += SPAN_HOIST_REGS if span else GEN_HOIST_REGS
+            NVGPR += GEN_HOIST_REGS
         h = generate(out_s, staged)
         header = header or h
         assert h[:-2] == header[:-2]   # identical but for the RETK-dependent lines
@@ -3478,8 +3031,6 @@ def main():
                             "#define AH_NVGPR_STAGED %d" % (64 if RETK_STAGED == 1 else 64 + 2 * RETK_STAGED),
                             "#define AH_RET_GROUPS_GENERAL 1",
                             "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS),
-                            "#define AH_SPAN_HOIST_REGS %d  // span image: hoisted-load VGPRs from v64" % SPAN_HOIST_REGS,
-                            "#define AH_NVGPR_SPAN %d" % (64 + SPAN_HOIST_REGS),
                             "#define AH_NVGPR_INTERP %d  // the interpreter's staged image (m3)"
                             % (64 if RETK_INTERP == 1 else 64 + 2 * RETK_INTERP),
                             "#define AH_RET_GROUPS_INTERP %d" % RETK_INTERP]
@@ -3566,7 +3117,6 @@ def generate(out_s, staged_image):
     header.append("#define AH_GEN_HOIST_REGS %d" % GEN_HOIST_REGS)
     header.append("#define AH_S_RUNMASK %d  // general image: s[76:77], a hoisted-load run's lanes" % S_RUNMASK)
     header.append("#define AH_V_IDX %d  // general image: the lane's packet index" % V_IDX)
-    header.append("#define AH_WIN_ARR_BYTES %d  // window launches: LDS per-window arrays" % W_ARR_BYTES)
     header.append("#define AH_RET_GROUPS %d" % RETK)
     header.append("#define AH_NVGPR %d" % NVGPR)
     A += link_kernel()
@@ -3585,7 +3135,7 @@ def generate(out_s, staged_image):
             vtop = max(vtop, int(a or c))
     assert vtop < NVGPR, "image code uses v%d, the kernels allocate %d VGPRs" % (vtop, NVGPR)
     kernarg = 232
-    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_SPAN if SPAN_IMAGE else NSGPR_GEN
+    nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
     if INTERP_IMAGE:
         # the interpreter kernel declares s0..s73 only: check that the image's code uses no more
         top = 0

@@ -179,33 +179,18 @@ struct dp_launch {
 	// the batch), set when the packet faults; the apply step skips a faulted packet's logged
 	// writes (a packet that faults leaves no write behind).  NULL for programs without map writes
 	uint32_t *upd_faulted;
-	// slot launches (general kernels; gen_interp.py "Slot mode": a window launch's overflow
-	// list): this launch runs slots perm[perm_cls[0] .. perm_cls[0] + perm_cls[1]) (packet
-	// indices, both on the device), span_g per group; NULL = every packet, 64 per group
-	const uint32_t *perm;
-	const uint32_t *perm_cls;
-	uint32_t reserved3;
-	uint32_t span_g;
-	uint32_t span_magic_g;    // ceil(2^32 / span_g)
+	const void *reserved3[2]; // (unused; keep vflags at the offset the assembly kernels load)
+	uint32_t reserved4[3];
 	// stores into map values (ebpf_gpu.h "Stores into map values"): bit 0 = the program reads
 	// its own stores (an overlay of the words it stored, per lane: DP_OVL_* below); bit 1 = it
 	// has value-store sites; bit 2 (DP_VF_EXTENTS) = `offsets` holds (start, end) pairs
 	// (EBPF_BATCH_EXTENTS); bits 8..15 = the overlay's entries per lane
 	uint32_t vflags;
-	// window launches (span image; gen_interp.py "Window mode"): LDS bytes of a window (0: not
-	// a window launch), packets per workgroup, the LDS offset of the per-window arrays, and the
-	// overflow slot list {0, n, packet indices...} the general kernels run after it
-	uint32_t win_bytes;
-	uint32_t win_chunk;
-	uint32_t win_arr;
-	uint32_t win_pad;
-	uint32_t *win_ovf;
+	uint32_t reserved5[4];
+	void *reserved6;
 };
 static_assert(sizeof(dp_launch) == 232, "dp_launch layout is shared with the assembly kernels");
-static_assert(offsetof(dp_launch, win_bytes) == 0xd0 && offsetof(dp_launch, win_ovf) == 0xe0,
-	      "gen_interp.py loads the window fields at fixed offsets");
-static_assert(offsetof(dp_launch, perm) == 176 && offsetof(dp_launch, span_g) == 196,
-	      "gen_interp.py loads these fields at fixed offsets");
+static_assert(offsetof(dp_launch, vflags) == 0xcc, "gen_interp.py VFLAGS_OFF");
 
 // The lane's LDS stack slice, below the frame the program addresses: the loop count (+0), the
 // overlay's entry count (+4), an 8-byte scratch a store into a map value is redirected to (+8),

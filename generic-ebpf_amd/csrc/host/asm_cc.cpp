@@ -70,7 +70,7 @@ enum : uint32_t {
 // DS opcodes (bits 24:17)
 enum : uint32_t {
 	DS_WRITE_B32 = 0x0d, DS_WRITE2_B32 = 0x0e, DS_WRITE_B8 = 0x1e, DS_WRITE_B16 = 0x1f,
-	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c, DS_READ_B128 = 0xff,
+	DS_READ_B32 = 0x36, DS_READ2_B32 = 0x37, DS_READ_U8 = 0x3a, DS_READ_U16 = 0x3c,
 };
 // VOPC compare codes: base + {lt 1, eq 2, le 3, gt 4, ne 5, ge 6}
 enum : uint32_t { VC_I32 = 0xc0, VC_U32 = 0xc8, VC_I64 = 0xe0, VC_U64 = 0xe8 };
@@ -873,41 +873,6 @@ struct emitter {
 		patch(to_end1);
 		patch(to_end2);
 	}
-	// z bytes at byte b of the 16-B block held in VGPRs base..base+3 (b + z <= 16) into d
-	void slot_extract(int d, int z, uint32_t b, int base)
-	{
-		const int k = (int)(b >> 2), sh = (int)(b & 3);
-		const int lo = base + k, nx = base + (k + 1 < 4 ? k + 1 : k);
-		if (z == 1) {
-			E.vop3(V3_BFE_U32, L(d), VGPR0 + lo, 128 + 8 * sh, 128 + 8);
-		} else if (z == 2) {
-			if (sh <= 2)
-				E.vop3(V3_BFE_U32, L(d), VGPR0 + lo, 128 + 8 * sh, 128 + 16);
-			else
-				E.vop3(V3_PERM_B32, L(d), VGPR0 + nx, VGPR0 + lo, sconst(0x0c0c0403u));
-		} else if (z == 4) {
-			if (sh == 0)
-				E.vop1(V1_MOV_B32, L(d), vreg(lo));
-			else
-				E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + nx, VGPR0 + lo, 128 + sh);
-		} else {
-			if (sh == 0) {
-				if ((lo & 1) == 0) {
-					E.vop1(V1_MOV_B64, L(d), vreg(lo));
-				} else {
-					E.vop1(V1_MOV_B32, L(d), vreg(lo));
-					E.vop1(V1_MOV_B32, Hi(d), vreg(lo + 1));
-				}
-			} else {
-				E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + lo + 1, VGPR0 + lo, 128 + sh);
-				E.vop3(V3_ALIGNBYTE, Hi(d), VGPR0 + lo + 2, VGPR0 + lo + 1, 128 + sh);
-			}
-			f.def(d, rf());
-			return;
-		}
-		hi0(d);
-		f.def(d, kbits(8 * z));
-	}
 	void ldxpkc(int d, int z, int off, int swap_bytes)
 	{
 		const int k = off >> 2, sh = off & 3;
@@ -1306,12 +1271,8 @@ struct emitter {
 	// With the run mask (s[76:77], see cc_compile) the lanes in the mask hold the load already
 	// and cannot fault on it; only when a running lane is outside the mask does the use compare:
 	// fault the lanes past their packet's end, load for the others directly (and wait for it).
-	//
-	// Span-staged launches (span: the packet is in LDS, asm_cc mode 2): the slot `tmp` holds the
-	// 16-B block of the packet that contains the load (ds_read_b128, one per hoisted load, waited
-	// for with lgkmcnt: LDS reads complete in order), and the value is extracted from it.
 	void ldx_hoisted(int d, int z, uint32_t off, int tmp, uint32_t later, uint32_t fault_off,
-			 bool runmask, bool span = false)
+			 bool runmask)
 	{
 		const int S_MASK = 48, S_CODE = 52, V_LEN = 40, S_JUNK_ = 60, V_PKT = 38;
 		size_t br = 0, from = 0;
@@ -1333,23 +1294,13 @@ struct emitter {
 			E.w(0xbf840000u | 6u);                                           // s_cbranch_scc0 +6
 			E.sop1(0x01, S_JUNK_, opnd{SRC_EXEC});                           // s_mov_b64 s60, exec
 			E.sop1(0x01, 126, opnd{(uint32_t)S_MASK});                       // s_mov_b64 exec, s48
-			if (span) {
-				E.ds(DS_READ_B128, V_PKT, 0, 0, tmp, off & ~15u);              // ds_read_b128 tmp
-				E.w(0xbf8cc07fu);                                            // s_waitcnt lgkmcnt(0)
-			} else {
-				E.w(0xdc008000u | (gop[zi] << 18) | off);                    // global_load_* tmp
-				E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)tmp << 24));
-				E.w(0xbf8c0f70u);                                            // s_waitcnt vmcnt(0)
-			}
+			E.w(0xdc008000u | (gop[zi] << 18) | off);                        // global_load_* tmp
+			E.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)tmp << 24));
+			E.w(0xbf8c0f70u);                                                // s_waitcnt vmcnt(0)
 			E.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});                      // s_mov_b64 exec, s60
 			const uint32_t skip = (uint32_t)((E.b.size() - from) / 4);
 			E.b[br] = (uint8_t)skip;
 			E.b[br + 1] = (uint8_t)(skip >> 8);
-		}
-		if (span) {
-			E.w(0xbf8c0000u | 15u | (7u << 4) | ((later & 15u) << 8) | (3u << 14)); // lgkmcnt(later)
-			slot_extract(d, z, off & 15u, tmp);
-			return;
 		}
 		E.w(0xbf8c0000u | (later & 15u) | (7u << 4) | (15u << 8) | ((later >> 4) & 3u) << 14);
 		if (z == 8) {
@@ -1712,122 +1663,6 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vecto
 			P.vop1(V1_MOV_B64, 2 * r, opnd{128});
 }
 
-namespace {
-
-// SOP2 / SOP1 / SOPC / SOPP opcodes used by the cut code (llvm-mc, gfx950)
-enum : uint32_t {
-	S2_ADD_U32 = 0x00, S2_SUB_U32 = 0x01, S2_ADDC_U32 = 0x04, S2_MIN_U32 = 0x07, S2_CSELECT_B32 = 0x0a,
-	S2_AND_B32 = 0x0c, S2_OR_B32 = 0x0e, S2_OR_B64 = 0x0f, S2_ANDN2_B64 = 0x13, S2_LSHL_B32 = 0x1c,
-	S2_BFE_U32 = 0x25,
-	S1_MOV_B32 = 0x00, S1_BCNT1_I32_B64 = 0x0d, S1_SETPC_B64 = 0x1d, S1_SWAPPC_B64 = 0x1e,
-	SC_CMP_GE_U32 = 0x09, SC_BITCMP1_B32 = 0x0d,
-	V3_MBCNT_LO = 0x28c, V3_MBCNT_HI = 0x28d,
-	G_LOAD_DWORDX2 = 0x15, G_STORE_DWORD = 0x1c, G_STORE_DWORDX2 = 0x1d,
-};
-
-void
-sopc(enc &E, uint32_t op, opnd a, opnd b)
-{
-	E.w(0xbf000000u | (op << 16) | (b.code << 8) | a.code);
-	E.lit(a);
-	E.lit(b);
-}
-
-// jump (or call, link s[50:51]) to .Lcb + off
-void
-jump_cb(enc &E, uint32_t off, bool call)
-{
-	const int P = call ? 50 : S_JUNK;
-	E.sop2(S2_ADD_U32, P, opnd{(uint32_t)S_CB}, opnd{SRC_LIT, off});
-	E.sop2(S2_ADDC_U32, P + 1, opnd{(uint32_t)S_CB + 1}, opnd{128});
-	E.sop1(call ? S1_SWAPPC_B64 : S1_SETPC_B64, call ? P : 0, opnd{(uint32_t)P});
-}
-
-} // namespace
-
-void
-cc_cut_plan(const dprog_host &xl, const std::vector<dp_entry> &low, const std::vector<uint32_t> &order,
-		 uint32_t max_cuts, std::vector<uint32_t> &cuts)
-{
-	cuts.clear();
-	if (xl.has_loops) // (the plan walks a tree)
-		return;
-	uint32_t min_size = 96; // (both sides of the divergent conditional at least this long)
-	if (const char *m = getenv("EBPF_WIN_CUT_MIN"))
-		min_size = (uint32_t)atoi(m);
-	const size_t n = low.size();
-	auto fam_of = [&](uint32_t e) { return (int)ah_fam[(uint32_t)low[e].handler]; };
-	auto is_term = [&](uint32_t e) { return fam_of(e) == AHF_EXIT || fam_of(e) == AHF_FAULT; };
-	auto is_cond = [&](uint32_t e) { return (ah_flags[(uint32_t)low[e].handler] & 1) != 0; };
-	// what the classifying run may execute: no store that can reach the packet or a map value,
-	// no map write (the main run executes it again from the packet as the caller gave it)
-	auto prefix_ok = [&](int fam) {
-		return !((fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) ||
-			 fam == AHF_UPDATE || fam == AHF_HDELETE || fam == AHF_LOOPINIT || fam == AHF_LOOPCNT ||
-			 is_value_store_fam(fam));
-	};
-	std::vector<uint32_t> parent(n, UINT32_MAX), npred(n, 0), sz(n, 0);
-	for (uint32_t e : order) {
-		if (is_term(e))
-			continue;
-		const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
-		for (uint32_t c : ch)
-			if (c < n) {
-				npred[c]++;
-				parent[c] = e;
-			}
-	}
-	for (size_t k = order.size(); k-- > 0;) {
-		const uint32_t e = order[k];
-		uint32_t size = 1;
-		if (!is_term(e)) {
-			const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
-			for (uint32_t c : ch)
-				if (c < n)
-					size += sz[c];
-		}
-		sz[e] = size;
-	}
-	// pre[e]: every entry on the path from the start to e (e excluded) is prefix_ok
-	std::vector<char> pre(n, 0), cand(n, 0), below(n, 0);
-	for (uint32_t e : order) {
-		const uint32_t p = parent[e];
-		pre[e] = e == xl.start ? 1 : (p < n && npred[e] == 1 && pre[p] && prefix_ok(fam_of(p)));
-		if (e != xl.start && pre[e] && p < n && is_cond(p) && sz[e] >= min_size) {
-			const uint32_t o = xl.entries[p].next == e ? xl.entries[p].target : xl.entries[p].next;
-			cand[e] = o < n && sz[o] >= min_size;
-		}
-	}
-	for (size_t k = order.size(); k-- > 0;) {
-		const uint32_t e = order[k];
-		if (is_term(e))
-			continue;
-		const uint32_t ch[2] = {xl.entries[e].next, is_cond(e) ? xl.entries[e].target : UINT32_MAX};
-		for (uint32_t c : ch)
-			if (c < n)
-				below[e] = below[e] || cand[c] || below[c];
-	}
-	for (uint32_t e : order)
-		if (cand[e] && !below[e])
-			cuts.push_back(e);
-	if (cuts.size() > max_cuts) { // the heaviest keep their class; the rest run as "other"
-		std::stable_sort(cuts.begin(), cuts.end(), [&](uint32_t a, uint32_t b) { return sz[a] > sz[b]; });
-		cuts.resize(max_cuts);
-	}
-	if (cuts.size() < 2)
-		cuts.clear();
-}
-
-void
-cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out)
-{
-	enc E{out};
-	sopc(E, SC_BITCMP1_B32, opnd{7}, opnd{128 + 12});              // s_bitcmp1_b32 s7, 12
-	E.w(0xbf840000u | 5u);                                        // s_cbranch_scc0 +5 (past the jump)
-	E.sop1(S1_MOV_B32, 52, opnd{128 + cls});                      // s_mov_b32 S_CODE, class
-	jump_cb(E, cut_off, false);                                   // (4 dwords) -> .Lr_cut
-}
-
 // VOP3 instructions this thread's compiler has emitted with two SGPR sources (a bug: see enc)
 unsigned
 cc_bus_violations()
@@ -1840,12 +1675,6 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	   const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 	   const std::vector<dp_map> &table, std::vector<cc_block> &out)
 {
-	// mode 2: the general kernels of a span-staged launch (the packet is in LDS: its constant-
-	// offset loads are LDS reads, hoisted as one ds_read_b128 of the 16-B block each); otherwise
-	// compiled as mode 0
-	const bool span = mode == 2;
-	if (span)
-		mode = 0;
 	const size_t n = low.size();
 	std::vector<mapinfo> maps(table.size());
 	for (size_t i = 0; i < table.size(); i++)
@@ -1878,8 +1707,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 	// per-load compares (A/B).
 	const bool runmask = mode == 0 && getenv("EBPF_CC_NORUNMASK") == nullptr;
 	std::vector<uint32_t> run_ext(n, 0); // run head: the largest off + size of its hoisted loads
-	const int hoist_regs = span ? AH_SPAN_HOIST_REGS : AH_GEN_HOIST_REGS;
-	const int slot_regs = span ? 4 : 2;
+	const int hoist_regs = AH_GEN_HOIST_REGS;
+	const int slot_regs = 2;
 	if (mode == 0 && hoist_regs > 0 && getenv("EBPF_CC_NOHOIST") == nullptr) {
 		size_t k = 0;
 		while (k < order.size()) {
@@ -1925,10 +1754,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				if (fam < AHF_LDXPKTG1 || fam > AHF_LDXPKTG8)
 					continue;
 				const int z = 1 << (fam - AHF_LDXPKTG1);
-				if (low[e].imm + (uint64_t)z > (span ? 65535u : 4095u))
+				if (low[e].imm + (uint64_t)z > 4095u)
 					continue;
-				if (span && (low[e].imm & 15) + (uint64_t)z > 16)
-					continue; // (straddles two blocks: the handler's own LDS read)
 				ld.push_back(e);
 			}
 			if (ld.size() >= 2) {
@@ -2013,12 +1840,8 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					Hq.vopc(VC_U32 + P_LE, k32(K32 + (uint32_t)z), V_LEN); // vcc = off+z <= len
 					Hq.sop1(0x20, S_JUNK_, opnd{SRC_VCC});                  // s_and_saveexec_b64
 				}
-				if (span) {
-					Hq.ds(DS_READ_B128, V_PKT, 0, 0, hoist_tmp[x], K32 & ~15u); // ds_read_b128
-				} else {
-					Hq.w(0xdc008000u | (gop[fx - AHF_LDXPKTG1] << 18) | K32);  // global_load_*
-					Hq.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)hoist_tmp[x] << 24));
-				}
+				Hq.w(0xdc008000u | (gop[fx - AHF_LDXPKTG1] << 18) | K32);      // global_load_*
+				Hq.w((uint32_t)V_PKT | (0x7fu << 16) | ((uint32_t)hoist_tmp[x] << 24));
 				if (!masked)
 					Hq.sop1(0x01, 126, opnd{(uint32_t)S_JUNK_});       // s_mov_b64 exec
 			};
@@ -2068,7 +1891,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = em.alu32i(movfuse_fam[e], d, (uint32_t)K, movfuse_src[e]);
 			} else if (hoist_tmp[e] >= 0) {
 				em.ldx_hoisted(d, 1 << (fam - AHF_LDXPKTG1), (uint32_t)K, hoist_tmp[e], hoist_later[e],
-					       rt.fault, runmask, span);
+					       rt.fault, runmask);
 				if (hoist_next[e] != UINT32_MAX)
 					issue(em.E, hoist_next[e]);
 			}

@@ -42,19 +42,6 @@ void cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const st
 		const std::vector<char> &entry_point, int mode, bool structured, const cc_routines &rt,
 		const std::vector<dp_map> &table, std::vector<cc_block> &out);
 
-// Window launches (gen_interp.py "Window mode"; compiled programs): the cut points of phase A —
-// heads of subtrees that both sides of a divergent conditional make heavy, the deepest, none
-// inside another, at most max_cuts (the heaviest) — whose path from the start holds no store that
-// may reach the packet or a map and no map write (phase C runs it again).  Empty when fewer than
-// two qualify.  EBPF_WIN_CUT_MIN sets the size threshold (tests).
-void cc_cut_plan(const dprog_host &xl, const std::vector<dp_entry> &low,
-		      const std::vector<uint32_t> &order, uint32_t max_cuts, std::vector<uint32_t> &cuts);
-
-// Window launches (gen_interp.py "Window mode"; span image): code at the head of cut point q,
-// class cls = q + 1.  In phase A (s7 bit 12) the running lanes record their class and leave the
-// group (.Lr_cut at cut_off from .Lcb); otherwise it falls through (2 SALU).  Cls <= 64.
-void cc_cut_code(uint32_t cls, uint32_t cut_off, std::vector<uint8_t> &out);
-
 // The group set-up a compiled program does itself (the kernel jumps straight to it): the packet
 // address (staged mode), r1 = packet, r10 = stack top, zeroes for r0, r2..r9 — the registers in
 // `live` (bit r), the packet address also if `needs_pkt` (generic memory routines read it).

@@ -34,7 +34,7 @@ enum jt_index {
 	JT_CS = 6, JT_CS_BR, JT_CS_VT, JT_CS_END,
 	JT_CL, JT_CL_LIT, JT_CL_VT, JT_CL_END,
 	JT_BR, JT_JL, JT_JL_END, JT_WAIT, JT_EXITK, JT_EXIT, JT_FAULT, JT_HLOOKUP, JT_GDONE,
-	JT_SCHED, JT_CUT, JT_AREA, JT_AREA_BYTES,
+	JT_SCHED, JT_AREA, JT_AREA_BYTES,
 	JT_COUNT
 };
 
@@ -174,19 +174,14 @@ layout_order(const dprog_host &xl, const std::vector<dp_entry> &low)
 
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
-// *win_cuts (mode 2): the cut points of the window launches' phase A.
 // Area layout: +0 a flags word (JIT_HDR_*) and 12 bytes of s_endpgm, +16 the program's start block (where the kernel enters
 // each group), then the blocks.
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	     std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-	     uint32_t *stack_stride, std::string *err, uint32_t *win_cuts)
+	     uint32_t *stack_stride, std::string *err)
 {
-	if (win_cuts)
-		*win_cuts = 0;
 	const uint32_t HDR = 16;
-	// mode 2 (span-staged general launches) compiles as mode 0 but for its packet loads (asm_cc)
-	const int gm = mode == 2 ? 0 : mode;
 	const jit_image &I = image_info(mode);
 	if (!I.ok) {
 		*err = I.why;
@@ -269,7 +264,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	std::vector<uint32_t> cont(n, GROUP_END); // where a path through the entry continues
 	std::vector<int> jdepth(n, 0);            // pending branches (join masks in use)
 	std::vector<int> join_of(n, -1);          // entry e is the taken block of conditional k
-	bool structured = (gm == 1 || AH_GEN_JOIN) && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
+	bool structured = (mode == 1 || AH_GEN_JOIN) && getenv("EBPF_JIT_NOSTRUCT") == nullptr &&
 			  getenv("EBPF_JIT_NOCC") == nullptr;
 	for (uint32_t e : order) {
 		const uint32_t h = (uint32_t)low[e].handler;
@@ -311,22 +306,6 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			}
 		}
 	}
-	// code heading a block (window cut points)
-	std::vector<std::vector<uint8_t>> push(n);
-	// window launches (mode 2, the span image; gen_interp.py "Window mode"): the cut points of
-	// phase A, class q + 1 at cut q, each block headed by its cut code (an entry point: the
-	// lanes that leave there end its hoisted-load run)
-	if (mode == 2 && getenv("EBPF_WINDOW_NOCUT") == nullptr) {
-		std::vector<uint32_t> cuts;
-		cc_cut_plan(xl, low, order, kPathMaxCuts, cuts);
-		for (size_t q = 0; q < cuts.size(); q++) {
-			const uint32_t e = cuts[q];
-			entry_point[e] = 1;
-			cc_cut_code((uint32_t)q + 1, T[JT_CUT], push[e]);
-		}
-		if (win_cuts)
-			*win_cuts = (uint32_t)cuts.size();
-	}
 	// per entry: optimised code (asm_cc.cpp) or the interpreter's handler body
 	std::vector<cc_block> cb;
 	const unsigned bus0 = cc_bus_violations();
@@ -335,7 +314,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			   cc_routines{T[JT_EXITK], T[JT_EXIT], T[JT_FAULT], T[JT_HLOOKUP]}, table, cb);
 	} else {
 		cb.assign(n, cc_block()); // every body copied: full group set-up
-		cc_prologue(gm, 0x7ff, true, false, cb[xl.start].prologue);
+		cc_prologue(mode, 0x7ff, true, false, cb[xl.start].prologue);
 	}
 	if (cc_bus_violations() != bus0) {
 		*err = "internal error: the compiler emitted a VOP3 instruction reading two SGPRs";
@@ -423,7 +402,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
-		uint32_t sz = (uint32_t)push[e].size() + join_len(e) + (uint32_t)cb[e].prologue.size() +
+		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() +
 			      (uint32_t)cb[e].hoist.size() + pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
@@ -551,10 +530,6 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			put32(a, 0xbf800000u | (op << 16) | ((uint32_t)d & 0xffffu));
 		};
 		const uint32_t OP_BRANCH = 0x02, OP_SCC0 = 0x04, OP_EXECZ = 0x08, OP_EXECNZ = 0x09;
-		if (!push[e].empty()) {
-			memcpy(&img[area + at], push[e].data(), push[e].size());
-			at += push[e].size();
-		}
 		if (structured && join_of[e] >= 0) {
 			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[join_of[e]];
 			put32(at, 0xbe800000u | (126u << 16) | (0x01u << 8) | sk); // s_mov_b64 exec, s[Tk]
@@ -720,7 +695,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	// the area's first word (never executed: code starts at +16) is read by the staged kernel's
 	// start: bit 0 = keep mode (gen_interp.py, s7 bit 14), when a packet load at a run-time
 	// offset (LDXPKTV) reads the wave's LDS packet buffer, so the next group's DMA waits
-	if (gm == 1 && getenv("EBPF_JIT_NOKEEP") == nullptr)
+	if (mode == 1 && getenv("EBPF_JIT_NOKEEP") == nullptr)
 		for (uint32_t e : order) {
 			const int fam = ah_fam[(uint32_t)low[e].handler];
 			if (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8) {
@@ -737,11 +712,10 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 // module and its kernel.
 int
 asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-	      uint32_t *win_cuts)
+	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err)
 {
 	std::vector<unsigned char> img;
-	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err, win_cuts);
+	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err);
 	if (e)
 		return e;
 	if (hipSetDevice(device) != hipSuccess)

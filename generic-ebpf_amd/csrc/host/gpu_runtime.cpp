@@ -28,23 +28,20 @@ hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device,
 			     bool hist_overwrite);
 int asm_available(int device);
 uint32_t asm_max_workgroups(int device);
-bool asm_window_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_lds_fits(int mode, uint32_t map_lds_bytes, uint32_t stack_stride);
 bool asm_program_needs_general(const dprog_host &xl);
 bool asm_program_gstage(const dprog_host &xl);
 bool asm_program_hdrlds(const dprog_host &xl);
 bool asm_hdrlds_fits(uint32_t map_lds_bytes, uint32_t stack_stride);
-bool asm_program_span(const dprog_host &xl);
 int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 // asm_jit.cpp
 int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err,
-		  uint32_t *win_cuts = nullptr);
+		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err);
 void asm_jit_release(void *mod);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
-		 uint32_t *stack_stride, std::string *err, uint32_t *win_cuts = nullptr);
+		 uint32_t *stack_stride, std::string *err);
 
 
 namespace {
@@ -98,9 +95,6 @@ struct rows_slot {
 	size_t log_bytes = 0;
 	void *win = nullptr;
 	size_t win_bytes = 0;
-	// window launches: the overflow slot list (any contents but its count, set per launch)
-	void *bk = nullptr;
-	size_t bk_bytes = 0;
 	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
 	// shard on the device (any contents: every launch overwrites its row), and fork/join events
 	void *mh = nullptr;
@@ -233,20 +227,6 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 	return 0;
 }
 
-// The stream's window scratch buffer (>= bytes, any contents).
-int
-bk_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
-{
-	std::lock_guard<std::mutex> g(g_rows_lock);
-	rows_slot *r;
-	int err = slot_for(device, stream, &r);
-	if (!err)
-		err = grow_zeroed(&r->bk, &r->bk_bytes, bytes);
-	if (!err)
-		*out = static_cast<uint8_t *>(r->bk);
-	return err;
-}
-
 // The leading stream's multi-device scratch: `rows` histogram rows and `nev` events.
 int
 multi_acquire(int device, hipStream_t stream, uint32_t rows, size_t nev, unsigned long long **mh,
@@ -323,7 +303,6 @@ ensure_translated(struct ebpf_prog *ep)
 		x->asm_gstage = asm_program_gstage(*x);
 		x->asm_pktv = asm_program_hdrlds(*x);
 		x->asm_hdrlds = x->asm_pktv && getenv("EBPF_NOHDRLDS") == nullptr;
-		x->asm_span = asm_program_span(*x);
 	}
 	ep->xlated = std::move(x);
 	if (ep->xlated->error)
@@ -626,7 +605,7 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	std::string msg;
 	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
-				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg, &dp->jit_cuts[mode]);
+				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg);
 	dp->build_ms[mode] =
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
@@ -735,98 +714,6 @@ upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t
 	return 0;
 }
 
-// Window launch of a large batch (offsets form) of a compiled program that reads past the
-// packets' first 64 bytes (gen_interp.py "Window mode"): the span image walks each workgroup's
-// share of the batch in windows of up to 256 packets staged in LDS as one contiguous DMA, runs
-// every packet to its exit or to the head of a heavy subtree (a cut point, asm_jit.cpp), sorts
-// the cut packets by subtree in LDS and runs them again from the start 64 per group, so a group
-// takes one subtree.  The packets that cannot open a window (not 16-B aligned, longer than a
-// window) are listed on the device and run next on the general kernels (slot mode), so every
-// packet keeps its own result, fault byte and verdict.  No map writes (a rerun packet must see
-// what it saw the first time; maps are read-only during a batch).
-constexpr uint64_t kWinMin = 1u << 14;     // smaller batches: one plain launch
-constexpr bool kWindowDefault = false;     // opt-in (EBPF_WINDOW=1) until measured
-constexpr uint64_t kWinMax = 1u << 28;     // (one chunk of launch_interp_asm)
-
-bool
-window_wanted(const struct ebpf_prog *ep, const dprog_device *dp, const dp_launch &L)
-{
-	// (EBPF_WINDOW=0 / 1: force off / on whatever the batch; EBPF_WINDOW_MINBATCH=n: the
-	// smallest batch that is windowed, for tests)
-	const char *on = getenv("EBPF_WINDOW");
-	if (on && *on == '0')
-		return false;
-	uint64_t min = kWinMin;
-	if (const char *m = getenv("EBPF_WINDOW_MINBATCH"))
-		min = strtoull(m, nullptr, 0);
-	// (the staged copy is not written back: no store that may reach the packet)
-	// (extents batches: packets in any order, a window needs them back to back)
-	const bool fits = L.offsets != nullptr && !(L.vflags & DP_VF_EXTENTS) && L.count >= min &&
-			  L.count <= kWinMax &&
-			  !ep->xlated->asm_needs_general && !prog_writes_maps(*ep->xlated);
-	if (on && *on == '1')
-		return fits;
-	return fits && ep->xlated->asm_span && kWindowDefault;
-}
-
-int
-launch_windowed(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L, hipStream_t stream,
-		hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist, bool overwrite,
-		bool *done)
-{
-	*done = false;
-	if (jit_entries(ep, dp, 2) != 0 || jit_entries(ep, dp, 0) != 0 ||
-	    !asm_window_fits(dp->map_lds_bytes, dp->jit_stride[2]))
-		return 0; // (no span code for this program, or no room for a window: the plain launch)
-	// (+ 512 bytes: EBPF_WIN_DEBUG's record after the list, gen_interp.py window_debug)
-	const size_t ovf_bytes = (8 + 4 * (size_t)L.count + 512 + 255) & ~(size_t)255;
-	uint8_t *ovf;
-	int err = bk_acquire(dp->device, stream, ovf_bytes, &ovf);
-	if (err)
-		return fail(err, "window overflow list");
-	hipError_t e;
-	if ((e = hipMemsetAsync(ovf, 0, 8, stream)) != hipSuccess)
-		return hip_fail(e, "hipMemsetAsync(window overflow)");
-	if (ev_start && (e = hipEventRecord(ev_start, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	dp_launch Lw = L;
-	Lw.win_ovf = reinterpret_cast<uint32_t *>(ovf);
-	Lw.stack_stride = dp->jit_stride[2];
-	Lw.win_bytes = 1; // (launch_interp_asm sizes the window)
-	static const bool dbg = getenv("EBPF_WIN_DEBUG") != nullptr;
-	Lw.win_pad = dbg ? 1u : 0u;
-	e = launch_interp_asm(Lw, stream, dp->device, 2, dp->map_lds_bytes, dp->jit_fn[2], 0, nullptr,
-			      nullptr, user_hist, overwrite);
-	if (e != hipSuccess)
-		return hip_fail(e, "window launch");
-	dp_launch Lo = L;
-	Lo.perm = reinterpret_cast<const uint32_t *>(ovf) + 2;
-	Lo.perm_cls = reinterpret_cast<const uint32_t *>(ovf);
-	Lo.span_g = 64;
-	Lo.span_magic_g = (uint32_t)((0x100000000ull + 63) / 64);
-	Lo.stack_stride = dp->jit_stride[0];
-	e = launch_interp_asm(Lo, stream, dp->device, 0, dp->map_lds_bytes, dp->jit_fn[0], 0, nullptr,
-			      nullptr, user_hist, false);
-	if (e != hipSuccess)
-		return hip_fail(e, "window overflow launch");
-	if (ev_stop && (e = hipEventRecord(ev_stop, stream)) != hipSuccess)
-		return hip_fail(e, "hipEventRecord");
-	if (dbg) {
-		uint32_t rec[64 + 3 + 16];
-		hipStreamSynchronize(stream);
-		hipMemcpy(rec, ovf + 8 + 4 * L.count, sizeof(rec), hipMemcpyDeviceToHost);
-		fprintf(stderr, "window dbg: W %u WC %u s7 %#x cnt", rec[64], rec[65], rec[66]);
-		for (int k = 0; k < 16; k++)
-			fprintf(stderr, " %u", rec[67 + k]);
-		fprintf(stderr, "\n  cls");
-		for (int k = 0; k < 64; k++)
-			fprintf(stderr, " %u", rec[k]);
-		fprintf(stderr, "\n");
-	}
-	dp->last_layout = 4;
-	*done = true;
-	return 0;
-}
 
 // A shard's write log brought to the host (a batch whose shards ran on several devices: the
 // logs are merged there, in global packet order).  Records as on the device (map_writes.h);
@@ -1150,15 +1037,9 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		bool probes = ep->xlated->has_loops;
 		for (const dp_map &m : dp->table)
 			probes = probes || (m.flags & DP_MAP_HASH) != 0;
-		bool done = false;
-		if (fn && mode == 0 && window_wanted(ep, dp, L) &&
-		    (err = launch_windowed(ep, dp, L, stream, ev_start, ev_stop, user_hist, hist_overwrite,
-					   &done)))
-			return err;
-		e = done ? hipSuccess
-			 : launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-					     (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
-					     hist_overwrite);
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
+				      (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
+				      hist_overwrite);
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;
@@ -1508,7 +1389,7 @@ ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *
 EBPF_EXPORT int
 ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len)
 {
-	if (ep == nullptr || len == nullptr || layout < 0 || layout > 2)
+	if (ep == nullptr || len == nullptr || layout < 0 || layout > 1)
 		return fail(EINVAL, "bad argument");
 	std::lock_guard<std::mutex> g(ep->dlock);
 	int err = ensure_translated(ep);

@@ -111,34 +111,28 @@ constexpr uint32_t kHistLds = 1024; // bins 0..255 (bin 256 is counted in global
 constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
-// window launches: the smallest window worth staging (gen_interp.py "Window mode")
-constexpr uint32_t kWinMinBytes = 4096;
 
 // The assembly interpreter's code objects (build/asm_image.cpp): mode 1 = staged 64-B kernels,
-// mode 0 = general kernels, mode 2 = general kernels of window launches, whose packets sit in
-// LDS (compiled programs only).  Image 3 is mode 1 for the interpreter
-// itself (variant 2): one result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU
-// are resident instead of 6 (gen_interp.py NSGPR_INTERP).
-constexpr int kModes = 3;
-// Window launches: the most cut points of a program (classes 1..15; 0 = no cut reached)
-constexpr uint32_t kPathMaxCuts = 15;
+// mode 0 = general kernels.  Image 3 is mode 1 for the interpreter itself (variant 2): one
+// result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU are resident instead of 6
+// (gen_interp.py NSGPR_INTERP).
+constexpr int kModes = 2;
 // Staged compiled programs: flags word at the head of the code area (asm_jit.cpp), bit 0 = keep
 // the group's packets in the LDS buffer until the program is done (LDXPKTV reads them there)
 constexpr uint32_t JIT_HDR_KEEP_PKT = 1;
 constexpr int kInterpStagedImage = 3;
-extern __attribute__((visibility("hidden"))) const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[], ebpf_asm_hsaco_m2[],
+extern __attribute__((visibility("hidden"))) const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[],
     ebpf_asm_hsaco_m3[];
-extern __attribute__((visibility("hidden"))) const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len, ebpf_asm_hsaco_m2_len,
+extern __attribute__((visibility("hidden"))) const size_t ebpf_asm_hsaco_m1_len, ebpf_asm_hsaco_m0_len,
     ebpf_asm_hsaco_m3_len;
 inline const unsigned char *asm_image(int mode)
 {
-	return mode == 1 ? ebpf_asm_hsaco_m1 : mode == 2 ? ebpf_asm_hsaco_m2
-		: mode == 3 ? ebpf_asm_hsaco_m3 : ebpf_asm_hsaco_m0;
+	return mode == 1 ? ebpf_asm_hsaco_m1 : mode == 3 ? ebpf_asm_hsaco_m3 : ebpf_asm_hsaco_m0;
 }
 inline size_t asm_image_len(int mode)
 {
-	return mode == 1 ? ebpf_asm_hsaco_m1_len : mode == 2 ? ebpf_asm_hsaco_m2_len
-		: mode == 3 ? ebpf_asm_hsaco_m3_len : ebpf_asm_hsaco_m0_len;
+	return mode == 1 ? ebpf_asm_hsaco_m1_len : mode == 3 ? ebpf_asm_hsaco_m3_len
+		: ebpf_asm_hsaco_m0_len;
 }
 
 // Per (program, device): entries for each interpreter variant and the map table.
@@ -156,7 +150,6 @@ struct dprog_device {
 	void *jit_mod[kModes] = {};              // variant 0: compiled program module, per mode
 	void *jit_fn[kModes] = {};               // its kernel
 	uint32_t jit_stride[kModes] = {};
-	uint32_t jit_cuts[kModes] = {};          // mode 2: the window launches' cut points
 	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
 	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode
 	void *d_upd = nullptr;                   // map writes: upd_map per table map (map_writes.h)
@@ -211,7 +204,6 @@ struct dprog_host {
 	bool asm_pktv = false;               // packet loads at run-time offsets (LDXPKTV), no packet stores
 	bool asm_hdrlds = false;             // ... and keep them in LDS for run-time-offset loads
 	                                     // (asm_program_hdrlds)
-	bool asm_span = false;               // window launches pay (asm_program_span)
 	uint32_t max_stack = 0;
 	double translate_ms = 0;             // host time of translate_program
 	// Map writes of a device batch (ebpf_gpu.h): the write log holds max_updates records per

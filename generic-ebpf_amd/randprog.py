@@ -280,7 +280,7 @@ def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None
     """writes: half the map helper calls are map_update_elem / map_delete_elem (the device
     batch semantics: ebpf_gpu.h "Map writes in a device batch"); vstores: every lookup hit
     stores into the value first (ebpf_gpu.h "Stores into map values"); pkt_stores=False: packet
-    loads where stores into the packet would be (programs the window launches take)."""
+    loads where stores into the packet would be (programs that leave the packet unchanged)."""
     gen = _Gen(seed, nmaps, map_value_size, writes, vstores)
     if not pkt_stores:
         gen.pkt_store = gen.ldx_pkt

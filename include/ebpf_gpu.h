@@ -308,9 +308,8 @@ int ebpf_prog_device_info(struct ebpf_prog *ep, struct ebpf_dprog_info *info);
                                     program too large for the code area) */
 struct ebpf_dexec_info {
 	int32_t exec;          /* EBPF_EXEC_* of the last launch on `device`; -1 = none yet */
-	int32_t layout;        /* its kernel: 1 = staged fixed 64-B packets, 0 = general, 4 = a
-	                          window launch (packets staged in LDS windows, sorted by subtree;
-	                          EBPF_WINDOW=1); -1 = none */
+	int32_t layout;        /* its kernel: 1 = staged fixed 64-B packets, 0 = general; -1 =
+	                          none */
 	double translate_ms;   /* host time of the state-tree translation (once per program) */
 	double build_ms;       /* compile (COMPILED) or lower + link (INTERPRETER) time for that
 	                          kernel on that device, paid at its first launch; 0 for HIP */
@@ -318,9 +317,8 @@ struct ebpf_dexec_info {
 int ebpf_prog_device_exec(struct ebpf_prog *ep, int device, struct ebpf_dexec_info *info);
 
 /* Diagnostics: the program as compiled for variant 0, raw gfx950 instruction bytes, for packet
- * `layout` 1 (fixed 64-B packets), 0 (any stride / offsets) or 2 (the window kernels: packets in
- * LDS, cut points headed by their phase-A code).  Host only (no GPU needed; map base addresses
- * are then 0).  *len: in = size of buf, out = bytes of code.  buf == NULL just
+ * `layout` 1 (fixed 64-B packets) or 0 (any stride / offsets); others EINVAL.  Host only (no
+ * GPU needed; map base addresses are then 0).  *len: in = size of buf, out = bytes of code.  buf == NULL just
  * sizes.  Returns 0, ENOSPC (buf too small), E2BIG (program too large to compile). */
 int ebpf_prog_device_code(struct ebpf_prog *ep, int layout, void *buf, size_t *len);
 

@@ -1,6 +1,6 @@
 """The GPU fuzzer (tools/fuzz_gpu.py) inside the suite, on seeds the fixed-seed parity tests do
 not use: random programs under the reference's semantics with array maps (every variant, staged
-and general kernels, window launches) and with hashtables, standard-semantics programs (loop-free,
+and general kernels) and with hashtables, standard-semantics programs (loop-free,
 counted loops, cursor walks), and randomly edited programs the oracle finds defined.  Each mode
 compares results, fault codes, packet bytes after the batch and the maps with the oracle.  The
 long campaigns (thousands of programs per configuration) stay in tools/fuzz_gpu.py; their logs

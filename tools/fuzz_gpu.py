@@ -1,9 +1,7 @@
 """Randomised parity sweep on the GPU (a longer run than tests/test_gpu_parity.py): seeded random
 programs (generic-ebpf_amd/randprog.py: every opcode and reference quirk) on the device against the
 oracle, for every device variant, on both kernels: 64-B packets (staged) and packets of random
-length 16..79 at CSR offsets (general kernels, short packets fault), and as window launches
-(EBPF_WINDOW=1 with cut threshold 2 and no batch threshold: random programs are cut anywhere,
-their packets staged in LDS windows and sorted by the subtree reached).
+length 16..79 at CSR offsets (general kernels, short packets fault).
 Odd-numbered programs also call map_update_elem / map_delete_elem (the device batch semantics).
 Compares results, fault codes, post-run packet bytes and the maps after the batch.
 --hash: the programs' two maps are hashtables instead (4-byte keys, a random live subset of a
@@ -258,36 +256,27 @@ def mutated(a, env):
 
 def reference(a, env):
     """Random programs under the reference's semantics (array maps, or hashtables with --hash)
-    on every variant and both kernels, plus window launches; returns True on any mismatch."""
+    on every variant and both kernels; returns True on any mismatch."""
     failed = False
-    configs = [(v, lay, 0) for v in (0, 1, 2) for lay in ("staged", "general")]
-    configs += [(0, "general", "win")]   # window launches, cut threshold 2, any batch size
-    for variant, layout, rg in configs:
-        if rg == "win":
-            os.environ.update(EBPF_WINDOW="1", EBPF_WIN_CUT_MIN="2", EBPF_WINDOW_MINBATCH="1")
-        t0 = time.time()
-        bad, faults = [], 0
-        try:
+    for variant in (0, 1, 2):
+        for layout in ("staged", "general"):
+            t0 = time.time()
+            bad, faults = [], 0
             for k in range(a.programs):
-                # (window launches take programs without map writes: those get none here)
-                c = case(k, a.seed, layout, a.hash, writes=False if rg == "win" else None)
+                c = case(k, a.seed, layout, a.hash)
                 want, wf, wdata, wmaps = oracle(c)
                 # (every other general-kernel case hands its packets over as extents)
-                got, gf, gdata, gmaps = device(env, c, variant, extents=bool(k & 2) and rg != "win")
+                got, gf, gdata, gmaps = device(env, c, variant, extents=bool(k & 2))
                 faults += int(np.count_nonzero(wf))
                 if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
                         np.array_equal(wdata, gdata) and wmaps == gmaps):
                     bad.append(k)
                 if k % 100 == 99:
                     print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        finally:
-            for k in ("EBPF_WINDOW", "EBPF_WIN_CUT_MIN", "EBPF_WINDOW_MINBATCH"):
-                os.environ.pop(k, None)
-        print("%svariant %d %-7s%s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            "hash " if a.hash else "", variant, layout,
-            " window" if rg == "win" else "", a.programs, faults, len(bad), bad[:20],
-            time.time() - t0), flush=True)
-        failed = failed or bool(bad)
+            print("%svariant %d %-7s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+                "hash " if a.hash else "", variant, layout, a.programs, faults, len(bad), bad[:20],
+                time.time() - t0), flush=True)
+            failed = failed or bool(bad)
     return failed
 
 
