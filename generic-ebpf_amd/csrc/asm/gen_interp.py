@@ -986,36 +986,9 @@ def _rot(d, x, k):
     return ["v_alignbit_b32 %s, %s, %s, %d" % (d, x, x, 32 - k)]
 
 
-def dma_next_full(tmp, save):
-    """LDS DMA of this wave's next group (a full one) into its packet buffer, as the group
-    set-up issues it; sets s7 bit 5.  Clobbers s[64:65], `tmp`, the SGPR pair `save`, m0."""
-    return ["s_or_b32 s7, s7, 32"] + next_group(tmp) + [
-            "s_lshr_b32 s65, %s, 20" % s(tmp),
-            "s_lshl_b32 s64, %s, 12" % s(tmp),
-            "s_add_u32 s64, s64, %s" % s(S_DATA),
-            "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
-            "s_mov_b64 %s, exec" % sp(save),
-            "s_mov_b64 exec, -1",
-            "s_mov_b32 m0, %s" % s(S_PKTLDS),
-            "s_nop 0"] + [
-            "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
-            for qq in range(4)] + [
-            "s_mov_b64 exec, %s" % sp(save)]
-
-
 def probe_wait(tag):
-    """Wait for the hashtable probe load just issued.  When the group set-up deferred the next
-    group's DMA (s7 bits 5:4 = 01), issue it now, behind the probe, and wait for the probe
-    alone (vmcnt(4): loads retire in issue order), so the probe's latency no longer includes
-    the 4-KB DMA's.  Uses s[64:65], s68 (not read by the probe loops), S_JUNK, m0."""
-    return ["s_and_b32 s68, s7, 48",
-            "s_cmp_eq_u32 s68, 16",
-            "s_cbranch_scc0 .L%s_w0" % tag] + dma_next_full(68, S_JUNK) + [
-            "s_waitcnt vmcnt(4)",
-            "s_branch .L%s_wd" % tag,
-            ".L%s_w0:" % tag,
-            "s_waitcnt vmcnt(0)",
-            ".L%s_wd:" % tag]
+    """Wait for the hashtable probe load just issued."""
+    return ["s_waitcnt vmcnt(0)"]
 
 
 def hlookup_routine():
@@ -2207,18 +2180,11 @@ def routines():
     # OVLFIX (called by generic loads when dp_launch.vflags bit 0): the packet's own stores over
     # the S_T0 bytes at H[0:1] just read into H[2:3]
     L += [".Lr_ovlfix:"] + ovl_fix("L", (H[2], H[3])) + ["s_setpc_b64 %s" % sp(S_LINK)]
-    # DMA_NEXT (staged kernel, deferred mode s7 bit 4): issue the LDS DMA of this wave's next
-    # group now, once per group (sets bit 5).  The group set-up defers only a full next group,
-    # so this is always the 4-instruction full-group DMA.  Preserves exec, S_T*, s[66:71];
-    # clobbers s[64:65], S_CODE, S_SAVE, m0.
-    L += [".Lr_dma_next:"] + dma_next_full(S_CODE, S_SAVE) + [
-          "s_setpc_b64 %s" % sp(S_LINK)]
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
     # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
     # past the batch end masked off.  Clobbers s[64:68], m0, exec.
-    # The lane mask is a VALU compare, so it is computed under exec = all lanes: a caller may
-    # arrive with any exec (.Lgroup_done in keep mode comes from .Lr_schedule with exec = 0, and
-    # a compare under it would DMA no chunk, leaving the previous group's bytes in the buffer)
+    # The lane mask is a VALU compare, so it is computed under exec = all lanes, whatever exec
+    # the caller arrives with (a compare under exec = 0 would DMA no chunk)
     L += [".Lr_prefetch:",
           "s_mov_b64 exec, -1",
           "s_cmp_ge_u32 %s, %s" % (s(S_T0), s(S_NGROUPS)),
@@ -2286,17 +2252,13 @@ def kernel(name, staged, jit=False):
           ".L%s_noext:" % k]
     if staged:
         # s7 bit 14 (keep mode): the program reads its packet at run-time offsets from the LDS
-        # packet buffer (LDXPKTV), so the next group's DMA waits for the group's end.  Compiled
-        # code flags it in the word at the head of its code area (asm_jit.cpp JIT_HDR_KEEP_PKT),
-        # the interpreter's launch in dp_launch.vflags (DP_VF_KEEP, still in S_T3)
-        if jit:
-            L += raddr("ebpf_jit_area", S_JUNK) + [
-                "s_load_dword %s, %s, 0x0" % (s(S_T3), sp(S_JUNK)),
-                "s_waitcnt lgkmcnt(0)",
-                "s_bitcmp1_b32 %s, 0" % s(S_T3)]
-        else:
-            L += ["s_bitcmp1_b32 %s, 3" % s(S_T3)]
-        L += ["s_cbranch_scc0 .L%s_nokeep" % k,
+        # packet buffer (LDXPKTV), so the next group's DMA waits for the group's end.  Set by
+        # the host in dp_launch.vflags (DP_VF_KEEP, still in S_T3) for compiled and interpreted
+        # programs alike.  (Double-buffering the packets instead, two 4-KB buffers per wave,
+        # measured slower on C3L: 0.294 against 0.284 ms, the LDS cutting 6 workgroups per CU
+        # to 4; profiles/r05/keep2/)
+        L += ["s_bitcmp1_b32 %s, 3" % s(S_T3),
+              "s_cbranch_scc0 .L%s_nokeep" % k,
               "s_or_b32 s7, s7, 0x4000",
               ".L%s_nokeep:" % k]
     if not staged:   # header staging requested by the host (dp_launch.lds_pkt_base bit 31)
@@ -2554,10 +2516,7 @@ def common_group_code():
           "s_mov_b32 %s, %s" % (s(S_T0), s(S_GROUP))] + call(".Lr_prefetch") + [
           "s_branch .Lgroup_check"]
     L += [".Lgroup_done:"]
-    L += ["s_and_b32 %s, s7, 48" % s(S_BYTES),
-          "s_cmp_eq_u32 %s, 16" % s(S_BYTES),                     # deferred and not issued
-          "s_cbranch_scc0 .Lgd_dma_ok"] + call(".Lr_dma_next") + [
-          ".Lgd_dma_ok:"] + slot_commit() + next_group(S_T0) + [
+    L += slot_commit() + next_group(S_T0) + [
           # keep mode (s7 bits 14 and 0: staged kernels): the next group's DMA, now that the
           # program is done with the packet buffer
           "s_and_b32 %s, s7, 0x4001" % s(S_BYTES),
@@ -2584,23 +2543,14 @@ def common_group_code():
                                                           v(H[1]), 16 * q))
     # next group's DMA: a full group (the common case) inline, with exec = all lanes and the
     # instruction offset stepping both the global and the LDS address (M0 set once); a partial
-    # group through the masking routine
-    # (s7 bit 4: a program that probes memory issues this DMA itself right after its first
-    # probe, so the two latencies overlap — see .Lr_dma_next; bit 5: issued for this group)
-    # (keep mode, s7 bit 14: none here; .Lgroup_done issues it once the program is done with
-    # the buffer)
+    # group through the masking routine.  (Keep mode, s7 bit 14: none here; .Lgroup_done
+    # issues it once the program is done with the buffer)
     L += ["s_waitcnt lgkmcnt(0)",
-          "s_or_b32 s7, s7, 32",
           "s_bitcmp1_b32 s7, 14",
-          "s_cbranch_scc1 .Lgs_pf_keep"] + next_group(S_T0) + [
+          "s_cbranch_scc1 .Lgs_pf_done"] + next_group(S_T0) + [
           "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),        # full groups
           "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
           "s_cbranch_scc0 .Lgs_pf_slow",
-          "s_bitcmp1_b32 s7, 4",                                   # deferred: left to .Lr_dma_next
-          "s_cbranch_scc0 .Lgs_pf_now",
-          "s_and_b32 s7, s7, ~32",
-          "s_branch .Lgs_pf_done",
-          ".Lgs_pf_now:",
           "s_lshr_b32 s65, %s, 20" % s(S_T0),
           "s_lshl_b32 s64, %s, 12" % s(S_T0),
           "s_add_u32 s64, s64, %s" % s(S_DATA),
@@ -2610,9 +2560,6 @@ def common_group_code():
           "s_nop 0"] + [
           "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
           for qq in range(4)] + [
-          "s_branch .Lgs_pf_done",
-          ".Lgs_pf_keep:",
-          "s_and_b32 s7, s7, ~32",
           "s_branch .Lgs_pf_done",
           ".Lgs_pf_slow:"] + call(".Lr_prefetch") + [
           ".Lgs_pf_done:",

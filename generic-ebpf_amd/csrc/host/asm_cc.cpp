@@ -2135,26 +2135,6 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 					enc P{out[xl.start].prologue};
 					P.vop3(VC_U32 + P_GT, 74, 128 + 64, VGPR0 + 40, 0);
 				}
-				// staged kernel, hashtable probes through the routine: the group set-up
-				// can leave the next group's packet DMA to the first probe (s7 bit 4,
-				// gen_interp.py probe_wait), so a probe does not also wait for the DMA.
-				// Opt-in (EBPF_CC_DEFER_DMA=1): measured 2.2% slower on C4H, the probe's own
-				// latency (a random line out of a 128-MB table) dominates, not the DMA's
-				const char *dd = getenv("EBPF_CC_DEFER_DMA");
-				// (not in keep mode, asm_jit.cpp JIT_HDR_KEEP_PKT: the program reads the packet
-				// buffer the early DMA would overwrite)
-				bool probes = false, pktv = false;
-				for (uint32_t e : order) {
-					const int f = ah_fam[(uint32_t)low[e].handler];
-					if (f == AHF_HLOOKUP && !out[e].fast)
-						probes = true;
-					if (f >= AHF_LDXPKTV1 && f <= AHF_LDXPKTV8)
-						pktv = true;
-				}
-				if (mode == 1 && probes && !pktv && dd && atoi(dd) != 0) {
-					enc P{out[xl.start].prologue};
-					P.sop2(0x0e, 7, opnd{7}, opnd{128 + 16}); // s_or_b32 s7, s7, 16
-				}
 			}
 			break;
 		}

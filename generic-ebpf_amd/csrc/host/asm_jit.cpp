@@ -174,7 +174,7 @@ layout_order(const dprog_host &xl, const std::vector<dp_entry> &low)
 
 // Compile the program for `mode` into a patched copy of the code object (*img) and return the
 // emitted code bytes (*code).  Host only.  E2BIG: the code does not fit the reserved area.
-// Area layout: +0 a flags word (JIT_HDR_*) and 12 bytes of s_endpgm, +16 the program's start block (where the kernel enters
+// Area layout: +0 16 bytes never executed (s_endpgm), +16 the program's start block (where the kernel enters
 // each group), then the blocks.
 int
 asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
@@ -692,17 +692,6 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		put32(a + 8, 0x80000000u | (0x04u << 23) | (61u << 16) | (128u << 8) | 5u);
 		put32(a + 12, 0xbe800000u | (0x1du << 8) | 60u);
 	}
-	// the area's first word (never executed: code starts at +16) is read by the staged kernel's
-	// start: bit 0 = keep mode (gen_interp.py, s7 bit 14), when a packet load at a run-time
-	// offset (LDXPKTV) reads the wave's LDS packet buffer, so the next group's DMA waits
-	if (mode == 1 && getenv("EBPF_JIT_NOKEEP") == nullptr)
-		for (uint32_t e : order) {
-			const int fam = ah_fam[(uint32_t)low[e].handler];
-			if (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8) {
-				put32(0, JIT_HDR_KEEP_PKT);
-				break;
-			}
-		}
 	if (code)
 		code->assign(img.begin() + area, img.begin() + area + total);
 	return 0;

@@ -983,15 +983,17 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	bool asm_fits = true;
 	if (variant == 0 || variant == 2) {
 		const bool compile = variant == 0;
+		uint32_t stride;
 		if (compile && (err = jit_entries(ep, dp, mode)) == 0) {
-			asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, dp->jit_stride[mode]);
+			stride = dp->jit_stride[mode];
 		} else {
 			if (compile && err != E2BIG)
 				return err;
 			if ((err = asm_entries(ep, dp, mode)))
 				return err;
-			asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, dp->asm_stride[mode]);
+			stride = dp->asm_stride[mode];
 		}
+		asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, stride);
 	}
 	if ((variant == 0 || variant == 2) && asm_fits) {
 		// variant 0: the compiled program; a program too large for the code area runs on the
@@ -1010,9 +1012,10 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		}
 		dp->last_exec = fn ? EBPF_EXEC_COMPILED : EBPF_EXEC_INTERPRETER;
 		dp->last_layout = mode;
-		// the interpreter's staged kernel: keep mode when the program loads its packet at
-		// run-time offsets (compiled code flags it in its own area, asm_jit.cpp)
-		if (fn == nullptr && mode == 1 && ep->xlated->asm_pktv)
+		// the staged kernels' keep mode (compiled and interpreted programs): a program that
+		// loads its packet at run-time offsets reads them from the wave's LDS packet buffer
+		// (gen_interp.py h_ldx_pktv), so the next group's DMA waits for the group's end
+		if (mode == 1 && ep->xlated->asm_pktv)
 			L.vflags |= DP_VF_KEEP;
 		// general kernels: header staging (bit 31), and the headers kept in LDS too (bit 30;
 		// when the 16 KB of packet buffers cost no resident workgroup: the VGPRs allow 6 per CU)

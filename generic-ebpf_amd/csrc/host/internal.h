@@ -117,9 +117,6 @@ constexpr uint32_t kPktLdsPerWG = 4 * 4096;
 // result group per burst, 64 VGPRs and s0..s73, so 8 workgroups per CU are resident instead of 6
 // (gen_interp.py NSGPR_INTERP).
 constexpr int kModes = 2;
-// Staged compiled programs: flags word at the head of the code area (asm_jit.cpp), bit 0 = keep
-// the group's packets in the LDS buffer until the program is done (LDXPKTV reads them there)
-constexpr uint32_t JIT_HDR_KEEP_PKT = 1;
 constexpr int kInterpStagedImage = 3;
 extern __attribute__((visibility("hidden"))) const unsigned char ebpf_asm_hsaco_m1[], ebpf_asm_hsaco_m0[],
     ebpf_asm_hsaco_m3[];

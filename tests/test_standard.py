@@ -194,10 +194,10 @@ def test_c3l_workload_oracle_and_cpu_path(native, env):
 
 def test_cursor_programs_cpu_and_code(native, env):
     """Cursor walks (stdprogs.gen_cursor_program, the GPU test's programs): the CPU
-    ebpf_prog_run equals the oracle on every packet the oracle does not fault MEM; the staged
-    compiled code (layout 1) flags keep mode in the first word of its area (asm_jit.cpp
-    JIT_HDR_KEEP_PKT: its packet loads at run-time offsets read the LDS packet buffer), the
-    general layout does not, and neither does a program without such loads."""
+    ebpf_prog_run equals the oracle on every packet the oracle does not fault MEM; both layouts
+    compile.  (Keep mode — the staged kernel double-buffering its packets so that the loads at
+    run-time offsets read LDS — is the host's choice per launch, dp_launch.vflags DP_VF_KEEP, and
+    is exercised by the GPU cursor tests.)"""
     for seed in range(4):
         code, rel = stdprogs.gen_cursor_program(7000 + seed)
         g = np.random.default_rng(seed)
@@ -208,17 +208,10 @@ def test_cursor_programs_cpu_and_code(native, env):
             p.set_semantics(native.SEM_STANDARD)
             for i in np.nonzero(wf == 0)[0]:   # (ebpf_prog_run has no packet bound to check)
                 assert p.run_cpu(pk[i].tobytes())[0] == int(want[i]), (seed, i)
-            assert int.from_bytes(p.device_code(1)[:4], "little") == 1
-            assert int.from_bytes(p.device_code(0)[:4], "little") != 1
+            for layout in (0, 1):
+                assert len(p.device_code(layout)) > 0
         finally:
             p.destroy()
-    code, _ = stdprogs.countdown(5)
-    p = native.Prog(env, code)
-    try:
-        p.set_semantics(native.SEM_STANDARD)
-        assert int.from_bytes(p.device_code(1)[:4], "little") != 1
-    finally:
-        p.destroy()
 
 
 def _keeps_loop_count(native, env, code):
