@@ -752,6 +752,40 @@ def h_ldx_gen(z, d, sr):
     return out
 
 
+def lds_pkt_dwords(base, save_exec=None):
+    """Write the lane's 64 staged bytes (v22..v37) into the wave's LDS packet buffer transposed:
+    dword c of lane l at S_PKTLDS + 4 l + 256 c (VGPR `base` = S_PKTLDS + 4 l).  The loads at
+    run-time offsets (lds_pkt_read) then read consecutive dwords across the lanes; in the DMA's
+    layout (lane l's 64 bytes at S_PKTLDS + 64 l) every lane reading the same offset hit the same
+    two banks (C3L: 112M conflict cycles per launch against 9M of LDS instructions)."""
+    return ["ds_write_b32 %s, v%d offset:%d" % (base, PKT0 + c, 256 * c) for c in range(16)]
+
+
+def lds_pkt_read(z, d, A, B, T):
+    """d = the z bytes at byte offset T (a VGPR, <= 64 - z) of the lane's packet in the transposed
+    LDS buffer (lds_pkt_dwords), A = S_PKTLDS + 4 lane (clobbered): the dwords around the bytes,
+    then one byte align by T's low bits (any alignment, no branch; a dword past the lane's 64
+    bytes is read but never selected).  Clobbers B, R[0..2]."""
+    t0, t1, t2 = v(R[0]), v(R[1]), v(R[2])
+    out = ["v_lshrrev_b32 %s, 2, %s" % (B, T),
+           "v_lshl_add_u32 %s, %s, 8, %s" % (B, B, A)]
+    if z == 1:
+        out += ["ds_read_b32 %s, %s" % (t0, B)]
+    else:
+        out += ["ds_read2_b32 v[%d:%d], %s offset1:64" % (R[0], R[1], B)]
+    if z == 8:
+        out.append("ds_read_b32 %s, %s offset:512" % (t2, B))
+    out += ["s_waitcnt lgkmcnt(0)",
+            "v_alignbyte_b32 %s, %s, %s, %s" % (lo(d), t0 if z == 1 else t1, t0, T)]
+    if z == 8:
+        out.append("v_alignbyte_b32 %s, %s, %s, %s" % (hi(d), t2, t1, T))
+    else:
+        if z < 4:
+            out.append("v_and_b32 %s, %s, %s" % (lo(d), "0xff" if z == 1 else "0xffff", lo(d)))
+        out.append("v_mov_b32 %s, 0" % hi(d))
+    return out
+
+
 def h_ldx_pktv(z, d, sr):
     """LDXPKTV: address = r_src + sext(off); when every running lane's address holds z bytes of
     its own packet ([V_PKT, V_PKT + V_LEN)), one flat load (or z byte loads when unaligned) —
@@ -773,40 +807,18 @@ def h_ldx_pktv(z, d, sr):
     out += ["s_and_b64 %s, %s, exec" % (sp(S_JUNK), sp(S_JUNK)),
             "s_cmp_eq_u64 %s, exec" % sp(S_JUNK),
             "s_cbranch_scc0 .Lpv_gen_{uid}"]
+    A, B = v(H[4]), v(H[5])
     if STAGED_IMAGE:
         # keep mode (s7 bit 14): the group's packets stay in the wave's LDS packet buffer while
-        # the program runs (lane l's 64 bytes at S_PKTLDS + 64 l), so read them there: the
-        # dwords around the bytes from the aligned address below them, then one byte align by
-        # the address's low bits (any alignment, no branch; a dword past the lane's 64 bytes is
-        # read but never selected)
-        A, B = v(H[4]), v(H[5])
+        # the program runs, transposed (lds_pkt_dwords), so read them there
         out += ["s_bitcmp1_b32 s7, 14",
                 "s_cbranch_scc0 .Lpv_flat_{uid}",
-                "v_lshl_add_u32 %s, v%d, 2, %s" % (A, V_L16, v(H[2])),
+                "v_lshrrev_b32 %s, 2, v%d" % (A, V_L16),
                 "v_add_u32 %s, %s, %s" % (A, s(S_PKTLDS), A)]
-        if z == 1:
-            out += ["ds_read_u8 %s, %s" % (lo(d), A), "s_waitcnt lgkmcnt(0)",
-                    "v_mov_b32 %s, 0" % hi(d)]
-        else:
-            t0, t1, t2 = v(R[0]), v(R[1]), v(R[2])
-            out += ["v_and_b32 %s, -4, %s" % (B, A),
-                    "ds_read2_b32 v[%d:%d], %s offset1:1" % (R[0], R[1], B)]
-            if z == 8:
-                out.append("ds_read_b32 %s, %s offset:8" % (t2, B))
-            out += ["s_waitcnt lgkmcnt(0)",
-                    "v_alignbyte_b32 %s, %s, %s, %s" % (lo(d), t1, t0, A)]
-            if z == 8:
-                out.append("v_alignbyte_b32 %s, %s, %s, %s" % (hi(d), t2, t1, A))
-            else:
-                if z == 2:
-                    out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
-                out.append("v_mov_b32 %s, 0" % hi(d))
-        out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
     else:
-        # general kernels with the headers kept in LDS (s7 bit 14, every lane's first 64 bytes
-        # at S_PKTLDS + 64 lane when its packet is at least that long): when every running lane's
-        # bytes lie in its first 64 and its packet has them staged, read them there
-        A, B = v(H[4]), v(H[5])
+        # general kernels with the headers kept in LDS (s7 bit 14, every lane's first 64 bytes,
+        # transposed, when its packet is at least that long): when every running lane's bytes
+        # lie in its first 64 and its packet has them staged, read them there
         out += ["s_bitcmp1_b32 s7, 14",
                 "s_cbranch_scc0 .Lpv_flat_{uid}",
                 "v_cmp_ge_u32_e64 vcc, %d, %s" % (64 - z, v(H[2])),
@@ -817,26 +829,9 @@ def h_ldx_pktv(z, d, sr):
                 "s_cbranch_scc0 .Lpv_flat_{uid}",
                 "v_mbcnt_lo_u32_b32 %s, -1, 0" % A,
                 "v_mbcnt_hi_u32_b32 %s, -1, %s" % (A, A),
-                "v_lshl_add_u32 %s, %s, 6, %s" % (A, A, v(H[2])),
-                "v_add_u32 %s, %s, %s" % (A, s(S_PKTLDS), A)]
-        if z == 1:
-            out += ["ds_read_u8 %s, %s" % (lo(d), A), "s_waitcnt lgkmcnt(0)",
-                    "v_mov_b32 %s, 0" % hi(d)]
-        else:
-            t0, t1, t2 = v(R[0]), v(R[1]), v(R[2])
-            out += ["v_and_b32 %s, -4, %s" % (B, A),
-                    "ds_read2_b32 v[%d:%d], %s offset1:1" % (R[0], R[1], B)]
-            if z == 8:
-                out.append("ds_read_b32 %s, %s offset:8" % (t2, B))
-            out += ["s_waitcnt lgkmcnt(0)",
-                    "v_alignbyte_b32 %s, %s, %s, %s" % (lo(d), t1, t0, A)]
-            if z == 8:
-                out.append("v_alignbyte_b32 %s, %s, %s, %s" % (hi(d), t2, t1, A))
-            else:
-                if z == 2:
-                    out.append("v_and_b32 %s, 0xffff, %s" % (lo(d), lo(d)))
-                out.append("v_mov_b32 %s, 0" % hi(d))
-        out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
+                "v_lshl_add_u32 %s, %s, 2, %s" % (A, A, s(S_PKTLDS))]
+    out += lds_pkt_read(z, d, A, B, v(H[2]))
+    out += ["s_branch .Lpv_done_{uid}", ".Lpv_flat_{uid}:"]
     out += gather(a0, (H[2], H[3]), [H[4]] + R[:7], z, "{uid}f")
     out += ["v_mov_b32 %s, %s" % (lo(d), v(H[2])), "v_mov_b32 %s, %s" % (hi(d), v(H[3])),
             "s_branch .Lpv_done_{uid}",
@@ -2339,15 +2334,13 @@ def pkt_setup(idx, tag):
                                                                        V_PKT, V_PKT + 1, 16 * q)
             for q in range(4)] + [
             "s_waitcnt vmcnt(0)",
-            # (s7 bit 14: the headers also into the lane's 64 bytes of the wave's LDS packet
-            # buffer, S_PKTLDS + 64 lane, for loads at run-time offsets: h_ldx_pktv)
+            # (s7 bit 14: the headers also into the wave's LDS packet buffer, transposed, for
+            # loads at run-time offsets: h_ldx_pktv)
             "s_bitcmp1_b32 s7, 14",
             "s_cbranch_scc0 .Lps_done_%s" % tag,
             "v_mbcnt_lo_u32_b32 %s, -1, 0" % v(H[1]),
             "v_mbcnt_hi_u32_b32 %s, -1, %s" % (v(H[1]), v(H[1])),
-            "v_lshl_add_u32 %s, %s, 6, %s" % (v(H[1]), v(H[1]), s(S_PKTLDS))] + [
-            "ds_write_b128 %s, v[%d:%d] offset:%d" % (v(H[1]), PKT0 + 4 * q, PKT0 + 4 * q + 3, 16 * q)
-            for q in range(4)] + [
+            "v_lshl_add_u32 %s, %s, 2, %s" % (v(H[1]), v(H[1]), s(S_PKTLDS))] + lds_pkt_dwords(v(H[1])) + [
             ".Lps_done_%s:" % tag,
             "s_mov_b64 exec, %s" % sp(S_MASK)]
 
@@ -2545,9 +2538,15 @@ def common_group_code():
     # instruction offset stepping both the global and the LDS address (M0 set once); a partial
     # group through the masking routine.  (Keep mode, s7 bit 14: none here; .Lgroup_done
     # issues it once the program is done with the buffer)
+    # (keep mode: the group's packets rewritten transposed for the program's loads at run-time
+    # offsets, lds_pkt_dwords, once every lane's staging read has returned)
     L += ["s_waitcnt lgkmcnt(0)",
           "s_bitcmp1_b32 s7, 14",
-          "s_cbranch_scc1 .Lgs_pf_done"] + next_group(S_T0) + [
+          "s_cbranch_scc0 .Lgs_pf_dma",
+          "v_lshrrev_b32 %s, 2, v%d" % (v(H[1]), V_L16),
+          "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_PKTLDS), v(H[1]))] + lds_pkt_dwords(v(H[1])) + [
+          "s_branch .Lgs_pf_done",
+          ".Lgs_pf_dma:"] + next_group(S_T0) + [
           "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),        # full groups
           "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
           "s_cbranch_scc0 .Lgs_pf_slow",

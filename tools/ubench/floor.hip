@@ -6,6 +6,9 @@
 //          3 = results staged in LDS, written as dwordx4 nt (1 KB per wave instruction)
 //   LDNT   packet DMA cache policy nt
 //   MAP    0 = superblocks of K groups interleaved over waves, 1 = one contiguous range per wave
+//   TR     0 = the DMA's contiguous layout (lane l's packet at 64 l: the staging ds_read_b128 of
+//          64 lanes at a 64-B stride conflict), 1 = chunk-transposed by the DMA itself (lane l
+//          of DMA q loads its packet's 16-B chunk q to 1024 q + 16 l: conflict-free reads)
 // plus waves per CU (workgroups per CU x 4).  Reports Gpkt/s of 64-B packets.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -13,7 +16,7 @@
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
 
-template <int NB, int K, int ST, int LDNT, int MAP, int COMP = 0>
+template <int NB, int K, int ST, int LDNT, int MAP, int COMP = 0, int TR = 0>
 __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, uint64_t *__restrict__ out,
 					       uint32_t ngroups, uint32_t nwaves_total) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -34,12 +37,12 @@ __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, u
 		uint32_t g = group_at(i);
 		if (g >= ngroups)
 			return;
-		const uint8_t *src = in + (uint64_t)g * 4096 + lane * 16;
+		const uint8_t *src = in + (uint64_t)g * 4096 + lane * (TR ? 64 : 16);
 		uint8_t *dst = buf + (i % NB) * 4096;
 #pragma unroll
 		for (int q = 0; q < 4; q++)
-			__builtin_amdgcn_global_load_lds((const void *)(src + q * 1024), LDS_PTR(dst + q * 1024), 16, 0,
-							 LDNT ? 2 : 0);
+			__builtin_amdgcn_global_load_lds((const void *)(src + q * (TR ? 16 : 1024)), LDS_PTR(dst + q * 1024), 16,
+							 0, LDNT ? 2 : 0);
 	};
 	uint64_t r[K];
 	for (int p = 0; p < NB; p++)
@@ -58,11 +61,17 @@ __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, u
 		else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 		typedef unsigned v4u __attribute__((ext_vector_type(4)));
 		v4u a, b, c, d;
-		const uint32_t la = (uint32_t)(uintptr_t)(buf + (i % NB) * 4096 + lane * 64);
-		asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-			     "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\t"
-			     "s_waitcnt lgkmcnt(0)"
-			     : "=v"(a), "=v"(b), "=v"(c), "=v"(d) : "v"(la) : "memory");
+		const uint32_t la = (uint32_t)(uintptr_t)(buf + (i % NB) * 4096 + lane * (TR ? 16 : 64));
+		if (TR)
+			asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+				     "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=v"(a), "=v"(b), "=v"(c), "=v"(d) : "v"(la) : "memory");
+		else
+			asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+				     "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=v"(a), "=v"(b), "=v"(c), "=v"(d) : "v"(la) : "memory");
 		issue(i + NB);
 		uint64_t res = (uint64_t)(a.x ^ b.y ^ c.z ^ d.w) | ((uint64_t)(a.w + d.x) << 32);
 		// synthetic per-group work like a classifier's hash: COMP dependent rounds of
@@ -103,7 +112,7 @@ __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, u
 		out[0] = acc;
 }
 
-template <int NB, int K, int ST, int LDNT, int MAP, int COMP = 0>
+template <int NB, int K, int ST, int LDNT, int MAP, int COMP = 0, int TR = 0>
 void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int cus, int wpc) {
 	const int lds = 4 * (NB * 4096 + (ST == 3 ? K * 512 : 0));
 	int wg_per_cu = wpc / 4;
@@ -115,16 +124,16 @@ void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int c
 	hipEvent_t a, b;
 	(void)hipEventCreate(&a);
 	(void)hipEventCreate(&b);
-	for (int it = 0; it < 3; it++) k_floor<NB, K, ST, LDNT, MAP, COMP><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4);
+	for (int it = 0; it < 3; it++) k_floor<NB, K, ST, LDNT, MAP, COMP, TR><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4);
 	(void)hipEventRecord(a);
-	for (int it = 0; it < 10; it++) k_floor<NB, K, ST, LDNT, MAP, COMP><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4);
+	for (int it = 0; it < 10; it++) k_floor<NB, K, ST, LDNT, MAP, COMP, TR><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4);
 	(void)hipEventRecord(b);
 	(void)hipEventSynchronize(b);
 	float ms;
 	(void)hipEventElapsedTime(&ms, a, b);
 	ms /= 10;
-	printf("COMP=%d NB=%d K=%2d ST=%d LDNT=%d MAP=%d waves/CU=%2d: %.3f ms  %.1f Gpkt/s  %.0f GB/s total\n", COMP, NB, K, ST,
-	       LDNT, MAP, wpc, ms, npk / ms / 1e6, npk * (ST == 2 ? 64.0 : 72.0) / ms / 1e6);
+	printf("TR=%d COMP=%d NB=%d K=%2d ST=%d LDNT=%d MAP=%d waves/CU=%2d: %.3f ms  %.1f Gpkt/s  %.0f GB/s total\n", TR, COMP,
+	       NB, K, ST, LDNT, MAP, wpc, ms, npk / ms / 1e6, npk * (ST == 2 ? 64.0 : 72.0) / ms / 1e6);
 }
 
 int main(int argc, char **argv) {
@@ -136,6 +145,21 @@ int main(int argc, char **argv) {
 	(void)hipMalloc(&out, npk * 8);
 	(void)hipMemset(in, 1, npk * 64);
 	const int cus = 256;
+	if (argc > 1 && argv[1][0] == 't') {
+		// round 5: the DMA's own layout against chunk-transposed DMA (conflict-free staging
+		// reads), with u64 results (ST 0), the read ceiling (ST 2), a little work (COMP 16)
+		for (int rep = 0; rep < 3; rep++) {
+			run<1, 8, 0, 1, 0, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 0, 1>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 0, 0>(in, out, ngroups, npk, cus, 24);
+			run<1, 8, 0, 1, 0, 0, 1>(in, out, ngroups, npk, cus, 24);
+			run<1, 8, 2, 1, 0, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 2, 1, 0, 0, 1>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 16, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 16, 1>(in, out, ngroups, npk, cus, 16);
+		}
+		return 0;
+	}
 	if (argc > 1 && argv[1][0] == 'k') {
 		// result-burst length K beyond the kernel's 8 (round 3): 8, 16, 32 groups per burst,
 		// u64 per lane (ST 0) or staged in LDS and written as 16-B lanes (ST 3), 16 / 24 waves
