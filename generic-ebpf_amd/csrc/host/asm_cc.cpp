@@ -57,7 +57,8 @@ enum : uint32_t {
 // VOP2 opcodes (bits 30:25)
 enum : uint32_t {
 	V2_LSHRREV_B32 = 0x10, V2_LSHLREV_B32 = 0x12, V2_AND = 0x13, V2_OR = 0x14, V2_XOR = 0x15,
-	V2_ADD_U32 = 0x34, V2_SUB_U32 = 0x35, V2_SUBREV_U32 = 0x36,
+	V2_ADD_U32 = 0x34, V2_SUB_U32 = 0x35, V2_SUBREV_U32 = 0x36, V2_SUB_CO_U32 = 0x1a,
+	V2_SUBB_CO_U32 = 0x1d,
 };
 // VOP1 opcodes (bits 16:9)
 enum : uint32_t { V1_MOV_B32 = 0x01, V1_MOV_B64 = 0x38 };
@@ -65,7 +66,7 @@ enum : uint32_t { V1_MOV_B32 = 0x01, V1_MOV_B64 = 0x38 };
 enum : uint32_t {
 	V3_MAD_U32_U24 = 0x1c3, V3_BFE_U32 = 0x1c8, V3_ALIGNBYTE = 0x1cf, V3_MAD_U64_U32 = 0x1e8,
 	V3_PERM_B32 = 0x1ed, V3_ADD3_U32 = 0x1ff, V3_LSHL_ADD_U64 = 0x208, V3_MUL_LO_U32 = 0x285,
-	V3_LSHLREV_B64 = 0x28f, V3_LSHRREV_B64 = 0x290,
+	V3_LSHLREV_B64 = 0x28f, V3_LSHRREV_B64 = 0x290, V3_LSHL_ADD_U32 = 0x1fd,
 };
 // DS opcodes (bits 24:17)
 enum : uint32_t {
@@ -343,6 +344,104 @@ struct emitter {
 	bool hz(int r) const { return f.r[r].lz >= 32; }
 	void use(int r) { used |= (uint16_t)(1u << r); }
 
+	// LDXPKTV in the staged kernels: d = the z bytes at r_sr + K of the lane's packet.
+	// * every running lane at the same offset (a cursor advanced by constants: C3L's header
+	//   words): from the packet dwords v22..v37 the staging left in registers, indexed by the
+	//   offset's dword (s_set_gpr_idx_on, M0) and aligned by its low bits — no memory access;
+	// * otherwise, in keep mode (s7 bit 14: gpu_runtime.cpp sets it for staged launches of
+	//   programs with these loads), from the wave's transposed LDS packet buffer (gen_interp.py
+	//   lds_pkt_read) when every running lane's bytes lie in its 64;
+	// * else the interpreter's handler body h (generic load, faults), spliced in by the code
+	//   generator.
+	// (The handler's own fast path re-derives the address from s[10:11] and tests the keep flag
+	// first: here r_sr is read directly and K folds into the bounds.)
+	void ldxpktv_staged(int d, int sr, int z, uint32_t K, int h)
+	{
+		const int V_PKT = 38, V_L16 = 43, S_PKTLDS = 47, S_U = 60, S_M = 48;
+		const int A = 50, B = 51, R0 = 52, R1 = 53, R2 = 54; // (gen_interp.py H[4], H[5], R[0..2])
+		const uint32_t C = 64u - (uint32_t)z - K;            // last in-bounds offset T
+		use(sr);
+		auto sopc = [&](uint32_t op, uint32_t s0, uint32_t s1) {
+			E.w(0xbf000000u | (op << 16) | (s1 << 8) | s0);
+		};
+		auto fwd = [&](uint32_t opw) { // a forward branch, patched by `to`
+			const size_t at = E.b.size();
+			E.w(opw);
+			return at;
+		};
+		auto to = [&](size_t at) { // point the branch at `at` to here
+			const uint32_t skip = (uint32_t)((E.b.size() - at - 4) / 4);
+			E.b[at] = (uint8_t)skip;
+			E.b[at + 1] = (uint8_t)(skip >> 8);
+		};
+		const uint32_t SCC0 = 0xbf840000u, SCC1 = 0xbf850000u, BR = 0xbf820000u;
+		E.vop2(V2_SUB_CO_U32, T2, vreg(L(sr)), V_PKT);               // T = r - pkt (64-bit)
+		E.vop2(V2_SUBB_CO_U32, T3, vreg(Hi(sr)), V_PKT + 1);
+		E.vop1(0x02, S_U, vreg(T2));                                 // v_readfirstlane_b32
+		E.vop1(0x02, S_U + 1, vreg(T3));
+		E.vopc(VC_U64 + P_EQ, opnd{(uint32_t)S_U}, T2);              // vcc = T == T(first lane)
+		E.sop2(0x13, S_M, opnd{SRC_EXEC}, opnd{SRC_VCC});            // s_andn2_b64: lanes differ
+		const size_t to_lds = fwd(SCC1);
+		sopc(0x07, S_U + 1, 128);                                    // s_cmp_lg_u32 hi, 0
+		const size_t slow0 = fwd(SCC1);
+		sopc(0x08, S_U, 128 + C);                                    // s_cmp_gt_u32 lo, C
+		const size_t slow1 = fwd(SCC1);
+		if (K)
+			E.sop2(0x00, S_U, opnd{(uint32_t)S_U}, opnd{128 + K});  // s_add_u32
+		E.sop2(0x1e, S_U + 1, opnd{(uint32_t)S_U}, opnd{128 + 2});  // s_lshr_b32: dword index
+		// (VOP3 sources are indexed too: profiles/r05/c3l_pktv/)
+		sopc(0x11, S_U + 1, 3);                                      // s_set_gpr_idx_on (SRC0, SRC1)
+		E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + PKT0 + 1, VGPR0 + PKT0, (uint32_t)S_U);
+		if (z == 8)
+			E.vop3(V3_ALIGNBYTE, Hi(d), VGPR0 + PKT0 + 2, VGPR0 + PKT0 + 1, (uint32_t)S_U);
+		E.w(0xbf9c0000u);                                            // s_set_gpr_idx_off
+		if (z < 4)
+			E.vop2(V2_AND, L(d), k32(z == 1 ? 0xffu : 0xffffu), L(d));
+		if (z < 8)
+			hi0(d);
+		const size_t done0 = fwd(BR);                                // (patched past the splice)
+		to(to_lds);
+		sopc(0x0d, 7, 128 + 14);                                     // s_bitcmp1_b32 s7, 14
+		const size_t slow2 = fwd(SCC0);                              // no keep mode: the handler
+		E.vopc(VC_U64 + P_GE, k32(C), T2);                           // vcc = T <= C
+		E.sop2(0x13, S_JUNK, opnd{SRC_EXEC}, opnd{SRC_VCC});        // s_andn2_b64: lanes out
+		const size_t slow3 = fwd(SCC1);
+		E.vop2(V2_LSHRREV_B32, A, opnd{128 + 2}, V_L16);             // A = S_PKTLDS + 4 lane
+		E.vop2(V2_ADD_U32, A, opnd{(uint32_t)S_PKTLDS}, A);
+		if (K)
+			E.vop2(V2_ADD_U32, T2, k32(K), T2);                  // T += K (<= 64 - z)
+		E.vop2(V2_LSHRREV_B32, B, opnd{128 + 2}, T2);                // B = A + 256 (T >> 2)
+		E.vop3(V3_LSHL_ADD_U32, B, VGPR0 + B, 128 + 8, VGPR0 + A);
+		if (z == 1)
+			E.ds(DS_READ_B32, B, 0, 0, R0, 0);
+		else
+			E.ds(DS_READ2_B32, B, 0, 0, R0, 0, 64);
+		if (z == 8)
+			E.ds(DS_READ_B32, B, 0, 0, R2, 0x200 & 0xff, 0x200 >> 8);
+		E.wait_lgkm();
+		E.vop3(V3_ALIGNBYTE, L(d), VGPR0 + (z == 1 ? R0 : R1), VGPR0 + R0, VGPR0 + T2);
+		if (z == 8) {
+			E.vop3(V3_ALIGNBYTE, Hi(d), VGPR0 + R2, VGPR0 + R1, VGPR0 + T2);
+			f.def(d, rf());
+		} else {
+			if (z < 4)
+				E.vop2(V2_AND, L(d), k32(z == 1 ? 0xffu : 0xffffu), L(d));
+			hi0(d);
+			f.def(d, kbits(8 * z));
+		}
+		const size_t done1 = fwd(BR);                                // (patched past the splice)
+		// the slow branches, and both done branches, to the body's end: the splice starts there,
+		// and the code generator moves the done branches past it
+		for (size_t at : {slow0, slow1, slow2, slow3, done0, done1})
+			to(at);
+		blk.splice_h = h;
+		blk.splice_at = (uint32_t)E.b.size();
+		blk.splice_br[0] = (uint32_t)done0;
+		blk.splice_br[1] = (uint32_t)done1;
+		blk.splice_sval[0] = K;
+		blk.splice_sval[1] = 0;
+		f.t2zero = false;
+	}
 	// an SGPR holding the 32-bit constant v for this body (s13, s14, s15)
 	uint32_t sconst(uint32_t v)
 	{
@@ -1954,6 +2053,17 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				em.ldxpkc(d, z, s, swap);
 				break;
 			}
+			case AHF_LDXPKTV1: case AHF_LDXPKTV2: case AHF_LDXPKTV4: case AHF_LDXPKTV8: {
+				const int z = 1 << (fam - AHF_LDXPKTV1);
+				const int64_t Ks = (int64_t)K;
+				ok = mode == 1 && Ks >= 0 && Ks <= 64 - z && d < AH_NREGS && s < AH_NREGS &&
+				     getenv("EBPF_CC_NOPKTV") == nullptr;
+				if (ok) {
+					em.ldxpktv_staged(d, s, z, (uint32_t)Ks, (int)h);
+					em.used |= copied_uses(fam, d, s); // (the spliced slow path's reads)
+				}
+				break;
+			}
 			case AHF_STXSTK1: case AHF_STXSTK2: case AHF_STXSTK4: case AHF_STXSTK8:
 				if (K + 8 <= 255 * 4)
 					em.stxstk(1 << (fam - AHF_STXSTK1), d, (uint32_t)K);
@@ -2062,6 +2172,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				f.t2zero = false; // (handler bodies use v46..v51 freely)
 				blk.fast = false;
 				blk.body.clear();
+				blk.splice_h = -1;
 				blk.reads = 0;
 				em.used = copied_uses(fam, d, s);
 				if (wr >= 0)
@@ -2083,6 +2194,7 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				// dead: no code, the register's VGPRs do not hold the (unused) value
 				blk.fast = true;
 				blk.body.clear();
+				blk.splice_h = -1;
 				blk.reads = 0;
 				f.pv[wr] = false;
 				f.t2zero = before.t2zero; // (its code, which may have zeroed v48, is gone)

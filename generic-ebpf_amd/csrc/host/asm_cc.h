@@ -21,6 +21,13 @@ struct cc_block {
 	std::vector<uint8_t> prologue;
 	std::vector<uint8_t> hoist; // general kernels: packet loads issued ahead for this straight run
 	int8_t sdir = -1; // conditional decided at compile time: 0 never taken, 1 always taken
+	// a fast body with a slow path: the interpreter's handler body `splice_h` (its operands
+	// s10, s11 = splice_sval, then an lgkmcnt(0) wait) is inserted at body offset splice_at, and
+	// the s_branches at body offsets splice_br[] (over the slow path; ~0 = none) grow by the
+	// inserted bytes
+	int32_t splice_h = -1;
+	uint32_t splice_at = 0, splice_br[2] = {~0u, ~0u};
+	uint32_t splice_sval[2] = {};
 };
 
 // Offsets from .Lcb of the interpreter routines compiled code calls or jumps to.

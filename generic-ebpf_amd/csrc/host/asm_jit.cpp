@@ -400,13 +400,17 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		const uint32_t nxt = k + 1 < order.size() ? order[k + 1] : GROUP_END;
 		return cont[e] != nxt;
 	};
+	// a fast body's spliced slow path (cc_block.splice_h): operands, the handler body, a wait
+	auto splice_len = [&](uint32_t e) -> uint32_t {
+		return cb[e].splice_h < 0 ? 0 : 16 + I.body_len[(uint32_t)cb[e].splice_h] + 4;
+	};
 	auto block_size = [&](uint32_t e, uint32_t *pre, uint32_t *body_end) {
 		const uint32_t h = (uint32_t)low[e].handler;
 		uint32_t sz = join_len(e) + (uint32_t)cb[e].prologue.size() +
 			      (uint32_t)cb[e].hoist.size() + pre_len(e);
 		*pre = sz;
 		if (cb[e].fast) {
-			sz += (uint32_t)cb[e].body.size();
+			sz += (uint32_t)cb[e].body.size() + splice_len(e);
 		} else {
 			sz += I.body_len[h];
 			if (ah_flags[h] & 2)
@@ -569,7 +573,35 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 			put32(at + 4, v);
 			at += 8;
 		}
-		if (cb[e].fast) {
+		if (cb[e].fast && cb[e].splice_h >= 0) {
+			// the fast body, the interpreter's handler body as its slow path, the rest
+			const cc_block &c = cb[e];
+			const uint32_t sh = (uint32_t)c.splice_h, sl = splice_len(e);
+			std::vector<uint8_t> b(c.body);
+			for (uint32_t at_br : c.splice_br) {
+				if (at_br == ~0u)
+					continue;
+				int32_t rel = (int16_t)(b[at_br] | (b[at_br + 1] << 8));
+				rel += (int32_t)(sl / 4);
+				if (rel > 32767)
+					return EINVAL; // (splice_len keeps a body far below this)
+				b[at_br] = (uint8_t)rel;
+				b[at_br + 1] = (uint8_t)(rel >> 8);
+			}
+			memcpy(&img[area + at], b.data(), c.splice_at);
+			at += c.splice_at;
+			for (int r = 0; r < 2; r++) { // s_mov_b32 s(10 + r), literal
+				put32(at, 0xbe8000ffu | ((uint32_t)(10 + r) << 16));
+				put32(at + 4, c.splice_sval[r]);
+				at += 8;
+			}
+			memcpy(&img[area + at], src + I.body_off[sh], I.body_len[sh]);
+			at += I.body_len[sh];
+			put32(at, 0xbf8cc07fu); // s_waitcnt lgkmcnt(0)
+			at += 4;
+			memcpy(&img[area + at], b.data() + c.splice_at, b.size() - c.splice_at);
+			at += b.size() - c.splice_at;
+		} else if (cb[e].fast) {
 			if (!cb[e].body.empty())
 				memcpy(&img[area + at], cb[e].body.data(), cb[e].body.size());
 			at += cb[e].body.size();
