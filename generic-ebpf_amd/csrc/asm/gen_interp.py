@@ -115,17 +115,13 @@ NSGPR_GEN = 88
 S_JOIN = 74
 JOIN_LEVELS = 12
 NSGPR_STAGED = S_JOIN + 2 * JOIN_LEVELS
-# general image with the join SGPRs too (structured compiled programs in the general kernels;
-# 98 SGPRs allow 7 instead of 8 waves per SIMD there)
-GEN_JOIN = int(os.environ.get("EBPF_ASM_GENJOIN", "0"))
-# (the join SGPRs s74..s97 would overlap the run mask and the short-lane mask, and structured exits
-# address the LDS histogram through lane 0 of v43, which the general image uses for V_IDX)
-assert not GEN_JOIN, "EBPF_ASM_GENJOIN conflicts with the run mask and V_IDX"
+# (no join SGPRs in the general image: s74..s97 would overlap the run mask and the short-lane
+# mask, and structured exits address the LDS histogram through lane 0 of v43, which the general
+# image uses for V_IDX; AH_GEN_JOIN stays 0)
+GEN_JOIN = 0
 # general image: spare VGPRs v64.. for packet loads the code generator issues ahead (asm_cc.cpp
 # hoist plan); 16 cost the general kernels 8 -> 6 waves per SIMD
 GEN_HOIST_REGS = int(os.environ.get("EBPF_ASM_GENHOIST", "16"))
-# A/B: XCD-major logical workgroup order (common_group_code)
-XCD_MAJOR = os.environ.get("EBPF_ASM_XCD") == "1"
 ALU64R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD"]
 ALU32R = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "MOV", "DIV", "MOD"]
 ALU64I = ["ADD", "MUL", "OR", "AND", "XOR", "LSH", "RSH", "DIV", "MOD", "MOV"]   # MOV = LDDW
@@ -2367,8 +2363,6 @@ def slot_commit():
 def store_prev_results(tag, final):
     """Write the result slots of the superblock that group S_PREVG ends (at the start of the
     next superblock, or at the end: `final`) as one burst of RETK x 512 B; clobbers exec."""
-    if os.environ.get("EBPF_ASM_NOSTORE"):   # experiment only: measures the read-side ceiling
-        return []
     L = ["s_cmp_eq_u32 %s, -1" % s(S_PREVG),
          "s_cbranch_scc1 .Lsp_none_%s" % tag]
     if not final and RETK > 1:
@@ -2472,24 +2466,9 @@ def common_group_code():
     # groups of 64 packets: group = workgroup*4 + wave, stride = total waves
     L += ["s_add_u32 %s, %s, 63" % (s(S_NGROUPS), s(S_COUNT)),
           "s_lshr_b32 %s, %s, 6" % (s(S_NGROUPS), s(S_NGROUPS)),
-          ] + ([
-          # (A/B, EBPF_ASM_XCD=1) XCD-major workgroup order: workgroups go to the 8 XCDs round
-          # robin, so logical workgroup (wg % 8) * (nwg / 8) + wg / 8 gives each XCD one
-          # contiguous share of the batch (when nwg is a multiple of 8)
-          "s_load_dword %s, s[0:1], 0x7c" % s(S_T1),
-          "s_waitcnt lgkmcnt(0)",
-          "s_mov_b32 %s, s2" % s(S_GROUP),
-          "s_and_b32 %s, %s, 7" % (s(S_T2), s(S_T1)),
-          "s_cmp_eq_u32 %s, 0" % s(S_T2),
-          "s_cbranch_scc0 .Lxcd_done",
-          "s_lshr_b32 %s, %s, 3" % (s(S_T1), s(S_T1)),
-          "s_and_b32 %s, s2, 7" % s(S_T2),
-          "s_mul_i32 %s, %s, %s" % (s(S_T2), s(S_T2), s(S_T1)),
-          "s_lshr_b32 %s, s2, 3" % s(S_GROUP),
-          "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_T2)),
-          ".Lxcd_done:",
-          "s_lshl_b32 %s, %s, 2" % (s(S_GROUP), s(S_GROUP))] if XCD_MAJOR else [
-          "s_lshl_b32 %s, s2, 2" % s(S_GROUP)]) + [
+          # (an XCD-major logical workgroup order, each XCD one contiguous share of the
+          # batch, measured 1-5% slower: profiles/r02/s3/ab_xcd_order.txt)
+          "s_lshl_b32 %s, s2, 2" % s(S_GROUP),
           "s_add_u32 %s, %s, %s" % (s(S_GROUP), s(S_GROUP), s(S_WAVE)),
           # K' = superblock size of this launch (total_waves bits 28..29 = log2 K')
           "s_lshr_b32 %s, %s, 28" % (s(S_T1), s(S_GSTRIDE)),

@@ -1097,160 +1097,6 @@ struct emitter {
 		f.def(0, v);
 		return true;
 	}
-	// ---- hashtable lookup (HLOOKUP) with the key in the frame at LDS offset `o` and at most 8
-	// bytes: jhash specialised for the key length (constants folded), the home slot probed
-	// inline (one 16-byte load compared in registers); lanes whose home slot holds another key
-	// continue in the generic routine (.Lr_hlookup), which probes from the home slot again.
-	struct hv { bool k; uint32_t c; int reg; };
-	// registers: v52/v53 key words, v54/v55/v46 hash a/b/c, v47 rotations, v48 slot index,
-	// v[56:59] the loaded slot head, v[60:61] the slot address (T0..T2 and routine temporaries:
-	// free between operations)
-	int htmp_next = 0;
-	int htmp()
-	{
-		static const int pool[] = {52, 53};
-		return pool[htmp_next++];
-	}
-	hv hxor(hv x, hv y, int dst)
-	{
-		if (x.k && y.k)
-			return hv{true, x.c ^ y.c, -1};
-		if (x.k)
-			std::swap(x, y);
-		E.vop2(V2_XOR, dst, y.k ? k32(y.c) : vreg(y.reg), x.reg);
-		return hv{false, 0, dst};
-	}
-	hv hrot(hv y, int k, int dst)
-	{
-		if (y.k)
-			return hv{true, (y.c << k) | (y.c >> (32 - k)), -1};
-		E.vop3(0x1ce, dst, VGPR0 + y.reg, VGPR0 + y.reg, 128 + (uint32_t)(32 - k)); // v_alignbit_b32
-		return hv{false, 0, dst};
-	}
-	hv hsub(hv x, hv y, int dst)
-	{
-		if (x.k && y.k)
-			return hv{true, x.c - y.c, -1};
-		if (y.k)
-			E.vop2(V2_SUBREV_U32, dst, k32(y.c), x.reg);   // x - const
-		else
-			E.vop2(V2_SUB_U32, dst, x.k ? k32(x.c) : vreg(x.reg), y.reg);
-		return hv{false, 0, dst};
-	}
-	bool hlookup_stk(int mi, uint32_t rec_off, uint32_t o, int ks, uint32_t flags, uint32_t hl_off)
-	{
-		if (mi < 0 || ks < 1 || ks > 8 || (off & 8))
-			return false;
-		const mapinfo &m = maps[mi];
-		// key words w0, w1 (zero-padded) from forwarded registers or the LDS frame
-		hv w[2] = {{true, 0, -1}, {true, 0, -1}};
-		const sslot *s8 = ks > 4 ? f.slot(o, 8) : nullptr;
-		const sslot *s4 = f.slot(o, ks >= 4 ? 4 : ks);
-		const sslot *s4b = ks > 4 ? f.slot(o + 4, ks - 4 >= 4 ? 4 : ks - 4) : nullptr;
-		auto masked = [&](int reg, int bytes) -> hv {
-			if (bytes >= 4)
-				return hv{false, 0, reg};
-			const int t = (reg == 52 || reg == 53) ? reg : htmp(); // (our own temporaries in place)
-			E.vop2(V2_AND, t, k32((1u << (8 * bytes)) - 1), reg);
-			return hv{false, 0, t};
-		};
-		if (s8) {
-			use(s8->reg);
-			w[0] = hv{false, 0, L(s8->reg)};
-			w[1] = masked(Hi(s8->reg), ks - 4);
-		} else if (s4 && (ks <= 4 || s4b)) {
-			use(s4->reg);
-			w[0] = masked(L(s4->reg), ks >= 4 ? 4 : ks);
-			if (ks > 4) {
-				use(s4b->reg);
-				w[1] = masked(L(s4b->reg), ks - 4);
-			}
-		} else {
-			if (o % 4)
-				return false;
-			const int t0 = htmp(), t1 = htmp(); // (consecutive)
-			if (ks > 4) {
-				if (o / 4 + 1 > 255)
-					return false;
-				E.ds(DS_READ2_B32, V_STK, 0, 0, t0, o / 4, o / 4 + 1);
-			} else {
-				E.ds(DS_READ_B32, V_STK, 0, 0, t0, o);
-			}
-			E.wait_lgkm();
-			w[0] = masked(t0, ks >= 4 ? 4 : ks);
-			if (ks > 4)
-				w[1] = masked(t1, ks - 4);
-		}
-		use(2); // (the generic routine reads r2)
-		// jhash (hashlittle, initval 0) of <= 8 bytes: no mixing rounds, the final mix only
-		const uint32_t init = 0xdeadbeefu + (uint32_t)ks;
-		const int ra = 54, rb = 55, rc = 46, rt = 47;
-		hv a = w[0].k ? hv{true, init + w[0].c, -1} : hv{false, 0, ra};
-		if (!w[0].k)
-			E.vop2(V2_ADD_U32, ra, k32(init), w[0].reg);
-		hv b = w[1].k ? hv{true, init + w[1].c, -1} : hv{false, 0, rb};
-		if (!w[1].k)
-			E.vop2(V2_ADD_U32, rb, k32(init), w[1].reg);
-		hv c{true, init, -1};
-		struct { hv *x, *y; int k; } fin[7] = {{&c, &b, 14}, {&a, &c, 11}, {&b, &a, 25}, {&c, &b, 16},
-						      {&a, &c, 4}, {&b, &a, 14}, {&c, &b, 24}};
-		for (auto &st : fin) {
-			const int dst = st.x == &a ? ra : st.x == &b ? rb : rc;
-			*st.x = hxor(*st.x, *st.y, dst);
-			*st.x = hsub(*st.x, hrot(*st.y, st.k, rt), dst);
-		}
-		if (c.k)
-			return false; // (a constant key: not worth a special case)
-		// probe: slot (hash & mask) * stride, then the next slots, until every lane has met its
-		// key (r0 = the slot's value) or an empty slot (r0 = NULL); the table is at most a
-		// quarter full, so the loop ends within a slot or two
-		const uint32_t lg = dp_hash_stride_log2(flags);
-		const int ti = 48;
-		const int A = 60, HD = 56;          // v[60:61] address, v[56:59] used/hash/key0/key1
-		const int S_PEND = 48, S_JK = 60, S_SAVE = 12;
-		E.vop2(V2_AND, ti, k32(m.max_entries - 1), c.reg);
-		E.vop1(V1_MOV_B64, 0, opnd{128});                                     // r0 = NULL
-		E.sop1(0x01, S_SAVE, opnd{SRC_EXEC});                                 // s_mov_b64 s[12:13], exec
-		E.sop1(0x01, S_PEND, opnd{SRC_EXEC});                                 // pending lanes
-		uint32_t stride_src;
-		if (!inline_i64((int64_t)(1u << lg), &stride_src))
-			return false; // (one SGPR per VOP3: the base pair takes it)
-		const uint32_t base_src = spair(m.dev_base);
-		const size_t loop_at = blk.body.size();
-		E.vop3(V3_MAD_U64_U32, A, VGPR0 + ti, stride_src, base_src, S_JUNK);
-		E.w(0xdc5c8000u);                                                     // global_load_dwordx4
-		E.w((uint32_t)A | (0x7fu << 16) | ((uint32_t)HD << 24));
-		E.w(0xbf8c0f70u);                                                     // s_waitcnt vmcnt(0)
-		E.vop3(VC_U32 + P_EQ, S_JK, 128, VGPR0 + HD, 0);                      // empty slot
-		E.sop2(0x13, S_PEND, opnd{(uint32_t)S_PEND}, opnd{(uint32_t)S_JK});   // s_andn2_b64
-		E.vop3(VC_U32 + P_EQ, S_JK, VGPR0 + HD + 1, VGPR0 + c.reg, 0);        // hash
-		E.sop2(0x0d, S_JK, opnd{(uint32_t)S_JK}, opnd{(uint32_t)S_PEND});
-		for (int q = 0; q < 2; q++) {                                         // key words
-			if (w[q].k)
-				E.vopc(VC_U32 + P_EQ, k32(w[q].c), HD + 2 + q);
-			else
-				E.vopc(VC_U32 + P_EQ, vreg(w[q].reg), HD + 2 + q);
-			E.sop2(0x0d, S_JK, opnd{(uint32_t)S_JK}, opnd{SRC_VCC});
-		}
-		E.vop3(V3_LSHL_ADD_U64, A, VGPR0 + A, 128, 128 + dp_hash_value_off((uint32_t)ks));
-		E.vop3(0x100, 0, VGPR0 + 0, VGPR0 + A, (uint32_t)S_JK);              // v_cndmask_b32_e64
-		E.vop3(0x100, 1, VGPR0 + 1, VGPR0 + A + 1, (uint32_t)S_JK);
-		E.sop2(0x13, S_PEND, opnd{(uint32_t)S_PEND}, opnd{(uint32_t)S_JK});   // (scc = any left)
-		E.w(0xbf840000u | 5u);                                                // s_cbranch_scc0 done
-		E.sop1(0x01, 126, opnd{(uint32_t)S_PEND});                            // exec = pending
-		E.vop2(V2_ADD_U32, ti, opnd{128 + 1}, ti);
-		E.vop2(V2_AND, ti, k32(m.max_entries - 1), ti);                       // (2 dwords: literal)
-		{
-			const int32_t back = -(int32_t)((blk.body.size() + 4 - loop_at) / 4);
-			E.w(0xbf820000u | ((uint32_t)back & 0xffffu));                    // s_branch loop
-		}
-		E.sop1(0x01, 126, opnd{(uint32_t)S_SAVE});                            // done: exec back
-		(void)rec_off;
-		(void)hl_off;
-		f.def(0, rf());
-		f.t2zero = false;
-		return true;
-	}
 	// LDXHV through a non-NULL hashtable lookup result whose value's first 8 bytes were
 	// loaded with the probe into register D's VGPRs: an extract, no memory access
 	bool ldxhv_fwd(int z, int d, int s, int32_t o)
@@ -1735,14 +1581,6 @@ cc_prologue(int mode, uint16_t live, bool needs_pkt, bool structured, std::vecto
 	enc P{out};
 	if (structured)
 		P.sop2(0x0e, 7, opnd{7}, opnd{128 + 4}); // s_or_b32 s7, s7, 4
-	// diagnostics only (EBPF_CC_PAD_SALU / _VALU = n): n filler instructions per group, to
-	// measure which issue port bounds a compiled program
-	if (const char *ps = getenv("EBPF_CC_PAD_SALU"))
-		for (int i = atoi(ps); i > 0; i--)
-			P.sop2(0x00, 60, opnd{60}, opnd{128 + 1}); // s_add_u32 s60, s60, 1
-	if (const char *pv = getenv("EBPF_CC_PAD_VALU"))
-		for (int i = atoi(pv); i > 0; i--)
-			P.vop2(V2_ADD_U32, 51, opnd{128 + 1}, 51); // v_add_u32 v51, 1, v51
 	const int V_PKT = 38, V_LEN = 40, H1 = 47, H3 = 49, S_DATA = 24;
 	if (mode == 1 && (needs_pkt || (live & (1u << 1)))) {
 		// staged kernel: packet address = data + index * 64 (index in v49, gen_interp.py H[3])
@@ -1812,30 +1650,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 		size_t k = 0;
 		while (k < order.size()) {
 			size_t j = k; // run [k, j]
-			// a conditional whose taken side is a short exit (<= 3 entries of ALU ending in EXIT
-			// or FAULT, the "rare early exit" shape): with EBPF_CC_RUN_XBR=1 the run goes on
-			// along the fall-through edge (A/B)
-			static const bool xbr = getenv("EBPF_CC_RUN_XBR") != nullptr;
-			auto short_exit = [&](uint32_t t) {
-				for (int steps = 0; steps < 3 && t < n; steps++) {
-					const uint32_t h = (uint32_t)low[t].handler;
-					const int fam = ah_fam[h];
-					if (fam == AHF_EXIT || fam == AHF_FAULT)
-						return true;
-					if ((ah_flags[h] & 1) || !((fam >= AHF_A64I_ADD && fam <= AHF_A64I_MOV) ||
-								   (fam >= AHF_A32I_ADD && fam <= AHF_A32I_MOD) ||
-								   (fam >= AHF_A32R_ADD && fam <= AHF_A32R_MOD)))
-						return false;
-					t = xl.entries[t].next;
-				}
-				return false;
-			};
 			auto breaks_after = [&](uint32_t e) {
 				const int fam = ah_fam[(uint32_t)low[e].handler];
-				// (letting runs continue past every conditional along the fall-through edge,
-				// loads issued for lanes that branch away, measured 3% slower on C5)
-				if ((ah_flags[(uint32_t)low[e].handler] & 1) && xbr && short_exit(xl.entries[e].target))
-					return false;
+				// (letting runs continue past conditionals along the fall-through edge, loads
+				// issued for lanes that branch away, measured 3% slower on C5)
 				return (ah_flags[(uint32_t)low[e].handler] & 1) || fam == AHF_EXIT ||
 				       fam == AHF_FAULT || fam == AHF_LOOKUPGEN ||
 				       (fam >= AHF_STXGEN1 && fam <= AHF_STXGEN8) ||
@@ -2089,14 +1907,10 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				ok = spec_map = em.ldxmap(1 << (fam - AHF_LDXMAP1), d, s, K);
 				break;
 			case AHF_HLOOKUP: {
-				// (opt-in, EBPF_CC_HSPEC=1: measured 3% slower than the generic routine on C4H —
-				// the probe's wait also waits for the next group's packet DMA issued before
-				// it, which dominates either way)
+				// (an inline jhash + home-slot probe, round 3, measured 3% slower than the
+				// generic routine on C4H and was retired in round 5)
 				const int mi = (int)(aux0 / 32);
-				ok = aux1 != 0 && getenv("EBPF_CC_HSPEC") != nullptr && mi < (int)table.size() &&
-				     (table[mi].flags & DP_MAP_HASH) &&
-				     em.hlookup_stk(mi, aux0, aux1 - 1, (int)dp_hash_key_size(table[mi].flags),
-						    table[mi].flags, rt.hlookup);
+				ok = false;
 				// the generic routine, whose probe of a key of <= 8 bytes also loads the
 				// slot's first 8 value bytes (v[50:51], gen_interp.py hlookup_routine): they
 				// are kept in a register D dead from here on, so that loads through the

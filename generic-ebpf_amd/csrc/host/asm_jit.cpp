@@ -506,6 +506,11 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 	img.assign(asm_image(mode), asm_image(mode) + asm_image_len(mode));
 	const size_t area = I.cb + T[JT_AREA];
 	const unsigned char *src = asm_image(mode) + I.cb;
+	// handler body h at area offset `at`; returns the bytes copied
+	auto copy_body = [&](size_t at, uint32_t h) -> uint32_t {
+		memcpy(&img[area + at], src + I.body_off[h], I.body_len[h]);
+		return I.body_len[h];
+	};
 	auto code_off = [&](uint32_t e) { return T[JT_AREA] + pos[e]; }; // from .Lcb
 	auto put32 = [&](size_t at, uint32_t v) { memcpy(&img[area + at], &v, 4); };
 	auto copy_t = [&](size_t at, int a, uint32_t len) {
@@ -595,8 +600,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				put32(at + 4, c.splice_sval[r]);
 				at += 8;
 			}
-			memcpy(&img[area + at], src + I.body_off[sh], I.body_len[sh]);
-			at += I.body_len[sh];
+			at += copy_body(at, sh);
 			put32(at, 0xbf8cc07fu); // s_waitcnt lgkmcnt(0)
 			at += 4;
 			memcpy(&img[area + at], b.data() + c.splice_at, b.size() - c.splice_at);
@@ -606,8 +610,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				memcpy(&img[area + at], cb[e].body.data(), cb[e].body.size());
 			at += cb[e].body.size();
 		} else {
-			memcpy(&img[area + at], src + I.body_off[h], I.body_len[h]);
-			at += I.body_len[h];
+			at += copy_body(at, h);
 			if (ah_flags[h] & 2) {
 				copy_t(at, JT_WAIT, 4);
 				at += 4;
