@@ -1,7 +1,8 @@
 """The GPU fuzzer (tools/fuzz_gpu.py) inside the suite, on seeds the fixed-seed parity tests do
 not use: random programs under the reference's semantics with array maps (every variant, staged
 and general kernels) and with hashtables, standard-semantics programs (loop-free,
-counted loops, cursor walks), and randomly edited programs the oracle finds defined.  Each mode
+counted loops, cursor walks), programs that write maps inside loops (round 5), and randomly
+edited programs the oracle finds defined.  Each mode
 compares results, fault codes, packet bytes after the batch and the maps with the oracle.  The
 long campaigns (thousands of programs per configuration) stay in tools/fuzz_gpu.py; their logs
 are under profiles/r03/fuzz/."""
@@ -28,7 +29,7 @@ def fuzz(gpu):
     return fuzz_gpu
 
 
-@pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate"])
+@pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites"])
 def test_fuzz_campaign(fuzz, env, mode):
     if mode == "reference":
         failed = fuzz.reference(_args(seed=11), env)
@@ -36,6 +37,8 @@ def test_fuzz_campaign(fuzz, env, mode):
         failed = fuzz.reference(_args(seed=12, hash=True), env)
     elif mode == "standard":
         failed = fuzz.standard(_args(seed=13, programs=80, standard=True), env)
+    elif mode == "loopwrites":
+        failed = fuzz.loop_writes(_args(seed=15, programs=40), env)
     else:
         failed = fuzz.mutated(_args(seed=14, programs=200, mutate=True), env)
     assert not failed, "mismatches (see the captured output for the failing program numbers)"

@@ -9,7 +9,7 @@ key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts
 lookups, updates and deletes against the oracle's replay model; the tables are compared through
 get_next_key's walk (order and values).
 
-  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate]
+  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate | --loopwrites]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
 import argparse
 import os
@@ -280,6 +280,54 @@ def reference(a, env):
     return failed
 
 
+def loop_writes(a, env):
+    """--loopwrites: random standard programs that write maps inside loops
+    (stdprogs.gen_loop_write_program: stores, loads back, updates, and every third program
+    counter updates; trip counts up to 24, so packets pass the 16 logged writes and fault
+    WRITES) on every variant, staged 64-B packets; results, faults and both maps against the
+    oracle's batch mode."""
+    import stdprogs
+    failed = False
+    for variant in (0, 1, 2):
+        t0, bad, faults = time.time(), [], 0
+        for k in range(a.programs):
+            seed = a.seed * 100000 + k
+            g = np.random.default_rng(seed)
+            code, rel = stdprogs.gen_loop_write_program(seed, counters=k % 3 == 2)
+            specs = [(16, 16, g.integers(0, 256, 256, dtype=np.uint8).tobytes()),
+                     (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
+            n = int(g.choice([1, 64, 65, 777, 4099]))
+            pk = g.integers(0, 256, (n, 64), dtype=np.uint8)
+            op = pyoracle.OracleProgram(code, rel, specs, semantics=1)
+            want, wf, _, _ = op.run(pk.reshape(-1), n, 64, nthreads=8)
+            faults += int(np.count_nonzero(wf))
+            maps = []
+            for vs, me, d in specs:
+                m = native.Map(env, me, vs)
+                m.fill(d)
+                maps.append(m)
+            p = native.Prog(env, native.patch_relocs(code, rel, [m.handle for m in maps]))
+            try:
+                p.set_semantics(native.SEM_STANDARD)
+                native.set_variant(variant)
+                got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, 64)
+                after = [b"".join(m.lookup(key)[1] for key in range(m.max_entries)) for m in maps]
+            finally:
+                native.set_variant(0)
+                p.destroy()
+                for m in maps:
+                    m.destroy()
+            if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
+                    after[0] == op.map_bytes(0) and after[1] == op.map_bytes(1)):
+                bad.append(k)
+            if k % 100 == 99:
+                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
+        print("loop writes variant %d: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+            variant, a.programs, faults, len(bad), bad[:20], time.time() - t0), flush=True)
+        failed = failed or bool(bad)
+    return failed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=500)
@@ -287,9 +335,12 @@ def main():
     ap.add_argument("--hash", action="store_true", help="hashtable maps (lookups and writes)")
     ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (loops too)")
     ap.add_argument("--mutate", action="store_true", help="randomly edited programs (defined ones)")
+    ap.add_argument("--loopwrites", action="store_true", help="map writes inside loops (standard)")
     a = ap.parse_args()
     env = native.Env()
-    if a.mutate and not a.standard:
+    if a.loopwrites:
+        failed = loop_writes(a, env)
+    elif a.mutate and not a.standard:
         failed = mutated(a, env)
     elif a.standard:
         failed = standard(a, env)
