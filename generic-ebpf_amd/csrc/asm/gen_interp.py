@@ -748,6 +748,19 @@ def h_ldx_gen(z, d, sr):
     return out
 
 
+def dma_lane_offsets(dst, tmp):
+    """dst = lane l's byte offset inside each 1-KB DMA block of a staged group: 64 (l & 15) +
+    16 (l >> 4), so DMA q's lane l fetches chunk l >> 4 of packet 16 q + (l & 15) and the LDS
+    block holds chunk c of its 16 packets as 256 contiguous bytes (packet m at 16 m).  Each DMA
+    instruction still covers its own 1 KB (same cache lines, lanes permuted: the same DMA rate,
+    profiles/r05/staging_layout/), and the staging reads of a chunk by 16 lanes are contiguous:
+    no LDS bank conflicts (in the packets' own layout lanes 64 B apart collide)."""
+    return ["v_bfe_u32 %s, v%d, 4, 4" % (dst, V_L16),
+            "v_bfe_u32 %s, v%d, 8, 2" % (tmp, V_L16),
+            "v_lshlrev_b32 %s, 4, %s" % (tmp, tmp),
+            "v_lshl_or_b32 %s, %s, 6, %s" % (dst, dst, tmp)]
+
+
 def lds_pkt_dwords(base, save_exec=None):
     """Write the lane's 64 staged bytes (v22..v37) into the wave's LDS packet buffer transposed:
     dword c of lane l at S_PKTLDS + 4 l + 256 c (VGPR `base` = S_PKTLDS + 4 l).  The loads at
@@ -2172,8 +2185,9 @@ def routines():
     # the S_T0 bytes at H[0:1] just read into H[2:3]
     L += [".Lr_ovlfix:"] + ovl_fix("L", (H[2], H[3])) + ["s_setpc_b64 %s" % sp(S_LINK)]
     # PREFETCH (staged kernel): LDS-DMA the 4 KB of 64-B packets of group s[S_T0] into this
-    # wave's packet buffer, coalesced (lane l of chunk q loads bytes q*1024 + l*16 ...), lanes
-    # past the batch end masked off.  Clobbers s[64:68], m0, exec.
+    # wave's packet buffer, coalesced (DMA q covers bytes q*1024 .. +1023, its lanes permuted:
+    # dma_lane_offsets), lanes past the batch end masked off.  Clobbers s[64:68], m0, exec,
+    # H[4:5].
     # The lane mask is a VALU compare, so it is computed under exec = all lanes, whatever exec
     # the caller arrives with (a compare under exec = 0 would DMA no chunk)
     L += [".Lr_prefetch:",
@@ -2187,17 +2201,19 @@ def routines():
           "s_lshl_b64 s[64:65], s[64:65], 12",
           "s_add_u32 s64, s64, %s" % s(S_DATA),
           "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
-          "s_mov_b32 s67, %s" % s(S_PKTLDS)]
+          "s_mov_b32 s67, %s" % s(S_PKTLDS)] + dma_lane_offsets(v(H[4]), v(H[5]))
     for qq in range(4):
+        # (lane l's bytes belong to packet 16 qq + (l & 15): inside the batch iff its offset,
+        # 64 (l & 15) + 16 (l >> 4), is below 64 x the block's packets left)
         L += ["s_sub_i32 s68, s66, %d" % (16 * qq),
               "s_max_i32 s68, s68, 0",
               "s_min_u32 s68, s68, 16",
               "s_lshl_b32 s68, s68, 6",
-              "v_cmp_gt_u32_e64 vcc, s68, v%d" % V_L16,
+              "v_cmp_gt_u32_e64 vcc, s68, %s" % v(H[4]),
               "s_mov_b64 exec, vcc",   # (a VALU write of EXEC would need 5 wait states here)
               "s_mov_b32 m0, s67",
               "s_nop 0",
-              "global_load_lds_dwordx4 v%d, s[64:65]%s" % (V_L16, LD_POLICY)]
+              "global_load_lds_dwordx4 %s, s[64:65]%s" % (v(H[4]), LD_POLICY)]
         if qq < 3:
             L += ["s_add_u32 s64, s64, 1024", "s_addc_u32 s65, s65, 0",
                   "s_add_u32 s67, s67, 1024"]
@@ -2508,11 +2524,14 @@ def common_group_code():
           "s_cbranch_scc0 .Lgs_general",
           # staged: this group's packets are (or are being) DMA'd into the packet buffer
           "s_waitcnt vmcnt(0)",
-          "v_lshlrev_b32 %s, 2, v%d" % (v(H[1]), V_L16),
+          # lane p's chunk c at 1024 (p >> 4) + 256 c + 16 (p & 15) (dma_lane_offsets):
+          # 16 p + 3 x (16 p & 0x300), then 256 c per chunk
+          "v_and_b32 %s, 0x300, v%d" % (v(H[1]), V_L16),
+          "v_mad_u32_u24 %s, %s, 3, v%d" % (v(H[1]), v(H[1]), V_L16),
           "v_add_u32 %s, %s, %s" % (v(H[1]), s(S_PKTLDS), v(H[1]))]
     for q in range(4):
         L.append("ds_read_b128 v[%d:%d], %s offset:%d" % (PKT0 + 4 * q, PKT0 + 4 * q + 3,
-                                                          v(H[1]), 16 * q))
+                                                          v(H[1]), 256 * q))
     # next group's DMA: a full group (the common case) inline, with exec = all lanes and the
     # instruction offset stepping both the global and the LDS address (M0 set once); a partial
     # group through the masking routine.  (Keep mode, s7 bit 14: none here; .Lgroup_done
@@ -2533,10 +2552,10 @@ def common_group_code():
           "s_lshl_b32 s64, %s, 12" % s(S_T0),
           "s_add_u32 s64, s64, %s" % s(S_DATA),
           "s_addc_u32 s65, s65, %s" % s(S_DATA + 1),
-          "s_mov_b64 exec, -1",
+          "s_mov_b64 exec, -1"] + dma_lane_offsets(v(H[4]), v(H[5])) + [
           "s_mov_b32 m0, %s" % s(S_PKTLDS),
           "s_nop 0"] + [
-          "global_load_lds_dwordx4 v%d, s[64:65] offset:%d%s" % (V_L16, 1024 * qq, LD_POLICY)
+          "global_load_lds_dwordx4 %s, s[64:65] offset:%d%s" % (v(H[4]), 1024 * qq, LD_POLICY)
           for qq in range(4)] + [
           "s_branch .Lgs_pf_done",
           ".Lgs_pf_slow:"] + call(".Lr_prefetch") + [

@@ -8,7 +8,10 @@
 //   MAP    0 = superblocks of K groups interleaved over waves, 1 = one contiguous range per wave
 //   TR     0 = the DMA's contiguous layout (lane l's packet at 64 l: the staging ds_read_b128 of
 //          64 lanes at a 64-B stride conflict), 1 = chunk-transposed by the DMA itself (lane l
-//          of DMA q loads its packet's 16-B chunk q to 1024 q + 16 l: conflict-free reads)
+//          of DMA q loads its packet's 16-B chunk q to 1024 q + 16 l: conflict-free reads),
+//          2 = permuted inside each DMA's own 1 KB (lane l of DMA q loads chunk l >> 4 of packet
+//          16 q + (l & 15): LDS chunk 64 q + 16 c + m holds packet 16 q + m's chunk c, so the
+//          reads of one chunk by 16 lanes are 256 contiguous bytes)
 // plus waves per CU (workgroups per CU x 4).  Reports Gpkt/s of 64-B packets.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -37,12 +40,13 @@ __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, u
 		uint32_t g = group_at(i);
 		if (g >= ngroups)
 			return;
-		const uint8_t *src = in + (uint64_t)g * 4096 + lane * (TR ? 64 : 16);
+		const uint8_t *src = in + (uint64_t)g * 4096 +
+				     (TR == 2 ? 64 * (lane & 15) + 16 * (lane >> 4) : lane * (TR ? 64 : 16));
 		uint8_t *dst = buf + (i % NB) * 4096;
 #pragma unroll
 		for (int q = 0; q < 4; q++)
-			__builtin_amdgcn_global_load_lds((const void *)(src + q * (TR ? 16 : 1024)), LDS_PTR(dst + q * 1024), 16,
-							 0, LDNT ? 2 : 0);
+			__builtin_amdgcn_global_load_lds((const void *)(src + q * (TR == 1 ? 16 : 1024)), LDS_PTR(dst + q * 1024),
+							 16, 0, LDNT ? 2 : 0);
 	};
 	uint64_t r[K];
 	for (int p = 0; p < NB; p++)
@@ -61,8 +65,14 @@ __global__ void __launch_bounds__(256) k_floor(const uint8_t *__restrict__ in, u
 		else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 		typedef unsigned v4u __attribute__((ext_vector_type(4)));
 		v4u a, b, c, d;
-		const uint32_t la = (uint32_t)(uintptr_t)(buf + (i % NB) * 4096 + lane * (TR ? 16 : 64));
-		if (TR)
+		const uint32_t la = (uint32_t)(uintptr_t)(buf + (i % NB) * 4096 +
+							  (TR == 2 ? 1024 * (lane >> 4) + 16 * (lane & 15) : lane * (TR ? 16 : 64)));
+		if (TR == 2)
+			asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:256\n\t"
+				     "ds_read_b128 %2, %4 offset:512\n\tds_read_b128 %3, %4 offset:768\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=v"(a), "=v"(b), "=v"(c), "=v"(d) : "v"(la) : "memory");
+		else if (TR)
 			asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
 				     "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
 				     "s_waitcnt lgkmcnt(0)"
@@ -157,6 +167,18 @@ int main(int argc, char **argv) {
 			run<1, 8, 2, 1, 0, 0, 1>(in, out, ngroups, npk, cus, 16);
 			run<1, 8, 0, 1, 0, 16, 0>(in, out, ngroups, npk, cus, 16);
 			run<1, 8, 0, 1, 0, 16, 1>(in, out, ngroups, npk, cus, 16);
+		}
+		return 0;
+	}
+	if (argc > 1 && argv[1][0] == 'p') {
+		// round 5: lanes permuted inside each DMA's 1 KB (TR 2) against the DMA's own layout
+		for (int rep = 0; rep < 3; rep++) {
+			run<1, 8, 0, 1, 0, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 0, 2>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 2, 1, 0, 0, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 2, 1, 0, 0, 2>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 16, 0>(in, out, ngroups, npk, cus, 16);
+			run<1, 8, 0, 1, 0, 16, 2>(in, out, ngroups, npk, cus, 16);
 		}
 		return 0;
 	}
