@@ -1060,6 +1060,7 @@ struct emitter {
 			low_bytes(d, sl->reg, z);
 			return;
 		}
+		blk.stack_read = true;
 		if (z == 8) {
 			E.ds(DS_READ2_B32, V_STK, 0, 0, L(d), o / 4, o / 4 + 1);
 			E.wait_lgkm();
@@ -1300,10 +1301,11 @@ struct emitter {
 	unsigned off = 0;
 	void decided(bool taken)
 	{
-		if (off & 16) { // s_mov_b64 vcc, exec | 0
-			E.sop1(0x01, (int)SRC_VCC, opnd{taken ? SRC_EXEC : 128u});
+		if ((off & 16) && taken) { // structured: s_mov_b64 vcc, exec (the split sends every lane)
+			E.sop1(0x01, (int)SRC_VCC, opnd{SRC_EXEC});
 			return;
 		}
+		// (structured and never taken: the code generator only empties the join mask)
 		blk.sdir = taken ? 1 : 0;
 	}
 	void cond_imm(int c, int d, uint64_t K)
@@ -2051,9 +2053,52 @@ cc_compile(const dprog_host &xl, const std::vector<dp_entry> &low, const std::ve
 				if (!out[e].fast &&
 				    ((fam >= AHF_LDXGEN1 && fam <= AHF_STXGEN8) || (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
 				     (fam >= AHF_STGEN1 && fam <= AHF_STGEN8) || fam == AHF_LOOKUPGEN ||
-				     (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8) || is_value_store_fam(fam) ||
-				     fam == AHF_UPDATE || fam == AHF_HDELETE))
+				     is_value_store_fam(fam) || fam == AHF_UPDATE || fam == AHF_HDELETE))
 					needs_pkt = true;
+				// (compiled LDXPKTV reads the packet address too, and so does its spliced slow path)
+				if (fam >= AHF_LDXPKTV1 && fam <= AHF_LDXPKTV8)
+					needs_pkt = true;
+			}
+			// Dead stack stores: when no code of the program can read its stack frame — every
+			// block is one of the families below, stack loads all forwarded from registers,
+			// lookups compiled with their key in a register — the stores into the frame are
+			// never observed, and emit nothing (C4: the key STXW, one LDS write per packet).
+			// Anything that may read the frame (generic or run-time-offset loads, the lookup,
+			// update and delete routines, hashtable probes, counters through pointers, a
+			// copied handler body of a load or a lookup) keeps every store.
+			if (getenv("EBPF_CC_KEEPSTORES") == nullptr) {
+				bool frame_read = false;
+				for (uint32_t e : order) {
+					const int fam = ah_fam[(uint32_t)low[e].handler];
+					const bool pure = (fam >= AHF_A64R_ADD && fam <= AHF_JSET_R) ||
+							  (fam >= AHF_A64I_ADD && fam <= AHF_JSET_I) ||
+							  (fam >= AHF_MOV64R && fam <= AHF_J32SET_I) ||
+							  (fam >= AHF_STXSTK1 && fam <= AHF_STXSTK8) ||
+							  (fam >= AHF_STSTK1 && fam <= AHF_STSTK8) ||
+							  (fam >= AHF_LDXPKTG1 && fam <= AHF_LDXPKTG8) ||
+							  (fam >= AHF_LDXPKC1 && fam <= AHF_LDXPKC8) ||
+							  fam == AHF_LDXPKBE16 || fam == AHF_LDXPKBE32 || fam == AHF_EXIT ||
+							  fam == AHF_FAULT || fam == AHF_NOP || fam == AHF_LOOPINIT ||
+							  fam == AHF_LOOPCNT || fam == AHF_OVLINIT;
+					const bool fast_ok = out[e].fast && !out[e].stack_read &&
+							     ((fam >= AHF_LDXMAP1 && fam <= AHF_LDXMAP8) ||
+							      (fam >= AHF_LDXSTK1 && fam <= AHF_LDXSTK8) || fam == AHF_LOOKUPSTK);
+					if (!pure && !fast_ok) {
+						frame_read = true;
+						break;
+					}
+				}
+				if (!frame_read)
+					for (uint32_t e : order) {
+						const int fam = ah_fam[(uint32_t)low[e].handler];
+						if ((fam >= AHF_STXSTK1 && fam <= AHF_STXSTK8) ||
+						    (fam >= AHF_STSTK1 && fam <= AHF_STSTK8)) {
+							out[e].fast = true;
+							out[e].body.clear();
+							out[e].splice_h = -1;
+							out[e].reads = 0;
+						}
+					}
 			}
 			if (xl.start < n) {
 				cc_prologue(mode, live_start, needs_pkt, structured, out[xl.start].prologue);

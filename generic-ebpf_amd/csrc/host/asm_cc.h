@@ -21,6 +21,7 @@ struct cc_block {
 	std::vector<uint8_t> prologue;
 	std::vector<uint8_t> hoist; // general kernels: packet loads issued ahead for this straight run
 	int8_t sdir = -1; // conditional decided at compile time: 0 never taken, 1 always taken
+	bool stack_read = false; // the fast body reads the lane's stack frame (an unforwarded LDX)
 	// a fast body with a slow path: the interpreter's handler body `splice_h` (its operands
 	// s10, s11 = splice_sval, then an lgkmcnt(0) wait) is inserted at body offset splice_at, and
 	// the s_branches at body offsets splice_br[] (over the slow path; ~0 = none) grow by the

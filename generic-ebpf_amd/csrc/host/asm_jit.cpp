@@ -417,7 +417,9 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				sz += 4;
 		}
 		*body_end = sz;
-		if (structured && (ah_flags[h] & 1)) {
+		if (structured && (ah_flags[h] & 1) && cb[e].sdir == 0) {
+			sz += 4; // s_mov_b64 s[Tk], 0: no lane takes it
+		} else if (structured && (ah_flags[h] & 1)) {
 			sz += long_cond[e] ? 12 + LJ : 12;
 		} else if (ah_flags[h] & 1) {
 			if (cb[e].sdir < 0 && rev_cond[e])
@@ -458,7 +460,7 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 					long_join[e] = 1;
 					changed = true;
 				}
-				if ((ah_flags[h] & 1) && !long_cond[e] &&
+				if ((ah_flags[h] & 1) && !long_cond[e] && cb[e].sdir != 0 &&
 				    !fits_simm16((int64_t)pos[xl.entries[e].target] - (int64_t)(pos[e] + be + 12))) {
 					long_cond[e] = 1;
 					changed = true;
@@ -616,7 +618,12 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 				at += 4;
 			}
 		}
-		if (structured && (ah_flags[h] & 1)) {
+		if (structured && (ah_flags[h] & 1) && cb[e].sdir == 0) {
+			// decided at compile time, never taken: the taken block's join finds no lane
+			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[e];
+			put32(at, 0xbe800000u | (sk << 16) | (0x01u << 8) | 128u); // s_mov_b64 s[Tk], 0
+			at += 4;
+		} else if (structured && (ah_flags[h] & 1)) {
 			// s_and_b64 s[Tk], vcc, exec; s_andn2_b64 exec, exec, vcc; s_cbranch_execz join
 			const uint32_t sk = AH_S_JOIN + 2 * (uint32_t)jdepth[e];
 			put32(at, 0x80000000u | (0x0du << 23) | (sk << 16) | (126u << 8) | 106u);

@@ -126,14 +126,15 @@ def test_optimised_c4_instruction_forms(native, env):
         "v_mad_u64_u32 v[16:17], s[60:61], v16, s13, v[48:49]",
         # XOR64 r8, imm with a zero high word: low half only
         "v_xor_b32_e32 v16, 0x5bd1e995, v16",
-        # STXW [r10-4] = r6: one LDS store, offset folded
-        "ds_write_b32 v42, v12",
         # lookup(map, key = r6 < 256 = max_entries) cannot fail: its NULL check is gone and the
         # value load reads the LDS copy of the map at lds_off + key * 8
         "v_mad_u32_u24 v46, v12, 8, s13", "ds_read2_b32 v[12:13], v46 offset1:1",
     ]
     for w in want:
         assert w in lines, (w, "\n".join(lines[:80]))
+    # STXW [r10-4] = r6 (the key): nothing reads the frame afterwards (the lookup takes the key
+    # from r6), so the store is dead and emits nothing (round 5)
+    assert not any(ln.startswith("ds_write") for ln in lines), "\n".join(lines)
     # dead code: r1 = map handle (LDDW) and r2 = r10 - 4 are only the statically resolved
     # lookup's arguments
     assert "v_mov_b64_e32 v[4:5], v[20:21]" not in lines
