@@ -186,11 +186,18 @@ struct dp_launch {
 	// has value-store sites; bit 2 (DP_VF_EXTENTS) = `offsets` holds (start, end) pairs
 	// (EBPF_BATCH_EXTENTS); bits 8..15 = the overlay's entries per lane
 	uint32_t vflags;
-	uint32_t reserved5[4];
+	// staged kernels with result bursts: write phasing (gen_interp.py store_phased).  A wave keeps
+	// its finished groups' results in registers and writes them while the GPU's constant clock
+	// (s_memrealtime) is in a write window — (t mod 2^bits 16..20) < bits 0..15 — or when its
+	// slots are full, so that result writes and packet reads reach HBM in separate phases.
+	// 0 = off: results written once per superblock
+	uint32_t wphase;
+	uint32_t reserved5[3];
 	void *reserved6;
 };
 static_assert(sizeof(dp_launch) == 232, "dp_launch layout is shared with the assembly kernels");
 static_assert(offsetof(dp_launch, vflags) == 0xcc, "gen_interp.py VFLAGS_OFF");
+static_assert(offsetof(dp_launch, wphase) == 0xd0, "gen_interp.py WPHASE_OFF");
 
 // The lane's LDS stack slice, below the frame the program addresses: the loop count (+0), the
 // overlay's entry count (+4), an 8-byte scratch a store into a map value is redirected to (+8),
