@@ -14,7 +14,7 @@
 
 template <int R>
 __global__ void __launch_bounds__(256) k_phase(const uint8_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t ngroups,
-					       uint32_t nwaves_total, uint32_t pmask, uint32_t win, uint32_t *stats) {
+					       uint32_t nwaves_total, uint32_t pmask, uint32_t win, uint32_t *stats, int hold) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
 	const int lane = threadIdx.x & 63;
 	const int wave = threadIdx.x >> 6;
@@ -72,6 +72,10 @@ __global__ void __launch_bounds__(256) k_phase(const uint8_t *__restrict__ in, u
 		if ((t & pmask) < win) {
 			windows++;
 			flush();
+			// HOLD: no packet reads inside the window (write-only phases)
+			if (hold)
+				while (((uint32_t)__builtin_amdgcn_s_memrealtime() & pmask) < win)
+					__builtin_amdgcn_s_sleep(2);
 		} else if (p == R) {
 			forced++;
 			flush();
@@ -88,7 +92,7 @@ __global__ void __launch_bounds__(256) k_phase(const uint8_t *__restrict__ in, u
 static uint32_t *stats;
 
 template <int R>
-void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int wpc, uint32_t pmask, uint32_t win) {
+void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int wpc, uint32_t pmask, uint32_t win, int hold = 0) {
 	const int lds = 4 * (4096 + R * 512);
 	const int wg_per_cu = wpc / 4;
 	if (lds * wg_per_cu > 160 * 1024) {
@@ -99,23 +103,23 @@ void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, int w
 	hipEvent_t a, b;
 	(void)hipEventCreate(&a);
 	(void)hipEventCreate(&b);
-	for (int it = 0; it < 3; it++) k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, nullptr);
+	for (int it = 0; it < 3; it++) k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, nullptr, hold);
 	(void)hipEventRecord(a);
-	for (int it = 0; it < 10; it++) k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, nullptr);
+	for (int it = 0; it < 10; it++) k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, nullptr, hold);
 	(void)hipEventRecord(b);
 	(void)hipEventSynchronize(b);
 	float ms;
 	(void)hipEventElapsedTime(&ms, a, b);
 	ms /= 10;
 	(void)hipMemset(stats, 0, 8);
-	k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, stats);
+	k_phase<R><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win, stats, hold);
 	uint32_t h[2];
 	(void)hipMemcpy(h, stats, 8, hipMemcpyDeviceToHost);
-	printf("R=%2d waves/CU=%d period=%5u ticks window=%4u: %.4f ms  %.1f Gpkt/s  (forced flushes %u, window flushes %u)\n", R,
+	printf("hold=%d R=%2d waves/CU=%d period=%5u ticks window=%4u: %.4f ms  %.1f Gpkt/s  (forced flushes %u, window flushes %u)\n", hold, R,
 	       wpc, pmask + 1, win, ms, npk / ms / 1e6, h[0], h[1]);
 }
 
-int main() {
+int main(int argc, char **argv) {
 	const uint64_t npk = 1ull << 26;
 	const uint32_t ngroups = npk / 64;
 	uint8_t *in;
@@ -125,6 +129,19 @@ int main() {
 		return 1;
 	}
 	(void)hipMemset(in, 1, npk * 64);
+	if (argc > 1 && argv[1][0] == 'h') {
+		// hold: waves issue no packet reads inside the window, against the kernel's way (reads go on)
+		for (int rep = 0; rep < 2; rep++) {
+			run<8>(in, out, ngroups, npk, 16, 0, 0);
+			for (uint32_t w : {640u, 512u})
+				run<8>(in, out, ngroups, npk, 16, 2047, w);
+			for (uint32_t w : {256u, 341u, 512u})
+				run<8>(in, out, ngroups, npk, 16, 2047, w, 1);
+			for (uint32_t w : {128u, 192u, 256u})
+				run<8>(in, out, ngroups, npk, 16, 1023, w, 1);
+		}
+		return 0;
+	}
 	for (int rep = 0; rep < 2; rep++) {
 		run<8>(in, out, ngroups, npk, 16, 0, 0);
 		run<12>(in, out, ngroups, npk, 16, 0, 0);
