@@ -308,3 +308,26 @@ def test_no_vop3_reads_two_sgprs(native, env):
         finally:
             p.destroy()
             m.destroy()
+
+
+def test_write_phasing_code(tmp_path):
+    """Write phasing (gen_interp.py store_phased) is generated into the staged image with result
+    slots only (m1): its shared group code reads the constant clock once (the window check) and
+    marks slots in s98; the general (m0) and interpreter-staged (m3) images have none of it.  The
+    kernels stay within the 102 addressable SGPRs, and the generator's dp_launch.wphase offset
+    matches dprog.h."""
+    import re
+    root = os.path.join(os.path.dirname(__file__), "..", "generic-ebpf_amd", "csrc")
+    out = [str(tmp_path / n) for n in ("m1.s", "m0.s", "m3.s", "h.h")]
+    subprocess.run(["python3", os.path.join(root, "asm", "gen_interp.py")] + out, check=True)
+    m1, m0, m3 = (open(p).read() for p in out[:3])
+    assert m1.count("s_memrealtime") == 1
+    assert "s_bitset1_b32 s98" in m1 and ".Lph_write_g:" in m1
+    for img in (m0, m3):
+        assert "s_memrealtime" not in img and "s98" not in img
+    for img in (m1, m0, m3):
+        assert all(int(x) <= 102 for x in re.findall(r"amdhsa_next_free_sgpr (\d+)", img))
+    gen = open(os.path.join(root, "asm", "gen_interp.py")).read()
+    off = int(re.search(r"WPHASE_OFF = (0x[0-9a-f]+)", gen).group(1), 16)
+    hdr = open(os.path.join(root, "dprog.h")).read()
+    assert "offsetof(dp_launch, wphase) == 0x%x" % off in hdr

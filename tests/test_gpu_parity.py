@@ -333,6 +333,58 @@ def test_superblock_sizes(gpu, env, superblock, monkeypatch):
         np.testing.assert_array_equal(wf, gf)
 
 
+@pytest.mark.parametrize("wphase", ["6,20", "20,1", "4,15"])
+@pytest.mark.parametrize("superblock", [2, 8])
+def test_write_phasing(gpu, env, superblock, wphase, monkeypatch):
+    """Write phasing (gen_interp.py store_phased, dp_launch.wphase) forced on every staged launch:
+    a wave writes its unwritten result slots when the clock is in the window, when the next
+    group's slot is taken, and at the end.  "6,20": windows every 640 ns (both kinds of writes
+    mixed); "20,1": a window once per 10 ms (nearly every write is a full-slot one, so the slots
+    span two superblocks); "4,15": almost always in the window (a write after every group).
+    Ragged batches that end inside a superblock and inside a group, faults included, against
+    the oracle, the fault codes and the histogram."""
+    import torch
+    from generic_ebpf_amd import isa, layout, workloads
+    monkeypatch.setenv("EBPF_SUPERBLOCK", str(superblock))
+    monkeypatch.setenv("EBPF_WPHASE", wphase)
+    lay = workloads.prog_c3()
+    for n in (1, 64 * 5 + 3, 64 * 4096 * superblock * 3 + 64 * 3 + 17):
+        pk = workloads.packets_l2l3(n, 64)
+        c = goldens.Case("c3", lay.code, [], [], pk.reshape(-1), n, 64, None)
+        got, gf, _ = device_run(gpu, env, c, 0)
+        want, wf, _, _ = oracle_run(c, nthreads=8)
+        np.testing.assert_array_equal(want, got)
+        np.testing.assert_array_equal(wf, gf)
+    # faults and the histogram (r0 = pkt[0] / (pkt[1] & 3))
+    I = isa.Insn
+    code = layout.assemble([I("ldxb", 0, 1, 0), I("ldxb", 2, 1, 1), I("and_imm", 2, imm=3),
+                            I("div64_reg", 0, 2), I("exit")]).code
+    n = 64 * 4096 * superblock * 2 + 77
+    pk = workloads.packets_random(n, 64, seed=41)
+    c = goldens.Case("wph", code, [], [], pk.reshape(-1), n, 64, None)
+    want, wf, _, _ = oracle_run(c, nthreads=8)
+    h = np.zeros(257, dtype=np.int64)
+    ok = wf == 0
+    np.add.at(h, np.minimum(want[ok], 255).astype(np.int64), 1)
+    h[256] = int((~ok).sum())
+    p = gpu.Prog(env, code)
+    try:
+        dev = torch.device("cuda:0")
+        d_pk = torch.from_numpy(pk.reshape(-1)).to(dev)
+        d_ret = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        d_flt = torch.zeros(n, dtype=torch.uint8, device=dev)
+        d_hist = torch.zeros(257, dtype=torch.int64, device=dev)
+        p.run_batch_dev(0, d_pk.data_ptr(), n, 64, d_ret.data_ptr(), None, d_flt.data_ptr(),
+                        d_hist.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = d_ret.cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(got[ok], want[ok])
+        np.testing.assert_array_equal(d_flt.cpu().numpy(), wf)
+        np.testing.assert_array_equal(d_hist.cpu().numpy(), h)
+    finally:
+        p.destroy()
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_general_kernels_header_staging(gpu, env, variant):
     """General kernels stage the first 64 bytes of each packet for constant-offset loads: ragged
