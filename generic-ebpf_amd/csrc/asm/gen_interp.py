@@ -118,7 +118,8 @@ JOIN_LEVELS = 12
 # (bit k = slot k), s99 = dp_launch.wphase (store_phased)
 S_PEND = S_JOIN + 2 * JOIN_LEVELS
 S_WPHASE = S_PEND + 1
-NSGPR_STAGED = S_WPHASE + 1
+S_CLOCK = S_WPHASE + 1   # s[100:101]: the constant clock, read at the group's start
+NSGPR_STAGED = S_CLOCK + 2
 # (no join SGPRs in the general image: s74..s97 would overlap the run mask and the short-lane
 # mask, and structured exits address the LDS histogram through lane 0 of v43, which the general
 # image uses for V_IDX; AH_GEN_JOIN stays 0)
@@ -2401,9 +2402,10 @@ def store_phased(tag, final):
     tools/ubench/phase.hip: 0.855 -> 0.773 ms for 64M packets).  The unwritten groups are the
     wave's last |S_PEND| groups, slot k = group & K'-1: slots up to S_PREVG's belong to its
     superblock, the others to the wave's previous one.  Falls through to the superblock burst
-    when wphase is 0; clobbers exec, S_T0..S_T3, S_BYTES, s[60:61], s[64:65], R[0], R[1]."""
+    when wphase is 0; clobbers exec, S_T0..S_T3, S_BYTES, s[60:65], R[0], R[1]."""
     P = s(S_PEND)
-    L = ["s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
+    L = (["s_waitcnt lgkmcnt(0)"] if not final else []) + [   # (the clock read; and see below)
+         "s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
          "s_cbranch_scc1 .Lph_off_%s" % tag,
          "s_cmp_eq_u32 %s, 0" % P,
          "s_cbranch_scc1 .Lsp_none_%s" % tag]
@@ -2412,21 +2414,42 @@ def store_phased(tag, final):
               "s_and_b32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_KMASK)),
               "s_bitcmp1_b32 %s, %s" % (P, s(S_T0)),
               "s_cbranch_scc1 .Lph_write_%s" % tag,
-              "s_memrealtime s[60:61]",
               "s_and_b32 %s, %s, 0x1f0000" % (s(S_T1), s(S_WPHASE)),   # width, offset 0
               "s_and_b32 %s, %s, 0xffff" % (s(S_T2), s(S_WPHASE)),
-              "s_waitcnt lgkmcnt(0)",
-              "s_bfe_u32 %s, s60, %s" % (s(S_T0), s(S_T1)),
+              "s_bfe_u32 %s, %s, %s" % (s(S_T0), s(S_CLOCK), s(S_T1)),
               "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_T2)),
               "s_cbranch_scc0 .Lsp_none_%s" % tag,
               ".Lph_write_%s:" % tag]
     L += ["s_mov_b64 exec, -1",
           "v_lshrrev_b32 %s, 1, v%d" % (v(R[0]), V_L16),                # lane * 8
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16),                # lane
           "s_andn2_b32 %s, %s, %s" % (s(S_T1), s(S_PREVG), s(S_KMASK)),  # S_PREVG's superblock
           "s_add_u32 %s, %s, %s" % (s(S_T2), s(S_GSTRIDE), s(S_KMASK)),
           "s_sub_u32 %s, %s, %s" % (s(S_T2), s(S_T1), s(S_T2)),         # the one before
-          "s_and_b32 %s, %s, %s" % (s(S_T3), s(S_PREVG), s(S_KMASK))]   # S_PREVG's slot
+          "s_and_b32 %s, %s, %s" % (s(S_T3), s(S_PREVG), s(S_KMASK)),   # S_PREVG's slot
+          # every packet of S_PREVG's superblock (and so of the one before) in the batch: no
+          # per-slot bounds (all but a launch's last superblock)
+          "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),
+          "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_T1), s(S_KMASK)),
+          "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
+          "s_cbranch_scc0 .Lph_ragged_%s" % tag]
+    # the two superblocks' result addresses: s[64:65] (S_PREVG's), s[60:61] (the one before; not
+    # used when the wave has none)
+    for lo, g in ((64, S_T1), (60, S_T2)):
+        L += ["s_lshl_b32 s%d, %s, 9" % (lo, s(g)),
+              "s_lshr_b32 s%d, %s, 23" % (lo + 1, s(g)),
+              "s_add_u32 s%d, s%d, %s" % (lo, lo, s(S_RET)),
+              "s_addc_u32 s%d, s%d, %s" % (lo + 1, lo + 1, s(S_RET + 1))]
+    for k in range(RETK):
+        L += ["s_bitcmp1_b32 %s, %d" % (P, k),
+              "s_cbranch_scc0 .Lph_f%d_%s" % (k, tag),
+              "s_cmp_ge_u32 %s, %d" % (s(S_T3), k),
+              "s_cselect_b64 s[62:63], s[64:65], s[60:61]",
+              "global_store_dwordx2 %s, v[%d:%d], s[62:63] offset:%d%s" % (
+                  v(R[0]), V_RB + 2 * k, V_RB + 2 * k + 1, 512 * k, ST_POLICY),
+              ".Lph_f%d_%s:" % (k, tag)]
+    L += ["s_branch .Lph_done_%s" % tag,
+          ".Lph_ragged_%s:" % tag,
+          "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16)]                # lane
     for k in range(RETK):
         L += ["s_bitcmp1_b32 %s, %d" % (P, k),
               "s_cbranch_scc0 .Lph_s%d_%s" % (k, tag),
@@ -2445,7 +2468,8 @@ def store_phased(tag, final):
                                                                 V_RB + 2 * k + 1, ST_POLICY),
               "s_mov_b64 exec, -1",
               ".Lph_s%d_%s:" % (k, tag)]
-    L += ["s_mov_b32 %s, 0" % P,
+    L += [".Lph_done_%s:" % tag,
+          "s_mov_b32 %s, 0" % P,
           "s_branch .Lsp_none_%s" % tag,
           ".Lph_off_%s:" % tag]
     return L
@@ -2593,7 +2617,10 @@ def common_group_code():
           "s_mov_b64 exec, -1",
           "s_cmp_lt_u32 %s, %s" % (s(S_GROUP), s(S_NGROUPS)),
           "s_cbranch_scc0 .Lfinish",
-          ] + lane_index(H[0]) + [
+          ] + (
+          # write phasing: the clock read for store_phased, early so that the group's staging
+          # waits cover its latency
+          ["s_memrealtime s[%d:%d]" % (S_CLOCK, S_CLOCK + 1)] if phased() else []) + lane_index(H[0]) + [
           "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
           ] + [
