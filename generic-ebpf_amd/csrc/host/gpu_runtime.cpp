@@ -1032,17 +1032,20 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 			L.hist_rows = static_cast<uint32_t *>(part);
 			L.hist = static_cast<unsigned long long *>(part);
 		}
-		// a compiled program that probes hashtables is bound by their latency and wants every
-		// wave; the others stream packets at 4 workgroups per CU (asm_runtime.cpp, occupancy).
-		// The interpreter (fn == NULL) is bound by its scalar dispatch and wants every wave too:
-		// C4 1.86 -> 1.42 ms at 6 instead of 4 workgroups per CU (profiles/r02/v2occ).  So is a
-		// program with loops (C3L 0.305 -> 0.277 ms at 6, profiles/r04/c3l_occ)
-		bool probes = ep->xlated->has_loops;
+		// workgroups per CU on the staged kernels (asm_runtime.cpp, occupancy): compiled programs
+		// that only stream packets run 4 (and are the ones write phasing serves); one that probes
+		// hashtables runs 5 (C4H 1.49 -> 1.46 ms against 6, 1.53 at 4, profiles/r05/c4h_occ/).
+		// The interpreter (fn == NULL) is bound by its scalar dispatch and wants every wave: C4
+		// 1.86 -> 1.42 ms at 6 instead of 4 (profiles/r02/v2occ).  So is a program with loops
+		// (C3L 0.305 -> 0.277 ms at 6, profiles/r04/c3l_occ)
+		bool hash = false;
 		for (const dp_map &m : dp->table)
-			probes = probes || (m.flags & DP_MAP_HASH) != 0;
-		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
-				      (mode == 1 && !probes && fn) ? 4u : 0u, ev_start, ev_stop, user_hist,
-				      hist_overwrite);
+			hash = hash || (m.flags & DP_MAP_HASH) != 0;
+		uint32_t wg_cap = 0;
+		if (mode == 1 && fn && !ep->xlated->has_loops)
+			wg_cap = hash ? kProbeWorkgroups : kStreamWorkgroups;
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn, wg_cap, ev_start,
+				      ev_stop, user_hist, hist_overwrite);
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;

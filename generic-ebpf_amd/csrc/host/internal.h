@@ -111,6 +111,11 @@ constexpr uint32_t kHistLds = 1024; // bins 0..255 (bin 256 is counted in global
 constexpr uint32_t kMapLdsBase = kHistLds;
 constexpr uint32_t kMapLdsBudget = 8192;
 constexpr uint32_t kPktLdsPerWG = 4 * 4096;
+// staged kernels, compiled programs: workgroups per CU for streaming programs (write phasing on
+// long launches) and for programs that probe hashtables (gpu_runtime.cpp; the others: as many as
+// LDS and VGPRs allow)
+constexpr uint32_t kStreamWorkgroups = 4;
+constexpr uint32_t kProbeWorkgroups = 5;
 
 // The assembly interpreter's code objects (build/asm_image.cpp): mode 1 = staged 64-B kernels,
 // mode 0 = general kernels.  Image 3 is mode 1 for the interpreter itself (variant 2): one
