@@ -72,10 +72,13 @@ HIST_TICKET_OFF = HIST_REPLICAS * HIST_REPLICA_BYTES
 
 
 def set_retk(k):
-    global RETK, V_RB, NVGPR
+    global RETK, V_RB, NVGPR, SLOTS
     RETK = k
     V_RB = 44 if RETK == 1 else 64
     NVGPR = 64 if RETK == 1 else 64 + 2 * RETK
+    # result slots: RETK, and 16 in the staged image with result bursts, whose wide kernel
+    # (ebpf_jit_s64w) allocates the second 8 for write phasing (store_phased)
+    SLOTS = 16 if RETK == 8 else RETK
 
 
 set_retk(RETK_STAGED)
@@ -2231,6 +2234,9 @@ def routines():
 def kernel(name, staged, jit=False):
     k = "K%s%s" % ("s" if staged else "g", "j" if jit else "")
     L = [".globl %s" % name, ".p2align 8", ".type %s,@function" % name, "%s:" % name]
+    if name == "ebpf_jit_s64" and phased() and SLOTS == 16:
+        # the wide kernel: the same code with 16 result slots allocated (store_phased)
+        L += [".globl ebpf_jit_s64w", ".type ebpf_jit_s64w,@function", "ebpf_jit_s64w:"]
     # v0 = workitem id; wave index within the 256-lane workgroup
     L += ["v_readfirstlane_b32 %s, v0" % s(S_WAVE),
           "s_lshr_b32 %s, %s, 6" % (s(S_WAVE), s(S_WAVE)),
@@ -2382,9 +2388,25 @@ def phased():
 def slot_commit():
     if RETK == 1:
         return []
-    return ["s_mov_b64 exec, -1",
-            "s_and_b32 %s, %s, %s" % (s(S_BYTES), s(S_GROUP), s(S_KMASK))] + (
-           ["s_bitset1_b32 %s, %s" % (s(S_PEND), s(S_BYTES))] if phased() else []) + [
+    L = ["s_mov_b64 exec, -1",
+         "s_and_b32 %s, %s, %s" % (s(S_BYTES), s(S_GROUP), s(S_KMASK))]
+    if phased() and SLOTS == 16:
+        # wide phasing (dp_launch.wphase bit 31, the 96-VGPR kernel): 16 slots, the superblocks
+        # of a wave alternating between slots 0-7 and 8-15 (s98 bit 31 = the running half,
+        # switched at each superblock's first group)
+        L += ["s_cmp_eq_u32 %s, 0" % s(S_BYTES),
+              "s_cbranch_scc0 .Lsc_half",
+              "s_bitcmp1_b32 %s, 31" % s(S_WPHASE),
+              "s_cbranch_scc0 .Lsc_half",
+              "s_xor_b32 %s, %s, 0x80000000" % (s(S_PEND), s(S_PEND)),
+              ".Lsc_half:",
+              "s_lshr_b32 %s, %s, 28" % (s(S_T0), s(S_PEND)),
+              "s_and_b32 %s, %s, 8" % (s(S_T0), s(S_T0)),
+              "s_or_b32 %s, %s, %s" % (s(S_BYTES), s(S_BYTES), s(S_T0)),
+              "s_bitset1_b32 %s, %s" % (s(S_PEND), s(S_BYTES))]
+    elif phased():
+        L.append("s_bitset1_b32 %s, %s" % (s(S_PEND), s(S_BYTES)))
+    return L + [
             "s_lshl_b32 %s, %s, 1" % (s(S_BYTES), s(S_BYTES)),
             "s_set_gpr_idx_on %s, gpr_idx(DST)" % s(S_BYTES),
             "v_mov_b32 v%d, v%d" % (V_RB, V_RES),
@@ -2394,24 +2416,37 @@ def slot_commit():
 
 def store_phased(tag, final):
     """Write phasing (dp_launch.wphase != 0, staged kernels with result slots): instead of one
-    burst per superblock, a wave writes the slots of all its finished groups (S_PEND) when the
-    GPU's constant clock is inside the write window, when the next group's slot still holds an
-    unwritten group (all slots full), and at the end (`final`).  Every wave reads the same 100-MHz
-    counter, so the result writes of the whole GPU bunch into the windows and the packet reads
-    run alone between them: HBM turns between reading and writing far less often (floor kernel,
-    tools/ubench/phase.hip: 0.855 -> 0.773 ms for 64M packets).  The unwritten groups are the
-    wave's last |S_PEND| groups, slot k = group & K'-1: slots up to S_PREVG's belong to its
-    superblock, the others to the wave's previous one.  Falls through to the superblock burst
-    when wphase is 0; clobbers exec, S_T0..S_T3, S_BYTES, s[60:65], R[0], R[1]."""
+    burst per superblock, a wave writes the slots of all its finished groups (S_PEND bits 0-15)
+    when the GPU's constant clock is inside the write window, when the next group's slot still
+    holds an unwritten group (all slots full), and at the end (`final`).  Every wave reads the same
+    100-MHz counter, so the result writes of the whole GPU bunch into the windows and the packet
+    reads run alone between them: HBM turns between reading and writing far less often (floor
+    kernel, tools/ubench/phase.hip: 0.855 -> 0.773 ms for 64M packets).
+    Slots: slot k = group & K'-1 of the wave's last superblocks; with wphase bit 31 (wide, the
+    96-VGPR kernel) a wave's superblocks alternate between slots 0-7 and 8-15 (s98 bit 31 = the
+    half of S_PREVG's superblock), so 16 groups fit (0.770 -> 0.753 ms, tools/ubench/phase2.hip).
+    An unwritten slot of S_PREVG's half belongs to its superblock (index <= S_PREVG's) or to the
+    one `back` (index above: two superblocks back when wide, one otherwise); a slot of the other
+    half to the previous superblock.  Falls through to the superblock burst when wphase is 0;
+    clobbers exec, S_T0..S_T3, S_BYTES, s[60:69], R[0], R[1]."""
     P = s(S_PEND)
-    L = (["s_waitcnt lgkmcnt(0)"] if not final else []) + [   # (the clock read; and see below)
+    L = (["s_waitcnt lgkmcnt(0)"] if not final else []) + [   # (the clock read)
          "s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
          "s_cbranch_scc1 .Lph_off_%s" % tag,
-         "s_cmp_eq_u32 %s, 0" % P,
-         "s_cbranch_scc1 .Lsp_none_%s" % tag]
+         "s_and_b32 %s, %s, 0xffff" % (s(S_T0), P),
+         "s_cbranch_scc0 .Lsp_none_%s" % tag]                   # nothing unwritten
     if not final:
         L += [# the next group's slot is taken: write now
               "s_and_b32 %s, %s, %s" % (s(S_T0), s(S_GROUP), s(S_KMASK)),
+              "s_lshr_b32 %s, %s, 28" % (s(S_T1), P),
+              "s_and_b32 %s, %s, 8" % (s(S_T1), s(S_T1)),
+              "s_cmp_eq_u32 %s, 0" % s(S_T0),
+              "s_cbranch_scc0 .Lph_nf_%s" % tag,
+              "s_bitcmp1_b32 %s, 31" % s(S_WPHASE),
+              "s_cbranch_scc0 .Lph_nf_%s" % tag,
+              "s_xor_b32 %s, %s, 8" % (s(S_T1), s(S_T1)),           # (a new superblock's half)
+              ".Lph_nf_%s:" % tag,
+              "s_or_b32 %s, %s, %s" % (s(S_T0), s(S_T0), s(S_T1)),
               "s_bitcmp1_b32 %s, %s" % (P, s(S_T0)),
               "s_cbranch_scc1 .Lph_write_%s" % tag,
               "s_and_b32 %s, %s, 0x1f0000" % (s(S_T1), s(S_WPHASE)),   # width, offset 0
@@ -2422,54 +2457,79 @@ def store_phased(tag, final):
               ".Lph_write_%s:" % tag]
     L += ["s_mov_b64 exec, -1",
           "v_lshrrev_b32 %s, 1, v%d" % (v(R[0]), V_L16),                # lane * 8
-          "s_andn2_b32 %s, %s, %s" % (s(S_T1), s(S_PREVG), s(S_KMASK)),  # S_PREVG's superblock
-          "s_add_u32 %s, %s, %s" % (s(S_T2), s(S_GSTRIDE), s(S_KMASK)),
-          "s_sub_u32 %s, %s, %s" % (s(S_T2), s(S_T1), s(S_T2)),         # the one before
-          "s_and_b32 %s, %s, %s" % (s(S_T3), s(S_PREVG), s(S_KMASK)),   # S_PREVG's slot
-          # every packet of S_PREVG's superblock (and so of the one before) in the batch: no
-          # per-slot bounds (all but a launch's last superblock)
-          "s_lshr_b32 %s, %s, 6" % (s(S_BYTES), s(S_COUNT)),
-          "s_add_u32 %s, %s, %s" % (s(S_T0), s(S_T1), s(S_KMASK)),
-          "s_cmp_lt_u32 %s, %s" % (s(S_T0), s(S_BYTES)),
+          "s_andn2_b32 %s, %s, %s" % (s(S_T1), s(S_PREVG), s(S_KMASK)),  # cur: S_PREVG's superblock
+          "s_add_u32 %s, %s, %s" % (s(S_T2), s(S_GSTRIDE), s(S_KMASK)),  # superblock stride
+          "s_sub_u32 %s, %s, %s" % (s(S_T0), s(S_T1), s(S_T2)),         # prev: the one before
+          "s_bitcmp1_b32 %s, 31" % s(S_WPHASE),
+          "s_cselect_b32 %s, %s, 0" % (s(S_T2), s(S_T2)),
+          "s_sub_u32 %s, %s, %s" % (s(S_T2), s(S_T0), s(S_T2)),         # back
+          "s_and_b32 %s, %s, %s" % (s(S_T3), s(S_PREVG), s(S_KMASK)),   # S_PREVG's slot index
+          # every packet of cur (and so of the older ones) in the batch: no per-slot bounds (all
+          # but a launch's last superblock)
+          "s_lshr_b32 s66, %s, 6" % s(S_COUNT),
+          "s_add_u32 s67, %s, %s" % (s(S_T1), s(S_KMASK)),
+          "s_cmp_lt_u32 s67, s66",
           "s_cbranch_scc0 .Lph_ragged_%s" % tag]
-    # the two superblocks' result addresses: s[64:65] (S_PREVG's), s[60:61] (the one before; not
-    # used when the wave has none)
-    for lo, g in ((64, S_T1), (60, S_T2)):
+    # result addresses of cur, prev and back: s[60:61], s[62:63], s[64:65]
+    for lo, g in ((60, S_T1), (62, S_T0), (64, S_T2)):
         L += ["s_lshl_b32 s%d, %s, 9" % (lo, s(g)),
               "s_lshr_b32 s%d, %s, 23" % (lo + 1, s(g)),
               "s_add_u32 s%d, s%d, %s" % (lo, lo, s(S_RET)),
               "s_addc_u32 s%d, s%d, %s" % (lo + 1, lo + 1, s(S_RET + 1))]
-    for k in range(RETK):
-        L += ["s_bitcmp1_b32 %s, %d" % (P, k),
-              "s_cbranch_scc0 .Lph_f%d_%s" % (k, tag),
-              "s_cmp_ge_u32 %s, %d" % (s(S_T3), k),
-              "s_cselect_b64 s[62:63], s[64:65], s[60:61]",
-              "global_store_dwordx2 %s, v[%d:%d], s[62:63] offset:%d%s" % (
-                  v(R[0]), V_RB + 2 * k, V_RB + 2 * k + 1, 512 * k, ST_POLICY),
-              ".Lph_f%d_%s:" % (k, tag)]
-    L += ["s_branch .Lph_done_%s" % tag,
-          ".Lph_ragged_%s:" % tag,
-          "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16)]                # lane
-    for k in range(RETK):
-        L += ["s_bitcmp1_b32 %s, %d" % (P, k),
-              "s_cbranch_scc0 .Lph_s%d_%s" % (k, tag),
-              "s_cmp_ge_u32 %s, %d" % (s(S_T3), k),
-              "s_cselect_b32 %s, %s, %s" % (s(S_BYTES), s(S_T1), s(S_T2)),
-              "s_add_u32 %s, %s, %d" % (s(S_BYTES), s(S_BYTES), k),     # the slot's group
-              "s_lshl_b32 %s, %s, 6" % (s(S_T0), s(S_BYTES)),
-              "s_sub_u32 %s, %s, %s" % (s(S_T0), s(S_COUNT), s(S_T0)),  # its packets (> 0)
-              "v_cmp_gt_u32_e64 vcc, %s, %s" % (s(S_T0), v(R[1])),
-              "s_mov_b64 exec, vcc",
-              "s_lshl_b32 s64, %s, 9" % s(S_BYTES),
-              "s_lshr_b32 s65, %s, 23" % s(S_BYTES),
-              "s_add_u32 s64, s64, %s" % s(S_RET),
-              "s_addc_u32 s65, s65, %s" % s(S_RET + 1),
-              "global_store_dwordx2 %s, v[%d:%d], s[64:65]%s" % (v(R[0]), V_RB + 2 * k,
-                                                                V_RB + 2 * k + 1, ST_POLICY),
-              "s_mov_b64 exec, -1",
-              ".Lph_s%d_%s:" % (k, tag)]
+    halves = [0] if RETK == SLOTS else [0, 1]
+
+    def slots_of(half, ragged):
+        """The writes for S_PREVG's half `half`: its own slots, then the other half's."""
+        out = []
+        for own in (True, False):
+            h = half if own else 1 - half
+            if h not in halves:
+                continue
+            for i in range(RETK):
+                j = 8 * h + i
+                sk = ".Lph_%s%d_%d_%s" % ("r" if ragged else "f", half, j, tag)
+                out += ["s_bitcmp1_b32 %s, %d" % (P, j), "s_cbranch_scc0 %s" % sk]
+                if not ragged:
+                    if own:
+                        out += ["s_cmp_ge_u32 %s, %d" % (s(S_T3), i),
+                                "s_cselect_b64 s[66:67], s[60:61], s[64:65]"]
+                    out.append("global_store_dwordx2 %s, v[%d:%d], s[%d:%d] offset:%d%s" % (
+                        v(R[0]), V_RB + 2 * j, V_RB + 2 * j + 1, 66 if own else 62,
+                        67 if own else 63, 512 * i, ST_POLICY))
+                else:
+                    if own:
+                        out += ["s_cmp_ge_u32 %s, %d" % (s(S_T3), i),
+                                "s_cselect_b32 %s, %s, %s" % (s(S_BYTES), s(S_T1), s(S_T2))]
+                    else:
+                        out.append("s_mov_b32 %s, %s" % (s(S_BYTES), s(S_T0)))
+                    out += ["s_add_u32 %s, %s, %d" % (s(S_BYTES), s(S_BYTES), i),   # the group
+                            "s_lshl_b32 s66, %s, 6" % s(S_BYTES),
+                            "s_sub_u32 s66, %s, s66" % s(S_COUNT),                 # its packets
+                            "v_cmp_gt_u32_e64 vcc, s66, %s" % v(R[1]),
+                            "s_mov_b64 exec, vcc",
+                            "s_lshl_b32 s66, %s, 9" % s(S_BYTES),
+                            "s_lshr_b32 s67, %s, 23" % s(S_BYTES),
+                            "s_add_u32 s66, s66, %s" % s(S_RET),
+                            "s_addc_u32 s67, s67, %s" % s(S_RET + 1),
+                            "global_store_dwordx2 %s, v[%d:%d], s[66:67]%s" % (
+                                v(R[0]), V_RB + 2 * j, V_RB + 2 * j + 1, ST_POLICY),
+                            "s_mov_b64 exec, -1"]
+                out.append(sk + ":")
+        return out
+
+    for ragged in (False, True):
+        if ragged:
+            L += [".Lph_ragged_%s:" % tag,
+                  "v_lshrrev_b32 %s, 4, v%d" % (v(R[1]), V_L16)]            # lane
+        if len(halves) > 1:
+            L += ["s_bitcmp1_b32 %s, 31" % P,
+                  "s_cbranch_scc1 .Lph_%sh1_%s" % ("r" if ragged else "f", tag)]
+        L += slots_of(0, ragged) + ["s_branch .Lph_done_%s" % tag]
+        if len(halves) > 1:
+            L += [".Lph_%sh1_%s:" % ("r" if ragged else "f", tag)] + slots_of(1, ragged) + [
+                  "s_branch .Lph_done_%s" % tag]
     L += [".Lph_done_%s:" % tag,
-          "s_mov_b32 %s, 0" % P,
+          "s_and_b32 %s, %s, 0x80000000" % (P, P),                  # (keeps the half)
           "s_branch .Lsp_none_%s" % tag,
           ".Lph_off_%s:" % tag]
     return L
@@ -3078,6 +3138,8 @@ def main():
                             % RETK_STAGED,
                             "#define AH_NVGPR_STAGED %d" % (64 if RETK_STAGED == 1 else 64 + 2 * RETK_STAGED),
                             "#define AH_RET_GROUPS_GENERAL 1",
+                            "#define AH_NVGPR_STAGED_WIDE %d  // ebpf_jit_s64w: 16 result slots "
+                            "(write phasing), 0 = none" % (96 if RETK_STAGED == 8 else 0),
                             "#define AH_NVGPR_GENERAL %d" % (64 + GEN_HOIST_REGS),
                             "#define AH_NVGPR_INTERP %d  // the interpreter's staged image (m3)"
                             % (64 if RETK_INTERP == 1 else 64 + 2 * RETK_INTERP),
@@ -3181,7 +3243,9 @@ def generate(out_s, staged_image):
         code = ln.split(";")[0].split("//")[0]
         for a, b, c in re.findall(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]", code):
             vtop = max(vtop, int(a or c))
-    assert vtop < NVGPR, "image code uses v%d, the kernels allocate %d VGPRs" % (vtop, NVGPR)
+    vwide = V_RB + 2 * SLOTS if (staged_image and SLOTS == 16) else NVGPR
+    assert vtop < max(NVGPR, vwide), "image code uses v%d, the kernels allocate %d VGPRs" % (
+        vtop, max(NVGPR, vwide))
     kernarg = 232
     nsg = NSGPR_STAGED if (staged_image or GEN_JOIN) else NSGPR_GEN
     if INTERP_IMAGE:
@@ -3196,6 +3260,8 @@ def generate(out_s, staged_image):
           ("ebpf_jit_s64", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_jit_gen", kernarg, 0, NVGPR, nsg, 256),
           ("ebpf_asm_link", 16, 0, 16, 16, 64)]
+    if vwide > NVGPR:
+        ks.append(("ebpf_jit_s64w", kernarg, 0, vwide, nsg, 256))
     for name, ka, lds, vg, sg, wg in ks:
         A += kd(name, lds, vg, sg, ka, wg)
     md = metadata(ks)

@@ -743,7 +743,8 @@ asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 // module and its kernel.
 int
 asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-	      void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err)
+	      void **mod_out, void **fn_out, void **fn_wide_out, uint32_t *stack_stride,
+	      std::string *err)
 {
 	std::vector<unsigned char> img;
 	int e = asm_jit_emit(xl, mode, table, &img, nullptr, stack_stride, err);
@@ -762,8 +763,15 @@ asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_m
 		*err = "compiled program kernel missing";
 		return EIO;
 	}
+	// the staged image's wide kernel (16 result slots for write phasing), where it has one
+	hipFunction_t fw = nullptr;
+	if (fn_wide_out && mode == 1 && AH_NVGPR_STAGED_WIDE &&
+	    hipModuleGetFunction(&fw, mod, "ebpf_jit_s64w") != hipSuccess)
+		fw = nullptr;
 	*mod_out = mod;
 	*fn_out = fn;
+	if (fn_wide_out)
+		*fn_wide_out = fw;
 	return 0;
 }
 

@@ -23,7 +23,7 @@
 hipError_t launch_interp_v0(const dp_launch &L, hipStream_t stream); // interp_v0.hip
 // asm_runtime.cpp
 hipError_t launch_interp_asm(const dp_launch &L, hipStream_t stream, int device, int mode,
-			     uint32_t map_lds_bytes, void *fn, uint32_t stream_cap,
+			     uint32_t map_lds_bytes, void *fn, void *fn_wide, uint32_t stream_cap,
 			     hipEvent_t ev_start, hipEvent_t ev_stop, unsigned long long *user_hist,
 			     bool hist_overwrite);
 int asm_available(int device);
@@ -37,7 +37,7 @@ int asm_build_entries(int device, const dprog_host &xl, int mode, const std::vec
 		      dp_entry **d_out, uint32_t *stack_stride, std::string *err);
 // asm_jit.cpp
 int asm_jit_build(int device, const dprog_host &xl, int mode, const std::vector<dp_map> &table,
-		  void **mod_out, void **fn_out, uint32_t *stack_stride, std::string *err);
+		  void **mod_out, void **fn_out, void **fn_wide_out, uint32_t *stack_stride, std::string *err);
 void asm_jit_release(void *mod);
 int asm_jit_emit(const dprog_host &xl, int mode, const std::vector<dp_map> &table,
 		 std::vector<unsigned char> *img_out, std::vector<unsigned char> *code,
@@ -605,7 +605,8 @@ jit_entries(struct ebpf_prog *ep, dprog_device *dp, int mode)
 	std::string msg;
 	const auto t0 = std::chrono::steady_clock::now();
 	int err = asm_jit_build(dp->device, *ep->xlated, mode, dp->table, &dp->jit_mod[mode],
-				&dp->jit_fn[mode], &dp->jit_stride[mode], &msg);
+				&dp->jit_fn[mode], mode == 1 ? &dp->jit_fn_wide : nullptr,
+				&dp->jit_stride[mode], &msg);
 	dp->build_ms[mode] =
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 	if (err) {
@@ -1044,8 +1045,9 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		uint32_t wg_cap = 0;
 		if (mode == 1 && fn && !ep->xlated->has_loops)
 			wg_cap = hash ? kProbeWorkgroups : kStreamWorkgroups;
-		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn, wg_cap, ev_start,
-				      ev_stop, user_hist, hist_overwrite);
+		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
+				      fn ? dp->jit_fn_wide : nullptr, wg_cap, ev_start, ev_stop, user_hist,
+				      hist_overwrite);
 	} else {
 		L.prog = dp->d_entries;
 		dp->last_exec = EBPF_EXEC_HIP;

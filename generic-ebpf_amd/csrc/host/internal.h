@@ -151,6 +151,7 @@ struct dprog_device {
 	int asm_err[kModes] = {};
 	void *jit_mod[kModes] = {};              // variant 0: compiled program module, per mode
 	void *jit_fn[kModes] = {};               // its kernel
+	void *jit_fn_wide = nullptr;             // mode 1: the same code with 16 result slots
 	uint32_t jit_stride[kModes] = {};
 	int jit_err[kModes] = {};                // E2BIG etc.: run the interpreter instead
 	double build_ms[kModes] = {};            // compile (variant 0) or lower + link time, per mode

@@ -327,6 +327,10 @@ def test_write_phasing_code(tmp_path):
         assert "s_memrealtime" not in img and "s98" not in img
     for img in (m1, m0, m3):
         assert all(int(x) <= 102 for x in re.findall(r"amdhsa_next_free_sgpr (\d+)", img))
+    # the wide kernel: the staged compiled kernel's code with 96 VGPRs (16 result slots)
+    assert "ebpf_jit_s64w:" in m1 and "ebpf_jit_s64w" not in m0 + m3
+    kds = dict(re.findall(r"\.amdhsa_kernel (\w+)\n(?:.*\n)*?\s*\.amdhsa_next_free_vgpr (\d+)", m1))
+    assert kds["ebpf_jit_s64w"] == "96" and kds["ebpf_jit_s64"] == "80"
     gen = open(os.path.join(root, "asm", "gen_interp.py")).read()
     off = int(re.search(r"WPHASE_OFF = (0x[0-9a-f]+)", gen).group(1), 16)
     hdr = open(os.path.join(root, "dprog.h")).read()

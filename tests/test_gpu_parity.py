@@ -333,14 +333,16 @@ def test_superblock_sizes(gpu, env, superblock, monkeypatch):
         np.testing.assert_array_equal(wf, gf)
 
 
-@pytest.mark.parametrize("wphase", ["6,20", "20,1", "4,15"])
+@pytest.mark.parametrize("wphase", ["6,20", "20,1", "4,15", "6,20,16", "20,1,16", "4,15,16"])
 @pytest.mark.parametrize("superblock", [2, 8])
 def test_write_phasing(gpu, env, superblock, wphase, monkeypatch):
     """Write phasing (gen_interp.py store_phased, dp_launch.wphase) forced on every staged launch:
     a wave writes its unwritten result slots when the clock is in the window, when the next
     group's slot is taken, and at the end.  "6,20": windows every 640 ns (both kinds of writes
     mixed); "20,1": a window once per 10 ms (nearly every write is a full-slot one, so the slots
-    span two superblocks); "4,15": almost always in the window (a write after every group).
+    span two superblocks); "4,15": almost always in the window (a write after every group);
+    ",16": the wide kernel's 16 slots (superblocks alternating between two halves, so the
+    unwritten slots span three superblocks).
     Ragged batches that end inside a superblock and inside a group, faults included, against
     the oracle, the fault codes and the histogram."""
     import torch
