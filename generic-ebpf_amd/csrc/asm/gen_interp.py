@@ -2430,9 +2430,9 @@ def store_phased(tag, final):
     half to the previous superblock.  Falls through to the superblock burst when wphase is 0;
     clobbers exec, S_T0..S_T3, S_BYTES, s[60:69], R[0], R[1]."""
     P = s(S_PEND)
-    L = (["s_waitcnt lgkmcnt(0)"] if not final else []) + [   # (the clock read)
-         "s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
-         "s_cbranch_scc1 .Lph_off_%s" % tag,
+    L = ["s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
+         "s_cbranch_scc1 .Lph_off_%s" % tag] + (
+        ["s_waitcnt lgkmcnt(0)"] if not final else []) + [   # (the clock read)
          "s_and_b32 %s, %s, 0xffff" % (s(S_T0), P),
          "s_cbranch_scc0 .Lsp_none_%s" % tag]                   # nothing unwritten
     if not final:
@@ -2680,7 +2680,10 @@ def common_group_code():
           ] + (
           # write phasing: the clock read for store_phased, early so that the group's staging
           # waits cover its latency
-          ["s_memrealtime s[%d:%d]" % (S_CLOCK, S_CLOCK + 1)] if phased() else []) + lane_index(H[0]) + [
+          ["s_cmp_eq_u32 %s, 0" % s(S_WPHASE),
+           "s_cbranch_scc1 .Lgc_noclock",
+           "s_memrealtime s[%d:%d]" % (S_CLOCK, S_CLOCK + 1),
+           ".Lgc_noclock:"] if phased() else []) + lane_index(H[0]) + [
           "v_lshl_add_u32 v%d, %s, 6, %s" % (H[3], s(S_GROUP), v(H[0])),      # packet index
           "v_cmp_gt_u32_e64 %s, %s, v%d" % (sp(S_ALIVE), s(S_COUNT), H[3]),
           ] + [
