@@ -1,3 +1,5 @@
+# (EBPF_NOKEEP was a temporary host switch for this probe, removed after it lost:
+# profiles/r05/c3l_nokeep/README.md)
 # C3L: keep mode (run-time-offset loads from the LDS packet buffer, the next DMA at the group's
 # end) against none (uniform offsets from the packet registers, others from global memory, the
 # next DMA prefetched), x write phasing x 4 / 6 workgroups per CU.  gpurun_out/keep/
