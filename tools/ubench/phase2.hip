@@ -10,7 +10,7 @@
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
 
-template <int R, int K = 8>
+template <int R, int K = 8, int PW = 0>
 __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t ngroups,
 						uint32_t nwaves_total, uint32_t pmask, uint32_t win) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 	};
 	uint64_t r[R];
 	uint32_t pend = 0;
+	int nst = 0; // PW: result stores issued after the newest DMA (waited for only as far as needed)
 	// write every pending slot; slot j holds sequence number base + j (j <= k) or base - R + j
 	auto flush = [&](uint32_t base, int k) {
 #pragma unroll
@@ -36,6 +37,7 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 			if (pend & (1u << j)) {
 				const uint32_t seq = j <= k ? base + j : base - R + j;
 				__builtin_nontemporal_store(r[j], out + (uint64_t)group_at(seq) * 64 + lane);
+				nst++;
 			}
 		pend = 0;
 	};
@@ -53,7 +55,16 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 			}
 			// the slot about to be written still pending: write everything first
 			if (pend & (1u << k)) flush(base, k - 1);
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			if (PW) {
+				// vmcnt retires in order: the DMA is done once at most nst younger stores remain
+#define W(n) case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+				switch (nst < 16 ? nst : 16) {
+				W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15) W(16)
+				}
+#undef W
+			} else {
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			}
 			typedef unsigned v4u __attribute__((ext_vector_type(4)));
 			v4u a, b, c, d;
 			const uint32_t la = (uint32_t)(uintptr_t)(buf + lane * 64);
@@ -62,6 +73,7 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 				     "s_waitcnt lgkmcnt(0)"
 				     : "=v"(a), "=v"(b), "=v"(c), "=v"(d) : "v"(la) : "memory");
 			issue(i + 1);
+			nst = 0;
 			r[k] = (uint64_t)(a.x ^ b.y ^ c.z ^ d.w) | ((uint64_t)(a.w + d.x) << 32);
 			pend |= 1u << k;
 			const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -72,21 +84,21 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 	}
 }
 
-template <int R, int K = 8>
+template <int R, int K = 8, int PW = 0>
 void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, uint32_t pmask, uint32_t win) {
 	const int lds = 4 * 4096, wgs = 256 * 4;
 	hipEvent_t a, b;
 	(void)hipEventCreate(&a);
 	(void)hipEventCreate(&b);
-	for (int it = 0; it < 3; it++) k_phase2<R, K><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
+	for (int it = 0; it < 3; it++) k_phase2<R, K, PW><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
 	(void)hipEventRecord(a);
-	for (int it = 0; it < 10; it++) k_phase2<R, K><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
+	for (int it = 0; it < 10; it++) k_phase2<R, K, PW><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
 	(void)hipEventRecord(b);
 	(void)hipEventSynchronize(b);
 	float ms;
 	(void)hipEventElapsedTime(&ms, a, b);
 	ms /= 10;
-	printf("K=%2d R=%2d period=%5u window=%5u: %.4f ms  %.1f Gpkt/s\n", K, R, pmask + 1, win, ms, npk / ms / 1e6);
+	printf("PW=%d K=%2d R=%2d period=%5u window=%5u: %.4f ms  %.1f Gpkt/s\n", PW, K, R, pmask + 1, win, ms, npk / ms / 1e6);
 }
 
 int main() {
@@ -99,15 +111,12 @@ int main() {
 		return 1;
 	}
 	(void)hipMemset(in, 1, npk * 64);
-	for (int rep = 0; rep < 2; rep++) {
+	for (int rep = 0; rep < 3; rep++) {
 		run<8>(in, out, ngroups, npk, 0, 0);
-		run<8>(in, out, ngroups, npk, 2047, 640);
 		run<16>(in, out, ngroups, npk, 4095, 1024);
-		run<16, 16>(in, out, ngroups, npk, 0, 0);
-		run<16, 16>(in, out, ngroups, npk, 4095, 1024);
-		run<16, 16>(in, out, ngroups, npk, 4095, 1280);
-		run<16, 16>(in, out, ngroups, npk, 4095, 768);
-		run<16, 16>(in, out, ngroups, npk, 2047, 640);
+		run<16, 8, 1>(in, out, ngroups, npk, 4095, 1024);
+		run<16, 8, 1>(in, out, ngroups, npk, 2047, 512);
+		run<8, 8, 1>(in, out, ngroups, npk, 0, 0);
 	}
 	return 0;
 }
