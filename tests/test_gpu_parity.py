@@ -334,7 +334,7 @@ def test_superblock_sizes(gpu, env, superblock, monkeypatch):
 
 
 @pytest.mark.parametrize("wphase", ["6,20", "20,1", "4,15", "6,20,16", "20,1,16", "4,15,16"])
-@pytest.mark.parametrize("superblock", [2, 8])
+@pytest.mark.parametrize("superblock", [2, 4, 8])
 def test_write_phasing(gpu, env, superblock, wphase, monkeypatch):
     """Write phasing (gen_interp.py store_phased, dp_launch.wphase) forced on every staged launch:
     a wave writes its unwritten result slots when the clock is in the window, when the next
