@@ -10,7 +10,7 @@
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
 
-template <int R, int K = 8, int PW = 0>
+template <int R, int K = 8, int PW = 0, int SP = 0, int XS = 0>
 __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t ngroups,
 						uint32_t nwaves_total, uint32_t pmask, uint32_t win) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -36,11 +36,16 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 		for (int j = 0; j < R; j++)
 			if (pend & (1u << j)) {
 				const uint32_t seq = j <= k ? base + j : base - R + j;
-				__builtin_nontemporal_store(r[j], out + (uint64_t)group_at(seq) * 64 + lane);
+				if (SP) out[(uint64_t)group_at(seq) * 64 + lane] = r[j];   // SP: plain stores
+				else __builtin_nontemporal_store(r[j], out + (uint64_t)group_at(seq) * 64 + lane);
 				nst++;
 			}
 		pend = 0;
 	};
+	// XS: each XCD's windows start XS ticks after the previous XCD's
+	uint32_t xcc = 0;
+	if (XS) asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+	const uint32_t tshift = XS * xcc;
 	issue(0);
 	for (uint32_t base = 0;; base += R) {
 		bool done = false;
@@ -76,7 +81,7 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 			nst = 0;
 			r[k] = (uint64_t)(a.x ^ b.y ^ c.z ^ d.w) | ((uint64_t)(a.w + d.x) << 32);
 			pend |= 1u << k;
-			const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+			const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime() + tshift;
 			if (win && (t & pmask) < win) flush(base, k);
 			else if (!win && k == R - 1) flush(base, k);   // no phasing: R-group bursts
 		}
@@ -84,21 +89,21 @@ __global__ void __launch_bounds__(256) k_phase2(const uint8_t *__restrict__ in, 
 	}
 }
 
-template <int R, int K = 8, int PW = 0>
+template <int R, int K = 8, int PW = 0, int SP = 0, int XS = 0>
 void run(const uint8_t *in, uint64_t *out, uint32_t ngroups, uint64_t npk, uint32_t pmask, uint32_t win) {
 	const int lds = 4 * 4096, wgs = 256 * 4;
 	hipEvent_t a, b;
 	(void)hipEventCreate(&a);
 	(void)hipEventCreate(&b);
-	for (int it = 0; it < 3; it++) k_phase2<R, K, PW><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
+	for (int it = 0; it < 3; it++) k_phase2<R, K, PW, SP, XS><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
 	(void)hipEventRecord(a);
-	for (int it = 0; it < 10; it++) k_phase2<R, K, PW><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
+	for (int it = 0; it < 10; it++) k_phase2<R, K, PW, SP, XS><<<wgs, 256, lds>>>(in, out, ngroups, wgs * 4, pmask, win);
 	(void)hipEventRecord(b);
 	(void)hipEventSynchronize(b);
 	float ms;
 	(void)hipEventElapsedTime(&ms, a, b);
 	ms /= 10;
-	printf("PW=%d K=%2d R=%2d period=%5u window=%5u: %.4f ms  %.1f Gpkt/s\n", PW, K, R, pmask + 1, win, ms, npk / ms / 1e6);
+	printf("SP=%d XS=%4d PW=%d K=%2d R=%2d period=%5u window=%5u: %.4f ms  %.1f Gpkt/s\n", SP, XS, PW, K, R, pmask + 1, win, ms, npk / ms / 1e6);
 }
 
 int main() {
@@ -114,9 +119,9 @@ int main() {
 	for (int rep = 0; rep < 3; rep++) {
 		run<8>(in, out, ngroups, npk, 0, 0);
 		run<16>(in, out, ngroups, npk, 4095, 1024);
-		run<16, 8, 1>(in, out, ngroups, npk, 4095, 1024);
-		run<16, 8, 1>(in, out, ngroups, npk, 2047, 512);
-		run<8, 8, 1>(in, out, ngroups, npk, 0, 0);
+		run<16, 8, 0, 1>(in, out, ngroups, npk, 4095, 1024);
+		run<16, 8, 0, 0, 128>(in, out, ngroups, npk, 4095, 1024);
+		run<16, 8, 0, 0, 512>(in, out, ngroups, npk, 4095, 1024);
 	}
 	return 0;
 }
