@@ -1344,7 +1344,10 @@ analyze_writes(dprog_host &out)
 	}
 	out.max_updates = best[out.start];
 	out.ovl_entries = out.vstore_overlay ? 2 * bests[out.start] : 0;
-	out.write_cap = out.max_updates > DP_WRITES_MAX;
+	// A loop-free program's log and overlay are sized by its path counts: every write it reaches
+	// lands, as in the reference (ebpf_interpreter.c:343-366, ebpf_map.c:101-108).  Only a loop
+	// has no per-path bound; its writes are capped (DP_WRITES_MAX)
+	out.write_cap = false;
 	if (out.has_loops) { // (the path counts above do not bound a loop)
 		bool logging = false;
 		for (size_t i = 0; i < n && !logging; i++)

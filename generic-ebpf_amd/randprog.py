@@ -184,6 +184,10 @@ class _Gen:
                     I({4: "stxw", 8: "stxdw"}[size], 0, x, off)]
         return out
 
+    def value_base(self):
+        """stack offset of an update's value: below the key at r10 - 4, inside the stack"""
+        return -8 - (self.vs + 7) // 8 * 8
+
     def update(self):
         """map_update_elem (helper 1) or map_delete_elem (helper 2, EINVAL on an array): key and
         value from the stack, flags 0..3 (3: EINVAL); the return code mixed into a scalar; the
@@ -200,21 +204,82 @@ class _Gen:
         key_mask = self.pick([0x7, 0xff, 0xffffffff])
         out += [I("mov_reg", 7, k), I("and64_imm", 7, imm=isa.s32(key_mask)),
                 I("stxw", 10, 7, -4)]
+        vb = self.value_base()
         for off in range(0, self.vs, 8):
-            out.append(I("stxdw", 10, self.scalar(), -32 + off))
-        for b in list(range(-4, 0)) + list(range(-32, -32 + self.vs)):
+            out.append(I("stxdw", 10, self.scalar(), vb + off))
+        for b in list(range(-4, 0)) + list(range(vb, vb + self.vs)):
             self.stack_ok.add(b)
         out += [LdDw(1, MapRef(self.r(self.nmaps))),
                 I("mov_imm", 2, imm=0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4)]
         if self.r(4) == 0:
             out += [I("call", imm=2)]
         else:
-            out += [I("mov_imm", 3, imm=0), I("mov64_reg", 3, 10), I("add64_imm", 3, imm=-32),
+            out += [I("mov_imm", 3, imm=0), I("mov64_reg", 3, 10), I("add64_imm", 3, imm=vb),
                     I("mov_imm", 4, imm=self.r(4)), I("call", imm=1)]
         dst = self.pick([3, 4, 5, 8, 9])
         out += [I("mov_imm", dst, imm=self.imm()), I("xor64_reg", dst, 0)]
         for r in (1, 2, 3, 4):
             if r != dst:
+                out.append(I("mov_imm", r, imm=self.imm()))
+        return out
+
+    def bulk_writes(self):
+        """More than 16 map writes on one path (a loop-free program has no write limit, as in
+        the reference: ebpf_gpu.h "Map writes in a device batch"): a lookup hit followed by
+        17..60 ST / STX into the value, or 17..40 map_update_elem calls.  Placed last on the
+        main path, after every load of a map value (no read-back: the overlay does not bound
+        the count); the pointer registers become scalars again afterwards."""
+        if self.nmaps == 0:
+            return self.alu()
+        out = []
+        if self.ctx != 6:
+            out += [I("mov_imm", 6, imm=0), I("mov64_reg", 6, self.ctx)]
+            self.ctx = 6
+            self.scalars = [0, 2, 3, 4, 5, 7, 8, 9]
+        src = [3, 4, 5, 8, 9]
+        if self.r(2) == 0:
+            k = self.scalar()
+            out += [I("mov_reg", 7, k), I("and64_imm", 7, imm=self.pick([0x7, 0xff, 0x1ff])),
+                    I("stxw", 10, 7, -4), LdDw(1, MapRef(self.r(self.nmaps))),
+                    I("mov_imm", 2, imm=0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                    I("call", imm=0),
+                    Branch(I("jeq_imm", 0, imm=0), [I("mov_imm", 0, imm=0x55), I("xor64_reg", 0, 7),
+                                                    I("exit")])]
+            for b in range(-4, 0):
+                self.stack_ok.add(b)
+            for _ in range(17 + self.r(44)):
+                size = self.pick([z for z in (1, 2, 4, 8) if z <= self.vs])
+                off = self.r(self.vs - size + 1)
+                if self.r(3) == 0:
+                    out.append(I({1: "stb", 2: "sth", 4: "stw", 8: "stdw"}[size], 0, 0, off, self.imm()))
+                else:
+                    out.append(I({1: "stxb", 2: "stxh", 4: "stxw", 8: "stxdw"}[size], 0,
+                                 self.pick(src), off))
+                if self.r(2) == 0:
+                    out.append(I("add64_imm", self.pick(src), imm=self.imm()))
+            out += [I("mov_imm", 0, imm=self.imm()), I("mov_imm", 1, imm=self.imm()),
+                    I("mov_imm", 2, imm=self.imm())]
+            return out
+        m = self.r(self.nmaps)
+        vb = self.value_base()
+        for b in list(range(-4, 0)) + list(range(vb, vb + self.vs)):
+            self.stack_ok.add(b)
+        for off in range(0, self.vs, 8):
+            out.append(I("stxdw", 10, self.scalar(), vb + off))
+        acc = self.pick([5, 8, 9])   # (r1..r4 are the call's arguments)
+        out += [I("mov_imm", acc, imm=self.imm())]
+        keyreg = self.pick([s for s in src if s != acc])
+        out += [I("mov_reg", 7, keyreg)]
+        for j in range(17 + self.r(24)):
+            out += [I("add_imm", 7, imm=1 + self.r(3)), I("and64_imm", 7, imm=self.pick([0x7, 0x7, 0xf, 0xff])),
+                    I("stxw", 10, 7, -4), I("stxw", 10, acc, vb),
+                    LdDw(1, MapRef(m)),
+                    I("mov_imm", 2, imm=0), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
+                    I("mov_imm", 3, imm=0), I("mov64_reg", 3, 10), I("add64_imm", 3, imm=vb),
+                    I("mov_imm", 4, imm=self.pick([0, 0, 0, 2, 1])), I("call", imm=1),
+                    I("xor64_reg", acc, 0), I("mul64_imm", acc, imm=0x2545F491)]
+        for r in (0, 1, 2, 3, 4):
+            if r != acc:
                 out.append(I("mov_imm", r, imm=self.imm()))
         return out
 
@@ -276,14 +341,18 @@ class _Gen:
 
 
 def random_program(seed, length=40, nmaps=1, map_value_size=8, reset_stride=None, writes=False,
-                   vstores=False, pkt_stores=True):
+                   vstores=False, pkt_stores=True, many_writes=False):
     """writes: half the map helper calls are map_update_elem / map_delete_elem (the device
     batch semantics: ebpf_gpu.h "Map writes in a device batch"); vstores: every lookup hit
     stores into the value first (ebpf_gpu.h "Stores into map values"); pkt_stores=False: packet
-    loads where stores into the packet would be (programs that leave the packet unchanged)."""
+    loads where stores into the packet would be (programs that leave the packet unchanged);
+    many_writes: the main path ends with more than 16 map writes (bulk_writes)."""
     gen = _Gen(seed, nmaps, map_value_size, writes, vstores)
     if not pkt_stores:
         gen.pkt_store = gen.ldx_pkt
-    nodes = gen.prologue() + gen.block(length) + gen.epilogue()
+    body = gen.block(length)
+    if many_writes:
+        body += gen.bulk_writes()
+    nodes = gen.prologue() + body + gen.epilogue()
     rs = reset_stride if reset_stride is not None else int(gen.g.integers(3, 12))
     return assemble(nodes, reset_stride=rs)

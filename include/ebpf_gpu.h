@@ -57,11 +57,13 @@ struct ebpf_map;
  *     against the maps of the program; r1 NULL (or a NULL key / value, or flags > EBPF_EXIST)
  *     is EINVAL as in ebpf_map.c:101-108 / :130-136, a pointer that is no map of them faults
  *     EBPF_FAULT_BAD_MAP (the reference dereferences it);
- *   - a packet may make 16 logged writes: successful map_update_elem / map_delete_elem calls
- *     and stores into map values, counter updates aligned to their width (below) not counted
- *     (they are additions).  The 17th faults the packet with EBPF_FAULT_WRITES (a fault: its
- *     writes do not land, its counter updates do).  A loop-free path of at most 16 such writes never meets the limit; programs
- *     with loops (standard semantics) may write inside them under it;
+ *   - a loop-free program makes every write its path reaches, however many, as the reference
+ *     does (the log is sized by the program's longest path).  A program with loops (standard
+ *     semantics: a backward jump) has no per-path bound, so there a packet may make 16 logged
+ *     writes: map_update_elem calls that return 0, every hashtable map_delete_elem (whether the
+ *     key exists is known only at the replay), and stores into map values; counter updates
+ *     aligned to their width (below) are not counted (they are additions).  The 17th faults the
+ *     packet with EBPF_FAULT_WRITES (a fault: its writes do not land, its counter updates do);
  *   - a writing program sharded over several devices (ebpf_prog_run_batch_multi*): the batch is
  *     the shards in order, every shard reads the batch-start maps, and the shards' writes are
  *     merged on the host in that global packet order after the last shard — the same result as

@@ -281,15 +281,19 @@ static __thread uint64_t t_pkt;
 static __thread uint32_t t_seq;
 static __thread uint32_t t_writes; /* the packet's logged writes (ebpf_oracle.h: at most 16) */
 static __thread int t_sequential; /* oracle_prog.sequential: writes land at once */
+static __thread int t_loops;      /* the batch's program loops (prog_has_loops) */
 #define ORACLE_WRITES_MAX 16u /* include/ebpf_gpu.h EBPF_FAULT_WRITES (dprog.h DP_WRITES_MAX) */
 
 /* A logged write of the batch (a map_update_elem / map_delete_elem that succeeds, a store into a
  * map value other than an aligned counter update): 0, or F_WRITES for the packet's 17th.  Only in
- * batch mode (the reference's own run, sequential or one packet, has no such limit). */
+ * batch mode, and only for a program with loops: a loop-free program writes as often as its path
+ * says, like the reference (ebpf_interpreter.c:343-366, ebpf_map.c:101-108 ->
+ * ebpf_map_array.c:198-211 run every store and update they reach); the reference's own run,
+ * sequential or one packet, has no limit at all. */
 static inline int
 count_write(void)
 {
-	if (t_sequential || t_wlog == NULL)
+	if (t_sequential || t_wlog == NULL || !t_loops)
 		return 0;
 	return ++t_writes > ORACLE_WRITES_MAX ? F_WRITES : 0;
 }
@@ -1370,6 +1374,68 @@ oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fau
 	return r;
 }
 
+/* Does the program loop?  Only standard semantics has loops (a taken jump goes to pc + 1 + off;
+ * the reference's stepping never lowers the slot, ebpf_interpreter.c:39,210).  Decided from the
+ * program's own bytes: a backward jump on the slot graph reachable from slot 0 (both arms of a
+ * conditional jump, LDDW over its second slot, EXIT and invalid opcodes end a path) — a
+ * conditional jump with off < 0 whose target is a slot of the program, or a JA with off < -1
+ * (JA -1 jumps to itself forever: F_LOOP at once, no loop body). */
+static int
+prog_has_loops(const struct oracle_prog *p)
+{
+	if (p->semantics != 1 || p->nslots == 0)
+		return 0;
+	uint8_t *seen = calloc(p->nslots, 1);
+	uint64_t *work = malloc((p->nslots * 2 + 2) * sizeof(uint64_t)); /* (<= 2 pushes a slot) */
+	size_t nw = 0;
+	int loops = 0;
+	work[nw++] = 0;
+	while (nw && !loops) {
+		const uint64_t pc = work[--nw];
+		if (pc >= p->nslots || seen[pc])
+			continue;
+		seen[pc] = 1;
+		const uint8_t *ip = p->insns + pc * 8;
+		const uint8_t op = ip[0];
+		int16_t off;
+		memcpy(&off, ip + 2, 2);
+		const int jmp32 = (op & 7) == 6;
+		if (!(valid_op(op) || op == 0xc3 || op == 0xdb ||
+		      (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 && op != 0x86 && op != 0x96)))
+			continue; /* F_BAD_OPCODE */
+		if (op == 0x95)
+			continue;
+		if (op == 0x18) {
+			work[nw++] = pc + 2;
+			continue;
+		}
+		const int64_t target = (int64_t)pc + 1 + off;
+		if (op == 0x05) {
+			if (off == -1)
+				continue;
+			if (off < 0) {
+				loops = 1;
+				break;
+			}
+			work[nw++] = (uint64_t)target;
+			continue;
+		}
+		if (((op & 7) == 5 || jmp32) && op != 0x85) {
+			if (target >= 0 && (uint64_t)target < p->nslots) {
+				if (off < 0) {
+					loops = 1;
+					break;
+				}
+				work[nw++] = (uint64_t)target;
+			}
+		}
+		work[nw++] = pc + 1;
+	}
+	free(work);
+	free(seen);
+	return loops;
+}
+
 static int
 wrec_cmp(const void *a, const void *b)
 {
@@ -1405,6 +1471,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 	if (p->sequential)
 		nthreads = 1;
 	struct wlog *logs = writes ? calloc((size_t)nthreads, sizeof(struct wlog)) : NULL;
+	const int loops = writes && prog_has_loops(p);
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(+ : total)
 #endif
@@ -1416,6 +1483,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 #endif
 		t_wlog = logs ? &logs[tid] : NULL;
 		t_sequential = p->sequential;
+		t_loops = loops;
 		t_ovl = logs && p->checked && !p->sequential ? malloc(sizeof(struct ovl)) : NULL;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
@@ -1454,6 +1522,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		free(t_ovl);
 		t_ovl = NULL;
 		t_sequential = 0;
+		t_loops = 0;
 	}
 	if (logs) {
 		/* after the batch: every write in packet order (last writer of a key wins) */

@@ -1,7 +1,8 @@
 """The GPU fuzzer (tools/fuzz_gpu.py) inside the suite, on seeds the fixed-seed parity tests do
 not use: random programs under the reference's semantics with array maps (every variant, staged
 and general kernels) and with hashtables, standard-semantics programs (loop-free,
-counted loops, cursor walks), programs that write maps inside loops (round 5), and randomly
+counted loops, cursor walks), programs that write maps inside loops (round 5), reference
+programs with more than 16 map writes on one path (round 6), and randomly
 edited programs the oracle finds defined.  Each mode
 compares results, fault codes, packet bytes after the batch and the maps with the oracle.  The
 long campaigns (thousands of programs per configuration) stay in tools/fuzz_gpu.py; their logs
@@ -29,7 +30,8 @@ def fuzz(gpu):
     return fuzz_gpu
 
 
-@pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites"])
+@pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites",
+                                  "manywrites"])
 def test_fuzz_campaign(fuzz, env, mode):
     if mode == "reference":
         failed = fuzz.reference(_args(seed=11), env)
@@ -39,6 +41,8 @@ def test_fuzz_campaign(fuzz, env, mode):
         failed = fuzz.standard(_args(seed=13, programs=80, standard=True), env)
     elif mode == "loopwrites":
         failed = fuzz.loop_writes(_args(seed=15, programs=40), env)
+    elif mode == "manywrites":   # (more than 16 writes on a loop-free path: no limit)
+        failed = fuzz.reference(_args(seed=16, programs=60, manywrites=True), env)
     else:
         failed = fuzz.mutated(_args(seed=14, programs=200, mutate=True), env)
     assert not failed, "mismatches (see the captured output for the failing program numbers)"

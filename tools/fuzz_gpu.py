@@ -9,7 +9,8 @@ key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts
 lookups, updates and deletes against the oracle's replay model; the tables are compared through
 get_next_key's walk (order and values).
 
-  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate | --loopwrites]
+  python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate | --loopwrites |
+                                                      --manywrites]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
 import argparse
 import os
@@ -48,13 +49,14 @@ def hash_spec(g, vs):
     return pyoracle.HashSpec(4, vs, items=items, capacity=cap)
 
 
-def case(k, seed, layout, hashed=False, writes=None):
+def case(k, seed, layout, hashed=False, writes=None, many=False):
     g = np.random.default_rng(seed * 7919 + k)
     vs = int(g.choice([8, 16, 72, 200]))   # (> 64: no inline constant, round 5)
     me = int(g.choice([16, 256]))
     lay = randprog.random_program(seed * 100000 + k, length=int(g.integers(10, 120)), nmaps=2,
                                   map_value_size=vs,
-                                  writes=(bool(k & 1) or hashed) if writes is None else writes)
+                                  writes=(bool(k & 1) or hashed) if writes is None else writes,
+                                  many_writes=many)
     if hashed:
         maps = [hash_spec(g, vs) for _ in range(2)]
     else:
@@ -256,14 +258,17 @@ def mutated(a, env):
 
 def reference(a, env):
     """Random programs under the reference's semantics (array maps, or hashtables with --hash)
-    on every variant and both kernels; returns True on any mismatch."""
+    on every variant and both kernels; returns True on any mismatch.  --manywrites: every
+    program's main path ends with 17..60 stores into a map value or 17..40 map_update_elem calls
+    (randprog bulk_writes: a loop-free program has no write limit)."""
     failed = False
+    many = getattr(a, "manywrites", False)
     for variant in (0, 1, 2):
         for layout in ("staged", "general"):
             t0 = time.time()
             bad, faults = [], 0
             for k in range(a.programs):
-                c = case(k, a.seed, layout, a.hash)
+                c = case(k, a.seed, layout, a.hash, many=many)
                 want, wf, wdata, wmaps = oracle(c)
                 # (every other general-kernel case hands its packets over as extents)
                 got, gf, gdata, gmaps = device(env, c, variant, extents=bool(k & 2))
@@ -273,9 +278,9 @@ def reference(a, env):
                     bad.append(k)
                 if k % 100 == 99:
                     print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-            print("%svariant %d %-7s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-                "hash " if a.hash else "", variant, layout, a.programs, faults, len(bad), bad[:20],
-                time.time() - t0), flush=True)
+            print("%s%svariant %d %-7s: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+                "hash " if a.hash else "", "many-writes " if many else "", variant, layout, a.programs,
+                faults, len(bad), bad[:20], time.time() - t0), flush=True)
             failed = failed or bool(bad)
     return failed
 
@@ -336,10 +341,14 @@ def main():
     ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (loops too)")
     ap.add_argument("--mutate", action="store_true", help="randomly edited programs (defined ones)")
     ap.add_argument("--loopwrites", action="store_true", help="map writes inside loops (standard)")
+    ap.add_argument("--manywrites", action="store_true",
+                    help="reference programs with more than 16 map writes on one path")
     a = ap.parse_args()
     env = native.Env()
     if a.loopwrites:
         failed = loop_writes(a, env)
+    elif a.manywrites:
+        failed = reference(a, env)
     elif a.mutate and not a.standard:
         failed = mutated(a, env)
     elif a.standard:
