@@ -1307,16 +1307,23 @@ def ovl_fix(T, acc):
 def ovl_store(T, nv):
     """Remember, in the lanes' overlays, the z = S_T0 bytes of nv (two VGPRs) stored at H[0:1]:
     for each of the (one or two) 8-byte words the store touches, its entry — made on first use
-    with the word's batch-start bytes from the mirror — gets the bytes.  For the lanes in exec;
-    clobbers R[0:3], R[8:10], H[2:4], S_T3, S_BYTES, S_MASK, S_JUNK (saved exec), vcc."""
-    W0, W1, CNT, IDX, E, X, Y = R[0], R[1], R[2], R[3], R[8], H[2], H[3]
+    with the word's batch-start bytes from the mirror — gets the bytes.  A lane whose overlay is
+    full (its entries = dp_launch.vflags bits 8..15; only a program with loops that reads its
+    counters back fills it, ebpf_gpu.h) when the store needs a new entry gets OVF = 1 and
+    stores nothing more.  For the lanes in exec; clobbers R[0:3], R[8:10], H[2:4], S_T3,
+    S_BYTES, S_MASK, S_JUNK (saved exec), vcc."""
+    W0, W1, CNT, IDX, E, X, Y, OVF = R[0], R[1], R[2], R[3], R[8], H[2], H[3], R[9]
     L = ["s_mov_b64 %s, exec" % sp(S_JUNK),
+         "v_mov_b32 %s, 0" % v(OVF),
          "v_add_u32 %s, %d, v%d" % (v(X), OVL_COUNT, V_STK),
          "ds_read_b32 %s, %s" % (v(CNT), v(X)),
          "s_waitcnt lgkmcnt(0)"]
     for wi in (0, 1):
         t = "%s%d" % (T, wi)
-        L += ["s_mov_b64 exec, %s" % sp(S_JUNK)]
+        L += ["s_mov_b64 exec, %s" % sp(S_JUNK),
+              "v_cmp_eq_u32_e64 vcc, 0, %s" % v(OVF),       # (not the lanes already full)
+              "s_and_b64 exec, exec, vcc",
+              "s_cbranch_execz .Los%s_end" % t]
         if wi:  # only lanes whose store reaches past its first word
             L += ["v_and_b32 %s, 7, %s" % (v(X), v(H[0])),
                   "v_add_u32 %s, %s, %s" % (v(X), s(S_T0), v(X)),
@@ -1349,9 +1356,16 @@ def ovl_store(T, nv):
               "s_add_u32 %s, %s, 1" % (s(S_T3), s(S_T3)),
               "s_branch .Los%s_find" % t,
               ".Los%s_found:" % t,
-              # none: a new entry with the word's batch-start bytes
+              # none: a new entry with the word's batch-start bytes (a full overlay: OVF)
               "v_cmp_eq_u32_e64 vcc, -1, %s" % v(IDX),
               "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
+              "s_cbranch_execz .Los%s_have" % t,
+              "s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
+              "s_waitcnt lgkmcnt(0)",
+              "s_bfe_u32 %s, %s, 0x80008" % (s(S_T3), s(S_T3)),
+              "v_cmp_le_u32_e64 vcc, %s, %s" % (s(S_T3), v(CNT)),
+              "v_cndmask_b32_e64 %s, %s, 1, vcc" % (v(OVF), v(OVF)),
+              "s_andn2_b64 exec, exec, vcc",
               "s_cbranch_execz .Los%s_have" % t,
               "v_mov_b32 %s, %s" % (v(IDX), v(CNT)),
               "v_add_u32 %s, 1, %s" % (v(CNT), v(CNT)),
@@ -1365,6 +1379,9 @@ def ovl_store(T, nv):
               "ds_write_b32 %s, %s" % (v(X), v(CNT)),
               ".Los%s_have:" % t,
               "s_or_b64 exec, exec, %s" % sp(S_MASK),
+              "v_cmp_eq_u32_e64 vcc, 0, %s" % v(OVF),
+              "s_and_b64 exec, exec, vcc",
+              "s_cbranch_execz .Los%s_end" % t,
               "v_lshl_add_u32 %s, %s, 4, v%d" % (v(E), v(IDX), V_STK),
               "v_add_u32 %s, %d, %s" % (v(E), OVL_ENTRIES + 8, v(E))]   # the entry's bytes
         # the bytes of the store that fall in this word
@@ -1440,8 +1457,16 @@ def vstore_routine():
          "v_mov_b32 %s, 0" % v(L_[0]),
          "v_mov_b32 %s, 0" % v(L_[1]),
          ".Lvs_have:"] + vflags_test(0, ".Lvs_noovl2") + ovl_store("vs", NV) + [
+         # (ovl_store kept exec there) lanes whose overlay was full fault WRITES, with nothing
+         # of this store done
+         "v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_JUNK), v(R[9])),
+         "s_andn2_b64 exec, exec, %s" % sp(S_JUNK),
+         "s_mov_b32 %s, %d" % (s(S_CODE), FAULT_WRITES),
+         "s_cbranch_execz .Lvs_ret",
+         "s_branch .Lvs_ovl_done",
          ".Lvs_noovl2:",
-         "s_mov_b64 %s, 0" % sp(S_JUNK),          # (ovl_store kept exec there)
+         "s_mov_b64 %s, 0" % sp(S_JUNK),
+         ".Lvs_ovl_done:",
          # offsets: OFF = address - the mirror (hashtables: SLOT, VOFF = in the value)
          "v_sub_co_u32 %s, vcc, %s, s66" % (v(OFF), v(H[0])),
          "v_mov_b32 %s, s67" % v(R[9]),

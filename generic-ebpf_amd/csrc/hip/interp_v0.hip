@@ -104,11 +104,20 @@ load_ovl(const overlay &o, uint64_t a, uint32_t size)
 	return v;
 }
 
-// Remember a store of `size` bytes of v at a; false when the overlay is full (the translator
-// sizes it: never)
+// Remember a store of `size` bytes of v at a; false, with nothing changed, when its words do not
+// fit (only a program with loops that reads its counters back fills the overlay)
 __device__ inline bool
 ovl_store(overlay &o, uint64_t a, uint32_t size, uint64_t v)
 {
+	uint32_t fresh = 0;
+	for (uint64_t w = a & ~7ull; w <= ((a + size - 1) & ~7ull); w += 8) {
+		uint32_t k = 0;
+		while (k < o.n && o.addr[k] != w)
+			k++;
+		fresh += k == o.n;
+	}
+	if (o.n + fresh > DP_OVL_MAX)
+		return false;
 	for (uint32_t i = 0; i < size; i++) {
 		const uint64_t b = a + i, w = b & ~7ull;
 		uint32_t k = 0;
@@ -223,8 +232,10 @@ value_store(const dp_launch &L, uint64_t gid, overlay &o, uint32_t &writes, int 
 	add = add && voff % size == 0;
 	if (!add && over_cap(L, writes)) // (aligned additions are not counted)
 		return F_WRITES;
+	// (a full overlay: only a program with loops that reads its counters back can fill it —
+	// ebpf_gpu.h, 32 words — the write that needs one more faults WRITES before it happens)
 	if ((L.vflags & 1) && !ovl_store(o, a, size, v))
-		return F_MEM;
+		return F_WRITES;
 	if (add && (mp.flags & DP_MAP_ATOMIC)) {
 		uint8_t *d = reinterpret_cast<uint8_t *>(mp.dev_base) + dp_delta_off(mp.value_size, mp.max_entries) + off;
 		if (size == 8)

@@ -95,6 +95,9 @@ struct rows_slot {
 	size_t log_bytes = 0;
 	void *win = nullptr;
 	size_t win_bytes = 0;
+	// a batch's log was handed out and its apply step has not been enqueued since: its offer
+	// kernel may have left winner words set, so the next batch clears them first
+	bool win_pending = false;
 	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
 	// shard on the device (any contents: every launch overwrites its row), and fork/join events
 	void *mh = nullptr;
@@ -211,7 +214,7 @@ grow_zeroed(void **p, size_t *have, size_t need)
 // The stream's map-write log (>= log_bytes) and winner words (>= win_bytes).
 int
 upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, uint8_t **log,
-	    unsigned long long **win)
+	    unsigned long long **win, bool **pending)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
 	rows_slot *r;
@@ -222,9 +225,24 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 		err = grow_zeroed(&r->win, &r->win_bytes, win_bytes);
 	if (err)
 		return err;
+	if (r->win_pending) { // (the previous batch on this stream stopped before its apply step)
+		if (hipMemsetAsync(r->win, 0, r->win_bytes, stream) != hipSuccess)
+			return EIO;
+	}
+	r->win_pending = true;
 	*log = static_cast<uint8_t *>(r->log);
 	*win = static_cast<unsigned long long *>(r->win);
+	*pending = &r->win_pending;
 	return 0;
+}
+
+// The batch's apply step is enqueued: the winner words will be zero again after it
+void
+upd_settled(bool *pending)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	if (pending)
+		*pending = false;
 }
 
 // The leading stream's multi-device scratch: `rows` histogram rows and `nev` events.
@@ -648,6 +666,7 @@ struct upd_plan {
 	uint64_t pkt_base = 0;
 	uint32_t *faulted = nullptr; // one bit per packet of the batch (after the records)
 	size_t faulted_bytes = 0;
+	bool *win_pending = nullptr; // the stream slot's flag (upd_acquire)
 	// per table map, the device table its launches read (hashtables whose values the batch
 	// stores into: a record names a slot, and this is the slot's key whatever is uploaded later)
 	std::vector<std::shared_ptr<const std::vector<uint8_t>>> tables;
@@ -676,17 +695,18 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 	size_t bytes, boff, bbytes;
 	int err = upd_size(ep, dp, count, &P->cap, &bytes, &boff, &bbytes);
 	if (!err)
-		err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &P->log, &P->win);
+		err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &P->log, &P->win,
+				  &P->win_pending);
 	if (err)
 		return fail(err, "map-write log");
 	P->faulted = reinterpret_cast<uint32_t *>(P->log + boff);
 	P->faulted_bytes = bbytes;
 	// (the buffer is reused at other sizes: whatever lies where the bitmap now starts is stale).
 	// The log's counter is zero after every apply step; it is zeroed here too, so that a batch
-	// whose launch failed before its apply leaves nothing behind.  The winner words need no
-	// clearing: they are zeroed when allocated, only the apply step writes them (its first kernel
-	// offers, its second re-arms every word that received an offer), so they are zero between
-	// batches whatever happened to the launch before
+	// whose launch failed before its apply leaves nothing behind.  The winner words are zeroed
+	// when allocated and only the apply step writes them (its first kernel offers, its second
+	// re-arms every word that received an offer); a batch that stopped before its apply step was
+	// enqueued leaves the stream's flag set, and upd_acquire clears them then
 	hipError_t e = hipMemsetAsync(P->faulted, 0, bbytes, stream);
 	if (e == hipSuccess)
 		e = hipMemsetAsync(P->log, 0, 4, stream);
@@ -710,6 +730,7 @@ upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t
 					 (uint32_t)dp->upd_host.size(), P.win, P.faulted, stream);
 	if (e != hipSuccess)
 		return hip_fail(e, "map writes");
+	upd_settled(P.win_pending);
 	for (uint16_t t : dev)
 		map_mark_device_write(ep->xlated->maps[t], dp->device, static_cast<void *>(stream));
 	return 0;
@@ -931,9 +952,12 @@ upd_finish(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_
 	int err;
 	if (host && (err = upd_fetch(dp, P, stream, 0, &logs[0])))
 		return err;
-	if ((!ep->xlated->upd_maps.empty() || !ep->xlated->atomic_maps.empty()) &&
-	    (err = upd_apply(ep, dp, P, stream)))
-		return err;
+	if (!ep->xlated->upd_maps.empty() || !ep->xlated->atomic_maps.empty()) {
+		if ((err = upd_apply(ep, dp, P, stream)))
+			return err;
+	} else {
+		upd_settled(P.win_pending); // (no offer kernel ran: the winner words are untouched)
+	}
 	return host ? upd_apply_host(ep, logs, false) : 0;
 }
 
@@ -1618,8 +1642,11 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 			return drain(hip_fail(e, "batch"));
 	}
 	if (prog_writes_maps(*ep->xlated) && hi > lo) {
-		if (log_out) // (several shards: the caller merges the logs)
-			return upd_fetch(dp, plan, S.stream[0], lo, log_out);
+		if (log_out) { // (several shards: the caller merges the logs; no offer kernel runs)
+			if ((err = upd_fetch(dp, plan, S.stream[0], lo, log_out)) == 0)
+				upd_settled(plan.win_pending);
+			return err;
+		}
 		if ((err = upd_finish(ep, dp, plan, S.stream[0])))
 			return drain(err);
 		if ((e = hipStreamSynchronize(S.stream[0])) != hipSuccess)
@@ -1802,6 +1829,8 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 			device_guard g2;
 			hipSetDevice(devices[d]);
 			rc = upd_fetch(ep->dev[devices[d]].get(), plan, st[d], first, &logs[d]);
+			if (rc == 0) // (merged on the host: no offer kernel runs)
+				upd_settled(plan.win_pending);
 		}
 		return rc;
 	};

@@ -227,6 +227,10 @@ struct dprog_host {
 	uint32_t ovl_entries = 0;            // ... overlay words per lane (2 per store on a path)
 	bool write_cap = false;              // a path may log more than DP_WRITES_MAX writes (loops):
 	                                     // the device counts them per packet (DP_VF_WCAP)
+	bool reads_counters = false;         // loops, and a live counter-idiom register or XADD with
+	                                     // BPF_FETCH on the slot graph (translate.cpp
+	                                     // slot_reads_counters): the overlay holds the packet's
+	                                     // view, DP_OVL_MAX words, the next faults WRITES
 	int error = 0;
 	std::string error_msg;
 };

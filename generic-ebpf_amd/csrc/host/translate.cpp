@@ -1125,6 +1125,218 @@ live_out(const dprog_host &out)
 	return lout;
 }
 
+// ---- the slot graph of a standard-semantics program (ebpf_gpu.h "Stores into map values": the
+// programs with loops that read their counter updates back).  A restatement of the contract on
+// the bytecode itself, not on the state graph above, so that the decision depends on nothing but
+// the program's bytes.
+
+// A CALL of a helper the device runs (lookup, update, delete); 1 update, 2 the others, 0 none
+int
+std_slot_helper(const struct ebpf_config *ec, int32_t imm)
+{
+	const struct ebpf_helper_type *h = (imm >= 0 && imm < EBPF_TYPE_MAX) ? ec->helper_types[imm] : nullptr;
+	if (h == &eht_map_update_elem)
+		return 1;
+	return (h != nullptr && (h == &eht_map_lookup_elem || h == &eht_map_delete_elem)) ? 2 : 0;
+}
+
+bool
+std_slot_valid(const struct ebpf_inst &in)
+{
+	const uint8_t op = in.opcode;
+	const bool jmp32 = (op & 7) == DP_CLS_JMP32;
+	if (jmp32) {
+		switch (op & 0xf0) {
+		case 0x10: case 0x20: case 0x30: case 0x40: case 0x50: case 0x60: case 0x70:
+		case 0xa0: case 0xb0: case 0xc0: case 0xd0:
+			break;
+		default:
+			return false;
+		}
+		return !(in.dst >= EBPF_REG_MAX || ((op & 0x08) && in.src >= EBPF_REG_MAX));
+	}
+	const bool xadd = op == 0xc3 || op == 0xdb;
+	if (!(valid_op(op) || xadd) || (xadd && in.imm != 0 && in.imm != 1))
+		return false;
+	return !((uses_dst(op) && in.dst >= EBPF_REG_MAX) || (uses_src(op) && in.src >= EBPF_REG_MAX));
+}
+
+// The slots execution may continue at after slot pc: both arms of a conditional jump (a target
+// outside the program faults), LDDW over its second slot, none after EXIT or a faulting slot;
+// a JA -1 spins (EBPF_FAULT_LOOP)
+int
+std_slot_succ(const struct ebpf_config *ec, const struct ebpf_inst *code, uint64_t n, uint64_t pc,
+	      uint64_t succ[2])
+{
+	const struct ebpf_inst &in = code[pc];
+	const uint8_t op = in.opcode;
+	if (!std_slot_valid(in) || op == EBPF_OP_EXIT || (op == EBPF_OP_CALL && !std_slot_helper(ec, in.imm)))
+		return 0;
+	if (op == EBPF_OP_LDDW) {
+		succ[0] = pc + 2;
+		return 1;
+	}
+	const int64_t target = (int64_t)pc + 1 + in.offset;
+	if (op == EBPF_OP_JA) {
+		if (in.offset == -1 || target < 0)
+			return 0;
+		succ[0] = (uint64_t)target;
+		return 1;
+	}
+	int k = 0;
+	const uint8_t cls = op & 7;
+	if ((cls == EBPF_CLS_JMP || cls == DP_CLS_JMP32) && op != EBPF_OP_CALL && target >= 0 &&
+	    (uint64_t)target < n)
+		succ[k++] = (uint64_t)target;
+	succ[k++] = pc + 1;
+	return k;
+}
+
+// Registers a standard-semantics slot reads / writes (a CALL reads its helper's arguments —
+// lookup and delete r1, r2, update r1..r4 — and writes r0; EXIT reads r0)
+void
+std_slot_regs(const struct ebpf_config *ec, const struct ebpf_inst &in, uint16_t *rd, uint16_t *wr)
+{
+	const uint8_t op = in.opcode, cls = op & 7;
+	const uint16_t d = (uint16_t)(1u << in.dst), s = (uint16_t)(1u << in.src);
+	*rd = *wr = 0;
+	if (!std_slot_valid(in))
+		return;
+	switch (cls) {
+	case EBPF_CLS_LD:
+		*wr = d;
+		return;
+	case EBPF_CLS_LDX:
+		*rd = s;
+		*wr = d;
+		return;
+	case EBPF_CLS_ST:
+		*rd = d;
+		return;
+	case EBPF_CLS_STX:
+		*rd = d | s;
+		if ((op == 0xc3 || op == 0xdb) && in.imm == 1)
+			*wr = s;
+		return;
+	case EBPF_CLS_JMP:
+	case DP_CLS_JMP32:
+		if (op == EBPF_OP_CALL) {
+			*rd = std_slot_helper(ec, in.imm) == 1 ? 0x1e : 0x06;
+			*wr = 1;
+		} else if (op == EBPF_OP_EXIT) {
+			*rd = 1;
+		} else if (op != EBPF_OP_JA) {
+			*rd = d | ((op & 0x08) ? s : 0);
+		}
+		return;
+	default: // ALU / ALU64: MOV writes only (reg: reads src); NEG, LE / BE read dst only
+		*wr = d;
+		if ((op & 0xf0) == 0xb0)
+			*rd = (op & 0x08) ? s : 0;
+		else if ((op & 0xf0) == 0xd0 || (op & 0xf0) == 0x80)
+			*rd = d;
+		else
+			*rd = d | ((op & 0x08) ? s : 0);
+		return;
+	}
+}
+
+// The slot execution continues at from pc, JA chains followed; n when none
+uint64_t
+std_slot_next_exec(const struct ebpf_inst *code, uint64_t n, uint64_t pc)
+{
+	for (uint64_t hops = 0; pc < n && hops <= n; hops++) {
+		if (code[pc].opcode != EBPF_OP_JA)
+			return pc;
+		const int64_t t = (int64_t)pc + 1 + code[pc].offset;
+		if (code[pc].offset == -1 || t < 0)
+			return n;
+		pc = (uint64_t)t;
+	}
+	return n;
+}
+
+// Does the program read its counter updates back?  A reachable XADD with BPF_FETCH, or a
+// reachable counter idiom (LDX{W,DW} X = [P + off], X != P; then, JA aside, ADD / SUB to X of
+// an immediate or of a register other than X, 64-bit or, for W, 32-bit; then STX [P + off] = X
+// of the same width) whose X is live after its STX on the slot graph
+bool
+slot_reads_counters(const struct ebpf_config *ec, const struct ebpf_inst *code, uint64_t n)
+{
+	if (n == 0)
+		return false;
+	std::vector<char> seen(n, 0);
+	std::vector<uint64_t> work{0};
+	while (!work.empty()) {
+		const uint64_t pc = work.back();
+		work.pop_back();
+		if (pc >= n || seen[pc])
+			continue;
+		seen[pc] = 1;
+		uint64_t sx[2];
+		const int k = std_slot_succ(ec, code, n, pc, sx);
+		for (int i = 0; i < k; i++)
+			work.push_back(sx[i]);
+	}
+	for (uint64_t i = 0; i < n; i++)
+		if (seen[i] && (code[i].opcode == 0xc3 || code[i].opcode == 0xdb) && code[i].imm == 1)
+			return true;
+	std::vector<uint16_t> lin;
+	for (uint64_t a = 0; a < n; a++) {
+		const struct ebpf_inst &la = code[a];
+		const uint8_t X = la.dst, P = la.src;
+		if (!seen[a] || !(la.opcode == EBPF_OP_LDXW || la.opcode == EBPF_OP_LDXDW) || X == P)
+			continue;
+		const int size = la.opcode == EBPF_OP_LDXDW ? 8 : 4;
+		const uint64_t b = std_slot_next_exec(code, n, a + 1);
+		if (b >= n || code[b].dst != X)
+			continue;
+		const uint8_t bs = code[b].src;
+		bool ok = false;
+		switch (code[b].opcode) {
+		case 0x07: case 0x17: ok = true; break;
+		case 0x0f: case 0x1f: ok = bs != X; break;
+		case 0x04: case 0x14: ok = size == 4; break;
+		case 0x0c: case 0x1c: ok = size == 4 && bs != X; break;
+		}
+		if (!ok)
+			continue;
+		const uint64_t c = std_slot_next_exec(code, n, b + 1);
+		if (c >= n)
+			continue;
+		const struct ebpf_inst &lc = code[c];
+		if (lc.opcode != (size == 8 ? EBPF_OP_STXDW : EBPF_OP_STXW) || lc.dst != P || lc.src != X ||
+		    lc.offset != la.offset)
+			continue;
+		if (lin.empty()) { // liveness to a fixed point: in = rd | (out & ~wr)
+			lin.assign(n, 0);
+			for (bool changed = true; changed;) {
+				changed = false;
+				for (uint64_t i = n; i-- > 0;) {
+					uint16_t rd, wr, o = 0;
+					std_slot_regs(ec, code[i], &rd, &wr);
+					uint64_t sx[2];
+					const int k = std_slot_succ(ec, code, n, i, sx);
+					for (int j = 0; j < k; j++)
+						if (sx[j] < n)
+							o |= lin[sx[j]];
+					const uint16_t in = (uint16_t)(rd | (o & ~wr));
+					if (in != lin[i]) {
+						lin[i] = in;
+						changed = true;
+					}
+				}
+			}
+		}
+		uint64_t sx[2];
+		const int k = std_slot_succ(ec, code, n, c, sx);
+		for (int j = 0; j < k; j++)
+			if (sx[j] < n && ((lin[sx[j]] >> X) & 1))
+				return true;
+	}
+	return false;
+}
+
 // Stores into map values (ebpf_gpu.h "Stores into map values"): which maps they may reach and
 // how each written map's writes land (dprog_host upd_maps / hupd_maps / atomic_maps), whether
 // the packet may read its own stores back (the overlay), and the write log's records per path.
@@ -1304,10 +1516,17 @@ analyze_writes(dprog_host &out)
 			}
 		}
 	}
-	if (out.has_loops && counters && out.vstore_overlay) {
+	// A program with loops that reads its counter updates back (slot_reads_counters: a live
+	// idiom register, XADD with BPF_FETCH) keeps the packet's view of them in the overlay, 32
+	// words (DP_OVL_MAX; the store that needs one more faults EBPF_FAULT_WRITES).  A read-back
+	// of another form (a later load of a counter's word) is refused
+	if (out.has_loops && counters && out.reads_counters) {
+		out.vstore_overlay = true;
+	} else if (out.has_loops && counters && out.vstore_overlay) {
 		out.error = EOPNOTSUPP;
-		out.error_msg = "in a program with loops, the packet may not read back the values its counter "
-				"updates change (run this one with ebpf_prog_run)";
+		out.error_msg = "in a program with loops, the packet may read back the values its counter "
+				"updates change only through the idiom's register or XADD with BPF_FETCH (run "
+				"this one with ebpf_prog_run)";
 		return EOPNOTSUPP;
 	}
 	// per path: records the log needs, stores the overlay holds
@@ -1602,6 +1821,7 @@ translate_program(struct ebpf_prog *ep, dprog_host &out)
 		}
 		dataflow(out);
 	}
+	out.reads_counters = std_sem && out.has_loops && slot_reads_counters(ep->eo.eo_ee->ec, code, nslots);
 	if (analyze_writes(out) != 0) {
 		out.maps.clear();
 		return out.error;

@@ -95,10 +95,18 @@ struct ebpf_map;
  *   - EBPF_FAULT_MAP_WRITE is left for a store into a map value the translation did not provide
  *     for (a packet-relative pointer that lands in a map);
  *   - in a program with loops (standard semantics) a counter update must go to an array that
- *     only aligned counter updates of one width change, and may not be read back by the packet
- *     (an XADD without BPF_FETCH, or the LDX / ADD / STX idiom whose register is dead after the
- *     STX): the batch functions return EOPNOTSUPP otherwise.  Plain stores and map_update_elem /
- *     map_delete_elem in loops are limited only by the 16 logged writes per packet.
+ *     only aligned counter updates of one width change (the batch functions return EOPNOTSUPP
+ *     otherwise).  The packet may read its counters back through an XADD with BPF_FETCH or
+ *     through the idiom's register (live after the STX: the program "reads its counters back",
+ *     decided from its bytecode on the slot graph — a reachable such XADD or idiom, a CALL
+ *     reading its helper's arguments (lookup, delete r1-r2; update r1-r4), EXIT r0); it then
+ *     sees the batch-start value plus its own additions,
+ *     kept in 32 8-byte words of map values per packet: a store, counter update or XADD that
+ *     needs a word beyond them faults EBPF_FAULT_WRITES before it happens (a word already held
+ *     is free: one counter updated on every trip takes one).  The map still lands as additions.
+ *     A read-back of another form (a later plain load of a counter's word) returns EOPNOTSUPP.
+ *     Plain stores and map_update_elem / map_delete_elem in loops are limited only by the 16
+ *     logged writes per packet.
  * How it runs: arrays changed only by aligned counter updates of one width take device atomics
  * into a delta area next to their mirror (added into the values after the batch); other arrays'
  * stores land on the device (per-byte winners); hashtables, and arrays that mix counter updates

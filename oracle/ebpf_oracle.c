@@ -3,8 +3,8 @@
  *
  * Follows generic-ebpf sys/dev/ebpf/ebpf_interpreter.c:23-372 case by case (line numbers in
  * the comments), compiled for x86-64 exactly as the reference is: shift counts are masked to
- * 5/6 bits (x86 SHL/SHR semantics, SURVEY.md Appendix A [probed]).  Parity with the genuine
- * reference is pinned by tests/golden/ (see ebpf_oracle.h).
+ * 5/6 bits (x86 SHL/SHR semantics, SURVEY.md Appendix A [probed]).  It agrees with the golden
+ * vectors under tests/golden/; run-result parity is unpinned (see ebpf_oracle.h).
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use this file.
  */
@@ -282,7 +282,37 @@ static __thread uint32_t t_seq;
 static __thread uint32_t t_writes; /* the packet's logged writes (ebpf_oracle.h: at most 16) */
 static __thread int t_sequential; /* oracle_prog.sequential: writes land at once */
 static __thread int t_loops;      /* the batch's program loops (prog_has_loops) */
+static __thread int t_rb;         /* ... and reads its counter updates back (prog_reads_counters) */
 #define ORACLE_WRITES_MAX 16u /* include/ebpf_gpu.h EBPF_FAULT_WRITES (dprog.h DP_WRITES_MAX) */
+#define ORACLE_OVL_WORDS 32u  /* the packet's own view: 8-byte words of map values (DP_OVL_MAX) */
+static __thread struct {
+	uint32_t n;
+	uint64_t w[ORACLE_OVL_WORDS]; /* map index << 40 | word index within the map's values */
+} t_words;
+
+/* A program with loops that reads its counter updates back keeps the packet's view of the map
+ * values it changed in 32 words (ebpf_oracle.h): the store or counter update of `size` bytes at
+ * byte `off` of map mi's values takes the 8-byte words it touches that the packet has not yet
+ * touched; F_WRITES when they do not fit (before anything happens), else 0. */
+static int
+take_words(int mi, uint64_t off, int size)
+{
+	uint64_t need[2];
+	uint32_t k = 0;
+	for (uint64_t w = off >> 3; w <= (off + (uint64_t)size - 1) >> 3; w++) {
+		const uint64_t key = (uint64_t)mi << 40 | w;
+		uint32_t i = 0;
+		while (i < t_words.n && t_words.w[i] != key)
+			i++;
+		if (i == t_words.n)
+			need[k++] = key;
+	}
+	if (t_words.n + k > ORACLE_OVL_WORDS)
+		return F_WRITES;
+	for (uint32_t i = 0; i < k; i++)
+		t_words.w[t_words.n++] = need[i];
+	return 0;
+}
 
 /* A logged write of the batch (a map_update_elem / map_delete_elem that succeeds, a store into a
  * map value other than an aligned counter update): 0, or F_WRITES for the packet's 17th.  Only in
@@ -387,6 +417,11 @@ value_store(const struct region_env *re, int mi, uint64_t addr, int size, uint64
 	}
 	if (!add) {
 		int f = count_write();
+		if (f)
+			return f;
+	}
+	if (t_loops && t_rb) {
+		int f = take_words(mi, addr - (uint64_t)(uintptr_t)m->data, size);
 		if (f)
 			return f;
 	}
@@ -1374,66 +1409,266 @@ oracle_run(const struct oracle_prog *p, uint8_t *pkt, uint64_t len, uint8_t *fau
 	return r;
 }
 
+/* ---- the slot graph of a standard-semantics program (ebpf_oracle.h: which programs loop, and
+ * which read their counter updates back) ---- */
+
+/* An opcode run_std executes (else F_BAD_OPCODE). */
+static inline int
+std_valid(uint8_t op)
+{
+	const int jmp32 = (op & 7) == 6;
+	return valid_op(op) || op == 0xc3 || op == 0xdb ||
+	       (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 && op != 0x86 && op != 0x96);
+}
+
+/* A CALL of a helper the batch runs (lookup, update, delete; any other faults) */
+static inline int
+std_call_ok(const struct oracle_prog *p, int32_t imm)
+{
+	if (imm < 0 || imm >= 64)
+		return 0;
+	const uint8_t k = p->helper_kind[imm];
+	return k == ORACLE_HELPER_MAP_LOOKUP || k == ORACLE_HELPER_MAP_UPDATE || k == ORACLE_HELPER_MAP_DELETE;
+}
+
+/* The slots execution may continue at after slot pc (both arms of a conditional jump; LDDW over
+ * its second slot; none after EXIT or an invalid opcode), into succ[0..1]; *back = 1 when one of
+ * them is a backward jump's target that makes a loop: a conditional jump with off < 0 whose
+ * target is a slot of the program, or a JA with off < -1 (JA -1 jumps to itself forever: F_LOOP
+ * at once, no loop body).  Returns the count. */
+static int
+std_succ(const struct oracle_prog *p, uint64_t pc, uint64_t succ[2], int *back)
+{
+	const uint8_t *ip = p->insns + pc * 8;
+	const uint8_t op = ip[0], d = ip[1] & 0x0f, sr = ip[1] >> 4;
+	int16_t off;
+	int32_t imm;
+	memcpy(&off, ip + 2, 2);
+	memcpy(&imm, ip + 4, 4);
+	*back = 0;
+	if (!std_valid(op) || op == 0x95)
+		return 0;
+	if ((op == 0xc3 || op == 0xdb) && imm != 0 && imm != 1)
+		return 0; /* F_BAD_OPCODE */
+	if ((op & 7) == 6 ? (d >= 11 || ((op & 0x08) && sr >= 11))
+			  : ((uses_dst(op) && d >= 11) || (uses_src(op) && sr >= 11)))
+		return 0; /* F_BAD_REG */
+	if (op == 0x85 && !std_call_ok(p, imm))
+		return 0; /* F_HELPER / F_HELPER_UNSUPPORTED */
+	if (op == 0x18) {
+		succ[0] = pc + 2;
+		return 1;
+	}
+	const int64_t target = (int64_t)pc + 1 + off;
+	if (op == 0x05) {
+		if (off == -1)
+			return 0;
+		*back = off < 0;
+		if (target < 0)
+			return 0;
+		succ[0] = (uint64_t)target;
+		return 1;
+	}
+	int n = 0;
+	if (((op & 7) == 5 || (op & 7) == 6) && op != 0x85 && target >= 0 && (uint64_t)target < p->nslots) {
+		*back = off < 0;
+		succ[n++] = (uint64_t)target;
+	}
+	succ[n++] = pc + 1;
+	return n;
+}
+
+/* Slots reachable from slot 0 (seen[], nslots bytes); returns 1 when a loop's backward jump is
+ * among them. */
+static int
+std_reach(const struct oracle_prog *p, uint8_t *seen)
+{
+	uint64_t *work = malloc((p->nslots * 2 + 2) * sizeof(uint64_t)); /* (<= 2 pushes a slot) */
+	size_t nw = 0;
+	int loops = 0;
+	memset(seen, 0, p->nslots);
+	work[nw++] = 0;
+	while (nw) {
+		const uint64_t pc = work[--nw];
+		if (pc >= p->nslots || seen[pc])
+			continue;
+		seen[pc] = 1;
+		uint64_t sx[2];
+		int back;
+		const int k = std_succ(p, pc, sx, &back);
+		loops |= back;
+		for (int i = 0; i < k; i++)
+			work[nw++] = sx[i];
+	}
+	free(work);
+	return loops;
+}
+
 /* Does the program loop?  Only standard semantics has loops (a taken jump goes to pc + 1 + off;
  * the reference's stepping never lowers the slot, ebpf_interpreter.c:39,210).  Decided from the
- * program's own bytes: a backward jump on the slot graph reachable from slot 0 (both arms of a
- * conditional jump, LDDW over its second slot, EXIT and invalid opcodes end a path) — a
- * conditional jump with off < 0 whose target is a slot of the program, or a JA with off < -1
- * (JA -1 jumps to itself forever: F_LOOP at once, no loop body). */
+ * program's own bytes: a backward jump (std_succ) reachable from slot 0. */
 static int
 prog_has_loops(const struct oracle_prog *p)
 {
 	if (p->semantics != 1 || p->nslots == 0)
 		return 0;
-	uint8_t *seen = calloc(p->nslots, 1);
-	uint64_t *work = malloc((p->nslots * 2 + 2) * sizeof(uint64_t)); /* (<= 2 pushes a slot) */
-	size_t nw = 0;
-	int loops = 0;
-	work[nw++] = 0;
-	while (nw && !loops) {
-		const uint64_t pc = work[--nw];
-		if (pc >= p->nslots || seen[pc])
-			continue;
-		seen[pc] = 1;
-		const uint8_t *ip = p->insns + pc * 8;
-		const uint8_t op = ip[0];
-		int16_t off;
-		memcpy(&off, ip + 2, 2);
-		const int jmp32 = (op & 7) == 6;
-		if (!(valid_op(op) || op == 0xc3 || op == 0xdb ||
-		      (jmp32 && valid_op((uint8_t)((op & 0xf8) | 5)) && op != 0x06 && op != 0x86 && op != 0x96)))
-			continue; /* F_BAD_OPCODE */
-		if (op == 0x95)
-			continue;
-		if (op == 0x18) {
-			work[nw++] = pc + 2;
-			continue;
-		}
-		const int64_t target = (int64_t)pc + 1 + off;
-		if (op == 0x05) {
-			if (off == -1)
-				continue;
-			if (off < 0) {
-				loops = 1;
-				break;
-			}
-			work[nw++] = (uint64_t)target;
-			continue;
-		}
-		if (((op & 7) == 5 || jmp32) && op != 0x85) {
-			if (target >= 0 && (uint64_t)target < p->nslots) {
-				if (off < 0) {
-					loops = 1;
-					break;
-				}
-				work[nw++] = (uint64_t)target;
-			}
-		}
-		work[nw++] = pc + 1;
-	}
-	free(work);
+	uint8_t *seen = malloc(p->nslots);
+	const int loops = std_reach(p, seen);
 	free(seen);
 	return loops;
+}
+
+/* Registers a standard-semantics instruction reads (*rd) and writes (*wr), as bit masks: a CALL
+ * reads its helper's arguments (lookup and delete r1, r2; update r1..r4) and writes r0, EXIT
+ * reads r0, an invalid opcode nothing. */
+static void
+std_regs(const struct oracle_prog *p, const uint8_t *ip, uint16_t *rd, uint16_t *wr)
+{
+	const uint8_t op = ip[0], cls = op & 7;
+	const uint16_t d = (uint16_t)(1u << (ip[1] & 0x0f)), s = (uint16_t)(1u << (ip[1] >> 4));
+	*rd = *wr = 0;
+	if (!std_valid(op))
+		return;
+	switch (cls) {
+	case 0: /* LDDW */
+		*wr = d;
+		return;
+	case 1: /* LDX */
+		*rd = s;
+		*wr = d;
+		return;
+	case 2: /* ST */
+		*rd = d;
+		return;
+	case 3: /* STX, XADD (imm 1: src receives the old value) */
+		*rd = d | s;
+		if ((op == 0xc3 || op == 0xdb) && (int32_t)(ip[4] | ip[5] << 8 | ip[6] << 16 | (uint32_t)ip[7] << 24) == 1)
+			*wr = s;
+		return;
+	case 5:
+	case 6:
+		if (op == 0x85) {
+			int32_t imm;
+			memcpy(&imm, ip + 4, 4);
+			*rd = std_call_ok(p, imm) && p->helper_kind[imm] == ORACLE_HELPER_MAP_UPDATE ? 0x1e : 0x06;
+			*wr = 1;
+		} else if (op == 0x95) {
+			*rd = 1;
+		} else if (op != 0x05) {
+			*rd = d | ((op & 0x08) ? s : 0);
+		}
+		return;
+	default: /* ALU / ALU64: MOV writes only (reg: reads src), LE / BE read dst only */
+		*wr = d;
+		if ((op & 0xf0) == 0xb0)
+			*rd = (op & 0x08) ? s : 0;
+		else if ((op & 0xf0) == 0xd0 || (op & 0xf0) == 0x80)
+			*rd = d;
+		else
+			*rd = d | ((op & 0x08) ? s : 0);
+		return;
+	}
+}
+
+/* The slot execution continues at from pc, JA chains followed (the counter idiom's "consecutive,
+ * JA aside"); nslots when there is none. */
+static uint64_t
+std_next_exec(const struct oracle_prog *p, uint64_t pc)
+{
+	for (uint64_t hops = 0; pc < p->nslots && hops <= p->nslots; hops++) {
+		const uint8_t *ip = p->insns + pc * 8;
+		if (ip[0] != 0x05)
+			return pc;
+		int16_t off;
+		memcpy(&off, ip + 2, 2);
+		const int64_t t = (int64_t)pc + 1 + off;
+		if (off == -1 || t < 0)
+			return p->nslots;
+		pc = (uint64_t)t;
+	}
+	return p->nslots;
+}
+
+/* Does a program with loops read its counter updates back (ebpf_oracle.h)?  From its bytes, on
+ * the slot graph: a reachable XADD with BPF_FETCH (imm 1), or a reachable counter idiom —
+ * LDX{W,DW} X = [P + off] (X != P), then (JA aside) ADD / SUB to X of an immediate or of a
+ * register other than X (64-bit; 32-bit too for W), then STX [P + off] = X of the same width —
+ * whose X is live after the STX (some path from there reads X before writing it; a backward
+ * fixed point of std_regs over the graph). */
+static int
+prog_reads_counters(const struct oracle_prog *p)
+{
+	if (p->semantics != 1 || p->nslots == 0)
+		return 0;
+	const uint64_t n = p->nslots;
+	uint8_t *seen = malloc(n);
+	std_reach(p, seen);
+	int rb = 0;
+	for (uint64_t i = 0; i < n && !rb; i++) {
+		const uint8_t *ip = p->insns + i * 8;
+		rb = seen[i] && (ip[0] == 0xc3 || ip[0] == 0xdb) &&
+		     (int32_t)(ip[4] | ip[5] << 8 | ip[6] << 16 | (uint32_t)ip[7] << 24) == 1;
+	}
+	uint16_t *lin = NULL;
+	for (uint64_t a = 0; a < n && !rb; a++) {
+		const uint8_t *la = p->insns + a * 8;
+		const uint8_t X = la[1] & 0x0f, P = la[1] >> 4;
+		if (!seen[a] || !(la[0] == 0x61 || la[0] == 0x79) || X == P)
+			continue;
+		const int size = la[0] == 0x79 ? 8 : 4;
+		const uint64_t b = std_next_exec(p, a + 1);
+		if (b >= n)
+			continue;
+		const uint8_t *lb = p->insns + b * 8;
+		const uint8_t bs = lb[1] >> 4;
+		int ok = 0;
+		if ((lb[1] & 0x0f) == X) {
+			switch (lb[0]) {
+			case 0x07: case 0x17: ok = 1; break;
+			case 0x0f: case 0x1f: ok = bs != X; break;
+			case 0x04: case 0x14: ok = size == 4; break;
+			case 0x0c: case 0x1c: ok = size == 4 && bs != X; break;
+			}
+		}
+		if (!ok)
+			continue;
+		const uint64_t c = std_next_exec(p, b + 1);
+		if (c >= n)
+			continue;
+		const uint8_t *lc = p->insns + c * 8;
+		if (lc[0] != (size == 8 ? 0x7b : 0x63) || (lc[1] & 0x0f) != P || (lc[1] >> 4) != X ||
+		    memcmp(lc + 2, la + 2, 2) != 0)
+			continue;
+		if (lin == NULL) { /* liveness, once: lin[i] = rd | (out & ~wr), out = OR of the successors' */
+			lin = calloc(n, sizeof(uint16_t));
+			for (int changed = 1; changed;) {
+				changed = 0;
+				for (uint64_t i = n; i-- > 0;) {
+					uint16_t rd, wr, o = 0;
+					std_regs(p, p->insns + i * 8, &rd, &wr);
+					uint64_t sx[2];
+					int back;
+					const int k = std_succ(p, i, sx, &back);
+					for (int j = 0; j < k; j++)
+						if (sx[j] < n)
+							o |= lin[sx[j]];
+					const uint16_t in = (uint16_t)(rd | (o & ~wr));
+					if (in != lin[i]) {
+						lin[i] = in;
+						changed = 1;
+					}
+				}
+			}
+		}
+		uint64_t sx[2];
+		int back;
+		const int k = std_succ(p, c, sx, &back);
+		for (int j = 0; j < k && !rb; j++)
+			rb = sx[j] < n && ((lin[sx[j]] >> X) & 1);
+	}
+	free(lin);
+	free(seen);
+	return rb;
 }
 
 static int
@@ -1472,6 +1707,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		nthreads = 1;
 	struct wlog *logs = writes ? calloc((size_t)nthreads, sizeof(struct wlog)) : NULL;
 	const int loops = writes && prog_has_loops(p);
+	const int rb = loops && prog_reads_counters(p);
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(+ : total)
 #endif
@@ -1484,6 +1720,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		t_wlog = logs ? &logs[tid] : NULL;
 		t_sequential = p->sequential;
 		t_loops = loops;
+		t_rb = rb;
 		t_ovl = logs && p->checked && !p->sequential ? malloc(sizeof(struct ovl)) : NULL;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
@@ -1503,6 +1740,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 			t_pkt = (uint64_t)i;
 			t_seq = 0;
 			t_writes = 0;
+			t_words.n = 0;
 			if (t_ovl)
 				t_ovl->n = 0;
 			size_t n0 = t_wlog ? t_wlog->n : 0;
@@ -1523,6 +1761,7 @@ oracle_run_batch_hlog(const struct oracle_prog *p, uint8_t *data, const uint64_t
 		t_ovl = NULL;
 		t_sequential = 0;
 		t_loops = 0;
+		t_rb = 0;
 	}
 	if (logs) {
 		/* after the batch: every write in packet order (last writer of a key wins) */

@@ -39,9 +39,9 @@ def _walk_tail(extra_exit=()):
         list(extra_exit) + [I("exit")]
 
 
-def _key_lookup(k=0):
-    """stack[-4] = type & 15; r0 = lookup(map k, &stack[-4]); a miss skips to "N"."""
-    return [I("mov64_reg", 4, 2), I("and64_imm", 4, imm=NKEYS - 1), I("stxw", 10, 4, -4),
+def _key_lookup(k=0, nkeys=NKEYS):
+    """stack[-4] = type & (nkeys - 1); r0 = lookup(map k, &stack[-4]); a miss skips to "N"."""
+    return [I("mov64_reg", 4, 2), I("and64_imm", 4, imm=nkeys - 1), I("stxw", 10, 4, -4),
             ("lddw_map", 1, k), I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4),
             I("call", imm=0), I("ldxb", 3, 7, 1), I("jeq_imm", 0, imm=0, off="N")]
 
@@ -83,6 +83,40 @@ def prog_stores():
         ("label", "N")] + _walk_tail([I("xor64_reg", 0, 9)]))
 
 
+def prog_limiter(thresh=3, nkeys=NKEYS):
+    """The per-option rate limiter (round 6): c = counters[type & (nkeys - 1)] (8-B values); c += 1;
+    counters[type & 15] = c; c > thresh: r0 = 0x1000 + the options before this one, exit — the
+    idiom's register read back, so the packet sees the batch-start count plus its own additions.
+    A walk that ends: r0 = options."""
+    return stdprogs.asm(_walk_head() + _key_lookup(nkeys=nkeys) + [
+        I("ldxdw", 5, 0, 0), I("add64_imm", 5, imm=1), I("stxdw", 0, 5, 0),
+        I("jgt_imm", 5, imm=thresh, off="D"), ("label", "N")] + _walk_tail() +
+        [("label", "D"), I("mov64_imm", 0, imm=0x1000), I("add64_reg", 0, 8), I("exit")])
+
+
+FETCH_KEYS = 64
+
+
+def prog_xadd_fetch():
+    """Per option, on counters[type & 63] (16-B values): old0 = XADD | FETCH word 0 += len,
+    r9 ^= old0; old1 = XADD | FETCH word 1 += 1, r9 += old1 (values as the packet sees them:
+    the batch start plus its own additions).  r0 = options ^ r9.  Two words an option: a walk
+    over more than 16 distinct types passes the 32 words of the packet's view and faults WRITES
+    at the counter update that needs one more (the additions before it land)."""
+    return stdprogs.asm(_walk_head() + _key_lookup(nkeys=FETCH_KEYS) + [
+        I("mov64_reg", 5, 3), (0xdb, 0, 5, 0, 1), I("xor64_reg", 9, 5),
+        I("mov64_imm", 5, imm=1), (0xdb, 0, 5, 8, 1), I("add64_reg", 9, 5), ("label", "N")] +
+        _walk_tail([I("xor64_reg", 0, 9)]))
+
+
+def prog_xadd_then_load():
+    """XADD (no fetch) into counters[type & 15], then a plain load of the same word: a read-back
+    the device does not provide for in a loop (EOPNOTSUPP)."""
+    return stdprogs.asm(_walk_head() + _key_lookup() + [
+        I("mov64_imm", 5, imm=1), (0xdb, 0, 5, 0, 0), I("ldxdw", 5, 0, 0), I("xor64_reg", 9, 5),
+        ("label", "N")] + _walk_tail([I("xor64_reg", 0, 9)]))
+
+
 def packets(n, seed, max_opts=24):
     """64-B packets whose TLV area holds 0..max_opts options, short ones mostly (len & 3 = 0 in
     70 %): most walks end at a type-0 option, some run off the end of the packet (MEM)."""
@@ -116,7 +150,8 @@ def expect(kind, pk, init, vs):
     for p in pk:
         own = bytearray(init)   # the packet's view (its own stores over the batch start)
         adds, writes, fault = [], [], 0
-        n, r9, at = 0, 0, START
+        words = set()           # (limiter, xadd_fetch) the 8-byte words of the packet's view
+        n, r9, at, r0 = 0, 0, START, None
         while True:
             if at >= 64:                      # ldxb type
                 fault = FAULT_MEM
@@ -137,6 +172,23 @@ def expect(kind, pk, init, vs):
                 fault = FAULT_MEM
                 break
             ln = int(p[at + 1])
+            if kind in ("limiter", "xadd_fetch"):
+                k = (t & (FETCH_KEYS - 1 if kind == "xadd_fetch" else NKEYS - 1)) * vs
+                ups = [(k, 1)] if kind == "limiter" else [(k, ln), (k + 8, 1)]
+                for j, (w, add) in enumerate(ups):
+                    if w not in words and len(words) == 32:
+                        fault = FAULT_WRITES
+                        break
+                    words.add(w)
+                    old = _u(own, w, 8)
+                    own[w:w + 8] = ((old + add) & M64).to_bytes(8, "little")
+                    adds.append((w, add))
+                    r9 = r9 ^ old if j == 0 else (r9 + old) & M64
+                if fault:
+                    break
+                if kind == "limiter" and (_u(own, k, 8)) > 3:
+                    r0 = 0x1000 + n
+                    break
             if kind == "xadd":
                 adds += [(k, 1), (k + 8, ln)]
             elif kind == "idiom":
@@ -158,7 +210,8 @@ def expect(kind, pk, init, vs):
         if not fault:
             for k, b in writes:
                 m[k:k + len(b)] = b
-        r0 = n ^ r9 if kind == "stores" else n
+        if r0 is None:
+            r0 = n ^ r9 if kind in ("stores", "xadd_fetch") else n
         ret.append(0 if fault else r0)
         flt.append(fault)
     return np.array(ret, dtype=np.uint64), np.array(flt, dtype=np.uint8), bytes(m)
@@ -181,6 +234,16 @@ def prog_mixed_counter_store():
         _walk_tail())
 
 
-VALUE_SIZE = {"xadd": 16, "idiom": 8, "updates": 8, "stores": 8}
+VALUE_SIZE = {"xadd": 16, "idiom": 8, "updates": 8, "stores": 8, "limiter": 8, "xadd_fetch": 16}
+MAP_KEYS = {"xadd_fetch": FETCH_KEYS}
 PROGS = {"xadd": prog_xadd_counters, "idiom": prog_idiom_counters, "updates": prog_updates,
-         "stores": prog_stores}
+         "stores": prog_stores, "limiter": prog_limiter, "xadd_fetch": prog_xadd_fetch}
+
+
+def initial_map(kind, seed):
+    """the batch-start map of a kind: random bytes; the limiter's counts 0..2"""
+    g = np.random.default_rng(seed)
+    keys = MAP_KEYS.get(kind, NKEYS)
+    if kind == "limiter":
+        return g.integers(0, 3, keys, dtype=np.uint64).tobytes()
+    return g.integers(0, 256, keys * VALUE_SIZE[kind], dtype=np.uint8).tobytes()

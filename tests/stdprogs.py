@@ -287,7 +287,7 @@ def gen_cursor_program(seed):
     return asm(items)
 
 
-def gen_loop_write_program(seed, counters=False):
+def gen_loop_write_program(seed, counters=False, fetched=False):
     """A standard program that writes maps inside loops (include/ebpf_gpu.h "Map writes in a
     device batch"): 1-2 counted loops (trip counts 1-24 from packet bytes, so some packets pass
     the 16 logged writes a packet may make and fault EBPF_FAULT_WRITES), each trip looking up
@@ -299,8 +299,14 @@ def gen_loop_write_program(seed, counters=False):
         NOEXIST: EEXIST, not logged);
       counters=True: XADD (W or DW, aligned, no fetch) into map 0's value, and the LDX / ADD /
         STX idiom on another word whose register is overwritten right after (a dead counter
-        register), no loads back.
+        register), no loads back;
+      fetched=True (round 6; map 0 then has 32-B values, 4 words a key): the counters read
+        back — XADD with BPF_FETCH whose old value r9 mixes in, and the idiom whose register r9
+        mixes in after the STX — so that a packet sees the batch start plus its own additions
+        and a long walk over many keys passes the 32 words of its view (EBPF_FAULT_WRITES).
     r0 mixes the trip count, loaded values and helper return codes."""
+    counters = counters or fetched
+    vs0 = 32 if fetched else 16
     g = np.random.default_rng(seed)
     items = [I("mov64_reg", 6, 1), I("mov64_imm", 0, imm=int(g.integers(0, 2**31))),
              I("mov64_imm", 9, imm=0)]
@@ -318,14 +324,17 @@ def gen_loop_write_program(seed, counters=False):
         for j in range(int(g.integers(1, 4))):
             r = g.random()
             if counters:
-                off = int(g.integers(0, 16 // cw)) * cw
+                off = int(g.integers(0, vs0 // cw)) * cw
                 if r < 0.6:
                     items += [I("mov64_reg", 3, 8), I("add64_imm", 3, imm=int(g.integers(0, 9))),
-                              (0xdb if cw == 8 else 0xc3, 0, 3, off, 0)]
+                              (0xdb if cw == 8 else 0xc3, 0, 3, off, 1 if fetched else 0)]
+                    if fetched:
+                        items += [I("mul64_imm", 9, imm=31), I("add64_reg", 9, 3)]
                 else:
                     ld, st = ("ldxdw", "stxdw") if cw == 8 else ("ldxw", "stxw")
                     items += [I(ld, 5, 0, off), I("add64_imm", 5, imm=int(g.integers(1, 100))),
-                              I(st, 0, 5, off), I("mov64_imm", 5, imm=0)]
+                              I(st, 0, 5, off)]
+                    items += [I("xor64_reg", 9, 5)] if fetched else [I("mov64_imm", 5, imm=0)]
             elif r < 0.45:
                 z = int(g.choice([1, 2, 4, 8]))
                 op = {1: "stxb", 2: "stxh", 4: "stxw", 8: "stxdw"}[z]

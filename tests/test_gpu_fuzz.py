@@ -31,7 +31,7 @@ def fuzz(gpu):
 
 
 @pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites",
-                                  "manywrites"])
+                                  "loopfetched", "manywrites"])
 def test_fuzz_campaign(fuzz, env, mode):
     if mode == "reference":
         failed = fuzz.reference(_args(seed=11), env)
@@ -41,6 +41,8 @@ def test_fuzz_campaign(fuzz, env, mode):
         failed = fuzz.standard(_args(seed=13, programs=80, standard=True), env)
     elif mode == "loopwrites":
         failed = fuzz.loop_writes(_args(seed=15, programs=40), env)
+    elif mode == "loopfetched":   # (counters read back inside loops: 40 of them fetch)
+        failed = fuzz.loop_writes(_args(seed=17, programs=120, fetched=True), env)
     elif mode == "manywrites":   # (more than 16 writes on a loop-free path: no limit)
         failed = fuzz.reference(_args(seed=16, programs=60, manywrites=True), env)
     else:

@@ -288,9 +288,10 @@ def reference(a, env):
 def loop_writes(a, env):
     """--loopwrites: random standard programs that write maps inside loops
     (stdprogs.gen_loop_write_program: stores, loads back, updates, and every third program
-    counter updates; trip counts up to 24, so packets pass the 16 logged writes and fault
-    WRITES) on every variant, staged 64-B packets; results, faults and both maps against the
-    oracle's batch mode."""
+    counter updates — read back, XADD with BPF_FETCH and live idiom registers, with --fetched;
+    trip counts up to 24, so packets pass the 16 logged writes (or the 32 words of the view)
+    and fault WRITES) on every variant, staged 64-B packets; results, faults and both maps
+    against the oracle's batch mode."""
     import stdprogs
     failed = False
     for variant in (0, 1, 2):
@@ -298,8 +299,11 @@ def loop_writes(a, env):
         for k in range(a.programs):
             seed = a.seed * 100000 + k
             g = np.random.default_rng(seed)
-            code, rel = stdprogs.gen_loop_write_program(seed, counters=k % 3 == 2)
-            specs = [(16, 16, g.integers(0, 256, 256, dtype=np.uint8).tobytes()),
+            # (every third program counts; with --fetched, the counters are read back)
+            fetched = k % 3 == 2 and getattr(a, "fetched", False)
+            code, rel = stdprogs.gen_loop_write_program(seed, counters=k % 3 == 2, fetched=fetched)
+            vs0 = 32 if fetched else 16
+            specs = [(vs0, 16, g.integers(0, 256, 16 * vs0, dtype=np.uint8).tobytes()),
                      (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
             n = int(g.choice([1, 64, 65, 777, 4099]))
             pk = g.integers(0, 256, (n, 64), dtype=np.uint8)
@@ -327,8 +331,9 @@ def loop_writes(a, env):
                 bad.append(k)
             if k % 100 == 99:
                 print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        print("loop writes variant %d: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            variant, a.programs, faults, len(bad), bad[:20], time.time() - t0), flush=True)
+        print("loop writes%s variant %d: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+            " (fetched)" if getattr(a, "fetched", False) else "", variant, a.programs, faults, len(bad),
+            bad[:20], time.time() - t0), flush=True)
         failed = failed or bool(bad)
     return failed
 
@@ -341,6 +346,8 @@ def main():
     ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (loops too)")
     ap.add_argument("--mutate", action="store_true", help="randomly edited programs (defined ones)")
     ap.add_argument("--loopwrites", action="store_true", help="map writes inside loops (standard)")
+    ap.add_argument("--fetched", action="store_true",
+                    help="with --loopwrites: the counter programs read their counters back")
     ap.add_argument("--manywrites", action="store_true",
                     help="reference programs with more than 16 map writes on one path")
     a = ap.parse_args()
