@@ -183,11 +183,14 @@ def test_device_loop_writes_vs_oracle(gpu, env, variant, kind, resident):
     np.testing.assert_array_equal(flt, wf)
     np.testing.assert_array_equal(ret, want)
     assert after == wafter
-    if variant == 0:
-        # (a loop program that reads its own stores back keeps 32 overlay words per lane: 256
-        # lanes' slices leave the assembly kernels no room unless the frame is small, so it
-        # may run on the portable HIP interpreter, DESIGN.md "Out of scope")
-        assert ex == "compiled" or (kind in ("stores", "limiter", "xadd_fetch") and ex == "hip")
+    if variant in (0, 2):
+        # (a loop program that reads map values back keeps 32 overlay words per lane, and a
+        # load through a map value the generic handler serves reserves the whole 512-B frame:
+        # 256 lanes' slices leave the assembly kernels no room, so it runs on the portable HIP
+        # interpreter, DESIGN.md "Out of scope".  xadd_fetch has no such load: it runs on the
+        # assembly paths, whose overlay fills and faults WRITES, round 6)
+        want_ex = "compiled" if variant == 0 else "interpreter"
+        assert ex == ("hip" if kind in ("stores", "limiter") else want_ex)
 
 
 @pytest.mark.gpu
