@@ -26,7 +26,9 @@ MEDIAN (the mean, min and max are in the line too; a median above ms_per_step is
 of this script under rocprofv3 --pmc (FETCH_SIZE, then WRITE_SIZE) on the same workload, after
 the timed region (null if rocprofv3 is unavailable or fails; --no-pmc skips them).  Programs on
 the general kernel (divergent, any packet size: C5) get a third pass (SQ_INSTS_VALU / _SALU /
-_VMEM_RD) for roofline.issue, the VALU-issue floor that divergence puts under such a launch.
+_VMEM_RD) for roofline.issue, the VALU-issue floor that divergence puts under such a launch, and
+a fourth (TCP tag accesses, L1->L2 requests, TD busy, GRBM active) for roofline.gather, the floor
+its per-lane loads meet at the rate tools/ubench/gather.hip sustains on C5's address shape.
 
 The same run also measures the other BASELINE configs (--also, default c2,c3,c5,c4h: C2 the
 8-insn ALU program over 1M packets, C3 the 64-insn classifier over 16M, C5 the 256-insn filter over
@@ -63,6 +65,18 @@ from generic_ebpf_amd import native, shard, workloads  # noqa: E402
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 SIMDS, CLOCK_GHZ, VALU_ISSUE_CYCLES = 256 * 4, 2.4, 4  # MI355X: 256 CUs x 4 SIMD16, wave64 VALU
 ISSUE_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD")
+# the gather roofline of a general-kernel line (per-lane loads at run-time addresses): TCP tag
+# accesses (a lane's load is one per 128-B line it touches), L1->L2 read requests, TD busy
+# cycles (summed over the 256 TDs) and GRBM active cycles (summed over the 8 XCDs), one pass
+GATHER_COUNTERS = ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TD_TD_BUSY_sum",
+                   "GRBM_GUI_ACTIVE")
+# Tag accesses per CU cycle the chip sustains on C5's address shape with every lane active:
+# tools/ubench/gather.hip mode 'i' (IMIX 64/576/1500 B packets, 26 loads of 1-8 B per lane at
+# per-class offsets drawn as C5's leaves draw theirs, no divergence, no other work), best
+# occupancy (4 waves per CU: 0.511-0.545 over 7 launches, median 0.517); 16-24 waves per CU,
+# where more lines miss L1, sustain 0.37-0.42 (profiles/r06/gather/README.md)
+GATHER_ACCESSES_PER_CU_CYCLE = 0.517
+CUS = 256
 METRIC = "Mpkt/s device-resident (64-insn filter, 64B pkts); achieved HBM GB/s vs peak"
 # Round-1 calibration in the build container, C4, 1 thread: the genuine reference libebpf.so
 # 9.1 Mpkt/s, this oracle (port) 7.6 Mpkt/s
@@ -363,7 +377,7 @@ def pmc_traffic(a, w, total, layout, cfg=None):
     # general kernels (divergent programs): also the instruction counts of the issue roofline
     passes = [("FETCH_SIZE",), ("WRITE_SIZE",)]
     if layout == 0:
-        passes.append(ISSUE_COUNTERS)
+        passes += [ISSUE_COUNTERS, GATHER_COUNTERS]
     for group in passes:
         counter = group[0]
         d = os.path.join(out, "pmc_%s_%s" % (cfg, counter))
@@ -399,7 +413,7 @@ def pmc_traffic(a, w, total, layout, cfg=None):
         note += "; staged 64-B packet DMA: half its bytes added (gfx950 16-B/lane undercount)"
     return {"bytes": fetch + vals["WRITE_SIZE"], "fetch_reported": vals["FETCH_SIZE"],
             "write": vals["WRITE_SIZE"], "note": note,
-            "insts": {c: vals[c] for c in ISSUE_COUNTERS if c in vals}}, None
+            "insts": {c: vals[c] for c in ISSUE_COUNTERS + GATHER_COUNTERS if c in vals}}, None
 
 
 def issue_roofline(insts, kern_ms, groups):
@@ -420,6 +434,30 @@ def issue_roofline(insts, kern_ms, groups):
             "frac": round(floor_ms / kern_ms, 4) if kern_ms > 0 else None,
             "model": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz), this run's PMC pass" % (
                 VALU_ISSUE_CYCLES, SIMDS, CLOCK_GHZ)}
+
+
+def gather_roofline(insts, kern_ms, groups):
+    """The roofline of per-lane gathers (general kernels): a launch cannot
+    finish before its TCP tag accesses pass at the rate the chip sustains on the same address
+    shape with every lane active and nothing else to do (GATHER_ACCESSES_PER_CU_CYCLE, measured
+    by tools/ubench/gather.hip), at the peak engine clock on every CU.  Beside it: how busy the
+    texture data path was (TD busy cycles per TD / GRBM active cycles per XCD), the L1 miss ratio
+    and the accesses per 64-packet group."""
+    acc = insts.get("TCP_TOTAL_CACHE_ACCESSES_sum")
+    if not acc:
+        return None
+    floor_ms = acc / (GATHER_ACCESSES_PER_CU_CYCLE * CUS * CLOCK_GHZ * 1e9) * 1e3
+    grbm = insts.get("GRBM_GUI_ACTIVE", 0) / 8.0
+    td = insts.get("TD_TD_BUSY_sum", 0) / CUS
+    req = insts.get("TCP_TCC_READ_REQ_sum", 0)
+    return {"bound": "gather", "tag_accesses": int(acc), "accesses_per_group": round(acc / max(1, groups), 1),
+            "l1_miss_ratio": round(req / acc, 4), "td_busy": round(td / grbm, 4) if grbm else None,
+            "accesses_per_cu_cycle": round(acc / (grbm * CUS), 4) if grbm else None,
+            "floor_ms": round(floor_ms, 4), "kernel_ms": round(kern_ms, 4),
+            "frac": round(floor_ms / kern_ms, 4) if kern_ms > 0 else None,
+            "model": "TCP_TOTAL_CACHE_ACCESSES / (%.3f per CU cycle x %d CUs x %.1f GHz): "
+                     "tools/ubench/gather.hip mode i, this run's PMC pass" % (
+                         GATHER_ACCESSES_PER_CU_CYCLE, CUS, CLOCK_GHZ)}
 
 
 def measure(a, cfg, packets, torch, dist, world, rank, local, dev, also=False):
@@ -650,6 +688,8 @@ def main():
             S["traffic"], S["traffic_note"] = (t["bytes"], t["note"]) if t else (None, err)
             S["issue"] = (issue_roofline(t["insts"], S["kern_ms"], (S["n"] + 63) // 64)
                           if t and t["insts"] else None)
+            S["gather"] = (gather_roofline(t["insts"], S["kern_ms"], (S["n"] + 63) // 64)
+                           if t and t["insts"] else None)
         also[c] = {"value": round(S["value"], 1), "unit": "Mpkt/s", "ms_per_step": round(S["ms_per_step"], 4),
                    "steps": S["steps"], "warmup": a.warmup + 10,
                    "packets_total": S["total"], "packets_per_gpu": S["n"], "verified": S["vinfo"].get("verified"),
@@ -661,7 +701,7 @@ def main():
                                 "traffic": S.get("traffic"),
                                 "traffic_note": S.get("traffic_note", "disabled (--no-pmc)"),
                                 "algorithmic_bytes_per_launch": S["bytes_per_launch"],
-                                "issue": S.get("issue")},
+                                "issue": S.get("issue"), "gather": S.get("gather")},
                    "desc": workloads.CONFIGS[c]["desc"]}
 
     if rank == 0:
@@ -669,12 +709,13 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(w, a.cpu_seconds)
         traffic, pmc_note = None, "disabled (--no-pmc)"
-        issue = None
+        issue = gather = None
         if not a.no_pmc:   # (N > 1: rank 0's shard, one launch on its GPU, as the roofline's)
             t, err = pmc_traffic(a, w, n if world > 1 else total, layout)
             traffic, pmc_note = (t["bytes"], t["note"]) if t else (None, err)
             if t and t["insts"]:
                 issue = issue_roofline(t["insts"], kern_ms, (n + 63) // 64)
+                gather = gather_roofline(t["insts"], kern_ms, (n + 63) // 64)
         out = {
             "metric": METRIC,
             "value": round(R["value"], 1), "unit": "Mpkt/s", "n_gpus": world, "steps": a.steps,
@@ -698,7 +739,7 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_samples": R["samples"],
                          "kernel_ms_stats": R["kern_stats"],
                          "algorithmic_bytes_per_launch": R["bytes_per_launch"],
-                         "issue": issue},
+                         "issue": issue, "gather": gather},
             "cpu_baseline": cpu,
             "also": also,
         }

@@ -154,6 +154,89 @@ static void run(int wpc, uint32_t npkt) {
 	hipFree(out);
 }
 
+// C5's address shape without its divergence (round 6, the gather roofline's calibration): IMIX
+// packets (64 / 576 / 1500 B in 7:4:1, each on a 64-B boundary, CSR offsets), every lane loading
+// NL values of 1/2/4/8 bytes at offsets drawn, per size class, uniformly in [18, limit - 8) the
+// way C5's leaves draw theirs (workloads._c5_nodes), all 64 lanes active and no other work.
+constexpr int kImixNL = 26;   // C5: 109.4M TCP tag accesses / 4M packets (profiles/r06/gather/)
+__constant__ uint16_t c_imix_off[3][kImixNL];
+
+__global__ void __launch_bounds__(64) k_imix(const uint8_t *__restrict__ in, const uint64_t *__restrict__ offs,
+					     const uint8_t *__restrict__ cls, uint64_t *__restrict__ out, uint32_t ngroups) {
+	const uint32_t lane = threadIdx.x;
+	for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+		const uint64_t pkt = (uint64_t)g * 64 + lane;
+		const uint8_t *p = in + offs[pkt];
+		const uint32_t c = cls[pkt];
+		uint64_t acc = 0;
+#pragma unroll
+		for (int i = 0; i < kImixNL; i++) {
+			const uint32_t o = c_imix_off[c][i];
+			uint64_t v;
+			switch (i & 3) {
+			case 0: v = *(const uint8_t *)(p + o); break;
+			case 1: v = *(const uint16_t *)(p + (o & ~1u)); break;
+			case 2: v = *(const uint32_t *)(p + (o & ~3u)); break;
+			default: v = *(const uint64_t *)(p + (o & ~7u)); break;
+			}
+			acc = (acc ^ v) * 0x9E3779B1ull;
+		}
+		out[pkt] = acc;
+	}
+}
+
+static void run_imix(int wpc, uint32_t npkt) {
+	std::vector<uint64_t> offs(npkt);
+	std::vector<uint8_t> cls(npkt);
+	uint64_t at = 0, x = 0x9E3779B97F4A7C15ull;
+	const uint32_t limit[3] = {64, 576, 1500};
+	for (uint32_t i = 0; i < npkt; i++) {
+		x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+		const uint32_t r = (uint32_t)(x % 12);   // IMIX 7:4:1
+		cls[i] = r < 7 ? 0 : r < 11 ? 1 : 2;
+		offs[i] = at;
+		at += (limit[cls[i]] + 63) / 64 * 64;
+	}
+	uint16_t tab[3][kImixNL];
+	for (int c = 0; c < 3; c++)
+		for (int i = 0; i < kImixNL; i++) {
+			x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+			tab[c][i] = (uint16_t)(18 + x % (limit[c] - 26));
+		}
+	hipMemcpyToSymbol(HIP_SYMBOL(c_imix_off), tab, sizeof(tab));
+	uint8_t *in, *d_cls;
+	uint64_t *d_offs, *out;
+	hipMalloc(&in, at + 64);
+	hipMemset(in, 0x5b, at + 64);
+	hipMalloc(&d_offs, npkt * 8ull);
+	hipMalloc(&d_cls, npkt);
+	hipMalloc(&out, npkt * 8ull);
+	hipMemcpy(d_offs, offs.data(), npkt * 8ull, hipMemcpyHostToDevice);
+	hipMemcpy(d_cls, cls.data(), npkt, hipMemcpyHostToDevice);
+	const int grid = 256 * wpc;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int w = 0; w < 2; w++)
+		k_imix<<<grid, 64>>>(in, d_offs, d_cls, out, npkt / 64);
+	hipEventRecord(a);
+	const int reps = 5;
+	for (int r = 0; r < reps; r++)
+		k_imix<<<grid, 64>>>(in, d_offs, d_cls, out, npkt / 64);
+	hipEventRecord(b);
+	hipEventSynchronize(b);
+	float ms = 0;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= reps;
+	printf("IMIX NL=%d waves/CU=%2d  %.4f ms  %.2f lane-loads/ns  %.1f GB/s of packets\n", kImixNL, wpc, ms,
+	       (double)npkt * kImixNL / (ms * 1e6), (double)at / (ms * 1e6));
+	fflush(stdout);
+	hipFree(in);
+	hipFree(d_offs);
+	hipFree(d_cls);
+	hipFree(out);
+}
+
 int main(int argc, char **argv) {
 	const uint32_t n = 1u << 22;
 	if (argc > 1 && argv[1][0] == 'f') {   // flat-to-LDS study
@@ -163,6 +246,18 @@ int main(int argc, char **argv) {
 			run<576, 56, 7>(w, n);
 		}
 		run<576, 56, 0>(8, n);
+		return 0;
+	}
+	if (argc > 1 && argv[1][0] == 'i') {   // C5's shape: the gather roofline's calibration
+		for (int w : {4, 8, 16, 24})
+			run_imix(w, n);
+		return 0;
+	}
+	if (argc > 1 && argv[1][0] == 'c') {   // the counters of the per-class gathers (round 6)
+		run<576, 56, 0>(8, n);
+		run<576, 56, 1>(8, n);
+		run<1536, 56, 0>(8, n);
+		run<64, 56, 0>(8, n);
 		return 0;
 	}
 	for (int w : {8, 24}) {
