@@ -59,7 +59,9 @@ struct ebpf_map;
  *     EBPF_FAULT_BAD_MAP (the reference dereferences it);
  *   - a loop-free program makes every write its path reaches, however many, as the reference
  *     does (the log is sized by the program's longest path).  A program with loops (standard
- *     semantics: a backward jump) has no per-path bound, so there a packet may make 16 logged
+ *     semantics: a backward jump reachable from slot 0 on the slot graph — not JA -1, which
+ *     spins into EBPF_FAULT_LOOP, nor a jump before slot 0, EBPF_FAULT_SLOT; decided from the
+ *     bytecode) has no per-path bound, so there a packet may make 16 logged
  *     writes: map_update_elem calls that return 0, every hashtable map_delete_elem (whether the
  *     key exists is known only at the replay), and stores into map values; counter updates
  *     aligned to their width (below) are not counted (they are additions).  The 17th faults the
