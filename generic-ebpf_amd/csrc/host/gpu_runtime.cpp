@@ -105,6 +105,11 @@ struct rows_slot {
 	std::vector<hipEvent_t> ev;
 	bool per_thread = false; // hipStreamPerThread: `stream` names a different stream per thread
 };
+// A batch's hold on its stream slot's winner words (upd_acquire -> upd_settled)
+struct upd_owner {
+	rows_slot *slot = nullptr;
+	unsigned long long sid = 0;
+};
 std::mutex g_rows_lock;
 std::vector<std::vector<rows_slot>> g_rows; // per device (capacity kRowsMax: slots never move)
 uint64_t g_rows_tick = 0;
@@ -214,7 +219,7 @@ grow_zeroed(void **p, size_t *have, size_t need)
 // The stream's map-write log (>= log_bytes) and winner words (>= win_bytes).
 int
 upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, uint8_t **log,
-	    unsigned long long **win, bool **pending)
+	    unsigned long long **win, upd_owner *owner)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
 	rows_slot *r;
@@ -232,17 +237,19 @@ upd_acquire(int device, hipStream_t stream, size_t log_bytes, size_t win_bytes, 
 	r->win_pending = true;
 	*log = static_cast<uint8_t *>(r->log);
 	*win = static_cast<unsigned long long *>(r->win);
-	*pending = &r->win_pending;
+	owner->slot = r;
+	owner->sid = r->sid;
 	return 0;
 }
 
-// The batch's apply step is enqueued: the winner words will be zero again after it
+// The batch's apply step is enqueued: the winner words will be zero again after it (unless the
+// slot went to another stream meanwhile: that stream's flag is its own)
 void
-upd_settled(bool *pending)
+upd_settled(const upd_owner &o)
 {
 	std::lock_guard<std::mutex> g(g_rows_lock);
-	if (pending)
-		*pending = false;
+	if (o.slot && o.slot->sid == o.sid)
+		o.slot->win_pending = false;
 }
 
 // The leading stream's multi-device scratch: `rows` histogram rows and `nev` events.
@@ -666,7 +673,7 @@ struct upd_plan {
 	uint64_t pkt_base = 0;
 	uint32_t *faulted = nullptr; // one bit per packet of the batch (after the records)
 	size_t faulted_bytes = 0;
-	bool *win_pending = nullptr; // the stream slot's flag (upd_acquire)
+	upd_owner owner;             // the stream slot whose winner words it uses (upd_acquire)
 	// per table map, the device table its launches read (hashtables whose values the batch
 	// stores into: a record names a slot, and this is the slot's key whatever is uploaded later)
 	std::vector<std::shared_ptr<const std::vector<uint8_t>>> tables;
@@ -696,7 +703,7 @@ upd_plan_for(struct ebpf_prog *ep, dprog_device *dp, uint64_t count, hipStream_t
 	int err = upd_size(ep, dp, count, &P->cap, &bytes, &boff, &bbytes);
 	if (!err)
 		err = upd_acquire(dp->device, stream, bytes, dp->win_words * 8, &P->log, &P->win,
-				  &P->win_pending);
+				  &P->owner);
 	if (err)
 		return fail(err, "map-write log");
 	P->faulted = reinterpret_cast<uint32_t *>(P->log + boff);
@@ -730,7 +737,7 @@ upd_apply(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_t
 					 (uint32_t)dp->upd_host.size(), P.win, P.faulted, stream);
 	if (e != hipSuccess)
 		return hip_fail(e, "map writes");
-	upd_settled(P.win_pending);
+	upd_settled(P.owner);
 	for (uint16_t t : dev)
 		map_mark_device_write(ep->xlated->maps[t], dp->device, static_cast<void *>(stream));
 	return 0;
@@ -956,7 +963,7 @@ upd_finish(struct ebpf_prog *ep, dprog_device *dp, const upd_plan &P, hipStream_
 		if ((err = upd_apply(ep, dp, P, stream)))
 			return err;
 	} else {
-		upd_settled(P.win_pending); // (no offer kernel ran: the winner words are untouched)
+		upd_settled(P.owner); // (no offer kernel ran: the winner words are untouched)
 	}
 	return host ? upd_apply_host(ep, logs, false) : 0;
 }
@@ -1644,7 +1651,7 @@ run_host_shard(struct ebpf_prog *ep, dprog_device *dp, staging &S,
 	if (prog_writes_maps(*ep->xlated) && hi > lo) {
 		if (log_out) { // (several shards: the caller merges the logs; no offer kernel runs)
 			if ((err = upd_fetch(dp, plan, S.stream[0], lo, log_out)) == 0)
-				upd_settled(plan.win_pending);
+				upd_settled(plan.owner);
 			return err;
 		}
 		if ((err = upd_finish(ep, dp, plan, S.stream[0])))
@@ -1830,7 +1837,7 @@ ebpf_prog_run_batch_multi_dev(struct ebpf_prog *ep, int ndev, const int *devices
 			hipSetDevice(devices[d]);
 			rc = upd_fetch(ep->dev[devices[d]].get(), plan, st[d], first, &logs[d]);
 			if (rc == 0) // (merged on the host: no offer kernel runs)
-				upd_settled(plan.win_pending);
+				upd_settled(plan.owner);
 		}
 		return rc;
 	};

@@ -287,20 +287,22 @@ static __thread int t_rb;         /* ... and reads its counter updates back (pro
 #define ORACLE_OVL_WORDS 32u  /* the packet's own view: 8-byte words of map values (DP_OVL_MAX) */
 static __thread struct {
 	uint32_t n;
-	uint64_t w[ORACLE_OVL_WORDS]; /* map index << 40 | word index within the map's values */
+	uint64_t w[ORACLE_OVL_WORDS]; /* map index << 56 | element << 16 | word within the value(s) */
 } t_words;
 
 /* A program with loops that reads its counter updates back keeps the packet's view of the map
  * values it changed in 32 words (ebpf_oracle.h): the store or counter update of `size` bytes at
- * byte `off` of map mi's values takes the 8-byte words it touches that the packet has not yet
- * touched; F_WRITES when they do not fit (before anything happens), else 0. */
+ * byte `voff` of element `elem`'s value (arrays: elem 0 and voff from the first value — their
+ * values are contiguous; hashtables: each value starts on 8 bytes, as the device's slots place
+ * them) takes the 8-byte words it touches that the packet has not yet touched; F_WRITES when
+ * they do not fit (before anything happens), else 0. */
 static int
-take_words(int mi, uint64_t off, int size)
+take_words(int mi, uint64_t elem, uint64_t voff, int size)
 {
 	uint64_t need[2];
 	uint32_t k = 0;
-	for (uint64_t w = off >> 3; w <= (off + (uint64_t)size - 1) >> 3; w++) {
-		const uint64_t key = (uint64_t)mi << 40 | w;
+	for (uint64_t w = voff >> 3; w <= (voff + (uint64_t)size - 1) >> 3; w++) {
+		const uint64_t key = (uint64_t)mi << 56 | elem << 16 | w;
 		uint32_t i = 0;
 		while (i < t_words.n && t_words.w[i] != key)
 			i++;
@@ -421,7 +423,9 @@ value_store(const struct region_env *re, int mi, uint64_t addr, int size, uint64
 			return f;
 	}
 	if (t_loops && t_rb) {
-		int f = take_words(mi, addr - (uint64_t)(uintptr_t)m->data, size);
+		const uint64_t o = addr - (uint64_t)(uintptr_t)m->data;
+		int f = m->kind == ORACLE_MAP_HASH ? take_words(mi, o / m->value_size, o % m->value_size, size)
+						   : take_words(mi, 0, o, size);
 		if (f)
 			return f;
 	}
