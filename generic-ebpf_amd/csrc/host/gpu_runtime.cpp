@@ -1068,14 +1068,15 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		// that only stream packets run 4 (and are the ones write phasing serves); one that probes
 		// hashtables runs 5 (C4H 1.49 -> 1.46 ms against 6, 1.53 at 4, profiles/r05/c4h_occ/).
 		// The interpreter (fn == NULL) is bound by its scalar dispatch and wants every wave: C4
-		// 1.86 -> 1.42 ms at 6 instead of 4 (profiles/r02/v2occ).  So is a program with loops
-		// (C3L 0.305 -> 0.277 ms at 6, profiles/r04/c3l_occ)
+		// 1.86 -> 1.42 ms at 6 instead of 4 (profiles/r02/v2occ).  A compiled program with loops
+		// runs 5, as a probing one does (C3L 0.2238 -> 0.2160 ms against 6, 0.241 at 4, three
+		// runs each, profiles/r06/c3l_occ/; round 4's code had gained from 4 to 6)
 		bool hash = false;
 		for (const dp_map &m : dp->table)
 			hash = hash || (m.flags & DP_MAP_HASH) != 0;
 		uint32_t wg_cap = 0;
-		if (mode == 1 && fn && !ep->xlated->has_loops)
-			wg_cap = hash ? kProbeWorkgroups : kStreamWorkgroups;
+		if (mode == 1 && fn)
+			wg_cap = (hash || ep->xlated->has_loops) ? kProbeWorkgroups : kStreamWorkgroups;
 		e = launch_interp_asm(L, stream, dp->device, mode, dp->map_lds_bytes, fn,
 				      fn ? dp->jit_fn_wide : nullptr, wg_cap, ev_start, ev_stop, user_hist,
 				      hist_overwrite);
