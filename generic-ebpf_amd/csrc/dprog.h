@@ -192,8 +192,15 @@ struct dp_launch {
 	// slots are full, so that result writes and packet reads reach HBM in separate phases.
 	// 0 = off: results written once per superblock
 	uint32_t wphase;
-	uint32_t reserved5[3];
-	void *reserved6;
+	// a loop-free program that reads back more stores into map values than DP_OVL_MAX words hold
+	// (the portable HIP interpreter only): every lane's overlay in global memory, ovl_cap
+	// {address, word} entries per lane at ovl_spill + 16 * ovl_cap * (lane's index in the launch);
+	// 0 = the lane's own DP_OVL_MAX entries.  The launch runs in chunks of ovl_chunk packets
+	// (what the buffer holds), in stream order
+	uint32_t ovl_cap;
+	uint32_t ovl_chunk;
+	uint32_t reserved5;
+	uint8_t *ovl_spill;
 };
 static_assert(sizeof(dp_launch) == 232, "dp_launch layout is shared with the assembly kernels");
 static_assert(offsetof(dp_launch, vflags) == 0xcc, "gen_interp.py VFLAGS_OFF");
@@ -208,7 +215,8 @@ static_assert(offsetof(dp_launch, wphase) == 0xd0, "gen_interp.py WPHASE_OFF");
 #define DP_OVL_SCRATCH 8u
 #define DP_WCOUNT 16u
 #define DP_OVL_ENTRIES 24u
-#define DP_OVL_MAX 32u // overlay entries per lane at most (more: the program runs on the CPU)
+#define DP_OVL_MAX 32u // overlay entries per lane kept on chip (more: dp_launch.ovl_spill)
+#define DP_OVL_SPILL_MAX 4096u // ... spilled entries per lane at most (more: EOPNOTSUPP)
 // Logged writes a packet may make in a device batch (ebpf_gpu.h "Map writes in a device batch":
 // successful map_update_elem / map_delete_elem calls and stores into map values other than
 // aligned counter updates); the next one faults EBPF_FAULT_WRITES.  Checked on the device only

@@ -81,11 +81,15 @@ check(const regions &rg, const dp_launch &L, uint64_t a, uint32_t size, bool wri
 }
 
 // The packet's own stores into map values (dp_launch.vflags bit 0): whole 8-byte words of the
-// mirror as the packet sees them (dprog.h DP_OVL_*), newest last.
+// mirror as the packet sees them (dprog.h DP_OVL_*), newest last — in the lane's own DP_OVL_MAX
+// entries, or in its slice of dp_launch.ovl_spill (a loop-free program that reads back more)
 struct overlay {
 	uint32_t n = 0;
-	uint64_t addr[DP_OVL_MAX];
-	uint64_t data[DP_OVL_MAX];
+	uint32_t cap = DP_OVL_MAX;
+	uint64_t *addr;
+	uint64_t *data;
+	uint64_t own_addr[DP_OVL_MAX];
+	uint64_t own_data[DP_OVL_MAX];
 };
 
 // `size` bytes at a: the mirror's (the batch-start values) with the packet's own stores over them
@@ -116,7 +120,7 @@ ovl_store(overlay &o, uint64_t a, uint32_t size, uint64_t v)
 			k++;
 		fresh += k == o.n;
 	}
-	if (o.n + fresh > DP_OVL_MAX)
+	if (o.n + fresh > o.cap)
 		return false;
 	for (uint32_t i = 0; i < size; i++) {
 		const uint64_t b = a + i, w = b & ~7ull;
@@ -124,7 +128,7 @@ ovl_store(overlay &o, uint64_t a, uint32_t size, uint64_t v)
 		while (k < o.n && o.addr[k] != w)
 			k++;
 		if (k == o.n) {
-			if (o.n == DP_OVL_MAX)
+			if (o.n == o.cap)
 				return false;
 			o.addr[k] = w;
 			o.data[k] = *reinterpret_cast<const uint64_t *>(w); // (mirrors are padded to 8)
@@ -296,6 +300,14 @@ ebpf_interp_v0(dp_launch L)
 	uint64_t result = 0;
 	uint32_t back = 0; // taken backward jumps (DK_LOOPCNT, standard semantics)
 	overlay ovl;       // stores into map values the packet reads back (dp_launch.vflags)
+	if (L.ovl_cap) {
+		ovl.cap = L.ovl_cap;
+		ovl.addr = reinterpret_cast<uint64_t *>(L.ovl_spill + (uint64_t)16 * L.ovl_cap * gid);
+		ovl.data = ovl.addr + L.ovl_cap;
+	} else {
+		ovl.addr = ovl.own_addr;
+		ovl.data = ovl.own_data;
+	}
 	uint32_t writes = 0; // logged writes (DP_VF_WCAP)
 
 	for (;;) {
@@ -664,7 +676,24 @@ launch_interp_v0(const dp_launch &L, hipStream_t stream)
 {
 	if (L.count == 0)
 		return hipSuccess;
-	const uint64_t blocks = (L.count + kWG - 1) / kWG;
-	hipLaunchKernelGGL(ebpf_interp_v0, dim3((unsigned)blocks), dim3(kWG), 0, stream, L);
-	return hipGetLastError();
+	// (a spilled overlay: in chunks of the packets its buffer holds, launched in stream order)
+	const uint64_t chunk = L.ovl_cap ? L.ovl_chunk : L.count;
+	for (uint64_t c0 = 0; c0 < L.count; c0 += chunk) {
+		dp_launch C = L;
+		C.count = L.count - c0 < chunk ? L.count - c0 : chunk;
+		if (L.offsets)
+			C.offsets = L.offsets + ((L.vflags & DP_VF_EXTENTS) ? 2 * c0 : c0);
+		else
+			C.data = L.data + c0 * L.stride;
+		C.ret = L.ret + c0;
+		if (L.faults)
+			C.faults = L.faults + c0;
+		C.pkt_base = L.pkt_base + c0;
+		const uint64_t blocks = (C.count + kWG - 1) / kWG;
+		hipLaunchKernelGGL(ebpf_interp_v0, dim3((unsigned)blocks), dim3(kWG), 0, stream, C);
+		hipError_t e = hipGetLastError();
+		if (e != hipSuccess)
+			return e;
+	}
+	return hipSuccess;
 }

@@ -98,6 +98,9 @@ struct rows_slot {
 	// a batch's log was handed out and its apply step has not been enqueued since: its offer
 	// kernel may have left winner words set, so the next batch clears them first
 	bool win_pending = false;
+	// the portable interpreter's spilled overlays (dp_launch.ovl_spill), grown on demand
+	void *ovl = nullptr;
+	size_t ovl_bytes = 0;
 	// ebpf_prog_run_batch_multi_dev, when this stream leads its device: one histogram row per
 	// shard on the device (any contents: every launch overwrites its row), and fork/join events
 	void *mh = nullptr;
@@ -195,7 +198,26 @@ rows_acquire(int device, hipStream_t stream, void **out)
 	return err;
 }
 
-// grow a zero-initialised buffer (synchronous: hipFree waits for the device)
+int grow_zeroed(void **p, size_t *have, size_t need);
+
+// The stream's spilled-overlay buffer of at least `bytes`
+int
+ovl_acquire(int device, hipStream_t stream, size_t bytes, uint8_t **out)
+{
+	std::lock_guard<std::mutex> g(g_rows_lock);
+	rows_slot *r;
+	int err = slot_for(device, stream, &r);
+	if (!err)
+		err = grow_zeroed(&r->ovl, &r->ovl_bytes, bytes);
+	if (!err)
+		*out = static_cast<uint8_t *>(r->ovl);
+	return err;
+}
+
+// grow a zero-initialised buffer (synchronous: hipFree waits for the device, and so does the
+// zeroing — hipMemset of device memory may return before it is done, and the launches that use
+// the buffer run on streams that do not wait for the null stream: a 1-GiB spilled-overlay buffer
+// was still being zeroed under the first kernel that wrote it)
 int
 grow_zeroed(void **p, size_t *have, size_t need)
 {
@@ -207,7 +229,7 @@ grow_zeroed(void **p, size_t *have, size_t need)
 	*have = 0;
 	if (hipMalloc(p, need) != hipSuccess)
 		return ENOMEM;
-	if (hipMemset(*p, 0, need) != hipSuccess) {
+	if (hipMemset(*p, 0, need) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
 		hipFree(*p);
 		*p = nullptr;
 		return ENOMEM;
@@ -363,6 +385,8 @@ ensure_map_mirror(struct ebpf_map *em, int device, void **dev)
 		hipError_t e = hipMalloc(&m.dev, bytes);
 		if (e == hipSuccess && !em->is_hashtable())
 			e = hipMemset(m.dev, 0, bytes);
+		if (e == hipSuccess) // (done before any stream uses it: grow_zeroed)
+			e = hipDeviceSynchronize();
 		if (e != hipSuccess)
 			return hip_fail(e, "hipMalloc(map mirror)");
 		m.version = ~0ull;
@@ -938,6 +962,8 @@ delta_merge_host(struct ebpf_prog *ep, int ndev, const int *devices)
 				e = hipMemcpy(d.data(), da, bytes, hipMemcpyDeviceToHost);
 			if (e == hipSuccess)
 				e = hipMemset(da, 0, bytes);
+			if (e == hipSuccess) // (done before the next launch's atomics: grow_zeroed)
+				e = hipDeviceSynchronize();
 			if (e != hipSuccess)
 				return hip_fail(e, "counter updates copy");
 			for (size_t o = 0; o < bytes; o += w)
@@ -979,7 +1005,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 	L.nentries = dp->nentries;
 	L.start = ep->xlated->start;
 	L.vflags = (ep->xlated->vstore_overlay ? 1u : 0u) | (ep->xlated->vstore_sites ? 2u : 0u) |
-		   (ep->xlated->ovl_entries << 8) | (L0.vflags & DP_VF_EXTENTS) |
+		   (std::min<uint32_t>(ep->xlated->ovl_entries, 255u) << 8) | (L0.vflags & DP_VF_EXTENTS) |
 		   (ep->xlated->write_cap ? DP_VF_WCAP : 0u);
 	launch_order order(ep->xlated->maps);
 	int err = sync_map_mirrors(ep, dp->device, stream);
@@ -1027,6 +1053,10 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		}
 		asm_fits = asm_lds_fits(mode, dp->map_lds_bytes, stride);
 	}
+	// an overlay larger than the lanes keep on chip: the portable interpreter, spilled
+	const bool spill = ep->xlated->vstore_overlay && ep->xlated->ovl_entries > DP_OVL_MAX;
+	if (spill)
+		asm_fits = false;
 	if ((variant == 0 || variant == 2) && asm_fits) {
 		// variant 0: the compiled program; a program too large for the code area runs on the
 		// assembly interpreter instead (still the device path).  Programs with loops compile
@@ -1088,9 +1118,20 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		    (e = hipMemsetAsync(L.hist, 0, EBPF_HIST_BINS * sizeof(uint64_t), stream)) !=
 			hipSuccess)
 			return hip_fail(e, "hipMemsetAsync(hist)");
+		if (spill) { // (chunks whose overlays fit 1 GiB)
+			const uint64_t per = 16ull * ep->xlated->ovl_entries;
+			uint64_t chunk = std::max<uint64_t>(256, ((1ull << 30) / per) & ~255ull);
+			chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(L.count, 1));
+			uint8_t *buf = nullptr;
+			if ((err = ovl_acquire(dp->device, stream, chunk * per, &buf)))
+				return fail(err, "spilled overlay");
+			L.ovl_cap = ep->xlated->ovl_entries;
+			L.ovl_chunk = (uint32_t)chunk;
+			L.ovl_spill = buf;
+		}
 		if (ev_start)
 			hipEventRecord(ev_start, stream);
-		e = launch_interp_v0(L, stream); // (one kernel: its histogram is added in-kernel)
+		e = launch_interp_v0(L, stream); // (one kernel per chunk: the histogram is added in-kernel)
 		if (ev_stop)
 			hipEventRecord(ev_stop, stream);
 	}

@@ -1575,7 +1575,9 @@ analyze_writes(dprog_host &out)
 		out.max_updates = logging ? DP_WRITES_MAX : 0;
 		out.ovl_entries = out.vstore_overlay ? 2 * DP_WRITES_MAX : 0;
 	}
-	if (out.ovl_entries > DP_OVL_MAX) {
+	// (a loop-free path with more than DP_OVL_MAX / 2 stores read back runs on the portable
+	// interpreter with its overlay spilled to memory, 16 B an entry per lane)
+	if (out.ovl_entries > DP_OVL_SPILL_MAX) {
 		out.error = EOPNOTSUPP;
 		out.error_msg = "the program stores into map values and reads them back more often on one "
 				"path than the device overlay holds (run it with ebpf_prog_run)";

@@ -80,7 +80,9 @@ struct ebpf_map;
  * (ebpf_interpreter.c:343-366).  In a device batch:
  *   - a packet's loads (LDX, and the load of a counter update or XADD below) see its own
  *     earlier stores into map values; other packets of the batch see the batch-start maps.
- *     Helper calls read keys and values as the batch started;
+ *     Helper calls read keys and values as the batch started.  (A loop-free path may store and
+ *     read back up to 2,048 times; past 16 such stores the batch runs on the portable
+ *     interpreter, the packets' views in device memory.  Loops: below);
  *   - after the batch the stores land in packet order, a packet's own in program order, byte by
  *     byte: the last store of each byte wins (together with map_update_elem's whole values);
  *   - counter updates land as additions: three consecutive instructions (JA aside)

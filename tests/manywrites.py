@@ -89,6 +89,17 @@ def prog_stores(count, vs, kmask=15):
     return assemble(_lookup(I, LdDw, MapRef, Branch, kmask) + _stores(I, count, vs) + _exit_with(I, 8))
 
 
+def prog_readback(count, vs, kmask=15):
+    """prog_stores, then the value read back (its first 8 bytes, and its last 8): the packet sees
+    its own stores, so the device keeps an overlay of 2 words per store on the path — past
+    DP_OVL_MAX (16 stores) spilled to memory on the portable interpreter.  r0 = the two words
+    xor the evolving register."""
+    I, LdDw, MapRef, Branch, assemble = _nodes()
+    n = _lookup(I, LdDw, MapRef, Branch, kmask) + _stores(I, count, vs)
+    n += [I("ldxdw", 7, 0, 0), I("xor64_reg", 8, 7), I("ldxdw", 7, 0, vs - 8), I("xor64_reg", 8, 7)]
+    return assemble(n + _exit_with(I, 8))
+
+
 def prog_updates(count, kmask=3):
     """map 0: (kmask + 1) * 64 entries of 8 bytes"""
     I, LdDw, MapRef, Branch, assemble = _nodes()
@@ -130,6 +141,14 @@ CASES = {
     "updates17": (lambda: prog_updates(17), 8, 4 * KEYS_PER_PKT),
     "updates40": (lambda: prog_updates(40), 8, 4 * KEYS_PER_PKT),
     "mixed17_17": (lambda: prog_mixed(17, 17), 8, 4 * KEYS_PER_PKT),
+}
+
+# stores read back (the overlay past DP_OVL_MAX: spilled, portable interpreter)
+READBACK = {
+    "readback16": (lambda: prog_readback(16, 16), 16, 16),
+    "readback17": (lambda: prog_readback(17, 16), 16, 16),
+    "readback40": (lambda: prog_readback(40, 72), 72, 16),
+    "readback120": (lambda: prog_readback(120, 200), 200, 16),
 }
 
 

@@ -9,7 +9,10 @@ held-back writes cannot change a result), the round-5 probe's known answer, a st
 loop-free program past 16 writes, and the translation (no EOPNOTSUPP, no cap).
 GPU: every variant, staged (64-B stride) and general (CSR offsets) kernels, host-buffer and
 device-resident: results, faults and the map against the oracle's batch mode, and against the
-sequential mode for batches whose packets write distinct keys."""
+sequential mode for batches whose packets write distinct keys.
+Stores read back (manywrites.READBACK, round 6): past 16 stores on a path the overlay of the
+packet's own stores no longer fits on chip; the portable interpreter runs them with the overlay
+spilled to memory (dp_launch.ovl_spill), on every variant, in chunks of its buffer."""
 import ctypes
 import os
 
@@ -104,9 +107,9 @@ class _Info(ctypes.Structure):
                 ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
 
 
-@pytest.mark.parametrize("case", sorted(mw.CASES))
+@pytest.mark.parametrize("case", sorted(mw.CASES) + sorted(mw.READBACK))
 def test_translation_accepts_many_writes(native, env, case):
-    mk, vs, me = mw.CASES[case]
+    mk, vs, me = (mw.CASES.get(case) or mw.READBACK[case])
     lay = mk()
     m = native.Map(env, me, vs)
     p = native.Prog(env, lay.patched([m.handle]))
@@ -200,3 +203,53 @@ def test_device_distinct_keys_equal_sequential_reference(gpu, env, variant, case
     np.testing.assert_array_equal(flt, sflt)
     np.testing.assert_array_equal(ret, sret)
     assert after == safter
+
+
+def test_oracle_readback_sees_own_stores():
+    """the read-back programs: r0 from the packet's own stores over the batch-start value, the
+    same in the batch and the reference's sequential run when no two packets share a key"""
+    for name, (mk, vs, me) in sorted(mw.READBACK.items()):
+        lay = mk()
+        pk = mw.distinct_key_packets(16, 21)
+        init = _init(vs, me, 22)
+        ret, flt, after = _oracle(lay, vs, me, init, pk.reshape(-1), 16, 64)
+        sret, sflt, safter = _oracle(lay, vs, me, init, pk.reshape(-1), 16, 64, sequential=True)
+        assert not flt.any(), name
+        np.testing.assert_array_equal(ret, sret)
+        assert after == safter, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("layout", ["staged", "general"])
+@pytest.mark.parametrize("case", sorted(mw.READBACK))
+def test_device_readback_vs_oracle(gpu, env, variant, layout, case):
+    """past 16 stores read back the overlay is spilled and the portable interpreter runs it (every
+    variant); readback120 over 300,007 packets runs in two chunks of the 1-GiB spill buffer"""
+    mk, vs, me = mw.READBACK[case]
+    lay = mk()
+    n = 300007 if case == "readback120" and layout == "staged" else (1 << 14) + 13
+    pk = mw.packets(n, 23)
+    init = _init(vs, me, 24)
+    if layout == "staged":
+        data, stride, offs = pk.reshape(-1), 64, None
+    else:
+        (data, offs), stride = _ragged(pk, 25), 0
+    want, wf, wafter = _oracle(lay, vs, me, init, data, n, stride, offs)
+    assert not wf.any()
+    ret, flt, after = _device(gpu, lay, vs, me, init, env, data, n, stride, offs, variant, False)
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == wafter
+    m = gpu.Map(env, me, vs)
+    p = gpu.Prog(env, lay.patched([m.handle]))
+    try:
+        gpu.set_variant(variant)
+        p.run_batch(np.ascontiguousarray(pk[:64].reshape(-1)), 64, 64)
+        ex = p.exec_info(0)[0]
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()
+    if case != "readback16" or variant == 1:   # (16 stores still fit the lanes' own overlay)
+        assert ex == "hip"
