@@ -1528,22 +1528,20 @@ def vstore_routine():
          "s_andn2_b64 exec, %s, exec" % sp(S_MASK),                # the lanes left: records
          ".Lvs_rec:",
          "s_cbranch_execz .Lvs_ret",
-         # capped writes (vflags bit 4, DP_VF_WCAP): a plain store (ADD = 0; an aligned addition
-         # is not counted) counts in the lane's slice; the one past WRITES_MAX faults
+         # capped writes (vflags bit 4, DP_VF_WCAP): every record (the lanes here: a DP_MAP_ATOMIC
+         # map's additions went to its delta area above) counts in the lane's slice; the one past
+         # WRITES_MAX faults
          "s_load_dword %s, s[0:1], 0x%x" % (s(S_T3), VFLAGS_OFF),
          "s_waitcnt lgkmcnt(0)",
          "s_bitcmp1_b32 %s, 4" % s(S_T3),
          "s_cbranch_scc0 .Lvs_wc_ok",
-         "v_cmp_eq_u32_e64 vcc, 0, %s" % v(ADD),
-         "s_and_saveexec_b64 %s, vcc" % sp(S_MASK),
-         "s_cbranch_execz .Lvs_wc_none",
+         "s_mov_b64 %s, exec" % sp(S_MASK),
          "v_add_u32 %s, %d, v%d" % (v(R[1]), WCOUNT, V_STK),
          "v_mov_b32 %s, 1" % v(R[9]),
          "ds_add_rtn_u32 %s, %s, %s" % (v(R[9]), v(R[1]), v(R[9])),
          "s_waitcnt lgkmcnt(0)",
          "v_cmp_le_u32_e64 vcc, %d, %s" % (WRITES_MAX, v(R[9])),
-         "s_and_b64 vcc, vcc, exec",
-         ".Lvs_wc_none:",                         # (vcc = the lanes past the cap, or none)
+         "s_and_b64 vcc, vcc, exec",              # (vcc = the lanes past the cap)
          "s_mov_b64 exec, %s" % sp(S_MASK),
          "s_andn2_b64 exec, exec, vcc",
          "s_or_b64 %s, %s, vcc" % (sp(S_JUNK), sp(S_JUNK)),

@@ -234,13 +234,14 @@ value_store(const dp_launch &L, uint64_t gid, overlay &o, uint32_t &writes, int 
 		voff = (off & ((1ull << lg) - 1)) - dp_hash_value_off(dp_hash_key_size(mp.flags));
 	}
 	add = add && voff % size == 0;
-	if (!add && over_cap(L, writes)) // (aligned additions are not counted)
+	const bool atomic = add && (mp.flags & DP_MAP_ATOMIC);
+	if (!atomic && over_cap(L, writes)) // (every record counts; device atomics do not)
 		return F_WRITES;
 	// (a full overlay: only a program with loops that reads its counters back can fill it —
 	// ebpf_gpu.h, 32 words — the write that needs one more faults WRITES before it happens)
 	if ((L.vflags & 1) && !ovl_store(o, a, size, v))
 		return F_WRITES;
-	if (add && (mp.flags & DP_MAP_ATOMIC)) {
+	if (atomic) {
 		uint8_t *d = reinterpret_cast<uint8_t *>(mp.dev_base) + dp_delta_off(mp.value_size, mp.max_entries) + off;
 		if (size == 8)
 			atomicAdd(reinterpret_cast<unsigned long long *>(d), (unsigned long long)delta);

@@ -1490,11 +1490,12 @@ analyze_writes(dprog_host &out)
 					     !idiom_head_dead(i);
 		}
 	}
-	// Programs with loops: a path has no bound on its writes.  Counter updates must be device
-	// atomics (an array only aligned counter updates of one width change) the packet never reads
-	// back (no overlay entry each); the logged writes are capped per packet (DP_WRITES_MAX, the
-	// next one faults EBPF_FAULT_WRITES), which also bounds the overlay (two words per store)
-	bool counters = false;
+	// Programs with loops: a path has no bound on its writes.  Counter updates are device atomics
+	// (an array only aligned counter updates of one width change) or records of a hashtable's
+	// values, which count as logged writes like every other record; the logged writes are capped
+	// per packet (DP_WRITES_MAX, the next one faults EBPF_FAULT_WRITES), which also bounds the
+	// overlay (two words per store).  An array mixing counter updates with other writes is refused
+	bool counters = false, atomic_cnt = false;
 	for (size_t i = 0; i < n; i++) {
 		const dp_entry &e = out.entries[i];
 		if (!out.annot[i].reached || !(e.kind == DK_CNT_STORE || e.kind == DK_XADD))
@@ -1506,12 +1507,14 @@ analyze_writes(dprog_host &out)
 		for (size_t m = 0; m < nm; m++) {
 			if ((b.kind == AV_MAPVAL || b.kind == AV_MAPVAL_NULL) && b.map >= 0 && (size_t)b.map != m)
 				continue;
-			if (std::find(out.atomic_maps.begin(), out.atomic_maps.end(), (uint16_t)m) ==
-			    out.atomic_maps.end()) {
+			const bool atomic = std::find(out.atomic_maps.begin(), out.atomic_maps.end(), (uint16_t)m) !=
+					    out.atomic_maps.end();
+			atomic_cnt = atomic_cnt || atomic;
+			if (!atomic && !out.maps[m]->is_hashtable()) {
 				out.error = EOPNOTSUPP;
-				out.error_msg = "in a program with loops, counter updates must go to an array map that "
-						"only aligned counter updates of one width change (run this one with "
-						"ebpf_prog_run)";
+				out.error_msg = "in a program with loops, counter updates must go to a hashtable or to "
+						"an array map that only aligned counter updates of one width change (run "
+						"this one with ebpf_prog_run)";
 				return EOPNOTSUPP;
 			}
 		}
@@ -1519,10 +1522,12 @@ analyze_writes(dprog_host &out)
 	// A program with loops that reads its counter updates back (slot_reads_counters: a live
 	// idiom register, XADD with BPF_FETCH) keeps the packet's view of them in the overlay, 32
 	// words (DP_OVL_MAX; the store that needs one more faults EBPF_FAULT_WRITES).  A read-back
-	// of another form (a later load of a counter's word) is refused
+	// of another form (a later load of a counter's word) is refused when device atomics take
+	// counter updates (they are not counted, so nothing else bounds the overlay); a hashtable's
+	// counter records are counted, so its overlay holds at most two words per logged write
 	if (out.has_loops && counters && out.reads_counters) {
 		out.vstore_overlay = true;
-	} else if (out.has_loops && counters && out.vstore_overlay) {
+	} else if (out.has_loops && atomic_cnt && out.vstore_overlay) {
 		out.error = EOPNOTSUPP;
 		out.error_msg = "in a program with loops, the packet may read back the values its counter "
 				"updates change only through the idiom's register or XADD with BPF_FETCH (run "

@@ -63,9 +63,11 @@ struct ebpf_map;
  *     spins into EBPF_FAULT_LOOP, nor a jump before slot 0, EBPF_FAULT_SLOT; decided from the
  *     bytecode) has no per-path bound, so there a packet may make 16 logged
  *     writes: map_update_elem calls that return 0, every hashtable map_delete_elem (whether the
- *     key exists is known only at the replay), and stores into map values; counter updates
- *     aligned to their width (below) are not counted (they are additions).  The 17th faults the
- *     packet with EBPF_FAULT_WRITES (a fault: its writes do not land, its counter updates do);
+ *     key exists is known only at the replay), stores into map values, and counter updates
+ *     into a hashtable's values (records replayed after the batch); counter updates into an
+ *     array aligned to their width (below) are not counted (device atomics).  The 17th faults
+ *     the packet with EBPF_FAULT_WRITES (a fault: its writes do not land, its counter updates
+ *     do);
  *   - a writing program sharded over several devices (ebpf_prog_run_batch_multi*): the batch is
  *     the shards in order, every shard reads the batch-start maps, and the shards' writes are
  *     merged on the host in that global packet order after the last shard — the same result as
@@ -98,9 +100,10 @@ struct ebpf_map;
  *     operations: they take effect when executed;
  *   - EBPF_FAULT_MAP_WRITE is left for a store into a map value the translation did not provide
  *     for (a packet-relative pointer that lands in a map);
- *   - in a program with loops (standard semantics) a counter update must go to an array that
- *     only aligned counter updates of one width change (the batch functions return EOPNOTSUPP
- *     otherwise).  The packet may read its counters back through an XADD with BPF_FETCH or
+ *   - in a program with loops (standard semantics) a counter update must go to a hashtable
+ *     (a logged write, counted as above) or to an array that only aligned counter updates of
+ *     one width change (the batch functions return EOPNOTSUPP for an array that mixes them with
+ *     other writes).  The packet may read its counters back through an XADD with BPF_FETCH or
  *     through the idiom's register (live after the STX: the program "reads its counters back",
  *     decided from its bytecode on the slot graph — a reachable such XADD or idiom, a CALL
  *     reading its helper's arguments (lookup, delete r1-r2; update r1-r4), EXIT r0); it then
@@ -108,9 +111,11 @@ struct ebpf_map;
  *     kept in 32 8-byte words of map values per packet: a store, counter update or XADD that
  *     needs a word beyond them faults EBPF_FAULT_WRITES before it happens (a word already held
  *     is free: one counter updated on every trip takes one).  The map still lands as additions.
- *     A read-back of another form (a later plain load of a counter's word) returns EOPNOTSUPP.
- *     Plain stores and map_update_elem / map_delete_elem in loops are limited only by the 16
- *     logged writes per packet.
+ *     A read-back of another form (a later plain load of a counter's word) returns EOPNOTSUPP
+ *     when the program also updates array counters (device atomics, not counted, so nothing
+ *     else bounds that view); with hashtable counters alone it is allowed.  Plain stores,
+ *     hashtable counter updates and map_update_elem / map_delete_elem in loops are limited
+ *     only by the 16 logged writes per packet.
  * How it runs: arrays changed only by aligned counter updates of one width take device atomics
  * into a delta area next to their mirror (added into the values after the batch); other arrays'
  * stores land on the device (per-byte winners); hashtables, and arrays that mix counter updates

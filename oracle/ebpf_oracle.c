@@ -317,7 +317,8 @@ take_words(int mi, uint64_t elem, uint64_t voff, int size)
 }
 
 /* A logged write of the batch (a map_update_elem / map_delete_elem that succeeds, a store into a
- * map value other than an aligned counter update): 0, or F_WRITES for the packet's 17th.  Only in
+ * map value other than an aligned counter update into an array, any counter update into a
+ * hashtable's value): 0, or F_WRITES for the packet's 17th.  Only in
  * batch mode, and only for a program with loops: a loop-free program writes as often as its path
  * says, like the reference (ebpf_interpreter.c:343-366, ebpf_map.c:101-108 ->
  * ebpf_map_array.c:198-211 run every store and update they reach); the reference's own run,
@@ -417,7 +418,7 @@ value_store(const struct region_env *re, int mi, uint64_t addr, int size, uint64
 		store_n(addr, size, v);
 		return 0;
 	}
-	if (!add) {
+	if (!add || m->kind == ORACLE_MAP_HASH) { /* (a hashtable's counter updates are records) */
 		int f = count_write();
 		if (f)
 			return f;

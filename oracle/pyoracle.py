@@ -214,7 +214,7 @@ class OracleProgram:
         # hash_models (a replay that fails leaves the model unchanged)
         used = ctypes.c_uint64(0)
         rmax = max(8 + m.key_size + m.value_size for m in self.specs if isinstance(m, HashSpec))
-        cap = max(4096, 4 * count * rmax)    # (up to 4 hashtable writes per packet)
+        cap = max(4096, 16 * count * rmax)   # (up to 16 hashtable writes per packet)
         buf = np.zeros(cap, dtype=np.uint8)
         steps = lib().oracle_run_batch_hlog(*args, buf.ctypes.data, cap, ctypes.byref(used))
         if used.value > cap:

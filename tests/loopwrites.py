@@ -110,8 +110,9 @@ def prog_xadd_fetch():
 
 
 def prog_xadd_then_load():
-    """XADD (no fetch) into counters[type & 15], then a plain load of the same word: a read-back
-    the device does not provide for in a loop (EOPNOTSUPP)."""
+    """XADD (no fetch) into counters[type & 15], then a plain load of the same word, r9 ^= it.
+    r0 = options ^ r9.  Into an array (device atomics): a read-back the device does not provide
+    for in a loop (EOPNOTSUPP); into a hashtable (counted records): allowed."""
     return stdprogs.asm(_walk_head() + _key_lookup() + [
         I("mov64_imm", 5, imm=1), (0xdb, 0, 5, 0, 0), I("ldxdw", 5, 0, 0), I("xor64_reg", 9, 5),
         ("label", "N")] + _walk_tail([I("xor64_reg", 0, 9)]))
@@ -141,16 +142,23 @@ def _u(b, at, w):
     return int.from_bytes(bytes(b[at:at + w]), "little")
 
 
-def expect(kind, pk, init, vs):
+def expect(kind, pk, init, vs, present=None):
     """(r0, fault, map bytes after the batch) of prog_<kind> over pk, step by step in each
-    program's own order of loads, checks and writes."""
+    program's own order of loads, checks and writes.  present: the map is a hashtable holding
+    only these keys (a lookup of another misses and skips the option's body), and its counter
+    updates are records, counted with the logged writes (16 a packet, the 17th faults WRITES
+    before it happens; the additions before it land)."""
     m = bytearray(init)
     M64 = 2**64 - 1
+    counted = present is not None
     ret, flt = [], []
     for p in pk:
         own = bytearray(init)   # the packet's view (its own stores over the batch start)
         adds, writes, fault = [], [], 0
         words = set()           # (limiter, xadd_fetch) the 8-byte words of the packet's view
+
+        def full():             # the next logged write would be the 17th
+            return len(writes) + (len(adds) if counted else 0) == 16
         n, r9, at, r0 = 0, 0, START, None
         while True:
             if at >= 64:                      # ldxb type
@@ -172,11 +180,15 @@ def expect(kind, pk, init, vs):
                 fault = FAULT_MEM
                 break
             ln = int(p[at + 1])
+            if present is not None and (t & (NKEYS - 1)) not in present:
+                n += 1                        # the lookup missed: on to the next option
+                at += 2 + (ln & 3)
+                continue
             if kind in ("limiter", "xadd_fetch"):
                 k = (t & (FETCH_KEYS - 1 if kind == "xadd_fetch" else NKEYS - 1)) * vs
                 ups = [(k, 1)] if kind == "limiter" else [(k, ln), (k + 8, 1)]
                 for j, (w, add) in enumerate(ups):
-                    if w not in words and len(words) == 32:
+                    if (w not in words and len(words) == 32) or (counted and full()):
                         fault = FAULT_WRITES
                         break
                     words.add(w)
@@ -189,10 +201,18 @@ def expect(kind, pk, init, vs):
                 if kind == "limiter" and (_u(own, k, 8)) > 3:
                     r0 = 0x1000 + n
                     break
-            if kind == "xadd":
-                adds += [(k, 1), (k + 8, ln)]
-            elif kind == "idiom":
-                adds.append((k, ln))
+            if kind in ("xadd", "idiom", "xadd_load"):
+                ups = {"xadd": [(k, 1), (k + 8, ln)], "idiom": [(k, ln)], "xadd_load": [(k, 1)]}[kind]
+                for w, add in ups:
+                    if counted and full():
+                        fault = FAULT_WRITES
+                        break
+                    own[w:w + 8] = ((_u(own, w, 8) + add) & M64).to_bytes(8, "little")
+                    adds.append((w, add))
+                if fault:
+                    break
+                if kind == "xadd_load":
+                    r9 ^= _u(own, k, 8)
             elif kind == "stores":
                 if at + 6 > 64:               # ldxw data
                     fault = FAULT_MEM
@@ -211,7 +231,7 @@ def expect(kind, pk, init, vs):
             for k, b in writes:
                 m[k:k + len(b)] = b
         if r0 is None:
-            r0 = n ^ r9 if kind in ("stores", "xadd_fetch") else n
+            r0 = n ^ r9 if kind in ("stores", "xadd_fetch", "xadd_load") else n
         ret.append(0 if fault else r0)
         flt.append(fault)
     return np.array(ret, dtype=np.uint64), np.array(flt, dtype=np.uint8), bytes(m)
@@ -234,7 +254,8 @@ def prog_mixed_counter_store():
         _walk_tail())
 
 
-VALUE_SIZE = {"xadd": 16, "idiom": 8, "updates": 8, "stores": 8, "limiter": 8, "xadd_fetch": 16}
+VALUE_SIZE = {"xadd": 16, "idiom": 8, "updates": 8, "stores": 8, "limiter": 8, "xadd_fetch": 16,
+              "xadd_load": 8}
 MAP_KEYS = {"xadd_fetch": FETCH_KEYS}
 PROGS = {"xadd": prog_xadd_counters, "idiom": prog_idiom_counters, "updates": prog_updates,
          "stores": prog_stores, "limiter": prog_limiter, "xadd_fetch": prog_xadd_fetch}
@@ -247,3 +268,25 @@ def initial_map(kind, seed):
     if kind == "limiter":
         return g.integers(0, 3, keys, dtype=np.uint64).tobytes()
     return g.integers(0, 256, keys * VALUE_SIZE[kind], dtype=np.uint8).tobytes()
+
+
+# Counter updates into a hashtable inside loops (round 6): the same walks over a hashtable of u32
+# keys that holds 12 of the 16 types (the other 4 miss); every counter update is a record, counted
+# with the logged writes
+HASH_PRESENT = frozenset(range(12))
+HASH_PROGS = {"xadd": prog_xadd_counters, "idiom": prog_idiom_counters, "limiter": prog_limiter,
+              "xadd_load": prog_xadd_then_load}
+
+
+def hash_items(init, vs):
+    """[(u32 key bytes, value bytes)] of the present keys, values from the array image init"""
+    return [(k.to_bytes(4, "little"), bytes(init[k * vs:(k + 1) * vs])) for k in sorted(HASH_PRESENT)]
+
+
+def hash_image(items, vs):
+    """the array image (NKEYS * vs bytes, absent keys zero) of [(key, value)]"""
+    m = bytearray(NKEYS * vs)
+    for key, val in items:
+        k = int.from_bytes(key, "little")
+        m[k * vs:(k + 1) * vs] = val
+    return bytes(m)

@@ -287,7 +287,7 @@ def gen_cursor_program(seed):
     return asm(items)
 
 
-def gen_loop_write_program(seed, counters=False, fetched=False):
+def gen_loop_write_program(seed, counters=False, fetched=False, mixed=False):
     """A standard program that writes maps inside loops (include/ebpf_gpu.h "Map writes in a
     device batch"): 1-2 counted loops (trip counts 1-24 from packet bytes, so some packets pass
     the 16 logged writes a packet may make and fault EBPF_FAULT_WRITES), each trip looking up
@@ -303,7 +303,10 @@ def gen_loop_write_program(seed, counters=False, fetched=False):
       fetched=True (round 6; map 0 then has 32-B values, 4 words a key): the counters read
         back — XADD with BPF_FETCH whose old value r9 mixes in, and the idiom whose register r9
         mixes in after the STX — so that a packet sees the batch start plus its own additions
-        and a long walk over many keys passes the 32 words of its view (EBPF_FAULT_WRITES).
+        and a long walk over many keys passes the 32 words of its view (EBPF_FAULT_WRITES);
+      mixed=True (round 6; map 0 a hashtable, 16-B values): everything into the same values —
+        XADD with and without BPF_FETCH, the idiom with a live or a dead register, plain stores
+        and loads back — and map_update_elem of map 1: every one of them a record, counted.
     r0 mixes the trip count, loaded values and helper return codes."""
     counters = counters or fetched
     vs0 = 32 if fetched else 16
@@ -323,7 +326,22 @@ def gen_loop_write_program(seed, counters=False, fetched=False):
                   I("call", imm=0), I("jeq_imm", 0, imm=0, off="M" + t)]
         for j in range(int(g.integers(1, 4))):
             r = g.random()
-            if counters:
+            if mixed and r < 0.5:
+                off = int(g.integers(0, vs0 // cw)) * cw
+                fetch = g.random() < 0.5
+                if r < 0.25:
+                    items += [I("mov64_reg", 3, 8), I("add64_imm", 3, imm=int(g.integers(0, 9))),
+                              (0xdb if cw == 8 else 0xc3, 0, 3, off, 1 if fetch else 0),
+                              I("mul64_imm", 9, imm=31), I("add64_reg", 9, 3)]
+                else:
+                    ld, st = ("ldxdw", "stxdw") if cw == 8 else ("ldxw", "stxw")
+                    items += [I(ld, 5, 0, off), I("add64_imm", 5, imm=int(g.integers(1, 100))),
+                              I(st, 0, 5, off)]
+                    items += [I("xor64_reg", 9, 5)] if fetch else [I("mov64_imm", 5, imm=0)]
+                continue
+            if mixed:
+                r = (r - 0.5) * 2           # stores, loads, updates as below
+            if counters and not mixed:
                 off = int(g.integers(0, vs0 // cw)) * cw
                 if r < 0.6:
                     items += [I("mov64_reg", 3, 8), I("add64_imm", 3, imm=int(g.integers(0, 9))),

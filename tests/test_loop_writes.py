@@ -140,12 +140,111 @@ def test_loop_translation_rules(native, env):
         m64.destroy()
 
 
-def _device(gpu, env, kind, pk, init, variant, resident):
-    import torch
-    code, rel = lw.PROGS[kind]()
+# ---- counter updates into a hashtable inside loops (round 6): records, counted writes ----
+
+def _hash_oracle(kind, pk, init, sequential=False):
+    """(ret, faults, array image of the table after the batch) on the oracle"""
+    code, rel = lw.HASH_PROGS[kind]()
     vs = lw.VALUE_SIZE[kind]
-    m = gpu.Map(env, _nkeys(kind), vs)
-    m.fill(init)
+    items = lw.hash_items(init, vs)
+    spec = pyoracle.HashSpec(4, vs, items=items, capacity=lw.NKEYS)
+    op = pyoracle.OracleProgram(code, rel, [spec], semantics=1, sequential=sequential)
+    ret, flt, _, _ = op.run(pk.reshape(-1), len(pk), 64, nthreads=1 if sequential else 4)
+    if sequential:   # (the values written in place, in the spec's order)
+        vals = op.map_bytes(0)
+        after = [(k, vals[i * vs:(i + 1) * vs]) for i, (k, _) in enumerate(items)]
+    else:
+        after = op.hash_models[0].items()
+    return ret, flt, lw.hash_image(after, vs)
+
+
+def _hash_init(kind, seed):
+    vs = lw.VALUE_SIZE[kind]
+    return lw.hash_image(lw.hash_items(lw.initial_map(kind, seed), vs), vs)
+
+
+@pytest.mark.parametrize("kind", sorted(lw.HASH_PROGS))
+def test_oracle_hash_loop_counters_known_answers(kind):
+    """the oracle's batch mode against the step-by-step restatement: hashtable counter updates
+    are counted records (the 17th logged write faults WRITES, the additions before it land);
+    over the walks that keep within 16, the map is the reference's sequential run's (the
+    limiter's additions depend on what it reads, so only its batch is checked)"""
+    pk = lw.packets(4000, 41)
+    vs = lw.VALUE_SIZE[kind]
+    init = _hash_init(kind, 42)
+    ret, flt, after = _hash_oracle(kind, pk, init)
+    want, wf, wafter = lw.expect(kind, pk, init, vs, present=lw.HASH_PRESENT)
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == wafter
+    assert (wf == 0).any() and (wf == lw.FAULT_MEM).any()
+    if kind == "xadd":
+        assert (wf == lw.FAULT_WRITES).any()    # two records an option
+    if kind != "limiter":
+        sel = pk[wf != lw.FAULT_WRITES]
+        assert _hash_oracle(kind, sel, init, sequential=True)[2] == _hash_oracle(kind, sel, init)[2]
+
+
+def test_hash_loop_translation_rules(native, env):
+    """Counter updates into a hashtable inside a loop translate (XADD, the idiom with a dead and
+    a live register, the limiter, XADD then a plain load of the word, a counter and a store into
+    one hashtable); the plain load after an array counter's XADD stays EOPNOTSUPP."""
+    h16 = native.HashMap(env, 4, 16, lw.NKEYS)
+    h8 = native.HashMap(env, 4, 8, lw.NKEYS)
+    m8 = native.Map(env, lw.NKEYS, 8)
+    try:
+        assert _translate_error(native, env, *lw.prog_xadd_counters(), [h16]) == 0
+        assert _translate_error(native, env, *lw.prog_idiom_counters(), [h8]) == 0
+        assert _translate_error(native, env, *lw.prog_idiom_counters(live=True), [h8]) == 0
+        assert _translate_error(native, env, *lw.prog_limiter(), [h8]) == 0
+        assert _translate_error(native, env, *lw.prog_xadd_then_load(), [h8]) == 0
+        assert _translate_error(native, env, *lw.prog_mixed_counter_store(), [h8]) == 0
+        assert _translate_error(native, env, *lw.prog_xadd_then_load(), [m8]) == errno.EOPNOTSUPP
+    finally:
+        h16.destroy()
+        h8.destroy()
+        m8.destroy()
+
+
+def _hash_device(gpu, env, kind, pk, init, variant, resident):
+    code, rel = lw.HASH_PROGS[kind]()
+    vs = lw.VALUE_SIZE[kind]
+    items = lw.hash_items(init, vs)
+    m = gpu.HashMap(env, 4, vs, lw.NKEYS)
+    try:
+        m.fill(np.frombuffer(b"".join(k for k, _ in items), np.uint8),
+               np.frombuffer(b"".join(v for _, v in items), np.uint8))
+        ret, flt, ex = _run(gpu, env, code, rel, m, pk, variant, resident)
+        after = []
+        for k, _ in items:
+            err, v = m.lookup(k)
+            assert err == 0
+            after.append((k, v))
+        return ret, flt, lw.hash_image(after, vs), ex
+    finally:
+        m.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("kind", sorted(lw.HASH_PROGS))
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_hash_loop_counters_vs_oracle(gpu, env, variant, kind, resident):
+    """hashtable counter walks on every variant: results, faults and the table against the
+    oracle's batch mode"""
+    pk = lw.packets((1 << 15) + 11, 43)
+    init = _hash_init(kind, 44)
+    want, wf, wafter = _hash_oracle(kind, pk, init)
+    ret, flt, after, _ = _hash_device(gpu, env, kind, pk, init, variant, resident)
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert after == wafter
+
+
+def _run(gpu, env, code, rel, m, pk, variant, resident):
+    """(ret, faults, exec path) of one batch of the program over map m, host buffers or
+    device-resident"""
+    import torch
     p = gpu.Prog(env, gpu.patch_relocs(code, rel, [m.handle]))
     n = len(pk)
     try:
@@ -162,12 +261,21 @@ def _device(gpu, env, kind, pk, init, variant, resident):
             ret, flt = d_ret.cpu().numpy().view(np.uint64), d_flt.cpu().numpy()
         else:
             ret, flt, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
-        ex = p.exec_info(0)[0]
-        after = b"".join(m.lookup(k)[1] for k in range(_nkeys(kind)))
-        return ret, flt, after, ex
+        return ret, flt, p.exec_info(0)[0]
     finally:
         gpu.set_variant(0)
         p.destroy()
+
+
+def _device(gpu, env, kind, pk, init, variant, resident):
+    code, rel = lw.PROGS[kind]()
+    m = gpu.Map(env, _nkeys(kind), lw.VALUE_SIZE[kind])
+    try:
+        m.fill(init)
+        ret, flt, ex = _run(gpu, env, code, rel, m, pk, variant, resident)
+        after = b"".join(m.lookup(k)[1] for k in range(_nkeys(kind)))
+        return ret, flt, after, ex
+    finally:
         m.destroy()
 
 
@@ -332,3 +440,97 @@ def test_device_loop_stores_through_spilled_packet_pointer(gpu, env, variant, st
 def test_spilled_packet_pointer_store_loop_translates(native, env):
     code, rel = prog_spilled_packet_stores()
     assert _translate_error(native, env, code, rel, []) == 0
+
+
+# ---- random loop programs over a hashtable: counters, stores, loads and updates mixed ----
+
+def _random_hash_maps(k):
+    """map 0: a hashtable of u32 keys holding 12 of the 16 the programs look up (16-B values);
+    map 1: an array of 16 8-B values (as _random_maps)"""
+    g = np.random.default_rng(700 + k)
+    items = [(key.to_bytes(4, "little"), g.integers(0, 256, 16, dtype=np.uint8).tobytes())
+             for key in sorted(lw.HASH_PRESENT)]
+    return items, (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())
+
+
+def _hash_oracle_random(code, rel, k, pk):
+    items, arr = _random_hash_maps(k)
+    spec = pyoracle.HashSpec(4, 16, items=items, capacity=lw.NKEYS)
+    op = pyoracle.OracleProgram(code, rel, [spec, arr], semantics=1)
+    ret, flt, _, _ = op.run(pk.reshape(-1), len(pk), 64, nthreads=8)
+    table = dict(op.hash_models[0].items())
+    return ret, flt, [table[key] for key, _ in items], op.map_bytes(1)
+
+
+def test_oracle_random_hash_loop_programs_fault_writes_somewhere():
+    """the mixed generator's programs translate, and over 30 of them some packets fault WRITES
+    (their counter records count) and some finish"""
+    import stdprogs
+    from generic_ebpf_amd import workloads
+    seen = set()
+    for k in range(30):
+        code, rel = stdprogs.gen_loop_write_program(1200 + k, mixed=True)
+        pk = workloads.packets_random(256, 64, seed=1300 + k)
+        _, flt, _, _ = _hash_oracle_random(code, rel, k, pk)
+        seen |= set(int(x) for x in np.unique(flt))
+    assert {0, lw.FAULT_WRITES} <= seen
+
+
+def test_random_hash_loop_programs_translate(native, env):
+    import stdprogs
+    h = native.HashMap(env, 4, 16, lw.NKEYS)
+    a = native.Map(env, 16, 8)
+    try:
+        for k in range(30):
+            code, rel = stdprogs.gen_loop_write_program(1200 + k, mixed=True)
+            p = native.Prog(env, native.patch_relocs(code, rel, [h.handle, a.handle]))
+            try:
+                p.set_semantics(native.SEM_STANDARD)
+
+                class Info(ctypes.Structure):
+                    _fields_ = [("nslots", ctypes.c_uint32), ("nentries", ctypes.c_uint32),
+                                ("nmaps", ctypes.c_uint32), ("max_stack", ctypes.c_uint32)]
+                i = Info()
+                assert native.lib().ebpf_prog_device_info(p.ptr, ctypes.byref(i)) == 0, k
+            finally:
+                p.destroy()
+    finally:
+        h.destroy()
+        a.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_device_random_hash_loop_programs_vs_oracle(gpu, env, variant):
+    """30 random loop programs mixing counter updates (fetched or not), stores, loads back and
+    updates in one hashtable's values: results, faults, the table and the array against the
+    oracle's batch mode"""
+    import stdprogs
+    from generic_ebpf_amd import workloads
+    bad = []
+    for k in range(30):
+        code, rel = stdprogs.gen_loop_write_program(1200 + k, mixed=True)
+        n = 4096 + k
+        pk = workloads.packets_random(n, 64, seed=1300 + k)
+        want, wf, wtab, warr = _hash_oracle_random(code, rel, k, pk)
+        items, (avs, ame, ad) = _random_hash_maps(k)
+        h = gpu.HashMap(env, 4, 16, lw.NKEYS)
+        a = gpu.Map(env, ame, avs)
+        h.fill(np.frombuffer(b"".join(key for key, _ in items), np.uint8),
+               np.frombuffer(b"".join(v for _, v in items), np.uint8))
+        a.fill(ad)
+        p = gpu.Prog(env, gpu.patch_relocs(code, rel, [h.handle, a.handle]))
+        try:
+            p.set_semantics(gpu.SEM_STANDARD)
+            gpu.set_variant(variant)
+            ret, flt, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1)), n, 64)
+            tab = [h.lookup(key)[1] for key, _ in items]
+            arr = b"".join(a.lookup(key)[1] for key in range(ame))
+        finally:
+            gpu.set_variant(0)
+            p.destroy()
+            h.destroy()
+            a.destroy()
+        if not (np.array_equal(ret, want) and np.array_equal(flt, wf) and tab == wtab and arr == warr):
+            bad.append((k, int((ret != want).sum()), int((flt != wf).sum()), tab == wtab, arr == warr))
+    assert not bad, bad
