@@ -2,7 +2,8 @@
 not use: random programs under the reference's semantics with array maps (every variant, staged
 and general kernels) and with hashtables, standard-semantics programs (loop-free,
 counted loops, cursor walks), programs that write maps inside loops (round 5), reference
-programs with more than 16 map writes on one path (round 6), and randomly
+programs with more than 16 map writes on one path and loop programs mixing every kind of write
+in one hashtable's values (round 6), and randomly
 edited programs the oracle finds defined.  Each mode
 compares results, fault codes, packet bytes after the batch and the maps with the oracle.  The
 long campaigns (thousands of programs per configuration) stay in tools/fuzz_gpu.py; their logs
@@ -31,7 +32,7 @@ def fuzz(gpu):
 
 
 @pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites",
-                                  "loopfetched", "manywrites"])
+                                  "loopfetched", "loophash", "manywrites"])
 def test_fuzz_campaign(fuzz, env, mode):
     if mode == "reference":
         failed = fuzz.reference(_args(seed=11), env)
@@ -43,6 +44,8 @@ def test_fuzz_campaign(fuzz, env, mode):
         failed = fuzz.loop_writes(_args(seed=15, programs=40), env)
     elif mode == "loopfetched":   # (counters read back inside loops: 40 of them fetch)
         failed = fuzz.loop_writes(_args(seed=17, programs=120, fetched=True), env)
+    elif mode == "loophash":   # (hashtable counters, stores, loads and updates inside loops)
+        failed = fuzz.loop_writes(_args(seed=18, programs=60, hash=True), env)
     elif mode == "manywrites":   # (more than 16 writes on a loop-free path: no limit)
         failed = fuzz.reference(_args(seed=16, programs=60, manywrites=True), env)
     else:

@@ -9,6 +9,9 @@ key universe the programs' keys hit and miss, capacity 16 or 256 so that inserts
 lookups, updates and deletes against the oracle's replay model; the tables are compared through
 get_next_key's walk (order and values).
 
+--loopwrites --hash: loop programs mixing counters (fetched or not), stores, loads back and
+update calls in one hashtable's values (round 6: its counter updates are counted records).
+
   python tools/fuzz_gpu.py [--programs N] [--seed S] [--hash | --standard | --mutate | --loopwrites |
                                                       --manywrites]
 Prints one line per configuration and exits 1 on any mismatch (the failing seeds are listed)."""
@@ -294,46 +297,63 @@ def loop_writes(a, env):
     against the oracle's batch mode."""
     import stdprogs
     failed = False
+    hashed = getattr(a, "hash", False)
     for variant in (0, 1, 2):
         t0, bad, faults = time.time(), [], 0
         for k in range(a.programs):
             seed = a.seed * 100000 + k
             g = np.random.default_rng(seed)
-            # (every third program counts; with --fetched, the counters are read back)
+            # (every third program counts; with --fetched, the counters are read back; with
+            # --hash map 0 is a hashtable and every program mixes counters, fetched or not,
+            # stores, loads back and updates of map 1 in its values)
             fetched = k % 3 == 2 and getattr(a, "fetched", False)
-            code, rel = stdprogs.gen_loop_write_program(seed, counters=k % 3 == 2, fetched=fetched)
+            code, rel = stdprogs.gen_loop_write_program(seed, counters=k % 3 == 2, fetched=fetched,
+                                                        mixed=hashed)
             vs0 = 32 if fetched else 16
-            specs = [(vs0, 16, g.integers(0, 256, 16 * vs0, dtype=np.uint8).tobytes()),
-                     (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())]
+            arr = (8, 16, g.integers(0, 256, 128, dtype=np.uint8).tobytes())
+            if hashed:   # (a random subset of the 16 keys the programs look up; capacity 16)
+                keys = g.permutation(16)[:int(g.integers(0, 17))]
+                specs = [pyoracle.HashSpec(4, 16, items=[(int(x).to_bytes(4, "little"), g.bytes(16))
+                                                         for x in keys], capacity=16), arr]
+            else:
+                specs = [(vs0, 16, g.integers(0, 256, 16 * vs0, dtype=np.uint8).tobytes()), arr]
             n = int(g.choice([1, 64, 65, 777, 4099]))
             pk = g.integers(0, 256, (n, 64), dtype=np.uint8)
             op = pyoracle.OracleProgram(code, rel, specs, semantics=1)
             want, wf, _, _ = op.run(pk.reshape(-1), n, 64, nthreads=8)
             faults += int(np.count_nonzero(wf))
             maps = []
-            for vs, me, d in specs:
-                m = native.Map(env, me, vs)
-                m.fill(d)
+            for spec in specs:
+                if isinstance(spec, pyoracle.HashSpec):
+                    m = native.HashMap(env, 4, spec.value_size, spec.capacity)
+                    for kk, vv in spec.items:
+                        assert m.update(kk, vv) == 0
+                else:
+                    vs, me, d = spec
+                    m = native.Map(env, me, vs)
+                    m.fill(d)
                 maps.append(m)
             p = native.Prog(env, native.patch_relocs(code, rel, [m.handle for m in maps]))
             try:
                 p.set_semantics(native.SEM_STANDARD)
                 native.set_variant(variant)
                 got, gf, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, 64)
-                after = [b"".join(m.lookup(key)[1] for key in range(m.max_entries)) for m in maps]
+                after = [walk(m) if isinstance(m, native.HashMap) else
+                         b"".join(m.lookup(key)[1] for key in range(m.max_entries)) for m in maps]
             finally:
                 native.set_variant(0)
                 p.destroy()
                 for m in maps:
                     m.destroy()
+            want0 = op.hash_models[0].items() if hashed else op.map_bytes(0)
             if not (np.array_equal(want, got) and np.array_equal(wf, gf) and
-                    after[0] == op.map_bytes(0) and after[1] == op.map_bytes(1)):
+                    after[0] == want0 and after[1] == op.map_bytes(1)):
                 bad.append(k)
             if k % 100 == 99:
                 print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        print("loop writes%s variant %d: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
-            " (fetched)" if getattr(a, "fetched", False) else "", variant, a.programs, faults, len(bad),
-            bad[:20], time.time() - t0), flush=True)
+        print("loop writes%s%s variant %d: %d programs, %d faulted packets, %d mismatches %s (%.0f s)" % (
+            " (fetched)" if getattr(a, "fetched", False) else "", " (hashtable)" if hashed else "",
+            variant, a.programs, faults, len(bad), bad[:20], time.time() - t0), flush=True)
         failed = failed or bool(bad)
     return failed
 
