@@ -1077,7 +1077,7 @@ launch(struct ebpf_prog *ep, dprog_device *dp, const dp_launch &L0, hipStream_t 
 		// the staged kernels' keep mode (compiled and interpreted programs): a program that
 		// loads its packet at run-time offsets reads them from the wave's LDS packet buffer
 		// (gen_interp.py h_ldx_pktv), so the next group's DMA waits for the group's end
-		if (mode == 1 && ep->xlated->asm_pktv)
+		if (mode == 1 && ep->xlated->asm_pktv && getenv("EBPF_NOKEEP") == nullptr)
 			L.vflags |= DP_VF_KEEP;
 		// general kernels: header staging (bit 31), and the headers kept in LDS too (bit 30;
 		// when the 16 KB of packet buffers cost no resident workgroup: the VGPRs allow 6 per CU)
