@@ -214,9 +214,19 @@ class OracleProgram:
         # hash_models (a replay that fails leaves the model unchanged)
         used = ctypes.c_uint64(0)
         rmax = max(8 + m.key_size + m.value_size for m in self.specs if isinstance(m, HashSpec))
-        cap = max(4096, 16 * count * rmax)   # (up to 16 hashtable writes per packet)
+        cap = max(4096, 16 * count * rmax)   # (16 hashtable writes per packet; else run again)
         buf = np.zeros(cap, dtype=np.uint8)
+        # (the run applies its array-map writes: kept to run again from the same start)
+        arrays = {k: self.map_data[k].copy() for k, m in enumerate(self.specs)
+                  if not isinstance(m, HashSpec)}
         steps = lib().oracle_run_batch_hlog(*args, buf.ctypes.data, cap, ctypes.byref(used))
+        if used.value > cap:   # (a loop-free path with more writes: the same run, a larger buffer)
+            cap = int(used.value)
+            buf = np.zeros(cap, dtype=np.uint8)
+            work[:] = np.asarray(data, dtype=np.uint8).reshape(-1)
+            for k, d in arrays.items():
+                self.map_data[k][:] = d
+            steps = lib().oracle_run_batch_hlog(*args, buf.ctypes.data, cap, ctypes.byref(used))
         if used.value > cap:
             raise RuntimeError("oracle: more hashtable writes than the replay buffer holds")
         self.last_hlog = []

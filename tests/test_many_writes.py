@@ -253,3 +253,63 @@ def test_device_readback_vs_oracle(gpu, env, variant, layout, case):
         m.destroy()
     if case != "readback16" or variant == 1:   # (16 stores still fit the lanes' own overlay)
         assert ex == "hip"
+
+
+# ---- the same read-back programs over a hashtable (the spilled overlay on a table's values) ----
+
+def _hash_items(vs, seed, present=12):
+    """u32 keys 0..present-1 of the 16 the programs look up (the others miss), random values"""
+    g = np.random.default_rng(seed)
+    return [(k.to_bytes(4, "little"), g.integers(0, 256, vs, dtype=np.uint8).tobytes())
+            for k in range(present)]
+
+
+def test_oracle_hash_readback_sees_own_stores():
+    """over a hashtable: r0 from the packet's own stores, equal to the sequential run when no two
+    packets share a key; packets whose key is absent exit with MISS"""
+    for name in ("readback17", "readback40"):
+        mk, vs, _ = mw.READBACK[name]
+        lay = mk()
+        pk = mw.distinct_key_packets(16, 31)
+        items = _hash_items(vs, 32)
+        outs = []
+        for seq in (False, True):
+            op = pyoracle.OracleProgram(lay.code, lay.relocs, [pyoracle.HashSpec(4, vs, items=items, capacity=16)],
+                                        sequential=seq)
+            ret, flt, _, _ = op.run(pk.reshape(-1), 16, 64, nthreads=1)
+            outs.append((ret, flt))
+        np.testing.assert_array_equal(outs[0][0], outs[1][0])
+        assert not outs[0][1].any()
+        assert (outs[0][0][12:] == mw.MISS).all() and (outs[0][0][:12] != mw.MISS).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["readback17", "readback40"])
+def test_device_hash_readback_vs_oracle(gpu, env, variant, case):
+    """past 16 stores read back into a hashtable's values: the spilled overlay on the portable
+    interpreter, the stores replayed into the table after the batch — results, faults and the
+    table against the oracle"""
+    mk, vs, _ = mw.READBACK[case]
+    lay = mk()
+    n = (1 << 14) + 13
+    pk = mw.packets(n, 33)
+    items = _hash_items(vs, 34)
+    op = pyoracle.OracleProgram(lay.code, lay.relocs, [pyoracle.HashSpec(4, vs, items=items, capacity=16)])
+    want, wf, _, _ = op.run(pk.reshape(-1), n, 64, nthreads=8)
+    wtab = dict(op.hash_models[0].items())
+    m = gpu.HashMap(env, 4, vs, 16)
+    for k, v in items:
+        assert m.update(k, v) == 0
+    p = gpu.Prog(env, lay.patched([m.handle]))
+    try:
+        gpu.set_variant(variant)
+        ret, flt, _ = p.run_batch(np.ascontiguousarray(pk.reshape(-1).copy()), n, 64)
+        tab = {k: m.lookup(k)[1] for k, _ in items}
+    finally:
+        gpu.set_variant(0)
+        p.destroy()
+        m.destroy()
+    np.testing.assert_array_equal(flt, wf)
+    np.testing.assert_array_equal(ret, want)
+    assert tab == {k: wtab[k] for k, _ in items}
