@@ -534,3 +534,39 @@ def test_device_random_hash_loop_programs_vs_oracle(gpu, env, variant):
         if not (np.array_equal(ret, want) and np.array_equal(flt, wf) and tab == wtab and arr == warr):
             bad.append((k, int((ret != want).sum()), int((flt != wf).sum()), tab == wtab, arr == warr))
     assert not bad, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_device_hash_loop_counters_other_entry_points(gpu, env, variant):
+    """the hashtable rate limiter and XADD walk sharded over [0, 0] (the shards' counted records
+    merged in global packet order on the host) and asynchronously: as one batch, against the
+    oracle"""
+    for kind in ("limiter", "xadd"):
+        code, rel = lw.HASH_PROGS[kind]()
+        vs = lw.VALUE_SIZE[kind]
+        pk = lw.packets((1 << 13) + 5, 51)
+        init = _hash_init(kind, 52)
+        want, wf, wafter = _hash_oracle(kind, pk, init)
+        items = lw.hash_items(init, vs)
+        for how in ("multi", "async"):
+            m = gpu.HashMap(env, 4, vs, lw.NKEYS)
+            m.fill(np.frombuffer(b"".join(k for k, _ in items), np.uint8),
+                   np.frombuffer(b"".join(v for _, v in items), np.uint8))
+            p = gpu.Prog(env, gpu.patch_relocs(code, rel, [m.handle]))
+            try:
+                p.set_semantics(gpu.SEM_STANDARD)
+                gpu.set_variant(variant)
+                data = np.ascontiguousarray(pk.reshape(-1).copy())
+                if how == "multi":
+                    ret, flt, _ = p.run_batch_multi([0, 0], data, len(pk), 64)
+                else:
+                    ret, flt, _ = p.run_batch_async(data, len(pk), 64).wait()
+                after = lw.hash_image([(k, m.lookup(k)[1]) for k, _ in items], vs)
+            finally:
+                gpu.set_variant(0)
+                p.destroy()
+                m.destroy()
+            np.testing.assert_array_equal(flt, wf, err_msg="%s %s" % (kind, how))
+            np.testing.assert_array_equal(ret, want, err_msg="%s %s" % (kind, how))
+            assert after == wafter, (kind, how)

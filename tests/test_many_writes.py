@@ -313,3 +313,47 @@ def test_device_hash_readback_vs_oracle(gpu, env, variant, case):
     np.testing.assert_array_equal(flt, wf)
     np.testing.assert_array_equal(ret, want)
     assert tab == {k: wtab[k] for k, _ in items}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_device_readback_spilled_other_entry_points(gpu, env, variant):
+    """the spilled overlay through the other batch entry points: sharded over [0, 0]
+    (ebpf_prog_run_batch_multi: each shard's chunks at its own packet base, the shards' logs
+    merged in global order), as (start, end) extents of ragged packets, and asynchronously —
+    each against the oracle"""
+    mk, vs, me = mw.READBACK["readback40"]
+    lay = mk()
+    n = (1 << 13) + 7
+    pk = mw.packets(n, 41)
+    init = _init(vs, me, 42)
+    want, wf, wafter = _oracle(lay, vs, me, init, pk.reshape(-1), n, 64)
+    (rdata, roffs) = _ragged(pk, 43)
+    rwant, rwf, rwafter = _oracle(lay, vs, me, init, rdata, n, 0, roffs)
+    ext = np.stack([roffs[:-1], roffs[1:]], axis=1).reshape(-1).astype(np.uint64)
+
+    def run(how):
+        m = gpu.Map(env, me, vs)
+        m.fill(init)
+        p = gpu.Prog(env, lay.patched([m.handle]))
+        try:
+            gpu.set_variant(variant)
+            if how == "multi":
+                ret, flt, _ = p.run_batch_multi([0, 0], np.ascontiguousarray(pk.reshape(-1).copy()), n, 64)
+            elif how == "extents":
+                ret, flt, _ = p.run_batch(np.ascontiguousarray(rdata.copy()), n, 0, ext, extents=True)
+            else:
+                data = np.ascontiguousarray(pk.reshape(-1).copy())
+                ret, flt, _ = p.run_batch_async(data, n, 64).wait()
+            return ret, flt, b"".join(m.lookup(k)[1] for k in range(me))
+        finally:
+            gpu.set_variant(0)
+            p.destroy()
+            m.destroy()
+
+    for how in ("multi", "extents", "async"):
+        ret, flt, after = run(how)
+        w, f, a = (rwant, rwf, rwafter) if how == "extents" else (want, wf, wafter)
+        np.testing.assert_array_equal(flt, f, err_msg=how)
+        np.testing.assert_array_equal(ret, w, err_msg=how)
+        assert after == a, how
