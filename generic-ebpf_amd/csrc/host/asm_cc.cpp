@@ -987,7 +987,9 @@ struct emitter {
 			const uint32_t sc = sel == 0x00010203u ? VGPR0 + V_SEL : sconst(sel);
 			E.vop3(V3_PERM_B32, L(d), VGPR0 + nx, VGPR0 + lo, sc);
 			hi0(d);
-			f.def(d, kbits(8 * std::min(z, swap_bytes)));
+			// (the loaded bytes land at the top of the swapped word: a byte under BE32 is b << 24,
+			// so the value needs all 8 * W bits, not 8 * z)
+			f.def(d, kbits(8 * swap_bytes));
 			return;
 		}
 		if (z == 1) {

@@ -580,3 +580,34 @@ def test_taken_jump_pc_wrap_leaves_program(gpu, env, variant):
         gpu.set_variant(0)
         p.destroy()
     assert (faults == 4).all() and (ret == 0).all()
+
+
+def _fused_swap_programs():
+    """A packet load fused with the BE16 / BE32 after it (asm_cc.cpp ldxpkc): the loaded bytes
+    land at the top of the swapped word, so a later shift or 64-bit multiply must see all 16 / 32
+    bits (fuzz_gpu.py seed 91 found the compiled code taking the load's own width: a carry into
+    the high word dropped by the multiply that followed)."""
+    from generic_ebpf_amd import isa, layout
+    I = isa.Insn
+    progs = []
+    for ld, be, sh in (("ldxb", 16, 8), ("ldxb", 32, 24), ("ldxh", 32, 16), ("ldxb", 32, 0)):
+        body = [I(ld, 0, 1, 13), I("be", 0, imm=be)]
+        if sh:
+            body.append(I("rsh64_imm", 0, imm=sh))
+        else:   # the seed-91 shape: a carry past bit 32, then a 64-bit multiply
+            body += [I("add64_imm", 0, imm=301528363), I("mul64_imm", 0, imm=625341585)]
+        progs.append(layout.assemble(body + [I("exit")]))
+    return progs
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_fused_load_swap_value_range(gpu, env, variant):
+    from generic_ebpf_amd import workloads
+    pk = workloads.packets_random(4099, 64, seed=61)
+    for lay in _fused_swap_programs():
+        c = goldens.Case("fused", lay.code, lay.relocs, [], pk.reshape(-1), len(pk), 64, None)
+        want, wf, _, _ = oracle_run(c)
+        ret, faults, _ = device_run(gpu, env, c, variant)
+        np.testing.assert_array_equal(faults, wf)
+        np.testing.assert_array_equal(ret, want)
+        assert len(np.unique(want)) > 100
