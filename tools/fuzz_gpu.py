@@ -136,7 +136,7 @@ def standard(a, env):
     72-B (general kernels)."""
     import stdprogs
     failed = False
-    for variant in (0, 1, 2):
+    for variant in getattr(a, "variants", (0, 1, 2)):
         for stride in (64, 72):
             t0, bad = time.time(), []
             for k in range(a.programs):
@@ -233,7 +233,8 @@ def mutated(a, env):
     new immediates), kept only when the oracle finds them defined, on every variant and both
     kernels."""
     failed = False
-    for variant, layout in [(v, lay) for v in (0, 1, 2) for lay in ("staged", "general")]:
+    for variant, layout in [(v, lay) for v in getattr(a, "variants", (0, 1, 2))
+                            for lay in ("staged", "general")]:
         t0, bad, kept = time.time(), [], 0
         for k in range(a.programs):
             # (seed 1 keeps the round-3 campaign's programs; other seeds mix in map writes)
@@ -266,7 +267,7 @@ def reference(a, env):
     (randprog bulk_writes: a loop-free program has no write limit)."""
     failed = False
     many = getattr(a, "manywrites", False)
-    for variant in (0, 1, 2):
+    for variant in getattr(a, "variants", (0, 1, 2)):
         for layout in ("staged", "general"):
             t0 = time.time()
             bad, faults = [], 0
@@ -298,7 +299,7 @@ def loop_writes(a, env):
     import stdprogs
     failed = False
     hashed = getattr(a, "hash", False)
-    for variant in (0, 1, 2):
+    for variant in getattr(a, "variants", (0, 1, 2)):
         t0, bad, faults = time.time(), [], 0
         for k in range(a.programs):
             seed = a.seed * 100000 + k
@@ -370,7 +371,9 @@ def main():
                     help="with --loopwrites: the counter programs read their counters back")
     ap.add_argument("--manywrites", action="store_true",
                     help="reference programs with more than 16 map writes on one path")
+    ap.add_argument("--variants", default="0,1,2", help="device variants to run (e.g. 0: compiled only)")
     a = ap.parse_args()
+    a.variants = tuple(int(v) for v in a.variants.split(","))
     env = native.Env()
     if a.loopwrites:
         failed = loop_writes(a, env)
