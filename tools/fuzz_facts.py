@@ -1,0 +1,105 @@
+"""Value-range fuzzing of the compiled path (round 6, after tools/fuzz_gpu.py seed 91 found a
+packet load fused with a wider BE32 given the load's own width): straight-line reference-semantics
+programs made of what the code generator keeps facts about — packet loads of every width (some
+followed by BE16 / BE32 / BE64 / LE on the same register: the fused forms), 32- and 64-bit ALU
+with immediates and registers, shifts by any amount, multiplies, NEG, MOV (64-bit MOV adds, as in
+the reference) — ending in a fold of every register into r0 with 64-bit multiplies, so that any
+wrong bit anywhere shows in the result.  Results and fault codes against the oracle, 64-B staged
+packets.
+
+  python tools/fuzz_facts.py [--programs N] [--seed S] [--variants 0,2]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+import pkgload  # noqa: E402
+
+pkgload.load()
+import goldens  # noqa: E402
+from helpers import device_run, oracle_run  # noqa: E402
+from generic_ebpf_amd import isa, layout, native, workloads  # noqa: E402
+
+I = isa.Insn
+ALU = ["add", "sub", "mul", "or", "and", "xor", "lsh", "rsh", "arsh"]
+
+
+def program(seed):
+    g = np.random.default_rng(seed)
+    regs = list(range(2, 10))
+    body = []
+
+    def load(r):
+        z = int(g.choice([1, 2, 4, 8]))
+        off = int(g.integers(0, 64 - z + 1))
+        body.append(I({1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[z], r, 1, off))
+        if g.random() < 0.5:   # a swap right after: the fused forms
+            body.append(I(str(g.choice(["be", "le"])), r, imm=int(g.choice([16, 32, 64]))))
+
+    for r in regs:
+        if g.random() < 0.7:
+            load(r)
+        else:
+            body.append(I("mov_imm", r, imm=int(g.integers(-2**31, 2**31))))
+    for _ in range(int(g.integers(10, 41))):
+        d = int(g.choice(regs))
+        u = g.random()
+        if u < 0.15:
+            load(d)
+        elif u < 0.2:
+            body.append(I(str(g.choice(["be", "le"])), d, imm=int(g.choice([16, 32, 64]))))
+        elif u < 0.25:
+            body.append(I(str(g.choice(["neg", "neg64"])), d))
+        else:
+            op = str(g.choice(ALU + ["mov"]))
+            w64 = g.random() < 0.6
+            name = op + ("64" if w64 else "")
+            if g.random() < 0.5:
+                if op in ("lsh", "rsh", "arsh"):
+                    imm = int(g.integers(0, 70))
+                else:
+                    imm = int(g.choice([int(g.integers(-2**31, 2**31)), int(g.integers(0, 256)),
+                                        int(g.integers(-256, 0)), 1 << int(g.integers(0, 31))]))
+                body.append(I(name + "_imm", d, imm=imm))
+            else:
+                body.append(I(name + "_reg", d, int(g.choice(regs))))
+    body += [I("mov_imm", 0, imm=0)]
+    for r in regs:
+        body += [I("xor64_reg", 0, r), I("mul64_imm", 0, imm=625341585)]
+    return layout.assemble(body + [I("exit")])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--programs", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--variants", default="0")
+    a = ap.parse_args()
+    env = native.Env()
+    failed = False
+    for variant in (int(v) for v in a.variants.split(",")):
+        t0, bad = time.time(), []
+        for k in range(a.programs):
+            lay = program(a.seed * 1000003 + k)
+            pk = workloads.packets_random(256, 64, seed=k)
+            c = goldens.Case("f%d" % k, lay.code, lay.relocs, [], pk.reshape(-1), 256, 64, None)
+            want, wf, _, _ = oracle_run(c)
+            got, gf, _ = device_run(native, env, c, variant)
+            if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+                bad.append(k)
+            if k % 1000 == 999:
+                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
+        print("facts variant %d: %d programs, %d mismatches %s (%.0f s)" % (
+            variant, a.programs, len(bad), bad[:20], time.time() - t0), flush=True)
+        failed = failed or bool(bad)
+    env.destroy()
+    sys.exit(1 if failed else 0)
+
+
+if __name__ == "__main__":
+    main()
