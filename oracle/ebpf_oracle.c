@@ -662,6 +662,8 @@ taint_pre(const struct region_env *re, uint8_t *taint, uint8_t op, int d, int s,
 			;
 		else if (code == 0x80 && cls == 4) /* NEG32 = -imm */
 			taint[d] = 0;
+		else if (code == 0xd0) /* LE / BE: the source bit picks the order, no register is read */
+			;
 		else if (x && code == 0x10 && taint[d] && taint[s]) /* pointer - pointer */
 			taint[d] = 0;
 		else if (x)

@@ -7,7 +7,9 @@ the reference) — ending in a fold of every register into r0 with 64-bit multip
 wrong bit anywhere shows in the result.  Results and fault codes against the oracle, 64-B staged
 packets.
 
-  python tools/fuzz_facts.py [--programs N] [--seed S] [--variants 0,2]"""
+--maps: stack stores with loads of other widths, and array lookups keyed by registers.
+
+  python tools/fuzz_facts.py [--programs N] [--seed S] [--variants 0,2] [--maps]"""
 import argparse
 import os
 import sys
@@ -29,10 +31,14 @@ I = isa.Insn
 ALU = ["add", "sub", "mul", "or", "and", "xor", "lsh", "rsh", "arsh"]
 
 
-def program(seed):
+def program(seed, maps=False):
+    """maps: also stack stores and loads at other widths (the generator's stack forwarding) and
+    array lookups keyed by a register (map 0: 16 x 8 B; the key masked to 15 or not, so the
+    lookup's NULL check may be proven away or not) with loads through the result"""
     g = np.random.default_rng(seed)
     regs = list(range(2, 10))
     body = []
+    from generic_ebpf_amd.layout import Branch, LdDw, MapRef
 
     def load(r):
         z = int(g.choice([1, 2, 4, 8]))
@@ -41,6 +47,10 @@ def program(seed):
         if g.random() < 0.5:   # a swap right after: the fused forms
             body.append(I(str(g.choice(["be", "le"])), r, imm=int(g.choice([16, 32, 64]))))
 
+    if maps:   # (the context pointer, reloaded after each lookup: LDDW r1 replaces it; the
+        # stack slots the loads read start defined)
+        body.append(I("stxdw", 10, 1, -64))
+        body += [I("stdw", 10, 0, -8 * j, int(g.integers(-2**31, 2**31))) for j in range(2, 6)]
     for r in regs:
         if g.random() < 0.7:
             load(r)
@@ -55,6 +65,23 @@ def program(seed):
             body.append(I(str(g.choice(["be", "le"])), d, imm=int(g.choice([16, 32, 64]))))
         elif u < 0.25:
             body.append(I(str(g.choice(["neg", "neg64"])), d))
+        elif maps and u < 0.33:   # a stack store, and a load of another width somewhere in it
+            zs, zl = int(g.choice([1, 2, 4, 8])), int(g.choice([1, 2, 4, 8]))
+            slot = -8 * int(g.integers(2, 6))
+            body.append(I({1: "stxb", 2: "stxh", 4: "stxw", 8: "stxdw"}[zs], 10, int(g.choice(regs)), slot))
+            body.append(I({1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[zl], d, 10,
+                          slot + int(g.integers(0, 8 - zl + 1))))
+        elif maps and u < 0.38:   # an array lookup keyed by a register, a load through it
+            k = int(g.choice(regs))
+            if g.random() < 0.6:
+                body.append(I("and_imm", k, imm=15))
+            body += [I("stxw", 10, k, -4), LdDw(1, MapRef(0)), I("mov_imm", 2, imm=0),
+                     I("mov64_reg", 2, 10), I("add64_imm", 2, imm=-4), I("call", imm=0),
+                     Branch(I("jeq_imm", 0, imm=0), [I("mov_imm", 0, imm=0x5a5a), I("exit")]),
+                     I("ldxdw", 1, 10, -64), I("mov_imm", 2, imm=int(g.integers(0, 2**31)))]
+            z = int(g.choice([1, 2, 4, 8]))
+            body.append(I({1: "ldxb", 2: "ldxh", 4: "ldxw", 8: "ldxdw"}[z], d, 0,
+                          int(g.integers(0, 8 - z + 1))))
         else:
             op = str(g.choice(ALU + ["mov"]))
             w64 = g.random() < 0.6
@@ -79,15 +106,18 @@ def main():
     ap.add_argument("--programs", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--maps", action="store_true", help="stack forwarding and array lookups too")
     a = ap.parse_args()
     env = native.Env()
     failed = False
     for variant in (int(v) for v in a.variants.split(",")):
         t0, bad = time.time(), []
         for k in range(a.programs):
-            lay = program(a.seed * 1000003 + k)
+            lay = program(a.seed * 1000003 + k, maps=a.maps)
             pk = workloads.packets_random(256, 64, seed=k)
-            c = goldens.Case("f%d" % k, lay.code, lay.relocs, [], pk.reshape(-1), 256, 64, None)
+            specs = [(8, 16, np.random.default_rng(k).integers(0, 256, 128, dtype=np.uint8).tobytes())] \
+                if a.maps else []
+            c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
             want, wf, _, _ = oracle_run(c)
             got, gf, _ = device_run(native, env, c, variant)
             if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
