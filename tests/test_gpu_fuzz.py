@@ -31,6 +31,15 @@ def fuzz(gpu):
     return fuzz_gpu
 
 
+@pytest.mark.parametrize("maps", [False, True])
+def test_value_range_campaign(gpu, env, maps):
+    """tools/fuzz_facts.py (round 6): straight-line programs aimed at the compiled code's
+    value-range facts (loads, fused swaps, ALU, shifts, multiplies; with maps: stack forwarding
+    and register-keyed lookups) on the compiled path and the assembly interpreter"""
+    import fuzz_facts
+    assert not fuzz_facts.campaign(env, 300, 161 + int(maps), (0, 2), maps)
+
+
 @pytest.mark.parametrize("mode", ["reference", "hash", "standard", "mutate", "loopwrites",
                                   "loopfetched", "loophash", "manywrites"])
 def test_fuzz_campaign(fuzz, env, mode):

@@ -101,6 +101,29 @@ def program(seed, maps=False):
     return layout.assemble(body + [I("exit")])
 
 
+def campaign(env, programs, seed, variants=(0,), maps=False):
+    """True when any program's results or faults differ from the oracle's (one line a variant)"""
+    failed = False
+    for variant in variants:
+        t0, bad = time.time(), []
+        for k in range(programs):
+            lay = program(seed * 1000003 + k, maps=maps)
+            pk = workloads.packets_random(256, 64, seed=k)
+            specs = [(8, 16, np.random.default_rng(k).integers(0, 256, 128, dtype=np.uint8).tobytes())] \
+                if maps else []
+            c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
+            want, wf, _, _ = oracle_run(c)
+            got, gf, _ = device_run(native, env, c, variant)
+            if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
+                bad.append(k)
+            if k % 1000 == 999:
+                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
+        print("facts%s variant %d: %d programs, %d mismatches %s (%.0f s)" % (
+            " (maps)" if maps else "", variant, programs, len(bad), bad[:20], time.time() - t0), flush=True)
+        failed = failed or bool(bad)
+    return failed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=2000)
@@ -109,24 +132,7 @@ def main():
     ap.add_argument("--maps", action="store_true", help="stack forwarding and array lookups too")
     a = ap.parse_args()
     env = native.Env()
-    failed = False
-    for variant in (int(v) for v in a.variants.split(",")):
-        t0, bad = time.time(), []
-        for k in range(a.programs):
-            lay = program(a.seed * 1000003 + k, maps=a.maps)
-            pk = workloads.packets_random(256, 64, seed=k)
-            specs = [(8, 16, np.random.default_rng(k).integers(0, 256, 128, dtype=np.uint8).tobytes())] \
-                if a.maps else []
-            c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
-            want, wf, _, _ = oracle_run(c)
-            got, gf, _ = device_run(native, env, c, variant)
-            if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
-                bad.append(k)
-            if k % 1000 == 999:
-                print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        print("facts variant %d: %d programs, %d mismatches %s (%.0f s)" % (
-            variant, a.programs, len(bad), bad[:20], time.time() - t0), flush=True)
-        failed = failed or bool(bad)
+    failed = campaign(env, a.programs, a.seed, tuple(int(v) for v in a.variants.split(",")), a.maps)
     env.destroy()
     sys.exit(1 if failed else 0)
 
