@@ -8,6 +8,7 @@ wrong bit anywhere shows in the result.  Results and fault codes against the ora
 packets.
 
 --maps: stack stores with loads of other widths, and array lookups keyed by registers.
+--general: ragged packets at CSR offsets (the general kernels: staged headers, short lanes).
 
   python tools/fuzz_facts.py [--programs N] [--seed S] [--variants 0,2] [--maps]"""
 import argparse
@@ -101,25 +102,41 @@ def program(seed, maps=False):
     return layout.assemble(body + [I("exit")])
 
 
-def campaign(env, programs, seed, variants=(0,), maps=False):
-    """True when any program's results or faults differ from the oracle's (one line a variant)"""
+def ragged(n, seed):
+    """n packets of 40..80 bytes at CSR offsets (the general kernels; a load past a short
+    packet's end faults MEM)"""
+    g = np.random.default_rng(seed)
+    sizes = g.integers(40, 81, n).astype(np.uint64)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(sizes, out=offs[1:])
+    return g.integers(0, 256, int(offs[-1]) + 64, dtype=np.uint8), offs
+
+
+def campaign(env, programs, seed, variants=(0,), maps=False, general=False):
+    """True when any program's results or faults differ from the oracle's (one line a variant);
+    general: ragged packets at CSR offsets (the general kernels) instead of 64-B staged ones"""
     failed = False
     for variant in variants:
         t0, bad = time.time(), []
         for k in range(programs):
             lay = program(seed * 1000003 + k, maps=maps)
-            pk = workloads.packets_random(256, 64, seed=k)
             specs = [(8, 16, np.random.default_rng(k).integers(0, 256, 128, dtype=np.uint8).tobytes())] \
                 if maps else []
-            c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
+            if general:
+                data, offs = ragged(256, k)
+                c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, data, 256, 0, offs)
+            else:
+                pk = workloads.packets_random(256, 64, seed=k)
+                c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
             want, wf, _, _ = oracle_run(c)
             got, gf, _ = device_run(native, env, c, variant)
             if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
                 bad.append(k)
             if k % 1000 == 999:
                 print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        print("facts%s variant %d: %d programs, %d mismatches %s (%.0f s)" % (
-            " (maps)" if maps else "", variant, programs, len(bad), bad[:20], time.time() - t0), flush=True)
+        print("facts%s%s variant %d: %d programs, %d mismatches %s (%.0f s)" % (
+            " (maps)" if maps else "", " general" if general else "", variant, programs, len(bad),
+            bad[:20], time.time() - t0), flush=True)
         failed = failed or bool(bad)
     return failed
 
@@ -130,9 +147,11 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--variants", default="0")
     ap.add_argument("--maps", action="store_true", help="stack forwarding and array lookups too")
+    ap.add_argument("--general", action="store_true", help="ragged packets: the general kernels")
     a = ap.parse_args()
     env = native.Env()
-    failed = campaign(env, a.programs, a.seed, tuple(int(v) for v in a.variants.split(",")), a.maps)
+    failed = campaign(env, a.programs, a.seed, tuple(int(v) for v in a.variants.split(",")), a.maps,
+                      a.general)
     env.destroy()
     sys.exit(1 if failed else 0)
 
