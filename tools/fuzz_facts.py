@@ -9,6 +9,7 @@ packets.
 
 --maps: stack stores with loads of other widths, and array lookups keyed by registers.
 --general: ragged packets at CSR offsets (the general kernels: staged headers, short lanes).
+--standard: the same programs under standard eBPF semantics (laid out slot after slot).
 
   python tools/fuzz_facts.py [--programs N] [--seed S] [--variants 0,2] [--maps]"""
 import argparse
@@ -25,14 +26,13 @@ import pkgload  # noqa: E402
 
 pkgload.load()
 import goldens  # noqa: E402
-from helpers import device_run, oracle_run  # noqa: E402
 from generic_ebpf_amd import isa, layout, native, workloads  # noqa: E402
 
 I = isa.Insn
 ALU = ["add", "sub", "mul", "or", "and", "xor", "lsh", "rsh", "arsh"]
 
 
-def program(seed, maps=False):
+def program(seed, maps=False, standard=False):
     """maps: also stack stores and loads at other widths (the generator's stack forwarding) and
     array lookups keyed by a register (map 0: 16 x 8 B; the key masked to 15 or not, so the
     lookup's NULL check may be proven away or not) with loads through the result"""
@@ -99,7 +99,11 @@ def program(seed, maps=False):
     body += [I("mov_imm", 0, imm=0)]
     for r in regs:
         body += [I("xor64_reg", 0, r), I("mul64_imm", 0, imm=625341585)]
-    return layout.assemble(body + [I("exit")])
+    body.append(I("exit"))
+    if standard:   # (straight-line, slot after slot: standard eBPF's own layout)
+        return b"".join(x.encode() for x in body), []
+    lay = layout.assemble(body)
+    return lay.code, lay.relocs
 
 
 def ragged(n, seed):
@@ -112,31 +116,55 @@ def ragged(n, seed):
     return g.integers(0, 256, int(offs[-1]) + 64, dtype=np.uint8), offs
 
 
-def campaign(env, programs, seed, variants=(0,), maps=False, general=False):
+def _run(env, code, relocs, specs, c, variant, standard):
+    import pyoracle
+    op = pyoracle.OracleProgram(code, relocs, specs, semantics=1 if standard else 0)
+    want, wf, _, _ = op.run(c.data, c.count, c.stride, c.offsets, nthreads=4)
+    maps = []
+    for vs, me, d in specs:
+        m = native.Map(env, me, vs)
+        m.fill(d)
+        maps.append(m)
+    p = native.Prog(env, native.patch_relocs(code, relocs, [m.handle for m in maps]))
+    try:
+        if standard:
+            p.set_semantics(native.SEM_STANDARD)
+        native.set_variant(variant)
+        got, gf, _ = p.run_batch(np.ascontiguousarray(c.data.copy()), c.count, c.stride, c.offsets)
+    finally:
+        native.set_variant(0)
+        p.destroy()
+        for m in maps:
+            m.destroy()
+    return want, wf, got, gf
+
+
+def campaign(env, programs, seed, variants=(0,), maps=False, general=False, standard=False):
     """True when any program's results or faults differ from the oracle's (one line a variant);
-    general: ragged packets at CSR offsets (the general kernels) instead of 64-B staged ones"""
+    general: ragged packets at CSR offsets (the general kernels) instead of 64-B staged ones;
+    standard: standard eBPF semantics (straight-line, no maps)"""
     failed = False
     for variant in variants:
         t0, bad = time.time(), []
         for k in range(programs):
-            lay = program(seed * 1000003 + k, maps=maps)
+            code, relocs = program(seed * 1000003 + k, maps=maps and not standard, standard=standard)
             specs = [(8, 16, np.random.default_rng(k).integers(0, 256, 128, dtype=np.uint8).tobytes())] \
-                if maps else []
+                if maps and not standard else []
             if general:
                 data, offs = ragged(256, k)
-                c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, data, 256, 0, offs)
+                c = goldens.Case("f%d" % k, code, relocs, specs, data, 256, 0, offs)
             else:
                 pk = workloads.packets_random(256, 64, seed=k)
-                c = goldens.Case("f%d" % k, lay.code, lay.relocs, specs, pk.reshape(-1), 256, 64, None)
-            want, wf, _, _ = oracle_run(c)
-            got, gf, _ = device_run(native, env, c, variant)
+                c = goldens.Case("f%d" % k, code, relocs, specs, pk.reshape(-1), 256, 64, None)
+            want, wf, got, gf = _run(env, code, relocs, specs, c, variant, standard)
             if not (np.array_equal(want, got) and np.array_equal(wf, gf)):
                 bad.append(k)
             if k % 1000 == 999:
                 print("  ... %d programs, %d mismatches" % (k + 1, len(bad)), flush=True)
-        print("facts%s%s variant %d: %d programs, %d mismatches %s (%.0f s)" % (
-            " (maps)" if maps else "", " general" if general else "", variant, programs, len(bad),
-            bad[:20], time.time() - t0), flush=True)
+        print("facts%s%s%s variant %d: %d programs, %d mismatches %s (%.0f s)" % (
+            " (maps)" if maps and not standard else "", " general" if general else "",
+            " standard" if standard else "", variant, programs, len(bad), bad[:20], time.time() - t0),
+            flush=True)
         failed = failed or bool(bad)
     return failed
 
@@ -148,10 +176,11 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--maps", action="store_true", help="stack forwarding and array lookups too")
     ap.add_argument("--general", action="store_true", help="ragged packets: the general kernels")
+    ap.add_argument("--standard", action="store_true", help="standard eBPF semantics (no maps)")
     a = ap.parse_args()
     env = native.Env()
     failed = campaign(env, a.programs, a.seed, tuple(int(v) for v in a.variants.split(",")), a.maps,
-                      a.general)
+                      a.general, a.standard)
     env.destroy()
     sys.exit(1 if failed else 0)
 
